@@ -1,0 +1,72 @@
+"""``add_model`` weights handler (reference ``commands/add_model_command.py:29-108``).
+
+Feeds a partial or full aggregate into the aggregator and, if it was accepted,
+announces the new contributor set with ``models_aggregated``.
+"""
+
+from __future__ import annotations
+
+from typing import Any, Callable, List, Optional
+
+from p2pfl_amd.commands.command import Command
+from p2pfl_amd.commands.models_agregated_command import ModelsAggregatedCommand
+from p2pfl_amd.learning.exceptions import DecodingParamsError, ModelNotMatchingError
+from p2pfl_amd.management.logger import logger
+
+
+class AddModelCommand(Command):
+    def __init__(self, state: Any, stop: Callable[[], None], aggregator: Any, comm_proto: Any) -> None:
+        self.state = state
+        self.stop = stop
+        self.aggregator = aggregator
+        self.communication_protocol = comm_proto
+
+    @staticmethod
+    def get_name() -> str:
+        return "add_model"
+
+    def execute(
+        self,
+        source: str,
+        round: int,
+        weights: Any = None,
+        contributors: Optional[List[str]] = None,
+        weight: Optional[int] = None,
+        **kwargs,
+    ) -> None:
+        if weights is None or contributors is None or weight is None:
+            raise ValueError("Weights, contributors and weight are required")
+        if self.state.round is None:
+            logger.debug(self.state.addr, "Tried to add a model while learning is not running")
+            return
+        if round != self.state.round:
+            logger.debug(self.state.addr, f"Model reception in a late round ({round} != {self.state.round}).")
+            return
+        if len(self.state.train_set) == 0:
+            logger.error(self.state.addr, "Model Reception when there is no trainset")
+            return
+        learner = self.state.learner
+        if learner is None:
+            return
+        try:
+            # cheap pre-check: skip decoding models the aggregator would reject
+            if not self.aggregator.would_accept(list(contributors)):
+                logger.debug(self.state.addr, f"Model from {contributors} not needed; skipped decode.")
+                return
+            models_added = self.aggregator.add_model(learner.decode_parameters(weights), list(contributors), weight)
+            if models_added:
+                self.state.changed.bump()
+                self.communication_protocol.broadcast(
+                    self.communication_protocol.build_msg(
+                        ModelsAggregatedCommand.get_name(), models_added, round=self.state.round
+                    )
+                )
+        except DecodingParamsError:
+            logger.error(self.state.addr, "Error decoding parameters.")
+            self.stop()
+        except ModelNotMatchingError:
+            logger.error(self.state.addr, "Models not matching.")
+            self.stop()
+        except Exception as e:
+            logger.error(self.state.addr, f"Unknown error adding model: {e}")
+            self.stop()

@@ -1,0 +1,173 @@
+"""Transport contract and shared wiring.
+
+:class:`CommunicationProtocol` is the abstract 14-method contract of the
+reference (``communication/communication_protocol.py:27-190``).
+:class:`BaseCommunicationProtocol` wires the transport-agnostic pieces
+(neighbours, client, gossiper, server core, heartbeater) once; transports only
+supply their neighbour/client/server classes.  The reference repeats that
+wiring in ``grpc_communication_protocol.py:45-64`` and
+``memory_communication_protocol.py:49-69``.
+"""
+
+from __future__ import annotations
+
+import threading
+from abc import ABC, abstractmethod
+from typing import Any, Callable, Dict, List, Optional, Union
+
+from p2pfl_amd.commands.command import Command
+from p2pfl_amd.commands.heartbeat_command import HeartbeatCommand
+from p2pfl_amd.communication.gossiper import Gossiper
+from p2pfl_amd.communication.heartbeater import Heartbeater
+from p2pfl_amd.settings import Settings
+
+
+class CommunicationProtocol(ABC):
+    @abstractmethod
+    def __init__(self, addr: str = "address", commands: Optional[List[Command]] = None) -> None: ...
+
+    @abstractmethod
+    def start(self) -> None: ...
+
+    @abstractmethod
+    def stop(self) -> None: ...
+
+    @abstractmethod
+    def add_command(self, cmds: Union[Command, List[Command]]) -> None: ...
+
+    @abstractmethod
+    def build_msg(self, cmd: str, args: Optional[List[str]] = None, round: Optional[int] = None) -> Any: ...
+
+    @abstractmethod
+    def build_weights(
+        self, cmd: str, round: int, serialized_model: Any, contributors: Optional[List[str]] = None, weight: int = 1
+    ) -> Any: ...
+
+    @abstractmethod
+    def send(self, nei: str, message: Any) -> None: ...
+
+    @abstractmethod
+    def broadcast(self, msg: Any, node_list: Optional[List[str]] = None) -> None: ...
+
+    @abstractmethod
+    def connect(self, addr: str, non_direct: bool = False) -> bool: ...
+
+    @abstractmethod
+    def disconnect(self, nei: str, disconnect_msg: bool = True) -> None: ...
+
+    @abstractmethod
+    def get_neighbors(self, only_direct: bool = False) -> Dict[str, Any]: ...
+
+    @abstractmethod
+    def get_address(self) -> str: ...
+
+    @abstractmethod
+    def wait_for_termination(self) -> None: ...
+
+    @abstractmethod
+    def gossip_weights(
+        self,
+        early_stopping_fn: Callable[[], bool],
+        get_candidates_fn: Callable[[], List[str]],
+        status_fn: Callable[[], Any],
+        model_fn: Callable[[str], Any],
+        period: Optional[float] = None,
+        create_connection: bool = False,
+        wakeup: Any = None,
+    ) -> None: ...
+
+    # -- optional capability (new) ---------------------------------------
+    @property
+    def supports_device_payloads(self) -> bool:
+        """True if weights may travel as device-resident arena snapshots."""
+        return False
+
+
+class BaseCommunicationProtocol(CommunicationProtocol):
+    neighbors_cls: Any = None
+    client_cls: Any = None
+    server_cls: Any = None
+
+    def __init__(self, addr: str = "127.0.0.1", commands: Optional[List[Command]] = None) -> None:
+        self.addr = self._resolve_address(addr)
+        self._neighbors = self.neighbors_cls(self.addr)
+        self._client = self.client_cls(self.addr, self._neighbors)
+        self._gossiper = Gossiper(self.addr, self._client)
+        self._server = self.server_cls(self.addr, self._gossiper, self._neighbors, commands)
+        self._heartbeater = Heartbeater(self.addr, self._neighbors, self._client)
+        self._server.add_command(HeartbeatCommand(self._heartbeater))
+        self._terminated = threading.Event()
+
+    def _resolve_address(self, addr: str) -> str:
+        return addr
+
+    # -- lifecycle -------------------------------------------------------
+    def get_address(self) -> str:
+        return self.addr
+
+    def start(self) -> None:
+        self._server.start()
+        self._heartbeater.start()
+        self._gossiper.start()
+
+    def stop(self) -> None:
+        self._heartbeater.stop()
+        self._gossiper.stop()
+        self._neighbors.clear_neighbors()
+        self._server.stop()
+        self._terminated.set()
+
+    def wait_for_termination(self) -> None:
+        self._terminated.wait()
+
+    # -- commands / messages ---------------------------------------------
+    def add_command(self, cmds: Union[Command, List[Command]]) -> None:
+        self._server.add_command(cmds)
+
+    def build_msg(self, cmd: str, args: Optional[List[str]] = None, round: Optional[int] = None) -> Any:
+        return self._client.build_message(cmd, args or [], round)
+
+    def build_weights(
+        self, cmd: str, round: int, serialized_model: Any, contributors: Optional[List[str]] = None, weight: int = 1
+    ) -> Any:
+        return self._client.build_weights(cmd, round, serialized_model, contributors or [], weight)
+
+    def send(self, nei: str, msg: Any, create_connection: bool = False) -> None:
+        self._client.send(nei, msg, create_connection=create_connection)
+
+    def broadcast(self, msg: Any, node_list: Optional[List[str]] = None) -> None:
+        self._client.broadcast(msg, node_list)
+
+    # -- topology --------------------------------------------------------
+    def connect(self, addr: str, non_direct: bool = False) -> bool:
+        return self._neighbors.add(addr, non_direct=non_direct)
+
+    def disconnect(self, nei: str, disconnect_msg: bool = True) -> None:
+        self._neighbors.remove(nei, disconnect_msg=disconnect_msg)
+
+    def get_neighbors(self, only_direct: bool = False) -> Dict[str, Any]:
+        return self._neighbors.get_all(only_direct)
+
+    def add_neighbor_listener(self, fn: Callable[[], None]) -> None:
+        self._neighbors.add_listener(fn)
+
+    # -- model gossip ----------------------------------------------------
+    def gossip_weights(
+        self,
+        early_stopping_fn: Callable[[], bool],
+        get_candidates_fn: Callable[[], List[str]],
+        status_fn: Callable[[], Any],
+        model_fn: Callable[[str], Any],
+        period: Optional[float] = None,
+        create_connection: bool = False,
+        wakeup: Any = None,
+    ) -> None:
+        self._gossiper.gossip_weights(
+            early_stopping_fn,
+            get_candidates_fn,
+            status_fn,
+            model_fn,
+            Settings.GOSSIP_MODELS_PERIOD if period is None else period,
+            create_connection,
+            wakeup,
+        )

@@ -1,0 +1,202 @@
+"""Partial / full aggregation bookkeeping (reference ``aggregators/aggregator.py:37-281``).
+
+Strategy base: subclasses implement only :meth:`aggregate`.  The base class
+tracks which train-set members' models have been folded in and enforces the
+decentralised-FedAvg invariant: a stored entry is keyed by its space-joined
+contributor list, and a new entry is accepted only if its contributors are all
+in the train set and disjoint from every contributor already present (or if it
+already covers the whole train set, which replaces everything).
+
+Differences from the reference:
+
+* completion is an ``Event`` instead of a lock released by another thread;
+* an empty contributor list returns ``[]`` (Q4: the reference released a lock
+  it did not hold and raised);
+* a node waiting for the full aggregate that times out with nothing gets
+  ``None`` back and keeps its local model (Q5: the reference logged that and
+  then raised); missing models are computed from flattened contributors;
+* :meth:`would_accept` lets the receive path skip decoding payloads that would
+  be rejected anyway;
+* partial aggregations are memoised per contributor subset until the stored
+  models change (gossip asks for the same subset once per neighbour per
+  iteration).
+"""
+
+from __future__ import annotations
+
+import threading
+from typing import Any, Dict, List, Optional, Tuple
+
+from p2pfl_amd.management.logger import logger
+from p2pfl_amd.settings import Settings
+
+
+class NoModelsToAggregateError(Exception):
+    """``aggregate`` called with no models."""
+
+
+ModelEntry = Tuple[Any, int]
+
+
+class Aggregator:
+    def __init__(self, node_name: str = "unknown") -> None:
+        self.node_name = node_name
+        self._train_set: List[str] = []
+        self._waiting_aggregated_model = False
+        self._models: Dict[str, ModelEntry] = {}
+        self._lock = threading.RLock()
+        self._done = threading.Event()
+        self._running = False
+        self._partial_cache: Dict[frozenset, Tuple[Any, List[str], int]] = {}
+
+    # ------------------------------------------------------------------
+    # strategy
+    # ------------------------------------------------------------------
+    def aggregate(self, models: Dict[str, ModelEntry]) -> Any:
+        raise NotImplementedError
+
+    # ------------------------------------------------------------------
+    # round control
+    # ------------------------------------------------------------------
+    def set_nodes_to_aggregate(self, nodes_to_aggregate: List[str]) -> None:
+        with self._lock:
+            if self._running:
+                raise Exception("It is not possible to set nodes to aggregate when the aggregation is running.")
+            self._train_set = list(nodes_to_aggregate)
+            self._running = True
+            self._done.clear()
+
+    def set_waiting_aggregated_model(self, nodes: List[str]) -> None:
+        self.set_nodes_to_aggregate(nodes)
+        with self._lock:
+            self._waiting_aggregated_model = True
+
+    def clear(self) -> None:
+        with self._lock:
+            self._train_set = []
+            self._models = {}
+            self._partial_cache = {}
+            self._waiting_aggregated_model = False
+            self._running = False
+            self._done.set()
+
+    # ------------------------------------------------------------------
+    # queries
+    # ------------------------------------------------------------------
+    def get_aggregated_models(self) -> List[str]:
+        with self._lock:
+            return [n for key in self._models for n in key.split()]
+
+    @property
+    def train_set(self) -> List[str]:
+        return list(self._train_set)
+
+    def _missing(self) -> List[str]:
+        have = set(self.get_aggregated_models())
+        return [n for n in self._train_set if n not in have]
+
+    def would_accept(self, contributors: List[str]) -> bool:
+        """Pure version of :meth:`add_model`'s acceptance test."""
+        if not contributors:
+            return False
+        with self._lock:
+            if self._waiting_aggregated_model and not self._models:
+                return set(contributors) == set(self._train_set)
+            aggregated = self.get_aggregated_models()
+            if len(self._train_set) <= len(aggregated):
+                return False
+            if not all(n in self._train_set for n in contributors):
+                return False
+            if len(contributors) == len(self._train_set):
+                return True
+            return all(n not in aggregated for n in contributors)
+
+    # ------------------------------------------------------------------
+    # model intake
+    # ------------------------------------------------------------------
+    def add_model(self, model: Any, contributors: List[str], weight: int) -> List[str]:
+        nodes = list(contributors)
+        if not nodes:
+            logger.debug(self.node_name, "Received a model without a list of contributors.")
+            return []
+        with self._lock:
+            if self._waiting_aggregated_model and not self._models:
+                if set(nodes) == set(self._train_set):
+                    logger.info(self.node_name, "Received an aggregated model.")
+                    self._models = {" ".join(nodes): (model, 1)}
+                    self._partial_cache = {}
+                    self._waiting_aggregated_model = False
+                    self._done.set()
+                    return nodes
+                return []
+            aggregated = self.get_aggregated_models()
+            if len(self._train_set) <= len(aggregated):
+                logger.debug(self.node_name, "Received a model when is not needed.")
+                return []
+            if not all(n in self._train_set for n in nodes):
+                logger.debug(self.node_name, f"Can't add a model from a node ({nodes}) that is not in the training set.")
+                return []
+            if len(nodes) == len(self._train_set):
+                self._models = {" ".join(nodes): (model, weight)}
+            elif all(n not in aggregated for n in nodes):
+                self._models[" ".join(nodes)] = (model, weight)
+            else:
+                logger.debug(self.node_name, f"Can't add a model that has already been added {nodes} / {aggregated}")
+                return []
+            self._partial_cache = {}
+            now = self.get_aggregated_models()
+            logger.info(self.node_name, f"Model added ({len(now)}/{len(self._train_set)}) from {nodes}")
+            if len(now) >= len(self._train_set):
+                self._done.set()
+            return now
+
+    # ------------------------------------------------------------------
+    # results
+    # ------------------------------------------------------------------
+    def wait_and_get_aggregation(self, timeout: Optional[float] = None) -> Any:
+        if timeout is None:
+            timeout = Settings.AGGREGATION_TIMEOUT
+        self._done.wait(timeout=timeout)
+        with self._lock:
+            models = dict(self._models)
+            waiting = self._waiting_aggregated_model
+            train_set = list(self._train_set)
+        if waiting:
+            if models:
+                return next(iter(models.values()))[0]
+            logger.info(self.node_name, "Timeout reached by waiting for an aggregated model. Continuing with the local model.")
+            return None
+        if len(models) == 1 and set(next(iter(models)).split()) == set(train_set):
+            return next(iter(models.values()))[0]  # a full aggregate arrived: nothing left to average
+        have = {n for key in models for n in key.split()}
+        missing = [n for n in train_set if n not in have]
+        if missing:
+            logger.info(self.node_name, f"Aggregating models, timeout reached. Missing models: {missing}")
+        else:
+            logger.info(self.node_name, "Aggregating models.")
+        if not models:
+            return None
+        with logger.span(self.node_name, "aggregate", k=len(models)):
+            return self.aggregate(models)
+
+    def get_partial_aggregation(self, except_nodes: List[str]) -> Tuple[Any, Optional[List[str]], Optional[int]]:
+        excl = set(except_nodes)
+        with self._lock:
+            chosen = {k: v for k, v in self._models.items() if not (set(k.split()) & excl)}
+            if not chosen:
+                return None, None, None
+            key = frozenset(chosen)
+            hit = self._partial_cache.get(key)
+            if hit is not None:
+                return hit
+        contributors = [n for k in chosen for n in k.split()]
+        weight = sum(w for _, w in chosen.values())
+        if len(chosen) == 1:
+            result = (next(iter(chosen.values()))[0], contributors, weight)
+        else:
+            with logger.span(self.node_name, "partial_aggregate", k=len(chosen)):
+                result = (self.aggregate(chosen), contributors, weight)
+        with self._lock:
+            if all(k in self._models for k in chosen):
+                self._partial_cache[key] = result
+        return result

@@ -1,0 +1,206 @@
+"""Flat parameter arenas.
+
+MI355X-first replacement for the reference's per-layer ``state_dict`` handling
+(``lightning_learner.py:113-164``, ``fedavg.py:49-58``): a model's parameters
+and buffers live in ONE contiguous fp32 device buffer, and every named tensor
+is a view into it.  Aggregation, optimizer steps, gossip snapshots and wire
+(de)serialisation then operate on a single buffer -- one kernel launch or one
+copy instead of one per layer.
+
+* :class:`ParamLayout` -- names, shapes, original dtypes and 64-element
+  (256-byte) aligned offsets; identical across peers running the same model.
+* :class:`FlatParams`  -- an ``OrderedDict`` of views that also carries
+  ``.flat`` (the 1-D buffer) and ``.layout``; it is what ``get_parameters``
+  returns, so ``params[name]`` indexing keeps working
+  (reference ``utils.py:129-137``).
+* :func:`bind_module` -- re-homes an ``nn.Module``'s parameters/buffers (and
+  optionally their gradients) into arenas, so the live model *is* the arena.
+"""
+
+from __future__ import annotations
+
+from collections import OrderedDict
+from dataclasses import dataclass
+from typing import Dict, Iterable, Mapping, Optional, Tuple
+
+import torch
+
+ALIGN = 64  # elements (256 B of fp32): keeps every view 16-B aligned for dwordx4 access
+
+
+def _align(n: int) -> int:
+    return (n + ALIGN - 1) // ALIGN * ALIGN
+
+
+@dataclass(frozen=True)
+class ParamLayout:
+    names: Tuple[str, ...]
+    shapes: Tuple[Tuple[int, ...], ...]
+    dtypes: Tuple[str, ...]
+    offsets: Tuple[int, ...]
+    numel: int  # padded total length of the flat buffer
+
+    @classmethod
+    def from_tensors(cls, items: Iterable[Tuple[str, torch.Tensor]]) -> "ParamLayout":
+        names, shapes, dtypes, offsets = [], [], [], []
+        off = 0
+        for name, t in items:
+            names.append(name)
+            shapes.append(tuple(int(s) for s in t.shape))
+            dtypes.append(str(t.dtype).replace("torch.", ""))
+            offsets.append(off)
+            off = _align(off + t.numel())
+        return cls(tuple(names), tuple(shapes), tuple(dtypes), tuple(offsets), max(off, ALIGN))
+
+    def sizes(self) -> Tuple[int, ...]:
+        out = []
+        for s in self.shapes:
+            n = 1
+            for d in s:
+                n *= d
+            out.append(n)
+        return tuple(out)
+
+    def compatible(self, other: "ParamLayout") -> bool:
+        return self.shapes == other.shapes and self.offsets == other.offsets and self.numel == other.numel
+
+    def to_json(self) -> Dict:
+        return {
+            "names": list(self.names),
+            "shapes": [list(s) for s in self.shapes],
+            "dtypes": list(self.dtypes),
+            "offsets": list(self.offsets),
+            "numel": self.numel,
+        }
+
+    @classmethod
+    def from_json(cls, d: Dict) -> "ParamLayout":
+        return cls(
+            tuple(d["names"]),
+            tuple(tuple(int(x) for x in s) for s in d["shapes"]),
+            tuple(d["dtypes"]),
+            tuple(int(o) for o in d["offsets"]),
+            int(d["numel"]),
+        )
+
+
+class FlatParams(OrderedDict):
+    """Named views into one contiguous fp32 buffer."""
+
+    flat: torch.Tensor
+    layout: ParamLayout
+
+    @classmethod
+    def from_flat(cls, flat: torch.Tensor, layout: ParamLayout) -> "FlatParams":
+        if flat.dim() != 1 or flat.numel() < layout.numel or not flat.is_contiguous():
+            raise ValueError("flat buffer does not match layout")
+        out = cls()
+        for name, shape, off, n in zip(layout.names, layout.shapes, layout.offsets, layout.sizes()):
+            out[name] = flat[off : off + n].view(shape)
+        out.flat = flat
+        out.layout = layout
+        return out
+
+    @property
+    def nbytes(self) -> int:
+        return self.flat.numel() * self.flat.element_size()
+
+    @property
+    def device(self) -> torch.device:
+        return self.flat.device
+
+    def clone(self) -> "FlatParams":  # type: ignore[override]
+        return FlatParams.from_flat(self.flat.clone(), self.layout)
+
+    def to(self, device: torch.device, non_blocking: bool = False) -> "FlatParams":
+        if self.flat.device == torch.device(device):
+            return self
+        return FlatParams.from_flat(self.flat.to(device, non_blocking=non_blocking), self.layout)
+
+
+def flatten(params: Mapping[str, torch.Tensor], device: Optional[torch.device] = None) -> FlatParams:
+    """Return ``params`` as a :class:`FlatParams` (no copy if it already is one)."""
+    if isinstance(params, FlatParams) and (device is None or params.flat.device == torch.device(device)):
+        return params
+    items = list(params.items())
+    layout = ParamLayout.from_tensors(items)
+    if device is None:
+        device = items[0][1].device if items else torch.device("cpu")
+    flat = torch.zeros(layout.numel, dtype=torch.float32, device=device)
+    for (name, t), off in zip(items, layout.offsets):
+        flat[off : off + t.numel()].copy_(t.detach().reshape(-1), non_blocking=True)
+    return FlatParams.from_flat(flat, layout)
+
+
+def is_arena_view(t: torch.Tensor, flat: torch.Tensor) -> bool:
+    base = flat.data_ptr()
+    return flat.device == t.device and base <= t.data_ptr() < base + flat.numel() * flat.element_size()
+
+
+class ModuleArena:
+    """Binds an ``nn.Module``'s state into flat arenas.
+
+    After binding, every float parameter and buffer of the module is a view of
+    ``self.params.flat``; with ``grads=True`` each parameter's ``.grad`` is a
+    view of ``self.grads`` (so a single fused optimizer kernel can update the
+    whole model).  Integer buffers (e.g. BatchNorm's ``num_batches_tracked``)
+    stay where they are but are mirrored into the arena by :meth:`sync_in`
+    and restored by :meth:`sync_out`.
+    """
+
+    def __init__(self, module: torch.nn.Module, device: Optional[torch.device] = None, grads: bool = False) -> None:
+        sd = module.state_dict(keep_vars=True)
+        if device is None:
+            device = next(iter(sd.values())).device if sd else torch.device("cpu")
+        self.module = module
+        self.layout = ParamLayout.from_tensors((k, v) for k, v in sd.items())
+        flat = torch.zeros(self.layout.numel, dtype=torch.float32, device=device)
+        self.params = FlatParams.from_flat(flat, self.layout)
+        self._int_buffers: Dict[str, torch.Tensor] = {}
+        for name, t in sd.items():
+            view = self.params[name]
+            view.copy_(t.detach().reshape(view.shape).to(device=device, dtype=torch.float32))
+            if t.is_floating_point():
+                t.data = view  # parameter / buffer now lives in the arena
+            else:
+                self._int_buffers[name] = t
+        self.grads: Optional[torch.Tensor] = None
+        if grads:
+            self.grads = torch.zeros_like(flat)
+            gviews = FlatParams.from_flat(self.grads, self.layout)
+            for name, p in module.named_parameters():
+                if name in gviews:
+                    p.grad = gviews[name]
+        # mask of trainable elements (params, not buffers)
+        self.param_names = [n for n, _ in module.named_parameters()]
+
+    @property
+    def flat(self) -> torch.Tensor:
+        return self.params.flat
+
+    def sync_in(self) -> None:
+        """Mirror non-float buffers into the arena (before sending / aggregating)."""
+        for name, t in self._int_buffers.items():
+            self.params[name].copy_(t.reshape(self.params[name].shape).float())
+
+    def sync_out(self) -> None:
+        """Copy averaged non-float buffers back to the module."""
+        for name, t in self._int_buffers.items():
+            t.copy_(self.params[name].reshape(t.shape).round().to(t.dtype))
+
+    def grads_bound(self) -> bool:
+        if self.grads is None:
+            return False
+        for _, p in self.module.named_parameters():
+            if p.grad is None or not is_arena_view(p.grad, self.grads):
+                return False
+        return True
+
+    def rebind_grads(self) -> None:
+        if self.grads is None:
+            return
+        gviews = FlatParams.from_flat(self.grads, self.layout)
+        for name, p in self.module.named_parameters():
+            if p.grad is not None and not is_arena_view(p.grad, self.grads):
+                gviews[name].copy_(p.grad)
+            p.grad = gviews[name]

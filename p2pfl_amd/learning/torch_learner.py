@@ -1,0 +1,248 @@
+"""PyTorch-ROCm learner (reference ``learning/pytorch/lightning_learner.py:45-236``).
+
+Replaces the Lightning ``Trainer`` with an explicit loop tuned for MI355X:
+
+* the model's parameters, buffers and gradients are re-homed into flat arenas
+  (:class:`~p2pfl_amd.learning.arena.ModuleArena`), so ``get_parameters`` is
+  zero-copy, ``set_parameters`` is one device copy, gossip snapshots are one
+  ``clone`` and FedAvg is one kernel;
+* when the model's ``configure_optimizers`` returns plain Adam/SGD over all
+  parameters, the step runs as ONE fused HIP kernel over the whole arena
+  (``ops.adam_step`` / ``ops.sgd_step``) instead of per-tensor launches;
+* data batches are produced on the device (no loader workers);
+* compute runs under bf16 autocast on the GPU (fp32 master weights and
+  optimizer state), fp32 on the CPU;
+* the optimizer is re-created on every :meth:`fit`, as Lightning does when a
+  new ``Trainer`` is built per round (reference quirk Q23, kept).
+
+Metrics: per-step ``train_loss`` (every ``log_every_n_steps``) and per-epoch
+validation metrics go to the local store, ``evaluate`` results to the global
+store, exactly where the reference's ``FederatedLogger`` put them.
+"""
+
+from __future__ import annotations
+
+import threading
+from collections import OrderedDict
+from typing import Any, Dict, Mapping, Optional, Tuple
+
+import torch
+
+from p2pfl_amd import ops
+from p2pfl_amd.learning.arena import FlatParams, ModuleArena
+from p2pfl_amd.learning.exceptions import DecodingParamsError, ModelNotMatchingError
+from p2pfl_amd.learning.learner import NodeLearner
+from p2pfl_amd.learning.wire import decode_params, encode_params
+from p2pfl_amd.management.logger import logger
+from p2pfl_amd.settings import Settings
+
+
+def default_device() -> torch.device:
+    return torch.device("cuda", torch.cuda.current_device()) if torch.cuda.is_available() else torch.device("cpu")
+
+
+class TorchLearner(NodeLearner):
+    def __init__(
+        self,
+        model: Any,
+        data: Any,
+        self_addr: str,
+        epochs: int,
+        device: Optional[torch.device] = None,
+        precision: Optional[str] = None,
+        log_every_n_steps: int = 50,
+        fused_optimizer: bool = True,
+    ) -> None:
+        if Settings.TORCH_NUM_THREADS:
+            torch.set_num_threads(Settings.TORCH_NUM_THREADS)
+        self._addr = self_addr
+        self.epochs = epochs
+        self.device = torch.device(device) if device is not None else default_device()
+        self.precision = precision or ("bf16" if self.device.type == "cuda" else "fp32")
+        self.log_every_n_steps = log_every_n_steps
+        self.fused_optimizer = fused_optimizer
+        self._interrupt = threading.Event()
+        self._step = 0
+        self.model: Any = None
+        self.arena: Optional[ModuleArena] = None
+        self.data: Any = None
+        self.set_model(model)
+        self.set_data(data)
+
+    # ------------------------------------------------------------------
+    # model / data
+    # ------------------------------------------------------------------
+    def set_model(self, model: Any) -> None:
+        self.model = model
+        if model is None:
+            self.arena = None
+            return
+        model.to(self.device)
+        self.arena = ModuleArena(model, device=self.device, grads=True)
+
+    def set_data(self, data: Any) -> None:
+        self.data = data
+        if data is not None and hasattr(data, "to"):
+            data.to(self.device)
+
+    def get_num_samples(self) -> Tuple[int, int]:
+        return (len(self.data.train_dataloader().dataset), len(self.data.test_dataloader().dataset))
+
+    # ------------------------------------------------------------------
+    # parameters
+    # ------------------------------------------------------------------
+    def get_parameters(self) -> FlatParams:
+        assert self.arena is not None
+        self.arena.sync_in()
+        return self.arena.params
+
+    def set_parameters(self, params: Mapping[str, torch.Tensor]) -> None:
+        assert self.arena is not None
+        try:
+            own = self.arena.params
+            if isinstance(params, FlatParams) and params.layout.compatible(own.layout):
+                own.flat.copy_(params.flat, non_blocking=True)
+            else:
+                if len(params) != len(own):
+                    raise ModelNotMatchingError(f"expected {len(own)} tensors, got {len(params)}")
+                # names may differ (positional compatibility), shapes must not
+                for (name, dst), src in zip(own.items(), params.values()):
+                    if tuple(src.shape) != tuple(dst.shape):
+                        raise ModelNotMatchingError(f"shape mismatch for {name}: {tuple(src.shape)} vs {tuple(dst.shape)}")
+                    dst.copy_(src.reshape(dst.shape), non_blocking=True)
+            self.arena.sync_out()
+        except ModelNotMatchingError:
+            raise
+        except Exception as e:
+            raise ModelNotMatchingError("Not matching models") from e
+
+    def encode_parameters(self, params: Optional[Mapping[str, torch.Tensor]] = None) -> bytes:
+        if params is None:
+            params = self.get_parameters()
+        return encode_params(params)
+
+    def snapshot_parameters(self, params: Optional[Mapping[str, torch.Tensor]] = None) -> FlatParams:
+        if params is None:
+            params = self.get_parameters()
+        if isinstance(params, FlatParams):
+            return params.clone()
+        from p2pfl_amd.learning.arena import flatten
+
+        return flatten(params, device=self.device)
+
+    def decode_parameters(self, data: Any) -> FlatParams:
+        assert self.arena is not None
+        try:
+            if isinstance(data, FlatParams):
+                params = data.to(self.device, non_blocking=True)
+            elif isinstance(data, (bytes, bytearray, memoryview)):
+                params = decode_params(data)
+                if isinstance(params, FlatParams):
+                    params = params.to(self.device)
+            else:
+                raise DecodingParamsError(f"unsupported payload type {type(data).__name__}")
+        except DecodingParamsError:
+            raise
+        except Exception as e:
+            raise DecodingParamsError("Error decoding parameters") from e
+        own = self.arena.params
+        if isinstance(params, FlatParams):
+            if not params.layout.compatible(own.layout):
+                raise ModelNotMatchingError("payload layout does not match the local model")
+            return FlatParams.from_flat(params.flat, own.layout)
+        # generic dict payload: validate then re-home
+        if len(params) != len(own) or any(tuple(a.shape) != tuple(b.shape) for a, b in zip(params.values(), own.values())):
+            raise ModelNotMatchingError("payload tensors do not match the local model")
+        flat = torch.zeros_like(own.flat)
+        out = FlatParams.from_flat(flat, own.layout)
+        for dst, src in zip(out.values(), params.values()):
+            dst.copy_(src.reshape(dst.shape))
+        return out
+
+    # ------------------------------------------------------------------
+    # training
+    # ------------------------------------------------------------------
+    def set_epochs(self, epochs: int) -> None:
+        self.epochs = epochs
+
+    def _autocast(self):
+        if self.precision == "bf16" and self.device.type == "cuda":
+            return torch.autocast(device_type="cuda", dtype=torch.bfloat16)
+        return torch.autocast(device_type="cpu", enabled=False)
+
+    def _make_optimizer(self):
+        opt = self.model.configure_optimizers()
+        if isinstance(opt, (list, tuple)):
+            opt = opt[0]
+        if not (self.fused_optimizer and self.device.type == "cuda" and self.arena is not None):
+            return opt
+        from p2pfl_amd.learning.optim import fuse_optimizer
+
+        return fuse_optimizer(opt, self.arena) or opt
+
+    def interrupt_fit(self) -> None:
+        self._interrupt.set()
+
+    def fit(self) -> None:
+        if self.epochs <= 0 or self.model is None:
+            return
+        self._interrupt.clear()
+        try:
+            opt = self._make_optimizer()
+            model = self.model
+            for _epoch in range(self.epochs):
+                model.train()
+                with logger.span(self._addr, "train_epoch"):
+                    for i, batch in enumerate(self.data.train_dataloader()):
+                        if self._interrupt.is_set():
+                            return
+                        opt.zero_grad(set_to_none=False)
+                        with self._autocast():
+                            loss = model.training_step(batch, i)
+                        loss.backward()
+                        opt.step()
+                        self._step += 1
+                        if self.log_every_n_steps and self._step % self.log_every_n_steps == 0:
+                            for k, v in model.pop_logged().items():
+                                logger.log_metric(self._addr, k, float(v), step=self._step)
+                if self.arena is not None and not self.arena.grads_bound():
+                    self.arena.rebind_grads()
+                self._validate()
+        except Exception as e:
+            logger.error(self._addr, f"Fit error: {e}")
+            raise
+
+    @torch.no_grad()
+    def _run_eval(self, loader, hook) -> Dict[str, float]:
+        self.model.eval()
+        sums: Dict[str, torch.Tensor] = {}
+        n = 0
+        for i, (x, y) in enumerate(loader):
+            with self._autocast():
+                hook((x, y), i)
+            bs = int(y.shape[0])
+            for k, v in self.model.pop_logged().items():
+                v = v.float() if isinstance(v, torch.Tensor) else torch.tensor(float(v))
+                sums[k] = sums.get(k, 0) + v * bs
+            n += bs
+        return {k: float(v) / max(1, n) for k, v in sums.items()}
+
+    def _validate(self) -> None:
+        loader = self.data.val_dataloader()
+        if loader is None or len(loader.dataset) == 0:
+            return
+        for k, v in self._run_eval(loader, self.model.validation_step).items():
+            logger.log_metric(self._addr, k, v, step=self._step)
+
+    def evaluate(self) -> Dict[str, float]:
+        if self.epochs <= 0 or self.model is None:
+            return {}
+        with logger.span(self._addr, "evaluate"):
+            results = self._run_eval(self.data.test_dataloader(), self.model.test_step)
+        for k, v in results.items():
+            logger.log_metric(self._addr, k, v)
+        return results
+
+
+# Reference-compatible name: users of ``LightningLearner`` keep their imports.
+LightningLearner = TorchLearner

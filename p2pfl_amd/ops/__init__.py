@@ -1,0 +1,139 @@
+"""Hand-written HIP/CDNA4 kernels (``csrc/*.hip``, extension ``p2pfl_amd._C``).
+
+Every op has a plain-torch implementation used for CPU tensors (the control
+plane and the CPU test-suite run without a GPU) and as the fp32 reference in
+numerics tests.  For GPU tensors the HIP kernel is mandatory: if the extension
+is missing on a GPU box the call raises instead of silently falling back, so a
+"passing" GPU run always exercised the native path.
+"""
+
+from __future__ import annotations
+
+import importlib
+import os
+from typing import List, Optional, Sequence
+
+import torch
+
+_ext = None
+_ext_error: Optional[BaseException] = None
+
+
+def _load():
+    global _ext, _ext_error
+    if _ext is None and _ext_error is None:
+        try:
+            _ext = importlib.import_module("p2pfl_amd._C")
+        except BaseException as e:  # ImportError, OSError (missing HIP runtime), ...
+            _ext_error = e
+    return _ext
+
+
+def available() -> bool:
+    return _load() is not None
+
+
+def ext():
+    """The native extension; raises loudly if it was not built."""
+    m = _load()
+    if m is None:
+        raise RuntimeError(
+            "p2pfl_amd native extension (p2pfl_amd._C) is not available: "
+            f"{_ext_error!r}. Build it with `python setup.py build_ext --inplace` "
+            "(PYTORCH_ROCM_ARCH=gfx950)."
+        )
+    return m
+
+
+def _gpu(t: torch.Tensor) -> bool:
+    return t.is_cuda and os.environ.get("P2PFL_FORCE_TORCH_OPS") != "1"
+
+
+# ----------------------------------------------------------------------------
+# aggregation
+# ----------------------------------------------------------------------------
+def normalized_weights(weights: Sequence[float]) -> List[float]:
+    total = float(sum(weights))
+    if total <= 0:
+        return [1.0 / len(weights)] * len(weights)
+    return [float(w) / total for w in weights]
+
+
+def weighted_average_reference(flats: Sequence[torch.Tensor], weights: Sequence[float]) -> torch.Tensor:
+    w = normalized_weights(weights)
+    acc = torch.zeros_like(flats[0], dtype=torch.float32)
+    for f, wi in zip(flats, w):
+        acc.add_(f.float(), alpha=wi)
+    return acc
+
+
+def weighted_average(
+    flats: Sequence[torch.Tensor], weights: Sequence[float], out: Optional[torch.Tensor] = None
+) -> torch.Tensor:
+    """``sum_i w_i * flats[i] / sum_i w_i`` in fp32 (one fused kernel on GPU)."""
+    if len(flats) == 0:
+        raise ValueError("no inputs")
+    n = flats[0].numel()
+    for f in flats:
+        if f.numel() != n:
+            raise ValueError("inputs differ in size")
+    if not _gpu(flats[0]):
+        res = weighted_average_reference(flats, weights)
+        if out is not None:
+            out.copy_(res)
+            return out
+        return res
+    dev = flats[0].device
+    srcs = [f if (f.device == dev and f.dtype == torch.float32 and f.is_contiguous()) else f.to(dev, torch.float32).contiguous() for f in flats]
+    if out is None:
+        out = torch.empty(n, dtype=torch.float32, device=dev)
+    ext().weighted_sum(srcs, normalized_weights(weights), out)
+    return out
+
+
+# ----------------------------------------------------------------------------
+# optimizers (whole-arena, in place)
+# ----------------------------------------------------------------------------
+def adam_step_reference(p, g, m, v, lr, beta1, beta2, eps, weight_decay, step, decoupled=False):
+    if weight_decay != 0:
+        if decoupled:
+            p.mul_(1 - lr * weight_decay)
+        else:
+            g = g + weight_decay * p
+    m.mul_(beta1).add_(g, alpha=1 - beta1)
+    v.mul_(beta2).addcmul_(g, g, value=1 - beta2)
+    bc1 = 1 - beta1**step
+    bc2 = 1 - beta2**step
+    denom = (v.sqrt() / (bc2**0.5)).add_(eps)
+    p.addcdiv_(m, denom, value=-lr / bc1)
+
+
+def adam_step(p, g, m, v, *, lr, beta1, beta2, eps, weight_decay, step, decoupled=False, p_bf16=None):
+    """In-place Adam/AdamW over flat fp32 buffers (optionally also writes a bf16 copy of p)."""
+    if not _gpu(p):
+        adam_step_reference(p, g, m, v, lr, beta1, beta2, eps, weight_decay, step, decoupled)
+        if p_bf16 is not None:
+            p_bf16.copy_(p)
+        return
+    ext().adam_step(p, g, m, v, p_bf16, float(lr), float(beta1), float(beta2), float(eps), float(weight_decay), int(step), bool(decoupled))
+
+
+def sgd_step_reference(p, g, buf, lr, momentum, dampening, weight_decay, nesterov, first_step):
+    if weight_decay != 0:
+        g = g + weight_decay * p
+    if momentum != 0:
+        if first_step:
+            buf.copy_(g)
+        else:
+            buf.mul_(momentum).add_(g, alpha=1 - dampening)
+        g = g + momentum * buf if nesterov else buf
+    p.add_(g, alpha=-lr)
+
+
+def sgd_step(p, g, buf, *, lr, momentum=0.0, dampening=0.0, weight_decay=0.0, nesterov=False, first_step=False, p_bf16=None):
+    if not _gpu(p):
+        sgd_step_reference(p, g, buf, lr, momentum, dampening, weight_decay, nesterov, first_step)
+        if p_bf16 is not None:
+            p_bf16.copy_(p)
+        return
+    ext().sgd_step(p, g, buf, p_bf16, float(lr), float(momentum), float(dampening), float(weight_decay), bool(nesterov), bool(first_step))

@@ -1,0 +1,74 @@
+"""Process-global tunables.
+
+Same attribute names and defaults as the reference ``Settings`` class
+(reference ``p2pfl/settings.py:26-115``) so user code that mutates them keeps
+working.  Periods here are *upper bounds*: the control plane is event driven
+(condition variables) and wakes up early when the state it waits on changes,
+instead of sleeping a full period like the reference's polling loops.
+
+MI355X-specific knobs (device data plane, kernel selection) are grouped at the
+bottom and are new.
+"""
+
+from __future__ import annotations
+
+
+class Settings:
+    """Global settings shared by every in-process node (reference quirk Q14)."""
+
+    # ---- general ---------------------------------------------------------
+    GRPC_TIMEOUT: float = 10
+    """Maximum time (s) to wait for a gRPC request."""
+    LOG_LEVEL: str = "INFO"
+    """Log level name."""
+    LOG_DIR: str = "logs"
+    """Directory for the rotating log file."""
+
+    # ---- heartbeat -------------------------------------------------------
+    HEARTBEAT_PERIOD: float = 2
+    """Period (s) between heartbeats."""
+    HEARTBEAT_TIMEOUT: float = 5
+    """Silence (s) after which a neighbour is evicted."""
+
+    # ---- gossip ----------------------------------------------------------
+    GOSSIP_PERIOD: float = 0.1
+    """Period (s) of the control-message relay loop."""
+    TTL: int = 10
+    """Hop budget of flooded control messages."""
+    GOSSIP_MESSAGES_PER_PERIOD: int = 100
+    """Relay rate limit: messages per ``GOSSIP_PERIOD``."""
+    AMOUNT_LAST_MESSAGES_SAVED: int = 100
+    """Size of the duplicate-suppression ring."""
+    GOSSIP_MODELS_PERIOD: float = 1
+    """Upper bound (s) between two model-gossip iterations."""
+    GOSSIP_MODELS_PER_ROUND: int = 2
+    """Fan-out of one model-gossip iteration."""
+    GOSSIP_EXIT_ON_X_EQUAL_ROUNDS: int = 10
+    """Model gossip stops after this many identical status snapshots."""
+
+    # ---- training --------------------------------------------------------
+    TRAIN_SET_SIZE: int = 4
+    """Number of nodes elected to train each experiment."""
+    VOTE_TIMEOUT: float = 60
+    """Timeout (s) while collecting train-set votes."""
+    AGGREGATION_TIMEOUT: float = 300
+    """Timeout (s) while waiting for the models of the train set."""
+    WAIT_HEARTBEATS_CONVERGENCE: float = 0.2 * HEARTBEAT_TIMEOUT
+    """Time (s) to let heartbeats converge before voting."""
+
+    # ---- web / monitoring ------------------------------------------------
+    RESOURCE_MONITOR_PERIOD: float = 1
+    """Period (s) of the resource monitor."""
+
+    # ---- MI355X data plane (new) ----------------------------------------
+    DEVICE_PAYLOADS: bool = True
+    """Transports that live in one process hand device-resident flat
+    parameter arenas to each other instead of host byte strings."""
+    GRPC_MAX_MESSAGE_BYTES: int = 1 << 30
+    """gRPC send/receive limit (the reference kept gRPC's 4 MiB default,
+    which the 26 MB MNIST CNN exceeds: reference quirk Q6)."""
+    TORCH_NUM_THREADS: int | None = None
+    """If set, ``torch.set_num_threads`` value used by the learners
+    (the reference hard-codes 1: ``lightning_learner.py:38``)."""
+    TRACE_SPANS: bool = True
+    """Record per-stage / per-gossip timing spans in the tracer."""

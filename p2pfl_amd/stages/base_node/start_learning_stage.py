@@ -1,0 +1,75 @@
+"""StartLearningStage (reference ``stages/base_node/start_learning_stage.py:36-136``).
+
+Sets up the experiment, instantiates the learner, waits until the initial
+weights are present (the initiator's own, or received via ``init_model``),
+pushes them to direct neighbours that have not announced
+``model_initialized`` yet, lets heartbeats converge, then votes.
+"""
+
+from __future__ import annotations
+
+import time
+from typing import Any, List, Optional, Type
+
+from p2pfl_amd.commands.init_model_command import InitModelCommand
+from p2pfl_amd.management.logger import logger
+from p2pfl_amd.settings import Settings
+from p2pfl_amd.stages.base_node.common import model_payload
+from p2pfl_amd.stages.stage import Stage
+from p2pfl_amd.stages.stage_factory import StageFactory
+
+
+class StartLearningStage(Stage):
+    @staticmethod
+    def name() -> str:
+        return "StartLearningStage"
+
+    @staticmethod
+    def execute(
+        rounds: Optional[int] = None,
+        epochs: Optional[int] = None,
+        model: Any = None,
+        data: Any = None,
+        state: Any = None,
+        learner_class: Any = None,
+        communication_protocol: Any = None,
+        aggregator: Any = None,
+        **kwargs,
+    ) -> Optional[Type[Stage]]:
+        if None in (rounds, epochs, state, learner_class, model, data, communication_protocol, aggregator):
+            raise Exception("Invalid parameters on StartLearningStage.")
+        with state.start_thread_lock:  # dedupe duplicate start messages
+            if state.round is not None:
+                return None
+            state.set_experiment("experiment", rounds)
+            logger.experiment_started(state.addr)
+            state.learner = learner_class(model, data, state.addr, epochs)
+        begin = time.time()
+        logger.info(state.addr, "Waiting initialization.")
+        while not state.model_initialized.wait(timeout=0.5):
+            if state.round is None:
+                return None
+        logger.info(state.addr, "Gossiping model initialization.")
+        StartLearningStage._gossip_model(state, communication_protocol, aggregator)
+        wait = Settings.WAIT_HEARTBEATS_CONVERGENCE - (time.time() - begin)
+        if wait > 0:
+            time.sleep(wait)
+        return StageFactory.get_stage("VoteTrainSetStage")
+
+    @staticmethod
+    def _gossip_model(state: Any, protocol: Any, aggregator: Any) -> None:
+        def candidates() -> List[str]:
+            return [n for n in protocol.get_neighbors(only_direct=True) if n not in state.nei_status]
+
+        def model_fn(_: str) -> Any:
+            if state.learner is None or state.round is None:
+                return None
+            return protocol.build_weights(
+                InitModelCommand.get_name(),
+                state.round,
+                model_payload(state, protocol),
+                aggregator.get_aggregated_models(),
+                1,
+            )
+
+        protocol.gossip_weights(lambda: state.round is None, candidates, candidates, model_fn, wakeup=state.changed)

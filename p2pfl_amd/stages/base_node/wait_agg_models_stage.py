@@ -1,0 +1,23 @@
+"""WaitAggregatedModelsStage (reference ``stages/base_node/wait_agg_models_stage.py:31-49``)."""
+
+from __future__ import annotations
+
+from typing import Any, Optional, Type
+
+from p2pfl_amd.management.logger import logger
+from p2pfl_amd.stages.stage import Stage
+from p2pfl_amd.stages.stage_factory import StageFactory
+
+
+class WaitAggregatedModelsStage(Stage):
+    @staticmethod
+    def name() -> str:
+        return "WaitAggregatedModelsStage"
+
+    @staticmethod
+    def execute(state: Any = None, aggregator: Any = None, **kwargs) -> Optional[Type[Stage]]:
+        if state is None or aggregator is None:
+            raise Exception("Invalid parameters on WaitAggregatedModelsStage.")
+        logger.info(state.addr, "Waiting aggregation.")
+        aggregator.set_waiting_aggregated_model(state.train_set)
+        return StageFactory.get_stage("GossipModelStage")
