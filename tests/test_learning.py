@@ -1,0 +1,215 @@
+"""Learner / aggregator / codec tests (reference ``test/learning_test.py`` + property tests)."""
+
+from __future__ import annotations
+
+import itertools
+import pickle
+import random
+from collections import OrderedDict
+
+import pytest
+import torch
+
+from p2pfl_amd.learning.aggregators import FedAvg
+from p2pfl_amd.learning.arena import FlatParams, ModuleArena, ParamLayout, flatten
+from p2pfl_amd.learning.exceptions import DecodingParamsError, ModelNotMatchingError
+from p2pfl_amd.learning.torch_learner import LightningLearner, TorchLearner
+from p2pfl_amd.learning.wire import decode_params, encode_params
+from p2pfl_amd.models import CNN, MLP
+
+
+def test_encoding():
+    nl1 = TorchLearner(MLP(), None, "", 1, device="cpu")
+    encoded = nl1.encode_parameters()
+    nl2 = LightningLearner(MLP(), None, "", 1, device="cpu")
+    nl2.set_parameters(nl2.decode_parameters(encoded))
+    assert encoded == nl2.encode_parameters()
+
+
+def test_avg_simple():
+    agg = FedAvg()
+    a = OrderedDict([("a", torch.tensor(-1)), ("b", torch.tensor(-1))])
+    b = OrderedDict([("a", torch.tensor(0)), ("b", torch.tensor(0))])
+    c = OrderedDict([("a", torch.tensor(1)), ("b", torch.tensor(1))])
+    res = agg.aggregate({"a": (a, 1), "b": (b, 1), "c": (c, 1)})
+    for layer in b:
+        assert res[layer] == b[layer]
+    res = agg.aggregate({"a": (a, 1), "b": (b, 7), "c": (c, 1)})
+    for layer in b:
+        assert res[layer] == b[layer]
+    res = agg.aggregate({"a": (a, 800), "b": (b, 0), "c": (c, 0)})
+    for layer in b:
+        assert res[layer] == a[layer]
+
+
+def test_avg_complex():
+    agg = FedAvg()
+    nl = TorchLearner(MLP(), None, "", 1, device="cpu")
+    params = {k: v.clone() for k, v in nl.get_parameters().items()}
+    res = agg.aggregate({"a": (params, 1)})
+    for layer in params:
+        assert torch.eq(params[layer], res[layer]).all()
+    p1 = {k: v + 1 for k, v in params.items()}
+    p2 = {k: v - 1 for k, v in params.items()}
+    res = agg.aggregate({"a": (p1, 1), "b": (p2, 1)})
+    for layer in params:
+        assert torch.allclose(params[layer], res[layer], atol=1e-5)
+
+
+@pytest.mark.parametrize("seed", range(5))
+def test_partial_aggregation_equals_fedavg(seed):
+    """Any disjoint partition, partially aggregated then combined, equals one-shot FedAvg."""
+    rng = random.Random(seed)
+    nodes = [f"n{i}" for i in range(6)]
+    models = {n: OrderedDict(w=torch.randn(33), b=torch.randn(4, 5)) for n in nodes}
+    weights = {n: rng.randint(1, 100) for n in nodes}
+    full = FedAvg().aggregate({n: (models[n], weights[n]) for n in nodes})
+    # random disjoint partition into partial aggregates
+    order = nodes[:]
+    rng.shuffle(order)
+    cuts = sorted(rng.sample(range(1, 6), 2))
+    groups = [order[: cuts[0]], order[cuts[0] : cuts[1]], order[cuts[1] :]]
+    agg = FedAvg("me")
+    agg.set_nodes_to_aggregate(nodes)
+    for g in groups:
+        sub = FedAvg().aggregate({n: (models[n], weights[n]) for n in g})
+        assert agg.add_model(sub, g, sum(weights[n] for n in g))
+    combined = agg.wait_and_get_aggregation(timeout=1)
+    for k in full:
+        assert torch.allclose(full[k], combined[k], atol=1e-5)
+
+
+def test_aggregator_rules():
+    agg = FedAvg("me")
+    m = OrderedDict(w=torch.ones(3))
+    agg.set_nodes_to_aggregate(["a", "b", "c"])
+    with pytest.raises(Exception):
+        agg.set_nodes_to_aggregate(["a"])
+    assert agg.add_model(m, [], 1) == []  # Q4: empty contributors
+    assert agg.add_model(m, ["x"], 1) == []  # not in train set
+    assert agg.add_model(m, ["a"], 1) == ["a"]
+    assert agg.would_accept(["b"]) and not agg.would_accept(["a", "b"])
+    assert agg.add_model(m, ["a", "b"], 1) == []  # overlap
+    assert sorted(agg.add_model(m, ["b", "c"], 2)) == ["a", "b", "c"]
+    assert agg.add_model(m, ["c"], 1) == []  # not needed anymore
+    agg.clear()
+    # a full model replaces partial ones
+    agg.set_nodes_to_aggregate(["a", "b"])
+    agg.add_model(OrderedDict(w=torch.zeros(3)), ["a"], 1)
+    agg.add_model(OrderedDict(w=torch.full((3,), 5.0)), ["a", "b"], 2)
+    res = agg.wait_and_get_aggregation(timeout=1)
+    assert torch.allclose(res["w"], torch.full((3,), 5.0))
+    agg.clear()
+
+
+def test_waiting_aggregated_model_timeout_returns_none():
+    agg = FedAvg("me")
+    agg.set_waiting_aggregated_model(["a", "b"])
+    assert agg.add_model(OrderedDict(w=torch.ones(2)), ["a"], 1) == []  # only the full aggregate is accepted
+    assert agg.wait_and_get_aggregation(timeout=0.2) is None  # Q5: keep local model
+    agg.clear()
+    agg.set_waiting_aggregated_model(["a", "b"])
+    assert agg.add_model(OrderedDict(w=torch.ones(2)), ["b", "a"], 1) == ["b", "a"]
+    assert torch.equal(agg.wait_and_get_aggregation(timeout=1)["w"], torch.ones(2))
+
+
+def test_partial_aggregation_excludes_and_caches():
+    agg = FedAvg("me")
+    agg.set_nodes_to_aggregate(["a", "b", "c"])
+    agg.add_model(OrderedDict(w=torch.full((4,), 1.0)), ["a"], 1)
+    agg.add_model(OrderedDict(w=torch.full((4,), 3.0)), ["b"], 3)
+    m, contrib, w = agg.get_partial_aggregation(["c"])
+    assert sorted(contrib) == ["a", "b"] and w == 4 and torch.allclose(m["w"], torch.full((4,), 2.5))
+    m2, _, _ = agg.get_partial_aggregation(["c"])
+    assert m2 is m  # memoised
+    m3, contrib3, w3 = agg.get_partial_aggregation(["a"])
+    assert contrib3 == ["b"] and w3 == 3
+    assert agg.get_partial_aggregation(["a", "b"]) == (None, None, None)
+
+
+def test_wire_codec_roundtrip_and_safety():
+    params = OrderedDict(
+        a=torch.randn(3, 4), b=torch.arange(5, dtype=torch.int64), c=torch.randn(2).to(torch.bfloat16), d=torch.tensor(True)
+    )
+    out = decode_params(encode_params(params))
+    for k in params:
+        assert out[k].dtype == params[k].dtype and torch.equal(out[k], params[k])
+    flat = flatten(OrderedDict(x=torch.randn(10), y=torch.randn(3, 3)))
+    back = decode_params(encode_params(flat))
+    assert isinstance(back, FlatParams) and torch.equal(back.flat, flat.flat) and back.layout == flat.layout
+    # a pickle payload (what the reference sends) is refused, never unpickled
+    with pytest.raises(DecodingParamsError):
+        decode_params(pickle.dumps([torch.zeros(2).numpy()]))
+    with pytest.raises(DecodingParamsError):
+        decode_params(encode_params(flat)[:-8])
+
+
+def test_decode_wrong_model_raises():
+    mlp = TorchLearner(MLP(), None, "", 1, device="cpu")
+    cnn = TorchLearner(CNN(), None, "", 1, device="cpu")
+    with pytest.raises(ModelNotMatchingError):
+        mlp.decode_parameters(cnn.encode_parameters())
+    with pytest.raises(ModelNotMatchingError):
+        mlp.set_parameters(cnn.get_parameters())
+
+
+def test_arena_binding_is_live():
+    model = MLP()
+    arena = ModuleArena(model, grads=True)
+    assert arena.layout.names == tuple(model.state_dict().keys())
+    arena.flat.zero_()
+    assert float(model.l1.weight.abs().sum()) == 0.0
+    x = torch.randn(4, 1, 28, 28)
+    model(x).sum().backward()
+    assert arena.grads_bound() and float(arena.grads.abs().sum()) > 0
+
+
+def test_layout_alignment():
+    lay = ParamLayout.from_tensors([("a", torch.zeros(3)), ("b", torch.zeros(70)), ("c", torch.zeros(1))])
+    assert lay.offsets == (0, 64, 192) and lay.numel == 256
+
+
+@pytest.mark.parametrize("opt_name", ["adam", "adamw", "sgd", "sgd_nesterov"])
+def test_fused_optimizer_matches_torch(opt_name):
+    from p2pfl_amd.learning.optim import fuse_optimizer
+
+    torch.manual_seed(0)
+    m1, m2 = MLP(), MLP()
+    m2.load_state_dict(m1.state_dict())
+    mk = {
+        "adam": lambda p: torch.optim.Adam(p, lr=1e-2, weight_decay=0.01),
+        "adamw": lambda p: torch.optim.AdamW(p, lr=1e-2, weight_decay=0.1),
+        "sgd": lambda p: torch.optim.SGD(p, lr=0.1, momentum=0.9, weight_decay=1e-3),
+        "sgd_nesterov": lambda p: torch.optim.SGD(p, lr=0.1, momentum=0.9, nesterov=True),
+    }[opt_name]
+    ref_opt = mk(m1.parameters())
+    arena = ModuleArena(m2, grads=True)
+    fused = fuse_optimizer(mk(m2.parameters()), arena)
+    assert fused is not None
+    for step in range(3):
+        x = torch.randn(8, 1, 28, 28)
+        y = torch.randint(0, 10, (8,))
+        for m, o in ((m1, ref_opt), (m2, fused)):
+            o.zero_grad()
+            torch.nn.functional.nll_loss(m(x), y).backward()
+            o.step()
+    for (k, a), b in zip(m1.state_dict().items(), m2.state_dict().values()):
+        assert torch.allclose(a, b, atol=1e-5, rtol=1e-4), k
+
+
+def test_learner_fit_evaluate_cpu():
+    from p2pfl_amd.data import MnistFederatedDM
+    from p2pfl_amd.management.logger import logger
+
+    dm = MnistFederatedDM(sub_id=0, number_sub=40)
+    nl = TorchLearner(MLP(seed=1), dm, "learner-test", 1, device="cpu")
+    assert nl.get_num_samples() == (1350, 250)
+    logger.register_node("learner-test", type("S", (), {"round": 0, "actual_exp_name": "exp"})(), True)
+    try:
+        before = nl.evaluate()
+        nl.fit()
+        after = nl.evaluate()
+    finally:
+        logger.unregister_node("learner-test")
+    assert after["test_loss"] < before["test_loss"]
+    assert after["test_metric"] > 0.3
