@@ -1,0 +1,96 @@
+// PyTorch bindings of the p2pfl_amd HIP kernels (module p2pfl_amd._C).
+// Every entry validates shapes/dtypes/devices on the host BEFORE launching,
+// so a mismatched call fails with a Python exception instead of a GPU fault.
+#include <torch/extension.h>
+#include <c10/hip/HIPStream.h>
+#include <c10/core/DeviceGuard.h>
+
+#include <cmath>
+#include <vector>
+
+#include "kernels.h"
+#include "cnn.h"
+
+namespace {
+
+hipStream_t stream() { return c10::hip::getCurrentHIPStream().stream(); }
+
+void check_f32(const torch::Tensor& t, const char* name) {
+  TORCH_CHECK(t.is_cuda(), name, " must be a GPU tensor");
+  TORCH_CHECK(t.scalar_type() == torch::kFloat32, name, " must be float32");
+  TORCH_CHECK(t.is_contiguous(), name, " must be contiguous");
+  TORCH_CHECK(reinterpret_cast<uintptr_t>(t.data_ptr()) % 16 == 0, name, " must be 16-byte aligned");
+}
+
+void weighted_sum(std::vector<torch::Tensor> srcs, std::vector<double> weights, torch::Tensor out) {
+  TORCH_CHECK(!srcs.empty() && srcs.size() == weights.size(), "weighted_sum: bad inputs");
+  check_f32(out, "out");
+  const c10::DeviceGuard guard(out.device());
+  const int64_t n = out.numel();
+  std::vector<const float*> ptrs;
+  std::vector<float> w;
+  for (size_t i = 0; i < srcs.size(); ++i) {
+    check_f32(srcs[i], "src");
+    TORCH_CHECK(srcs[i].numel() == n, "weighted_sum: size mismatch");
+    TORCH_CHECK(srcs[i].device() == out.device(), "weighted_sum: device mismatch");
+    ptrs.push_back(srcs[i].data_ptr<float>());
+    w.push_back(float(weights[i]));
+  }
+  p2::weighted_sum(ptrs.data(), w.data(), int(ptrs.size()), out.data_ptr<float>(), n, stream());
+}
+
+uint16_t* opt_bf16(const c10::optional<torch::Tensor>& t, int64_t n) {
+  if (!t.has_value() || !t->defined()) return nullptr;
+  TORCH_CHECK(t->is_cuda() && t->scalar_type() == torch::kBFloat16 && t->is_contiguous() && t->numel() >= n,
+              "bf16 shadow must be a contiguous bf16 GPU tensor of the arena size");
+  return reinterpret_cast<uint16_t*>(t->data_ptr());
+}
+
+void adam_step(torch::Tensor p, torch::Tensor g, torch::Tensor m, torch::Tensor v, c10::optional<torch::Tensor> pbf,
+               double lr, double b1, double b2, double eps, double wd, int64_t step, bool decoupled) {
+  for (auto* t : {&p, &g, &m, &v}) check_f32(*t, "adam operand");
+  const int64_t n = p.numel();
+  TORCH_CHECK(g.numel() == n && m.numel() == n && v.numel() == n, "adam: size mismatch");
+  TORCH_CHECK(n % 4 == 0, "adam: arena length must be a multiple of 4");
+  const c10::DeviceGuard guard(p.device());
+  p2::AdamParams h{};
+  h.lr = float(lr);
+  h.beta1 = float(b1);
+  h.beta2 = float(b2);
+  h.eps = float(eps);
+  h.weight_decay = float(wd);
+  h.step_size = float(lr / (1.0 - std::pow(b1, double(step))));
+  h.inv_sqrt_bc2 = float(1.0 / std::sqrt(1.0 - std::pow(b2, double(step))));
+  h.decoupled = decoupled ? 1 : 0;
+  p2::adam_step(p.data_ptr<float>(), g.data_ptr<float>(), m.data_ptr<float>(), v.data_ptr<float>(), opt_bf16(pbf, n),
+                n, h, stream());
+}
+
+void sgd_step(torch::Tensor p, torch::Tensor g, c10::optional<torch::Tensor> buf, c10::optional<torch::Tensor> pbf,
+              double lr, double momentum, double dampening, double wd, bool nesterov, bool first_step) {
+  check_f32(p, "p");
+  check_f32(g, "g");
+  const int64_t n = p.numel();
+  TORCH_CHECK(g.numel() == n && n % 4 == 0, "sgd: size mismatch");
+  float* b = nullptr;
+  if (buf.has_value() && buf->defined()) {
+    check_f32(*buf, "buf");
+    TORCH_CHECK(buf->numel() == n, "sgd: buf size mismatch");
+    b = buf->data_ptr<float>();
+  }
+  const c10::DeviceGuard guard(p.device());
+  p2::SgdParams h{float(lr), float(momentum), float(dampening), float(wd), nesterov ? 1 : 0, first_step ? 1 : 0};
+  p2::sgd_step(p.data_ptr<float>(), g.data_ptr<float>(), b, opt_bf16(pbf, n), n, h, stream());
+}
+
+}  // namespace
+
+void register_cnn(pybind11::module& m);
+
+PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
+  m.doc() = "p2pfl_amd native HIP/CDNA4 kernels (gfx950)";
+  m.def("weighted_sum", &weighted_sum, "out = sum_i w_i * src_i (fp32 flat arenas)");
+  m.def("adam_step", &adam_step, "fused whole-arena Adam/AdamW step");
+  m.def("sgd_step", &sgd_step, "fused whole-arena SGD(+momentum/nesterov) step");
+  register_cnn(m);
+}

@@ -1,0 +1,221 @@
+// PyTorch bindings of the fused MNIST-CNN training kernels (csrc/cnn_*.hip).
+// Every binding checks dtypes, sizes and devices on the host before it
+// launches, so a wrong call raises instead of faulting the GPU.
+#include <torch/extension.h>
+#include <c10/hip/HIPStream.h>
+#include <c10/core/DeviceGuard.h>
+
+#include "cnn.h"
+
+namespace {
+
+using p2cnn::AdamCfg;
+using p2cnn::Offsets;
+
+hipStream_t stream() { return c10::hip::getCurrentHIPStream().stream(); }
+
+template <typename T>
+T* ptr(const torch::Tensor& t, c10::ScalarType st, int64_t min_numel, const char* name, int align = 16) {
+  TORCH_CHECK(t.defined() && t.is_cuda(), name, ": expected a GPU tensor");
+  TORCH_CHECK(t.scalar_type() == st, name, ": wrong dtype ", t.scalar_type());
+  TORCH_CHECK(t.is_contiguous(), name, ": must be contiguous");
+  TORCH_CHECK(t.numel() >= min_numel, name, ": needs >= ", min_numel, " elements, got ", t.numel());
+  TORCH_CHECK(reinterpret_cast<uintptr_t>(t.data_ptr()) % align == 0, name, ": must be ", align, "-byte aligned");
+  return reinterpret_cast<T*>(t.data_ptr());
+}
+template <typename T>
+T* optr(const c10::optional<torch::Tensor>& t, c10::ScalarType st, int64_t min_numel, const char* name,
+        int align = 16) {
+  if (!t.has_value() || !t->defined()) return nullptr;
+  return ptr<T>(*t, st, min_numel, name, align);
+}
+
+Offsets offsets(const std::vector<int64_t>& o) {
+  TORCH_CHECK(o.size() == 8, "offsets: expected 8 entries");
+  for (auto v : o) TORCH_CHECK(v >= 0, "offsets: negative");
+  return Offsets{o[0], o[1], o[2], o[3], o[4], o[5], o[6], o[7]};
+}
+
+int64_t params_end(const Offsets& o) {
+  return std::max({o.c1w + 800, o.c1b + 32, o.c2w + 51200, o.c2b + 64, o.l1w + int64_t(2048) * 3136, o.l1b + 2048,
+                   o.l2w + 20480, o.l2b + 10});
+}
+
+void check_batch(int B, int mrows) {
+  TORCH_CHECK(mrows == 32 || mrows == 64, "mrows must be 32 or 64");
+  TORCH_CHECK(B >= 1 && B <= mrows, "batch ", B, " exceeds mrows ", mrows);
+}
+
+const int64_t* idx_ptr(const c10::optional<torch::Tensor>& idx, int B) {
+  return optr<int64_t>(idx, torch::kInt64, B, "idx", 8);
+}
+
+// NOTE: gathers through idx are bounds-checked on the host only by shape; the
+// learner guarantees idx values are permutations of the dataset rows.
+
+void k_step_begin(torch::Tensor adam_t) {
+  const c10::DeviceGuard g(adam_t.device());
+  p2cnn::step_begin(ptr<int>(adam_t, torch::kInt32, 1, "adam_t", 4), stream());
+}
+
+void k_conv1_fwd(torch::Tensor x, c10::optional<torch::Tensor> idx, torch::Tensor params, std::vector<int64_t> off,
+                 torch::Tensor p1, torch::Tensor am1, int64_t B) {
+  const c10::DeviceGuard g(params.device());
+  Offsets o = offsets(off);
+  TORCH_CHECK(x.numel() % 784 == 0, "x must be [N,1,28,28] uint8");
+  if (!idx.has_value()) TORCH_CHECK(x.numel() / 784 >= B, "x has fewer than B rows");
+  p2cnn::conv1_fwd(ptr<uint8_t>(x, torch::kUInt8, 784, "x", 1), idx_ptr(idx, B),
+                   ptr<float>(params, torch::kFloat32, params_end(o), "params"), o,
+                   reinterpret_cast<uint16_t*>(ptr<at::BFloat16>(p1, torch::kBFloat16, B * 196 * 32, "p1")),
+                   ptr<uint8_t>(am1, torch::kUInt8, B * 196 * 32, "am1"), int(B), stream());
+}
+
+void k_conv2_fwd(torch::Tensor p1, torch::Tensor w2r, torch::Tensor params, std::vector<int64_t> off,
+                 torch::Tensor a1, torch::Tensor a1t, torch::Tensor am2, int64_t B, int64_t mrows) {
+  const c10::DeviceGuard g(params.device());
+  check_batch(int(B), int(mrows));
+  Offsets o = offsets(off);
+  p2cnn::conv2_fwd(reinterpret_cast<uint16_t*>(ptr<at::BFloat16>(p1, torch::kBFloat16, B * 196 * 32, "p1")),
+                   reinterpret_cast<uint16_t*>(ptr<at::BFloat16>(w2r, torch::kBFloat16, 51200, "w2r")),
+                   ptr<float>(params, torch::kFloat32, params_end(o), "params"), o,
+                   reinterpret_cast<uint16_t*>(ptr<at::BFloat16>(a1, torch::kBFloat16, mrows * 3136, "a1")),
+                   reinterpret_cast<uint16_t*>(ptr<at::BFloat16>(a1t, torch::kBFloat16, mrows * 3136, "a1t")),
+                   ptr<uint8_t>(am2, torch::kUInt8, B * 3136, "am2"), int(B), int(mrows), stream());
+}
+
+void k_gemm_skinny(torch::Tensor A, torch::Tensor Bt, torch::Tensor slabs, int64_t mrows, int64_t N, int64_t K,
+                   int64_t S) {
+  const c10::DeviceGuard g(A.device());
+  TORCH_CHECK(mrows == 32 || mrows == 64, "mrows must be 32 or 64");
+  TORCH_CHECK(N % 32 == 0 && K % 64 == 0 && S >= 1, "gemm_skinny: N%32, K%64 required");
+  p2cnn::gemm_skinny(reinterpret_cast<uint16_t*>(ptr<at::BFloat16>(A, torch::kBFloat16, mrows * K, "A")),
+                     reinterpret_cast<uint16_t*>(ptr<at::BFloat16>(Bt, torch::kBFloat16, N * K, "Bt")),
+                     ptr<float>(slabs, torch::kFloat32, S * mrows * N, "slabs"), int(mrows), int(N), int(K), int(S),
+                     stream());
+}
+
+void k_head(torch::Tensor slabs, int64_t S, int64_t mrows, torch::Tensor params, std::vector<int64_t> off,
+            torch::Tensor labels, c10::optional<torch::Tensor> idx, int64_t B, bool train, torch::Tensor H,
+            torch::Tensor dH, torch::Tensor dHt, torch::Tensor dlogits, torch::Tensor stats) {
+  const c10::DeviceGuard g(params.device());
+  check_batch(int(B), int(mrows));
+  Offsets o = offsets(off);
+  if (!idx.has_value()) TORCH_CHECK(labels.numel() >= B, "labels has fewer than B rows");
+  p2cnn::head(ptr<float>(slabs, torch::kFloat32, S * mrows * 2048, "slabs"), int(S), int(mrows),
+              ptr<float>(params, torch::kFloat32, params_end(o), "params"), o,
+              ptr<int64_t>(labels, torch::kInt64, 1, "labels", 8), idx_ptr(idx, B), int(B), train ? 1 : 0,
+              reinterpret_cast<uint16_t*>(ptr<at::BFloat16>(H, torch::kBFloat16, mrows * 2048, "H")),
+              reinterpret_cast<uint16_t*>(ptr<at::BFloat16>(dH, torch::kBFloat16, mrows * 2048, "dH")),
+              reinterpret_cast<uint16_t*>(ptr<at::BFloat16>(dHt, torch::kBFloat16, mrows * 2048, "dHt")),
+              ptr<float>(dlogits, torch::kFloat32, mrows * 10, "dlogits"), ptr<float>(stats, torch::kFloat32, 2, "stats", 4),
+              stream());
+}
+
+AdamCfg cfg(double lr, double b1, double b2, double eps, double wd) {
+  return AdamCfg{float(lr), float(b1), float(b2), float(eps), float(wd)};
+}
+
+void k_fc2_wgrad_adam(torch::Tensor dlogits, torch::Tensor H, int64_t B, torch::Tensor params, torch::Tensor m,
+                      torch::Tensor v, c10::optional<torch::Tensor> gdump, std::vector<int64_t> off,
+                      torch::Tensor adam_t, double lr, double b1, double b2, double eps, double wd) {
+  const c10::DeviceGuard g(params.device());
+  Offsets o = offsets(off);
+  const int64_t n = params_end(o);
+  p2cnn::fc2_wgrad_adam(ptr<float>(dlogits, torch::kFloat32, B * 10, "dlogits"),
+                        reinterpret_cast<uint16_t*>(ptr<at::BFloat16>(H, torch::kBFloat16, B * 2048, "H")), int(B),
+                        ptr<float>(params, torch::kFloat32, n, "params"), ptr<float>(m, torch::kFloat32, n, "m"),
+                        ptr<float>(v, torch::kFloat32, n, "v"), optr<float>(gdump, torch::kFloat32, n, "gdump"), o,
+                        ptr<int>(adam_t, torch::kInt32, 1, "adam_t", 4), cfg(lr, b1, b2, eps, wd), stream());
+}
+
+void k_fc1_wgrad_adam(torch::Tensor dHt, torch::Tensor a1t, int64_t mrows, torch::Tensor params, torch::Tensor m,
+                      torch::Tensor v, c10::optional<torch::Tensor> gdump, torch::Tensor w1bf, torch::Tensor w1tbf,
+                      std::vector<int64_t> off, torch::Tensor adam_t, double lr, double b1, double b2, double eps,
+                      double wd) {
+  const c10::DeviceGuard g(params.device());
+  TORCH_CHECK(mrows == 32 || mrows == 64, "mrows must be 32 or 64");
+  Offsets o = offsets(off);
+  const int64_t n = params_end(o);
+  p2cnn::fc1_wgrad_adam(reinterpret_cast<uint16_t*>(ptr<at::BFloat16>(dHt, torch::kBFloat16, 2048 * mrows, "dHt")),
+                        reinterpret_cast<uint16_t*>(ptr<at::BFloat16>(a1t, torch::kBFloat16, 3136 * mrows, "a1t")),
+                        int(mrows), ptr<float>(params, torch::kFloat32, n, "params"),
+                        ptr<float>(m, torch::kFloat32, n, "m"), ptr<float>(v, torch::kFloat32, n, "v"),
+                        optr<float>(gdump, torch::kFloat32, n, "gdump"),
+                        reinterpret_cast<uint16_t*>(ptr<at::BFloat16>(w1bf, torch::kBFloat16, 2048 * 3136, "w1bf")),
+                        reinterpret_cast<uint16_t*>(ptr<at::BFloat16>(w1tbf, torch::kBFloat16, 2048 * 3136, "w1tbf")),
+                        o, ptr<int>(adam_t, torch::kInt32, 1, "adam_t", 4), cfg(lr, b1, b2, eps, wd), stream());
+}
+
+void k_conv2_wgrad(torch::Tensor slabs2, int64_t S2, int64_t mrows, torch::Tensor am2, torch::Tensor p1,
+                   torch::Tensor wslab2, int64_t B) {
+  const c10::DeviceGuard g(p1.device());
+  check_batch(int(B), int(mrows));
+  p2cnn::conv2_wgrad(ptr<float>(slabs2, torch::kFloat32, S2 * mrows * 3136, "slabs2"), int(S2), int(mrows),
+                     ptr<uint8_t>(am2, torch::kUInt8, B * 3136, "am2"),
+                     reinterpret_cast<uint16_t*>(ptr<at::BFloat16>(p1, torch::kBFloat16, B * 196 * 32, "p1")),
+                     ptr<float>(wslab2, torch::kFloat32, B * p2cnn::kSlab2, "wslab2"), int(B), stream());
+}
+
+void k_conv2_dgrad(torch::Tensor slabs2, int64_t S2, int64_t mrows, torch::Tensor am2, torch::Tensor am1,
+                   torch::Tensor w2q, torch::Tensor x, c10::optional<torch::Tensor> idx, torch::Tensor wslab1,
+                   int64_t B) {
+  const c10::DeviceGuard g(w2q.device());
+  check_batch(int(B), int(mrows));
+  if (!idx.has_value()) TORCH_CHECK(x.numel() / 784 >= B, "x has fewer than B rows");
+  p2cnn::conv2_dgrad_conv1_wgrad(
+      ptr<float>(slabs2, torch::kFloat32, S2 * mrows * 3136, "slabs2"), int(S2), int(mrows),
+      ptr<uint8_t>(am2, torch::kUInt8, B * 3136, "am2"), ptr<uint8_t>(am1, torch::kUInt8, B * 196 * 32, "am1"),
+      reinterpret_cast<uint16_t*>(ptr<at::BFloat16>(w2q, torch::kBFloat16, 51200, "w2q")),
+      ptr<uint8_t>(x, torch::kUInt8, 784, "x", 1), idx_ptr(idx, B),
+      ptr<float>(wslab1, torch::kFloat32, B * p2cnn::kSlab1, "wslab1"), int(B), stream());
+}
+
+void k_conv_adam(torch::Tensor wslab1, torch::Tensor wslab2, int64_t B, torch::Tensor params, torch::Tensor m,
+                 torch::Tensor v, c10::optional<torch::Tensor> gdump, torch::Tensor w2r, torch::Tensor w2q,
+                 std::vector<int64_t> off, torch::Tensor adam_t, double lr, double b1, double b2, double eps,
+                 double wd) {
+  const c10::DeviceGuard g(params.device());
+  Offsets o = offsets(off);
+  const int64_t n = params_end(o);
+  p2cnn::conv_adam(ptr<float>(wslab1, torch::kFloat32, B * p2cnn::kSlab1, "wslab1"),
+                   ptr<float>(wslab2, torch::kFloat32, B * p2cnn::kSlab2, "wslab2"), int(B),
+                   ptr<float>(params, torch::kFloat32, n, "params"), ptr<float>(m, torch::kFloat32, n, "m"),
+                   ptr<float>(v, torch::kFloat32, n, "v"), optr<float>(gdump, torch::kFloat32, n, "gdump"),
+                   reinterpret_cast<uint16_t*>(ptr<at::BFloat16>(w2r, torch::kBFloat16, 51200, "w2r")),
+                   reinterpret_cast<uint16_t*>(ptr<at::BFloat16>(w2q, torch::kBFloat16, 51200, "w2q")), o,
+                   ptr<int>(adam_t, torch::kInt32, 1, "adam_t", 4), cfg(lr, b1, b2, eps, wd), stream());
+}
+
+void k_pack_shadows(torch::Tensor params, std::vector<int64_t> off, torch::Tensor w2r, torch::Tensor w2q,
+                    torch::Tensor w1bf, torch::Tensor w1tbf) {
+  const c10::DeviceGuard g(params.device());
+  Offsets o = offsets(off);
+  p2cnn::pack_shadows(ptr<float>(params, torch::kFloat32, params_end(o), "params"), o,
+                      reinterpret_cast<uint16_t*>(ptr<at::BFloat16>(w2r, torch::kBFloat16, 51200, "w2r")),
+                      reinterpret_cast<uint16_t*>(ptr<at::BFloat16>(w2q, torch::kBFloat16, 51200, "w2q")),
+                      reinterpret_cast<uint16_t*>(ptr<at::BFloat16>(w1bf, torch::kBFloat16, 2048 * 3136, "w1bf")),
+                      reinterpret_cast<uint16_t*>(ptr<at::BFloat16>(w1tbf, torch::kBFloat16, 2048 * 3136, "w1tbf")),
+                      stream());
+}
+
+}  // namespace
+
+namespace p2cnn {
+void init_attributes();
+}
+
+void register_cnn(pybind11::module& m) {
+  auto c = m.def_submodule("cnn", "fused MNIST-CNN training step kernels");
+  c.def("init", &p2cnn::init_attributes, "set kernel attributes (call before HIP graph capture)");
+  c.def("step_begin", &k_step_begin);
+  c.def("conv1_fwd", &k_conv1_fwd);
+  c.def("conv2_fwd", &k_conv2_fwd);
+  c.def("gemm_skinny", &k_gemm_skinny);
+  c.def("head", &k_head);
+  c.def("fc2_wgrad_adam", &k_fc2_wgrad_adam);
+  c.def("fc1_wgrad_adam", &k_fc1_wgrad_adam);
+  c.def("conv2_wgrad", &k_conv2_wgrad);
+  c.def("conv2_dgrad_conv1_wgrad", &k_conv2_dgrad);
+  c.def("conv_adam", &k_conv_adam);
+  c.def("pack_shadows", &k_pack_shadows);
+}

@@ -1,0 +1,398 @@
+// Fused MNIST-CNN training step -- forward kernels (see cnn.h for the pipeline).
+//
+// Layouts (all bf16 activations are raw uint16 bit patterns):
+//   x    uint8  [N][28*28]           dataset, gathered by idx[b] (the /255 is folded in)
+//   P1   bf16   [B][196][32]         pooled conv1 output, HWC (channels contiguous)
+//   AM1  uint8  [B][196][32]         pool1 argmax (dy*2+dx) or 4 = dead (ReLU zero)
+//   A1   bf16   [mrows][3136]        pooled conv2 output, PyTorch flatten order c*49+y*7+x
+//   A1T  bf16   [3136][mrows]        the same, transposed (B operand of dW1)
+//   AM2  uint8  [B][3136]            pool2 argmax / dead
+//   W2r  bf16   [64][25][32]         conv2 weight, (oc, tap, ic)   -- conv2_fwd B operand
+//   W1bf bf16   [2048][3136]         FC1 weight (row-major = [N][K]) -- FC1 forward
+//   W1T  bf16   [3136][2048]         FC1 weight transposed          -- dA1 = dH W1
+// MFMA: v_mfma_f32_32x32x16_bf16.  Lane l (r = l & 31, h = l >> 5) supplies
+// A[row r][k = 8h + j] and B[k = 8h + j][col r], j = 0..7; the accumulator
+// register i of lane l holds C[row (i&3) + 8(i>>2) + 4h][col r].
+#include "cnn.h"
+#include "common.h"
+
+namespace p2cnn {
+using namespace p2;
+
+typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
+
+P2_DEVICE bf16x8_t as_bf16x8(uint4 v) { return __builtin_bit_cast(bf16x8_t, v); }
+P2_DEVICE f32x16 mfma32(uint4 a, uint4 b, f32x16 c) {
+  return __builtin_amdgcn_mfma_f32_32x32x16_bf16(as_bf16x8(a), as_bf16x8(b), c, 0, 0, 0);
+}
+P2_DEVICE int acc_row(int i, int h) { return (i & 3) + 8 * (i >> 2) + 4 * h; }
+
+// ---------------------------------------------------------------------------
+// 1. step counter
+// ---------------------------------------------------------------------------
+__global__ void step_begin_kernel(int* t) { *t += 1; }
+void step_begin(int* adam_t, hipStream_t s) { hipLaunchKernelGGL(step_begin_kernel, dim3(1), dim3(1), 0, s, adam_t); }
+
+// ---------------------------------------------------------------------------
+// 2. conv1 (1->32, 5x5, pad 2) + bias + ReLU + maxpool 2x2.  Grid (4, B):
+//    part p of image b handles pooled positions [49p, 49p+49).  oc = tid & 31
+//    is fixed per thread, so its 25 taps live in registers; the 6x6 input window
+//    of a pooled output is read once from LDS (broadcast to the 32 oc lanes).
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void conv1_fwd_kernel(const uint8_t* __restrict__ x, const int64_t* __restrict__ idx,
+                                                        const float* __restrict__ w1, const float* __restrict__ b1,
+                                                        uint16_t* __restrict__ p1, uint8_t* __restrict__ am1) {
+  __shared__ float img[32][33];
+  const int b = blockIdx.y, part = blockIdx.x, tid = threadIdx.x;
+  const int64_t row = idx ? idx[b] : b;
+  const uint8_t* src = x + row * (kImg * kImg);
+  for (int i = tid; i < 32 * 32; i += 256) {
+    const int yy = i >> 5, xx = i & 31, sy = yy - 2, sx = xx - 2;
+    float v = 0.f;
+    if (sy >= 0 && sy < kImg && sx >= 0 && sx < kImg) v = float(src[sy * kImg + sx]) * (1.f / 255.f);
+    img[yy][xx] = v;
+  }
+  const int oc = tid & 31;
+  float w[kTaps];
+#pragma unroll
+  for (int t = 0; t < kTaps; ++t) w[t] = w1[oc * kTaps + t];
+  const float bias = b1[oc];
+  __syncthreads();
+  for (int q = tid >> 5; q < 49; q += 8) {
+    const int pp = part * 49 + q, py = pp / 14, px = pp % 14;
+    float win[6][6];
+#pragma unroll
+    for (int i = 0; i < 6; ++i)
+#pragma unroll
+      for (int j = 0; j < 6; ++j) win[i][j] = img[2 * py + i][2 * px + j];
+    float best = -3.4e38f;
+    int arg = 0;
+#pragma unroll
+    for (int d = 0; d < 4; ++d) {
+      const int dy = d >> 1, dx = d & 1;
+      float s = bias;
+#pragma unroll
+      for (int ky = 0; ky < 5; ++ky)
+#pragma unroll
+        for (int kx = 0; kx < 5; ++kx) s = fmaf(w[ky * 5 + kx], win[dy + ky][dx + kx], s);
+      if (s > best) {
+        best = s;
+        arg = d;
+      }
+    }
+    const size_t o = (size_t(b) * 196 + pp) * kC1 + oc;
+    p1[o] = f32_to_bf16(fmaxf(best, 0.f));
+    am1[o] = best > 0.f ? uint8_t(arg) : uint8_t(4);
+  }
+}
+
+void conv1_fwd(const uint8_t* x, const int64_t* idx, const float* params, Offsets off, uint16_t* p1, uint8_t* am1,
+               int B, hipStream_t s) {
+  hipLaunchKernelGGL(conv1_fwd_kernel, dim3(4, B), dim3(256), 0, s, x, idx, params + off.c1w, params + off.c1b, p1,
+                     am1);
+}
+
+// ---------------------------------------------------------------------------
+// 3. conv2 (32->64, 5x5, pad 2) as implicit GEMM on MFMA + bias/ReLU/maxpool.
+//    Grid (2, B): block = (oc half, image).  GEMM M = 196 positions (7 wave
+//    tiles of 32), N = 32 oc, K = 25 taps x 32 ic with ic fastest, so every
+//    A/B fragment is ONE 16-byte LDS read (ds_read_b128) from the HWC image /
+//    the (oc, tap, ic) weight copy.  Pixel stride 40 channels (80 B) spreads
+//    the 16-lane b128 groups over all 64 banks.
+// ---------------------------------------------------------------------------
+constexpr int kICP = 40;                                  // padded channels per pixel / weight row
+constexpr int kImgLds = 18 * 18 * kICP * 2;               // 25920 B
+constexpr int kW2Lds = 32 * kTaps * kICP * 2;             // 64000 B
+constexpr int kConv2Lds = kImgLds + kW2Lds;
+
+__global__ __launch_bounds__(448) void conv2_fwd_kernel(const uint16_t* __restrict__ p1,
+                                                        const uint16_t* __restrict__ w2r,
+                                                        const float* __restrict__ b2, uint16_t* __restrict__ a1,
+                                                        uint16_t* __restrict__ a1t, uint8_t* __restrict__ am2,
+                                                        int mrows) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  uint16_t* simg = reinterpret_cast<uint16_t*>(smem);
+  uint16_t* sw = reinterpret_cast<uint16_t*>(smem + kImgLds);
+  const int b = blockIdx.y, nh = blockIdx.x, tid = threadIdx.x;
+  const uint4 zero4 = make_uint4(0, 0, 0, 0);
+  for (int i = tid; i < kImgLds / 16; i += 448) reinterpret_cast<uint4*>(simg)[i] = zero4;
+  __syncthreads();
+  for (int i = tid; i < 196 * 4; i += 448) {
+    const int pix = i >> 2, q = i & 3, y = pix / 14, xx = pix % 14;
+    const uint4 v = reinterpret_cast<const uint4*>(p1 + (size_t(b) * 196 + pix) * kC1)[q];
+    *reinterpret_cast<uint4*>(simg + ((y + 2) * 18 + (xx + 2)) * kICP + q * 8) = v;
+  }
+  for (int i = tid; i < 32 * kTaps * 4; i += 448) {
+    const int rr = i >> 2, q = i & 3;  // rr = oc_local * 25 + tap
+    const uint4 v = reinterpret_cast<const uint4*>(w2r + (size_t(nh * 32) * kTaps + rr) * kC1)[q];
+    *reinterpret_cast<uint4*>(sw + rr * kICP + q * 8) = v;
+  }
+  __syncthreads();
+
+  const int wave = tid >> 6, lane = tid & 63, r = lane & 31, h = lane >> 5;
+  const int m = wave * 32 + r;
+  const int mm = m < 196 ? m : 195;
+  const int y = mm / 14, xx = mm % 14;
+  f32x16 acc = {};
+#pragma unroll 10
+  for (int s = 0; s < 50; ++s) {
+    const int t = s >> 1, ky = t / 5, kx = t % 5, ic0 = (s & 1) * 16 + 8 * h;
+    const uint4 av = *reinterpret_cast<const uint4*>(simg + ((y + ky) * 18 + (xx + kx)) * kICP + ic0);
+    const uint4 bv = *reinterpret_cast<const uint4*>(sw + (r * kTaps + t) * kICP + ic0);
+    acc = mfma32(av, bv, acc);
+  }
+  __syncthreads();  // image no longer needed: reuse LDS for the conv output
+  float* sout = reinterpret_cast<float*>(smem);  // [196][32] f32 = 25088 B
+  const float bias = b2[nh * 32 + r];
+#pragma unroll
+  for (int i = 0; i < 16; ++i) {
+    const int row = wave * 32 + acc_row(i, h);
+    if (row < 196) sout[row * 32 + r] = fmaxf(acc[i] + bias, 0.f);
+  }
+  __syncthreads();
+  for (int i = tid; i < 49 * 32; i += 448) {
+    const int oc = i / 49, pp = i % 49, py = pp / 7, px = pp % 7;
+    float best = -1.f;
+    int arg = 0;
+#pragma unroll
+    for (int d = 0; d < 4; ++d) {
+      const float v = sout[((2 * py + (d >> 1)) * 14 + 2 * px + (d & 1)) * 32 + oc];
+      if (v > best) {
+        best = v;
+        arg = d;
+      }
+    }
+    const int feat = (nh * 32 + oc) * 49 + pp;
+    const uint16_t hv = f32_to_bf16(best);
+    a1[size_t(b) * kFeat + feat] = hv;
+    a1t[size_t(feat) * mrows + b] = hv;
+    am2[size_t(b) * kFeat + feat] = best > 0.f ? uint8_t(arg) : uint8_t(4);
+  }
+}
+
+void init_fwd_attributes() {
+  P2_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(conv2_fwd_kernel),
+                               hipFuncAttributeMaxDynamicSharedMemorySize, kConv2Lds));
+}
+
+void conv2_fwd(const uint16_t* p1, const uint16_t* w2r, const float* params, Offsets off, uint16_t* a1, uint16_t* a1t,
+               uint8_t* am2, int B, int mrows, hipStream_t s) {
+  hipLaunchKernelGGL(conv2_fwd_kernel, dim3(2, B), dim3(448), kConv2Lds, s, p1, w2r, params + off.c2b, a1, a1t, am2,
+                     mrows);
+}
+
+// ---------------------------------------------------------------------------
+// 4/7. Skinny GEMM  slabs[s][m][n] = sum_{k in split s} A[m][k] * Bt[n][k]
+//    (M = mrows = 32*MT rows, N multiple of 32, K multiple of 64).  Block =
+//    32 output columns x one K split; its 4 waves take interleaved 64-wide K
+//    groups.  Each lane streams 64 contiguous bytes of an A row and of a Bt row
+//    per group (the two half-waves cover a full 128-B line), and the group's
+//    four 16-wide MFMA k-steps consume them with the SAME k permutation on both
+//    operands, so no shuffles are needed.  Waves reduce through LDS; one fp32
+//    slab per split keeps the result deterministic.
+// ---------------------------------------------------------------------------
+template <int MT>
+__global__ __launch_bounds__(256) void gemm_skinny_kernel(const uint16_t* __restrict__ A,
+                                                          const uint16_t* __restrict__ Bt, float* __restrict__ slabs,
+                                                          int N, int K, int S) {
+  __shared__ float red[4 * MT * 16 * 64];
+  const int nt = blockIdx.x, sp = blockIdx.y, tid = threadIdx.x;
+  const int wave = tid >> 6, lane = tid & 63, r = lane & 31, h = lane >> 5;
+  const int n0 = nt * 32;
+  const int ng = K / 64, gps = (ng + S - 1) / S;
+  const int g0 = sp * gps, g1 = min(ng, g0 + gps);
+  f32x16 acc[MT];
+#pragma unroll
+  for (int mt = 0; mt < MT; ++mt) acc[mt] = f32x16{};
+  const uint16_t* brow = Bt + size_t(n0 + r) * K + 32 * h;
+  const uint16_t* arow[MT];
+#pragma unroll
+  for (int mt = 0; mt < MT; ++mt) arow[mt] = A + size_t(mt * 32 + r) * K + 32 * h;
+#pragma unroll 2
+  for (int g = g0 + wave; g < g1; g += 4) {
+    const int k0 = g * 64;
+    uint4 bq[4], aq[MT][4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) bq[q] = ld_nt16(brow + k0 + q * 8);
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) aq[mt][q] = reinterpret_cast<const uint4*>(arow[mt] + k0)[q];
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt) acc[mt] = mfma32(aq[mt][q], bq[q], acc[mt]);
+  }
+#pragma unroll
+  for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+    for (int i = 0; i < 16; ++i) red[((wave * MT + mt) * 16 + i) * 64 + lane] = acc[mt][i];
+  __syncthreads();
+  const int mrows = MT * 32;
+  for (int e = tid; e < MT * 1024; e += 256) {
+    const float sum = red[e] + red[MT * 1024 + e] + red[2 * MT * 1024 + e] + red[3 * MT * 1024 + e];
+    const int mt = e >> 10, i = (e >> 6) & 15, ln = e & 63;
+    const int row = mt * 32 + acc_row(i, ln >> 5), col = ln & 31;
+    slabs[(size_t(sp) * mrows + row) * N + n0 + col] = sum;
+  }
+}
+
+void gemm_skinny(const uint16_t* A, const uint16_t* Bt, float* slabs, int mrows, int N, int K, int S, hipStream_t s) {
+  const dim3 grid(N / 32, S);
+  if (mrows == 32)
+    hipLaunchKernelGGL(gemm_skinny_kernel<1>, grid, dim3(256), 0, s, A, Bt, slabs, N, K, S);
+  else
+    hipLaunchKernelGGL(gemm_skinny_kernel<2>, grid, dim3(256), 0, s, A, Bt, slabs, N, K, S);
+}
+
+// ---------------------------------------------------------------------------
+// 5. Head: FC1 epilogue (split-K reduce + bias + ReLU), FC2, softmax
+//    cross-entropy (mean over the batch), accuracy, and the backward pass down
+//    to dH = relu'(H) * (dlogits x W2).  Grid = mrows blocks (one per sample;
+//    padding rows write zeros so the batch-dimension GEMMs stay exact).
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void head_kernel(const float* __restrict__ slabs, int S, int mrows,
+                                                   const float* __restrict__ bl1, const float* __restrict__ wl2,
+                                                   const float* __restrict__ bl2, const int64_t* __restrict__ labels,
+                                                   const int64_t* __restrict__ idx, int B, int train,
+                                                   uint16_t* __restrict__ H, uint16_t* __restrict__ dH,
+                                                   uint16_t* __restrict__ dHt, float* __restrict__ dlogits,
+                                                   float* __restrict__ stats) {
+  __shared__ float red[4][kCls];
+  __shared__ float dl[kCls];
+  const int b = blockIdx.x, tid = threadIdx.x, k0 = tid * 8;
+  const int wave = tid >> 6, lane = tid & 63;
+  if (b >= B) {
+    if (train) {
+      reinterpret_cast<uint4*>(dH + size_t(b) * kHid + k0)[0] = make_uint4(0, 0, 0, 0);
+      reinterpret_cast<uint4*>(H + size_t(b) * kHid + k0)[0] = make_uint4(0, 0, 0, 0);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) dHt[size_t(k0 + j) * mrows + b] = 0;
+      if (tid < kCls) dlogits[b * kCls + tid] = 0.f;
+    }
+    return;
+  }
+  float hv[8];
+  {
+    const float4* bp = reinterpret_cast<const float4*>(bl1 + k0);
+    float4 u = bp[0], w = bp[1];
+    hv[0] = u.x; hv[1] = u.y; hv[2] = u.z; hv[3] = u.w; hv[4] = w.x; hv[5] = w.y; hv[6] = w.z; hv[7] = w.w;
+    for (int s = 0; s < S; ++s) {
+      const float4* sp = reinterpret_cast<const float4*>(slabs + (size_t(s) * mrows + b) * kHid + k0);
+      u = sp[0];
+      w = sp[1];
+      hv[0] += u.x; hv[1] += u.y; hv[2] += u.z; hv[3] += u.w; hv[4] += w.x; hv[5] += w.y; hv[6] += w.z; hv[7] += w.w;
+    }
+  }
+  uint4 hb;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) hv[j] = fmaxf(hv[j], 0.f);
+  hb.x = pack_bf16x2(hv[0], hv[1]);
+  hb.y = pack_bf16x2(hv[2], hv[3]);
+  hb.z = pack_bf16x2(hv[4], hv[5]);
+  hb.w = pack_bf16x2(hv[6], hv[7]);
+  reinterpret_cast<uint4*>(H + size_t(b) * kHid + k0)[0] = hb;
+
+  float part[kCls];
+#pragma unroll
+  for (int c = 0; c < kCls; ++c) {
+    const float4* wp = reinterpret_cast<const float4*>(wl2 + size_t(c) * kHid + k0);
+    const float4 u = wp[0], w = wp[1];
+    part[c] = hv[0] * u.x + hv[1] * u.y + hv[2] * u.z + hv[3] * u.w + hv[4] * w.x + hv[5] * w.y + hv[6] * w.z +
+              hv[7] * w.w;
+    part[c] = wave_sum(part[c]);
+  }
+  if (lane == 0)
+#pragma unroll
+    for (int c = 0; c < kCls; ++c) red[wave][c] = part[c];
+  __syncthreads();
+  if (tid == 0) {
+    float lg[kCls], mx = -3.4e38f;
+    int am = 0;
+#pragma unroll
+    for (int c = 0; c < kCls; ++c) {
+      lg[c] = red[0][c] + red[1][c] + red[2][c] + red[3][c] + bl2[c];
+      if (lg[c] > mx) {
+        mx = lg[c];
+        am = c;
+      }
+    }
+    float se = 0.f;
+#pragma unroll
+    for (int c = 0; c < kCls; ++c) se += __expf(lg[c] - mx);
+    const float lse = mx + __logf(se);
+    const int y = int(labels[idx ? idx[b] : b]);
+    atomicAdd(&stats[0], lse - lg[y]);
+    atomicAdd(&stats[1], am == y ? 1.f : 0.f);
+    const float invB = 1.f / float(B);
+#pragma unroll
+    for (int c = 0; c < kCls; ++c) {
+      const float g = (__expf(lg[c] - lse) - (c == y ? 1.f : 0.f)) * invB;
+      dl[c] = g;
+      if (train) dlogits[b * kCls + c] = g;
+    }
+  }
+  if (!train) return;
+  __syncthreads();
+  float g[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) g[j] = 0.f;
+#pragma unroll
+  for (int c = 0; c < kCls; ++c) {
+    const float d = dl[c];
+    const float4* wp = reinterpret_cast<const float4*>(wl2 + size_t(c) * kHid + k0);
+    const float4 u = wp[0], w = wp[1];
+    g[0] = fmaf(d, u.x, g[0]); g[1] = fmaf(d, u.y, g[1]); g[2] = fmaf(d, u.z, g[2]); g[3] = fmaf(d, u.w, g[3]);
+    g[4] = fmaf(d, w.x, g[4]); g[5] = fmaf(d, w.y, g[5]); g[6] = fmaf(d, w.z, g[6]); g[7] = fmaf(d, w.w, g[7]);
+  }
+#pragma unroll
+  for (int j = 0; j < 8; ++j) g[j] = hv[j] > 0.f ? g[j] : 0.f;
+  uint4 gb;
+  gb.x = pack_bf16x2(g[0], g[1]);
+  gb.y = pack_bf16x2(g[2], g[3]);
+  gb.z = pack_bf16x2(g[4], g[5]);
+  gb.w = pack_bf16x2(g[6], g[7]);
+  reinterpret_cast<uint4*>(dH + size_t(b) * kHid + k0)[0] = gb;
+  const uint16_t* gs = reinterpret_cast<const uint16_t*>(&gb);
+#pragma unroll
+  for (int j = 0; j < 8; ++j) dHt[size_t(k0 + j) * mrows + b] = gs[j];
+}
+
+void head(const float* slabs, int S, int mrows, const float* params, Offsets off, const int64_t* labels,
+          const int64_t* idx, int B, int train, uint16_t* H, uint16_t* dH, uint16_t* dHt, float* dlogits,
+          float* stats, hipStream_t s) {
+  hipLaunchKernelGGL(head_kernel, dim3(train ? mrows : B), dim3(256), 0, s, slabs, S, mrows, params + off.l1b,
+                     params + off.l2w, params + off.l2b, labels, idx, B, train, H, dH, dHt, dlogits, stats);
+}
+
+// ---------------------------------------------------------------------------
+// bf16 shadows from fp32 params (used after set_parameters / before training)
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void pack_shadows_kernel(const float* __restrict__ params, Offsets off,
+                                                           uint16_t* __restrict__ w2r, uint16_t* __restrict__ w2q,
+                                                           uint16_t* __restrict__ w1bf,
+                                                           uint16_t* __restrict__ w1tbf) {
+  const int64_t n2 = int64_t(kC2) * kC1 * kTaps, n1 = int64_t(kHid) * kFeat;
+  const int64_t stride = int64_t(gridDim.x) * blockDim.x;
+  for (int64_t e = int64_t(blockIdx.x) * blockDim.x + threadIdx.x; e < n2 + n1; e += stride) {
+    if (e < n2) {
+      const int oc = int(e / (kC1 * kTaps)), rem = int(e % (kC1 * kTaps)), ic = rem / kTaps, t = rem % kTaps;
+      const uint16_t v = f32_to_bf16(params[off.c2w + e]);
+      w2r[(oc * kTaps + t) * kC1 + ic] = v;
+      w2q[(ic * kTaps + t) * kC2 + oc] = v;
+    } else {
+      const int64_t j = e - n2;
+      const int n = int(j / kFeat), k = int(j % kFeat);
+      const uint16_t v = f32_to_bf16(params[off.l1w + j]);
+      w1bf[j] = v;
+      w1tbf[size_t(k) * kHid + n] = v;
+    }
+  }
+}
+
+void pack_shadows(const float* params, Offsets off, uint16_t* w2r, uint16_t* w2q, uint16_t* w1bf, uint16_t* w1tbf,
+                  hipStream_t s) {
+  hipLaunchKernelGGL(pack_shadows_kernel, dim3(2048), dim3(256), 0, s, params, off, w2r, w2q, w1bf, w1tbf);
+}
+
+}  // namespace p2cnn

@@ -1,0 +1,66 @@
+// Shared helpers for p2pfl_amd HIP kernels (gfx950 / CDNA4, wave64).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <hip/hip_bf16.h>
+#include <stdint.h>
+#include <stdexcept>
+
+#define P2_DEVICE __device__ __forceinline__
+
+namespace p2 {
+
+constexpr int kWave = 64;
+
+// clang vector types: usable with __builtin_nontemporal_* and MFMA builtins
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef short bf16x8 __attribute__((ext_vector_type(8)));
+typedef unsigned short u16x4 __attribute__((ext_vector_type(4)));
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+
+// 16-byte streaming (non-temporal) load: for data read once (weights streamed
+// through a GEMM) so it does not evict reused operands from L2/MALL.
+P2_DEVICE uint4 ld_nt16(const void* p) {
+  const u32x4 v = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(p));
+  return __builtin_bit_cast(uint4, v);
+}
+
+// bf16 <-> f32 (round-to-nearest-even), bit-level so it vectorises cleanly.
+P2_DEVICE float bf16_to_f32(uint16_t h) { return __uint_as_float(uint32_t(h) << 16); }
+P2_DEVICE uint16_t f32_to_bf16(float f) {
+  uint32_t u = __float_as_uint(f);
+  if ((u & 0x7f800000u) == 0x7f800000u && (u & 0x7fffffu)) return uint16_t((u >> 16) | 0x40);  // quiet NaN
+  u += 0x7fffu + ((u >> 16) & 1u);
+  return uint16_t(u >> 16);
+}
+P2_DEVICE uint32_t pack_bf16x2(float lo, float hi) {
+  return uint32_t(f32_to_bf16(lo)) | (uint32_t(f32_to_bf16(hi)) << 16);
+}
+
+// Grid size for a grid-stride memory-bound kernel: enough blocks to cover the
+// 256 CUs several times over, capped (Guideline 11).
+inline int stream_grid(int64_t work_items, int block) {
+  int64_t g = (work_items + block - 1) / block;
+  if (g > 2048) g = 2048;
+  if (g < 1) g = 1;
+  return int(g);
+}
+
+P2_DEVICE float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+P2_DEVICE float wave_max(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+
+}  // namespace p2
+
+#define P2_CHECK(expr)                                                        \
+  do {                                                                        \
+    hipError_t _e = (expr);                                                   \
+    if (_e != hipSuccess) throw std::runtime_error(hipGetErrorString(_e));    \
+  } while (0)

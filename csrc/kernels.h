@@ -1,0 +1,29 @@
+// Host-side launch API of the p2pfl_amd HIP kernels (raw pointers + stream;
+// no torch headers, so kernel files compile fast and stay reusable from C++).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace p2 {
+
+constexpr int kMaxInputs = 16;
+
+// out[i] = sum_j weights[j] * srcs[j][i]   (fp32; k may exceed kMaxInputs)
+void weighted_sum(const float* const* srcs, const float* weights, int k, float* out, int64_t n, hipStream_t s);
+
+struct AdamParams {
+  float lr, beta1, beta2, eps, weight_decay;
+  float step_size;     // lr / (1 - beta1^t)
+  float inv_sqrt_bc2;  // 1 / sqrt(1 - beta2^t)
+  int decoupled;
+};
+void adam_step(float* p, const float* g, float* m, float* v, uint16_t* p_bf16, int64_t n, const AdamParams& h,
+               hipStream_t s);
+
+struct SgdParams {
+  float lr, momentum, dampening, weight_decay;
+  int nesterov, first_step;
+};
+void sgd_step(float* p, const float* g, float* buf, uint16_t* p_bf16, int64_t n, const SgdParams& h, hipStream_t s);
+
+}  // namespace p2

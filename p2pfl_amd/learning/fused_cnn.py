@@ -1,0 +1,288 @@
+"""MI355X-native training engine for the reference MNIST CNN.
+
+:class:`FusedCNNEngine` runs the whole training step of
+:class:`~p2pfl_amd.models.cnn.CNN` through the hand-written HIP kernels of
+``csrc/cnn_fwd.hip`` / ``csrc/cnn_bwd.hip`` (pipeline in ``csrc/cnn.h``): no
+autograd, no per-layer optimizer launches, bf16 MFMA compute with fp32 master
+weights and fp32 Adam state kept in the model's flat arena.  A whole epoch
+(every step, with its data indices) is captured ONCE as a HIP graph and then
+replayed, so a step costs ~10 kernel boundaries and zero host work.
+
+:class:`FusedCNNLearner` is the :class:`~p2pfl_amd.learning.learner.NodeLearner`
+on top of it (same parameter/wire behaviour as ``TorchLearner``, so fused and
+torch peers interoperate).  It is selected automatically for ``CNN`` models on
+a GPU by :func:`auto_learner`.
+"""
+
+from __future__ import annotations
+
+import math
+import threading
+from typing import Any, Dict, List, Optional, Tuple
+
+import torch
+
+from p2pfl_amd import ops
+from p2pfl_amd.learning.arena import FlatParams, ModuleArena
+from p2pfl_amd.learning.torch_learner import TorchLearner
+from p2pfl_amd.management.logger import logger
+
+_NAMES = ("conv1.weight", "conv1.bias", "conv2.weight", "conv2.bias", "l1.weight", "l1.bias", "l2.weight", "l2.bias")
+FEAT, HID = 3136, 2048
+
+
+class FusedCNNEngine:
+    """Kernel-level forward/backward/Adam for the MNIST CNN on one GPU."""
+
+    def __init__(
+        self,
+        model: torch.nn.Module,
+        device: Optional[torch.device] = None,
+        lr: float = 1e-3,
+        betas: Tuple[float, float] = (0.9, 0.999),
+        eps: float = 1e-8,
+        weight_decay: float = 0.0,
+        mrows: int = 32,
+        arena: Optional[ModuleArena] = None,
+        split_fc1: int = 7,
+        split_dA1: int = 4,
+    ) -> None:
+        self.C = ops.ext().cnn
+        self.C.init()
+        self.device = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
+        model.to(self.device)
+        self.arena = arena if arena is not None else ModuleArena(model, device=self.device)
+        lay = self.arena.layout
+        if tuple(lay.names) != _NAMES:
+            raise ValueError(f"FusedCNNEngine needs the reference CNN layout {_NAMES}, got {lay.names}")
+        shapes = dict(zip(lay.names, lay.shapes))
+        if shapes["conv1.weight"] != (32, 1, 5, 5) or shapes["l2.weight"][1] != HID or shapes["l2.weight"][0] != 10:
+            raise ValueError("unsupported CNN configuration (needs 1x28x28 input, 10 classes)")
+        self.off: List[int] = [int(o) for o in lay.offsets]
+        self.lr, self.betas, self.eps, self.wd = lr, betas, eps, weight_decay
+        self.mrows = mrows
+        self.S1, self.S2 = split_fc1, split_dA1
+        dev, bf = self.device, torch.bfloat16
+        z = lambda *s, dt=torch.float32: torch.zeros(*s, dtype=dt, device=dev)  # noqa: E731
+        n = self.arena.flat.numel()
+        self.m, self.v = z(n), z(n)
+        self.adam_t = torch.zeros(1, dtype=torch.int32, device=dev)
+        # bf16 weight shadows in kernel-friendly layouts
+        self.w2r, self.w2q = z(51200, dt=bf), z(51200, dt=bf)
+        self.w1bf, self.w1tbf = z(HID * FEAT, dt=bf), z(HID * FEAT, dt=bf)
+        # activations / workspaces (sized for mrows samples)
+        M = mrows
+        self.p1, self.am1 = z(M * 196 * 32, dt=bf), z(M * 196 * 32, dt=torch.uint8)
+        self.a1, self.a1t, self.am2 = z(M * FEAT, dt=bf), z(FEAT * M, dt=bf), z(M * FEAT, dt=torch.uint8)
+        self.slabs1 = z(self.S1 * M * HID)
+        self.H, self.dH, self.dHt = z(M * HID, dt=bf), z(M * HID, dt=bf), z(HID * M, dt=bf)
+        self.dlogits = z(M * 10)
+        self.slabs2 = z(self.S2 * M * FEAT)
+        self.wslab1, self.wslab2 = z(M * 832), z(M * 51264)
+        self.stats = z(2)
+        self.gdump: Optional[torch.Tensor] = None
+        self.pack_shadows()
+
+    # -- parameters -------------------------------------------------------
+    @property
+    def params(self) -> torch.Tensor:
+        return self.arena.flat
+
+    def pack_shadows(self) -> None:
+        """Refresh the bf16 weight copies after the fp32 parameters changed externally."""
+        self.C.pack_shadows(self.params, self.off, self.w2r, self.w2q, self.w1bf, self.w1tbf)
+
+    def reset_optimizer(self) -> None:
+        self.m.zero_()
+        self.v.zero_()
+        self.adam_t.zero_()
+
+    # -- kernels ------------------------------------------------------------
+    def _adam(self):
+        return (self.lr, self.betas[0], self.betas[1], self.eps, self.wd)
+
+    def forward(self, x: torch.Tensor, labels: torch.Tensor, idx: Optional[torch.Tensor], B: int, stats: torch.Tensor, train: bool) -> None:
+        C, M = self.C, self.mrows
+        C.conv1_fwd(x, idx, self.params, self.off, self.p1, self.am1, B)
+        C.conv2_fwd(self.p1, self.w2r, self.params, self.off, self.a1, self.a1t, self.am2, B, M)
+        C.gemm_skinny(self.a1, self.w1bf, self.slabs1, M, HID, FEAT, self.S1)
+        C.head(self.slabs1, self.S1, M, self.params, self.off, labels, idx, B, train, self.H, self.dH, self.dHt, self.dlogits, stats)
+
+    def train_step_async(self, x: torch.Tensor, labels: torch.Tensor, idx: Optional[torch.Tensor], B: int, stats: torch.Tensor) -> None:
+        """Enqueue one training step (no host sync; graph-capturable)."""
+        if B > self.mrows:
+            raise ValueError(f"batch {B} > engine capacity {self.mrows}")
+        C, M, a = self.C, self.mrows, self._adam()
+        C.step_begin(self.adam_t)
+        self.forward(x, labels, idx, B, stats, True)
+        C.fc2_wgrad_adam(self.dlogits, self.H, B, self.params, self.m, self.v, self.gdump, self.off, self.adam_t, *a)
+        C.gemm_skinny(self.dH, self.w1tbf, self.slabs2, M, FEAT, HID, self.S2)
+        C.fc1_wgrad_adam(self.dHt, self.a1t, M, self.params, self.m, self.v, self.gdump, self.w1bf, self.w1tbf, self.off, self.adam_t, *a)
+        C.conv2_wgrad(self.slabs2, self.S2, M, self.am2, self.p1, self.wslab2, B)
+        C.conv2_dgrad_conv1_wgrad(self.slabs2, self.S2, M, self.am2, self.am1, self.w2q, x, idx, self.wslab1, B)
+        C.conv_adam(self.wslab1, self.wslab2, B, self.params, self.m, self.v, self.gdump, self.w2r, self.w2q, self.off, self.adam_t, *a)
+
+    def train_step(self, x: torch.Tensor, y: torch.Tensor) -> float:
+        """Convenience: one step on a uint8 batch ``x`` [B,1,28,28] with labels ``y``; returns the loss."""
+        B = int(y.shape[0])
+        self.stats.zero_()
+        self.train_step_async(x.contiguous(), y.to(torch.int64).contiguous(), None, B, self.stats)
+        return float(self.stats[0]) / B
+
+    @torch.no_grad()
+    def logits_reference(self, x: torch.Tensor) -> torch.Tensor:
+        return self.arena.module(x.float() / 255.0)
+
+
+class _EpochGraph:
+    """One captured HIP graph per (dataset, batch plan)."""
+
+    def __init__(self, graph: Optional[torch.cuda.CUDAGraph], key: Tuple) -> None:
+        self.graph = graph
+        self.key = key
+
+
+class FusedCNNLearner(TorchLearner):
+    """NodeLearner running the MNIST CNN through the fused HIP engine.
+
+    Parameters, wire encoding and device snapshots come from
+    :class:`TorchLearner` (same arena layout); ``fit``/``evaluate`` replay HIP
+    graphs of whole epochs / evaluation passes.
+    """
+
+    def __init__(self, model: Any, data: Any, self_addr: str, epochs: int, device: Optional[torch.device] = None, use_graphs: bool = True, **kw) -> None:
+        super().__init__(model, data, self_addr, epochs, device=device, fused_optimizer=False)
+        if self.device.type != "cuda":
+            raise RuntimeError("FusedCNNLearner needs an AMD GPU")
+        opt = model.configure_optimizers() if hasattr(model, "configure_optimizers") else None
+        lr = float(opt.param_groups[0]["lr"]) if opt is not None else 1e-3
+        betas = tuple(opt.param_groups[0].get("betas", (0.9, 0.999))) if opt is not None else (0.9, 0.999)
+        eps = float(opt.param_groups[0].get("eps", 1e-8)) if opt is not None else 1e-8
+        wd = float(opt.param_groups[0].get("weight_decay", 0.0)) if opt is not None else 0.0
+        self.engine = FusedCNNEngine(model, self.device, lr=lr, betas=betas, eps=eps, weight_decay=wd, arena=self.arena)
+        self.use_graphs = use_graphs
+        self._graphs: Dict[str, _EpochGraph] = {}
+        self._lock = threading.Lock()
+        self._stream = torch.cuda.Stream(self.device)
+        self._dirty_shadows = False
+
+    # -- parameters: keep the bf16 shadows in sync -------------------------
+    def set_parameters(self, params) -> None:
+        super().set_parameters(params)
+        with torch.cuda.stream(torch.cuda.current_stream(self.device)):
+            self.engine.pack_shadows()
+
+    # -- plans ----------------------------------------------------------------
+    def _plan(self, n: int, B: int) -> List[Tuple[int, int]]:
+        return [(s, min(B, n - s)) for s in range(0, n, B)]
+
+    def _run(self, name: str, loader, train: bool, perm: Optional[torch.Tensor]) -> torch.Tensor:
+        """Enqueue a pass over ``loader``; returns a [steps, 2] stats tensor (loss sum, correct)."""
+        eng = self.engine
+        n = len(loader.dataset)
+        B = loader.batch_size
+        plan = self._plan(n, B)
+        key = (name, n, B, loader.x.data_ptr(), loader.y.data_ptr())
+        g = self._graphs.get(name)
+        if g is None or g.key != key:
+            g = self._capture(name, loader, plan, train, key)
+            self._graphs[name] = g
+        if perm is not None:
+            g.perm.copy_(perm, non_blocking=True)
+        g.stats.zero_()
+        if g.graph is not None:
+            g.graph.replay()
+        else:
+            self._enqueue(loader, plan, train, g.perm, g.stats)
+        return g.stats
+
+    def _enqueue(self, loader, plan, train, perm, stats) -> None:
+        x = loader.x.reshape(-1, 784)
+        y = loader.y
+        for j, (s, b) in enumerate(plan):
+            idx = perm[s : s + b]
+            st = stats[j] if train else stats[0]
+            if train:
+                self.engine.train_step_async(x, y, idx, b, st)
+            else:
+                self.engine.forward(x, y, idx, b, st, False)
+
+    def _capture(self, name, loader, plan, train, key) -> _EpochGraph:
+        n = len(loader.dataset)
+        eg = _EpochGraph(None, key)
+        eg.perm = torch.arange(n, dtype=torch.int64, device=self.device)
+        eg.stats = torch.zeros((len(plan) if train else 1, 4), dtype=torch.float32, device=self.device)
+        if not self.use_graphs:
+            return eg
+        # capture on a side stream; state that the graph mutates (weights,
+        # Adam moments, step counter) is saved and restored around the capture
+        torch.cuda.synchronize(self.device)
+        saved = [t.clone() for t in (self.engine.params, self.engine.m, self.engine.v, self.engine.adam_t)]
+        graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(graph, stream=self._stream):
+            self._enqueue(loader, plan, train, eg.perm, eg.stats)
+        torch.cuda.synchronize(self.device)
+        for dst, src in zip((self.engine.params, self.engine.m, self.engine.v, self.engine.adam_t), saved):
+            dst.copy_(src)
+        self.engine.pack_shadows()
+        eg.graph = graph
+        return eg
+
+    # -- NodeLearner ------------------------------------------------------
+    def fit(self) -> None:
+        if self.epochs <= 0 or self.model is None:
+            return
+        self._interrupt.clear()
+        with self._lock:
+            self.engine.reset_optimizer()  # Adam re-created per fit (reference quirk Q23)
+            loader = self.data.train_dataloader()
+            for _ in range(self.epochs):
+                if self._interrupt.is_set():
+                    return
+                with logger.span(self._addr, "train_epoch"):
+                    stats = self._run("train", loader, True, loader.permutation())
+                    st = stats.cpu()
+                steps = st.shape[0]
+                self._step += steps
+                bs = loader.batch_size
+                n = len(loader.dataset)
+                per_step = [float(st[j, 0]) / min(bs, n - j * bs) for j in range(steps)]
+                every = max(1, self.log_every_n_steps)
+                for j in range(steps):
+                    if (self._step - steps + j + 1) % every == 0:
+                        self._log("train_loss", per_step[j], step=self._step - steps + j + 1)
+                self.last_train_loss = sum(float(st[j, 0]) for j in range(steps)) / n
+                self._validate()
+
+    def _eval_pass(self, name: str, loader) -> Dict[str, float]:
+        with self._lock:
+            st = self._run(name, loader, False, None).cpu()
+        n = max(1, len(loader.dataset))
+        return {"loss": float(st[0, 0]) / n, "metric": float(st[0, 1]) / n}
+
+    def _validate(self) -> None:
+        loader = self.data.val_dataloader()
+        if loader is None or len(loader.dataset) == 0:
+            return
+        r = self._eval_pass("val", loader)
+        self._log("val_loss", r["loss"], step=self._step)
+        self._log("val_metric", r["metric"], step=self._step)
+
+    def evaluate(self) -> Dict[str, float]:
+        if self.epochs <= 0 or self.model is None:
+            return {}
+        with logger.span(self._addr, "evaluate"):
+            r = self._eval_pass("test", self.data.test_dataloader())
+        results = {"test_loss": r["loss"], "test_metric": r["metric"]}
+        for k, v in results.items():
+            self._log(k, v)
+        return results
+
+
+def auto_learner(model: Any, data: Any, self_addr: str, epochs: int, **kw):
+    """Pick the fastest learner for ``model`` on this machine."""
+    from p2pfl_amd.models.cnn import CNN
+
+    if isinstance(model, CNN) and torch.cuda.is_available() and ops.available():
+        return FusedCNNLearner(model, data, self_addr, epochs, **kw)
+    return TorchLearner(model, data, self_addr, epochs, **kw)

@@ -204,7 +204,7 @@ class TorchLearner(NodeLearner):
                         self._step += 1
                         if self.log_every_n_steps and self._step % self.log_every_n_steps == 0:
                             for k, v in model.pop_logged().items():
-                                logger.log_metric(self._addr, k, float(v), step=self._step)
+                                self._log(k, float(v), step=self._step)
                 if self.arena is not None and not self.arena.grads_bound():
                     self.arena.rebind_grads()
                 self._validate()
@@ -232,7 +232,7 @@ class TorchLearner(NodeLearner):
         if loader is None or len(loader.dataset) == 0:
             return
         for k, v in self._run_eval(loader, self.model.validation_step).items():
-            logger.log_metric(self._addr, k, v, step=self._step)
+            self._log(k, v, step=self._step)
 
     def evaluate(self) -> Dict[str, float]:
         if self.epochs <= 0 or self.model is None:
@@ -240,8 +240,14 @@ class TorchLearner(NodeLearner):
         with logger.span(self._addr, "evaluate"):
             results = self._run_eval(self.data.test_dataloader(), self.model.test_step)
         for k, v in results.items():
-            logger.log_metric(self._addr, k, v)
+            self._log(k, v)
         return results
+
+    def _log(self, key: str, value: float, step=None) -> None:
+        try:
+            logger.log_metric(self._addr, key, value, step=step)
+        except Exception:
+            pass  # learner used outside a registered node (benchmarks, unit tests)
 
 
 # Reference-compatible name: users of ``LightningLearner`` keep their imports.
