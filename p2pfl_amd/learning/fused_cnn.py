@@ -162,7 +162,7 @@ class FusedCNNLearner(TorchLearner):
         self.engine = FusedCNNEngine(model, self.device, lr=lr, betas=betas, eps=eps, weight_decay=wd, arena=self.arena)
         self.use_graphs = use_graphs
         self._graphs: Dict[str, _EpochGraph] = {}
-        self._lock = threading.Lock()
+        self._lock = threading.RLock()  # fit() -> _validate() re-enters
         self._stream = torch.cuda.Stream(self.device)
         self._dirty_shadows = False
 
