@@ -138,7 +138,11 @@ def main() -> None:
     ap.add_argument("--epochs", type=int, default=1)
     ap.add_argument("--number-sub", type=int, default=20)
     ap.add_argument("--batch", type=int, default=32)
+    ap.add_argument("--watchdog", type=float, default=900, help="dump stacks and exit if the run hangs")
     args = ap.parse_args()
+    import faulthandler
+
+    faulthandler.dump_traceback_later(args.watchdog, exit=True)
 
     env = init_distributed()
     assert env.world_size == args.gpus, f"--gpus {args.gpus} but WORLD_SIZE={env.world_size}"
@@ -162,8 +166,9 @@ def main() -> None:
         runner = FederatedRoundRunner(learner, fed, name=f"peer{env.rank}")
         run = lambda: runner.run_round().seconds  # noqa: E731
 
-    for _ in range(args.warmup):
-        run()
+    for i in range(args.warmup):
+        t = run()
+        print(f"[bench rank {env.rank}] warmup round {i}: {t * 1e3:.2f} ms", file=sys.stderr, flush=True)
     fed.barrier()
     _sync()
     t0 = time.perf_counter()
