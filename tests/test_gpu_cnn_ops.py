@@ -1,0 +1,262 @@
+"""Per-kernel numerics of the fused CNN step (MI355X only).
+
+Each HIP kernel gets exactly the bf16 inputs it sees in training and is
+compared against a plain PyTorch fp32 implementation of the same op computed
+from those same inputs, so bf16 storage of activations is the only expected
+difference (plus fp32 summation order).
+"""
+
+from __future__ import annotations
+
+import pytest
+import torch
+import torch.nn.functional as F
+
+from p2pfl_amd import ops
+from p2pfl_amd.models import CNN
+
+pytestmark = pytest.mark.gpu
+
+B = 32
+
+
+@pytest.fixture(scope="module")
+def eng():
+    from p2pfl_amd.learning.fused_cnn import FusedCNNEngine
+
+    ops.ext()
+    torch.manual_seed(0)
+    return FusedCNNEngine(CNN(seed=3).cuda(), device=torch.device("cuda"))
+
+
+def _p(eng, name):
+    return eng.arena.params[name]
+
+
+def _bf(t):
+    return t.to(torch.bfloat16).float()
+
+
+def _close(got, want, rtol=1e-2, atol=1e-3):
+    err = (got.float() - want.float()).abs()
+    bound = atol + rtol * want.float().abs()
+    frac = float((err > bound).float().mean())
+    return frac
+
+
+def _forward(eng, x):
+    stats = torch.zeros(4, device="cuda")
+    y = torch.zeros(B, dtype=torch.int64, device="cuda")
+    eng.forward(x.reshape(-1, 784), y, None, B, stats, False)
+    torch.cuda.synchronize()
+
+
+def _x(seed=0):
+    g = torch.Generator(device="cuda").manual_seed(seed)
+    return torch.randint(0, 256, (B, 1, 28, 28), dtype=torch.uint8, device="cuda", generator=g)
+
+
+def _decode_pool(val_nchw, am, H):
+    """Expand pooled values to the pre-pool map using the kernel's argmax codes."""
+    Bn, C, h, w = val_nchw.shape
+    out = torch.zeros(Bn, C, H, H, device=val_nchw.device)
+    a = am.long()
+    alive = a < 4
+    dy, dx = (a.clamp(max=3) >> 1), (a.clamp(max=3) & 1)
+    py = torch.arange(h, device=a.device).view(1, 1, h, 1).expand_as(a)
+    px = torch.arange(w, device=a.device).view(1, 1, 1, w).expand_as(a)
+    bi = torch.arange(Bn, device=a.device).view(Bn, 1, 1, 1).expand_as(a)
+    ci = torch.arange(C, device=a.device).view(1, C, 1, 1).expand_as(a)
+    out[bi[alive], ci[alive], (2 * py + dy)[alive], (2 * px + dx)[alive]] = val_nchw[alive]
+    return out
+
+
+def test_conv1_fwd(eng):
+    x = _x(1)
+    _forward(eng, x)
+    w, b = _p(eng, "conv1.weight"), _p(eng, "conv1.bias")
+    conv = F.relu(F.conv2d(x.float() / 255.0, w, b, padding=2))
+    ref = F.max_pool2d(conv, 2)  # [B,32,14,14]
+    got = eng.p1.view(B, 14, 14, 32).permute(0, 3, 1, 2).float()
+    assert _close(got, _bf(ref), rtol=8e-3, atol=1e-6) == 0.0
+    # argmax codes point at the maximum of each 2x2 window (or 4 = ReLU-dead)
+    am = eng.am1.view(B, 14, 14, 32).permute(0, 3, 1, 2).long()
+    alive = am < 4
+    a = am.clamp(max=3)
+    py = torch.arange(14, device="cuda").view(1, 1, 14, 1)
+    px = torch.arange(14, device="cuda").view(1, 1, 1, 14)
+    flat = ((2 * py + (a >> 1)) * 28 + 2 * px + (a & 1)).reshape(B, 32, 196)
+    picked = conv.reshape(B, 32, 784).gather(2, flat).view(B, 32, 14, 14)
+    torch.testing.assert_close(picked[alive], ref[alive], atol=1e-5, rtol=1e-5)
+    assert bool(((am == 4) == (ref <= 0)).all())
+
+
+def test_conv2_fwd(eng):
+    x = _x(2)
+    _forward(eng, x)
+    p1 = eng.p1.view(B, 14, 14, 32).permute(0, 3, 1, 2).float()
+    w, b = _bf(_p(eng, "conv2.weight")), _p(eng, "conv2.bias")
+    ref = F.max_pool2d(F.relu(F.conv2d(p1, w, b, padding=2)), 2).reshape(B, -1)  # [B,3136]
+    got = eng.a1.view(-1, 3136)[:B].float()
+    assert _close(got, _bf(ref), rtol=1e-2, atol=1e-4) < 1e-3
+    got_t = eng.a1t.view(3136, -1)[:, :B].t().float()
+    assert torch.equal(got_t, got)
+
+
+@pytest.mark.parametrize("N,K,S", [(2048, 3136, 7), (3136, 2048, 4), (64, 128, 3)])
+def test_gemm_skinny(eng, N, K, S):
+    g = torch.Generator(device="cuda").manual_seed(N + K)
+    A = torch.randn(32, K, device="cuda", generator=g).to(torch.bfloat16)
+    Bt = torch.randn(N, K, device="cuda", generator=g).to(torch.bfloat16)
+    slabs = torch.zeros(S * 32 * N, device="cuda")
+    eng.C.gemm_skinny(A, Bt, slabs, 32, N, K, S)
+    got = slabs.view(S, 32, N).sum(0)
+    want = A.float() @ Bt.float().t()
+    torch.testing.assert_close(got, want, atol=2e-3 * K**0.5, rtol=1e-4)
+
+
+def test_head_and_fc2_wgrad(eng):
+    g = torch.Generator(device="cuda").manual_seed(7)
+    slabs = torch.randn(eng.S1 * 32 * 2048, device="cuda", generator=g) * 0.05
+    labels = torch.randint(0, 10, (B,), device="cuda", generator=g)
+    stats = torch.zeros(4, device="cuda")
+    eng.C.head(slabs, eng.S1, 32, eng.params, eng.off, labels, None, B, True, eng.H, eng.dH, eng.dHt, eng.dlogits, stats)
+    torch.cuda.synchronize()
+    b1, w2, b2 = _p(eng, "l1.bias"), _p(eng, "l2.weight"), _p(eng, "l2.bias")
+    h = F.relu(slabs.view(eng.S1, 32, 2048).sum(0)[:B] + b1)
+    logits = h @ w2.t() + b2
+    loss = F.cross_entropy(logits, labels, reduction="sum")
+    dlog = (torch.softmax(logits, 1) - F.one_hot(labels, 10).float()) / B
+    dh = (dlog @ w2) * (h > 0)
+    assert abs(float(stats[0]) - float(loss)) < 1e-3 * float(loss) + 1e-3
+    assert int(stats[1]) == int((logits.argmax(1) == labels).sum())
+    torch.testing.assert_close(eng.dlogits.view(-1, 10)[:B], dlog, atol=1e-6, rtol=1e-4)
+    torch.testing.assert_close(eng.H.view(-1, 2048)[:B].float(), _bf(h), atol=0, rtol=0)
+    torch.testing.assert_close(eng.dH.view(-1, 2048)[:B].float(), _bf(dh), atol=1e-7, rtol=8e-3)
+    torch.testing.assert_close(eng.dHt.view(2048, -1)[:, :B].t(), eng.dH.view(-1, 2048)[:B])
+    # FC2 gradient (+Adam) from the same H / dlogits
+    eng.gdump = torch.zeros_like(eng.params)
+    before = eng.params.clone()
+    eng.adam_t.fill_(1)
+    m_save, v_save = eng.m.clone(), eng.v.clone()
+    eng.C.fc2_wgrad_adam(eng.dlogits, eng.H, B, eng.params, eng.m, eng.v, eng.gdump, eng.off, eng.adam_t, *eng._adam())
+    torch.cuda.synchronize()
+    gw = eng.gdump[eng.off[6] : eng.off[6] + 20480].view(10, 2048)
+    gb = eng.gdump[eng.off[7] : eng.off[7] + 10]
+    torch.testing.assert_close(gw, dlog.t() @ _bf(h), atol=1e-6, rtol=1e-4)
+    torch.testing.assert_close(gb, dlog.sum(0), atol=1e-6, rtol=1e-4)
+    # first Adam step moves every weight with a non-zero gradient by ~lr
+    moved = (eng.params[eng.off[6] : eng.off[6] + 20480] - before[eng.off[6] : eng.off[6] + 20480]).abs()
+    assert float(moved.max()) <= 1.0001e-3
+    eng.params.copy_(before)
+    eng.m.copy_(m_save)
+    eng.v.copy_(v_save)
+    eng.gdump = None
+
+
+def test_fc1_wgrad_adam(eng):
+    g = torch.Generator(device="cuda").manual_seed(9)
+    dht = (torch.randn(2048, 32, device="cuda", generator=g) * 1e-2).to(torch.bfloat16)
+    a1t = torch.rand(3136, 32, device="cuda", generator=g).to(torch.bfloat16)
+    before, m0, v0 = eng.params.clone(), eng.m.clone(), eng.v.clone()
+    eng.gdump = torch.zeros_like(eng.params)
+    eng.adam_t.fill_(1)
+    eng.C.fc1_wgrad_adam(dht, a1t, 32, eng.params, eng.m, eng.v, eng.gdump, eng.w1bf, eng.w1tbf, eng.off, eng.adam_t, *eng._adam())
+    torch.cuda.synchronize()
+    o, ob = eng.off[4], eng.off[5]
+    gw = eng.gdump[o : o + 2048 * 3136].view(2048, 3136)
+    torch.testing.assert_close(gw, dht.float() @ a1t.float().t(), atol=1e-6, rtol=1e-4)
+    torch.testing.assert_close(eng.gdump[ob : ob + 2048], dht.float().sum(1), atol=1e-6, rtol=1e-4)
+    # Adam: reference update from the same gradient
+    p_ref, m_ref, v_ref = before[o : o + 2048 * 3136].clone(), m0[o : o + 2048 * 3136].clone(), v0[o : o + 2048 * 3136].clone()
+    ops.adam_step_reference(p_ref, gw.flatten(), m_ref, v_ref, eng.lr, eng.betas[0], eng.betas[1], eng.eps, eng.wd, 1)
+    torch.testing.assert_close(eng.params[o : o + 2048 * 3136], p_ref, atol=1e-6, rtol=1e-5)
+    # bf16 shadows are the updated weights, in both layouts
+    W = eng.params[o : o + 2048 * 3136].view(2048, 3136)
+    assert torch.equal(eng.w1bf.view(2048, 3136), W.to(torch.bfloat16))
+    assert torch.equal(eng.w1tbf.view(3136, 2048), W.t().to(torch.bfloat16))
+    eng.params.copy_(before)
+    eng.m.copy_(m0)
+    eng.v.copy_(v0)
+    eng.gdump = None
+    eng.pack_shadows()
+
+
+def _dc2_from(eng, slabs2):
+    """dC2 [B,64,14,14] from the split-K slabs and the pool2 argmax codes (bf16 like the kernels)."""
+    da1 = slabs2.view(eng.S2, 32, 3136).sum(0)[:B].view(B, 64, 7, 7)
+    am2 = eng.am2.view(-1, 3136)[:B].view(B, 64, 7, 7)
+    return _decode_pool(_bf(da1), am2, 14), _decode_pool(da1, am2, 14)
+
+
+def test_conv2_wgrad(eng):
+    x = _x(3)
+    _forward(eng, x)
+    g = torch.Generator(device="cuda").manual_seed(11)
+    slabs2 = torch.randn(eng.S2 * 32 * 3136, device="cuda", generator=g) * 1e-3
+    eng.C.conv2_wgrad(slabs2, eng.S2, 32, eng.am2, eng.p1, eng.wslab2, B)
+    torch.cuda.synchronize()
+    dc2_bf, dc2 = _dc2_from(eng, slabs2)
+    p1 = eng.p1.view(B, 14, 14, 32).permute(0, 3, 1, 2).float()
+    want_w = torch.nn.grad.conv2d_weight(p1, (64, 32, 5, 5), dc2_bf, padding=2)
+    ws = eng.wslab2.view(-1, 51264)[:B].sum(0)
+    torch.testing.assert_close(ws[:51200].view(64, 32, 5, 5), want_w, atol=1e-6, rtol=2e-3)
+    torch.testing.assert_close(ws[51200:], dc2.sum((0, 2, 3)), atol=1e-6, rtol=1e-4)
+
+
+def test_conv2_dgrad_conv1_wgrad(eng):
+    x = _x(4)
+    _forward(eng, x)
+    g = torch.Generator(device="cuda").manual_seed(12)
+    slabs2 = torch.randn(eng.S2 * 32 * 3136, device="cuda", generator=g) * 1e-3
+    eng.C.conv2_dgrad_conv1_wgrad(slabs2, eng.S2, 32, eng.am2, eng.am1, eng.w2q, x.reshape(-1, 784), None, eng.wslab1, B)
+    torch.cuda.synchronize()
+    dc2_bf, _ = _dc2_from(eng, slabs2)
+    w2 = _bf(_p(eng, "conv2.weight"))
+    dp1 = torch.nn.grad.conv2d_input((B, 32, 14, 14), w2, dc2_bf, padding=2)
+    am1 = eng.am1.view(B, 14, 14, 32).permute(0, 3, 1, 2)
+    dc1 = _decode_pool(dp1, am1, 28)
+    want_w = torch.nn.grad.conv2d_weight(x.float() / 255.0, (32, 1, 5, 5), dc1, padding=2)
+    ws = eng.wslab1.view(-1, 832)[:B].sum(0)
+    torch.testing.assert_close(ws[:800].view(32, 1, 5, 5), want_w, atol=1e-6, rtol=2e-3)
+    torch.testing.assert_close(ws[800:], dc1.sum((0, 2, 3)), atol=1e-6, rtol=1e-3)
+
+
+def test_conv_adam_and_shadows(eng):
+    g = torch.Generator(device="cuda").manual_seed(13)
+    ws1 = torch.randn(32 * 832, device="cuda", generator=g) * 1e-3
+    ws2 = torch.randn(32 * 51264, device="cuda", generator=g) * 1e-3
+    before, m0, v0 = eng.params.clone(), eng.m.clone(), eng.v.clone()
+    eng.gdump = torch.zeros_like(eng.params)
+    eng.adam_t.fill_(1)
+    eng.C.conv_adam(ws1, ws2, B, eng.params, eng.m, eng.v, eng.gdump, eng.w2r, eng.w2q, eng.off, eng.adam_t, *eng._adam())
+    torch.cuda.synchronize()
+    o = eng.off
+    torch.testing.assert_close(eng.gdump[o[0] : o[0] + 800], ws1.view(32, 832)[:, :800].sum(0), atol=1e-7, rtol=1e-5)
+    torch.testing.assert_close(eng.gdump[o[3] : o[3] + 64], ws2.view(32, 51264)[:, 51200:].sum(0), atol=1e-7, rtol=1e-5)
+    W = eng.params[o[2] : o[2] + 51200].view(64, 32, 25)
+    assert torch.equal(eng.w2r.view(64, 25, 32), W.permute(0, 2, 1).to(torch.bfloat16))
+    assert torch.equal(eng.w2q.view(32, 25, 64), W.permute(1, 2, 0).to(torch.bfloat16))
+    eng.params.copy_(before)
+    eng.m.copy_(m0)
+    eng.v.copy_(v0)
+    eng.gdump = None
+    eng.pack_shadows()
+
+
+def test_bf16_reference_has_similar_gradient_error():
+    """Calibrates the end-to-end gradient tolerance: torch's own bf16 autocast vs fp32."""
+    torch.manual_seed(0)
+    m32 = CNN(seed=2).cuda()
+    m16 = CNN(seed=2).cuda()
+    x = _x(5).float() / 255.0
+    y = torch.randint(0, 10, (B,), device="cuda")
+    F.cross_entropy(m32(x), y).backward()
+    with torch.autocast("cuda", dtype=torch.bfloat16):
+        loss = F.cross_entropy(m16(x), y)
+    loss.backward()
+    rel = {
+        n: float((p16.grad - p32.grad).norm() / p32.grad.norm())
+        for (n, p32), (_, p16) in zip(m32.named_parameters(), m16.named_parameters())
+    }
+    print("torch bf16-autocast vs fp32 gradient rel err:", rel)
