@@ -5,24 +5,24 @@
 //   -> maxpool2 -> flatten(3136) -> FC 3136->2048 -> ReLU -> FC 2048->10 -> CE
 // trained with Adam.  One training step is 10 kernels (cnn_*.hip):
 //
-//  1 step_begin        adam_t += 1 (device counter: graph-replay safe)
-//  2 conv1_fwd         direct 5x5 conv + bias + ReLU + maxpool, input gathered
+//  1 conv1_fwd         direct 5x5 conv + bias + ReLU + maxpool, input gathered
 //                      by index from the uint8 dataset (/255 folded in) -> P1 (HWC bf16) + argmax
-//  3 conv2_fwd         implicit-GEMM on MFMA 32x32x16 bf16, image + weights in
+//  2 conv2_fwd         implicit-GEMM on MFMA 32x32x16 bf16, image + weights in
 //                      LDS, bias + ReLU + maxpool epilogue -> A1 (+ A1^T) + argmax
-//  4 gemm_skinny       FC1: [B x 3136] x [3136 x 2048], split-K fp32 slabs
-//  5 head              slab reduce + bias + ReLU -> H; FC2; softmax-xent; dlogits;
+//  3 gemm_skinny       FC1: [B x 3136] x [3136 x 2048], split-K fp32 slabs
+//  4 head              slab reduce + bias + ReLU -> H; FC2; softmax-xent; dlogits;
 //                      dH = relu'(H) * dlogits W2 (and dH^T); loss/accuracy stats
-//  6 fc2_wgrad_adam    dW2 = dlogits^T H and db2, Adam applied in place
-//  7 gemm_skinny       dA1 = dH x W1 (reads the W1^T bf16 shadow), split-K slabs
-//  8 fc1_wgrad_adam    dW1 = dH^T A1 on MFMA with Adam fused into the epilogue:
+//  5 fc2_wgrad_adam    dW2 = dlogits^T H and db2, Adam applied in place
+//  6 gemm_skinny       dA1 = dH x W1 (reads the W1^T bf16 shadow), split-K slabs
+//  7 fc1_wgrad_adam    dW1 = dH^T A1 on MFMA with Adam fused into the epilogue:
 //                      the 6.4 M-element gradient never touches memory; writes
 //                      W1 (fp32), m, v and both bf16 shadows (W1, W1^T)
-//  9 conv2_wgrad       per image: maxpool/ReLU backward of dA1 -> dC2, then
+//  8 conv2_wgrad       per image: maxpool/ReLU backward of dA1 -> dC2, then
 //                      dW2c = dC2 x im2col(P1) on MFMA -> per-image slab
-// 10 conv2_dgrad_c1    per image: dP1 = transposed conv on MFMA, then pool1/ReLU
-//                      backward and conv1 weight gradient in the epilogue -> slab
-// 11 conv_adam         reduce the per-image slabs + Adam for conv params + packed
+//  9 conv2_dgrad_c1    per image: dP1 = transposed conv on MFMA, pool1/ReLU
+//                      backward into a dense LDS map, conv1 weight gradient as a
+//                      second MFMA GEMM -> slab
+// 10 conv_adam         reduce the per-image slabs + Adam for conv params + packed
 //                      bf16 shadows of conv2 (two layouts)
 #pragma once
 #include <hip/hip_runtime.h>
@@ -38,7 +38,10 @@ constexpr int kHid = 2048;
 constexpr int kCls = 10;
 constexpr int kTaps = 25;
 
-// Device-resident Adam state shared by all fused optimizer epilogues.
+// Adam hyper-parameters.  The step count t is read from device memory as
+// (*adam_t + t_off): the host sets the base once per epoch and each captured
+// step bakes in its own offset, so a whole epoch replays as one HIP graph
+// with no per-step counter kernel.
 struct AdamCfg {
   float lr, beta1, beta2, eps, weight_decay;
 };
@@ -47,8 +50,6 @@ struct AdamCfg {
 struct Offsets {
   int64_t c1w, c1b, c2w, c2b, l1w, l1b, l2w, l2b;
 };
-
-void step_begin(int* adam_t, hipStream_t s);
 
 void conv1_fwd(const uint8_t* x, const int64_t* idx, const float* params, Offsets off, uint16_t* p1, uint8_t* am1,
                int B, hipStream_t s);
@@ -63,11 +64,11 @@ void head(const float* slabs, int S, int mrows, const float* params, Offsets off
           float* stats, hipStream_t s);
 
 void fc2_wgrad_adam(const float* dlogits, const uint16_t* H, int B, float* params, float* m, float* v,
-                    float* gdump, Offsets off, const int* adam_t, AdamCfg cfg, hipStream_t s);
+                    float* gdump, Offsets off, const int* adam_t, int t_off, AdamCfg cfg, hipStream_t s);
 
 void fc1_wgrad_adam(const uint16_t* dHt, const uint16_t* a1t, int mrows, float* params, float* m, float* v,
-                    float* gdump, uint16_t* w1bf, uint16_t* w1tbf, Offsets off, const int* adam_t, AdamCfg cfg,
-                    hipStream_t s);
+                    float* gdump, uint16_t* w1bf, uint16_t* w1tbf, Offsets off, const int* adam_t, int t_off,
+                    AdamCfg cfg, hipStream_t s);
 
 void conv2_wgrad(const float* slabs2, int S2, int mrows, const uint8_t* am2, const uint16_t* p1, float* wslab, int B,
                  hipStream_t s);
@@ -77,7 +78,7 @@ void conv2_dgrad_conv1_wgrad(const float* slabs2, int S2, int mrows, const uint8
                              hipStream_t s);
 
 void conv_adam(const float* wslab1, const float* wslab2, int B, float* params, float* m, float* v, float* gdump,
-               uint16_t* w2r, uint16_t* w2q, Offsets off, const int* adam_t, AdamCfg cfg, hipStream_t s);
+               uint16_t* w2r, uint16_t* w2q, Offsets off, const int* adam_t, int t_off, AdamCfg cfg, hipStream_t s);
 
 // Standalone packing of the bf16 shadows from fp32 params (after set_parameters).
 void pack_shadows(const float* params, Offsets off, uint16_t* w2r, uint16_t* w2q, uint16_t* w1bf, uint16_t* w1tbf,

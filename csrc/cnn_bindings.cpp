@@ -53,11 +53,6 @@ const int64_t* idx_ptr(const c10::optional<torch::Tensor>& idx, int B) {
 // NOTE: gathers through idx are bounds-checked on the host only by shape; the
 // learner guarantees idx values are permutations of the dataset rows.
 
-void k_step_begin(torch::Tensor adam_t) {
-  const c10::DeviceGuard g(adam_t.device());
-  p2cnn::step_begin(ptr<int>(adam_t, torch::kInt32, 1, "adam_t", 4), stream());
-}
-
 void k_conv1_fwd(torch::Tensor x, c10::optional<torch::Tensor> idx, torch::Tensor params, std::vector<int64_t> off,
                  torch::Tensor p1, torch::Tensor am1, int64_t B) {
   const c10::DeviceGuard g(params.device());
@@ -117,7 +112,7 @@ AdamCfg cfg(double lr, double b1, double b2, double eps, double wd) {
 
 void k_fc2_wgrad_adam(torch::Tensor dlogits, torch::Tensor H, int64_t B, torch::Tensor params, torch::Tensor m,
                       torch::Tensor v, c10::optional<torch::Tensor> gdump, std::vector<int64_t> off,
-                      torch::Tensor adam_t, double lr, double b1, double b2, double eps, double wd) {
+                      torch::Tensor adam_t, int64_t t_off, double lr, double b1, double b2, double eps, double wd) {
   const c10::DeviceGuard g(params.device());
   Offsets o = offsets(off);
   const int64_t n = params_end(o);
@@ -125,13 +120,13 @@ void k_fc2_wgrad_adam(torch::Tensor dlogits, torch::Tensor H, int64_t B, torch::
                         reinterpret_cast<uint16_t*>(ptr<at::BFloat16>(H, torch::kBFloat16, B * 2048, "H")), int(B),
                         ptr<float>(params, torch::kFloat32, n, "params"), ptr<float>(m, torch::kFloat32, n, "m"),
                         ptr<float>(v, torch::kFloat32, n, "v"), optr<float>(gdump, torch::kFloat32, n, "gdump"), o,
-                        ptr<int>(adam_t, torch::kInt32, 1, "adam_t", 4), cfg(lr, b1, b2, eps, wd), stream());
+                        ptr<int>(adam_t, torch::kInt32, 1, "adam_t", 4), int(t_off), cfg(lr, b1, b2, eps, wd), stream());
 }
 
 void k_fc1_wgrad_adam(torch::Tensor dHt, torch::Tensor a1t, int64_t mrows, torch::Tensor params, torch::Tensor m,
                       torch::Tensor v, c10::optional<torch::Tensor> gdump, torch::Tensor w1bf, torch::Tensor w1tbf,
-                      std::vector<int64_t> off, torch::Tensor adam_t, double lr, double b1, double b2, double eps,
-                      double wd) {
+                      std::vector<int64_t> off, torch::Tensor adam_t, int64_t t_off, double lr, double b1, double b2,
+                      double eps, double wd) {
   const c10::DeviceGuard g(params.device());
   TORCH_CHECK(mrows == 32 || mrows == 64, "mrows must be 32 or 64");
   Offsets o = offsets(off);
@@ -143,7 +138,7 @@ void k_fc1_wgrad_adam(torch::Tensor dHt, torch::Tensor a1t, int64_t mrows, torch
                         optr<float>(gdump, torch::kFloat32, n, "gdump"),
                         reinterpret_cast<uint16_t*>(ptr<at::BFloat16>(w1bf, torch::kBFloat16, 2048 * 3136, "w1bf")),
                         reinterpret_cast<uint16_t*>(ptr<at::BFloat16>(w1tbf, torch::kBFloat16, 2048 * 3136, "w1tbf")),
-                        o, ptr<int>(adam_t, torch::kInt32, 1, "adam_t", 4), cfg(lr, b1, b2, eps, wd), stream());
+                        o, ptr<int>(adam_t, torch::kInt32, 1, "adam_t", 4), int(t_off), cfg(lr, b1, b2, eps, wd), stream());
 }
 
 void k_conv2_wgrad(torch::Tensor slabs2, int64_t S2, int64_t mrows, torch::Tensor am2, torch::Tensor p1,
@@ -172,8 +167,8 @@ void k_conv2_dgrad(torch::Tensor slabs2, int64_t S2, int64_t mrows, torch::Tenso
 
 void k_conv_adam(torch::Tensor wslab1, torch::Tensor wslab2, int64_t B, torch::Tensor params, torch::Tensor m,
                  torch::Tensor v, c10::optional<torch::Tensor> gdump, torch::Tensor w2r, torch::Tensor w2q,
-                 std::vector<int64_t> off, torch::Tensor adam_t, double lr, double b1, double b2, double eps,
-                 double wd) {
+                 std::vector<int64_t> off, torch::Tensor adam_t, int64_t t_off, double lr, double b1, double b2,
+                 double eps, double wd) {
   const c10::DeviceGuard g(params.device());
   Offsets o = offsets(off);
   const int64_t n = params_end(o);
@@ -183,7 +178,7 @@ void k_conv_adam(torch::Tensor wslab1, torch::Tensor wslab2, int64_t B, torch::T
                    ptr<float>(v, torch::kFloat32, n, "v"), optr<float>(gdump, torch::kFloat32, n, "gdump"),
                    reinterpret_cast<uint16_t*>(ptr<at::BFloat16>(w2r, torch::kBFloat16, 51200, "w2r")),
                    reinterpret_cast<uint16_t*>(ptr<at::BFloat16>(w2q, torch::kBFloat16, 51200, "w2q")), o,
-                   ptr<int>(adam_t, torch::kInt32, 1, "adam_t", 4), cfg(lr, b1, b2, eps, wd), stream());
+                   ptr<int>(adam_t, torch::kInt32, 1, "adam_t", 4), int(t_off), cfg(lr, b1, b2, eps, wd), stream());
 }
 
 void k_pack_shadows(torch::Tensor params, std::vector<int64_t> off, torch::Tensor w2r, torch::Tensor w2q,
@@ -207,7 +202,6 @@ void init_attributes();
 void register_cnn(pybind11::module& m) {
   auto c = m.def_submodule("cnn", "fused MNIST-CNN training step kernels");
   c.def("init", &p2cnn::init_attributes, "set kernel attributes (call before HIP graph capture)");
-  c.def("step_begin", &k_step_begin);
   c.def("conv1_fwd", &k_conv1_fwd);
   c.def("conv2_fwd", &k_conv2_fwd);
   c.def("gemm_skinny", &k_gemm_skinny);

@@ -6,8 +6,8 @@
 //   W2q   bf16 [32][25][64]      conv2 weight, (ic, tap, oc) -- B operand of the transposed conv
 //   wslab1 f32 [B][832]          per-image conv1 weight/bias gradients
 //   wslab2 f32 [B][51264]        per-image conv2 weight/bias gradients
-// Adam's step counter lives in device memory (step_begin increments it), so
-// the whole step can be captured once in a HIP graph and replayed.
+// Adam's step count is (*adam_t + t_off): a device base plus an offset baked
+// into each launch, so a whole epoch is captured once as a HIP graph.
 #include "cnn.h"
 #include "common.h"
 
@@ -24,8 +24,8 @@ P2_DEVICE int acc_row_b(int i, int h) { return (i & 3) + 8 * (i >> 2) + 4 * h; }
 struct AdamScal {
   float step_size, inv_sqrt_bc2;
 };
-P2_DEVICE AdamScal adam_scal(const AdamCfg& c, const int* t) {
-  const float tt = float(*t);
+P2_DEVICE AdamScal adam_scal(const AdamCfg& c, const int* t, int t_off) {
+  const float tt = float(*t + t_off);
   AdamScal s;
   s.step_size = c.lr / (1.f - powf(c.beta1, tt));
   s.inv_sqrt_bc2 = 1.f / sqrtf(1.f - powf(c.beta2, tt));
@@ -53,7 +53,7 @@ __global__ __launch_bounds__(256) void fc2_wgrad_adam_kernel(const float* __rest
                                                              const uint16_t* __restrict__ H, int B,
                                                              float* __restrict__ p, float* __restrict__ m,
                                                              float* __restrict__ v, float* __restrict__ gdump,
-                                                             Offsets off, const int* __restrict__ adam_t, AdamCfg cfg) {
+                                                             Offsets off, const int* __restrict__ adam_t, int t_off, AdamCfg cfg) {
   const int e = blockIdx.x * 256 + threadIdx.x;
   const int nW = kCls * kHid;
   if (e >= nW + kCls) return;
@@ -61,6 +61,7 @@ __global__ __launch_bounds__(256) void fc2_wgrad_adam_kernel(const float* __rest
   int64_t pi;
   if (e < nW) {
     const int c = e / kHid, k = e % kHid;
+#pragma unroll 8
     for (int b = 0; b < B; ++b) g = fmaf(dlogits[b * kCls + c], bf16_to_f32(H[size_t(b) * kHid + k]), g);
     pi = off.l2w + e;
   } else {
@@ -69,15 +70,15 @@ __global__ __launch_bounds__(256) void fc2_wgrad_adam_kernel(const float* __rest
     pi = off.l2b + c;
   }
   if (gdump) gdump[pi] = g;
-  const AdamScal s = adam_scal(cfg, adam_t);
+  const AdamScal s = adam_scal(cfg, adam_t, t_off);
   adam_apply(p, m, v, pi, g, cfg, s);
 }
 
 void fc2_wgrad_adam(const float* dlogits, const uint16_t* H, int B, float* params, float* m, float* v, float* gdump,
-                    Offsets off, const int* adam_t, AdamCfg cfg, hipStream_t s) {
+                    Offsets off, const int* adam_t, int t_off, AdamCfg cfg, hipStream_t s) {
   const int n = kCls * kHid + kCls;
   hipLaunchKernelGGL(fc2_wgrad_adam_kernel, dim3((n + 255) / 256), dim3(256), 0, s, dlogits, H, B, params, m, v,
-                     gdump, off, adam_t, cfg);
+                     gdump, off, adam_t, t_off, cfg);
 }
 
 // ---------------------------------------------------------------------------
@@ -96,7 +97,7 @@ __global__ __launch_bounds__(256) void fc1_wgrad_adam_kernel(const uint16_t* __r
                                                              float* __restrict__ v, float* __restrict__ gdump,
                                                              uint16_t* __restrict__ w1bf,
                                                              uint16_t* __restrict__ w1tbf, Offsets off,
-                                                             const int* __restrict__ adam_t, AdamCfg cfg) {
+                                                             const int* __restrict__ adam_t, int t_off, AdamCfg cfg) {
   __shared__ __attribute__((aligned(16))) uint16_t tr[128][40];
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, r = lane & 31, h = lane >> 5;
   const int n0 = blockIdx.y * 32;
@@ -110,7 +111,7 @@ __global__ __launch_bounds__(256) void fc1_wgrad_adam_kernel(const uint16_t* __r
                           : make_uint4(0, 0, 0, 0);
     acc = mfma32b(a, b, acc);
   }
-  const AdamScal s = adam_scal(cfg, adam_t);
+  const AdamScal s = adam_scal(cfg, adam_t, t_off);
   float* pw = p + off.l1w;
   float* mw = m + off.l1w;
   float* vw = v + off.l1w;
@@ -143,101 +144,106 @@ __global__ __launch_bounds__(256) void fc1_wgrad_adam_kernel(const uint16_t* __r
 }
 
 void fc1_wgrad_adam(const uint16_t* dHt, const uint16_t* a1t, int mrows, float* params, float* m, float* v,
-                    float* gdump, uint16_t* w1bf, uint16_t* w1tbf, Offsets off, const int* adam_t, AdamCfg cfg,
-                    hipStream_t s) {
+                    float* gdump, uint16_t* w1bf, uint16_t* w1tbf, Offsets off, const int* adam_t, int t_off,
+                    AdamCfg cfg, hipStream_t s) {
   const dim3 grid((kFeat / 32 + 3) / 4, kHid / 32);
   if (mrows == 32)
     hipLaunchKernelGGL(fc1_wgrad_adam_kernel<2>, grid, dim3(256), 0, s, dHt, a1t, mrows, params, m, v, gdump, w1bf,
-                       w1tbf, off, adam_t, cfg);
+                       w1tbf, off, adam_t, t_off, cfg);
   else
     hipLaunchKernelGGL(fc1_wgrad_adam_kernel<4>, grid, dim3(256), 0, s, dHt, a1t, mrows, params, m, v, gdump, w1bf,
-                       w1tbf, off, adam_t, cfg);
-}
-
-// ---------------------------------------------------------------------------
-// shared: dC2 = maxpool2/ReLU backward of dA1 (sum of the split-K slabs),
-// routed to the argmax position of each 2x2 window.
-// ---------------------------------------------------------------------------
-P2_DEVICE float dA1_value(const float* __restrict__ slabs2, int S2, int mrows, int b, int feat) {
-  float g = 0.f;
-  for (int s = 0; s < S2; ++s) g += slabs2[(size_t(s) * mrows + b) * kFeat + feat];
-  return g;
+                       w1tbf, off, adam_t, t_off, cfg);
 }
 
 // ---------------------------------------------------------------------------
 // 9. conv2 weight gradient on MFMA, per image and tap group.
-//    Grid (4, B), 8 waves.  C[oc][ic] for tap t = sum_pos dC2[oc][pos] *
-//    P1pad[pos + tap][ic]; M = 64 oc (2 tiles), N = 32 ic per tap, K = 196
-//    positions (14 k-steps).  A fragments are 16-B LDS reads of the [oc][pos]
-//    dC2 image; B fragments gather 8 positions of one channel from the HWC
-//    image (a position->pixel offset table in LDS keeps the address math out
-//    of the loop).  Output: per-image slab in PyTorch [oc][ic][ky][kx] order.
+//    Grid (4, B), 8 waves.  For tap t: C[oc][ic] = sum_pos dC2[oc][pos] *
+//    P1pad[ic][pos + tap]; M = 64 oc (2 tiles), N = 32 ic, K = positions.
+//    Positions are laid out 14 rows x 16 (2 zero columns), so one 16-wide
+//    MFMA k-step is one image row.  The image is kept as five kx-shifted
+//    channel-planar copies ([kx][ic][18 rows][16 cols]), which makes every B
+//    fragment (8 consecutive positions of one channel) ONE aligned 16-B LDS
+//    read; A fragments are 16-B reads of the [oc][pos] dC2 map.  The ic pitch
+//    (296 elements = 148 dwords) puts the 16 lanes of a b128 group on disjoint
+//    banks.  Bias gradients: wave reductions of the fp32 dC2 values.
 // ---------------------------------------------------------------------------
-constexpr int kICP2 = 40;
-constexpr int kWgImg = 18 * 18 * kICP2 * 2;  // 25920
-constexpr int kWgDc2 = 64 * 224 * 2;         // 28672
-constexpr int kWgTab = 224 * 4;              // 896
-constexpr int kWgLds = kWgImg + kWgDc2 + kWgTab;
+constexpr int kWgPitch = 18 * 16 + 8;                    // 296 elements per (kx, ic) plane
+constexpr int kWgCopies = 5 * kC1 * kWgPitch * 2;        // 94720 B
+constexpr int kWgDc2 = kC2 * 224 * 2;                    // 28672 B  [oc][14*16]
+constexpr int kWgG = kFeat * 4;                          // 12544 B  fp32 dA1 (alive-masked) for bias
+constexpr int kWgHwc = 196 * kC1 * 2;                    // 12544 B  staging of the HWC image
+constexpr int kWgLds = kWgCopies + kWgDc2 + kWgG + kWgHwc;  // 148480 B
+
+P2_DEVICE float dA1_value(const float* __restrict__ slabs2, int S2, int mrows, int b, int feat) {
+  float g = 0.f;
+#pragma unroll 4
+  for (int s = 0; s < S2; ++s) g += slabs2[(size_t(s) * mrows + b) * kFeat + feat];
+  return g;
+}
 
 __global__ __launch_bounds__(512) void conv2_wgrad_kernel(const float* __restrict__ slabs2, int S2, int mrows,
                                                           const uint8_t* __restrict__ am2,
                                                           const uint16_t* __restrict__ p1,
                                                           float* __restrict__ wslab) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  uint16_t* simg = reinterpret_cast<uint16_t*>(smem);
-  uint16_t* dc2 = reinterpret_cast<uint16_t*>(smem + kWgImg);
-  int* tab = reinterpret_cast<int*>(smem + kWgImg + kWgDc2);
+  uint16_t* cp = reinterpret_cast<uint16_t*>(smem);
+  uint16_t* dc2 = reinterpret_cast<uint16_t*>(smem + kWgCopies);
+  float* gb = reinterpret_cast<float*>(smem + kWgCopies + kWgDc2);
+  uint16_t* hwc = reinterpret_cast<uint16_t*>(smem + kWgCopies + kWgDc2 + kWgG);
   const int b = blockIdx.y, grp = blockIdx.x, tid = threadIdx.x;
   const uint4 z4 = make_uint4(0, 0, 0, 0);
-  for (int i = tid; i < kWgImg / 16; i += 512) reinterpret_cast<uint4*>(simg)[i] = z4;
   for (int i = tid; i < kWgDc2 / 16; i += 512) reinterpret_cast<uint4*>(dc2)[i] = z4;
-  for (int i = tid; i < 224; i += 512) {
-    const int pc = i < 196 ? i : 195;
-    tab[i] = ((pc / 14) * 18 + (pc % 14)) * kICP2;
-  }
+  for (int i = tid; i < 196 * 4; i += 512)
+    reinterpret_cast<uint4*>(hwc)[i] = reinterpret_cast<const uint4*>(p1 + size_t(b) * 196 * kC1)[i];
   __syncthreads();
-  for (int i = tid; i < 196 * 4; i += 512) {
-    const int pix = i >> 2, q = i & 3, y = pix / 14, x = pix % 14;
-    *reinterpret_cast<uint4*>(simg + ((y + 2) * 18 + (x + 2)) * kICP2 + q * 8) =
-        reinterpret_cast<const uint4*>(p1 + (size_t(b) * 196 + pix) * kC1)[q];
+  // shifted planar copies: cp[kx][ic][yy][c] = P1pad[ic][yy][c + kx], P1pad = P1 padded by 2
+  for (int i = tid; i < 5 * kC1 * 18 * 2; i += 512) {
+    const int half = i & 1, yy = (i >> 1) % 18, ic = (i / 36) % kC1, kx = i / (36 * kC1);
+    uint16_t v[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int y = yy - 2, x = half * 8 + j + kx - 2;
+      v[j] = (y >= 0 && y < 14 && x >= 0 && x < 14) ? hwc[(y * 14 + x) * kC1 + ic] : uint16_t(0);
+    }
+    uint4 q;
+    q.x = uint32_t(v[0]) | (uint32_t(v[1]) << 16);
+    q.y = uint32_t(v[2]) | (uint32_t(v[3]) << 16);
+    q.z = uint32_t(v[4]) | (uint32_t(v[5]) << 16);
+    q.w = uint32_t(v[6]) | (uint32_t(v[7]) << 16);
+    *reinterpret_cast<uint4*>(cp + (kx * kC1 + ic) * kWgPitch + yy * 16 + half * 8) = q;
   }
-  for (int i = tid; i < kC2 * 49; i += 512) {
-    const int oc = i / 49, pp = i % 49;
-    const int feat = oc * 49 + pp;
+  // dC2: pool2/ReLU backward of dA1, routed to the argmax position (coalesced over features)
+  for (int feat = tid; feat < kFeat; feat += 512) {
     const uint8_t a = am2[size_t(b) * kFeat + feat];
+    float g = 0.f;
     if (a < 4) {
-      const float g = dA1_value(slabs2, S2, mrows, b, feat);
-      const int pos = (2 * (pp / 7) + (a >> 1)) * 14 + 2 * (pp % 7) + (a & 1);
+      g = dA1_value(slabs2, S2, mrows, b, feat);
+      const int oc = feat / 49, pp = feat % 49;
+      const int pos = (2 * (pp / 7) + (a >> 1)) * 16 + 2 * (pp % 7) + (a & 1);
       dc2[oc * 224 + pos] = f32_to_bf16(g);
     }
-  }
-  if (grp == 0 && tid < kC2) {  // conv2 bias gradient (fp32, unrounded)
-    float gb = 0.f;
-    for (int pp = 0; pp < 49; ++pp) {
-      const int feat = tid * 49 + pp;
-      if (am2[size_t(b) * kFeat + feat] < 4) gb += dA1_value(slabs2, S2, mrows, b, feat);
-    }
-    wslab[size_t(b) * kSlab2 + kC2 * kC1 * kTaps + tid] = gb;
+    gb[feat] = g;
   }
   __syncthreads();
   const int wave = tid >> 6, lane = tid & 63, r = lane & 31, h = lane >> 5;
+  if (grp == 0) {  // conv2 bias gradient: 8 waves x 8 output channels, 49 values each
+    for (int oc = wave * 8; oc < wave * 8 + 8; ++oc) {
+      const float v = wave_sum(lane < 49 ? gb[oc * 49 + lane] : 0.f);
+      if (lane == 0) wslab[size_t(b) * kSlab2 + kC2 * kC1 * kTaps + oc] = v;
+    }
+  }
   const int mt = wave & 1, tw = wave >> 1;
   for (int tj = tw; tj < 7; tj += 4) {
     const int t = grp + 4 * tj;
     if (t >= kTaps) break;
-    const int tap_off = ((t / 5) * 18 + (t % 5)) * kICP2 + r;
+    const int ky = t / 5, kx = t % 5;
+    const uint16_t* brow = cp + (kx * kC1 + r) * kWgPitch + ky * 16 + 8 * h;
+    const uint16_t* arow = dc2 + (mt * 32 + r) * 224 + 8 * h;
     f32x16 acc = {};
-#pragma unroll 2
+#pragma unroll 7
     for (int ks = 0; ks < 14; ++ks) {
-      const uint4 a = *reinterpret_cast<const uint4*>(dc2 + (mt * 32 + r) * 224 + ks * 16 + 8 * h);
-      uint16_t bv[8];
-#pragma unroll
-      for (int j = 0; j < 8; ++j) bv[j] = simg[tab[ks * 16 + 8 * h + j] + tap_off];
-      uint4 bq;
-      bq.x = uint32_t(bv[0]) | (uint32_t(bv[1]) << 16);
-      bq.y = uint32_t(bv[2]) | (uint32_t(bv[3]) << 16);
-      bq.z = uint32_t(bv[4]) | (uint32_t(bv[5]) << 16);
-      bq.w = uint32_t(bv[6]) | (uint32_t(bv[7]) << 16);
+      const uint4 a = *reinterpret_cast<const uint4*>(arow + ks * 16);
+      const uint4 bq = *reinterpret_cast<const uint4*>(brow + ks * 16);
       acc = mfma32b(a, bq, acc);
     }
 #pragma unroll
@@ -254,22 +260,28 @@ void conv2_wgrad(const float* slabs2, int S2, int mrows, const uint8_t* am2, con
 }
 
 // ---------------------------------------------------------------------------
-// 10. conv2 input gradient (transposed conv on MFMA) with pool1/ReLU backward
-//     and the conv1 weight gradient fused into the epilogue.  Grid B, 7 waves
-//     (one 32-position tile each).  C[pos][ic] = sum_{tap,oc}
-//     dC2pad[pos - tap][oc] * W2[oc][ic][tap]: K = 25 x 64 (100 k-steps), A from
-//     the padded HWC dC2 image, B from the (ic, tap, oc) weight copy, both
-//     16-B LDS reads.  The resulting dP1 never leaves registers: each lane owns
-//     one channel, routes its values through the pool1 argmax and accumulates
-//     that channel's 25 conv1 weight gradients + bias gradient against the
-//     input image in LDS; lanes and waves are then reduced through LDS.
+// 10. conv2 input gradient (transposed conv on MFMA) + pool1/ReLU backward +
+//     conv1 weight gradient (second MFMA GEMM), one block per image, 7 waves.
+//     Phase 1: C[pos][ic] = sum_{tap,oc} dC2pad[pos - tap][oc] * W2[oc][ic][tap]
+//       (K = 25 x 64 = 100 k-steps; A from the padded HWC dC2 image, B from the
+//       (ic, tap, oc) weight copy; both 16-B LDS reads, conflict-free pitches).
+//     Phase 2: the dP1 tile is routed through the pool1 argmax into a dense
+//       dC1 map [32 ch][28 rows][32 cols] in LDS, then
+//       dW1[c][tap] = sum_pos dC1[c][pos] * Xpad[pos + tap] as a 32x32 MFMA GEMM
+//       over 896 positions with five kx-shifted bf16 copies of the input image
+//       (aligned 16-B B fragments).  Bias gradient: LDS float atomics.
 // ---------------------------------------------------------------------------
 constexpr int kW2qRow = kTaps * kC2 + 8;            // 1608 elements per ic (pad breaks bank aliasing)
 constexpr int kDgW = kC1 * kW2qRow * 2;             // 102912
 constexpr int kOCP = 72;                            // dC2 pixel stride (144 B)
 constexpr int kDgDc2 = 18 * 18 * kOCP * 2;          // 46656
-constexpr int kDgX = 32 * 32 * 4;                   // 4096
-constexpr int kDgLds = kDgW + kDgDc2 + kDgX;        // 153664
+constexpr int kDgLds = kDgW + kDgDc2;               // 149568
+// phase-2 carve of the (dead) weight region
+constexpr int kDc1Pitch = 28 * 32 + 8;              // 904 elements per channel (pad: 452 dwords = 4 mod 64)
+constexpr int kDgDc1 = kC1 * kDc1Pitch * 2;         // 57856
+constexpr int kXsPitch = 32 * 32;                   // per-kx copy [32 rows][32 cols]
+constexpr int kDgXs = 5 * kXsPitch * 2;             // 10240
+static_assert(kDgDc1 + kDgXs + 32 * 4 <= kDgW, "phase-2 LDS carve exceeds the weight region");
 
 __global__ __launch_bounds__(448) void conv2_dgrad_kernel(const float* __restrict__ slabs2, int S2, int mrows,
                                                           const uint8_t* __restrict__ am2,
@@ -281,7 +293,6 @@ __global__ __launch_bounds__(448) void conv2_dgrad_kernel(const float* __restric
   extern __shared__ __attribute__((aligned(16))) char smem[];
   uint16_t* sw = reinterpret_cast<uint16_t*>(smem);
   uint16_t* dch = reinterpret_cast<uint16_t*>(smem + kDgW);
-  float* ximg = reinterpret_cast<float*>(smem + kDgW + kDgDc2);
   const int b = blockIdx.x, tid = threadIdx.x;
   const uint4 z4 = make_uint4(0, 0, 0, 0);
   for (int i = tid; i < kDgDc2 / 16; i += 448) reinterpret_cast<uint4*>(dch)[i] = z4;
@@ -290,19 +301,12 @@ __global__ __launch_bounds__(448) void conv2_dgrad_kernel(const float* __restric
     *reinterpret_cast<uint4*>(sw + ic * kW2qRow + q * 8) =
         reinterpret_cast<const uint4*>(w2q + size_t(ic) * kTaps * kC2)[q];
   }
-  const int64_t row = idx ? idx[b] : b;
-  const uint8_t* src = xds + row * (kImg * kImg);
-  for (int i = tid; i < 32 * 32; i += 448) {
-    const int yy = i >> 5, xx = i & 31, sy = yy - 2, sx = xx - 2;
-    ximg[i] = (sy >= 0 && sy < kImg && sx >= 0 && sx < kImg) ? float(src[sy * kImg + sx]) * (1.f / 255.f) : 0.f;
-  }
   __syncthreads();
-  for (int i = tid; i < kC2 * 49; i += 448) {
-    const int oc = i % kC2, pp = i / kC2;  // oc fastest: neighbouring threads write neighbouring LDS halves
-    const int feat = oc * 49 + pp;
+  for (int feat = tid; feat < kFeat; feat += 448) {
     const uint8_t a = am2[size_t(b) * kFeat + feat];
     if (a < 4) {
       const float g = dA1_value(slabs2, S2, mrows, b, feat);
+      const int oc = feat / 49, pp = feat % 49;
       const int y = 2 * (pp / 7) + (a >> 1), x = 2 * (pp % 7) + (a & 1);
       dch[((y + 2) * 18 + (x + 2)) * kOCP + oc] = f32_to_bf16(g);
     }
@@ -321,42 +325,71 @@ __global__ __launch_bounds__(448) void conv2_dgrad_kernel(const float* __restric
     const uint4 bb = *reinterpret_cast<const uint4*>(sw + r * kW2qRow + t * kC2 + oc0);
     acc = mfma32b(a, bb, acc);
   }
-  // epilogue: pool1/ReLU backward + conv1 weight gradient for channel c = r
-  float dw[kTaps + 1];
+  __syncthreads();  // weights and dC2 are dead: carve phase-2 buffers out of the weight region
+  uint16_t* dc1 = reinterpret_cast<uint16_t*>(smem);
+  uint16_t* xs = reinterpret_cast<uint16_t*>(smem + kDgDc1);
+  float* db1 = reinterpret_cast<float*>(smem + kDgDc1 + kDgXs);
+  for (int i = tid; i < kDgDc1 / 16; i += 448) reinterpret_cast<uint4*>(dc1)[i] = z4;
+  if (tid < kC1) db1[tid] = 0.f;
+  const int64_t row = idx ? idx[b] : b;
+  const uint8_t* src = xds + row * (kImg * kImg);
+  for (int i = tid; i < 5 * 32 * 4; i += 448) {  // xs[kx][yy][c] = Xpad[yy][c + kx], 8 columns per item
+    const int q = i & 3, yy = (i >> 2) & 31, kx = i >> 7;
+    uint16_t v[8];
 #pragma unroll
-  for (int t = 0; t < kTaps + 1; ++t) dw[t] = 0.f;
+    for (int j = 0; j < 8; ++j) {
+      const int sy = yy - 2, sx = q * 8 + j + kx - 2;
+      v[j] = (sy >= 0 && sy < kImg && sx >= 0 && sx < kImg) ? f32_to_bf16(float(src[sy * kImg + sx]) * (1.f / 255.f))
+                                                           : uint16_t(0);
+    }
+    uint4 u;
+    u.x = uint32_t(v[0]) | (uint32_t(v[1]) << 16);
+    u.y = uint32_t(v[2]) | (uint32_t(v[3]) << 16);
+    u.z = uint32_t(v[4]) | (uint32_t(v[5]) << 16);
+    u.w = uint32_t(v[6]) | (uint32_t(v[7]) << 16);
+    *reinterpret_cast<uint4*>(xs + kx * kXsPitch + yy * 32 + q * 8) = u;
+  }
+  __syncthreads();
+  float bsum = 0.f;
 #pragma unroll
   for (int i = 0; i < 16; ++i) {
     const int pos = wave * 32 + acc_row_b(i, h);
     if (pos < 196) {
       const uint8_t a = am1[(size_t(b) * 196 + pos) * kC1 + r];
       if (a < 4) {
-        const float g = acc[i];
         const int yy = 2 * (pos / 14) + (a >> 1), xx = 2 * (pos % 14) + (a & 1);
-#pragma unroll
-        for (int ky = 0; ky < 5; ++ky)
-#pragma unroll
-          for (int kx = 0; kx < 5; ++kx) dw[ky * 5 + kx] = fmaf(g, ximg[(yy + ky) * 32 + xx + kx], dw[ky * 5 + kx]);
-        dw[kTaps] += g;
+        dc1[r * kDc1Pitch + yy * 32 + xx] = f32_to_bf16(acc[i]);
+        bsum += acc[i];
       }
     }
   }
-#pragma unroll
-  for (int t = 0; t < kTaps + 1; ++t) dw[t] += __shfl_xor(dw[t], 32, 64);
-  __syncthreads();  // weights no longer needed: reuse their LDS for the wave reduction
-  float* red = reinterpret_cast<float*>(smem);  // [7][32][26]
-  if (h == 0)
-#pragma unroll
-    for (int t = 0; t < kTaps + 1; ++t) red[(wave * kC1 + r) * (kTaps + 1) + t] = dw[t];
+  bsum += __shfl_xor(bsum, 32, 64);
+  if (h == 0) atomicAdd(&db1[r], bsum);
   __syncthreads();
-  for (int e = tid; e < kC1 * (kTaps + 1); e += 448) {
+  // conv1 weight gradient: C[c][tap] over K = 28 rows x 32 cols of positions (56 k-steps);
+  // waves split K, partial tiles reduced through LDS (reusing the dC2 region).
+  f32x16 wacc = {};
+  const int t = r < kTaps ? r : kTaps - 1;  // lanes 25..31 compute a duplicate column, discarded
+  const int ky = t / 5, kx = t % 5;
+  for (int ks = wave; ks < 56; ks += 7) {
+    const int yy = ks >> 1, x0 = (ks & 1) * 16 + 8 * h;
+    const uint4 a = *reinterpret_cast<const uint4*>(dc1 + r * kDc1Pitch + yy * 32 + x0);
+    const uint4 bq = *reinterpret_cast<const uint4*>(xs + kx * kXsPitch + (yy + ky) * 32 + x0);
+    wacc = mfma32b(a, bq, wacc);
+  }
+  float* red = reinterpret_cast<float*>(smem + kDgW);  // [7 waves][16 regs][64 lanes] f32 = 28672 B
+#pragma unroll
+  for (int i = 0; i < 16; ++i) red[(wave * 16 + i) * 64 + lane] = wacc[i];
+  __syncthreads();
+  for (int e = tid; e < 16 * 64; e += 448) {
     float sum = 0.f;
 #pragma unroll
-    for (int w = 0; w < 7; ++w) sum += red[w * kC1 * (kTaps + 1) + e];
-    const int c = e / (kTaps + 1), t = e % (kTaps + 1);
-    const int o = t < kTaps ? c * kTaps + t : kC1 * kTaps + c;
-    wslab1[size_t(b) * kSlab1 + o] = sum;
+    for (int w = 0; w < 7; ++w) sum += red[w * 1024 + e];
+    const int i = e >> 6, ln = e & 63;
+    const int c = acc_row_b(i, ln >> 5), tt = ln & 31;
+    if (tt < kTaps) wslab1[size_t(b) * kSlab1 + c * kTaps + tt] = sum;
   }
+  if (tid < kC1) wslab1[size_t(b) * kSlab1 + kC1 * kTaps + tid] = db1[tid];
 }
 
 void conv2_dgrad_conv1_wgrad(const float* slabs2, int S2, int mrows, const uint8_t* am2, const uint8_t* am1,
@@ -374,8 +407,8 @@ __global__ __launch_bounds__(256) void conv_adam_kernel(const float* __restrict_
                                                         int B, float* __restrict__ p, float* __restrict__ m,
                                                         float* __restrict__ v, float* __restrict__ gdump,
                                                         uint16_t* __restrict__ w2r, uint16_t* __restrict__ w2q,
-                                                        Offsets off, const int* __restrict__ adam_t, AdamCfg cfg,
-                                                        int64_t end) {
+                                                        Offsets off, const int* __restrict__ adam_t, int t_off,
+                                                        AdamCfg cfg, int64_t end) {
   const int64_t e = int64_t(blockIdx.x) * 256 + threadIdx.x;
   if (e >= end) return;
   const float* slab;
@@ -393,9 +426,10 @@ __global__ __launch_bounds__(256) void conv_adam_kernel(const float* __restrict_
     return;  // arena padding
   }
   float g = 0.f;
+#pragma unroll 8
   for (int b = 0; b < B; ++b) g += slab[size_t(b) * stride + j];
   if (gdump) gdump[e] = g;
-  const AdamScal s = adam_scal(cfg, adam_t);
+  const AdamScal s = adam_scal(cfg, adam_t, t_off);
   const float pn = adam_apply(p, m, v, e, g, cfg, s);
   if (is_c2w) {
     const int oc = j / (kC1 * kTaps), rem = j % (kC1 * kTaps), ic = rem / kTaps, t = rem % kTaps;
@@ -406,10 +440,10 @@ __global__ __launch_bounds__(256) void conv_adam_kernel(const float* __restrict_
 }
 
 void conv_adam(const float* wslab1, const float* wslab2, int B, float* params, float* m, float* v, float* gdump,
-               uint16_t* w2r, uint16_t* w2q, Offsets off, const int* adam_t, AdamCfg cfg, hipStream_t s) {
+               uint16_t* w2r, uint16_t* w2q, Offsets off, const int* adam_t, int t_off, AdamCfg cfg, hipStream_t s) {
   const int64_t end = off.c2b + kC2;
   hipLaunchKernelGGL(conv_adam_kernel, dim3(int((end + 255) / 256)), dim3(256), 0, s, wslab1, wslab2, B, params, m, v,
-                     gdump, w2r, w2q, off, adam_t, cfg, end);
+                     gdump, w2r, w2q, off, adam_t, t_off, cfg, end);
 }
 
 void init_fwd_attributes();

@@ -28,12 +28,6 @@ P2_DEVICE f32x16 mfma32(uint4 a, uint4 b, f32x16 c) {
 P2_DEVICE int acc_row(int i, int h) { return (i & 3) + 8 * (i >> 2) + 4 * h; }
 
 // ---------------------------------------------------------------------------
-// 1. step counter
-// ---------------------------------------------------------------------------
-__global__ void step_begin_kernel(int* t) { *t += 1; }
-void step_begin(int* adam_t, hipStream_t s) { hipLaunchKernelGGL(step_begin_kernel, dim3(1), dim3(1), 0, s, adam_t); }
-
-// ---------------------------------------------------------------------------
 // 2. conv1 (1->32, 5x5, pad 2) + bias + ReLU + maxpool 2x2.  Grid (4, B):
 //    part p of image b handles pooled positions [49p, 49p+49).  oc = tid & 31
 //    is fixed per thread, so its 25 taps live in registers; the 6x6 input window
@@ -208,20 +202,36 @@ __global__ __launch_bounds__(256) void gemm_skinny_kernel(const uint16_t* __rest
   const uint16_t* arow[MT];
 #pragma unroll
   for (int mt = 0; mt < MT; ++mt) arow[mt] = A + size_t(mt * 32 + r) * K + 32 * h;
-#pragma unroll 2
-  for (int g = g0 + wave; g < g1; g += 4) {
-    const int k0 = g * 64;
-    uint4 bq[4], aq[MT][4];
+  // software pipeline: the next group's 16-B loads are in flight while the
+  // current group's MFMAs run
+  uint4 bq[4], aq[MT][4];
+  int g = g0 + wave;
+  auto load = [&](int gg, uint4 (&bb)[4], uint4 (&aa)[MT][4]) {
+    const int k0 = gg * 64;
 #pragma unroll
-    for (int q = 0; q < 4; ++q) bq[q] = ld_nt16(brow + k0 + q * 8);
+    for (int q = 0; q < 4; ++q) bb[q] = ld_nt16(brow + k0 + q * 8);
 #pragma unroll
     for (int mt = 0; mt < MT; ++mt)
 #pragma unroll
-      for (int q = 0; q < 4; ++q) aq[mt][q] = reinterpret_cast<const uint4*>(arow[mt] + k0)[q];
+      for (int q = 0; q < 4; ++q) aa[mt][q] = reinterpret_cast<const uint4*>(arow[mt] + k0)[q];
+  };
+  if (g < g1) load(g, bq, aq);
+  for (; g < g1; g += 4) {
+    uint4 nb[4], na[MT][4];
+    const bool more = g + 4 < g1;
+    if (more) load(g + 4, nb, na);
 #pragma unroll
     for (int q = 0; q < 4; ++q)
 #pragma unroll
       for (int mt = 0; mt < MT; ++mt) acc[mt] = mfma32(aq[mt][q], bq[q], acc[mt]);
+    if (more) {
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        bq[q] = nb[q];
+#pragma unroll
+        for (int mt = 0; mt < MT; ++mt) aq[mt][q] = na[mt][q];
+      }
+    }
   }
 #pragma unroll
   for (int mt = 0; mt < MT; ++mt)
@@ -272,11 +282,22 @@ __global__ __launch_bounds__(256) void head_kernel(const float* __restrict__ sla
     }
     return;
   }
+  // issue every global load up front: this thread's 8-column slice of W2
+  // (reused by the backward), the bias, and the split-K partial sums
+  float wv[kCls][8];
+#pragma unroll
+  for (int c = 0; c < kCls; ++c) {
+    const float4* wp = reinterpret_cast<const float4*>(wl2 + size_t(c) * kHid + k0);
+    const float4 u = wp[0], w = wp[1];
+    wv[c][0] = u.x; wv[c][1] = u.y; wv[c][2] = u.z; wv[c][3] = u.w;
+    wv[c][4] = w.x; wv[c][5] = w.y; wv[c][6] = w.z; wv[c][7] = w.w;
+  }
   float hv[8];
   {
     const float4* bp = reinterpret_cast<const float4*>(bl1 + k0);
     float4 u = bp[0], w = bp[1];
     hv[0] = u.x; hv[1] = u.y; hv[2] = u.z; hv[3] = u.w; hv[4] = w.x; hv[5] = w.y; hv[6] = w.z; hv[7] = w.w;
+#pragma unroll 4
     for (int s = 0; s < S; ++s) {
       const float4* sp = reinterpret_cast<const float4*>(slabs + (size_t(s) * mrows + b) * kHid + k0);
       u = sp[0];
@@ -296,11 +317,10 @@ __global__ __launch_bounds__(256) void head_kernel(const float* __restrict__ sla
   float part[kCls];
 #pragma unroll
   for (int c = 0; c < kCls; ++c) {
-    const float4* wp = reinterpret_cast<const float4*>(wl2 + size_t(c) * kHid + k0);
-    const float4 u = wp[0], w = wp[1];
-    part[c] = hv[0] * u.x + hv[1] * u.y + hv[2] * u.z + hv[3] * u.w + hv[4] * w.x + hv[5] * w.y + hv[6] * w.z +
-              hv[7] * w.w;
-    part[c] = wave_sum(part[c]);
+    float acc = 0.f;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc = fmaf(hv[j], wv[c][j], acc);
+    part[c] = wave_sum(acc);
   }
   if (lane == 0)
 #pragma unroll
@@ -340,10 +360,8 @@ __global__ __launch_bounds__(256) void head_kernel(const float* __restrict__ sla
 #pragma unroll
   for (int c = 0; c < kCls; ++c) {
     const float d = dl[c];
-    const float4* wp = reinterpret_cast<const float4*>(wl2 + size_t(c) * kHid + k0);
-    const float4 u = wp[0], w = wp[1];
-    g[0] = fmaf(d, u.x, g[0]); g[1] = fmaf(d, u.y, g[1]); g[2] = fmaf(d, u.z, g[2]); g[3] = fmaf(d, u.w, g[3]);
-    g[4] = fmaf(d, w.x, g[4]); g[5] = fmaf(d, w.y, g[5]); g[6] = fmaf(d, w.z, g[6]); g[7] = fmaf(d, w.w, g[7]);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) g[j] = fmaf(d, wv[c][j], g[j]);
   }
 #pragma unroll
   for (int j = 0; j < 8; ++j) g[j] = hv[j] > 0.f ? g[j] : 0.f;

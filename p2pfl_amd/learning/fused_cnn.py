@@ -108,25 +108,31 @@ class FusedCNNEngine:
         C.gemm_skinny(self.a1, self.w1bf, self.slabs1, M, HID, FEAT, self.S1)
         C.head(self.slabs1, self.S1, M, self.params, self.off, labels, idx, B, train, self.H, self.dH, self.dHt, self.dlogits, stats)
 
-    def train_step_async(self, x: torch.Tensor, labels: torch.Tensor, idx: Optional[torch.Tensor], B: int, stats: torch.Tensor) -> None:
-        """Enqueue one training step (no host sync; graph-capturable)."""
+    def train_step_async(
+        self, x: torch.Tensor, labels: torch.Tensor, idx: Optional[torch.Tensor], B: int, stats: torch.Tensor, t_off: int
+    ) -> None:
+        """Enqueue one training step (no host sync; graph-capturable).
+
+        Adam uses step ``t = adam_t[0] + t_off`` (base on the device, offset baked
+        into the launch), so a captured epoch needs no per-step counter kernel.
+        """
         if B > self.mrows:
             raise ValueError(f"batch {B} > engine capacity {self.mrows}")
         C, M, a = self.C, self.mrows, self._adam()
-        C.step_begin(self.adam_t)
         self.forward(x, labels, idx, B, stats, True)
-        C.fc2_wgrad_adam(self.dlogits, self.H, B, self.params, self.m, self.v, self.gdump, self.off, self.adam_t, *a)
+        C.fc2_wgrad_adam(self.dlogits, self.H, B, self.params, self.m, self.v, self.gdump, self.off, self.adam_t, t_off, *a)
         C.gemm_skinny(self.dH, self.w1tbf, self.slabs2, M, FEAT, HID, self.S2)
-        C.fc1_wgrad_adam(self.dHt, self.a1t, M, self.params, self.m, self.v, self.gdump, self.w1bf, self.w1tbf, self.off, self.adam_t, *a)
+        C.fc1_wgrad_adam(self.dHt, self.a1t, M, self.params, self.m, self.v, self.gdump, self.w1bf, self.w1tbf, self.off, self.adam_t, t_off, *a)
         C.conv2_wgrad(self.slabs2, self.S2, M, self.am2, self.p1, self.wslab2, B)
         C.conv2_dgrad_conv1_wgrad(self.slabs2, self.S2, M, self.am2, self.am1, self.w2q, x, idx, self.wslab1, B)
-        C.conv_adam(self.wslab1, self.wslab2, B, self.params, self.m, self.v, self.gdump, self.w2r, self.w2q, self.off, self.adam_t, *a)
+        C.conv_adam(self.wslab1, self.wslab2, B, self.params, self.m, self.v, self.gdump, self.w2r, self.w2q, self.off, self.adam_t, t_off, *a)
 
     def train_step(self, x: torch.Tensor, y: torch.Tensor) -> float:
-        """Convenience: one step on a uint8 batch ``x`` [B,1,28,28] with labels ``y``; returns the loss."""
+        """Convenience: one eager step on a uint8 batch ``x`` [B,1,28,28] with labels ``y``; returns the loss."""
         B = int(y.shape[0])
         self.stats.zero_()
-        self.train_step_async(x.contiguous(), y.to(torch.int64).contiguous(), None, B, self.stats)
+        self.train_step_async(x.contiguous(), y.to(torch.int64).contiguous(), None, B, self.stats, 1)
+        self.adam_t += 1
         return float(self.stats[0]) / B
 
     @torch.no_grad()
@@ -203,7 +209,7 @@ class FusedCNNLearner(TorchLearner):
             idx = perm[s : s + b]
             st = stats[j] if train else stats[0]
             if train:
-                self.engine.train_step_async(x, y, idx, b, st)
+                self.engine.train_step_async(x, y, idx, b, st, j + 1)
             else:
                 self.engine.forward(x, y, idx, b, st, False)
 
@@ -236,9 +242,11 @@ class FusedCNNLearner(TorchLearner):
         with self._lock:
             self.engine.reset_optimizer()  # Adam re-created per fit (reference quirk Q23)
             loader = self.data.train_dataloader()
-            for _ in range(self.epochs):
+            steps = math.ceil(len(loader.dataset) / loader.batch_size)
+            for epoch in range(self.epochs):
                 if self._interrupt.is_set():
                     return
+                self.engine.adam_t.fill_(epoch * steps)  # Adam step base for this epoch's graph
                 with logger.span(self._addr, "train_epoch"):
                     stats = self._run("train", loader, True, loader.permutation())
                     st = stats.cpu()

@@ -139,7 +139,7 @@ def test_head_and_fc2_wgrad(eng):
     before = eng.params.clone()
     eng.adam_t.fill_(1)
     m_save, v_save = eng.m.clone(), eng.v.clone()
-    eng.C.fc2_wgrad_adam(eng.dlogits, eng.H, B, eng.params, eng.m, eng.v, eng.gdump, eng.off, eng.adam_t, *eng._adam())
+    eng.C.fc2_wgrad_adam(eng.dlogits, eng.H, B, eng.params, eng.m, eng.v, eng.gdump, eng.off, eng.adam_t, 0, *eng._adam())
     torch.cuda.synchronize()
     gw = eng.gdump[eng.off[6] : eng.off[6] + 20480].view(10, 2048)
     gb = eng.gdump[eng.off[7] : eng.off[7] + 10]
@@ -161,7 +161,7 @@ def test_fc1_wgrad_adam(eng):
     before, m0, v0 = eng.params.clone(), eng.m.clone(), eng.v.clone()
     eng.gdump = torch.zeros_like(eng.params)
     eng.adam_t.fill_(1)
-    eng.C.fc1_wgrad_adam(dht, a1t, 32, eng.params, eng.m, eng.v, eng.gdump, eng.w1bf, eng.w1tbf, eng.off, eng.adam_t, *eng._adam())
+    eng.C.fc1_wgrad_adam(dht, a1t, 32, eng.params, eng.m, eng.v, eng.gdump, eng.w1bf, eng.w1tbf, eng.off, eng.adam_t, 0, *eng._adam())
     torch.cuda.synchronize()
     o, ob = eng.off[4], eng.off[5]
     gw = eng.gdump[o : o + 2048 * 3136].view(2048, 3136)
@@ -229,7 +229,7 @@ def test_conv_adam_and_shadows(eng):
     before, m0, v0 = eng.params.clone(), eng.m.clone(), eng.v.clone()
     eng.gdump = torch.zeros_like(eng.params)
     eng.adam_t.fill_(1)
-    eng.C.conv_adam(ws1, ws2, B, eng.params, eng.m, eng.v, eng.gdump, eng.w2r, eng.w2q, eng.off, eng.adam_t, *eng._adam())
+    eng.C.conv_adam(ws1, ws2, B, eng.params, eng.m, eng.v, eng.gdump, eng.w2r, eng.w2q, eng.off, eng.adam_t, 0, *eng._adam())
     torch.cuda.synchronize()
     o = eng.off
     torch.testing.assert_close(eng.gdump[o[0] : o[0] + 800], ws1.view(32, 832)[:, :800].sum(0), atol=1e-7, rtol=1e-5)
