@@ -13,12 +13,13 @@
 //  4 head              slab reduce + bias + ReLU -> H; FC2; softmax-xent; dlogits;
 //                      dH = relu'(H) * dlogits W2 (and dH^T); loss/accuracy stats
 //  5 fc2_wgrad_adam    dW2 = dlogits^T H and db2, Adam applied in place
-//  6 gemm_skinny       dA1 = dH x W1 (reads the W1^T bf16 shadow), split-K slabs
+//  6 gemm_da1_route    dA1 = dH x W1 (W1^T bf16 shadow) + pool2/ReLU backward in
+//                      the epilogue -> dC2 maps (two layouts) + fp32 bias terms
 //  7 fc1_wgrad_adam    dW1 = dH^T A1 on MFMA with Adam fused into the epilogue:
 //                      the 6.4 M-element gradient never touches memory; writes
 //                      W1 (fp32), m, v and both bf16 shadows (W1, W1^T)
-//  8 conv2_wgrad       per image: maxpool/ReLU backward of dA1 -> dC2, then
-//                      dW2c = dC2 x im2col(P1) on MFMA -> per-image slab
+//  8 conv2_wgrad       per image and tap group: dW2c = dC2 x im2col(P1) on MFMA
+//                      (aligned shifted-image LDS copies) -> per-image slab
 //  9 conv2_dgrad_c1    per image: dP1 = transposed conv on MFMA, pool1/ReLU
 //                      backward into a dense LDS map, conv1 weight gradient as a
 //                      second MFMA GEMM -> slab
@@ -54,28 +55,34 @@ struct Offsets {
 void conv1_fwd(const uint8_t* x, const int64_t* idx, const float* params, Offsets off, uint16_t* p1, uint8_t* am1,
                int B, hipStream_t s);
 
-void conv2_fwd(const uint16_t* p1, const uint16_t* w2r, const float* params, Offsets off, uint16_t* a1, uint16_t* a1t,
-               uint8_t* am2, int B, int mrows, hipStream_t s);
+void conv2_fwd(const uint16_t* p1, const uint16_t* w2r, const float* params, Offsets off, uint16_t* a1, uint8_t* am2,
+               int B, hipStream_t s);
 
 void gemm_skinny(const uint16_t* A, const uint16_t* Bt, float* slabs, int mrows, int N, int K, int S, hipStream_t s);
 
 void head(const float* slabs, int S, int mrows, const float* params, Offsets off, const int64_t* labels,
-          const int64_t* idx, int B, int train, uint16_t* H, uint16_t* dH, uint16_t* dHt, float* dlogits,
-          float* stats, hipStream_t s);
+          const int64_t* idx, int B, int train, uint16_t* H, uint16_t* dH, float* dlogits, float* stats,
+          hipStream_t s);
 
 void fc2_wgrad_adam(const float* dlogits, const uint16_t* H, int B, float* params, float* m, float* v,
                     float* gdump, Offsets off, const int* adam_t, int t_off, AdamCfg cfg, hipStream_t s);
 
-void fc1_wgrad_adam(const uint16_t* dHt, const uint16_t* a1t, int mrows, float* params, float* m, float* v,
+void fc1_wgrad_adam(const uint16_t* dH, const uint16_t* a1, int mrows, float* params, float* m, float* v,
                     float* gdump, uint16_t* w1bf, uint16_t* w1tbf, Offsets off, const int* adam_t, int t_off,
                     AdamCfg cfg, hipStream_t s);
 
-void conv2_wgrad(const float* slabs2, int S2, int mrows, const uint8_t* am2, const uint16_t* p1, float* wslab, int B,
-                 hipStream_t s);
+// dA1 = dH x W1 (reads the W1^T shadow) with the pool2/ReLU backward fused into
+// the epilogue: writes dC2 as a [B][64][14x16] map (wgrad A operand), as a
+// padded HWC [B][18x18][64] image (dgrad A operand), and the fp32 alive-masked
+// dA1 [B][3136] (bias gradient).  Every 2x2 window writes all 4 positions, so
+// no per-step clearing is needed (padding is zero from allocation).
+void gemm_da1_route(const uint16_t* dH, const uint16_t* w1t, const uint8_t* am2, int mrows, int B, uint16_t* dc2m,
+                    uint16_t* dch, float* gb, hipStream_t s);
 
-void conv2_dgrad_conv1_wgrad(const float* slabs2, int S2, int mrows, const uint8_t* am2, const uint8_t* am1,
-                             const uint16_t* w2q, const uint8_t* x, const int64_t* idx, float* wslab1, int B,
-                             hipStream_t s);
+void conv2_wgrad(const uint16_t* dc2m, const float* gb, const uint16_t* p1, float* wslab, int B, hipStream_t s);
+
+void conv2_dgrad_conv1_wgrad(const uint16_t* dch, const uint8_t* am1, const uint16_t* w2q, const uint8_t* x,
+                             const int64_t* idx, float* wslab1, int B, hipStream_t s);
 
 void conv_adam(const float* wslab1, const float* wslab2, int B, float* params, float* m, float* v, float* gdump,
                uint16_t* w2r, uint16_t* w2q, Offsets off, const int* adam_t, int t_off, AdamCfg cfg, hipStream_t s);

@@ -66,7 +66,7 @@ void k_conv1_fwd(torch::Tensor x, c10::optional<torch::Tensor> idx, torch::Tenso
 }
 
 void k_conv2_fwd(torch::Tensor p1, torch::Tensor w2r, torch::Tensor params, std::vector<int64_t> off,
-                 torch::Tensor a1, torch::Tensor a1t, torch::Tensor am2, int64_t B, int64_t mrows) {
+                 torch::Tensor a1, torch::Tensor am2, int64_t B, int64_t mrows) {
   const c10::DeviceGuard g(params.device());
   check_batch(int(B), int(mrows));
   Offsets o = offsets(off);
@@ -74,8 +74,7 @@ void k_conv2_fwd(torch::Tensor p1, torch::Tensor w2r, torch::Tensor params, std:
                    reinterpret_cast<uint16_t*>(ptr<at::BFloat16>(w2r, torch::kBFloat16, 51200, "w2r")),
                    ptr<float>(params, torch::kFloat32, params_end(o), "params"), o,
                    reinterpret_cast<uint16_t*>(ptr<at::BFloat16>(a1, torch::kBFloat16, mrows * 3136, "a1")),
-                   reinterpret_cast<uint16_t*>(ptr<at::BFloat16>(a1t, torch::kBFloat16, mrows * 3136, "a1t")),
-                   ptr<uint8_t>(am2, torch::kUInt8, B * 3136, "am2"), int(B), int(mrows), stream());
+                   ptr<uint8_t>(am2, torch::kUInt8, B * 3136, "am2"), int(B), stream());
 }
 
 void k_gemm_skinny(torch::Tensor A, torch::Tensor Bt, torch::Tensor slabs, int64_t mrows, int64_t N, int64_t K,
@@ -91,7 +90,7 @@ void k_gemm_skinny(torch::Tensor A, torch::Tensor Bt, torch::Tensor slabs, int64
 
 void k_head(torch::Tensor slabs, int64_t S, int64_t mrows, torch::Tensor params, std::vector<int64_t> off,
             torch::Tensor labels, c10::optional<torch::Tensor> idx, int64_t B, bool train, torch::Tensor H,
-            torch::Tensor dH, torch::Tensor dHt, torch::Tensor dlogits, torch::Tensor stats) {
+            torch::Tensor dH, torch::Tensor dlogits, torch::Tensor stats) {
   const c10::DeviceGuard g(params.device());
   check_batch(int(B), int(mrows));
   Offsets o = offsets(off);
@@ -101,7 +100,6 @@ void k_head(torch::Tensor slabs, int64_t S, int64_t mrows, torch::Tensor params,
               ptr<int64_t>(labels, torch::kInt64, 1, "labels", 8), idx_ptr(idx, B), int(B), train ? 1 : 0,
               reinterpret_cast<uint16_t*>(ptr<at::BFloat16>(H, torch::kBFloat16, mrows * 2048, "H")),
               reinterpret_cast<uint16_t*>(ptr<at::BFloat16>(dH, torch::kBFloat16, mrows * 2048, "dH")),
-              reinterpret_cast<uint16_t*>(ptr<at::BFloat16>(dHt, torch::kBFloat16, mrows * 2048, "dHt")),
               ptr<float>(dlogits, torch::kFloat32, mrows * 10, "dlogits"), ptr<float>(stats, torch::kFloat32, 2, "stats", 4),
               stream());
 }
@@ -123,7 +121,7 @@ void k_fc2_wgrad_adam(torch::Tensor dlogits, torch::Tensor H, int64_t B, torch::
                         ptr<int>(adam_t, torch::kInt32, 1, "adam_t", 4), int(t_off), cfg(lr, b1, b2, eps, wd), stream());
 }
 
-void k_fc1_wgrad_adam(torch::Tensor dHt, torch::Tensor a1t, int64_t mrows, torch::Tensor params, torch::Tensor m,
+void k_fc1_wgrad_adam(torch::Tensor dH, torch::Tensor a1, int64_t mrows, torch::Tensor params, torch::Tensor m,
                       torch::Tensor v, c10::optional<torch::Tensor> gdump, torch::Tensor w1bf, torch::Tensor w1tbf,
                       std::vector<int64_t> off, torch::Tensor adam_t, int64_t t_off, double lr, double b1, double b2,
                       double eps, double wd) {
@@ -131,8 +129,8 @@ void k_fc1_wgrad_adam(torch::Tensor dHt, torch::Tensor a1t, int64_t mrows, torch
   TORCH_CHECK(mrows == 32 || mrows == 64, "mrows must be 32 or 64");
   Offsets o = offsets(off);
   const int64_t n = params_end(o);
-  p2cnn::fc1_wgrad_adam(reinterpret_cast<uint16_t*>(ptr<at::BFloat16>(dHt, torch::kBFloat16, 2048 * mrows, "dHt")),
-                        reinterpret_cast<uint16_t*>(ptr<at::BFloat16>(a1t, torch::kBFloat16, 3136 * mrows, "a1t")),
+  p2cnn::fc1_wgrad_adam(reinterpret_cast<uint16_t*>(ptr<at::BFloat16>(dH, torch::kBFloat16, mrows * 2048, "dH")),
+                        reinterpret_cast<uint16_t*>(ptr<at::BFloat16>(a1, torch::kBFloat16, mrows * 3136, "a1")),
                         int(mrows), ptr<float>(params, torch::kFloat32, n, "params"),
                         ptr<float>(m, torch::kFloat32, n, "m"), ptr<float>(v, torch::kFloat32, n, "v"),
                         optr<float>(gdump, torch::kFloat32, n, "gdump"),
@@ -141,25 +139,35 @@ void k_fc1_wgrad_adam(torch::Tensor dHt, torch::Tensor a1t, int64_t mrows, torch
                         o, ptr<int>(adam_t, torch::kInt32, 1, "adam_t", 4), int(t_off), cfg(lr, b1, b2, eps, wd), stream());
 }
 
-void k_conv2_wgrad(torch::Tensor slabs2, int64_t S2, int64_t mrows, torch::Tensor am2, torch::Tensor p1,
-                   torch::Tensor wslab2, int64_t B) {
-  const c10::DeviceGuard g(p1.device());
+void k_gemm_da1_route(torch::Tensor dH, torch::Tensor w1tbf, torch::Tensor am2, int64_t mrows, int64_t B,
+                      torch::Tensor dc2m, torch::Tensor dch, torch::Tensor gb) {
+  const c10::DeviceGuard g(dH.device());
   check_batch(int(B), int(mrows));
-  p2cnn::conv2_wgrad(ptr<float>(slabs2, torch::kFloat32, S2 * mrows * 3136, "slabs2"), int(S2), int(mrows),
-                     ptr<uint8_t>(am2, torch::kUInt8, B * 3136, "am2"),
+  p2cnn::gemm_da1_route(reinterpret_cast<uint16_t*>(ptr<at::BFloat16>(dH, torch::kBFloat16, mrows * 2048, "dH")),
+                        reinterpret_cast<uint16_t*>(ptr<at::BFloat16>(w1tbf, torch::kBFloat16, 2048 * 3136, "w1tbf")),
+                        ptr<uint8_t>(am2, torch::kUInt8, B * 3136, "am2"), int(mrows), int(B),
+                        reinterpret_cast<uint16_t*>(ptr<at::BFloat16>(dc2m, torch::kBFloat16, B * 64 * 224, "dc2m")),
+                        reinterpret_cast<uint16_t*>(ptr<at::BFloat16>(dch, torch::kBFloat16, B * 324 * 64, "dch")),
+                        ptr<float>(gb, torch::kFloat32, B * 3136, "gb"), stream());
+}
+
+void k_conv2_wgrad(torch::Tensor dc2m, torch::Tensor gb, torch::Tensor p1, torch::Tensor wslab2, int64_t B) {
+  const c10::DeviceGuard g(p1.device());
+  TORCH_CHECK(B >= 1 && B <= 64, "bad batch");
+  p2cnn::conv2_wgrad(reinterpret_cast<uint16_t*>(ptr<at::BFloat16>(dc2m, torch::kBFloat16, B * 64 * 224, "dc2m")),
+                     ptr<float>(gb, torch::kFloat32, B * 3136, "gb"),
                      reinterpret_cast<uint16_t*>(ptr<at::BFloat16>(p1, torch::kBFloat16, B * 196 * 32, "p1")),
                      ptr<float>(wslab2, torch::kFloat32, B * p2cnn::kSlab2, "wslab2"), int(B), stream());
 }
 
-void k_conv2_dgrad(torch::Tensor slabs2, int64_t S2, int64_t mrows, torch::Tensor am2, torch::Tensor am1,
-                   torch::Tensor w2q, torch::Tensor x, c10::optional<torch::Tensor> idx, torch::Tensor wslab1,
-                   int64_t B) {
+void k_conv2_dgrad(torch::Tensor dch, torch::Tensor am1, torch::Tensor w2q, torch::Tensor x,
+                   c10::optional<torch::Tensor> idx, torch::Tensor wslab1, int64_t B) {
   const c10::DeviceGuard g(w2q.device());
-  check_batch(int(B), int(mrows));
+  TORCH_CHECK(B >= 1 && B <= 64, "bad batch");
   if (!idx.has_value()) TORCH_CHECK(x.numel() / 784 >= B, "x has fewer than B rows");
   p2cnn::conv2_dgrad_conv1_wgrad(
-      ptr<float>(slabs2, torch::kFloat32, S2 * mrows * 3136, "slabs2"), int(S2), int(mrows),
-      ptr<uint8_t>(am2, torch::kUInt8, B * 3136, "am2"), ptr<uint8_t>(am1, torch::kUInt8, B * 196 * 32, "am1"),
+      reinterpret_cast<uint16_t*>(ptr<at::BFloat16>(dch, torch::kBFloat16, B * 324 * 64, "dch")),
+      ptr<uint8_t>(am1, torch::kUInt8, B * 196 * 32, "am1"),
       reinterpret_cast<uint16_t*>(ptr<at::BFloat16>(w2q, torch::kBFloat16, 51200, "w2q")),
       ptr<uint8_t>(x, torch::kUInt8, 784, "x", 1), idx_ptr(idx, B),
       ptr<float>(wslab1, torch::kFloat32, B * p2cnn::kSlab1, "wslab1"), int(B), stream());
@@ -208,6 +216,7 @@ void register_cnn(pybind11::module& m) {
   c.def("head", &k_head);
   c.def("fc2_wgrad_adam", &k_fc2_wgrad_adam);
   c.def("fc1_wgrad_adam", &k_fc1_wgrad_adam);
+  c.def("gemm_da1_route", &k_gemm_da1_route);
   c.def("conv2_wgrad", &k_conv2_wgrad);
   c.def("conv2_dgrad_conv1_wgrad", &k_conv2_dgrad);
   c.def("conv_adam", &k_conv_adam);

@@ -5,7 +5,6 @@
 //   P1   bf16   [B][196][32]         pooled conv1 output, HWC (channels contiguous)
 //   AM1  uint8  [B][196][32]         pool1 argmax (dy*2+dx) or 4 = dead (ReLU zero)
 //   A1   bf16   [mrows][3136]        pooled conv2 output, PyTorch flatten order c*49+y*7+x
-//   A1T  bf16   [3136][mrows]        the same, transposed (B operand of dW1)
 //   AM2  uint8  [B][3136]            pool2 argmax / dead
 //   W2r  bf16   [64][25][32]         conv2 weight, (oc, tap, ic)   -- conv2_fwd B operand
 //   W1bf bf16   [2048][3136]         FC1 weight (row-major = [N][K]) -- FC1 forward
@@ -102,8 +101,7 @@ constexpr int kConv2Lds = kImgLds + kW2Lds;
 __global__ __launch_bounds__(448) void conv2_fwd_kernel(const uint16_t* __restrict__ p1,
                                                         const uint16_t* __restrict__ w2r,
                                                         const float* __restrict__ b2, uint16_t* __restrict__ a1,
-                                                        uint16_t* __restrict__ a1t, uint8_t* __restrict__ am2,
-                                                        int mrows) {
+                                                        uint8_t* __restrict__ am2) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   uint16_t* simg = reinterpret_cast<uint16_t*>(smem);
   uint16_t* sw = reinterpret_cast<uint16_t*>(smem + kImgLds);
@@ -157,9 +155,7 @@ __global__ __launch_bounds__(448) void conv2_fwd_kernel(const uint16_t* __restri
       }
     }
     const int feat = (nh * 32 + oc) * 49 + pp;
-    const uint16_t hv = f32_to_bf16(best);
-    a1[size_t(b) * kFeat + feat] = hv;
-    a1t[size_t(feat) * mrows + b] = hv;
+    a1[size_t(b) * kFeat + feat] = f32_to_bf16(best);
     am2[size_t(b) * kFeat + feat] = best > 0.f ? uint8_t(arg) : uint8_t(4);
   }
 }
@@ -169,10 +165,9 @@ void init_fwd_attributes() {
                                hipFuncAttributeMaxDynamicSharedMemorySize, kConv2Lds));
 }
 
-void conv2_fwd(const uint16_t* p1, const uint16_t* w2r, const float* params, Offsets off, uint16_t* a1, uint16_t* a1t,
-               uint8_t* am2, int B, int mrows, hipStream_t s) {
-  hipLaunchKernelGGL(conv2_fwd_kernel, dim3(2, B), dim3(448), kConv2Lds, s, p1, w2r, params + off.c2b, a1, a1t, am2,
-                     mrows);
+void conv2_fwd(const uint16_t* p1, const uint16_t* w2r, const float* params, Offsets off, uint16_t* a1,
+               uint8_t* am2, int B, hipStream_t s) {
+  hipLaunchKernelGGL(conv2_fwd_kernel, dim3(2, B), dim3(448), kConv2Lds, s, p1, w2r, params + off.c2b, a1, am2);
 }
 
 // ---------------------------------------------------------------------------
@@ -266,7 +261,7 @@ __global__ __launch_bounds__(256) void head_kernel(const float* __restrict__ sla
                                                    const float* __restrict__ bl2, const int64_t* __restrict__ labels,
                                                    const int64_t* __restrict__ idx, int B, int train,
                                                    uint16_t* __restrict__ H, uint16_t* __restrict__ dH,
-                                                   uint16_t* __restrict__ dHt, float* __restrict__ dlogits,
+                                                   float* __restrict__ dlogits,
                                                    float* __restrict__ stats) {
   __shared__ float red[4][kCls];
   __shared__ float dl[kCls];
@@ -276,8 +271,6 @@ __global__ __launch_bounds__(256) void head_kernel(const float* __restrict__ sla
     if (train) {
       reinterpret_cast<uint4*>(dH + size_t(b) * kHid + k0)[0] = make_uint4(0, 0, 0, 0);
       reinterpret_cast<uint4*>(H + size_t(b) * kHid + k0)[0] = make_uint4(0, 0, 0, 0);
-#pragma unroll
-      for (int j = 0; j < 8; ++j) dHt[size_t(k0 + j) * mrows + b] = 0;
       if (tid < kCls) dlogits[b * kCls + tid] = 0.f;
     }
     return;
@@ -371,16 +364,13 @@ __global__ __launch_bounds__(256) void head_kernel(const float* __restrict__ sla
   gb.z = pack_bf16x2(g[4], g[5]);
   gb.w = pack_bf16x2(g[6], g[7]);
   reinterpret_cast<uint4*>(dH + size_t(b) * kHid + k0)[0] = gb;
-  const uint16_t* gs = reinterpret_cast<const uint16_t*>(&gb);
-#pragma unroll
-  for (int j = 0; j < 8; ++j) dHt[size_t(k0 + j) * mrows + b] = gs[j];
 }
 
 void head(const float* slabs, int S, int mrows, const float* params, Offsets off, const int64_t* labels,
-          const int64_t* idx, int B, int train, uint16_t* H, uint16_t* dH, uint16_t* dHt, float* dlogits,
+          const int64_t* idx, int B, int train, uint16_t* H, uint16_t* dH, float* dlogits,
           float* stats, hipStream_t s) {
   hipLaunchKernelGGL(head_kernel, dim3(train ? mrows : B), dim3(256), 0, s, slabs, S, mrows, params + off.l1b,
-                     params + off.l2w, params + off.l2b, labels, idx, B, train, H, dH, dHt, dlogits, stats);
+                     params + off.l2w, params + off.l2b, labels, idx, B, train, H, dH, dlogits, stats);
 }
 
 // ---------------------------------------------------------------------------

@@ -45,7 +45,6 @@ class FusedCNNEngine:
         mrows: int = 32,
         arena: Optional[ModuleArena] = None,
         split_fc1: int = 7,
-        split_dA1: int = 4,
     ) -> None:
         self.C = ops.ext().cnn
         self.C.init()
@@ -61,7 +60,7 @@ class FusedCNNEngine:
         self.off: List[int] = [int(o) for o in lay.offsets]
         self.lr, self.betas, self.eps, self.wd = lr, betas, eps, weight_decay
         self.mrows = mrows
-        self.S1, self.S2 = split_fc1, split_dA1
+        self.S1 = split_fc1
         dev, bf = self.device, torch.bfloat16
         z = lambda *s, dt=torch.float32: torch.zeros(*s, dtype=dt, device=dev)  # noqa: E731
         n = self.arena.flat.numel()
@@ -73,11 +72,12 @@ class FusedCNNEngine:
         # activations / workspaces (sized for mrows samples)
         M = mrows
         self.p1, self.am1 = z(M * 196 * 32, dt=bf), z(M * 196 * 32, dt=torch.uint8)
-        self.a1, self.a1t, self.am2 = z(M * FEAT, dt=bf), z(FEAT * M, dt=bf), z(M * FEAT, dt=torch.uint8)
+        self.a1, self.am2 = z(M * FEAT, dt=bf), z(M * FEAT, dt=torch.uint8)
         self.slabs1 = z(self.S1 * M * HID)
-        self.H, self.dH, self.dHt = z(M * HID, dt=bf), z(M * HID, dt=bf), z(HID * M, dt=bf)
+        self.H, self.dH = z(M * HID, dt=bf), z(M * HID, dt=bf)
         self.dlogits = z(M * 10)
-        self.slabs2 = z(self.S2 * M * FEAT)
+        # dC2 maps written by gemm_da1_route (padding stays zero from here on)
+        self.dc2m, self.dch, self.gb = z(M * 64 * 224, dt=bf), z(M * 324 * 64, dt=bf), z(M * FEAT)
         self.wslab1, self.wslab2 = z(M * 832), z(M * 51264)
         self.stats = z(2)
         self.gdump: Optional[torch.Tensor] = None
@@ -104,9 +104,9 @@ class FusedCNNEngine:
     def forward(self, x: torch.Tensor, labels: torch.Tensor, idx: Optional[torch.Tensor], B: int, stats: torch.Tensor, train: bool) -> None:
         C, M = self.C, self.mrows
         C.conv1_fwd(x, idx, self.params, self.off, self.p1, self.am1, B)
-        C.conv2_fwd(self.p1, self.w2r, self.params, self.off, self.a1, self.a1t, self.am2, B, M)
+        C.conv2_fwd(self.p1, self.w2r, self.params, self.off, self.a1, self.am2, B, M)
         C.gemm_skinny(self.a1, self.w1bf, self.slabs1, M, HID, FEAT, self.S1)
-        C.head(self.slabs1, self.S1, M, self.params, self.off, labels, idx, B, train, self.H, self.dH, self.dHt, self.dlogits, stats)
+        C.head(self.slabs1, self.S1, M, self.params, self.off, labels, idx, B, train, self.H, self.dH, self.dlogits, stats)
 
     def train_step_async(
         self, x: torch.Tensor, labels: torch.Tensor, idx: Optional[torch.Tensor], B: int, stats: torch.Tensor, t_off: int
@@ -121,10 +121,10 @@ class FusedCNNEngine:
         C, M, a = self.C, self.mrows, self._adam()
         self.forward(x, labels, idx, B, stats, True)
         C.fc2_wgrad_adam(self.dlogits, self.H, B, self.params, self.m, self.v, self.gdump, self.off, self.adam_t, t_off, *a)
-        C.gemm_skinny(self.dH, self.w1tbf, self.slabs2, M, FEAT, HID, self.S2)
-        C.fc1_wgrad_adam(self.dHt, self.a1t, M, self.params, self.m, self.v, self.gdump, self.w1bf, self.w1tbf, self.off, self.adam_t, t_off, *a)
-        C.conv2_wgrad(self.slabs2, self.S2, M, self.am2, self.p1, self.wslab2, B)
-        C.conv2_dgrad_conv1_wgrad(self.slabs2, self.S2, M, self.am2, self.am1, self.w2q, x, idx, self.wslab1, B)
+        C.gemm_da1_route(self.dH, self.w1tbf, self.am2, M, B, self.dc2m, self.dch, self.gb)
+        C.fc1_wgrad_adam(self.dH, self.a1, M, self.params, self.m, self.v, self.gdump, self.w1bf, self.w1tbf, self.off, self.adam_t, t_off, *a)
+        C.conv2_wgrad(self.dc2m, self.gb, self.p1, self.wslab2, B)
+        C.conv2_dgrad_conv1_wgrad(self.dch, self.am1, self.w2q, x, idx, self.wslab1, B)
         C.conv_adam(self.wslab1, self.wslab2, B, self.params, self.m, self.v, self.gdump, self.w2r, self.w2q, self.off, self.adam_t, t_off, *a)
 
     def train_step(self, x: torch.Tensor, y: torch.Tensor) -> float:
