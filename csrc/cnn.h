@@ -7,24 +7,25 @@
 //
 //  1 conv1_fwd         direct 5x5 conv + bias + ReLU + maxpool, input gathered
 //                      by index from the uint8 dataset (/255 folded in) -> P1 (HWC bf16) + argmax
-//  2 conv2_fwd         implicit-GEMM on MFMA 32x32x16 bf16, image + weights in
-//                      LDS, bias + ReLU + maxpool epilogue -> A1 (+ A1^T) + argmax
+//                      (+ kx-shifted planar copies of P1 for conv2_wgrad when training)
+//  2 conv2_fwd         implicit-GEMM on MFMA 32x32x16 bf16, one wave per pooled row,
+//                      operands streamed from L2, bias + ReLU + maxpool epilogue -> A1 + argmax
 //  3 gemm_skinny       FC1: [B x 3136] x [3136 x 2048], split-K fp32 slabs
 //  4 head              slab reduce + bias + ReLU -> H; FC2; softmax-xent; dlogits;
-//                      dH = relu'(H) * dlogits W2 (and dH^T); loss/accuracy stats
+//                      dH = relu'(H) * dlogits W2; loss/accuracy stats
 //  5 fc2_wgrad_adam    dW2 = dlogits^T H and db2, Adam applied in place
 //  6 gemm_da1_route    dA1 = dH x W1 (W1^T bf16 shadow) + pool2/ReLU backward in
 //                      the epilogue -> dC2 maps (two layouts) + fp32 bias terms
 //  7 fc1_wgrad_adam    dW1 = dH^T A1 on MFMA with Adam fused into the epilogue:
 //                      the 6.4 M-element gradient never touches memory; writes
 //                      W1 (fp32), m, v and both bf16 shadows (W1, W1^T)
-//  8 conv2_wgrad       per image and tap group: dW2c = dC2 x im2col(P1) on MFMA
-//                      (aligned shifted-image LDS copies) -> per-image slab
-//  9 conv2_dgrad_c1    per image: dP1 = transposed conv on MFMA, pool1/ReLU
-//                      backward into a dense LDS map, conv1 weight gradient as a
-//                      second MFMA GEMM -> slab
-// 10 conv_adam         reduce the per-image slabs + Adam for conv params + packed
-//                      bf16 shadows of conv2 (two layouts)
+//  8 conv2_wgrad       one wave per (tap, image pair): dW2[:, :, tap] = dC2 x
+//                      shifted P1 on MFMA, operands streamed from L2 -> slab per pair
+//  9 conv2_dgrad_c1    one wave per (image, 32-position tile): dP1 = transposed
+//                      conv on MFMA, then the conv1 weight gradient as a sparse
+//                      fp32 gather at each pool1 argmax pixel -> slab per tile
+// 10 conv_adam         fixed-order slab reduction (+ conv2 bias from gB) + Adam
+//                      for the conv params + packed bf16 conv2 shadows (two layouts)
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -52,8 +53,9 @@ struct Offsets {
   int64_t c1w, c1b, c2w, c2b, l1w, l1b, l2w, l2b;
 };
 
+// p1s (may be null = inference): [B][5][32][18][16] shifted copies, zero padding.
 void conv1_fwd(const uint8_t* x, const int64_t* idx, const float* params, Offsets off, uint16_t* p1, uint8_t* am1,
-               int B, hipStream_t s);
+               uint16_t* p1s, int B, hipStream_t s);
 
 void conv2_fwd(const uint16_t* p1, const uint16_t* w2r, const float* params, Offsets off, uint16_t* a1, uint8_t* am2,
                int B, hipStream_t s);
@@ -79,19 +81,25 @@ void fc1_wgrad_adam(const uint16_t* dH, const uint16_t* a1, int mrows, float* pa
 void gemm_da1_route(const uint16_t* dH, const uint16_t* w1t, const uint8_t* am2, int mrows, int B, uint16_t* dc2m,
                     uint16_t* dch, float* gb, hipStream_t s);
 
-void conv2_wgrad(const uint16_t* dc2m, const float* gb, const uint16_t* p1, float* wslab, int B, hipStream_t s);
+void conv2_wgrad(const uint16_t* dc2m, const uint16_t* p1s, float* wslab2, int B, hipStream_t s);
 
 void conv2_dgrad_conv1_wgrad(const uint16_t* dch, const uint8_t* am1, const uint16_t* w2q, const uint8_t* x,
                              const int64_t* idx, float* wslab1, int B, hipStream_t s);
 
-void conv_adam(const float* wslab1, const float* wslab2, int B, float* params, float* m, float* v, float* gdump,
-               uint16_t* w2r, uint16_t* w2q, Offsets off, const int* adam_t, int t_off, AdamCfg cfg, hipStream_t s);
+void conv_adam(const float* wslab1, const float* wslab2, const float* gb, int B, float* params, float* m, float* v,
+               float* gdump, uint16_t* w2r, uint16_t* w2q, Offsets off, const int* adam_t, int t_off, AdamCfg cfg,
+               hipStream_t s);
 
 // Standalone packing of the bf16 shadows from fp32 params (after set_parameters).
 void pack_shadows(const float* params, Offsets off, uint16_t* w2r, uint16_t* w2q, uint16_t* w1bf, uint16_t* w1tbf,
                   hipStream_t s);
 
-constexpr int kSlab1 = kC1 * kTaps + kC1;         // conv1 weight + bias grads per image (832)
-constexpr int kSlab2 = kC2 * kC1 * kTaps + kC2;   // conv2 weight + bias grads per image (51264)
+constexpr int kP1sPlane = 18 * 16;                 // one shifted padded P1 channel plane
+constexpr int kP1s = 5 * kC1 * kP1sPlane;          // P1s elements per image (46080)
+constexpr int kDgTiles = 7;                        // 32-position tiles per image in conv2_dgrad
+constexpr int kSlab1 = kC1 * kTaps + kC1;          // conv1 weight + bias partial per (image, tile) (832)
+constexpr int kWgG = 2;                            // images per conv2_wgrad wave
+constexpr int kSlab2 = kTaps * kC2 * kC1;          // conv2 weight partial per image pair, [tap][oc][ic]
+__host__ __device__ inline int wgrad_groups(int B) { return (B + kWgG - 1) / kWgG; }
 
 }  // namespace p2cnn

@@ -54,15 +54,18 @@ const int64_t* idx_ptr(const c10::optional<torch::Tensor>& idx, int B) {
 // learner guarantees idx values are permutations of the dataset rows.
 
 void k_conv1_fwd(torch::Tensor x, c10::optional<torch::Tensor> idx, torch::Tensor params, std::vector<int64_t> off,
-                 torch::Tensor p1, torch::Tensor am1, int64_t B) {
+                 torch::Tensor p1, torch::Tensor am1, c10::optional<torch::Tensor> p1s, int64_t B) {
   const c10::DeviceGuard g(params.device());
+  TORCH_CHECK(B >= 1 && B <= 64, "bad batch");
   Offsets o = offsets(off);
   TORCH_CHECK(x.numel() % 784 == 0, "x must be [N,1,28,28] uint8");
   if (!idx.has_value()) TORCH_CHECK(x.numel() / 784 >= B, "x has fewer than B rows");
   p2cnn::conv1_fwd(ptr<uint8_t>(x, torch::kUInt8, 784, "x", 1), idx_ptr(idx, B),
                    ptr<float>(params, torch::kFloat32, params_end(o), "params"), o,
                    reinterpret_cast<uint16_t*>(ptr<at::BFloat16>(p1, torch::kBFloat16, B * 196 * 32, "p1")),
-                   ptr<uint8_t>(am1, torch::kUInt8, B * 196 * 32, "am1"), int(B), stream());
+                   ptr<uint8_t>(am1, torch::kUInt8, B * 196 * 32, "am1"),
+                   reinterpret_cast<uint16_t*>(optr<at::BFloat16>(p1s, torch::kBFloat16, B * p2cnn::kP1s, "p1s")),
+                   int(B), stream());
 }
 
 void k_conv2_fwd(torch::Tensor p1, torch::Tensor w2r, torch::Tensor params, std::vector<int64_t> off,
@@ -151,13 +154,13 @@ void k_gemm_da1_route(torch::Tensor dH, torch::Tensor w1tbf, torch::Tensor am2, 
                         ptr<float>(gb, torch::kFloat32, B * 3136, "gb"), stream());
 }
 
-void k_conv2_wgrad(torch::Tensor dc2m, torch::Tensor gb, torch::Tensor p1, torch::Tensor wslab2, int64_t B) {
-  const c10::DeviceGuard g(p1.device());
+void k_conv2_wgrad(torch::Tensor dc2m, torch::Tensor p1s, torch::Tensor wslab2, int64_t B) {
+  const c10::DeviceGuard g(dc2m.device());
   TORCH_CHECK(B >= 1 && B <= 64, "bad batch");
   p2cnn::conv2_wgrad(reinterpret_cast<uint16_t*>(ptr<at::BFloat16>(dc2m, torch::kBFloat16, B * 64 * 224, "dc2m")),
-                     ptr<float>(gb, torch::kFloat32, B * 3136, "gb"),
-                     reinterpret_cast<uint16_t*>(ptr<at::BFloat16>(p1, torch::kBFloat16, B * 196 * 32, "p1")),
-                     ptr<float>(wslab2, torch::kFloat32, B * p2cnn::kSlab2, "wslab2"), int(B), stream());
+                     reinterpret_cast<uint16_t*>(ptr<at::BFloat16>(p1s, torch::kBFloat16, B * p2cnn::kP1s, "p1s")),
+                     ptr<float>(wslab2, torch::kFloat32, p2cnn::wgrad_groups(int(B)) * int64_t(p2cnn::kSlab2), "wslab2"),
+                     int(B), stream());
 }
 
 void k_conv2_dgrad(torch::Tensor dch, torch::Tensor am1, torch::Tensor w2q, torch::Tensor x,
@@ -170,18 +173,21 @@ void k_conv2_dgrad(torch::Tensor dch, torch::Tensor am1, torch::Tensor w2q, torc
       ptr<uint8_t>(am1, torch::kUInt8, B * 196 * 32, "am1"),
       reinterpret_cast<uint16_t*>(ptr<at::BFloat16>(w2q, torch::kBFloat16, 51200, "w2q")),
       ptr<uint8_t>(x, torch::kUInt8, 784, "x", 1), idx_ptr(idx, B),
-      ptr<float>(wslab1, torch::kFloat32, B * p2cnn::kSlab1, "wslab1"), int(B), stream());
+      ptr<float>(wslab1, torch::kFloat32, B * p2cnn::kDgTiles * p2cnn::kSlab1, "wslab1"), int(B), stream());
 }
 
-void k_conv_adam(torch::Tensor wslab1, torch::Tensor wslab2, int64_t B, torch::Tensor params, torch::Tensor m,
+void k_conv_adam(torch::Tensor wslab1, torch::Tensor wslab2, torch::Tensor gb, int64_t B, torch::Tensor params,
+                 torch::Tensor m,
                  torch::Tensor v, c10::optional<torch::Tensor> gdump, torch::Tensor w2r, torch::Tensor w2q,
                  std::vector<int64_t> off, torch::Tensor adam_t, int64_t t_off, double lr, double b1, double b2,
                  double eps, double wd) {
   const c10::DeviceGuard g(params.device());
   Offsets o = offsets(off);
   const int64_t n = params_end(o);
-  p2cnn::conv_adam(ptr<float>(wslab1, torch::kFloat32, B * p2cnn::kSlab1, "wslab1"),
-                   ptr<float>(wslab2, torch::kFloat32, B * p2cnn::kSlab2, "wslab2"), int(B),
+  TORCH_CHECK(B >= 1 && B <= 64, "bad batch");
+  p2cnn::conv_adam(ptr<float>(wslab1, torch::kFloat32, B * p2cnn::kDgTiles * p2cnn::kSlab1, "wslab1"),
+                   ptr<float>(wslab2, torch::kFloat32, p2cnn::wgrad_groups(int(B)) * int64_t(p2cnn::kSlab2), "wslab2"),
+                   ptr<float>(gb, torch::kFloat32, B * 3136, "gb"), int(B),
                    ptr<float>(params, torch::kFloat32, n, "params"), ptr<float>(m, torch::kFloat32, n, "m"),
                    ptr<float>(v, torch::kFloat32, n, "v"), optr<float>(gdump, torch::kFloat32, n, "gdump"),
                    reinterpret_cast<uint16_t*>(ptr<at::BFloat16>(w2r, torch::kBFloat16, 51200, "w2r")),

@@ -5,8 +5,8 @@
 //   dCh    bf16 [mrows][324][64]   dC2 as padded HWC image (18x18 pixels)
 //   gB     f32  [mrows][3136]      alive-masked dA1 (conv2 bias gradient terms)
 //   W2q    bf16 [32][25][64]       conv2 weight, (ic, tap, oc) -- transposed-conv B operand
-//   wslab1 f32  [B][832]           per-image conv1 weight/bias gradients
-//   wslab2 f32  [B][51264]         per-image conv2 weight/bias gradients
+//   wslab1 f32  [B][7][832]        conv1 weight/bias partials per (image, position tile)
+//   wslab2 f32  [ceil(B/2)][25][64][32]  conv2 weight partials per image pair, (tap, oc, ic)
 // Every reduction has a fixed order (no float atomics), so a step is bitwise
 // reproducible -- required because Adam amplifies last-bit differences in
 // near-zero gradients.  Adam's step count is (*adam_t + t_off): a device base
@@ -115,22 +115,29 @@ __global__ __launch_bounds__(512) void gemm_da1_route_kernel(const uint16_t* __r
 #pragma unroll
   for (int mt = 0; mt < MT; ++mt) acc[mt] = f32x16{};
   const uint16_t* brow = w1t + size_t(n0 + r) * K + 32 * h;
+  // all of this wave's loads are issued before the first MFMA (one HBM
+  // round-trip instead of one per k-group; the compiler would otherwise
+  // interleave them with the MFMAs and serialise the latency)
+  constexpr int NGW = NG / 8;
+  uint4 bq[NGW][4], aq[NGW][MT][4];
 #pragma unroll
-  for (int g = wave; g < NG; g += 8) {
-    const int k0 = g * 64;
-    uint4 bq[4], aq[MT][4];
+  for (int gi = 0; gi < NGW; ++gi) {
+    const int k0 = (wave + 8 * gi) * 64;
 #pragma unroll
-    for (int q = 0; q < 4; ++q) bq[q] = ld_nt16(brow + k0 + q * 8);
+    for (int q = 0; q < 4; ++q) bq[gi][q] = ld_nt16(brow + k0 + q * 8);
 #pragma unroll
     for (int mt = 0; mt < MT; ++mt)
 #pragma unroll
       for (int q = 0; q < 4; ++q)
-        aq[mt][q] = reinterpret_cast<const uint4*>(dH + size_t(mt * 32 + r) * K + 32 * h + k0)[q];
+        aq[gi][mt][q] = reinterpret_cast<const uint4*>(dH + size_t(mt * 32 + r) * K + 32 * h + k0)[q];
+  }
+  __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+  for (int gi = 0; gi < NGW; ++gi)
 #pragma unroll
     for (int q = 0; q < 4; ++q)
 #pragma unroll
-      for (int mt = 0; mt < MT; ++mt) acc[mt] = mfma32b(aq[mt][q], bq[q], acc[mt]);
-  }
+      for (int mt = 0; mt < MT; ++mt) acc[mt] = mfma32b(aq[gi][mt][q], bq[gi][q], acc[mt]);
 #pragma unroll
   for (int mt = 0; mt < MT; ++mt)
 #pragma unroll
@@ -262,269 +269,280 @@ void fc1_wgrad_adam(const uint16_t* dH, const uint16_t* a1, int mrows, float* pa
 }
 
 // ---------------------------------------------------------------------------
-// 8. conv2 weight gradient on MFMA, per image and tap group.
-//    Grid (4, B), 8 waves.  For tap t: C[oc][ic] = sum_pos dC2[oc][pos] *
-//    P1pad[ic][pos + tap]; M = 64 oc (2 tiles), N = 32 ic, K = positions laid
-//    out 14 rows x 16 (one 16-wide MFMA k-step per image row).  The image is
-//    kept as five kx-shifted channel-planar copies ([kx][ic][18 rows][16 cols]),
-//    so every B fragment (8 consecutive positions of one channel) is ONE
-//    aligned 16-B LDS read; A fragments are 16-B reads of the dC2 map.  The ic
-//    pitch (296 elements = 148 dwords) puts a b128 lane group on disjoint
-//    banks.  The conv2 bias gradient is a fixed-order wave reduction.
+// 8. conv2 weight gradient.  dW2[oc][ic][tap] = sum_{b,pos} dC2[b][oc][pos] *
+//    P1pad[b][ic][pos + tap].  Grid (25 taps, ceil(B/2)): one wave per (tap,
+//    image pair) computes the full 64 oc x 32 ic tile (two accumulators) over
+//    K = 2 images x 14 rows x 16 cols.  A fragments are 16-B rows of the dC2
+//    map (cols 14/15 are zero), B fragments 16-B rows of the kx-shifted P1
+//    copy -- both aligned, streamed from L2 with loads one half-image ahead.
+//    The tile is written as one coalesced [tap][oc][ic] slab row per pair.
 // ---------------------------------------------------------------------------
-constexpr int kWgPitch = 18 * 16 + 8;                    // 296 elements per (kx, ic) plane
-constexpr int kWgCopies = 5 * kC1 * kWgPitch * 2;        // 94720 B
-constexpr int kWgDc2 = kC2 * 224 * 2;                    // 28672 B
-constexpr int kWgHwc = 196 * kC1 * 2;                    // 12544 B staging of the HWC image
-constexpr int kWgLds = kWgCopies + kWgDc2 + kWgHwc;      // 135936 B
-
-__global__ __launch_bounds__(512) void conv2_wgrad_kernel(const uint16_t* __restrict__ dc2m,
-                                                          const float* __restrict__ gb,
-                                                          const uint16_t* __restrict__ p1,
-                                                          float* __restrict__ wslab) {
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  uint16_t* cp = reinterpret_cast<uint16_t*>(smem);
-  uint16_t* dc2 = reinterpret_cast<uint16_t*>(smem + kWgCopies);
-  uint16_t* hwc = reinterpret_cast<uint16_t*>(smem + kWgCopies + kWgDc2);
-  const int b = blockIdx.y, grp = blockIdx.x, tid = threadIdx.x;
-  for (int i = tid; i < kWgDc2 / 16; i += 512)
-    reinterpret_cast<uint4*>(dc2)[i] = reinterpret_cast<const uint4*>(dc2m + size_t(b) * kC2 * 224)[i];
-  for (int i = tid; i < kWgHwc / 16; i += 512)
-    reinterpret_cast<uint4*>(hwc)[i] = reinterpret_cast<const uint4*>(p1 + size_t(b) * 196 * kC1)[i];
-  __syncthreads();
-  // shifted planar copies: cp[kx][ic][yy][c] = P1pad[ic][yy][c + kx], P1pad = P1 zero-padded by 2
-  for (int i = tid; i < 5 * kC1 * 18 * 2; i += 512) {
-    const int half = i & 1, yy = (i >> 1) % 18, ic = (i / 36) % kC1, kx = i / (36 * kC1);
-    uint16_t v[8];
+__global__ __launch_bounds__(64) void conv2_wgrad_kernel(const uint16_t* __restrict__ dc2m,
+                                                         const uint16_t* __restrict__ p1s,
+                                                         float* __restrict__ wslab, int B) {
+  const int t = blockIdx.x, g = blockIdx.y, lane = threadIdx.x, r = lane & 31, h = lane >> 5;
+  const int ky = t / 5, kx = t % 5;
+  const int b0 = g * kWgG, nb = min(kWgG, B - b0);
+  // half-image chunks: 7 k-steps (rows) each
+  auto load = [&](int c, uint4 (&A0)[7], uint4 (&A1)[7], uint4 (&Bv)[7]) {
+    const int b = b0 + (c >> 1), row0 = (c & 1) * 7;
+    const uint16_t* a = dc2m + (size_t(b) * kC2 + r) * 224 + 8 * h;
+    const uint16_t* bb = p1s + ((size_t(b) * 5 + kx) * kC1 + r) * kP1sPlane + ky * 16 + 8 * h;
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const int y = yy - 2, x = half * 8 + j + kx - 2;
-      v[j] = (y >= 0 && y < 14 && x >= 0 && x < 14) ? hwc[(y * 14 + x) * kC1 + ic] : uint16_t(0);
+    for (int j = 0; j < 7; ++j) {
+      const int ks = row0 + j;
+      A0[j] = *reinterpret_cast<const uint4*>(a + ks * 16);
+      A1[j] = *reinterpret_cast<const uint4*>(a + 32 * 224 + ks * 16);
+      Bv[j] = *reinterpret_cast<const uint4*>(bb + ks * 16);
     }
-    *reinterpret_cast<uint4*>(cp + (kx * kC1 + ic) * kWgPitch + yy * 16 + half * 8) = pack8(v);
-  }
-  __syncthreads();
-  const int wave = tid >> 6, lane = tid & 63, r = lane & 31, h = lane >> 5;
-  if (grp == 0) {  // conv2 bias gradient: 8 waves x 8 output channels, 49 terms each
-    for (int oc = wave * 8; oc < wave * 8 + 8; ++oc) {
-      const float v = wave_sum(lane < 49 ? gb[size_t(b) * kFeat + oc * 49 + lane] : 0.f);
-      if (lane == 0) wslab[size_t(b) * kSlab2 + kC2 * kC1 * kTaps + oc] = v;
-    }
-  }
-  const int mt = wave & 1, tw = wave >> 1;
-  for (int tj = tw; tj < 7; tj += 4) {
-    const int t = grp + 4 * tj;
-    if (t >= kTaps) break;
-    const int ky = t / 5, kx = t % 5;
-    const uint16_t* brow = cp + (kx * kC1 + r) * kWgPitch + ky * 16 + 8 * h;
-    const uint16_t* arow = dc2 + (mt * 32 + r) * 224 + 8 * h;
-    f32x16 acc = {};
-#pragma unroll 7
-    for (int ks = 0; ks < 14; ++ks) {
-      const uint4 a = *reinterpret_cast<const uint4*>(arow + ks * 16);
-      const uint4 bq = *reinterpret_cast<const uint4*>(brow + ks * 16);
-      acc = mfma32b(a, bq, acc);
-    }
+  };
+  f32x16 acc0 = {}, acc1 = {};
+  uint4 xa0[7], xa1[7], xb[7], ya0[7], ya1[7], yb[7];
+  const int nch = 2 * nb;
+  load(0, xa0, xa1, xb);
 #pragma unroll
-    for (int i = 0; i < 16; ++i) {
-      const int oc = mt * 32 + acc_row_b(i, h);
-      wslab[size_t(b) * kSlab2 + (oc * kC1 + r) * kTaps + t] = acc[i];
-    }
-  }
-}
-
-void conv2_wgrad(const uint16_t* dc2m, const float* gb, const uint16_t* p1, float* wslab, int B, hipStream_t s) {
-  hipLaunchKernelGGL(conv2_wgrad_kernel, dim3(4, B), dim3(512), kWgLds, s, dc2m, gb, p1, wslab);
-}
-
-// ---------------------------------------------------------------------------
-// 9. conv2 input gradient (transposed conv on MFMA) + pool1/ReLU backward +
-//    conv1 weight gradient (second MFMA GEMM), one block per image, 7 waves.
-//    Phase 1: C[pos][ic] = sum_{tap,oc} dC2pad[pos - tap][oc] * W2[oc][ic][tap]
-//      (K = 25 x 64 = 100 k-steps; A from the padded HWC dC2 image, B from the
-//      (ic, tap, oc) weight copy; both 16-B LDS reads, conflict-free pitches).
-//    Phase 2: the dP1 tile is routed through the pool1 argmax into a dense dC1
-//      map [32 ch][28 rows][32 cols] in LDS, then
-//      dW1[c][tap] = sum_pos dC1[c][pos] * Xpad[pos + tap] runs as a 32x32
-//      MFMA GEMM over 896 positions, with five kx-shifted bf16 copies of the
-//      input image giving aligned 16-B B fragments.  Bias gradient and the
-//      cross-wave sums are fixed-order LDS reductions (no float atomics).
-// ---------------------------------------------------------------------------
-constexpr int kW2qRow = kTaps * kC2 + 8;            // 1608 elements per ic (pad breaks bank aliasing)
-constexpr int kDgW = kC1 * kW2qRow * 2;             // 102912
-constexpr int kOCP = 72;                            // dC2 pixel stride (144 B)
-constexpr int kDgDc2 = 18 * 18 * kOCP * 2;          // 46656
-constexpr int kDgLds = kDgW + kDgDc2;               // 149568
-constexpr int kDc1Pitch = 28 * 32 + 8;              // 904 elements per channel
-constexpr int kDgDc1 = kC1 * kDc1Pitch * 2;         // 57856
-constexpr int kXsPitch = 32 * 32;                   // per-kx copy [32 rows][32 cols]
-constexpr int kDgXs = 5 * kXsPitch * 2;             // 10240
-constexpr int kDgBias = 7 * kC1 * 4;                // 896
-static_assert(kDgDc1 + kDgXs + kDgBias <= kDgW, "phase-2 LDS carve exceeds the weight region");
-
-__global__ __launch_bounds__(448) void conv2_dgrad_kernel(const uint16_t* __restrict__ dchg,
-                                                          const uint8_t* __restrict__ am1,
-                                                          const uint16_t* __restrict__ w2q,
-                                                          const uint8_t* __restrict__ xds,
-                                                          const int64_t* __restrict__ idx,
-                                                          float* __restrict__ wslab1) {
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  uint16_t* sw = reinterpret_cast<uint16_t*>(smem);
-  uint16_t* dch = reinterpret_cast<uint16_t*>(smem + kDgW);
-  const int b = blockIdx.x, tid = threadIdx.x;
-  const uint4 z4 = make_uint4(0, 0, 0, 0);
-  for (int i = tid; i < kC1 * (kTaps * kC2 / 8); i += 448) {
-    const int ic = i / (kTaps * kC2 / 8), q = i % (kTaps * kC2 / 8);
-    *reinterpret_cast<uint4*>(sw + ic * kW2qRow + q * 8) =
-        reinterpret_cast<const uint4*>(w2q + size_t(ic) * kTaps * kC2)[q];
-  }
-  for (int i = tid; i < 324 * 8; i += 448) {  // padded HWC dC2 image, 64 ch per pixel (8 x 16 B)
-    const int pix = i >> 3, q = i & 7;
-    *reinterpret_cast<uint4*>(dch + pix * kOCP + q * 8) =
-        reinterpret_cast<const uint4*>(dchg + (size_t(b) * 324 + pix) * kC2)[q];
-  }
-  __syncthreads();
-
-  const int wave = tid >> 6, lane = tid & 63, r = lane & 31, h = lane >> 5;
-  const int m = wave * 32 + r;
-  const int mc = m < 196 ? m : 195;
-  const int y = mc / 14, x = mc % 14;
-  f32x16 acc = {};
-#pragma unroll 4
-  for (int s = 0; s < 100; ++s) {
-    const int t = s >> 2, ky = t / 5, kx = t % 5, oc0 = (s & 3) * 16 + 8 * h;
-    const uint4 a = *reinterpret_cast<const uint4*>(dch + ((y + 4 - ky) * 18 + (x + 4 - kx)) * kOCP + oc0);
-    const uint4 bb = *reinterpret_cast<const uint4*>(sw + r * kW2qRow + t * kC2 + oc0);
-    acc = mfma32b(a, bb, acc);
-  }
-  __syncthreads();  // weights and dC2 are dead: carve phase-2 buffers out of the weight region
-  uint16_t* dc1 = reinterpret_cast<uint16_t*>(smem);
-  uint16_t* xs = reinterpret_cast<uint16_t*>(smem + kDgDc1);
-  float* bsum_w = reinterpret_cast<float*>(smem + kDgDc1 + kDgXs);  // [7 waves][32 ch]
-  for (int i = tid; i < kDgDc1 / 16; i += 448) reinterpret_cast<uint4*>(dc1)[i] = z4;
-  const int64_t row = idx ? idx[b] : b;
-  const uint8_t* src = xds + row * (kImg * kImg);
-  for (int i = tid; i < 5 * 32 * 4; i += 448) {  // xs[kx][yy][c] = Xpad[yy][c + kx], 8 columns per item
-    const int q = i & 3, yy = (i >> 2) & 31, kx = i >> 7;
-    uint16_t v[8];
+  for (int c = 0; c < 2 * kWgG; c += 2) {
+    if (c < nch) {
+      if (c + 1 < nch) load(c + 1, ya0, ya1, yb);
+      __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const int sy = yy - 2, sx = q * 8 + j + kx - 2;
-      v[j] = (sy >= 0 && sy < kImg && sx >= 0 && sx < kImg) ? f32_to_bf16(float(src[sy * kImg + sx]) * (1.f / 255.f))
-                                                           : uint16_t(0);
+      for (int j = 0; j < 7; ++j) {
+        acc0 = mfma32b(xa0[j], xb[j], acc0);
+        acc1 = mfma32b(xa1[j], xb[j], acc1);
+      }
+      __builtin_amdgcn_sched_barrier(0);
     }
-    *reinterpret_cast<uint4*>(xs + kx * kXsPitch + yy * 32 + q * 8) = pack8(v);
+    if (c + 1 < nch) {
+      if (c + 2 < nch) load(c + 2, xa0, xa1, xb);
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int j = 0; j < 7; ++j) {
+        acc0 = mfma32b(ya0[j], yb[j], acc0);
+        acc1 = mfma32b(ya1[j], yb[j], acc1);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    }
   }
-  __syncthreads();
-  float bsum = 0.f;
+  float* out = wslab + (size_t(g) * kTaps + t) * kC2 * kC1 + r;
 #pragma unroll
   for (int i = 0; i < 16; ++i) {
-    const int pos = wave * 32 + acc_row_b(i, h);
+    const int oc = acc_row_b(i, h);
+    out[oc * kC1] = acc0[i];
+    out[(oc + 32) * kC1] = acc1[i];
+  }
+}
+
+void conv2_wgrad(const uint16_t* dc2m, const uint16_t* p1s, float* wslab2, int B, hipStream_t s) {
+  hipLaunchKernelGGL(conv2_wgrad_kernel, dim3(kTaps, wgrad_groups(B)), dim3(64), 0, s, dc2m, p1s, wslab2, B);
+}
+
+// ---------------------------------------------------------------------------
+// 9. conv2 input gradient + pool1/ReLU backward + conv1 weight gradient.
+//    Grid (7, B): one wave per (32-position tile, image).
+//    Phase 1 (MFMA): C[pos][ic] = sum_{tap,oc} dC2pad[pos - tap][oc] W2[oc][ic][tap],
+//      K = 25 taps x 64 oc = 100 k-steps; A = 16-B pixel rows of the padded HWC
+//      dC2 image, B = 16-B rows of the (ic, tap, oc) weight copy, streamed from
+//      L2 one 10-step chunk ahead.
+//    Phase 2 (sparse, fp32): pooling routes dP1[pos][ic] to ONE conv1 pixel (its
+//      argmax) or nowhere (ReLU-dead), so dW1[ic][tap] += dP1 * Xpad[pixel + tap]
+//      is a 25-term gather from the input image in LDS -- no dense dC1 map, no
+//      second GEMM.  Each lane owns one channel and 16 positions; the half-waves
+//      are combined with one shuffle and the tile's partial goes to its slab row.
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(64) void conv2_dgrad_kernel(const uint16_t* __restrict__ dch,
+                                                         const uint8_t* __restrict__ am1,
+                                                         const uint16_t* __restrict__ w2q,
+                                                         const uint8_t* __restrict__ xds,
+                                                         const int64_t* __restrict__ idx,
+                                                         float* __restrict__ wslab1) {
+  __shared__ float xs[32][33];  // zero-padded input image, /255 applied
+  const int tile = blockIdx.x, b = blockIdx.y, lane = threadIdx.x, r = lane & 31, h = lane >> 5;
+  const int m = tile * 32 + r, mc = m < 196 ? m : 195;
+  const int y = mc / 14, x = mc % 14;
+  const uint16_t* abase = dch + size_t(b) * 324 * kC2 + 8 * h;
+  const uint16_t* bbase = w2q + size_t(r) * kTaps * kC2 + 8 * h;
+  auto load = [&](int c, uint4 (&A)[10], uint4 (&Bv)[10]) {
+#pragma unroll
+    for (int j = 0; j < 10; ++j) {
+      const int s = c * 10 + j, t = s >> 2, ky = t / 5, kx = t % 5, oc0 = (s & 3) * 16;
+      A[j] = *reinterpret_cast<const uint4*>(abase + ((y + 4 - ky) * 18 + (x + 4 - kx)) * kC2 + oc0);
+      Bv[j] = *reinterpret_cast<const uint4*>(bbase + t * kC2 + oc0);
+    }
+  };
+  uint4 A0[10], B0[10], A1[10], B1[10];
+  f32x16 acc = {};
+  load(0, A0, B0);
+  {
+    const int64_t row = idx ? idx[b] : b;
+    const uint8_t* src = xds + row * (kImg * kImg);
+    for (int i = lane; i < 32 * 32; i += 64) {
+      const int yy = i >> 5, xx = i & 31, sy = yy - 2, sx = xx - 2;
+      float v = 0.f;
+      if (sy >= 0 && sy < kImg && sx >= 0 && sx < kImg) v = float(src[sy * kImg + sx]) * (1.f / 255.f);
+      xs[yy][xx] = v;
+    }
+  }
+#pragma unroll
+  for (int c = 0; c < 10; c += 2) {
+    load(c + 1, A1, B1);
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int j = 0; j < 10; ++j) acc = mfma32b(A0[j], B0[j], acc);
+    __builtin_amdgcn_sched_barrier(0);
+    if (c + 2 < 10) load(c + 2, A0, B0);
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int j = 0; j < 10; ++j) acc = mfma32b(A1[j], B1[j], acc);
+    __builtin_amdgcn_sched_barrier(0);
+  }
+  __syncthreads();
+  float wg[kTaps];
+#pragma unroll
+  for (int t = 0; t < kTaps; ++t) wg[t] = 0.f;
+  float bs = 0.f;
+#pragma unroll
+  for (int i = 0; i < 16; ++i) {
+    const int pos = tile * 32 + acc_row_b(i, h);
     if (pos < 196) {
       const uint8_t a = am1[(size_t(b) * 196 + pos) * kC1 + r];
       if (a < 4) {
         const int yy = 2 * (pos / 14) + (a >> 1), xx = 2 * (pos % 14) + (a & 1);
-        dc1[r * kDc1Pitch + yy * 32 + xx] = f32_to_bf16(acc[i]);
-        bsum += acc[i];
+        const float gv = acc[i];
+        bs += gv;
+#pragma unroll
+        for (int ky = 0; ky < 5; ++ky)
+#pragma unroll
+          for (int kx = 0; kx < 5; ++kx) wg[ky * 5 + kx] = fmaf(gv, xs[yy + ky][xx + kx], wg[ky * 5 + kx]);
       }
     }
   }
-  bsum += __shfl_xor(bsum, 32, 64);
-  if (h == 0) bsum_w[wave * kC1 + r] = bsum;
-  __syncthreads();
-  // conv1 weight gradient: C[c][tap] over K = 28 rows x 32 cols of positions
-  // (56 k-steps); waves split K, partial tiles reduced in fixed order.
-  f32x16 wacc = {};
-  const int t = r < kTaps ? r : kTaps - 1;  // lanes 25..31 compute a duplicate column, discarded
-  const int ky = t / 5, kx = t % 5;
-  for (int ks = wave; ks < 56; ks += 7) {
-    const int yy = ks >> 1, x0 = (ks & 1) * 16 + 8 * h;
-    const uint4 a = *reinterpret_cast<const uint4*>(dc1 + r * kDc1Pitch + yy * 32 + x0);
-    const uint4 bq = *reinterpret_cast<const uint4*>(xs + kx * kXsPitch + (yy + ky) * 32 + x0);
-    wacc = mfma32b(a, bq, wacc);
-  }
-  float* red = reinterpret_cast<float*>(smem + kDgW);  // [7 waves][16 regs][64 lanes] f32 = 28672 B
 #pragma unroll
-  for (int i = 0; i < 16; ++i) red[(wave * 16 + i) * 64 + lane] = wacc[i];
-  __syncthreads();
-  for (int e = tid; e < 16 * 64; e += 448) {
-    float sum = 0.f;
+  for (int t = 0; t < kTaps; ++t) wg[t] += __shfl_xor(wg[t], 32, 64);
+  bs += __shfl_xor(bs, 32, 64);
+  if (h == 0) {
+    float* o = wslab1 + (size_t(b) * kDgTiles + tile) * kSlab1;
 #pragma unroll
-    for (int w = 0; w < 7; ++w) sum += red[w * 1024 + e];
-    const int i = e >> 6, ln = e & 63;
-    const int c = acc_row_b(i, ln >> 5), tt = ln & 31;
-    if (tt < kTaps) wslab1[size_t(b) * kSlab1 + c * kTaps + tt] = sum;
-  }
-  if (tid < kC1) {
-    float sb = 0.f;
-#pragma unroll
-    for (int w = 0; w < 7; ++w) sb += bsum_w[w * kC1 + tid];
-    wslab1[size_t(b) * kSlab1 + kC1 * kTaps + tid] = sb;
+    for (int t = 0; t < kTaps; ++t) o[r * kTaps + t] = wg[t];
+    o[kC1 * kTaps + r] = bs;
   }
 }
 
 void conv2_dgrad_conv1_wgrad(const uint16_t* dch, const uint8_t* am1, const uint16_t* w2q, const uint8_t* x,
                              const int64_t* idx, float* wslab1, int B, hipStream_t s) {
-  hipLaunchKernelGGL(conv2_dgrad_kernel, dim3(B), dim3(448), kDgLds, s, dch, am1, w2q, x, idx, wslab1);
+  hipLaunchKernelGGL(conv2_dgrad_kernel, dim3(kDgTiles, B), dim3(64), 0, s, dch, am1, w2q, x, idx, wslab1);
 }
 
 // ---------------------------------------------------------------------------
-// 10. Conv parameters: reduce the per-image gradient slabs, Adam, and repack
-//     the conv2 bf16 shadows (W2r for the forward, W2q for the transposed conv).
+// 10. Conv parameters: fixed-order reduction of the gradient partials, Adam,
+//     and the conv2 bf16 shadows (W2r for the forward, W2q for the dgrad).
+//     Blocks 0..63: one conv2 output channel each -- its 800 weights are
+//     summed over the image-pair slabs ([tap][oc][ic] rows, coalesced),
+//     transposed through LDS into parameter order, and its bias gradient is
+//     the block sum of the alive-masked dA1 terms (gB).  Blocks 64..115: 16
+//     conv1 parameters each, the 7B tile partials split 16 ways.  Every load
+//     loop is batched so a thread keeps 8-16 independent loads in flight.
 // ---------------------------------------------------------------------------
+constexpr int kC1Blocks = kSlab1 / 16;  // 52
+
 __global__ __launch_bounds__(256) void conv_adam_kernel(const float* __restrict__ ws1, const float* __restrict__ ws2,
-                                                        int B, float* __restrict__ p, float* __restrict__ m,
-                                                        float* __restrict__ v, float* __restrict__ gdump,
-                                                        uint16_t* __restrict__ w2r, uint16_t* __restrict__ w2q,
-                                                        Offsets off, const int* __restrict__ adam_t, int t_off,
-                                                        AdamCfg cfg, int64_t end) {
-  const int64_t e = int64_t(blockIdx.x) * 256 + threadIdx.x;
-  if (e >= end) return;
-  const float* slab;
-  int stride, j;
-  bool is_c2w = false;
-  if (e >= off.c1w && e < off.c1w + kC1 * kTaps) {
-    slab = ws1; stride = kSlab1; j = int(e - off.c1w);
-  } else if (e >= off.c1b && e < off.c1b + kC1) {
-    slab = ws1; stride = kSlab1; j = kC1 * kTaps + int(e - off.c1b);
-  } else if (e >= off.c2w && e < off.c2w + kC2 * kC1 * kTaps) {
-    slab = ws2; stride = kSlab2; j = int(e - off.c2w); is_c2w = true;
-  } else if (e >= off.c2b && e < off.c2b + kC2) {
-    slab = ws2; stride = kSlab2; j = kC2 * kC1 * kTaps + int(e - off.c2b);
+                                                        const float* __restrict__ gb, int B, float* __restrict__ p,
+                                                        float* __restrict__ m, float* __restrict__ v,
+                                                        float* __restrict__ gdump, uint16_t* __restrict__ w2r,
+                                                        uint16_t* __restrict__ w2q, Offsets off,
+                                                        const int* __restrict__ adam_t, int t_off, AdamCfg cfg) {
+  __shared__ float g2[kTaps][kC1 + 1];
+  __shared__ float red[256];
+  const int tid = threadIdx.x;
+  const AdamScal sc = adam_scal(cfg, adam_t, t_off);
+  if (blockIdx.x < kC2) {
+    const int oc = blockIdx.x, ng = wgrad_groups(B);
+    float acc[4] = {0.f, 0.f, 0.f, 0.f};
+    for (int g0 = 0; g0 < ng; g0 += 8) {
+      float t[4][8];
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          const int j = tid + 256 * u, t_ = j >> 5, ic = j & 31, gg = g0 + k;
+          t[u][k] = (j < kTaps * kC1 && gg < ng) ? ws2[((size_t(gg) * kTaps + t_) * kC2 + oc) * kC1 + ic] : 0.f;
+        }
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+#pragma unroll
+        for (int k = 0; k < 8; ++k) acc[u] += t[u][k];
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int j = tid + 256 * u;
+      if (j < kTaps * kC1) g2[j >> 5][j & 31] = acc[u];
+    }
+    float bs = 0.f;
+    for (int e0 = 0; e0 < B * 49; e0 += 256 * 4) {
+      float t[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int e = e0 + tid + 256 * u;
+        t[u] = e < B * 49 ? gb[size_t(e / 49) * kFeat + oc * 49 + e % 49] : 0.f;
+      }
+      bs += (t[0] + t[1]) + (t[2] + t[3]);
+    }
+    red[tid] = bs;
+    __syncthreads();
+    for (int w = 128; w > 0; w >>= 1) {
+      if (tid < w) red[tid] += red[tid + w];
+      __syncthreads();
+    }
+    for (int j = tid; j < kC1 * kTaps; j += 256) {
+      const int ic = j / kTaps, t = j % kTaps;
+      const float g = g2[t][ic];
+      const int64_t e = off.c2w + int64_t(oc) * kC1 * kTaps + j;
+      if (gdump) gdump[e] = g;
+      const uint16_t hb = f32_to_bf16(adam_apply(p, m, v, e, g, cfg, sc));
+      w2r[(oc * kTaps + t) * kC1 + ic] = hb;
+      w2q[(ic * kTaps + t) * kC2 + oc] = hb;
+    }
+    if (tid == 0) {
+      if (gdump) gdump[off.c2b + oc] = red[0];
+      adam_apply(p, m, v, off.c2b + oc, red[0], cfg, sc);
+    }
   } else {
-    return;  // arena padding
-  }
-  float g = 0.f;
-#pragma unroll 8
-  for (int b = 0; b < B; ++b) g += slab[size_t(b) * stride + j];
-  if (gdump) gdump[e] = g;
-  const AdamScal s = adam_scal(cfg, adam_t, t_off);
-  const float pn = adam_apply(p, m, v, e, g, cfg, s);
-  if (is_c2w) {
-    const int oc = j / (kC1 * kTaps), rem = j % (kC1 * kTaps), ic = rem / kTaps, t = rem % kTaps;
-    const uint16_t hb = f32_to_bf16(pn);
-    w2r[(oc * kTaps + t) * kC1 + ic] = hb;
-    w2q[(ic * kTaps + t) * kC2 + oc] = hb;
+    const int j = (blockIdx.x - kC2) * 16 + (tid & 15), q = tid >> 4;  // 16 row splits
+    const int rows = B * kDgTiles;
+    float s = 0.f;
+    for (int r0 = q; r0 < rows; r0 += 16 * 8) {
+      float t[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const int rw = r0 + 16 * u;
+        t[u] = rw < rows ? ws1[size_t(rw) * kSlab1 + j] : 0.f;
+      }
+#pragma unroll
+      for (int u = 0; u < 8; ++u) s += t[u];
+    }
+    red[tid] = s;
+    __syncthreads();
+    if (q == 0) {
+      float g = 0.f;
+#pragma unroll
+      for (int k = 0; k < 16; ++k) g += red[k * 16 + tid];
+      const int64_t e = j < kC1 * kTaps ? off.c1w + j : off.c1b + (j - kC1 * kTaps);
+      if (gdump) gdump[e] = g;
+      adam_apply(p, m, v, e, g, cfg, sc);
+    }
   }
 }
 
-void conv_adam(const float* wslab1, const float* wslab2, int B, float* params, float* m, float* v, float* gdump,
-               uint16_t* w2r, uint16_t* w2q, Offsets off, const int* adam_t, int t_off, AdamCfg cfg, hipStream_t s) {
-  const int64_t end = off.c2b + kC2;
-  hipLaunchKernelGGL(conv_adam_kernel, dim3(int((end + 255) / 256)), dim3(256), 0, s, wslab1, wslab2, B, params, m, v,
-                     gdump, w2r, w2q, off, adam_t, t_off, cfg, end);
+void conv_adam(const float* wslab1, const float* wslab2, const float* gb, int B, float* params, float* m, float* v,
+               float* gdump, uint16_t* w2r, uint16_t* w2q, Offsets off, const int* adam_t, int t_off, AdamCfg cfg,
+               hipStream_t s) {
+  hipLaunchKernelGGL(conv_adam_kernel, dim3(kC2 + kC1Blocks), dim3(256), 0, s, wslab1, wslab2, gb, B, params, m, v,
+                     gdump, w2r, w2q, off, adam_t, t_off, cfg);
 }
 
 void init_fwd_attributes();
 
 // Raise the dynamic-LDS limit of the kernels that stage > 64 KB.  Called once
 // (from the bindings) before any HIP-graph capture.
-void init_attributes() {
-  init_fwd_attributes();
-  P2_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(conv2_wgrad_kernel),
-                               hipFuncAttributeMaxDynamicSharedMemorySize, kWgLds));
-  P2_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(conv2_dgrad_kernel),
-                               hipFuncAttributeMaxDynamicSharedMemorySize, kDgLds));
-}
+void init_attributes() { init_fwd_attributes(); }
 
 }  // namespace p2cnn

@@ -4,6 +4,9 @@
 //   x    uint8  [N][28*28]           dataset, gathered by idx[b] (the /255 is folded in)
 //   P1   bf16   [B][196][32]         pooled conv1 output, HWC (channels contiguous)
 //   AM1  uint8  [B][196][32]         pool1 argmax (dy*2+dx) or 4 = dead (ReLU zero)
+//   P1s  bf16   [B][5][32][18][16]   kx-shifted planar copies of zero-padded P1 (training
+//                                    only): P1s[b][kx][ic][yy][c] = P1pad[ic][yy][c + kx],
+//                                    the conv2-wgrad B operand as aligned 16-B rows
 //   A1   bf16   [mrows][3136]        pooled conv2 output, PyTorch flatten order c*49+y*7+x
 //   AM2  uint8  [B][3136]            pool2 argmax / dead
 //   W2r  bf16   [64][25][32]         conv2 weight, (oc, tap, ic)   -- conv2_fwd B operand
@@ -27,16 +30,23 @@ P2_DEVICE f32x16 mfma32(uint4 a, uint4 b, f32x16 c) {
 P2_DEVICE int acc_row(int i, int h) { return (i & 3) + 8 * (i >> 2) + 4 * h; }
 
 // ---------------------------------------------------------------------------
-// 2. conv1 (1->32, 5x5, pad 2) + bias + ReLU + maxpool 2x2.  Grid (4, B):
-//    part p of image b handles pooled positions [49p, 49p+49).  oc = tid & 31
-//    is fixed per thread, so its 25 taps live in registers; the 6x6 input window
-//    of a pooled output is read once from LDS (broadcast to the 32 oc lanes).
+// 2. conv1 (1->32, 5x5, pad 2) + bias + ReLU + maxpool 2x2.  Grid (7, B):
+//    block q of image b produces pooled rows 2q and 2q+1 (28 positions x 32
+//    oc).  oc = tid & 31 is fixed per thread, so its 25 taps live in
+//    registers; the 6x6 input window of a pooled output is read from LDS
+//    (broadcast to the 32 oc lanes).  Results are staged in LDS and written
+//    as whole 16-B chunks: P1 (HWC), AM1, and -- when training -- the two
+//    rows of all five kx-shifted planar copies (P1s) this block owns,
+//    including their zero padding columns.
 // ---------------------------------------------------------------------------
 __global__ __launch_bounds__(256) void conv1_fwd_kernel(const uint8_t* __restrict__ x, const int64_t* __restrict__ idx,
                                                         const float* __restrict__ w1, const float* __restrict__ b1,
-                                                        uint16_t* __restrict__ p1, uint8_t* __restrict__ am1) {
+                                                        uint16_t* __restrict__ p1, uint8_t* __restrict__ am1,
+                                                        uint16_t* __restrict__ p1s) {
   __shared__ float img[32][33];
-  const int b = blockIdx.y, part = blockIdx.x, tid = threadIdx.x;
+  __shared__ uint16_t sv[kC1][2][16];  // pooled values [oc][row][px], cols 14/15 zero
+  __shared__ __attribute__((aligned(16))) uint8_t sa[28][kC1];  // argmax codes [pos][oc]
+  const int b = blockIdx.y, q = blockIdx.x, tid = threadIdx.x;
   const int64_t row = idx ? idx[b] : b;
   const uint8_t* src = x + row * (kImg * kImg);
   for (int i = tid; i < 32 * 32; i += 256) {
@@ -50,9 +60,10 @@ __global__ __launch_bounds__(256) void conv1_fwd_kernel(const uint8_t* __restric
 #pragma unroll
   for (int t = 0; t < kTaps; ++t) w[t] = w1[oc * kTaps + t];
   const float bias = b1[oc];
+  if (tid < kC1 * 2 * 2) sv[tid >> 2][(tid >> 1) & 1][14 + (tid & 1)] = 0;
   __syncthreads();
-  for (int q = tid >> 5; q < 49; q += 8) {
-    const int pp = part * 49 + q, py = pp / 14, px = pp % 14;
+  for (int k = tid >> 5; k < 28; k += 8) {
+    const int rr = k / 14, px = k % 14, py = 2 * q + rr;
     float win[6][6];
 #pragma unroll
     for (int i = 0; i < 6; ++i)
@@ -73,101 +84,136 @@ __global__ __launch_bounds__(256) void conv1_fwd_kernel(const uint8_t* __restric
         arg = d;
       }
     }
-    const size_t o = (size_t(b) * 196 + pp) * kC1 + oc;
-    p1[o] = f32_to_bf16(fmaxf(best, 0.f));
-    am1[o] = best > 0.f ? uint8_t(arg) : uint8_t(4);
+    sv[oc][rr][px] = f32_to_bf16(fmaxf(best, 0.f));
+    sa[k][oc] = best > 0.f ? uint8_t(arg) : uint8_t(4);
+  }
+  __syncthreads();
+  const size_t pix0 = size_t(b) * 196 + q * 28;
+  // P1 (HWC): 28 pixels x 4 chunks of 8 channels;  AM1: 28 pixels x 2 chunks of 16
+  if (tid < 28 * 4) {
+    const int k = tid >> 2, c0 = (tid & 3) * 8;
+    uint16_t u[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) u[j] = sv[c0 + j][k / 14][k % 14];
+    uint4 o;
+    o.x = uint32_t(u[0]) | (uint32_t(u[1]) << 16);
+    o.y = uint32_t(u[2]) | (uint32_t(u[3]) << 16);
+    o.z = uint32_t(u[4]) | (uint32_t(u[5]) << 16);
+    o.w = uint32_t(u[6]) | (uint32_t(u[7]) << 16);
+    reinterpret_cast<uint4*>(p1 + (pix0 + k) * kC1)[tid & 3] = o;
+  } else if (tid < 28 * 4 + 28 * 2) {
+    const int i = tid - 28 * 4, k = i >> 1, c0 = (i & 1) * 16;
+    reinterpret_cast<uint4*>(am1 + (pix0 + k) * kC1)[i & 1] = *reinterpret_cast<const uint4*>(&sa[k][c0]);
+  }
+  if (p1s) {
+    // P1s[b][kx][oc][2q + rr + 2][c] = P1[oc][2q + rr][c + kx - 2]  (0 outside)
+    for (int i = tid; i < 5 * kC1 * 2 * 2; i += 256) {
+      const int half = i & 1, rr = (i >> 1) & 1, o = (i >> 2) % kC1, kx = i / (4 * kC1);
+      uint16_t u[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int xs = half * 8 + j + kx - 2;
+        u[j] = (xs >= 0 && xs < 14) ? sv[o][rr][xs] : uint16_t(0);
+      }
+      uint4 v;
+      v.x = uint32_t(u[0]) | (uint32_t(u[1]) << 16);
+      v.y = uint32_t(u[2]) | (uint32_t(u[3]) << 16);
+      v.z = uint32_t(u[4]) | (uint32_t(u[5]) << 16);
+      v.w = uint32_t(u[6]) | (uint32_t(u[7]) << 16);
+      *reinterpret_cast<uint4*>(p1s + ((size_t(b) * 5 + kx) * kC1 + o) * kP1sPlane + (2 * q + rr + 2) * 16 + half * 8) = v;
+    }
   }
 }
 
 void conv1_fwd(const uint8_t* x, const int64_t* idx, const float* params, Offsets off, uint16_t* p1, uint8_t* am1,
-               int B, hipStream_t s) {
-  hipLaunchKernelGGL(conv1_fwd_kernel, dim3(4, B), dim3(256), 0, s, x, idx, params + off.c1w, params + off.c1b, p1,
-                     am1);
+               uint16_t* p1s, int B, hipStream_t s) {
+  hipLaunchKernelGGL(conv1_fwd_kernel, dim3(7, B), dim3(256), 0, s, x, idx, params + off.c1w, params + off.c1b, p1,
+                     am1, p1s);
 }
 
 // ---------------------------------------------------------------------------
 // 3. conv2 (32->64, 5x5, pad 2) as implicit GEMM on MFMA + bias/ReLU/maxpool.
-//    Grid (2, B): block = (oc half, image).  GEMM M = 196 positions (7 wave
-//    tiles of 32), N = 32 oc, K = 25 taps x 32 ic with ic fastest, so every
-//    A/B fragment is ONE 16-byte LDS read (ds_read_b128) from the HWC image /
-//    the (oc, tap, ic) weight copy.  Pixel stride 40 channels (80 B) spreads
-//    the 16-lane b128 groups over all 64 banks.
+//    Grid (7, 2, B): one wave per (pooled row, oc half, image) -- 448 waves,
+//    so the whole chip is busy.  GEMM M = the 28 conv positions of two conv
+//    rows (= one pooled row; lanes 28..31 duplicate a valid row and are
+//    discarded), N = 32 oc, K = 25 taps x 32 ic with ic fastest: every A
+//    fragment is one 16-B load of an HWC pixel (zero outside the image), every
+//    B fragment one 16-B load of the (oc, tap, ic) weight copy, both straight
+//    from L2/L1 -- no LDS staging.  Loads run one 5-tap chunk ahead of the
+//    MFMAs (explicit double buffer; sched barriers stop the compiler from
+//    serialising them).  The 2x2 pool is an exchange through 4 KB of LDS.
 // ---------------------------------------------------------------------------
-constexpr int kICP = 40;                                  // padded channels per pixel / weight row
-constexpr int kImgLds = 18 * 18 * kICP * 2;               // 25920 B
-constexpr int kW2Lds = 32 * kTaps * kICP * 2;             // 64000 B
-constexpr int kConv2Lds = kImgLds + kW2Lds;
-
-__global__ __launch_bounds__(448) void conv2_fwd_kernel(const uint16_t* __restrict__ p1,
-                                                        const uint16_t* __restrict__ w2r,
-                                                        const float* __restrict__ b2, uint16_t* __restrict__ a1,
-                                                        uint8_t* __restrict__ am2) {
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  uint16_t* simg = reinterpret_cast<uint16_t*>(smem);
-  uint16_t* sw = reinterpret_cast<uint16_t*>(smem + kImgLds);
-  const int b = blockIdx.y, nh = blockIdx.x, tid = threadIdx.x;
-  const uint4 zero4 = make_uint4(0, 0, 0, 0);
-  for (int i = tid; i < kImgLds / 16; i += 448) reinterpret_cast<uint4*>(simg)[i] = zero4;
-  __syncthreads();
-  for (int i = tid; i < 196 * 4; i += 448) {
-    const int pix = i >> 2, q = i & 3, y = pix / 14, xx = pix % 14;
-    const uint4 v = reinterpret_cast<const uint4*>(p1 + (size_t(b) * 196 + pix) * kC1)[q];
-    *reinterpret_cast<uint4*>(simg + ((y + 2) * 18 + (xx + 2)) * kICP + q * 8) = v;
-  }
-  for (int i = tid; i < 32 * kTaps * 4; i += 448) {
-    const int rr = i >> 2, q = i & 3;  // rr = oc_local * 25 + tap
-    const uint4 v = reinterpret_cast<const uint4*>(w2r + (size_t(nh * 32) * kTaps + rr) * kC1)[q];
-    *reinterpret_cast<uint4*>(sw + rr * kICP + q * 8) = v;
-  }
-  __syncthreads();
-
-  const int wave = tid >> 6, lane = tid & 63, r = lane & 31, h = lane >> 5;
-  const int m = wave * 32 + r;
-  const int mm = m < 196 ? m : 195;
-  const int y = mm / 14, xx = mm % 14;
+__global__ __launch_bounds__(64) void conv2_fwd_kernel(const uint16_t* __restrict__ p1,
+                                                       const uint16_t* __restrict__ w2r,
+                                                       const float* __restrict__ b2, uint16_t* __restrict__ a1,
+                                                       uint8_t* __restrict__ am2) {
+  __shared__ float sout[32][33];
+  const int py = blockIdx.x, nh = blockIdx.y, b = blockIdx.z;
+  const int lane = threadIdx.x, r = lane & 31, h = lane >> 5;
+  const int rr = r < 28 ? r : 27;
+  const int y = 2 * py + (rr >= 14 ? 1 : 0), x = rr >= 14 ? rr - 14 : rr;
+  const uint16_t* img = p1 + size_t(b) * 196 * kC1 + 8 * h;
+  const uint16_t* wrow = w2r + size_t(nh * 32 + r) * kTaps * kC1 + 8 * h;
+  const uint4 z4 = make_uint4(0, 0, 0, 0);
+  auto load = [&](int c, uint4 (&A)[10], uint4 (&Bv)[10]) {
+#pragma unroll
+    for (int j = 0; j < 10; ++j) {
+      const int s = c * 10 + j, t = s >> 1, ky = t / 5, kx = t % 5, ic = (s & 1) * 16;
+      const int iy = y + ky - 2, ix = x + kx - 2;
+      const bool ok = iy >= 0 && iy < 14 && ix >= 0 && ix < 14;
+      const int pix = ok ? iy * 14 + ix : 0;
+      const uint4 v = *reinterpret_cast<const uint4*>(img + pix * kC1 + ic);
+      A[j] = ok ? v : z4;
+      Bv[j] = *reinterpret_cast<const uint4*>(wrow + t * kC1 + ic);
+    }
+  };
+  uint4 A0[10], B0[10], A1[10], B1[10];
   f32x16 acc = {};
-#pragma unroll 10
-  for (int s = 0; s < 50; ++s) {
-    const int t = s >> 1, ky = t / 5, kx = t % 5, ic0 = (s & 1) * 16 + 8 * h;
-    const uint4 av = *reinterpret_cast<const uint4*>(simg + ((y + ky) * 18 + (xx + kx)) * kICP + ic0);
-    const uint4 bv = *reinterpret_cast<const uint4*>(sw + (r * kTaps + t) * kICP + ic0);
-    acc = mfma32(av, bv, acc);
+  load(0, A0, B0);
+#pragma unroll
+  for (int c = 0; c < 5; c += 2) {
+    if (c + 1 < 5) load(c + 1, A1, B1);
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int j = 0; j < 10; ++j) acc = mfma32(A0[j], B0[j], acc);
+    __builtin_amdgcn_sched_barrier(0);
+    if (c + 1 < 5) {
+      if (c + 2 < 5) load(c + 2, A0, B0);
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int j = 0; j < 10; ++j) acc = mfma32(A1[j], B1[j], acc);
+      __builtin_amdgcn_sched_barrier(0);
+    }
   }
-  __syncthreads();  // image no longer needed: reuse LDS for the conv output
-  float* sout = reinterpret_cast<float*>(smem);  // [196][32] f32 = 25088 B
-  const float bias = b2[nh * 32 + r];
 #pragma unroll
   for (int i = 0; i < 16; ++i) {
-    const int row = wave * 32 + acc_row(i, h);
-    if (row < 196) sout[row * 32 + r] = fmaxf(acc[i] + bias, 0.f);
+    const int row = acc_row(i, h);
+    if (row < 28) sout[row][r] = acc[i];
   }
   __syncthreads();
-  for (int i = tid; i < 49 * 32; i += 448) {
-    const int oc = i / 49, pp = i % 49, py = pp / 7, px = pp % 7;
-    float best = -1.f;
+  for (int e = lane; e < 7 * 32; e += 64) {
+    const int oc = e / 7, px = e % 7;
+    const float v[4] = {sout[2 * px][oc], sout[2 * px + 1][oc], sout[14 + 2 * px][oc], sout[15 + 2 * px][oc]};
+    float best = v[0];
     int arg = 0;
 #pragma unroll
-    for (int d = 0; d < 4; ++d) {
-      const float v = sout[((2 * py + (d >> 1)) * 14 + 2 * px + (d & 1)) * 32 + oc];
-      if (v > best) {
-        best = v;
+    for (int d = 1; d < 4; ++d)
+      if (v[d] > best) {
+        best = v[d];
         arg = d;
       }
-    }
-    const int feat = (nh * 32 + oc) * 49 + pp;
-    a1[size_t(b) * kFeat + feat] = f32_to_bf16(best);
-    am2[size_t(b) * kFeat + feat] = best > 0.f ? uint8_t(arg) : uint8_t(4);
+    best += b2[nh * 32 + oc];
+    const size_t o = size_t(b) * kFeat + (nh * 32 + oc) * 49 + py * 7 + px;
+    a1[o] = f32_to_bf16(fmaxf(best, 0.f));
+    am2[o] = best > 0.f ? uint8_t(arg) : uint8_t(4);
   }
 }
 
-void init_fwd_attributes() {
-  P2_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(conv2_fwd_kernel),
-                               hipFuncAttributeMaxDynamicSharedMemorySize, kConv2Lds));
-}
+void init_fwd_attributes() {}
 
 void conv2_fwd(const uint16_t* p1, const uint16_t* w2r, const float* params, Offsets off, uint16_t* a1,
                uint8_t* am2, int B, hipStream_t s) {
-  hipLaunchKernelGGL(conv2_fwd_kernel, dim3(2, B), dim3(448), kConv2Lds, s, p1, w2r, params + off.c2b, a1, am2);
+  hipLaunchKernelGGL(conv2_fwd_kernel, dim3(7, 2, B), dim3(64), 0, s, p1, w2r, params + off.c2b, a1, am2);
 }
 
 // ---------------------------------------------------------------------------

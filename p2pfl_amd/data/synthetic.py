@@ -3,8 +3,10 @@
 There is no network on the build or GPU boxes, so the reference's torchvision
 MNIST download (``mnistfederated_dm.py:85-101``) is replaced by deterministic
 synthetic data of the same shapes.  Each class has a smooth random prototype
-image; a sample is its class prototype under a random contrast, a small random
-translation and additive noise, stored as ``uint8`` like MNIST.  Models reach
+stroke-like image (zero background); a sample is its class prototype under a
+weaker distractor prototype of another class, a random contrast,
+multiplicative stroke noise, a faint background and a per-sample random
+translation, stored as ``uint8`` like MNIST.  Models reach
 high accuracy on it, so convergence tests are meaningful, and the same seed
 gives bit-identical data on every peer.
 
@@ -42,18 +44,20 @@ class ImageSet:
 
 
 def _prototypes(shape: Tuple[int, int, int], classes: int, g: torch.Generator) -> torch.Tensor:
+    """Sparse, stroke-like class prototypes in [0, 1] (background exactly 0, like MNIST)."""
     c, h, w = shape
     low = torch.rand(classes, c, max(2, h // 4), max(2, w // 4), generator=g)
     protos = torch.nn.functional.interpolate(low, size=(h, w), mode="bilinear", align_corners=False)
-    protos = (protos - protos.amin(dim=(1, 2, 3), keepdim=True)) / (
-        protos.amax(dim=(1, 2, 3), keepdim=True) - protos.amin(dim=(1, 2, 3), keepdim=True) + 1e-6
-    )
-    return protos
+    flat = protos.reshape(classes, -1)
+    lo = torch.quantile(flat, 0.70, dim=1).view(classes, 1, 1, 1)
+    hi = flat.amax(dim=1).view(classes, 1, 1, 1)
+    return ((protos - lo) / (hi - lo + 1e-6)).clamp(min=0.0)
 
 
 def make_split(
     shape: Tuple[int, int, int], classes: int, n: int, seed: int, protos: torch.Tensor, chunk: int = 8192
 ) -> ImageSet:
+    """Samples = prototype x random contrast + stroke noise, translated by a per-sample random shift."""
     g = torch.Generator().manual_seed(seed)
     c, h, w = shape
     y = torch.randint(0, classes, (n,), generator=g)
@@ -61,12 +65,19 @@ def make_split(
     for s in range(0, n, chunk):
         e = min(n, s + chunk)
         yy = y[s:e]
-        img = protos[yy]
-        contrast = 0.6 + 0.4 * torch.rand(e - s, 1, 1, 1, generator=g)
-        img = img * contrast + 0.25 * torch.rand(img.shape, generator=g)
-        dx, dy = torch.randint(-2, 3, (2,), generator=g).tolist()
-        img = torch.roll(img, shifts=(dy, dx), dims=(2, 3))
-        x[s:e] = (img.clamp(0, 1.25) / 1.25 * 255).to(torch.uint8)
+        # the true class prototype plus a weaker distractor of another class
+        other = (yy + torch.randint(1, classes, (e - s,), generator=g)) % classes
+        mix = 0.75 * torch.rand(e - s, 1, 1, 1, generator=g)
+        img = protos[yy] + mix * protos[other]
+        contrast = 0.5 + 0.5 * torch.rand(e - s, 1, 1, 1, generator=g)
+        img = img * contrast * (0.5 + torch.rand(img.shape, generator=g))
+        img = img + 0.1 * torch.rand(img.shape, generator=g)
+        shifts = torch.randint(-2, 3, (e - s, 2), generator=g)
+        code = (shifts[:, 0] + 2) * 5 + (shifts[:, 1] + 2)
+        for k in torch.unique(code).tolist():
+            sel = code == k
+            img[sel] = torch.roll(img[sel], shifts=(k // 5 - 2, k % 5 - 2), dims=(2, 3))
+        x[s:e] = (img.clamp(0, 1) * 255).to(torch.uint8)
     return ImageSet(x, y)
 
 

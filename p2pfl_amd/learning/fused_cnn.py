@@ -72,13 +72,15 @@ class FusedCNNEngine:
         # activations / workspaces (sized for mrows samples)
         M = mrows
         self.p1, self.am1 = z(M * 196 * 32, dt=bf), z(M * 196 * 32, dt=torch.uint8)
+        # kx-shifted planar P1 copies for conv2_wgrad; padding cells stay zero
+        self.p1s = z(M * 5 * 32 * 18 * 16, dt=bf)
         self.a1, self.am2 = z(M * FEAT, dt=bf), z(M * FEAT, dt=torch.uint8)
         self.slabs1 = z(self.S1 * M * HID)
         self.H, self.dH = z(M * HID, dt=bf), z(M * HID, dt=bf)
         self.dlogits = z(M * 10)
         # dC2 maps written by gemm_da1_route (padding stays zero from here on)
         self.dc2m, self.dch, self.gb = z(M * 64 * 224, dt=bf), z(M * 324 * 64, dt=bf), z(M * FEAT)
-        self.wslab1, self.wslab2 = z(M * 832), z(M * 51264)
+        self.wslab1, self.wslab2 = z(M * 7 * 832), z(((M + 1) // 2) * 51200)
         self.stats = z(2)
         self.gdump: Optional[torch.Tensor] = None
         self.pack_shadows()
@@ -103,7 +105,7 @@ class FusedCNNEngine:
 
     def forward(self, x: torch.Tensor, labels: torch.Tensor, idx: Optional[torch.Tensor], B: int, stats: torch.Tensor, train: bool) -> None:
         C, M = self.C, self.mrows
-        C.conv1_fwd(x, idx, self.params, self.off, self.p1, self.am1, B)
+        C.conv1_fwd(x, idx, self.params, self.off, self.p1, self.am1, self.p1s if train else None, B)
         C.conv2_fwd(self.p1, self.w2r, self.params, self.off, self.a1, self.am2, B, M)
         C.gemm_skinny(self.a1, self.w1bf, self.slabs1, M, HID, FEAT, self.S1)
         C.head(self.slabs1, self.S1, M, self.params, self.off, labels, idx, B, train, self.H, self.dH, self.dlogits, stats)
@@ -123,9 +125,9 @@ class FusedCNNEngine:
         C.fc2_wgrad_adam(self.dlogits, self.H, B, self.params, self.m, self.v, self.gdump, self.off, self.adam_t, t_off, *a)
         C.gemm_da1_route(self.dH, self.w1tbf, self.am2, M, B, self.dc2m, self.dch, self.gb)
         C.fc1_wgrad_adam(self.dH, self.a1, M, self.params, self.m, self.v, self.gdump, self.w1bf, self.w1tbf, self.off, self.adam_t, t_off, *a)
-        C.conv2_wgrad(self.dc2m, self.gb, self.p1, self.wslab2, B)
+        C.conv2_wgrad(self.dc2m, self.p1s, self.wslab2, B)
         C.conv2_dgrad_conv1_wgrad(self.dch, self.am1, self.w2q, x, idx, self.wslab1, B)
-        C.conv_adam(self.wslab1, self.wslab2, B, self.params, self.m, self.v, self.gdump, self.w2r, self.w2q, self.off, self.adam_t, t_off, *a)
+        C.conv_adam(self.wslab1, self.wslab2, self.gb, B, self.params, self.m, self.v, self.gdump, self.w2r, self.w2q, self.off, self.adam_t, t_off, *a)
 
     def train_step(self, x: torch.Tensor, y: torch.Tensor) -> float:
         """Convenience: one eager step on a uint8 batch ``x`` [B,1,28,28] with labels ``y``; returns the loss."""

@@ -44,10 +44,10 @@ def _close(got, want, rtol=1e-2, atol=1e-3):
     return frac
 
 
-def _forward(eng, x):
+def _forward(eng, x, train=False):
     stats = torch.zeros(4, device="cuda")
     y = torch.zeros(B, dtype=torch.int64, device="cuda")
-    eng.forward(x.reshape(-1, 784), y, None, B, stats, False)
+    eng.forward(x.reshape(-1, 784), y, None, B, stats, train)
     torch.cuda.synchronize()
 
 
@@ -89,6 +89,16 @@ def test_conv1_fwd(eng):
     picked = conv.reshape(B, 32, 784).gather(2, flat).view(B, 32, 14, 14)
     torch.testing.assert_close(picked[alive], ref[alive], atol=1e-5, rtol=1e-5)
     assert bool(((am == 4) == (ref <= 0)).all())
+
+
+def test_conv1_shifted_planar_copies(eng):
+    x = _x(8)
+    _forward(eng, x, train=True)
+    p1 = eng.p1.view(B, 14, 14, 32).permute(0, 3, 1, 2)  # [B,32,14,14]
+    pad = F.pad(p1.float(), (2, 6, 2, 2))  # [B,32,18,22]: P1pad plus room for the kx shift
+    want = torch.stack([pad[..., kx : kx + 16] for kx in range(5)], 1)  # [B,5,32,18,16]
+    got = eng.p1s.view(-1, 5, 32, 18, 16)[:B].float()
+    assert torch.equal(got, want)
 
 
 def test_conv2_fwd(eng):
@@ -211,22 +221,22 @@ def test_gemm_da1_route(eng):
 
 def test_conv2_wgrad(eng):
     x = _x(3)
-    _forward(eng, x)
+    _forward(eng, x, train=True)
     _route(eng, 11)
-    eng.C.conv2_wgrad(eng.dc2m, eng.gb, eng.p1, eng.wslab2, B)
+    eng.C.conv2_wgrad(eng.dc2m, eng.p1s, eng.wslab2, B)
     torch.cuda.synchronize()
     dc2 = eng.dc2m.view(-1, 64, 14, 16)[:B, :, :, :14].float()
     p1 = eng.p1.view(B, 14, 14, 32).permute(0, 3, 1, 2).float()
     want_w = torch.nn.grad.conv2d_weight(p1, (64, 32, 5, 5), dc2, padding=2)
-    ws = eng.wslab2.view(-1, 51264)[:B].sum(0)
-    torch.testing.assert_close(ws[:51200].view(64, 32, 5, 5), want_w, atol=1e-6, rtol=2e-3)
-    want_b = eng.gb.view(-1, 64, 49)[:B].sum((0, 2))
-    torch.testing.assert_close(ws[51200:], want_b, atol=1e-6, rtol=1e-4)
+    ng = (B + 1) // 2
+    ws = eng.wslab2[: ng * 51200].view(ng, 25, 64, 32).sum(0)  # [tap][oc][ic]
+    got = ws.permute(1, 2, 0).reshape(64, 32, 5, 5)
+    torch.testing.assert_close(got, want_w, atol=1e-6, rtol=2e-3)
 
 
 def test_conv2_dgrad_conv1_wgrad(eng):
     x = _x(4)
-    _forward(eng, x)
+    _forward(eng, x, train=True)
     _route(eng, 12)
     eng.C.conv2_dgrad_conv1_wgrad(eng.dch, eng.am1, eng.w2q, x.reshape(-1, 784), None, eng.wslab1, B)
     torch.cuda.synchronize()
@@ -235,25 +245,33 @@ def test_conv2_dgrad_conv1_wgrad(eng):
     dp1 = torch.nn.grad.conv2d_input((B, 32, 14, 14), w2, dc2, padding=2)
     am1 = eng.am1.view(B, 14, 14, 32).permute(0, 3, 1, 2)
     dc1 = _decode_pool(dp1, am1, 28)
-    # the kernel feeds bf16 operands to the conv1-wgrad MFMA
-    want_w = torch.nn.grad.conv2d_weight(_bf(x.float() / 255.0), (32, 1, 5, 5), _bf(dc1), padding=2)
-    ws = eng.wslab1.view(-1, 832)[:B].sum(0)
-    torch.testing.assert_close(ws[:800].view(32, 1, 5, 5), want_w, atol=1e-6, rtol=5e-3)
+    want_w = torch.nn.grad.conv2d_weight(x.float() / 255.0, (32, 1, 5, 5), dc1, padding=2)
+    ws = eng.wslab1[: B * 7 * 832].view(B * 7, 832).sum(0)
+    torch.testing.assert_close(ws[:800].view(32, 1, 5, 5), want_w, atol=1e-6, rtol=2e-3)
     torch.testing.assert_close(ws[800:], dc1.sum((0, 2, 3)), atol=1e-6, rtol=1e-3)
 
 
 def test_conv_adam_and_shadows(eng):
     g = torch.Generator(device="cuda").manual_seed(13)
-    ws1 = torch.randn(32 * 832, device="cuda", generator=g) * 1e-3
-    ws2 = torch.randn(32 * 51264, device="cuda", generator=g) * 1e-3
+    ng = (B + 1) // 2
+    ws1 = torch.randn(B * 7 * 832, device="cuda", generator=g) * 1e-3
+    ws2 = torch.randn(ng * 51200, device="cuda", generator=g) * 1e-3
+    gb = torch.randn(B * 3136, device="cuda", generator=g) * 1e-3
     before, m0, v0 = eng.params.clone(), eng.m.clone(), eng.v.clone()
     eng.gdump = torch.zeros_like(eng.params)
     eng.adam_t.fill_(1)
-    eng.C.conv_adam(ws1, ws2, B, eng.params, eng.m, eng.v, eng.gdump, eng.w2r, eng.w2q, eng.off, eng.adam_t, 0, *eng._adam())
+    eng.C.conv_adam(ws1, ws2, gb, B, eng.params, eng.m, eng.v, eng.gdump, eng.w2r, eng.w2q, eng.off, eng.adam_t, 0, *eng._adam())
     torch.cuda.synchronize()
     o = eng.off
-    torch.testing.assert_close(eng.gdump[o[0] : o[0] + 800], ws1.view(32, 832)[:, :800].sum(0), atol=1e-7, rtol=1e-5)
-    torch.testing.assert_close(eng.gdump[o[3] : o[3] + 64], ws2.view(32, 51264)[:, 51200:].sum(0), atol=1e-7, rtol=1e-5)
+    s1 = ws1.view(B * 7, 832).sum(0)
+    torch.testing.assert_close(eng.gdump[o[0] : o[0] + 800], s1[:800], atol=1e-7, rtol=1e-5)
+    torch.testing.assert_close(eng.gdump[o[1] : o[1] + 32], s1[800:], atol=1e-7, rtol=1e-5)
+    w2g = ws2.view(ng, 25, 64, 32).sum(0).permute(1, 2, 0).reshape(-1)
+    torch.testing.assert_close(eng.gdump[o[2] : o[2] + 51200], w2g, atol=1e-7, rtol=1e-5)
+    torch.testing.assert_close(eng.gdump[o[3] : o[3] + 64], gb.view(B, 64, 49).sum((0, 2)), atol=1e-6, rtol=1e-4)
+    p_ref, m_ref, v_ref = before[o[2] : o[2] + 51200].clone(), m0[o[2] : o[2] + 51200].clone(), v0[o[2] : o[2] + 51200].clone()
+    ops.adam_step_reference(p_ref, w2g, m_ref, v_ref, eng.lr, eng.betas[0], eng.betas[1], eng.eps, eng.wd, 1)
+    torch.testing.assert_close(eng.params[o[2] : o[2] + 51200], p_ref, atol=1e-6, rtol=1e-5)
     W = eng.params[o[2] : o[2] + 51200].view(64, 32, 25)
     assert torch.equal(eng.w2r.view(64, 25, 32), W.permute(0, 2, 1).to(torch.bfloat16))
     assert torch.equal(eng.w2q.view(32, 25, 64), W.permute(1, 2, 0).to(torch.bfloat16))
