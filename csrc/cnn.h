@@ -3,7 +3,7 @@
 // Model (reference p2pfl/learning/pytorch/mnist_examples/models/cnn.py:55-98):
 //   conv5x5(1->32,"same") -> ReLU -> maxpool2 -> conv5x5(32->64,"same") -> ReLU
 //   -> maxpool2 -> flatten(3136) -> FC 3136->2048 -> ReLU -> FC 2048->10 -> CE
-// trained with Adam.  One training step is 10 kernels (cnn_*.hip):
+// trained with Adam.  One training step is 8 kernel launches (cnn_*.hip):
 //
 //  1 conv1_fwd         direct 5x5 conv + bias + ReLU + maxpool, input gathered
 //                      by index from the uint8 dataset (/255 folded in) -> P1 (HWC bf16) + argmax
@@ -13,18 +13,19 @@
 //  3 gemm_skinny       FC1: [B x 3136] x [3136 x 2048], split-K fp32 slabs
 //  4 head              slab reduce + bias + ReLU -> H; FC2; softmax-xent; dlogits;
 //                      dH = relu'(H) * dlogits W2; loss/accuracy stats
-//  5 fc2_wgrad_adam    dW2 = dlogits^T H and db2, Adam applied in place
-//  6 gemm_da1_route    dA1 = dH x W1 (W1^T bf16 shadow) + pool2/ReLU backward in
-//                      the epilogue -> dC2 maps (two layouts) + fp32 bias terms
-//  7 fc1_wgrad_adam    dW1 = dH^T A1 on MFMA with Adam fused into the epilogue:
+//  5 route_fc2         dA1 = dH x W1 (W1^T bf16 shadow) + pool2/ReLU backward in
+//                      the epilogue -> dC2 map + fp32 bias terms;  extra blocks:
+//                      dW2 = dlogits^T H and db2 with Adam applied in place
+//  6 fc1_wgrad_adam    dW1 = dH^T A1 on MFMA with Adam fused into the epilogue:
 //                      the 6.4 M-element gradient never touches memory; writes
 //                      W1 (fp32), m, v and both bf16 shadows (W1, W1^T)
-//  8 conv2_wgrad       one wave per (tap, image pair): dW2[:, :, tap] = dC2 x
-//                      shifted P1 on MFMA, operands streamed from L2 -> slab per pair
-//  9 conv2_dgrad_c1    one wave per (image, 32-position tile): dP1 = transposed
-//                      conv on MFMA, then the conv1 weight gradient as a sparse
-//                      fp32 gather at each pool1 argmax pixel -> slab per tile
-// 10 conv_adam         fixed-order slab reduction (+ conv2 bias from gB) + Adam
+//  7 conv2_bwd         single-wave blocks, two roles:
+//                      dgrad (image, 32-position tile): dP1 = transposed conv on
+//                      MFMA from an LDS HWC window of dC2, then the conv1 weight
+//                      gradient as a sparse fp32 gather at each pool1 argmax pixel;
+//                      wgrad (tap, image pair): dW2[:, :, tap] = dC2 x shifted P1
+//                      on MFMA, operands streamed from L2 -> slab per pair
+//  8 conv_adam         fixed-order slab reduction (+ conv2 bias from gB) + Adam
 //                      for the conv params + packed bf16 conv2 shadows (two layouts)
 #pragma once
 #include <hip/hip_runtime.h>
@@ -66,25 +67,24 @@ void head(const float* slabs, int S, int mrows, const float* params, Offsets off
           const int64_t* idx, int B, int train, uint16_t* H, uint16_t* dH, float* dlogits, float* stats,
           hipStream_t s);
 
-void fc2_wgrad_adam(const float* dlogits, const uint16_t* H, int B, float* params, float* m, float* v,
-                    float* gdump, Offsets off, const int* adam_t, int t_off, AdamCfg cfg, hipStream_t s);
-
 void fc1_wgrad_adam(const uint16_t* dH, const uint16_t* a1, int mrows, float* params, float* m, float* v,
                     float* gdump, uint16_t* w1bf, uint16_t* w1tbf, Offsets off, const int* adam_t, int t_off,
                     AdamCfg cfg, hipStream_t s);
 
-// dA1 = dH x W1 (reads the W1^T shadow) with the pool2/ReLU backward fused into
-// the epilogue: writes dC2 as a [B][64][14x16] map (wgrad A operand), as a
-// padded HWC [B][18x18][64] image (dgrad A operand), and the fp32 alive-masked
-// dA1 [B][3136] (bias gradient).  Every 2x2 window writes all 4 positions, so
-// no per-step clearing is needed (padding is zero from allocation).
-void gemm_da1_route(const uint16_t* dH, const uint16_t* w1t, const uint8_t* am2, int mrows, int B, uint16_t* dc2m,
-                    uint16_t* dch, float* gb, hipStream_t s);
+// One launch: dA1 = dH x W1 (reads the W1^T shadow) with the pool2/ReLU
+// backward fused into the epilogue -> dC2 map [B][64][14x16] (all 4 window
+// positions written, so no clearing; cols 14/15 stay zero from allocation) and
+// the fp32 alive-masked dA1 [B][3136] (conv2 bias terms); plus, in extra
+// blocks, the FC2 weight/bias gradient with Adam.
+void route_fc2(const uint16_t* dH, const uint16_t* w1t, const uint8_t* am2, int mrows, int B, uint16_t* dc2m,
+               float* gb, const float* dlogits, const uint16_t* H, float* params, float* m, float* v, float* gdump,
+               Offsets off, const int* adam_t, int t_off, AdamCfg cfg, hipStream_t s);
 
-void conv2_wgrad(const uint16_t* dc2m, const uint16_t* p1s, float* wslab2, int B, hipStream_t s);
-
-void conv2_dgrad_conv1_wgrad(const uint16_t* dch, const uint8_t* am1, const uint16_t* w2q, const uint8_t* x,
-                             const int64_t* idx, float* wslab1, int B, hipStream_t s);
+// One launch: conv2 input gradient + pool1/ReLU backward + conv1 weight
+// gradient (-> wslab1 [B][7][832]) and conv2 weight gradient
+// (-> wslab2 [ceil(B/2)][25][64][32]).
+void conv2_bwd(const uint16_t* dc2m, const uint16_t* p1s, const uint8_t* am1, const uint16_t* w2q, const uint8_t* x,
+               const int64_t* idx, float* wslab1, float* wslab2, int B, hipStream_t s);
 
 void conv_adam(const float* wslab1, const float* wslab2, const float* gb, int B, float* params, float* m, float* v,
                float* gdump, uint16_t* w2r, uint16_t* w2q, Offsets off, const int* adam_t, int t_off, AdamCfg cfg,

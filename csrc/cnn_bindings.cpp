@@ -111,19 +111,6 @@ AdamCfg cfg(double lr, double b1, double b2, double eps, double wd) {
   return AdamCfg{float(lr), float(b1), float(b2), float(eps), float(wd)};
 }
 
-void k_fc2_wgrad_adam(torch::Tensor dlogits, torch::Tensor H, int64_t B, torch::Tensor params, torch::Tensor m,
-                      torch::Tensor v, c10::optional<torch::Tensor> gdump, std::vector<int64_t> off,
-                      torch::Tensor adam_t, int64_t t_off, double lr, double b1, double b2, double eps, double wd) {
-  const c10::DeviceGuard g(params.device());
-  Offsets o = offsets(off);
-  const int64_t n = params_end(o);
-  p2cnn::fc2_wgrad_adam(ptr<float>(dlogits, torch::kFloat32, B * 10, "dlogits"),
-                        reinterpret_cast<uint16_t*>(ptr<at::BFloat16>(H, torch::kBFloat16, B * 2048, "H")), int(B),
-                        ptr<float>(params, torch::kFloat32, n, "params"), ptr<float>(m, torch::kFloat32, n, "m"),
-                        ptr<float>(v, torch::kFloat32, n, "v"), optr<float>(gdump, torch::kFloat32, n, "gdump"), o,
-                        ptr<int>(adam_t, torch::kInt32, 1, "adam_t", 4), int(t_off), cfg(lr, b1, b2, eps, wd), stream());
-}
-
 void k_fc1_wgrad_adam(torch::Tensor dH, torch::Tensor a1, int64_t mrows, torch::Tensor params, torch::Tensor m,
                       torch::Tensor v, c10::optional<torch::Tensor> gdump, torch::Tensor w1bf, torch::Tensor w1tbf,
                       std::vector<int64_t> off, torch::Tensor adam_t, int64_t t_off, double lr, double b1, double b2,
@@ -142,38 +129,40 @@ void k_fc1_wgrad_adam(torch::Tensor dH, torch::Tensor a1, int64_t mrows, torch::
                         o, ptr<int>(adam_t, torch::kInt32, 1, "adam_t", 4), int(t_off), cfg(lr, b1, b2, eps, wd), stream());
 }
 
-void k_gemm_da1_route(torch::Tensor dH, torch::Tensor w1tbf, torch::Tensor am2, int64_t mrows, int64_t B,
-                      torch::Tensor dc2m, torch::Tensor dch, torch::Tensor gb) {
+void k_route_fc2(torch::Tensor dH, torch::Tensor w1tbf, torch::Tensor am2, int64_t mrows, int64_t B,
+                 torch::Tensor dc2m, torch::Tensor gb, torch::Tensor dlogits, torch::Tensor H, torch::Tensor params,
+                 torch::Tensor m, torch::Tensor v, c10::optional<torch::Tensor> gdump, std::vector<int64_t> off,
+                 torch::Tensor adam_t, int64_t t_off, double lr, double b1, double b2, double eps, double wd) {
   const c10::DeviceGuard g(dH.device());
   check_batch(int(B), int(mrows));
-  p2cnn::gemm_da1_route(reinterpret_cast<uint16_t*>(ptr<at::BFloat16>(dH, torch::kBFloat16, mrows * 2048, "dH")),
-                        reinterpret_cast<uint16_t*>(ptr<at::BFloat16>(w1tbf, torch::kBFloat16, 2048 * 3136, "w1tbf")),
-                        ptr<uint8_t>(am2, torch::kUInt8, B * 3136, "am2"), int(mrows), int(B),
-                        reinterpret_cast<uint16_t*>(ptr<at::BFloat16>(dc2m, torch::kBFloat16, B * 64 * 224, "dc2m")),
-                        reinterpret_cast<uint16_t*>(ptr<at::BFloat16>(dch, torch::kBFloat16, B * 324 * 64, "dch")),
-                        ptr<float>(gb, torch::kFloat32, B * 3136, "gb"), stream());
+  Offsets o = offsets(off);
+  const int64_t n = params_end(o);
+  p2cnn::route_fc2(reinterpret_cast<uint16_t*>(ptr<at::BFloat16>(dH, torch::kBFloat16, mrows * 2048, "dH")),
+                   reinterpret_cast<uint16_t*>(ptr<at::BFloat16>(w1tbf, torch::kBFloat16, 2048 * 3136, "w1tbf")),
+                   ptr<uint8_t>(am2, torch::kUInt8, B * 3136, "am2"), int(mrows), int(B),
+                   reinterpret_cast<uint16_t*>(ptr<at::BFloat16>(dc2m, torch::kBFloat16, B * 64 * 224, "dc2m")),
+                   ptr<float>(gb, torch::kFloat32, B * 3136, "gb"),
+                   ptr<float>(dlogits, torch::kFloat32, B * 10, "dlogits"),
+                   reinterpret_cast<uint16_t*>(ptr<at::BFloat16>(H, torch::kBFloat16, B * 2048, "H")),
+                   ptr<float>(params, torch::kFloat32, n, "params"), ptr<float>(m, torch::kFloat32, n, "m"),
+                   ptr<float>(v, torch::kFloat32, n, "v"), optr<float>(gdump, torch::kFloat32, n, "gdump"), o,
+                   ptr<int>(adam_t, torch::kInt32, 1, "adam_t", 4), int(t_off), cfg(lr, b1, b2, eps, wd), stream());
 }
 
-void k_conv2_wgrad(torch::Tensor dc2m, torch::Tensor p1s, torch::Tensor wslab2, int64_t B) {
+void k_conv2_bwd(torch::Tensor dc2m, torch::Tensor p1s, torch::Tensor am1, torch::Tensor w2q, torch::Tensor x,
+                 c10::optional<torch::Tensor> idx, torch::Tensor wslab1, torch::Tensor wslab2, int64_t B) {
   const c10::DeviceGuard g(dc2m.device());
   TORCH_CHECK(B >= 1 && B <= 64, "bad batch");
-  p2cnn::conv2_wgrad(reinterpret_cast<uint16_t*>(ptr<at::BFloat16>(dc2m, torch::kBFloat16, B * 64 * 224, "dc2m")),
-                     reinterpret_cast<uint16_t*>(ptr<at::BFloat16>(p1s, torch::kBFloat16, B * p2cnn::kP1s, "p1s")),
-                     ptr<float>(wslab2, torch::kFloat32, p2cnn::wgrad_groups(int(B)) * int64_t(p2cnn::kSlab2), "wslab2"),
-                     int(B), stream());
-}
-
-void k_conv2_dgrad(torch::Tensor dch, torch::Tensor am1, torch::Tensor w2q, torch::Tensor x,
-                   c10::optional<torch::Tensor> idx, torch::Tensor wslab1, int64_t B) {
-  const c10::DeviceGuard g(w2q.device());
-  TORCH_CHECK(B >= 1 && B <= 64, "bad batch");
+  TORCH_CHECK(x.numel() % 784 == 0, "x must be [N,1,28,28] uint8");
   if (!idx.has_value()) TORCH_CHECK(x.numel() / 784 >= B, "x has fewer than B rows");
-  p2cnn::conv2_dgrad_conv1_wgrad(
-      reinterpret_cast<uint16_t*>(ptr<at::BFloat16>(dch, torch::kBFloat16, B * 324 * 64, "dch")),
-      ptr<uint8_t>(am1, torch::kUInt8, B * 196 * 32, "am1"),
-      reinterpret_cast<uint16_t*>(ptr<at::BFloat16>(w2q, torch::kBFloat16, 51200, "w2q")),
-      ptr<uint8_t>(x, torch::kUInt8, 784, "x", 1), idx_ptr(idx, B),
-      ptr<float>(wslab1, torch::kFloat32, B * p2cnn::kDgTiles * p2cnn::kSlab1, "wslab1"), int(B), stream());
+  p2cnn::conv2_bwd(reinterpret_cast<uint16_t*>(ptr<at::BFloat16>(dc2m, torch::kBFloat16, B * 64 * 224, "dc2m")),
+                   reinterpret_cast<uint16_t*>(ptr<at::BFloat16>(p1s, torch::kBFloat16, B * p2cnn::kP1s, "p1s")),
+                   ptr<uint8_t>(am1, torch::kUInt8, B * 196 * 32, "am1"),
+                   reinterpret_cast<uint16_t*>(ptr<at::BFloat16>(w2q, torch::kBFloat16, 51200, "w2q")),
+                   ptr<uint8_t>(x, torch::kUInt8, 784, "x", 1), idx_ptr(idx, B),
+                   ptr<float>(wslab1, torch::kFloat32, B * p2cnn::kDgTiles * p2cnn::kSlab1, "wslab1"),
+                   ptr<float>(wslab2, torch::kFloat32, p2cnn::wgrad_groups(int(B)) * int64_t(p2cnn::kSlab2), "wslab2"),
+                   int(B), stream());
 }
 
 void k_conv_adam(torch::Tensor wslab1, torch::Tensor wslab2, torch::Tensor gb, int64_t B, torch::Tensor params,
@@ -220,11 +209,9 @@ void register_cnn(pybind11::module& m) {
   c.def("conv2_fwd", &k_conv2_fwd);
   c.def("gemm_skinny", &k_gemm_skinny);
   c.def("head", &k_head);
-  c.def("fc2_wgrad_adam", &k_fc2_wgrad_adam);
+  c.def("route_fc2", &k_route_fc2);
   c.def("fc1_wgrad_adam", &k_fc1_wgrad_adam);
-  c.def("gemm_da1_route", &k_gemm_da1_route);
-  c.def("conv2_wgrad", &k_conv2_wgrad);
-  c.def("conv2_dgrad_conv1_wgrad", &k_conv2_dgrad);
+  c.def("conv2_bwd", &k_conv2_bwd);
   c.def("conv_adam", &k_conv_adam);
   c.def("pack_shadows", &k_pack_shadows);
 }

@@ -1,8 +1,7 @@
 // Fused MNIST-CNN training step -- backward kernels with fused Adam epilogues.
 // Layouts: see cnn_fwd.hip.  Backward buffers:
 //   dH     bf16 [mrows][2048]      dLoss/dH (ReLU mask applied), rows >= B are zero
-//   dC2m   bf16 [mrows][64][224]   dC2 map, positions laid out 14 rows x 16 cols
-//   dCh    bf16 [mrows][324][64]   dC2 as padded HWC image (18x18 pixels)
+//   dC2m   bf16 [mrows][64][224]   dC2 map, positions laid out 14 rows x 16 cols (cols 14/15 zero)
 //   gB     f32  [mrows][3136]      alive-masked dA1 (conv2 bias gradient terms)
 //   W2q    bf16 [32][25][64]       conv2 weight, (ic, tap, oc) -- transposed-conv B operand
 //   wslab1 f32  [B][7][832]        conv1 weight/bias partials per (image, position tile)
@@ -57,24 +56,42 @@ P2_DEVICE float adam_apply(float* __restrict__ p, float* __restrict__ m, float* 
 }
 
 // ---------------------------------------------------------------------------
-// 5. FC2 weight/bias gradient + Adam: dW2[c][k] = sum_b dlogits[b][c] H[b][k].
-//    20,490 parameters, one thread each, Adam applied in place.
+// 5+6. One launch, two independent block roles (both only need the head's
+//    outputs, so sharing a launch saves a kernel boundary):
+//  * blocks [0, 98): dA1 = dH x W1 on MFMA with the pool2/ReLU backward fused
+//    into the epilogue.  32 features per block, 8 waves splitting K = 2048 in
+//    64-wide groups (same streaming scheme and k permutation as gemm_skinny),
+//    all of a wave's loads issued before its first MFMA, partial tiles reduced
+//    in LDS in fixed wave order.  Each output (b, feature) is routed to the
+//    argmax of its 2x2 pooling window; all four window positions of the dC2
+//    map are written (so it never needs clearing), plus the fp32 alive-masked
+//    dA1 (conv2 bias terms).  The block's 32 features are contiguous, so its
+//    dC2 rows are shared with at most one neighbour block.
+//  * blocks [98, 139): FC2 weight/bias gradient + Adam, one thread per
+//    parameter: dW2[c][k] = sum_b dlogits[b][c] H[b][k].
 // ---------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void fc2_wgrad_adam_kernel(const float* __restrict__ dlogits,
-                                                             const uint16_t* __restrict__ H, int B,
-                                                             float* __restrict__ p, float* __restrict__ m,
-                                                             float* __restrict__ v, float* __restrict__ gdump,
-                                                             Offsets off, const int* __restrict__ adam_t, int t_off,
-                                                             AdamCfg cfg) {
-  const int e = blockIdx.x * 256 + threadIdx.x;
+constexpr int kRouteBlocks = kFeat / 32;                       // 98
+constexpr int kFc2Blocks = (kCls * kHid + kCls + 511) / 512;   // 41
+
+P2_DEVICE void fc2_role(int blk, const float* __restrict__ dlogits, const uint16_t* __restrict__ H, int B,
+                        float* __restrict__ p, float* __restrict__ m, float* __restrict__ v,
+                        float* __restrict__ gdump, const Offsets& off, const int* __restrict__ adam_t, int t_off,
+                        const AdamCfg& cfg) {
+  const int e = blk * 512 + threadIdx.x;
   const int nW = kCls * kHid;
   if (e >= nW + kCls) return;
   float g = 0.f;
   int64_t pi;
   if (e < nW) {
     const int c = e / kHid, k = e % kHid;
-#pragma unroll 8
-    for (int b = 0; b < B; ++b) g = fmaf(dlogits[b * kCls + c], bf16_to_f32(H[size_t(b) * kHid + k]), g);
+    for (int b0 = 0; b0 < B; b0 += 8) {
+      float t[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u)
+        t[u] = b0 + u < B ? dlogits[(b0 + u) * kCls + c] * bf16_to_f32(H[size_t(b0 + u) * kHid + k]) : 0.f;
+#pragma unroll
+      for (int u = 0; u < 8; ++u) g += t[u];
+    }
     pi = off.l2w + e;
   } else {
     const int c = e - nW;
@@ -86,27 +103,20 @@ __global__ __launch_bounds__(256) void fc2_wgrad_adam_kernel(const float* __rest
   adam_apply(p, m, v, pi, g, cfg, s);
 }
 
-void fc2_wgrad_adam(const float* dlogits, const uint16_t* H, int B, float* params, float* m, float* v, float* gdump,
-                    Offsets off, const int* adam_t, int t_off, AdamCfg cfg, hipStream_t s) {
-  const int n = kCls * kHid + kCls;
-  hipLaunchKernelGGL(fc2_wgrad_adam_kernel, dim3((n + 255) / 256), dim3(256), 0, s, dlogits, H, B, params, m, v,
-                     gdump, off, adam_t, t_off, cfg);
-}
-
-// ---------------------------------------------------------------------------
-// 6. dA1 = dH x W1 on MFMA, pool2/ReLU backward fused into the epilogue.
-//    Grid 98 (32 features each), 8 waves splitting K = 2048 in 64-wide groups
-//    (same streaming scheme and k permutation as gemm_skinny), reduced in LDS
-//    in fixed wave order.  Each output (b, feature) is routed to the argmax of
-//    its 2x2 pooling window and all four window positions are written, in
-//    both dC2 layouts.
-// ---------------------------------------------------------------------------
 template <int MT>
-__global__ __launch_bounds__(512) void gemm_da1_route_kernel(const uint16_t* __restrict__ dH,
-                                                             const uint16_t* __restrict__ w1t,
-                                                             const uint8_t* __restrict__ am2, int B,
-                                                             uint16_t* __restrict__ dc2m, uint16_t* __restrict__ dch,
-                                                             float* __restrict__ gb) {
+__global__ __launch_bounds__(512) void route_fc2_kernel(const uint16_t* __restrict__ dH,
+                                                        const uint16_t* __restrict__ w1t,
+                                                        const uint8_t* __restrict__ am2, int B,
+                                                        uint16_t* __restrict__ dc2m, float* __restrict__ gb,
+                                                        const float* __restrict__ dlogits,
+                                                        const uint16_t* __restrict__ H, float* __restrict__ p,
+                                                        float* __restrict__ m, float* __restrict__ v,
+                                                        float* __restrict__ gdump, Offsets off,
+                                                        const int* __restrict__ adam_t, int t_off, AdamCfg cfg) {
+  if (blockIdx.x >= kRouteBlocks) {
+    fc2_role(blockIdx.x - kRouteBlocks, dlogits, H, B, p, m, v, gdump, off, adam_t, t_off, cfg);
+    return;
+  }
   __shared__ float red[8 * MT * 1024];
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, r = lane & 31, h = lane >> 5;
   const int n0 = blockIdx.x * 32;
@@ -115,9 +125,8 @@ __global__ __launch_bounds__(512) void gemm_da1_route_kernel(const uint16_t* __r
 #pragma unroll
   for (int mt = 0; mt < MT; ++mt) acc[mt] = f32x16{};
   const uint16_t* brow = w1t + size_t(n0 + r) * K + 32 * h;
-  // all of this wave's loads are issued before the first MFMA (one HBM
-  // round-trip instead of one per k-group; the compiler would otherwise
-  // interleave them with the MFMAs and serialise the latency)
+  // all of this wave's loads are issued before the first MFMA (one memory
+  // round-trip instead of one per k-group)
   constexpr int NGW = NG / 8;
   uint4 bq[NGW][4], aq[NGW][MT][4];
 #pragma unroll
@@ -154,22 +163,25 @@ __global__ __launch_bounds__(512) void gemm_da1_route_kernel(const uint16_t* __r
     const int oc = feat / 49, pp = feat % 49, py = pp / 7, px = pp % 7;
     gb[size_t(b) * kFeat + feat] = a < 4 ? g : 0.f;
     const uint16_t gv = f32_to_bf16(g);
-#pragma unroll
-    for (int d = 0; d < 4; ++d) {
-      const int y = 2 * py + (d >> 1), x = 2 * px + (d & 1);
-      const uint16_t v = (d == a) ? gv : uint16_t(0);
-      dc2m[(size_t(b) * kC2 + oc) * 224 + y * 16 + x] = v;
-      dch[(size_t(b) * 324 + (y + 2) * 18 + (x + 2)) * kC2 + oc] = v;
-    }
+    uint16_t* row = dc2m + (size_t(b) * kC2 + oc) * 224 + (2 * py) * 16 + 2 * px;
+    // two 4-byte stores: (dy=0: dx 0,1) and (dy=1: dx 0,1)
+    const uint32_t top = (a == 0 ? gv : 0u) | (uint32_t(a == 1 ? gv : 0u) << 16);
+    const uint32_t bot = (a == 2 ? gv : 0u) | (uint32_t(a == 3 ? gv : 0u) << 16);
+    *reinterpret_cast<uint32_t*>(row) = top;
+    *reinterpret_cast<uint32_t*>(row + 16) = bot;
   }
 }
 
-void gemm_da1_route(const uint16_t* dH, const uint16_t* w1t, const uint8_t* am2, int mrows, int B, uint16_t* dc2m,
-                    uint16_t* dch, float* gb, hipStream_t s) {
+void route_fc2(const uint16_t* dH, const uint16_t* w1t, const uint8_t* am2, int mrows, int B, uint16_t* dc2m,
+               float* gb, const float* dlogits, const uint16_t* H, float* params, float* m, float* v, float* gdump,
+               Offsets off, const int* adam_t, int t_off, AdamCfg cfg, hipStream_t s) {
+  const dim3 grid(kRouteBlocks + kFc2Blocks);
   if (mrows == 32)
-    hipLaunchKernelGGL(gemm_da1_route_kernel<1>, dim3(kFeat / 32), dim3(512), 0, s, dH, w1t, am2, B, dc2m, dch, gb);
+    hipLaunchKernelGGL(route_fc2_kernel<1>, grid, dim3(512), 0, s, dH, w1t, am2, B, dc2m, gb, dlogits, H, params, m,
+                       v, gdump, off, adam_t, t_off, cfg);
   else
-    hipLaunchKernelGGL(gemm_da1_route_kernel<2>, dim3(kFeat / 32), dim3(512), 0, s, dH, w1t, am2, B, dc2m, dch, gb);
+    hipLaunchKernelGGL(route_fc2_kernel<2>, grid, dim3(512), 0, s, dH, w1t, am2, B, dc2m, gb, dlogits, H, params, m,
+                       v, gdump, off, adam_t, t_off, cfg);
 }
 
 // ---------------------------------------------------------------------------
@@ -269,18 +281,34 @@ void fc1_wgrad_adam(const uint16_t* dH, const uint16_t* a1, int mrows, float* pa
 }
 
 // ---------------------------------------------------------------------------
-// 8. conv2 weight gradient.  dW2[oc][ic][tap] = sum_{b,pos} dC2[b][oc][pos] *
-//    P1pad[b][ic][pos + tap].  Grid (25 taps, ceil(B/2)): one wave per (tap,
-//    image pair) computes the full 64 oc x 32 ic tile (two accumulators) over
-//    K = 2 images x 14 rows x 16 cols.  A fragments are 16-B rows of the dC2
-//    map (cols 14/15 are zero), B fragments 16-B rows of the kx-shifted P1
-//    copy -- both aligned, streamed from L2 with loads one half-image ahead.
-//    The tile is written as one coalesced [tap][oc][ic] slab row per pair.
+// 8+9. conv2 backward: one launch of single-wave blocks with two roles, both
+//    consuming the dC2 map.  The longer dgrad waves come first in the grid.
+//
+//  dgrad role, block j < 7B: (tile = j % 7, image b = j / 7).
+//    Phase 1 (MFMA): C[pos][ic] = sum_{tap,oc} dC2pad[pos - tap][oc] W2[oc][ic][tap],
+//      K = 25 taps x 64 oc = 100 k-steps.  A: the tile's window of the padded dC2
+//      image (<= 8 rows x 18 cols x 64 oc) is transposed from the planar map
+//      into HWC in LDS (pairs of channels per 4-B write), so every A fragment is
+//      one 16-B LDS read; B: 16-B rows of the (ic, tap, oc) weight copy
+//      streamed from L2 one 10-step chunk ahead.
+//    Phase 2 (sparse, fp32): pooling routes dP1[pos][ic] to ONE conv1 pixel (its
+//      argmax) or nowhere (ReLU-dead), so dW1[ic][tap] += dP1 * Xpad[pixel + tap]
+//      is a 25-term gather from the input image in LDS -- no dense dC1 map.
+//      Each lane owns one channel and 16 positions; half-waves are combined
+//      with one shuffle; the tile's partial goes to its slab row.
+//  wgrad role, block j - 7B = (tap t, image pair g): dW2[oc][ic][t] over
+//    K = 2 images x 14 rows x 16 cols, 64 oc x 32 ic (two accumulators).  A
+//    fragments are 16-B rows of the dC2 map (cols 14/15 are zero), B fragments
+//    16-B rows of the kx-shifted P1 copy -- both aligned, streamed from L2
+//    with loads one half-image ahead.  Written as one coalesced
+//    [tap][oc][ic] slab row per image pair.
 // ---------------------------------------------------------------------------
-__global__ __launch_bounds__(64) void conv2_wgrad_kernel(const uint16_t* __restrict__ dc2m,
-                                                         const uint16_t* __restrict__ p1s,
-                                                         float* __restrict__ wslab, int B) {
-  const int t = blockIdx.x, g = blockIdx.y, lane = threadIdx.x, r = lane & 31, h = lane >> 5;
+constexpr int kOCP = 72;                      // LDS pixel pitch of the dC2 window (144 B)
+constexpr int kWinRows = 8;
+
+P2_DEVICE void conv2_wgrad_role(int t, int g, const uint16_t* __restrict__ dc2m, const uint16_t* __restrict__ p1s,
+                                float* __restrict__ wslab, int B) {
+  const int lane = threadIdx.x, r = lane & 31, h = lane >> 5;
   const int ky = t / 5, kx = t % 5;
   const int b0 = g * kWgG, nb = min(kWgG, B - b0);
   // half-image chunks: 7 k-steps (rows) each
@@ -332,46 +360,27 @@ __global__ __launch_bounds__(64) void conv2_wgrad_kernel(const uint16_t* __restr
   }
 }
 
-void conv2_wgrad(const uint16_t* dc2m, const uint16_t* p1s, float* wslab2, int B, hipStream_t s) {
-  hipLaunchKernelGGL(conv2_wgrad_kernel, dim3(kTaps, wgrad_groups(B)), dim3(64), 0, s, dc2m, p1s, wslab2, B);
-}
-
-// ---------------------------------------------------------------------------
-// 9. conv2 input gradient + pool1/ReLU backward + conv1 weight gradient.
-//    Grid (7, B): one wave per (32-position tile, image).
-//    Phase 1 (MFMA): C[pos][ic] = sum_{tap,oc} dC2pad[pos - tap][oc] W2[oc][ic][tap],
-//      K = 25 taps x 64 oc = 100 k-steps; A = 16-B pixel rows of the padded HWC
-//      dC2 image, B = 16-B rows of the (ic, tap, oc) weight copy, streamed from
-//      L2 one 10-step chunk ahead.
-//    Phase 2 (sparse, fp32): pooling routes dP1[pos][ic] to ONE conv1 pixel (its
-//      argmax) or nowhere (ReLU-dead), so dW1[ic][tap] += dP1 * Xpad[pixel + tap]
-//      is a 25-term gather from the input image in LDS -- no dense dC1 map, no
-//      second GEMM.  Each lane owns one channel and 16 positions; the half-waves
-//      are combined with one shuffle and the tile's partial goes to its slab row.
-// ---------------------------------------------------------------------------
-__global__ __launch_bounds__(64) void conv2_dgrad_kernel(const uint16_t* __restrict__ dch,
-                                                         const uint8_t* __restrict__ am1,
-                                                         const uint16_t* __restrict__ w2q,
-                                                         const uint8_t* __restrict__ xds,
-                                                         const int64_t* __restrict__ idx,
-                                                         float* __restrict__ wslab1) {
-  __shared__ float xs[32][33];  // zero-padded input image, /255 applied
-  const int tile = blockIdx.x, b = blockIdx.y, lane = threadIdx.x, r = lane & 31, h = lane >> 5;
+P2_DEVICE void conv2_dgrad_role(int tile, int b, const uint16_t* __restrict__ dc2m, const uint8_t* __restrict__ am1,
+                                const uint16_t* __restrict__ w2q, const uint8_t* __restrict__ xds,
+                                const int64_t* __restrict__ idx, float* __restrict__ wslab1, uint16_t* win,
+                                float (*xs)[33]) {
+  const int lane = threadIdx.x, r = lane & 31, h = lane >> 5;
   const int m = tile * 32 + r, mc = m < 196 ? m : 195;
   const int y = mc / 14, x = mc % 14;
-  const uint16_t* abase = dch + size_t(b) * 324 * kC2 + 8 * h;
+  const int ylo = (tile * 32) / 14;  // first padded window row
   const uint16_t* bbase = w2q + size_t(r) * kTaps * kC2 + 8 * h;
-  auto load = [&](int c, uint4 (&A)[10], uint4 (&Bv)[10]) {
+  auto loadb = [&](int c, uint4 (&Bv)[10]) {
 #pragma unroll
     for (int j = 0; j < 10; ++j) {
-      const int s = c * 10 + j, t = s >> 2, ky = t / 5, kx = t % 5, oc0 = (s & 3) * 16;
-      A[j] = *reinterpret_cast<const uint4*>(abase + ((y + 4 - ky) * 18 + (x + 4 - kx)) * kC2 + oc0);
+      const int s = c * 10 + j, t = s >> 2, oc0 = (s & 3) * 16;
       Bv[j] = *reinterpret_cast<const uint4*>(bbase + t * kC2 + oc0);
     }
   };
-  uint4 A0[10], B0[10], A1[10], B1[10];
-  f32x16 acc = {};
-  load(0, A0, B0);
+  uint4 B0[10], B1[10];
+  loadb(0, B0);
+  // dC2 window -> LDS (HWC, zero padding), input image -> LDS
+  const uint4 z4 = make_uint4(0, 0, 0, 0);
+  for (int i = lane; i < kWinRows * 18 * kOCP / 8; i += 64) reinterpret_cast<uint4*>(win)[i] = z4;
   {
     const int64_t row = idx ? idx[b] : b;
     const uint8_t* src = xds + row * (kImg * kImg);
@@ -382,20 +391,43 @@ __global__ __launch_bounds__(64) void conv2_dgrad_kernel(const uint16_t* __restr
       xs[yy][xx] = v;
     }
   }
+  __syncthreads();
+  for (int i = lane; i < kWinRows * 32 * 2; i += 64) {
+    const int wr = i >> 6, pr = (i >> 1) & 31, c = i & 1, yd = ylo + wr - 2;
+    if (yd < 0 || yd > 13) continue;
+    const uint16_t* src = dc2m + (size_t(b) * kC2 + 2 * pr) * 224 + yd * 16 + c * 8;
+    const uint4 u0 = *reinterpret_cast<const uint4*>(src);
+    const uint4 u1 = *reinterpret_cast<const uint4*>(src + 224);
+    const uint16_t* e0 = reinterpret_cast<const uint16_t*>(&u0);
+    const uint16_t* e1 = reinterpret_cast<const uint16_t*>(&u1);
+    uint16_t* dst = win + (wr * 18 + c * 8 + 2) * kOCP + 2 * pr;
 #pragma unroll
-  for (int c = 0; c < 10; c += 2) {
-    load(c + 1, A1, B1);
-    __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-    for (int j = 0; j < 10; ++j) acc = mfma32b(A0[j], B0[j], acc);
-    __builtin_amdgcn_sched_barrier(0);
-    if (c + 2 < 10) load(c + 2, A0, B0);
-    __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-    for (int j = 0; j < 10; ++j) acc = mfma32b(A1[j], B1[j], acc);
-    __builtin_amdgcn_sched_barrier(0);
+    for (int j = 0; j < 8; ++j) *reinterpret_cast<uint32_t*>(dst + j * kOCP) = uint32_t(e0[j]) | (uint32_t(e1[j]) << 16);
   }
   __syncthreads();
+  const uint16_t* abase = win + ((y - ylo) * 18 + x) * kOCP + 8 * h;
+  f32x16 acc = {};
+#pragma unroll
+  for (int c = 0; c < 10; c += 2) {
+    loadb(c + 1, B1);
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int j = 0; j < 10; ++j) {
+      const int s = c * 10 + j, t = s >> 2, ky = t / 5, kx = t % 5, oc0 = (s & 3) * 16;
+      const uint4 a = *reinterpret_cast<const uint4*>(abase + ((4 - ky) * 18 + (4 - kx)) * kOCP + oc0);
+      acc = mfma32b(a, B0[j], acc);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    if (c + 2 < 10) loadb(c + 2, B0);
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int j = 0; j < 10; ++j) {
+      const int s = (c + 1) * 10 + j, t = s >> 2, ky = t / 5, kx = t % 5, oc0 = (s & 3) * 16;
+      const uint4 a = *reinterpret_cast<const uint4*>(abase + ((4 - ky) * 18 + (4 - kx)) * kOCP + oc0);
+      acc = mfma32b(a, B1[j], acc);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+  }
   float wg[kTaps];
 #pragma unroll
   for (int t = 0; t < kTaps; ++t) wg[t] = 0.f;
@@ -427,9 +459,29 @@ __global__ __launch_bounds__(64) void conv2_dgrad_kernel(const uint16_t* __restr
   }
 }
 
-void conv2_dgrad_conv1_wgrad(const uint16_t* dch, const uint8_t* am1, const uint16_t* w2q, const uint8_t* x,
-                             const int64_t* idx, float* wslab1, int B, hipStream_t s) {
-  hipLaunchKernelGGL(conv2_dgrad_kernel, dim3(kDgTiles, B), dim3(64), 0, s, dch, am1, w2q, x, idx, wslab1);
+__global__ __launch_bounds__(64) void conv2_bwd_kernel(const uint16_t* __restrict__ dc2m,
+                                                       const uint16_t* __restrict__ p1s,
+                                                       const uint8_t* __restrict__ am1,
+                                                       const uint16_t* __restrict__ w2q,
+                                                       const uint8_t* __restrict__ xds,
+                                                       const int64_t* __restrict__ idx, float* __restrict__ wslab1,
+                                                       float* __restrict__ wslab2, int B) {
+  __shared__ __attribute__((aligned(16))) uint16_t win[kWinRows * 18 * kOCP];
+  __shared__ float xs[32][33];
+  const int nd = B * kDgTiles;
+  const int j = blockIdx.x;
+  if (j < nd) {
+    conv2_dgrad_role(j % kDgTiles, j / kDgTiles, dc2m, am1, w2q, xds, idx, wslab1, win, xs);
+  } else {
+    const int k = j - nd;
+    conv2_wgrad_role(k % kTaps, k / kTaps, dc2m, p1s, wslab2, B);
+  }
+}
+
+void conv2_bwd(const uint16_t* dc2m, const uint16_t* p1s, const uint8_t* am1, const uint16_t* w2q, const uint8_t* x,
+               const int64_t* idx, float* wslab1, float* wslab2, int B, hipStream_t s) {
+  const int blocks = B * kDgTiles + kTaps * wgrad_groups(B);
+  hipLaunchKernelGGL(conv2_bwd_kernel, dim3(blocks), dim3(64), 0, s, dc2m, p1s, am1, w2q, x, idx, wslab1, wslab2, B);
 }
 
 // ---------------------------------------------------------------------------

@@ -146,7 +146,8 @@ def test_head_and_fc2_wgrad(eng):
     before = eng.params.clone()
     eng.adam_t.fill_(1)
     m_save, v_save = eng.m.clone(), eng.v.clone()
-    eng.C.fc2_wgrad_adam(eng.dlogits, eng.H, B, eng.params, eng.m, eng.v, eng.gdump, eng.off, eng.adam_t, 0, *eng._adam())
+    eng.C.route_fc2(eng.dH, eng.w1tbf, eng.am2, 32, B, eng.dc2m, eng.gb, eng.dlogits, eng.H,
+                    eng.params, eng.m, eng.v, eng.gdump, eng.off, eng.adam_t, 0, *eng._adam())
     torch.cuda.synchronize()
     gw = eng.gdump[eng.off[6] : eng.off[6] + 20480].view(10, 2048)
     gb = eng.gdump[eng.off[7] : eng.off[7] + 10]
@@ -191,10 +192,15 @@ def test_fc1_wgrad_adam(eng):
 
 
 def _route(eng, seed):
-    """Random dH through gemm_da1_route (dA1 = dH W1, pool2/ReLU backward) into the dC2 maps."""
+    """Random dH through route_fc2 (dA1 = dH W1, pool2/ReLU backward) into the dC2 map.
+
+    The launch's FC2-Adam blocks update scratch copies, not the engine's weights.
+    """
     g = torch.Generator(device="cuda").manual_seed(seed)
     dh = (torch.randn(32, 2048, device="cuda", generator=g) * 1e-2).to(torch.bfloat16)
-    eng.C.gemm_da1_route(dh, eng.w1tbf, eng.am2, 32, B, eng.dc2m, eng.dch, eng.gb)
+    P, Mm, V = eng.params.clone(), eng.m.clone(), eng.v.clone()
+    eng.C.route_fc2(dh, eng.w1tbf, eng.am2, 32, B, eng.dc2m, eng.gb, eng.dlogits, eng.H,
+                    P, Mm, V, None, eng.off, eng.adam_t, 1, *eng._adam())
     torch.cuda.synchronize()
     return dh
 
@@ -212,43 +218,53 @@ def test_gemm_da1_route(eng):
     m = eng.dc2m.view(-1, 64, 14, 16)[:B]
     assert _close(m[..., :14], _bf(want), rtol=8e-3, atol=1e-6) < 1e-4
     assert not bool(m[..., 14:].any())  # row padding stays zero
-    hwc = eng.dch.view(-1, 18, 18, 64)[:B]
-    assert torch.equal(hwc[:, 2:16, 2:16, :].permute(0, 3, 1, 2), m[..., :14])
-    border = hwc.clone()
-    border[:, 2:16, 2:16, :] = 0
-    assert not bool(border.any())  # 2-pixel halo stays zero
 
 
-def test_conv2_wgrad(eng):
+def test_conv2_bwd(eng):
+    """conv2_bwd: conv2 weight gradient (wgrad role) and dP1 -> conv1 weight/bias gradient (dgrad role)."""
     x = _x(3)
     _forward(eng, x, train=True)
     _route(eng, 11)
-    eng.C.conv2_wgrad(eng.dc2m, eng.p1s, eng.wslab2, B)
+    eng.C.conv2_bwd(eng.dc2m, eng.p1s, eng.am1, eng.w2q, x.reshape(-1, 784), None, eng.wslab1, eng.wslab2, B)
     torch.cuda.synchronize()
     dc2 = eng.dc2m.view(-1, 64, 14, 16)[:B, :, :, :14].float()
+    # wgrad
     p1 = eng.p1.view(B, 14, 14, 32).permute(0, 3, 1, 2).float()
-    want_w = torch.nn.grad.conv2d_weight(p1, (64, 32, 5, 5), dc2, padding=2)
+    want_w2 = torch.nn.grad.conv2d_weight(p1, (64, 32, 5, 5), dc2, padding=2)
     ng = (B + 1) // 2
-    ws = eng.wslab2[: ng * 51200].view(ng, 25, 64, 32).sum(0)  # [tap][oc][ic]
-    got = ws.permute(1, 2, 0).reshape(64, 32, 5, 5)
-    torch.testing.assert_close(got, want_w, atol=1e-6, rtol=2e-3)
-
-
-def test_conv2_dgrad_conv1_wgrad(eng):
-    x = _x(4)
-    _forward(eng, x, train=True)
-    _route(eng, 12)
-    eng.C.conv2_dgrad_conv1_wgrad(eng.dch, eng.am1, eng.w2q, x.reshape(-1, 784), None, eng.wslab1, B)
-    torch.cuda.synchronize()
-    dc2 = eng.dc2m.view(-1, 64, 14, 16)[:B, :, :, :14].float()
+    ws2 = eng.wslab2[: ng * 51200].view(ng, 25, 64, 32).sum(0)  # [tap][oc][ic]
+    torch.testing.assert_close(ws2.permute(1, 2, 0).reshape(64, 32, 5, 5), want_w2, atol=1e-6, rtol=2e-3)
+    # dgrad + conv1 wgrad
     w2 = _bf(_p(eng, "conv2.weight"))
     dp1 = torch.nn.grad.conv2d_input((B, 32, 14, 14), w2, dc2, padding=2)
     am1 = eng.am1.view(B, 14, 14, 32).permute(0, 3, 1, 2)
     dc1 = _decode_pool(dp1, am1, 28)
-    want_w = torch.nn.grad.conv2d_weight(x.float() / 255.0, (32, 1, 5, 5), dc1, padding=2)
-    ws = eng.wslab1[: B * 7 * 832].view(B * 7, 832).sum(0)
-    torch.testing.assert_close(ws[:800].view(32, 1, 5, 5), want_w, atol=1e-6, rtol=2e-3)
-    torch.testing.assert_close(ws[800:], dc1.sum((0, 2, 3)), atol=1e-6, rtol=1e-3)
+    want_w1 = torch.nn.grad.conv2d_weight(x.float() / 255.0, (32, 1, 5, 5), dc1, padding=2)
+    ws1 = eng.wslab1[: B * 7 * 832].view(B * 7, 832).sum(0)
+    torch.testing.assert_close(ws1[:800].view(32, 1, 5, 5), want_w1, atol=1e-6, rtol=2e-3)
+    torch.testing.assert_close(ws1[800:], dc1.sum((0, 2, 3)), atol=1e-6, rtol=1e-3)
+
+
+@pytest.mark.parametrize("Bp", [7, 1])
+def test_conv2_bwd_partial_batch(eng, Bp):
+    """Odd / tiny batches: the last wgrad image pair holds one image."""
+    x = _x(9)
+    stats = torch.zeros(4, device="cuda")
+    y = torch.zeros(Bp, dtype=torch.int64, device="cuda")
+    eng.forward(x.reshape(-1, 784), y, None, Bp, stats, True)
+    g = torch.Generator(device="cuda").manual_seed(5)
+    dh = (torch.randn(32, 2048, device="cuda", generator=g) * 1e-2).to(torch.bfloat16)
+    dh[Bp:] = 0
+    P, Mm, V = eng.params.clone(), eng.m.clone(), eng.v.clone()
+    eng.C.route_fc2(dh, eng.w1tbf, eng.am2, 32, Bp, eng.dc2m, eng.gb, eng.dlogits, eng.H, P, Mm, V, None, eng.off, eng.adam_t, 1, *eng._adam())
+    eng.C.conv2_bwd(eng.dc2m, eng.p1s, eng.am1, eng.w2q, x.reshape(-1, 784), None, eng.wslab1, eng.wslab2, Bp)
+    torch.cuda.synchronize()
+    dc2 = eng.dc2m.view(-1, 64, 14, 16)[:Bp, :, :, :14].float()
+    p1 = eng.p1.view(-1, 14, 14, 32)[:Bp].permute(0, 3, 1, 2).float()
+    want = torch.nn.grad.conv2d_weight(p1, (64, 32, 5, 5), dc2, padding=2)
+    ng = (Bp + 1) // 2
+    got = eng.wslab2[: ng * 51200].view(ng, 25, 64, 32).sum(0).permute(1, 2, 0).reshape(64, 32, 5, 5)
+    torch.testing.assert_close(got, want, atol=1e-6, rtol=2e-3)
 
 
 def test_conv_adam_and_shadows(eng):

@@ -169,3 +169,4 @@ def test_fused_and_torch_peers_federate():
     finally:
         a.stop()
         b.stop()
+
