@@ -41,7 +41,15 @@ P2_DEVICE AdamScal adam_scal(const AdamCfg& c, const int* t, int t_off) {
   s.inv_sqrt_bc2 = 1.f / sqrtf(1.f - powf(c.beta2, tt));
   return s;
 }
-// torch.optim.Adam semantics (L2 weight decay added to the gradient).
+// torch.optim.Adam semantics (L2 weight decay added to the gradient), on
+// values already in registers (lets a caller batch its loads).
+P2_DEVICE void adam_regs(float& pv, float& mv, float& vv, float g, const AdamCfg& c, const AdamScal& s) {
+  if (c.weight_decay != 0.f) g = fmaf(c.weight_decay, pv, g);
+  mv = fmaf(c.beta1, mv, (1.f - c.beta1) * g);
+  vv = fmaf(c.beta2, vv, (1.f - c.beta2) * g * g);
+  pv -= s.step_size * (mv / (sqrtf(vv) * s.inv_sqrt_bc2 + c.eps));
+}
+// Same, loading and storing in place.
 P2_DEVICE float adam_apply(float* __restrict__ p, float* __restrict__ m, float* __restrict__ v, int64_t e, float g,
                            const AdamCfg& c, const AdamScal& s) {
   float pv = p[e];
@@ -209,6 +217,24 @@ __global__ __launch_bounds__(256) void fc1_wgrad_adam_kernel(const uint16_t* __r
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, r = lane & 31, h = lane >> 5;
   const int n0 = blockIdx.y * 32;
   const int kb = blockIdx.x * 128;
+  const int k0 = kb + wave * 32;
+  const bool valid = k0 < kFeat;
+  // This lane's 16 Adam elements: all 48 fp32 loads (W1, m, v) are issued
+  // first, so their latency overlaps the staging and the MFMA (one memory
+  // round trip per lane instead of one per element).
+  float* pw = p + off.l1w;
+  float* mw = m + off.l1w;
+  float* vw = v + off.l1w;
+  float pr[16], mr[16], vr[16];
+  if (valid) {
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      const int64_t e = int64_t(n0 + acc_row_b(i, h)) * kFeat + k0 + r;
+      pr[i] = pw[e];
+      mr[i] = mw[e];
+      vr[i] = vw[e];
+    }
+  }
   // stage and transpose: dH[b][n0..n0+31] -> sdh[n][b];  A1[b][kb..kb+127] -> sa1[k][b]
   for (int i = tid; i < MR * 4; i += 256) {
     const int b = i >> 2, q = i & 3;
@@ -227,8 +253,6 @@ __global__ __launch_bounds__(256) void fc1_wgrad_adam_kernel(const uint16_t* __r
     for (int j = 0; j < 8; ++j) sa1[q * 8 + j][b] = e[j];
   }
   __syncthreads();
-  const int k0 = kb + wave * 32;
-  const bool valid = k0 < kFeat;
   f32x16 acc = {};
 #pragma unroll
   for (int ks = 0; ks < MR / 16; ++ks) {
@@ -237,17 +261,17 @@ __global__ __launch_bounds__(256) void fc1_wgrad_adam_kernel(const uint16_t* __r
     acc = mfma32b(a, b, acc);
   }
   const AdamScal s = adam_scal(cfg, adam_t, t_off);
-  float* pw = p + off.l1w;
-  float* mw = m + off.l1w;
-  float* vw = v + off.l1w;
   if (valid) {
 #pragma unroll
     for (int i = 0; i < 16; ++i) {
       const int nl = acc_row_b(i, h);
       const int64_t e = int64_t(n0 + nl) * kFeat + k0 + r;
       if (gdump) gdump[off.l1w + e] = acc[i];
-      const float pn = adam_apply(pw, mw, vw, e, acc[i], cfg, s);
-      const uint16_t hb = f32_to_bf16(pn);
+      adam_regs(pr[i], mr[i], vr[i], acc[i], cfg, s);
+      pw[e] = pr[i];
+      mw[e] = mr[i];
+      vw[e] = vr[i];
+      const uint16_t hb = f32_to_bf16(pr[i]);
       w1bf[e] = hb;
       tr[wave * 32 + r][nl] = hb;
     }
