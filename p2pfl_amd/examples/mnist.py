@@ -1,0 +1,94 @@
+"""Decentralized MNIST: N in-process nodes train an MLP or CNN and FedAvg over gossip.
+
+Reference: p2pfl/examples/mnist.py (same flags: --nodes --rounds --epochs
+--show_metrics --measure_time), plus --model, --protocol, --partition and
+--device.  Data is synthetic MNIST-shaped unless P2PFL_MNIST_DIR points at the
+IDX files.  Metrics are printed as a table (no plotting dependency).
+"""
+
+from __future__ import annotations
+
+import argparse
+import time
+from typing import List
+
+from p2pfl_amd.communication.grpc import GrpcCommunicationProtocol
+from p2pfl_amd.communication.memory import InMemoryCommunicationProtocol
+from p2pfl_amd.data import MnistFederatedDM
+from p2pfl_amd.management.logger import logger
+from p2pfl_amd.models import CNN, MLP
+from p2pfl_amd.node import Node
+from p2pfl_amd.settings import Settings
+from p2pfl_amd.utils import wait_4_results, wait_convergence
+
+
+def parse_args(argv=None) -> argparse.Namespace:
+    p = argparse.ArgumentParser(description=__doc__.splitlines()[0])
+    p.add_argument("--nodes", type=int, default=2, help="number of nodes")
+    p.add_argument("--rounds", type=int, default=2, help="number of rounds")
+    p.add_argument("--epochs", type=int, default=1, help="epochs per round")
+    p.add_argument("--show_metrics", action="store_true", default=True, help="print the metric tables")
+    p.add_argument("--measure_time", action="store_true", default=False, help="print the wall-clock time")
+    p.add_argument("--model", choices=["mlp", "cnn"], default="mlp")
+    p.add_argument("--protocol", choices=["memory", "grpc"], default="memory")
+    p.add_argument("--partition", choices=["iid", "label_sorted", "dirichlet"], default="iid")
+    p.add_argument("--alpha", type=float, default=0.5, help="Dirichlet concentration")
+    p.add_argument("--batch", type=int, default=32)
+    p.add_argument("--device", default=None, help="cpu / cuda / cuda:N (default: GPU if present)")
+    p.add_argument("--fast", action="store_true", help="shrink gossip/heartbeat periods (test settings)")
+    return p.parse_args(argv)
+
+
+def _print_metrics() -> None:
+    glob = logger.get_global_logs()
+    for exp, nodes in glob.items():
+        print(f"\n== global metrics ({exp}) ==")
+        for node, metrics in sorted(nodes.items()):
+            for name, series in sorted(metrics.items()):
+                vals = ", ".join(f"r{r}:{v:.4f}" for r, v in series)
+                print(f"  {node:24s} {name:14s} {vals}")
+
+
+def mnist(n: int, r: int, e: int, show_metrics: bool = True, measure_time: bool = False, model: str = "mlp",
+          protocol: str = "memory", partition: str = "iid", alpha: float = 0.5, batch: int = 32,
+          device=None) -> List[Node]:
+    start = time.time()
+    proto = InMemoryCommunicationProtocol if protocol == "memory" else GrpcCommunicationProtocol
+    nodes: List[Node] = []
+    for i in range(n):
+        net = MLP() if model == "mlp" else CNN()
+        data = MnistFederatedDM(sub_id=i, number_sub=n, batch_size=batch, partitioner=partition, alpha=alpha)
+        kw = {"device": device} if device else {}
+        node = Node(net, data, protocol=proto, **kw)
+        node.start()
+        nodes.append(node)
+    try:
+        for i in range(n - 1):
+            nodes[i + 1].connect(nodes[i].addr)
+        wait_convergence(nodes, n - 1, only_direct=False)
+        nodes[0].set_start_learning(rounds=r, epochs=e)
+        wait_4_results(nodes)
+    finally:
+        for node in nodes:
+            node.stop()
+    if show_metrics:
+        _print_metrics()
+    if measure_time:
+        print(f"--- {time.time() - start:.2f} seconds ---")
+    return nodes
+
+
+def main(argv=None) -> None:
+    args = parse_args(argv)
+    if args.fast:
+        from p2pfl_amd.utils import set_test_settings
+
+        set_test_settings()
+    else:
+        Settings.LOG_LEVEL = "INFO"
+    mnist(args.nodes, args.rounds, args.epochs, args.show_metrics, args.measure_time, args.model, args.protocol,
+          args.partition, args.alpha, args.batch, args.device)
+
+
+if __name__ == "__main__":
+    main()

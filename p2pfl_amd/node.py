@@ -18,6 +18,8 @@ from __future__ import annotations
 import threading
 from typing import Any, Dict, Optional, Type
 
+import torch
+
 from p2pfl_amd.commands import (
     AddModelCommand,
     InitModelCommand,
@@ -68,6 +70,8 @@ class Node:
         self.data = data
         self.model = model
         self.learner_class = learner or _default_learner()
+        # extra keyword arguments are forwarded to the learner (e.g. device=...)
+        self.learner_kwargs = dict(kwargs)
         self.aggregator = aggregator(node_name=self.addr)
 
         self._running = False
@@ -201,6 +205,7 @@ class Node:
                 early_stopping_fn=lambda: self.state.round is None,
                 aggregator=self.aggregator,
                 learner_class=self.learner_class,
+                learner_kwargs=self.learner_kwargs,
             )
         except Exception as e:
             logger.error(self.addr, f"Error: {e}")
@@ -217,6 +222,51 @@ class Node:
         self.aggregator.clear()
         self.state.clear()
         logger.experiment_finished(self.addr)
+
+    # ------------------------------------------------------------------
+    # checkpoints
+    # ------------------------------------------------------------------
+    def save_checkpoint(self, path: str) -> str:
+        """Write this peer's current model (flat arena + manifest + round info) to ``path``."""
+        from p2pfl_amd.learning.checkpoint import save_checkpoint
+
+        if self.state.learner is not None:
+            params = self.state.learner.get_parameters()
+            samples = self.state.learner.get_num_samples()
+        elif isinstance(self.model, torch.nn.Module):
+            params = self.model.state_dict()
+            samples = None
+        else:
+            raise LearnerNotSetException("no model to checkpoint")
+        meta = {
+            "addr": self.addr,
+            "experiment": self.state.actual_exp_name,
+            "round": self.state.round,
+            "total_rounds": self.state.total_rounds,
+            "num_samples": list(samples) if samples else None,
+        }
+        return save_checkpoint(path, params, meta)
+
+    def load_checkpoint(self, path: str) -> dict:
+        """Load model weights from ``path`` (into the learner if one exists, else the model); returns the metadata."""
+        from p2pfl_amd.learning.checkpoint import load_checkpoint
+
+        if self.state.learner is not None:
+            params, meta, _ = load_checkpoint(path)
+            self.state.learner.set_parameters(params)
+        elif isinstance(self.model, torch.nn.Module):
+            params, meta, _ = load_checkpoint(path)
+            own = self.model.state_dict()
+            if [tuple(t.shape) for t in own.values()] != [tuple(t.shape) for t in params.values()]:
+                from p2pfl_amd.learning.checkpoint import CheckpointError
+
+                raise CheckpointError(f"{path}: parameter shapes do not match the model")
+            with torch.no_grad():
+                for dst, src in zip(own.values(), params.values()):
+                    dst.copy_(src)
+        else:
+            raise LearnerNotSetException("no model to load into")
+        return meta
 
     def wait_learning(self, timeout: Optional[float] = None) -> bool:
         """Join the local learning thread (new helper); True if it finished."""

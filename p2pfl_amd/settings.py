@@ -72,3 +72,7 @@ class Settings:
     (the reference hard-codes 1: ``lightning_learner.py:38``)."""
     TRACE_SPANS: bool = True
     """Record per-stage / per-gossip timing spans in the tracer."""
+    CHECKPOINT_DIR: str | None = None
+    """If set, every node writes ``<dir>/<addr>/round_<r>.safetensors`` (its
+    aggregated model, flat arena + manifest) at the end of each round; see
+    :mod:`p2pfl_amd.learning.checkpoint` and ``Node.load_checkpoint``."""

@@ -5,6 +5,7 @@ from __future__ import annotations
 from typing import Any, Optional, Type
 
 from p2pfl_amd.management.logger import logger
+from p2pfl_amd.settings import Settings
 from p2pfl_amd.stages.base_node.common import evaluate_and_share
 from p2pfl_amd.stages.stage import Stage
 from p2pfl_amd.stages.stage_factory import StageFactory
@@ -29,6 +30,7 @@ class RoundFinishedStage(Stage):
             logger.info(state.addr, "Early stopping.")
             return None
         aggregator.clear()
+        _auto_checkpoint(state)
         state.increase_round()
         logger.round_finished(state.addr)
         logger.info(state.addr, f"Round {state.round} of {state.total_rounds} finished.")
@@ -46,3 +48,21 @@ class RoundFinishedStage(Stage):
         state.clear()
         logger.info(state.addr, "Training finished!!.")
         return None
+
+
+def _auto_checkpoint(state: Any) -> None:
+    """``Settings.CHECKPOINT_DIR``: persist the round's aggregated model (new; the reference has none)."""
+    if not Settings.CHECKPOINT_DIR or state.learner is None:
+        return
+    import os
+    import re
+
+    from p2pfl_amd.learning.checkpoint import save_checkpoint
+
+    safe = re.sub(r"[^A-Za-z0-9_.-]+", "_", str(state.addr))
+    path = os.path.join(Settings.CHECKPOINT_DIR, safe, f"round_{state.round}.safetensors")
+    meta = {"addr": state.addr, "experiment": state.actual_exp_name, "round": state.round, "total_rounds": state.total_rounds}
+    try:
+        save_checkpoint(path, state.learner.get_parameters(), meta)
+    except Exception as e:  # a full disk must not kill the round
+        logger.error(state.addr, f"checkpoint {path} failed: {e}")

@@ -34,6 +34,7 @@ class StartLearningStage(Stage):
         learner_class: Any = None,
         communication_protocol: Any = None,
         aggregator: Any = None,
+        learner_kwargs: Optional[dict] = None,
         **kwargs,
     ) -> Optional[Type[Stage]]:
         if None in (rounds, epochs, state, learner_class, model, data, communication_protocol, aggregator):
@@ -43,7 +44,7 @@ class StartLearningStage(Stage):
                 return None
             state.set_experiment("experiment", rounds)
             logger.experiment_started(state.addr)
-            state.learner = learner_class(model, data, state.addr, epochs)
+            state.learner = learner_class(model, data, state.addr, epochs, **(learner_kwargs or {}))
         begin = time.time()
         logger.info(state.addr, "Waiting initialization.")
         while not state.model_initialized.wait(timeout=0.5):
