@@ -43,13 +43,16 @@ def init_distributed(backend: Optional[str] = None) -> DistEnv:
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if torch.cuda.is_available():
-        torch.cuda.set_device(local)
-        device = torch.device("cuda", local)
+        # one rank per GPU; more ranks than GPUs (tests on a 1-GPU box) share devices round-robin
+        local_dev = local % torch.cuda.device_count()
+        torch.cuda.set_device(local_dev)
+        device = torch.device("cuda", local_dev)
     else:
         device = torch.device("cpu")
     if world > 1 and not dist.is_initialized():
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        backend = backend or ("nccl" if device.type == "cuda" else "gloo")
+        # P2PFL_DIST_BACKEND=gloo: ranks sharing one GPU (RCCL rejects duplicate devices)
+        backend = backend or os.environ.get("P2PFL_DIST_BACKEND") or ("nccl" if device.type == "cuda" else "gloo")
         kwargs = {"device_id": device} if backend == "nccl" else {}
         dist.init_process_group(backend=backend, rank=rank, world_size=world, **kwargs)
     return DistEnv(rank, world, local, device)
