@@ -22,6 +22,12 @@ Implementations (``--impl``):
              per-layer FedAvg loop (what p2pfl's Lightning learner executes),
              used to measure the baseline on the same MI355X.
 
+Other BASELINE.json configurations (``--model``, PyTorch-ROCm path with the
+fused arena optimiser and, for ViT, the fused LayerNorm/GELU/xent kernels):
+  resnet18   CIFAR-10-shaped, non-IID Dirichlet(0.5) shards, SGD-momentum (config 3)
+  resnet50   CIFAR-10-shaped, Dirichlet shards (config 5's model)
+  vit_b16    ImageNet-shaped 224x224 (197 tokens), AdamW (config 4)
+
 Run:  python bench.py --gpus 1 --steps 3 --warmup 1
       python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
 """
@@ -124,6 +130,47 @@ def reference_round(learner, env, weight, total):
     return time.perf_counter() - t0
 
 
+def build_config(args, env):
+    """(model, data module, model description, data description) for ``--model``."""
+    sub = env.rank
+    if args.model == "cnn":
+        ns = args.number_sub or 20
+        data = MnistFederatedDM(sub_id=sub % ns, number_sub=ns, batch_size=args.batch)
+        return (
+            CNN(seed=1234),
+            data,
+            "MNIST-CNN (p2pfl CNN: conv5x5 32/64 + FC 3136-2048-10, 6.5M params), Adam 1e-3",
+            "synthetic MNIST-shaped (uint8 1x28x28, 10 classes), random-init weights",
+        )
+    if args.model in ("resnet18", "resnet50"):
+        from p2pfl_amd.data import Cifar10FederatedDM
+        from p2pfl_amd.models.resnet import ResNet18, ResNet50
+
+        ns = args.number_sub or 40
+        data = Cifar10FederatedDM(sub_id=sub % ns, number_sub=ns, batch_size=args.batch, partitioner="dirichlet", alpha=0.5)
+        make = ResNet18 if args.model == "resnet18" else ResNet50
+        n = "ResNet-18 (11.2M params)" if args.model == "resnet18" else "ResNet-50 (23.5M params)"
+        return (
+            make(num_classes=10, seed=1234),
+            data,
+            f"{n}, CIFAR stem, SGD(0.05, momentum 0.9, wd 5e-4)",
+            "synthetic CIFAR-10-shaped (uint8 3x32x32), Dirichlet(0.5) non-IID shards, random-init weights",
+        )
+    if args.model == "vit_b16":
+        from p2pfl_amd.data import ImageNetFederatedDM
+        from p2pfl_amd.models.vit import ViT_B16
+
+        ns = args.number_sub or 1
+        data = ImageNetFederatedDM(sub_id=sub % ns, number_sub=ns, batch_size=args.batch, n_train=1024, seed=sub)
+        return (
+            ViT_B16(num_classes=1000, seed=1234),
+            data,
+            "ViT-B/16 (86.6M params, 197 tokens), AdamW(3e-4, wd 0.05)",
+            "synthetic ImageNet-shaped (uint8 3x224x224, 1000 classes), random-init weights",
+        )
+    raise ValueError(args.model)
+
+
 def _sync() -> None:
     if torch.cuda.is_available():
         torch.cuda.synchronize()
@@ -135,8 +182,9 @@ def main() -> None:
     ap.add_argument("--steps", type=int, default=3, help="timed federated rounds")
     ap.add_argument("--warmup", type=int, default=1, help="untimed federated rounds")
     ap.add_argument("--impl", choices=["fused", "torch", "reference"], default="fused")
+    ap.add_argument("--model", choices=["cnn", "resnet18", "resnet50", "vit_b16"], default="cnn")
     ap.add_argument("--epochs", type=int, default=1)
-    ap.add_argument("--number-sub", type=int, default=20)
+    ap.add_argument("--number-sub", type=int, default=None, help="shards of the dataset (default per model)")
     ap.add_argument("--batch", type=int, default=32)
     ap.add_argument("--watchdog", type=float, default=900, help="dump stacks and exit if the run hangs")
     args = ap.parse_args()
@@ -148,8 +196,7 @@ def main() -> None:
     assert env.world_size == args.gpus, f"--gpus {args.gpus} but WORLD_SIZE={env.world_size}"
     dev = env.device
     torch.manual_seed(1234)  # identical init on every peer (the initiator's model)
-    model = CNN(seed=1234)
-    data = MnistFederatedDM(sub_id=env.rank % args.number_sub, number_sub=args.number_sub, batch_size=args.batch)
+    model, data, desc, data_desc = build_config(args, env)
     fed = CollectiveFedAvg(env)
 
     if args.impl == "reference":
@@ -158,7 +205,7 @@ def main() -> None:
         total = fed.total_weight(weight)
         run = lambda: reference_round(learner, env, weight, total)  # noqa: E731
     else:
-        if args.impl == "fused":
+        if args.impl == "fused" and args.model == "cnn":
             from p2pfl_amd.learning.fused_cnn import FusedCNNLearner as L
         else:
             from p2pfl_amd.learning.torch_learner import TorchLearner as L
@@ -198,14 +245,15 @@ def main() -> None:
                     "higher_is_better": True,
                     "scaling": "weak",
                     "vs_baseline": (round(per_peer / base, 3) if base else None),
-                    "dtype": "bf16" if args.impl != "reference" else "fp32",
-                    "data": "synthetic MNIST-shaped (uint8 1x28x28, 10 classes), random-init weights",
-                    "impl": args.impl,
+                    "dtype": "bf16" if (args.impl != "reference" and dev.type == "cuda") else "fp32",
+                    "data": data_desc,
+                    "impl": args.impl if (args.model == "cnn" or args.impl != "fused") else "torch",
                     "config": {
-                        "model": "MNIST-CNN (p2pfl CNN: conv5x5 32/64 + FC 3136-2048-10, 6.5M params)",
+                        "model": desc,
                         "global_batch": args.batch * env.world_size,
-                        "seq_len": None,
-                        "per_peer_round": f"{n_train} train + 300 val + 500 test samples, {args.epochs} epoch, Adam 1e-3",
+                        "seq_len": 197 if args.model == "vit_b16" else None,
+                        "per_peer_round": f"{n_train} train + {len(data.val_dataloader().dataset)} val + "
+                        f"{len(data.test_dataloader().dataset)} test samples, {args.epochs} epoch",
                         "parallelism": f"fedavg-dp{env.world_size}",
                     },
                 }

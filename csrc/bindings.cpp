@@ -86,6 +86,7 @@ void sgd_step(torch::Tensor p, torch::Tensor g, c10::optional<torch::Tensor> buf
 }  // namespace
 
 void register_cnn(pybind11::module& m);
+void register_fused(pybind11::module& m);
 
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.doc() = "p2pfl_amd native HIP/CDNA4 kernels (gfx950)";
@@ -93,4 +94,5 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("adam_step", &adam_step, "fused whole-arena Adam/AdamW step");
   m.def("sgd_step", &sgd_step, "fused whole-arena SGD(+momentum/nesterov) step");
   register_cnn(m);
+  register_fused(m);
 }

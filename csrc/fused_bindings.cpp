@@ -1,0 +1,128 @@
+// PyTorch bindings of the fused transformer / classifier ops (fused_ops.hip).
+#include <c10/core/DeviceGuard.h>
+#include <c10/hip/HIPStream.h>
+#include <torch/extension.h>
+
+#include "fused_ops.h"
+
+namespace {
+
+hipStream_t stream() { return c10::hip::getCurrentHIPStream().stream(); }
+
+bool act_dtype(const torch::Tensor& t, const char* name) {
+  TORCH_CHECK(t.is_cuda() && t.is_contiguous(), name, " must be a contiguous GPU tensor");
+  TORCH_CHECK(t.scalar_type() == torch::kBFloat16 || t.scalar_type() == torch::kFloat32, name, " must be bf16 or fp32");
+  TORCH_CHECK(reinterpret_cast<uintptr_t>(t.data_ptr()) % 16 == 0, name, " must be 16-byte aligned");
+  return t.scalar_type() == torch::kBFloat16;
+}
+
+void check_f32(const torch::Tensor& t, int64_t n, const char* name) {
+  TORCH_CHECK(t.is_cuda() && t.is_contiguous() && t.scalar_type() == torch::kFloat32, name, " must be contiguous fp32 on GPU");
+  TORCH_CHECK(t.numel() >= n, name, " too small");
+}
+
+std::vector<torch::Tensor> ln_fwd(torch::Tensor x, torch::Tensor w, torch::Tensor b, double eps) {
+  const c10::DeviceGuard g(x.device());
+  TORCH_CHECK(x.dim() == 2, "x must be [N, C]");
+  const int64_t N = x.size(0), C = x.size(1);
+  TORCH_CHECK(C % 8 == 0 && C <= p2fused::kMaxLnCols, "C must be a multiple of 8 and <= 2048");
+  const bool bf = act_dtype(x, "x");
+  check_f32(w, C, "weight");
+  check_f32(b, C, "bias");
+  auto y = torch::empty_like(x);
+  auto opt = x.options().dtype(torch::kFloat32);
+  auto mean = torch::empty({N}, opt), rstd = torch::empty({N}, opt);
+  if (N > 0)
+    p2fused::layer_norm_fwd(bf, x.data_ptr(), w.data_ptr<float>(), b.data_ptr<float>(), y.data_ptr(),
+                            mean.data_ptr<float>(), rstd.data_ptr<float>(), int(N), int(C), float(eps), stream());
+  return {y, mean, rstd};
+}
+
+std::vector<torch::Tensor> ln_bwd(torch::Tensor dy, torch::Tensor x, torch::Tensor w, torch::Tensor mean,
+                                  torch::Tensor rstd) {
+  const c10::DeviceGuard g(x.device());
+  const int64_t N = x.size(0), C = x.size(1);
+  TORCH_CHECK(dy.sizes() == x.sizes() && dy.scalar_type() == x.scalar_type(), "dy must match x");
+  const bool bf = act_dtype(x, "x");
+  act_dtype(dy, "dy");
+  check_f32(w, C, "weight");
+  check_f32(mean, N, "mean");
+  check_f32(rstd, N, "rstd");
+  auto dx = torch::empty_like(x);
+  auto opt = x.options().dtype(torch::kFloat32);
+  auto dw = torch::zeros({C}, opt), db = torch::zeros({C}, opt);
+  if (N > 0) {
+    const int G = p2fused::layer_norm_bwd_blocks(int(N));
+    auto pdw = torch::empty({G, C}, opt), pdb = torch::empty({G, C}, opt);
+    p2fused::layer_norm_bwd(bf, dy.data_ptr(), x.data_ptr(), w.data_ptr<float>(), mean.data_ptr<float>(),
+                            rstd.data_ptr<float>(), dx.data_ptr(), pdw.data_ptr<float>(), pdb.data_ptr<float>(),
+                            dw.data_ptr<float>(), db.data_ptr<float>(), int(N), int(C), stream());
+  }
+  return {dx, dw, db};
+}
+
+torch::Tensor bias_gelu_fwd(torch::Tensor x, torch::Tensor b) {
+  const c10::DeviceGuard g(x.device());
+  const int64_t H = x.size(-1);
+  TORCH_CHECK(H % 8 == 0, "last dim must be a multiple of 8");
+  const bool bf = act_dtype(x, "x");
+  check_f32(b, H, "bias");
+  auto y = torch::empty_like(x);
+  if (x.numel() > 0) p2fused::bias_gelu_fwd(bf, x.data_ptr(), b.data_ptr<float>(), y.data_ptr(), x.numel(), int(H), stream());
+  return y;
+}
+
+std::vector<torch::Tensor> bias_gelu_bwd(torch::Tensor dy, torch::Tensor x, torch::Tensor b) {
+  const c10::DeviceGuard g(x.device());
+  const int64_t H = x.size(-1), N = x.numel() / H;
+  TORCH_CHECK(dy.sizes() == x.sizes() && dy.scalar_type() == x.scalar_type(), "dy must match x");
+  const bool bf = act_dtype(x, "x");
+  act_dtype(dy, "dy");
+  check_f32(b, H, "bias");
+  auto dx = torch::empty_like(x);
+  auto db = torch::zeros({H}, x.options().dtype(torch::kFloat32));
+  if (N > 0) {
+    auto pdb = torch::empty({p2fused::bias_gelu_bwd_splits(int(N)), H}, x.options().dtype(torch::kFloat32));
+    p2fused::bias_gelu_bwd(bf, dy.data_ptr(), x.data_ptr(), b.data_ptr<float>(), dx.data_ptr(), pdb.data_ptr<float>(),
+                           db.data_ptr<float>(), int(N), int(H), stream());
+  }
+  return {dx, db};
+}
+
+std::vector<torch::Tensor> xent_fwd(torch::Tensor z, torch::Tensor y) {
+  const c10::DeviceGuard g(z.device());
+  TORCH_CHECK(z.dim() == 2, "logits must be [N, K]");
+  TORCH_CHECK(y.is_cuda() && y.scalar_type() == torch::kInt64 && y.is_contiguous() && y.numel() == z.size(0),
+              "labels must be int64 [N] on the GPU");
+  const bool bf = act_dtype(z, "logits");
+  const int64_t N = z.size(0), K = z.size(1);
+  auto opt = z.options().dtype(torch::kFloat32);
+  auto loss = torch::empty({N}, opt), lse = torch::empty({N}, opt);
+  if (N > 0) p2fused::xent_fwd(bf, z.data_ptr(), y.data_ptr<int64_t>(), loss.data_ptr<float>(), lse.data_ptr<float>(), int(N), int(K), stream());
+  return {loss, lse};
+}
+
+torch::Tensor xent_bwd(torch::Tensor z, torch::Tensor y, torch::Tensor lse, torch::Tensor gscale) {
+  const c10::DeviceGuard g(z.device());
+  const bool bf = act_dtype(z, "logits");
+  const int64_t N = z.size(0), K = z.size(1);
+  check_f32(lse, N, "lse");
+  check_f32(gscale, 1, "grad");
+  auto dz = torch::empty_like(z);
+  if (N > 0)
+    p2fused::xent_bwd(bf, z.data_ptr(), y.data_ptr<int64_t>(), lse.data_ptr<float>(), gscale.data_ptr<float>(),
+                      dz.data_ptr(), int(N), int(K), stream());
+  return dz;
+}
+
+}  // namespace
+
+void register_fused(pybind11::module& m) {
+  auto f = m.def_submodule("fused", "fused LayerNorm / bias+GELU / softmax cross-entropy kernels");
+  f.def("ln_fwd", &ln_fwd);
+  f.def("ln_bwd", &ln_bwd);
+  f.def("bias_gelu_fwd", &bias_gelu_fwd);
+  f.def("bias_gelu_bwd", &bias_gelu_bwd);
+  f.def("xent_fwd", &xent_fwd);
+  f.def("xent_bwd", &xent_bwd);
+}

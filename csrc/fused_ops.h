@@ -1,0 +1,28 @@
+// Fused transformer / classifier ops (fused_ops.hip).  bf16 selects uint16
+// bf16 activations, else fp32; parameters, statistics and partials are fp32.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace p2fused {
+
+constexpr int kMaxLnCols = 2048;  // row kept in registers (C % 8 == 0)
+
+void layer_norm_fwd(bool bf16, const void* x, const float* w, const float* b, void* y, float* mean, float* rstd,
+                    int N, int C, float eps, hipStream_t s);
+// partial buffers: [layer_norm_bwd_blocks(N)][C] each
+int layer_norm_bwd_blocks(int N);
+void layer_norm_bwd(bool bf16, const void* dy, const void* x, const float* w, const float* mean, const float* rstd,
+                    void* dx, float* pdw, float* pdb, float* dw, float* db, int N, int C, hipStream_t s);
+
+void bias_gelu_fwd(bool bf16, const void* x, const float* b, void* y, int64_t n, int H, hipStream_t s);
+// partial buffer: [bias_gelu_bwd_splits(N)][H]
+int bias_gelu_bwd_splits(int N);
+void bias_gelu_bwd(bool bf16, const void* dy, const void* x, const float* b, void* dx, float* pdb, float* db, int N,
+                   int H, hipStream_t s);
+
+void xent_fwd(bool bf16, const void* z, const int64_t* y, float* loss, float* lse, int N, int K, hipStream_t s);
+void xent_bwd(bool bf16, const void* z, const int64_t* y, const float* lse, const float* gscale, void* dz, int N, int K,
+              hipStream_t s);
+
+}  // namespace p2fused

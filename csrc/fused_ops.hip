@@ -1,0 +1,428 @@
+// Fused transformer / classifier ops for MI355X (gfx950, wave64):
+//   LayerNorm forward / backward, bias + GELU forward / backward,
+//   softmax cross-entropy forward / backward.
+// Activations are bf16 or fp32 (T), parameters and statistics fp32.  Every
+// row-wise op gives one row to one wave (64 lanes x 16-B vector loads), keeps
+// the row in registers between its passes, and reduces with cross-lane
+// shuffles.  Column reductions (LayerNorm dgamma/dbeta, GELU dbias) are
+// per-block partial rows summed by col_reduce in fixed order: no float
+// atomics, bitwise-reproducible results.
+#include "common.h"
+#include "fused_ops.h"
+
+namespace p2fused {
+using namespace p2;
+
+// ---- 8-element vector load/store for bf16 (16 B) and fp32 (2 x 16 B) ----
+template <typename T>
+struct Vec8;
+template <>
+struct Vec8<uint16_t> {
+  static P2_DEVICE void load(const uint16_t* p, float (&v)[8]) {
+    const uint4 u = *reinterpret_cast<const uint4*>(p);
+    const uint32_t w[4] = {u.x, u.y, u.z, u.w};
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      v[2 * j] = __uint_as_float(w[j] << 16);
+      v[2 * j + 1] = __uint_as_float(w[j] & 0xffff0000u);
+    }
+  }
+  static P2_DEVICE void store(uint16_t* p, const float (&v)[8]) {
+    uint4 u;
+    u.x = pack_bf16x2(v[0], v[1]);
+    u.y = pack_bf16x2(v[2], v[3]);
+    u.z = pack_bf16x2(v[4], v[5]);
+    u.w = pack_bf16x2(v[6], v[7]);
+    *reinterpret_cast<uint4*>(p) = u;
+  }
+};
+template <>
+struct Vec8<float> {
+  static P2_DEVICE void load(const float* p, float (&v)[8]) {
+    const float4 a = reinterpret_cast<const float4*>(p)[0], b = reinterpret_cast<const float4*>(p)[1];
+    v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w;
+    v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
+  }
+  static P2_DEVICE void store(float* p, const float (&v)[8]) {
+    reinterpret_cast<float4*>(p)[0] = make_float4(v[0], v[1], v[2], v[3]);
+    reinterpret_cast<float4*>(p)[1] = make_float4(v[4], v[5], v[6], v[7]);
+  }
+};
+P2_DEVICE void load8f(const float* p, float (&v)[8]) { Vec8<float>::load(p, v); }
+
+// ---------------------------------------------------------------------------
+// LayerNorm forward: y = (x - mean) * rstd * w + b over the last dim C.
+// One wave per row; the row (C <= 512 * K elements, C <= 2048) stays in registers
+// between the mean and the variance pass (two-pass variance: no
+// cancellation).  Saves mean / rstd for the backward.
+// ---------------------------------------------------------------------------
+template <typename T, int K>
+__global__ __launch_bounds__(256) void ln_fwd_kernel(const T* __restrict__ x, const float* __restrict__ w,
+                                                     const float* __restrict__ b, T* __restrict__ y,
+                                                     float* __restrict__ mean_out, float* __restrict__ rstd_out,
+                                                     int N, int C, float eps) {
+  const int lane = threadIdx.x & 63;
+  const int nw = gridDim.x * 4;
+  for (int row = blockIdx.x * 4 + (threadIdx.x >> 6); row < N; row += nw) {
+    const T* xr = x + size_t(row) * C;
+    float v[K][8];
+    float s = 0.f;
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+      const int c = (lane + 64 * k) * 8;
+      if (c < C) {
+        Vec8<T>::load(xr + c, v[k]);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) s += v[k][j];
+      }
+    }
+    const float mean = wave_sum(s) / float(C);
+    float q = 0.f;
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+      const int c = (lane + 64 * k) * 8;
+      if (c < C)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const float d = v[k][j] - mean;
+          q = fmaf(d, d, q);
+        }
+    }
+    const float rstd = rsqrtf(wave_sum(q) / float(C) + eps);
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+      const int c = (lane + 64 * k) * 8;
+      if (c < C) {
+        float wv[8], bv[8], o[8];
+        load8f(w + c, wv);
+        load8f(b + c, bv);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) o[j] = fmaf((v[k][j] - mean) * rstd, wv[j], bv[j]);
+        Vec8<T>::store(y + size_t(row) * C + c, o);
+      }
+    }
+    if (lane == 0) {
+      mean_out[row] = mean;
+      rstd_out[row] = rstd;
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// LayerNorm backward.  Per row (xhat = (x - mean) * rstd, g = dy * w):
+//   dx = rstd * (g - mean(g) - xhat * mean(g * xhat))
+// and per-block partial column sums of dy * xhat (dgamma) and dy (dbeta),
+// combined across the block's 4 waves in fixed order through LDS.
+// ---------------------------------------------------------------------------
+template <typename T, int K>
+__global__ __launch_bounds__(256) void ln_bwd_kernel(const T* __restrict__ dy, const T* __restrict__ x,
+                                                     const float* __restrict__ w, const float* __restrict__ mean_in,
+                                                     const float* __restrict__ rstd_in, T* __restrict__ dx,
+                                                     float* __restrict__ part_dw, float* __restrict__ part_db, int N,
+                                                     int C) {
+  extern __shared__ float sred[];  // [2][C]
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int nw = gridDim.x * 4;
+  float adw[K][8], adb[K][8];
+#pragma unroll
+  for (int k = 0; k < K; ++k)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) adw[k][j] = adb[k][j] = 0.f;
+  for (int row = blockIdx.x * 4 + wave; row < N; row += nw) {
+    const float mean = mean_in[row], rstd = rstd_in[row];
+    float xh[K][8], g[K][8];
+    float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+      const int c = (lane + 64 * k) * 8;
+      if (c < C) {
+        float xv[8], dv[8], wv[8];
+        Vec8<T>::load(x + size_t(row) * C + c, xv);
+        Vec8<T>::load(dy + size_t(row) * C + c, dv);
+        load8f(w + c, wv);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          xh[k][j] = (xv[j] - mean) * rstd;
+          g[k][j] = dv[j] * wv[j];
+          s1 += g[k][j];
+          s2 = fmaf(g[k][j], xh[k][j], s2);
+          adw[k][j] = fmaf(dv[j], xh[k][j], adw[k][j]);
+          adb[k][j] += dv[j];
+        }
+      }
+    }
+    const float m1 = wave_sum(s1) / float(C), m2 = wave_sum(s2) / float(C);
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+      const int c = (lane + 64 * k) * 8;
+      if (c < C) {
+        float o[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) o[j] = rstd * (g[k][j] - m1 - xh[k][j] * m2);
+        Vec8<T>::store(dx + size_t(row) * C + c, o);
+      }
+    }
+  }
+  // fixed-order cross-wave sum of the column partials
+  for (int wv = 0; wv < 4; ++wv) {
+    if (wave == wv) {
+#pragma unroll
+      for (int k = 0; k < K; ++k) {
+        const int c = (lane + 64 * k) * 8;
+        if (c < C)
+#pragma unroll
+          for (int j = 0; j < 8; ++j) {
+            sred[c + j] = (wv == 0 ? 0.f : sred[c + j]) + adw[k][j];
+            sred[C + c + j] = (wv == 0 ? 0.f : sred[C + c + j]) + adb[k][j];
+          }
+      }
+    }
+    __syncthreads();
+  }
+  for (int c = threadIdx.x; c < C; c += 256) {
+    part_dw[size_t(blockIdx.x) * C + c] = sred[c];
+    part_db[size_t(blockIdx.x) * C + c] = sred[C + c];
+  }
+}
+
+// out[c] = sum_r part[r][c] (fixed order), for one or two partial arrays.
+__global__ __launch_bounds__(256) void col_reduce_kernel(const float* __restrict__ a, float* __restrict__ oa,
+                                                         const float* __restrict__ b, float* __restrict__ ob, int R,
+                                                         int C) {
+  const int c = blockIdx.x * 256 + threadIdx.x;
+  if (c >= C) return;
+  float sa = 0.f, sb = 0.f;
+  for (int r = 0; r < R; ++r) {
+    sa += a[size_t(r) * C + c];
+    if (b) sb += b[size_t(r) * C + c];
+  }
+  oa[c] = sa;
+  if (b) ob[c] = sb;
+}
+
+// ---------------------------------------------------------------------------
+// bias + GELU (exact erf form, = torch.nn.functional.gelu default)
+// ---------------------------------------------------------------------------
+P2_DEVICE float gelu_f(float z) { return 0.5f * z * (1.f + erff(z * 0.70710678118654752f)); }
+P2_DEVICE float gelu_grad(float z) {
+  return 0.5f * (1.f + erff(z * 0.70710678118654752f)) + z * 0.39894228040143268f * __expf(-0.5f * z * z);
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void bias_gelu_fwd_kernel(const T* __restrict__ x, const float* __restrict__ b,
+                                                            T* __restrict__ y, int64_t n8, int H) {
+  for (int64_t i = blockIdx.x * int64_t(256) + threadIdx.x; i < n8; i += int64_t(gridDim.x) * 256) {
+    const int64_t e = i * 8;
+    const int c = int(e % H);
+    float v[8], bv[8];
+    Vec8<T>::load(x + e, v);
+    load8f(b + c, bv);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] = gelu_f(v[j] + bv[j]);
+    Vec8<T>::store(y + e, v);
+  }
+}
+
+// dx = dy * gelu'(x + b); per-block partial column sums of dx (dbias).
+// Grid (ceil(H / 512), S): 64 lanes x 8 columns per block, 4 row phases,
+// rows strided by 4 * S.
+template <typename T>
+__global__ __launch_bounds__(256) void bias_gelu_bwd_kernel(const T* __restrict__ dy, const T* __restrict__ x,
+                                                            const float* __restrict__ b, T* __restrict__ dx,
+                                                            float* __restrict__ part_db, int N, int H) {
+  __shared__ float red[4][512];
+  const int lane = threadIdx.x & 63, ph = threadIdx.x >> 6;
+  const int c = (blockIdx.x * 64 + lane) * 8;
+  const int S = gridDim.y;
+  float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  if (c < H) {
+    float bv[8];
+    load8f(b + c, bv);
+    for (int r = blockIdx.y * 4 + ph; r < N; r += 4 * S) {
+      float xv[8], dv[8], o[8];
+      Vec8<T>::load(x + size_t(r) * H + c, xv);
+      Vec8<T>::load(dy + size_t(r) * H + c, dv);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        o[j] = dv[j] * gelu_grad(xv[j] + bv[j]);
+        acc[j] += o[j];
+      }
+      Vec8<T>::store(dx + size_t(r) * H + c, o);
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < 8; ++j) red[ph][lane * 8 + j] = acc[j];
+  __syncthreads();
+  for (int i = threadIdx.x; i < 512; i += 256) {
+    const int cc = blockIdx.x * 512 + i;
+    if (cc < H) part_db[size_t(blockIdx.y) * H + cc] = (red[0][i] + red[1][i]) + (red[2][i] + red[3][i]);
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Softmax cross-entropy: loss_r = logsumexp(z_r) - z_r[y_r]; one wave per
+// row, online max/sum per lane then combined across the wave.
+// Backward: dz = (softmax(z) - onehot(y)) * (*gscale) / N, with the upstream
+// gradient read from device memory (no host sync).
+// ---------------------------------------------------------------------------
+template <typename T>
+P2_DEVICE float ld1(const T* p);
+template <>
+P2_DEVICE float ld1<uint16_t>(const uint16_t* p) { return bf16_to_f32(*p); }
+template <>
+P2_DEVICE float ld1<float>(const float* p) { return *p; }
+template <typename T>
+P2_DEVICE void st1(T* p, float v);
+template <>
+P2_DEVICE void st1<uint16_t>(uint16_t* p, float v) { *p = f32_to_bf16(v); }
+template <>
+P2_DEVICE void st1<float>(float* p, float v) { *p = v; }
+
+template <typename T>
+__global__ __launch_bounds__(256) void xent_fwd_kernel(const T* __restrict__ z, const int64_t* __restrict__ y,
+                                                       float* __restrict__ loss, float* __restrict__ lse_out, int N,
+                                                       int K) {
+  const int lane = threadIdx.x & 63;
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= N) return;
+  const T* zr = z + size_t(row) * K;
+  float m = -INFINITY, s = 0.f;
+  for (int k = lane; k < K; k += 64) {
+    const float v = ld1<T>(zr + k);
+    if (v > m) {
+      s = s * __expf(m - v) + 1.f;
+      m = v;
+    } else {
+      s += __expf(v - m);
+    }
+  }
+  const float gm = wave_max(m);
+  s = (m == -INFINITY) ? 0.f : s * __expf(m - gm);
+  const float lse = gm + __logf(wave_sum(s));
+  if (lane == 0) {
+    const int64_t t = y[row];
+    lse_out[row] = lse;
+    loss[row] = (t >= 0 && t < K) ? lse - ld1<T>(zr + t) : 0.f;
+  }
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void xent_bwd_kernel(const T* __restrict__ z, const int64_t* __restrict__ y,
+                                                       const float* __restrict__ lse, const float* __restrict__ gscale,
+                                                       T* __restrict__ dz, int N, int K, float inv_n) {
+  const int64_t total = int64_t(N) * K;
+  const float g = *gscale * inv_n;
+  for (int64_t e = blockIdx.x * int64_t(256) + threadIdx.x; e < total; e += int64_t(gridDim.x) * 256) {
+    const int row = int(e / K), k = int(e % K);
+    const float p = __expf(ld1<T>(z + e) - lse[row]);
+    st1<T>(dz + e, (p - (y[row] == k ? 1.f : 0.f)) * g);
+  }
+}
+
+// ---------------------------------------------------------------------------
+// launchers
+// ---------------------------------------------------------------------------
+static int rows_grid(int N) {
+  int g = (N + 3) / 4;
+  return g > 4096 ? 4096 : (g < 1 ? 1 : g);
+}
+
+template <typename T>
+static void ln_fwd_t(const void* x, const float* w, const float* b, void* y, float* mean, float* rstd, int N, int C,
+                     float eps, hipStream_t s) {
+  const dim3 grid(rows_grid(N)), blk(256);
+  const T* xp = static_cast<const T*>(x);
+  T* yp = static_cast<T*>(y);
+  if (C <= 512)
+    hipLaunchKernelGGL((ln_fwd_kernel<T, 1>), grid, blk, 0, s, xp, w, b, yp, mean, rstd, N, C, eps);
+  else
+    hipLaunchKernelGGL((ln_fwd_kernel<T, 4>), grid, blk, 0, s, xp, w, b, yp, mean, rstd, N, C, eps);
+}
+
+void layer_norm_fwd(bool bf16, const void* x, const float* w, const float* b, void* y, float* mean, float* rstd,
+                    int N, int C, float eps, hipStream_t s) {
+  if (bf16)
+    ln_fwd_t<uint16_t>(x, w, b, y, mean, rstd, N, C, eps, s);
+  else
+    ln_fwd_t<float>(x, w, b, y, mean, rstd, N, C, eps, s);
+}
+
+int layer_norm_bwd_blocks(int N) {
+  int g = (N + 15) / 16;  // >= 4 rows per wave
+  return g > 512 ? 512 : (g < 1 ? 1 : g);
+}
+
+template <typename T>
+static void ln_bwd_t(const void* dy, const void* x, const float* w, const float* mean, const float* rstd, void* dx,
+                     float* pdw, float* pdb, float* dw, float* db, int N, int C, hipStream_t s) {
+  const int G = layer_norm_bwd_blocks(N);
+  const dim3 grid(G), blk(256);
+  const size_t lds = size_t(2) * C * sizeof(float);
+  const T* dyp = static_cast<const T*>(dy);
+  const T* xp = static_cast<const T*>(x);
+  T* dxp = static_cast<T*>(dx);
+  if (C <= 512)
+    hipLaunchKernelGGL((ln_bwd_kernel<T, 1>), grid, blk, lds, s, dyp, xp, w, mean, rstd, dxp, pdw, pdb, N, C);
+  else
+    hipLaunchKernelGGL((ln_bwd_kernel<T, 4>), grid, blk, lds, s, dyp, xp, w, mean, rstd, dxp, pdw, pdb, N, C);
+  hipLaunchKernelGGL(col_reduce_kernel, dim3((C + 255) / 256), blk, 0, s, pdw, dw, pdb, db, G, C);
+}
+
+void layer_norm_bwd(bool bf16, const void* dy, const void* x, const float* w, const float* mean, const float* rstd,
+                    void* dx, float* pdw, float* pdb, float* dw, float* db, int N, int C, hipStream_t s) {
+  if (bf16)
+    ln_bwd_t<uint16_t>(dy, x, w, mean, rstd, dx, pdw, pdb, dw, db, N, C, s);
+  else
+    ln_bwd_t<float>(dy, x, w, mean, rstd, dx, pdw, pdb, dw, db, N, C, s);
+}
+
+void bias_gelu_fwd(bool bf16, const void* x, const float* b, void* y, int64_t n, int H, hipStream_t s) {
+  const int64_t n8 = n / 8;
+  const dim3 grid(stream_grid(n8, 256)), blk(256);
+  if (bf16)
+    hipLaunchKernelGGL(bias_gelu_fwd_kernel<uint16_t>, grid, blk, 0, s, static_cast<const uint16_t*>(x), b,
+                       static_cast<uint16_t*>(y), n8, H);
+  else
+    hipLaunchKernelGGL(bias_gelu_fwd_kernel<float>, grid, blk, 0, s, static_cast<const float*>(x), b,
+                       static_cast<float*>(y), n8, H);
+}
+
+int bias_gelu_bwd_splits(int N) {
+  int S = (N + 31) / 32;
+  return S > 128 ? 128 : (S < 1 ? 1 : S);
+}
+
+void bias_gelu_bwd(bool bf16, const void* dy, const void* x, const float* b, void* dx, float* pdb, float* db, int N,
+                   int H, hipStream_t s) {
+  const int S = bias_gelu_bwd_splits(N);
+  const dim3 grid((H + 511) / 512, S), blk(256);
+  if (bf16)
+    hipLaunchKernelGGL(bias_gelu_bwd_kernel<uint16_t>, grid, blk, 0, s, static_cast<const uint16_t*>(dy),
+                       static_cast<const uint16_t*>(x), b, static_cast<uint16_t*>(dx), pdb, N, H);
+  else
+    hipLaunchKernelGGL(bias_gelu_bwd_kernel<float>, grid, blk, 0, s, static_cast<const float*>(dy),
+                       static_cast<const float*>(x), b, static_cast<float*>(dx), pdb, N, H);
+  hipLaunchKernelGGL(col_reduce_kernel, dim3((H + 255) / 256), blk, 0, s, pdb, db, nullptr, nullptr, S, H);
+}
+
+void xent_fwd(bool bf16, const void* z, const int64_t* y, float* loss, float* lse, int N, int K, hipStream_t s) {
+  const dim3 grid((N + 3) / 4), blk(256);
+  if (bf16)
+    hipLaunchKernelGGL(xent_fwd_kernel<uint16_t>, grid, blk, 0, s, static_cast<const uint16_t*>(z), y, loss, lse, N, K);
+  else
+    hipLaunchKernelGGL(xent_fwd_kernel<float>, grid, blk, 0, s, static_cast<const float*>(z), y, loss, lse, N, K);
+}
+
+void xent_bwd(bool bf16, const void* z, const int64_t* y, const float* lse, const float* gscale, void* dz, int N, int K,
+              hipStream_t s) {
+  const dim3 grid(stream_grid(int64_t(N) * K, 256)), blk(256);
+  const float inv_n = 1.f / float(N);
+  if (bf16)
+    hipLaunchKernelGGL(xent_bwd_kernel<uint16_t>, grid, blk, 0, s, static_cast<const uint16_t*>(z), y, lse, gscale,
+                       static_cast<uint16_t*>(dz), N, K, inv_n);
+  else
+    hipLaunchKernelGGL(xent_bwd_kernel<float>, grid, blk, 0, s, static_cast<const float*>(z), y, lse, gscale,
+                       static_cast<float*>(dz), N, K, inv_n);
+}
+
+}  // namespace p2fused

@@ -29,6 +29,24 @@ class _ArenaOptimizer:
         self.lr = lr
         self.weight_decay = weight_decay
         self.t = 0
+        # Buffers (BatchNorm running stats, mirrored integer counters) share the
+        # arena with the parameters but must not be touched by the update
+        # (weight decay would shrink them): their elements are saved before and
+        # restored after each fused step -- a few KB against a full-arena kernel.
+        params = set(arena.param_names)
+        lay = arena.layout
+        idx = [
+            torch.arange(off, off + n, dtype=torch.int64)
+            for name, off, n in zip(lay.names, lay.offsets, lay.sizes())
+            if name not in params and n > 0
+        ]
+        self._buf_idx = torch.cat(idx).to(arena.flat.device) if idx else None
+
+    def _step_keep_buffers(self, fn) -> None:
+        saved = self.arena.flat.index_select(0, self._buf_idx) if self._buf_idx is not None else None
+        fn()
+        if saved is not None:
+            self.arena.flat.index_copy_(0, self._buf_idx, saved)
 
     def zero_grad(self, set_to_none: bool = False) -> None:
         assert self.arena.grads is not None
@@ -60,18 +78,20 @@ class ArenaAdam(_ArenaOptimizer):
 
     def step(self) -> None:
         self.t += 1
-        ops.adam_step(
-            self.arena.flat,
-            self._grads(),
-            self.m,
-            self.v,
-            lr=self.lr,
-            beta1=self.beta1,
-            beta2=self.beta2,
-            eps=self.eps,
-            weight_decay=self.weight_decay,
-            step=self.t,
-            decoupled=self.decoupled,
+        self._step_keep_buffers(
+            lambda: ops.adam_step(
+                self.arena.flat,
+                self._grads(),
+                self.m,
+                self.v,
+                lr=self.lr,
+                beta1=self.beta1,
+                beta2=self.beta2,
+                eps=self.eps,
+                weight_decay=self.weight_decay,
+                step=self.t,
+                decoupled=self.decoupled,
+            )
         )
 
 
@@ -91,16 +111,18 @@ class ArenaSGD(_ArenaOptimizer):
 
     def step(self) -> None:
         self.t += 1
-        ops.sgd_step(
-            self.arena.flat,
-            self._grads(),
-            self.buf,
-            lr=self.lr,
-            momentum=self.momentum,
-            dampening=self.dampening,
-            weight_decay=self.weight_decay,
-            nesterov=self.nesterov,
-            first_step=self.t == 1,
+        self._step_keep_buffers(
+            lambda: ops.sgd_step(
+                self.arena.flat,
+                self._grads(),
+                self.buf,
+                lr=self.lr,
+                momentum=self.momentum,
+                dampening=self.dampening,
+                weight_decay=self.weight_decay,
+                nesterov=self.nesterov,
+                first_step=self.t == 1,
+            )
         )
 
 

@@ -1,0 +1,136 @@
+"""ResNet-18/34/50 (BASELINE.json configs 3 and 5).
+
+Not in the reference (its zoo is the MNIST MLP/CNN only);
+these are the target architectures of the MI355X build plan.
+Standard He et al. layouts; ``stem="cifar"`` uses the 3x3/stride-1 stem
+without max-pool for 32x32 inputs, ``stem="imagenet"`` the 7x7/stride-2 stem
+plus max-pool.  Inputs are uint8 images (the data modules keep datasets as
+uint8 on the device); normalisation to [0, 1] happens in ``forward``.
+
+Activations run channels-last on the GPU (MIOpen NHWC convolutions under
+bf16 autocast); weights stay NCHW views of the flat parameter arena.  Optimiser: SGD with momentum 0.9 and weight decay 5e-4 (fused
+into one arena kernel by the learner), a standard federated CIFAR setup.
+"""
+
+from __future__ import annotations
+
+from typing import List, Optional, Type, Union
+
+import torch
+from torch import nn
+
+from p2pfl_amd.models.base import FLModule, seed_everything
+
+
+class BasicBlock(nn.Module):
+    expansion = 1
+
+    def __init__(self, cin: int, cout: int, stride: int = 1) -> None:
+        super().__init__()
+        self.conv1 = nn.Conv2d(cin, cout, 3, stride, 1, bias=False)
+        self.bn1 = nn.BatchNorm2d(cout)
+        self.conv2 = nn.Conv2d(cout, cout, 3, 1, 1, bias=False)
+        self.bn2 = nn.BatchNorm2d(cout)
+        self.shortcut: nn.Module = nn.Identity()
+        if stride != 1 or cin != cout:
+            self.shortcut = nn.Sequential(nn.Conv2d(cin, cout, 1, stride, bias=False), nn.BatchNorm2d(cout))
+
+    def forward(self, x: torch.Tensor) -> torch.Tensor:
+        out = torch.relu(self.bn1(self.conv1(x)))
+        out = self.bn2(self.conv2(out))
+        return torch.relu(out + self.shortcut(x))
+
+
+class Bottleneck(nn.Module):
+    expansion = 4
+
+    def __init__(self, cin: int, width: int, stride: int = 1) -> None:
+        super().__init__()
+        cout = width * self.expansion
+        self.conv1 = nn.Conv2d(cin, width, 1, bias=False)
+        self.bn1 = nn.BatchNorm2d(width)
+        self.conv2 = nn.Conv2d(width, width, 3, stride, 1, bias=False)
+        self.bn2 = nn.BatchNorm2d(width)
+        self.conv3 = nn.Conv2d(width, cout, 1, bias=False)
+        self.bn3 = nn.BatchNorm2d(cout)
+        self.shortcut: nn.Module = nn.Identity()
+        if stride != 1 or cin != cout:
+            self.shortcut = nn.Sequential(nn.Conv2d(cin, cout, 1, stride, bias=False), nn.BatchNorm2d(cout))
+
+    def forward(self, x: torch.Tensor) -> torch.Tensor:
+        out = torch.relu(self.bn1(self.conv1(x)))
+        out = torch.relu(self.bn2(self.conv2(out)))
+        out = self.bn3(self.conv3(out))
+        return torch.relu(out + self.shortcut(x))
+
+
+class ResNet(FLModule):
+    def __init__(
+        self,
+        block: Type[Union[BasicBlock, Bottleneck]],
+        layers: List[int],
+        num_classes: int = 10,
+        in_channels: int = 3,
+        stem: str = "cifar",
+        lr_rate: float = 0.05,
+        momentum: float = 0.9,
+        weight_decay: float = 5e-4,
+        seed: Optional[int] = None,
+    ) -> None:
+        super().__init__()
+        if seed is not None:
+            seed_everything(seed)
+        self.lr_rate, self.momentum, self.weight_decay = lr_rate, momentum, weight_decay
+        if stem == "cifar":
+            self.stem = nn.Sequential(nn.Conv2d(in_channels, 64, 3, 1, 1, bias=False), nn.BatchNorm2d(64), nn.ReLU(inplace=True))
+        elif stem == "imagenet":
+            self.stem = nn.Sequential(
+                nn.Conv2d(in_channels, 64, 7, 2, 3, bias=False),
+                nn.BatchNorm2d(64),
+                nn.ReLU(inplace=True),
+                nn.MaxPool2d(3, 2, 1),
+            )
+        else:
+            raise ValueError(f"unknown stem {stem!r}")
+        cin = 64
+        stages = []
+        for i, (n, width) in enumerate(zip(layers, (64, 128, 256, 512))):
+            blocks = []
+            for j in range(n):
+                stride = 2 if (i > 0 and j == 0) else 1
+                blocks.append(block(cin, width, stride))
+                cin = width * block.expansion
+            stages.append(nn.Sequential(*blocks))
+        self.layer1, self.layer2, self.layer3, self.layer4 = stages
+        self.fc = nn.Linear(cin, num_classes)
+        for m in self.modules():
+            if isinstance(m, nn.Conv2d):
+                nn.init.kaiming_normal_(m.weight, mode="fan_out", nonlinearity="relu")
+            elif isinstance(m, nn.BatchNorm2d):
+                nn.init.ones_(m.weight)
+                nn.init.zeros_(m.bias)
+
+    def forward(self, x: torch.Tensor) -> torch.Tensor:
+        if x.dtype == torch.uint8:
+            x = x.float().mul_(1.0 / 255.0)
+        if x.is_cuda:
+            x = x.contiguous(memory_format=torch.channels_last)
+        x = self.stem(x)
+        x = self.layer4(self.layer3(self.layer2(self.layer1(x))))
+        x = torch.flatten(nn.functional.adaptive_avg_pool2d(x, 1), 1)
+        return self.fc(x)
+
+    def configure_optimizers(self) -> torch.optim.Optimizer:
+        return torch.optim.SGD(self.parameters(), lr=self.lr_rate, momentum=self.momentum, weight_decay=self.weight_decay)
+
+
+def ResNet18(num_classes: int = 10, stem: str = "cifar", **kw) -> ResNet:
+    return ResNet(BasicBlock, [2, 2, 2, 2], num_classes, stem=stem, **kw)
+
+
+def ResNet34(num_classes: int = 10, stem: str = "cifar", **kw) -> ResNet:
+    return ResNet(BasicBlock, [3, 4, 6, 3], num_classes, stem=stem, **kw)
+
+
+def ResNet50(num_classes: int = 10, stem: str = "cifar", **kw) -> ResNet:
+    return ResNet(Bottleneck, [3, 4, 6, 3], num_classes, stem=stem, **kw)

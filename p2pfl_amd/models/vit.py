@@ -1,0 +1,141 @@
+"""Vision Transformer (ViT-B/16 for BASELINE.json config 4; small variants for tests).
+
+Not in the reference (SURVEY §7.2 target architecture).  Pre-norm encoder
+(Dosovitskiy et al.): 16x16 patch embedding, class token, learned position
+embedding, ``depth`` blocks of LayerNorm -> multi-head self-attention ->
+residual -> LayerNorm -> MLP(GELU) -> residual, final LayerNorm and a linear
+head.  ViT-B/16 at 224x224: 197 tokens, width 768, 12 heads, 12 layers,
+MLP 3072, 86.6 M parameters.
+
+On an AMD GPU with the native extension loaded, the fused ops come from
+:mod:`p2pfl_amd.ops` (hand-written HIP kernels): LayerNorm forward/backward,
+bias+GELU forward/backward and the softmax cross-entropy loss; the plain
+GEMMs are hipBLASLt (``torch.matmul``) and attention uses PyTorch's fused
+SDPA.  Optimiser: AdamW (fused over the arena by the learner).
+"""
+
+from __future__ import annotations
+
+import math
+from typing import Optional
+
+import torch
+from torch import nn
+
+from p2pfl_amd import ops
+from p2pfl_amd.models.base import FLModule, seed_everything
+
+
+def _fused(x: torch.Tensor) -> bool:
+    return x.is_cuda and ops.available()
+
+
+class LayerNorm(nn.LayerNorm):
+    """nn.LayerNorm whose GPU path is the fused HIP kernel."""
+
+    def forward(self, x: torch.Tensor) -> torch.Tensor:
+        if _fused(x):
+            return ops.layer_norm(x, self.weight, self.bias, self.eps)
+        return super().forward(x)
+
+
+class Mlp(nn.Module):
+    def __init__(self, dim: int, hidden: int) -> None:
+        super().__init__()
+        self.fc1 = nn.Linear(dim, hidden)
+        self.fc2 = nn.Linear(hidden, dim)
+
+    def forward(self, x: torch.Tensor) -> torch.Tensor:
+        if _fused(x):
+            h = ops.bias_gelu(torch.matmul(x, self.fc1.weight.t().to(x.dtype)), self.fc1.bias)
+        else:
+            h = nn.functional.gelu(self.fc1(x))
+        return self.fc2(h)
+
+
+class Attention(nn.Module):
+    def __init__(self, dim: int, heads: int) -> None:
+        super().__init__()
+        self.heads = heads
+        self.qkv = nn.Linear(dim, dim * 3)
+        self.proj = nn.Linear(dim, dim)
+
+    def forward(self, x: torch.Tensor) -> torch.Tensor:
+        B, T, C = x.shape
+        qkv = self.qkv(x).view(B, T, 3, self.heads, C // self.heads).permute(2, 0, 3, 1, 4)
+        y = nn.functional.scaled_dot_product_attention(qkv[0], qkv[1], qkv[2])
+        return self.proj(y.transpose(1, 2).reshape(B, T, C))
+
+
+class Block(nn.Module):
+    def __init__(self, dim: int, heads: int, mlp_ratio: float) -> None:
+        super().__init__()
+        self.norm1 = LayerNorm(dim, eps=1e-6)
+        self.attn = Attention(dim, heads)
+        self.norm2 = LayerNorm(dim, eps=1e-6)
+        self.mlp = Mlp(dim, int(dim * mlp_ratio))
+
+    def forward(self, x: torch.Tensor) -> torch.Tensor:
+        x = x + self.attn(self.norm1(x))
+        return x + self.mlp(self.norm2(x))
+
+
+class ViT(FLModule):
+    def __init__(
+        self,
+        img_size: int = 224,
+        patch: int = 16,
+        in_channels: int = 3,
+        num_classes: int = 1000,
+        dim: int = 768,
+        depth: int = 12,
+        heads: int = 12,
+        mlp_ratio: float = 4.0,
+        lr_rate: float = 3e-4,
+        weight_decay: float = 0.05,
+        seed: Optional[int] = None,
+    ) -> None:
+        super().__init__()
+        if seed is not None:
+            seed_everything(seed)
+        self.lr_rate, self.weight_decay = lr_rate, weight_decay
+        self.patch_embed = nn.Conv2d(in_channels, dim, patch, patch)
+        n = (img_size // patch) ** 2
+        self.cls_token = nn.Parameter(torch.zeros(1, 1, dim))
+        self.pos_embed = nn.Parameter(torch.zeros(1, n + 1, dim))
+        self.blocks = nn.Sequential(*[Block(dim, heads, mlp_ratio) for _ in range(depth)])
+        self.norm = LayerNorm(dim, eps=1e-6)
+        self.head = nn.Linear(dim, num_classes)
+        nn.init.trunc_normal_(self.pos_embed, std=0.02)
+        nn.init.trunc_normal_(self.cls_token, std=0.02)
+        for m in self.modules():
+            if isinstance(m, nn.Linear):
+                nn.init.trunc_normal_(m.weight, std=0.02)
+                nn.init.zeros_(m.bias)
+        w = self.patch_embed.weight
+        nn.init.uniform_(w, -1 / math.sqrt(w[0].numel()), 1 / math.sqrt(w[0].numel()))
+
+    def forward(self, x: torch.Tensor) -> torch.Tensor:
+        if x.dtype == torch.uint8:
+            x = x.float().mul_(1.0 / 255.0)
+        x = self.patch_embed(x).flatten(2).transpose(1, 2)
+        x = torch.cat([self.cls_token.expand(x.shape[0], -1, -1).to(x.dtype), x], dim=1) + self.pos_embed.to(x.dtype)
+        x = self.norm(self.blocks(x))
+        return self.head(x[:, 0])
+
+    def loss_fn(self, out: torch.Tensor, y: torch.Tensor) -> torch.Tensor:
+        if _fused(out):
+            return ops.softmax_xent(out, y)
+        return nn.functional.cross_entropy(out, y)
+
+    def configure_optimizers(self) -> torch.optim.Optimizer:
+        return torch.optim.AdamW(self.parameters(), lr=self.lr_rate, weight_decay=self.weight_decay)
+
+
+def ViT_B16(num_classes: int = 1000, img_size: int = 224, **kw) -> ViT:
+    return ViT(img_size=img_size, patch=16, num_classes=num_classes, dim=768, depth=12, heads=12, **kw)
+
+
+def ViT_Tiny(num_classes: int = 10, img_size: int = 32, patch: int = 4, **kw) -> ViT:
+    """Small test variant (CIFAR-sized input)."""
+    return ViT(img_size=img_size, patch=patch, num_classes=num_classes, dim=192, depth=4, heads=3, **kw)

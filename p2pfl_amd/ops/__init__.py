@@ -137,3 +137,16 @@ def sgd_step(p, g, buf, *, lr, momentum=0.0, dampening=0.0, weight_decay=0.0, ne
             p_bf16.copy_(p)
         return
     ext().sgd_step(p, g, buf, p_bf16, float(lr), float(momentum), float(dampening), float(weight_decay), bool(nesterov), bool(first_step))
+
+
+# ----------------------------------------------------------------------------
+# fused transformer / classifier ops (csrc/fused_ops.hip)
+# ----------------------------------------------------------------------------
+from p2pfl_amd.ops.fused import (  # noqa: E402
+    bias_gelu,
+    bias_gelu_reference,
+    layer_norm,
+    layer_norm_reference,
+    softmax_xent,
+    softmax_xent_reference,
+)

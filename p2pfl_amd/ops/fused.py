@@ -1,0 +1,116 @@
+"""Autograd wrappers of the fused transformer / classifier kernels (``csrc/fused_ops.hip``).
+
+``layer_norm``, ``bias_gelu`` and ``softmax_xent`` run the hand-written HIP
+kernels for GPU tensors (bf16 or fp32 activations, fp32 parameters) and plain
+PyTorch otherwise; the ``*_reference`` functions are the fp32 PyTorch
+definitions the numerics tests compare against.
+"""
+
+from __future__ import annotations
+
+import torch
+import torch.nn.functional as F
+
+
+def _native(x: torch.Tensor) -> bool:
+    from p2pfl_amd.ops import _gpu
+
+    return _gpu(x) and x.dtype in (torch.bfloat16, torch.float32)
+
+
+def _fx():
+    from p2pfl_amd.ops import ext
+
+    return ext().fused
+
+
+# -- references ---------------------------------------------------------------
+def layer_norm_reference(x, w, b, eps):
+    return F.layer_norm(x.float(), (x.shape[-1],), w.float(), b.float(), eps)
+
+
+def bias_gelu_reference(x, b):
+    return F.gelu(x.float() + b.float())
+
+
+def softmax_xent_reference(z, y):
+    return F.cross_entropy(z.float(), y)
+
+
+# -- LayerNorm ----------------------------------------------------------------
+class _LayerNorm(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, w, b, eps):
+        shape = x.shape
+        x2 = x.reshape(-1, shape[-1]).contiguous()
+        y, mean, rstd = _fx().ln_fwd(x2, w.contiguous(), b.contiguous(), float(eps))
+        ctx.save_for_backward(x2, w, mean, rstd)
+        ctx.shape = shape
+        return y.view(shape)
+
+    @staticmethod
+    def backward(ctx, dy):
+        x2, w, mean, rstd = ctx.saved_tensors
+        dy2 = dy.reshape(x2.shape).to(x2.dtype).contiguous()
+        dx, dw, db = _fx().ln_bwd(dy2, x2, w.contiguous(), mean, rstd)
+        return dx.view(ctx.shape), dw.to(w.dtype), db.to(w.dtype), None
+
+
+def layer_norm(x: torch.Tensor, weight: torch.Tensor, bias: torch.Tensor, eps: float = 1e-5) -> torch.Tensor:
+    """LayerNorm over the last dim; output dtype = input dtype (statistics in fp32)."""
+    C = x.shape[-1]
+    if (
+        _native(x)
+        and weight is not None
+        and bias is not None
+        and weight.dtype == torch.float32
+        and C % 8 == 0
+        and C <= 2048
+    ):
+        return _LayerNorm.apply(x, weight, bias, eps)
+    return F.layer_norm(x, (C,), weight, bias, eps)
+
+
+# -- bias + GELU ----------------------------------------------------------------
+class _BiasGelu(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, b):
+        xc = x.contiguous()
+        ctx.save_for_backward(xc, b)
+        return _fx().bias_gelu_fwd(xc, b.contiguous())
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, b = ctx.saved_tensors
+        dx, db = _fx().bias_gelu_bwd(dy.to(x.dtype).contiguous(), x, b.contiguous())
+        return dx, db.to(b.dtype)
+
+
+def bias_gelu(x: torch.Tensor, bias: torch.Tensor) -> torch.Tensor:
+    """``gelu(x + bias)`` (exact erf GELU) with bias broadcast over the last dim."""
+    if _native(x) and bias.dtype == torch.float32 and x.shape[-1] % 8 == 0:
+        return _BiasGelu.apply(x, bias)
+    return F.gelu(x + bias.to(x.dtype))
+
+
+# -- softmax cross-entropy --------------------------------------------------------
+class _SoftmaxXent(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, z, y):
+        zc = z.contiguous()
+        loss_rows, lse = _fx().xent_fwd(zc, y.contiguous())
+        ctx.save_for_backward(zc, y, lse)
+        return loss_rows.mean()
+
+    @staticmethod
+    def backward(ctx, g):
+        z, y, lse = ctx.saved_tensors
+        gs = g.detach().float().reshape(1).contiguous()
+        return _fx().xent_bwd(z, y, lse, gs), None
+
+
+def softmax_xent(logits: torch.Tensor, labels: torch.Tensor) -> torch.Tensor:
+    """Mean softmax cross-entropy (= ``F.cross_entropy`` with integer labels), fp32 result."""
+    if _native(logits) and logits.dim() == 2 and labels.dtype == torch.int64 and labels.is_cuda:
+        return _SoftmaxXent.apply(logits, labels)
+    return F.cross_entropy(logits, labels)
