@@ -27,6 +27,12 @@ from p2pfl_amd.learning.arena import FlatParams, ModuleArena
 from p2pfl_amd.learning.torch_learner import TorchLearner
 from p2pfl_amd.management.logger import logger
 
+# Several learners (virtual peers on one GPU, each on its own node thread)
+# may capture epoch graphs concurrently: captures are serialised process-wide
+# and run in thread-local capture mode, so the other peers' kernels and
+# allocations on their own threads stay legal while one peer captures.
+_CAPTURE_LOCK = threading.Lock()
+
 _NAMES = ("conv1.weight", "conv1.bias", "conv2.weight", "conv2.bias", "l1.weight", "l1.bias", "l2.weight", "l2.bias")
 FEAT, HID = 3136, 2048
 
@@ -228,15 +234,16 @@ class FusedCNNLearner(TorchLearner):
             return eg
         # capture on a side stream; state that the graph mutates (weights,
         # Adam moments, step counter) is saved and restored around the capture
-        torch.cuda.synchronize(self.device)
-        saved = [t.clone() for t in (self.engine.params, self.engine.m, self.engine.v, self.engine.adam_t)]
-        graph = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(graph, stream=self._stream):
-            self._enqueue(loader, plan, train, eg.perm, eg.stats)
-        torch.cuda.synchronize(self.device)
-        for dst, src in zip((self.engine.params, self.engine.m, self.engine.v, self.engine.adam_t), saved):
-            dst.copy_(src)
-        self.engine.pack_shadows()
+        with _CAPTURE_LOCK:
+            torch.cuda.synchronize(self.device)
+            saved = [t.clone() for t in (self.engine.params, self.engine.m, self.engine.v, self.engine.adam_t)]
+            graph = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(graph, stream=self._stream, capture_error_mode="thread_local"):
+                self._enqueue(loader, plan, train, eg.perm, eg.stats)
+            torch.cuda.synchronize(self.device)
+            for dst, src in zip((self.engine.params, self.engine.m, self.engine.v, self.engine.adam_t), saved):
+                dst.copy_(src)
+            self.engine.pack_shadows()
         eg.graph = graph
         return eg
 

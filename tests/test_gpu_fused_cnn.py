@@ -170,3 +170,30 @@ def test_fused_and_torch_peers_federate():
         a.stop()
         b.stop()
 
+
+
+def test_three_fused_peers_in_one_process():
+    """Virtual peers on one GPU capture their epoch graphs from concurrent node threads."""
+    from p2pfl_amd.communication.memory import InMemoryCommunicationProtocol
+    from p2pfl_amd.data import MnistFederatedDM
+    from p2pfl_amd.learning.fused_cnn import FusedCNNLearner
+    from p2pfl_amd.node import Node
+    from p2pfl_amd.utils import check_equal_models, wait_4_results, wait_convergence
+
+    nodes = [
+        Node(CNN(seed=i), MnistFederatedDM(sub_id=i, number_sub=60), learner=FusedCNNLearner, protocol=InMemoryCommunicationProtocol)
+        for i in range(3)
+    ]
+    for n in nodes:
+        n.start()
+    try:
+        for n in nodes[1:]:
+            n.connect(nodes[0].addr)
+        wait_convergence(nodes, 2, only_direct=False)
+        nodes[0].set_start_learning(rounds=2, epochs=1)
+        wait_4_results(nodes, timeout=300)
+        check_equal_models(nodes, atol=1e-6)
+        assert nodes[0].state.learner.evaluate()["test_metric"] > 0.8
+    finally:
+        for n in nodes:
+            n.stop()
