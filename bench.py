@@ -227,6 +227,15 @@ def main() -> None:
     fed.barrier()
     elapsed = fed.max_over_ranks(time.perf_counter() - t0)
 
+    if args.impl != "reference" and runner.history:
+        h = runner.history[-args.steps:]
+        k = len(h)
+        print(
+            f"[bench rank {env.rank}] per-round phases (mean of {k}): evaluate {sum(x.eval_s for x in h) / k * 1e3:.2f} ms, "
+            f"fit {sum(x.fit_s for x in h) / k * 1e3:.2f} ms, fedavg+load {sum(x.agg_s for x in h) / k * 1e3:.2f} ms",
+            file=sys.stderr,
+            flush=True,
+        )
     n_train = len(data.train_dataloader().dataset)
     ms_per_round = elapsed / args.steps * 1e3
     per_peer = n_train * args.epochs * args.steps / elapsed

