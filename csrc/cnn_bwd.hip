@@ -340,11 +340,10 @@ void fc1_wgrad_adam(const uint16_t* dH, const uint16_t* a1, int mrows, float* pa
 //    [tap][oc][ic] slab row per image pair.
 // ---------------------------------------------------------------------------
 constexpr int kOCP = 72;                      // LDS pixel pitch of the dC2 window (144 B)
-constexpr int kWinRows = 8;
 
 P2_DEVICE void conv2_wgrad_role(int t, int g, const uint16_t* __restrict__ dc2m, const uint16_t* __restrict__ p1s,
                                 float* __restrict__ wslab, int B) {
-  const int lane = threadIdx.x, r = lane & 31, h = lane >> 5;
+  const int lane = threadIdx.x & 63, r = lane & 31, h = lane >> 5;
   const int ky = t / 5, kx = t % 5;
   const int b0 = g * kWgG, nb = min(kWgG, B - b0);
   // half-image chunks: 7 k-steps (rows) each
@@ -396,31 +395,48 @@ P2_DEVICE void conv2_wgrad_role(int t, int g, const uint16_t* __restrict__ dc2m,
   }
 }
 
-P2_DEVICE void conv2_dgrad_role(int tile, int b, const uint16_t* __restrict__ dc2m, const uint8_t* __restrict__ am1,
-                                const uint16_t* __restrict__ w2q, const uint8_t* __restrict__ xds,
-                                const int64_t* __restrict__ idx, float* __restrict__ wslab1, uint16_t* win,
-                                float (*xs)[33]) {
-  const int lane = threadIdx.x, r = lane & 31, h = lane >> 5;
+// dgrad block: 4 waves = 4 consecutive 32-position tiles of one image
+// (group 0: tiles 0-3 = conv rows 0..9, group 1: tiles 4-6 = rows 9..13; the
+// 4th wave of group 1 only helps staging).  The block stages, in one memory
+// round trip, the whole W2q weight copy (32 ic rows x 25 taps x 64 oc, padded
+// rows) and the group's zero-padded HWC window of the dC2 map into LDS, so
+// every MFMA operand of the 100 k-steps is a 16-B LDS read.
+constexpr int kW2qRow = kTaps * kC2 + 8;                 // 1608 elements per ic row (pad breaks bank aliasing)
+constexpr int kDgW = kC1 * kW2qRow * 2;                  // 102912 B
+constexpr int kDgWinRows = 14;                           // padded rows of a group's window
+constexpr int kDgWin = kDgWinRows * 18 * kOCP * 2;       // 36288 B
+constexpr int kDgXs = 32 * 33 * 4;                       // 4224 B
+constexpr int kDgLds = kDgW + kDgWin + kDgXs;            // 143424 B (one dgrad block per CU)
+
+P2_DEVICE void conv2_dgrad_block(int grp, int b, const uint16_t* __restrict__ dc2m, const uint8_t* __restrict__ am1,
+                                 const uint16_t* __restrict__ w2q, const uint8_t* __restrict__ xds,
+                                 const int64_t* __restrict__ idx, float* __restrict__ wslab1, char* smem) {
+  uint16_t* sw = reinterpret_cast<uint16_t*>(smem);
+  uint16_t* win = reinterpret_cast<uint16_t*>(smem + kDgW);
+  float(*xs)[33] = reinterpret_cast<float(*)[33]>(smem + kDgW + kDgWin);
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, r = lane & 31, h = lane >> 5;
+  const int tile = grp * 4 + wave;
+  const bool active = tile < kDgTiles;
+  const int ylo = grp ? (4 * 32) / 14 : 0;  // first padded window row of the group
   const int m = tile * 32 + r, mc = m < 196 ? m : 195;
   const int y = mc / 14, x = mc % 14;
-  const int ylo = (tile * 32) / 14;  // first padded window row
-  const uint16_t* bbase = w2q + size_t(r) * kTaps * kC2 + 8 * h;
-  auto loadb = [&](int c, uint4 (&Bv)[10]) {
+  // ---- issue every load.  W2q goes global -> LDS directly (no VGPRs): each
+  // ic row (1600 elements = 3200 B) is 4 wave instructions of 50 lanes x 16 B,
+  // so no instruction crosses the 16-B row padding; 32 instructions per wave.
+#pragma unroll 4
+  for (int k = 0; k < 32; ++k) {
+    const int id = wave * 32 + k, ic = id >> 2, q = id & 3;
+    if (lane < 50)
+      __builtin_amdgcn_global_load_lds(
+          (const __attribute__((address_space(1))) void*)(w2q + ic * (kTaps * kC2) + q * 400 + lane * 8),
+          (__attribute__((address_space(3))) void*)(sw + ic * kW2qRow + q * 400), 16, 0, 0);
+  }
+  // the window (4 items of two channels x 8 columns), this lane's pool1
+  // argmax codes and the image go through registers
+  uint4 wu0[4], wu1[4];
 #pragma unroll
-    for (int j = 0; j < 10; ++j) {
-      const int s = c * 10 + j, t = s >> 2, oc0 = (s & 3) * 16;
-      Bv[j] = *reinterpret_cast<const uint4*>(bbase + t * kC2 + oc0);
-    }
-  };
-  uint4 B0[10], B1[10];
-  loadb(0, B0);
-  // Issue every independent load before any wait: the window of the dC2 map
-  // (8 items per lane, two channels x 8 columns each), the pool1 argmax codes
-  // of this lane's 16 positions, and the idx -> image gather.
-  uint4 wu0[8], wu1[8];
-#pragma unroll
-  for (int it = 0; it < 8; ++it) {
-    const int i = lane + 64 * it;
+  for (int it = 0; it < 4; ++it) {
+    const int i = tid + 256 * it;  // 14 rows x 32 channel pairs x 2 chunks = 896 items
     const int wr = i >> 6, pr = (i >> 1) & 31, c = i & 1, yd = ylo + wr - 2;
     const int ydc = yd < 0 ? 0 : (yd > 13 ? 13 : yd);
     const uint16_t* src = dc2m + (size_t(b) * kC2 + 2 * pr) * 224 + ydc * 16 + c * 8;
@@ -431,14 +447,13 @@ P2_DEVICE void conv2_dgrad_role(int tile, int b, const uint16_t* __restrict__ dc
 #pragma unroll
   for (int i = 0; i < 16; ++i) {
     const int pos = tile * 32 + acc_row_b(i, h);
-    acode[i] = pos < 196 ? am1[(size_t(b) * 196 + pos) * kC1 + r] : uint8_t(4);
+    acode[i] = (active && pos < 196) ? am1[(size_t(b) * 196 + pos) * kC1 + r] : uint8_t(4);
   }
   const int64_t row = idx ? idx[b] : b;
   const uint8_t* xsrc = xds + row * (kImg * kImg);
-  // zero the window (padding rows / columns stay zero), stage the image
   const uint4 z4 = make_uint4(0, 0, 0, 0);
-  for (int i = lane; i < kWinRows * 18 * kOCP / 8; i += 64) reinterpret_cast<uint4*>(win)[i] = z4;
-  for (int i = lane; i < 32 * 32; i += 64) {
+  for (int i = tid; i < kDgWin / 16; i += 256) reinterpret_cast<uint4*>(win)[i] = z4;
+  for (int i = tid; i < 32 * 32; i += 256) {
     const int yy = i >> 5, xx = i & 31, sy = yy - 2, sx = xx - 2;
     float v = 0.f;
     if (sy >= 0 && sy < kImg && sx >= 0 && sx < kImg) v = float(xsrc[sy * kImg + sx]) * (1.f / 255.f);
@@ -446,10 +461,10 @@ P2_DEVICE void conv2_dgrad_role(int tile, int b, const uint16_t* __restrict__ dc
   }
   __syncthreads();
 #pragma unroll
-  for (int it = 0; it < 8; ++it) {
-    const int i = lane + 64 * it;
+  for (int it = 0; it < 4; ++it) {
+    const int i = tid + 256 * it;
     const int wr = i >> 6, pr = (i >> 1) & 31, c = i & 1, yd = ylo + wr - 2;
-    if (yd < 0 || yd > 13) continue;
+    if (i >= kDgWinRows * 64 || yd < 0 || yd > 13) continue;
     const uint16_t* e0 = reinterpret_cast<const uint16_t*>(&wu0[it]);
     const uint16_t* e1 = reinterpret_cast<const uint16_t*>(&wu1[it]);
     uint16_t* dst = win + (wr * 18 + c * 8 + 2) * kOCP + 2 * pr;
@@ -457,29 +472,19 @@ P2_DEVICE void conv2_dgrad_role(int tile, int b, const uint16_t* __restrict__ dc
     for (int j = 0; j < 8; ++j) *reinterpret_cast<uint32_t*>(dst + j * kOCP) = uint32_t(e0[j]) | (uint32_t(e1[j]) << 16);
   }
   __syncthreads();
+  if (!active) return;
+  // ---- phase 1: C[pos][ic], 100 k-steps, both operands from LDS
   const uint16_t* abase = win + ((y - ylo) * 18 + x) * kOCP + 8 * h;
+  const uint16_t* bbase = sw + r * kW2qRow + 8 * h;
   f32x16 acc = {};
-#pragma unroll
-  for (int c = 0; c < 10; c += 2) {
-    loadb(c + 1, B1);
-    __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-    for (int j = 0; j < 10; ++j) {
-      const int s = c * 10 + j, t = s >> 2, ky = t / 5, kx = t % 5, oc0 = (s & 3) * 16;
-      const uint4 a = *reinterpret_cast<const uint4*>(abase + ((4 - ky) * 18 + (4 - kx)) * kOCP + oc0);
-      acc = mfma32b(a, B0[j], acc);
-    }
-    __builtin_amdgcn_sched_barrier(0);
-    if (c + 2 < 10) loadb(c + 2, B0);
-    __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-    for (int j = 0; j < 10; ++j) {
-      const int s = (c + 1) * 10 + j, t = s >> 2, ky = t / 5, kx = t % 5, oc0 = (s & 3) * 16;
-      const uint4 a = *reinterpret_cast<const uint4*>(abase + ((4 - ky) * 18 + (4 - kx)) * kOCP + oc0);
-      acc = mfma32b(a, B1[j], acc);
-    }
-    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll 4
+  for (int s = 0; s < 100; ++s) {
+    const int t = s >> 2, ky = t / 5, kx = t % 5, oc0 = (s & 3) * 16;
+    const uint4 a = *reinterpret_cast<const uint4*>(abase + ((4 - ky) * 18 + (4 - kx)) * kOCP + oc0);
+    const uint4 bq = *reinterpret_cast<const uint4*>(bbase + t * kC2 + oc0);
+    acc = mfma32b(a, bq, acc);
   }
+  // ---- phase 2: sparse conv1 weight gradient at each pool1 argmax pixel
   float wg[kTaps];
 #pragma unroll
   for (int t = 0; t < kTaps; ++t) wg[t] = 0.f;
@@ -487,17 +492,15 @@ P2_DEVICE void conv2_dgrad_role(int tile, int b, const uint16_t* __restrict__ dc
 #pragma unroll
   for (int i = 0; i < 16; ++i) {
     const int pos = tile * 32 + acc_row_b(i, h);
-    if (pos < 196) {
-      const uint8_t a = acode[i];
-      if (a < 4) {
-        const int yy = 2 * (pos / 14) + (a >> 1), xx = 2 * (pos % 14) + (a & 1);
-        const float gv = acc[i];
-        bs += gv;
+    const uint8_t a = acode[i];
+    if (pos < 196 && a < 4) {
+      const int yy = 2 * (pos / 14) + (a >> 1), xx = 2 * (pos % 14) + (a & 1);
+      const float gv = acc[i];
+      bs += gv;
 #pragma unroll
-        for (int ky = 0; ky < 5; ++ky)
+      for (int ky = 0; ky < 5; ++ky)
 #pragma unroll
-          for (int kx = 0; kx < 5; ++kx) wg[ky * 5 + kx] = fmaf(gv, xs[yy + ky][xx + kx], wg[ky * 5 + kx]);
-      }
+        for (int kx = 0; kx < 5; ++kx) wg[ky * 5 + kx] = fmaf(gv, xs[yy + ky][xx + kx], wg[ky * 5 + kx]);
     }
   }
 #pragma unroll
@@ -511,29 +514,30 @@ P2_DEVICE void conv2_dgrad_role(int tile, int b, const uint16_t* __restrict__ dc
   }
 }
 
-__global__ __launch_bounds__(64) void conv2_bwd_kernel(const uint16_t* __restrict__ dc2m,
-                                                       const uint16_t* __restrict__ p1s,
-                                                       const uint8_t* __restrict__ am1,
-                                                       const uint16_t* __restrict__ w2q,
-                                                       const uint8_t* __restrict__ xds,
-                                                       const int64_t* __restrict__ idx, float* __restrict__ wslab1,
-                                                       float* __restrict__ wslab2, int B) {
-  __shared__ __attribute__((aligned(16))) uint16_t win[kWinRows * 18 * kOCP];
-  __shared__ float xs[32][33];
-  const int nd = B * kDgTiles;
-  const int j = blockIdx.x;
+// 256-thread blocks: [0, 2B) dgrad blocks (image b = j / 2, group j % 2),
+// then wgrad blocks of 4 independent (tap, image pair) waves.
+__global__ __launch_bounds__(256) void conv2_bwd_kernel(const uint16_t* __restrict__ dc2m,
+                                                        const uint16_t* __restrict__ p1s,
+                                                        const uint8_t* __restrict__ am1,
+                                                        const uint16_t* __restrict__ w2q,
+                                                        const uint8_t* __restrict__ xds,
+                                                        const int64_t* __restrict__ idx, float* __restrict__ wslab1,
+                                                        float* __restrict__ wslab2, int B) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int j = blockIdx.x, nd = 2 * B;
   if (j < nd) {
-    conv2_dgrad_role(j % kDgTiles, j / kDgTiles, dc2m, am1, w2q, xds, idx, wslab1, win, xs);
+    conv2_dgrad_block(j & 1, j >> 1, dc2m, am1, w2q, xds, idx, wslab1, smem);
   } else {
-    const int k = j - nd;
-    conv2_wgrad_role(k % kTaps, k / kTaps, dc2m, p1s, wslab2, B);
+    const int k = (j - nd) * 4 + (threadIdx.x >> 6);
+    if (k < kTaps * wgrad_groups(B)) conv2_wgrad_role(k % kTaps, k / kTaps, dc2m, p1s, wslab2, B);
   }
 }
 
 void conv2_bwd(const uint16_t* dc2m, const uint16_t* p1s, const uint8_t* am1, const uint16_t* w2q, const uint8_t* x,
                const int64_t* idx, float* wslab1, float* wslab2, int B, hipStream_t s) {
-  const int blocks = B * kDgTiles + kTaps * wgrad_groups(B);
-  hipLaunchKernelGGL(conv2_bwd_kernel, dim3(blocks), dim3(64), 0, s, dc2m, p1s, am1, w2q, x, idx, wslab1, wslab2, B);
+  const int blocks = 2 * B + (kTaps * wgrad_groups(B) + 3) / 4;
+  hipLaunchKernelGGL(conv2_bwd_kernel, dim3(blocks), dim3(256), kDgLds, s, dc2m, p1s, am1, w2q, x, idx, wslab1, wslab2,
+                     B);
 }
 
 // ---------------------------------------------------------------------------
@@ -684,6 +688,10 @@ void init_fwd_attributes();
 
 // Raise the dynamic-LDS limit of the kernels that stage > 64 KB.  Called once
 // (from the bindings) before any HIP-graph capture.
-void init_attributes() { init_fwd_attributes(); }
+void init_attributes() {
+  init_fwd_attributes();
+  P2_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(conv2_bwd_kernel),
+                               hipFuncAttributeMaxDynamicSharedMemorySize, kDgLds));
+}
 
 }  // namespace p2cnn
