@@ -9,6 +9,7 @@ IDX files.  Metrics are printed as a table (no plotting dependency).
 from __future__ import annotations
 
 import argparse
+import os
 import time
 from typing import List
 
@@ -36,7 +37,18 @@ def parse_args(argv=None) -> argparse.Namespace:
     p.add_argument("--batch", type=int, default=32)
     p.add_argument("--device", default=None, help="cpu / cuda / cuda:N (default: GPU if present)")
     p.add_argument("--fast", action="store_true", help="shrink gossip/heartbeat periods (test settings)")
-    return p.parse_args(argv)
+    # reference flag names (p2pfl/examples/mnist.py:44-66)
+    p.add_argument("--use_unix_socket", action="store_true", help="gRPC over unix domain sockets")
+    p.add_argument("--use_local_protocol", action="store_true", help="in-memory transport (= --protocol memory)")
+    p.add_argument("--token", type=str, default="", help="API token for the web logger (http://localhost:3000)")
+    args = p.parse_args(argv)
+    if args.use_unix_socket and args.use_local_protocol:
+        p.error("Cannot use the unix socket and the local protocol at the same time.")
+    if args.use_local_protocol:
+        args.protocol = "memory"
+    if args.use_unix_socket:
+        args.protocol = "grpc"
+    return args
 
 
 def _print_metrics() -> None:
@@ -51,7 +63,7 @@ def _print_metrics() -> None:
 
 def mnist(n: int, r: int, e: int, show_metrics: bool = True, measure_time: bool = False, model: str = "mlp",
           protocol: str = "memory", partition: str = "iid", alpha: float = 0.5, batch: int = 32,
-          device=None) -> List[Node]:
+          device=None, use_unix_socket: bool = False) -> List[Node]:
     start = time.time()
     proto = InMemoryCommunicationProtocol if protocol == "memory" else GrpcCommunicationProtocol
     nodes: List[Node] = []
@@ -59,7 +71,8 @@ def mnist(n: int, r: int, e: int, show_metrics: bool = True, measure_time: bool 
         net = MLP() if model == "mlp" else CNN()
         data = MnistFederatedDM(sub_id=i, number_sub=n, batch_size=batch, partitioner=partition, alpha=alpha)
         kw = {"device": device} if device else {}
-        node = Node(net, data, protocol=proto, **kw)
+        addr = f"unix:///tmp/p2pfl_amd-{os.getpid()}-{i}.sock" if use_unix_socket else "127.0.0.1"
+        node = Node(net, data, address=addr, protocol=proto, **kw)
         node.start()
         nodes.append(node)
     try:
@@ -80,6 +93,8 @@ def mnist(n: int, r: int, e: int, show_metrics: bool = True, measure_time: bool 
 
 def main(argv=None) -> None:
     args = parse_args(argv)
+    if args.token:
+        logger.connect_web("http://localhost:3000/api/v1", args.token)
     if args.fast:
         from p2pfl_amd.utils import set_test_settings
 
@@ -87,7 +102,7 @@ def main(argv=None) -> None:
     else:
         Settings.LOG_LEVEL = "INFO"
     mnist(args.nodes, args.rounds, args.epochs, args.show_metrics, args.measure_time, args.model, args.protocol,
-          args.partition, args.alpha, args.batch, args.device)
+          args.partition, args.alpha, args.batch, args.device, args.use_unix_socket)
 
 
 if __name__ == "__main__":
