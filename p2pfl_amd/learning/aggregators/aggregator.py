@@ -48,6 +48,8 @@ class Aggregator:
         self._done = threading.Event()
         self._running = False
         self._partial_cache: Dict[frozenset, Tuple[Any, List[str], int]] = {}
+        # train-set members that left the network mid-round (see mark_lost)
+        self._lost: set = set()
 
     # ------------------------------------------------------------------
     # strategy
@@ -63,6 +65,7 @@ class Aggregator:
             if self._running:
                 raise Exception("It is not possible to set nodes to aggregate when the aggregation is running.")
             self._train_set = list(nodes_to_aggregate)
+            self._lost = set()
             self._running = True
             self._done.clear()
 
@@ -78,6 +81,7 @@ class Aggregator:
             self._partial_cache = {}
             self._waiting_aggregated_model = False
             self._running = False
+            self._lost = set()
             self._done.set()
 
     # ------------------------------------------------------------------
@@ -95,19 +99,48 @@ class Aggregator:
         have = set(self.get_aggregated_models())
         return [n for n in self._train_set if n not in have]
 
+    # ------------------------------------------------------------------
+    # membership changes (new: the reference waits for a dead train-set
+    # member until AGGREGATION_TIMEOUT -- 300 s by default -- and non-members
+    # then reject the trainers' aggregate because it lacks that member)
+    # ------------------------------------------------------------------
+    def mark_lost(self, nodes: List[str]) -> None:
+        """Train-set members that left the network: stop waiting for them."""
+        with self._lock:
+            if not self._running:
+                return
+            new = (set(nodes) & set(self._train_set)) - self._lost
+            if not new:
+                return
+            self._lost |= new
+            logger.info(self.node_name, f"Train-set members lost: {sorted(new)}; aggregating without them")
+            if self._complete_locked():
+                self._done.set()
+
+    def _complete_locked(self) -> bool:
+        if self._waiting_aggregated_model:
+            return bool(self._models)
+        have = set(self.get_aggregated_models())
+        return all(n in have or n in self._lost for n in self._train_set)
+
+    def _full_aggregate_locked(self, contributors: List[str]) -> bool:
+        """A diffused model is final if it covers every live train-set member."""
+        c = set(contributors)
+        return c <= set(self._train_set) and (set(self._train_set) - self._lost) <= c
+
     def would_accept(self, contributors: List[str]) -> bool:
         """Pure version of :meth:`add_model`'s acceptance test."""
         if not contributors:
             return False
         with self._lock:
             if self._waiting_aggregated_model and not self._models:
-                return set(contributors) == set(self._train_set)
+                return self._full_aggregate_locked(contributors)
             aggregated = self.get_aggregated_models()
-            if len(self._train_set) <= len(aggregated):
+            if self._complete_locked():
                 return False
             if not all(n in self._train_set for n in contributors):
                 return False
-            if len(contributors) == len(self._train_set):
+            if len(contributors) == len(self._train_set) or self._full_aggregate_locked(contributors):
                 return True
             return all(n not in aggregated for n in contributors)
 
@@ -121,7 +154,7 @@ class Aggregator:
             return []
         with self._lock:
             if self._waiting_aggregated_model and not self._models:
-                if set(nodes) == set(self._train_set):
+                if self._full_aggregate_locked(nodes):
                     logger.info(self.node_name, "Received an aggregated model.")
                     self._models = {" ".join(nodes): (model, 1)}
                     self._partial_cache = {}
@@ -130,13 +163,14 @@ class Aggregator:
                     return nodes
                 return []
             aggregated = self.get_aggregated_models()
-            if len(self._train_set) <= len(aggregated):
+            if self._complete_locked():
                 logger.debug(self.node_name, "Received a model when is not needed.")
                 return []
             if not all(n in self._train_set for n in nodes):
                 logger.debug(self.node_name, f"Can't add a model from a node ({nodes}) that is not in the training set.")
                 return []
-            if len(nodes) == len(self._train_set):
+            if len(nodes) == len(self._train_set) or self._full_aggregate_locked(nodes):
+                # a full aggregate (of every live member) supersedes the partials
                 self._models = {" ".join(nodes): (model, weight)}
             elif all(n not in aggregated for n in nodes):
                 self._models[" ".join(nodes)] = (model, weight)
@@ -145,8 +179,9 @@ class Aggregator:
                 return []
             self._partial_cache = {}
             now = self.get_aggregated_models()
+            self._lost -= set(nodes)  # a "lost" member whose model still arrived
             logger.info(self.node_name, f"Model added ({len(now)}/{len(self._train_set)}) from {nodes}")
-            if len(now) >= len(self._train_set):
+            if self._complete_locked():
                 self._done.set()
             return now
 

@@ -93,10 +93,20 @@ class Node:
                 AddModelCommand(self.state, self.stop, self.aggregator, self._communication_protocol),
             ]
         )
-        # neighbour changes wake event-driven gossip loops
+        # neighbour changes wake event-driven gossip loops and tell the
+        # aggregator about train-set members that left the network
         listener = getattr(self._communication_protocol, "add_neighbor_listener", None)
         if listener is not None:
-            listener(self.state.changed.bump)
+            listener(self._on_neighbors_changed)
+
+    def _on_neighbors_changed(self) -> None:
+        self.state.changed.bump()
+        train_set = self.aggregator.train_set
+        if train_set and self._running:
+            live = set(self._communication_protocol.get_neighbors(only_direct=False)) | {self.addr}
+            lost = [n for n in train_set if n not in live]
+            if lost:
+                self.aggregator.mark_lost(lost)
 
     # ------------------------------------------------------------------
     # neighbourhood

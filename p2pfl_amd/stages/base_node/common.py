@@ -28,3 +28,18 @@ def evaluate_and_share(state: Any, protocol: Any) -> Dict[str, float]:
         flat = [str(x) for kv in results.items() for x in kv]
         protocol.broadcast(protocol.build_msg(MetricsCommand.get_name(), flat, round=state.round))
     return results
+
+
+def mark_dead_train_set_members(state: Any, protocol: Any, aggregator: Any) -> None:
+    """Tell the aggregator which train-set members are no longer in the neighbour table.
+
+    The train set is voted once per experiment (reference
+    ``round_finished_stage.py:69-70``), so a member that died in an earlier
+    round is still expected in later ones; without this every later round
+    would wait ``AGGREGATION_TIMEOUT`` for it.  A "lost" member whose model
+    still arrives is accepted (the aggregator un-marks it).
+    """
+    live = set(protocol.get_neighbors(only_direct=False)) | {state.addr}
+    lost = [n for n in state.train_set if n not in live]
+    if lost:
+        aggregator.mark_lost(lost)

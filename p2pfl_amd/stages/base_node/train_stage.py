@@ -14,7 +14,7 @@ from typing import Any, List, Optional, Type
 from p2pfl_amd.commands.add_model_command import AddModelCommand
 from p2pfl_amd.commands.models_agregated_command import ModelsAggregatedCommand
 from p2pfl_amd.management.logger import logger
-from p2pfl_amd.stages.base_node.common import evaluate_and_share, model_payload
+from p2pfl_amd.stages.base_node.common import evaluate_and_share, model_payload, mark_dead_train_set_members
 from p2pfl_amd.stages.stage import Stage
 from p2pfl_amd.stages.stage_factory import StageFactory
 
@@ -38,6 +38,7 @@ class TrainStage(Stage):
             return StageFactory.get_stage("WaitAggregatedModelsStage")
         if not early_stopping_fn():
             aggregator.set_nodes_to_aggregate(state.train_set)
+            mark_dead_train_set_members(state, communication_protocol, aggregator)
         if not early_stopping_fn():
             evaluate_and_share(state, communication_protocol)
         if not early_stopping_fn():
@@ -60,8 +61,19 @@ class TrainStage(Stage):
             return state.models_aggregated.get(n, [])
 
         def candidates() -> List[str]:
+            # A train-set peer is a candidate while it lacks some of the models
+            # this node holds (per its models_aggregated reports).  The
+            # reference (train_stage.py:134-139) used "its model is not in my
+            # aggregate", which stops pushing as soon as the peer's model
+            # arrived here even if the peer never received this node's model
+            # (its own comment flags the hazard): on a partial topology that
+            # leaves peers waiting for AGGREGATION_TIMEOUT.
             have = set(aggregator.get_aggregated_models())
-            return [n for n in protocol.get_neighbors(only_direct=False) if n not in have and n in state.train_set]
+            return [
+                n
+                for n in protocol.get_neighbors(only_direct=False)
+                if n in state.train_set and n != state.addr and (have - set(peer_has(n)))
+            ]
 
         def status() -> Any:
             return [(n, peer_has(n)) for n in protocol.get_neighbors(only_direct=False) if n in state.train_set]

@@ -213,3 +213,42 @@ def test_learner_fit_evaluate_cpu():
         logger.unregister_node("learner-test")
     assert after["test_loss"] < before["test_loss"]
     assert after["test_metric"] > 0.3
+
+
+def test_aggregator_lost_members():
+    """A train-set member that leaves mid-round stops being waited for (trainer and waiting node)."""
+    import torch
+
+    from p2pfl_amd.learning.aggregators import FedAvg
+
+    t = lambda v: {"w": torch.full((4,), float(v))}  # noqa: E731
+    agg = FedAvg("a")
+    agg.set_nodes_to_aggregate(["a", "b", "c"])
+    agg.add_model(t(1), ["a"], 1)
+    agg.add_model(t(3), ["b"], 1)
+    assert not agg._done.is_set()
+    agg.mark_lost(["c"])
+    assert agg._done.is_set()
+    out = agg.wait_and_get_aggregation(timeout=0.1)
+    assert torch.allclose(out["w"], torch.full((4,), 2.0))
+    # an aggregate of every live member supersedes overlapping partials
+    agg.clear()
+    agg.set_nodes_to_aggregate(["a", "b", "c", "d"])
+    agg.mark_lost(["d"])
+    agg.add_model(t(1), ["a"], 1)
+    assert agg.would_accept(["a", "b", "c"])
+    assert agg.add_model(t(5), ["a", "b", "c"], 3)
+    assert agg._done.is_set()
+    # a waiting (non-trainer) node accepts the aggregate of the live members
+    w = FedAvg("w")
+    w.set_waiting_aggregated_model(["a", "b", "c"])
+    assert not w.would_accept(["a", "b"])
+    w.mark_lost(["c"])
+    assert w.would_accept(["a", "b"]) and w.add_model(t(7), ["a", "b"], 1)
+    assert torch.equal(w.wait_and_get_aggregation(timeout=0.1)["w"], t(7)["w"])
+    # a "lost" member whose model still arrives is accepted and un-marked
+    x = FedAvg("x")
+    x.set_nodes_to_aggregate(["a", "b", "c"])
+    x.mark_lost(["c"])
+    x.add_model(t(1), ["c"], 1)
+    assert "c" in x.get_aggregated_models() and not x._lost
