@@ -186,18 +186,38 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const T* __restrict__ dy, c
 }
 
 // out[c] = sum_r part[r][c] (fixed order), for one or two partial arrays.
+// Block = 64 columns x 4 row phases; each thread keeps 8 independent loads in
+// flight, the 4 phase partials are combined in LDS in fixed order.
 __global__ __launch_bounds__(256) void col_reduce_kernel(const float* __restrict__ a, float* __restrict__ oa,
                                                          const float* __restrict__ b, float* __restrict__ ob, int R,
                                                          int C) {
-  const int c = blockIdx.x * 256 + threadIdx.x;
-  if (c >= C) return;
+  __shared__ float red[2][4][64];
+  const int lane = threadIdx.x & 63, q = threadIdx.x >> 6;
+  const int c = blockIdx.x * 64 + lane;
   float sa = 0.f, sb = 0.f;
-  for (int r = 0; r < R; ++r) {
-    sa += a[size_t(r) * C + c];
-    if (b) sb += b[size_t(r) * C + c];
+  if (c < C) {
+    for (int r0 = q; r0 < R; r0 += 4 * 8) {
+      float ta[8], tb[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const int r = r0 + 4 * u;
+        ta[u] = r < R ? a[size_t(r) * C + c] : 0.f;
+        tb[u] = (b && r < R) ? b[size_t(r) * C + c] : 0.f;
+      }
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        sa += ta[u];
+        sb += tb[u];
+      }
+    }
   }
-  oa[c] = sa;
-  if (b) ob[c] = sb;
+  red[0][q][lane] = sa;
+  red[1][q][lane] = sb;
+  __syncthreads();
+  if (q == 0 && c < C) {
+    oa[c] = (red[0][0][lane] + red[0][1][lane]) + (red[0][2][lane] + red[0][3][lane]);
+    if (b) ob[c] = (red[1][0][lane] + red[1][1][lane]) + (red[1][2][lane] + red[1][3][lane]);
+  }
 }
 
 // ---------------------------------------------------------------------------
@@ -348,8 +368,8 @@ void layer_norm_fwd(bool bf16, const void* x, const float* w, const float* b, vo
 }
 
 int layer_norm_bwd_blocks(int N) {
-  int g = (N + 15) / 16;  // >= 4 rows per wave
-  return g > 512 ? 512 : (g < 1 ? 1 : g);
+  int g = (N + 63) / 64;  // >= 16 rows per wave keeps the partial count small
+  return g > 256 ? 256 : (g < 1 ? 1 : g);
 }
 
 template <typename T>
@@ -365,7 +385,7 @@ static void ln_bwd_t(const void* dy, const void* x, const float* w, const float*
     hipLaunchKernelGGL((ln_bwd_kernel<T, 1>), grid, blk, lds, s, dyp, xp, w, mean, rstd, dxp, pdw, pdb, N, C);
   else
     hipLaunchKernelGGL((ln_bwd_kernel<T, 4>), grid, blk, lds, s, dyp, xp, w, mean, rstd, dxp, pdw, pdb, N, C);
-  hipLaunchKernelGGL(col_reduce_kernel, dim3((C + 255) / 256), blk, 0, s, pdw, dw, pdb, db, G, C);
+  hipLaunchKernelGGL(col_reduce_kernel, dim3((C + 63) / 64), blk, 0, s, pdw, dw, pdb, db, G, C);
 }
 
 void layer_norm_bwd(bool bf16, const void* dy, const void* x, const float* w, const float* mean, const float* rstd,
@@ -402,7 +422,7 @@ void bias_gelu_bwd(bool bf16, const void* dy, const void* x, const float* b, voi
   else
     hipLaunchKernelGGL(bias_gelu_bwd_kernel<float>, grid, blk, 0, s, static_cast<const float*>(dy),
                        static_cast<const float*>(x), b, static_cast<float*>(dx), pdb, N, H);
-  hipLaunchKernelGGL(col_reduce_kernel, dim3((H + 255) / 256), blk, 0, s, pdb, db, nullptr, nullptr, S, H);
+  hipLaunchKernelGGL(col_reduce_kernel, dim3((H + 63) / 64), blk, 0, s, pdb, db, nullptr, nullptr, S, H);
 }
 
 void xent_fwd(bool bf16, const void* z, const int64_t* y, float* loss, float* lse, int N, int K, hipStream_t s) {

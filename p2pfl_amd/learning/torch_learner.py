@@ -58,6 +58,11 @@ class TorchLearner(NodeLearner):
         self._addr = self_addr
         self.epochs = epochs
         self.device = torch.device(device) if device is not None else default_device()
+        if self.device.type == "cuda":
+            # MIOpen "find" mode: benchmark the solvers once per conv shape.
+            # Without it several ResNet shapes fall back to MIOpen's naive
+            # kernels (77 % of a ResNet-18 round on MI355X).
+            torch.backends.cudnn.benchmark = True
         self.precision = precision or ("bf16" if self.device.type == "cuda" else "fp32")
         self.log_every_n_steps = log_every_n_steps
         self.fused_optimizer = fused_optimizer

@@ -14,12 +14,16 @@ into one arena kernel by the learner), a standard federated CIFAR setup.
 
 from __future__ import annotations
 
+import os
 from typing import List, Optional, Type, Union
 
 import torch
 from torch import nn
 
 from p2pfl_amd.models.base import FLModule, seed_everything
+
+# NHWC activations on the GPU (P2PFL_CHANNELS_LAST=0 keeps NCHW)
+_CHANNELS_LAST = os.environ.get("P2PFL_CHANNELS_LAST", "1") != "0"
 
 
 class BasicBlock(nn.Module):
@@ -113,7 +117,7 @@ class ResNet(FLModule):
     def forward(self, x: torch.Tensor) -> torch.Tensor:
         if x.dtype == torch.uint8:
             x = x.float().mul_(1.0 / 255.0)
-        if x.is_cuda:
+        if x.is_cuda and _CHANNELS_LAST:
             x = x.contiguous(memory_format=torch.channels_last)
         x = self.stem(x)
         x = self.layer4(self.layer3(self.layer2(self.layer1(x))))

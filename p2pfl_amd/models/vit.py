@@ -118,10 +118,24 @@ class ViT(FLModule):
     def forward(self, x: torch.Tensor) -> torch.Tensor:
         if x.dtype == torch.uint8:
             x = x.float().mul_(1.0 / 255.0)
-        x = self.patch_embed(x).flatten(2).transpose(1, 2)
+        x = self._patchify_embed(x)
         x = torch.cat([self.cls_token.expand(x.shape[0], -1, -1).to(x.dtype), x], dim=1) + self.pos_embed.to(x.dtype)
         x = self.norm(self.blocks(x))
         return self.head(x[:, 0])
+
+    def _patchify_embed(self, x: torch.Tensor) -> torch.Tensor:
+        """Conv2d(C, D, P, stride=P) as patchify + one GEMM (identical math).
+
+        MIOpen has no tuned solver for the 16x16 / stride-16 convolution and
+        falls back to its naive kernel (measured 2.8 ms per call on MI355X at
+        batch 32); as [B*196, C*P*P] x [C*P*P, D] it is a plain hipBLASLt GEMM.
+        The conv weight [D, C, P, P] flattens in exactly the patch order.
+        """
+        w = self.patch_embed.weight
+        D, C, P, _ = w.shape
+        B, _, H, W = x.shape
+        patches = x.view(B, C, H // P, P, W // P, P).permute(0, 2, 4, 1, 3, 5).reshape(B, (H // P) * (W // P), C * P * P)
+        return nn.functional.linear(patches, w.view(D, C * P * P), self.patch_embed.bias)
 
     def loss_fn(self, out: torch.Tensor, y: torch.Tensor) -> torch.Tensor:
         if _fused(out):
