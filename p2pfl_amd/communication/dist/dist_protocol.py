@@ -44,6 +44,7 @@ from p2pfl_amd.communication.grpc.grpc_protocol import GrpcClient, GrpcCommunica
 from p2pfl_amd.communication.messages import WeightsMessage
 from p2pfl_amd.learning.arena import FlatParams, ParamLayout, flatten
 from p2pfl_amd.management.logger import logger
+from p2pfl_amd.utils.lockcheck import make_lock
 
 MAGIC = b"P2FDIST1"
 
@@ -81,11 +82,11 @@ class DistDataPlane:
         dist.all_gather_object(addrs, addr)
         self.addr_of = {r: a for r, a in enumerate(addrs)}
         self.rank_of = {a: r for r, a in self.addr_of.items()}
-        self._send_locks = {r: threading.Lock() for r in range(self.world) if r != self.rank}
+        self._send_locks = {r: make_lock("DistDataPlane._send_lock") for r in range(self.world) if r != self.rank}
         self._recv_q: Dict[int, "queue.Queue"] = {}
         self._recv_threads: Dict[int, threading.Thread] = {}
         self._deliver: Optional[Callable[[WeightsMessage], Optional[str]]] = None
-        self._lock = threading.Lock()
+        self._lock = make_lock("DistDataPlane._lock")
         self._stopped = False
 
     # -- setup -----------------------------------------------------------

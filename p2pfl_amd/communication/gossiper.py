@@ -33,6 +33,7 @@ from typing import Any, Callable, Deque, Dict, List, Optional, Set, Tuple
 
 from p2pfl_amd.management.logger import logger
 from p2pfl_amd.settings import Settings
+from p2pfl_amd.utils.lockcheck import make_condition, make_lock
 
 
 class Gossiper(threading.Thread):
@@ -53,10 +54,10 @@ class Gossiper(threading.Thread):
         # duplicate suppression: O(1) membership + FIFO eviction
         self._seen: Set[int] = set()
         self._seen_order: Deque[int] = collections.deque()
-        self._seen_lock = threading.Lock()
+        self._seen_lock = make_lock("Gossiper._seen_lock")
         # relay queue
         self._pending: Deque[Tuple[Any, List[str]]] = collections.deque()
-        self._cv = threading.Condition()
+        self._cv = make_condition("Gossiper._cv")
         self._terminate = threading.Event()
 
     # ------------------------------------------------------------------

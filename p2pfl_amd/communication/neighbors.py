@@ -17,6 +17,7 @@ import time
 from typing import Any, Dict, NamedTuple, Optional
 
 from p2pfl_amd.management.logger import logger
+from p2pfl_amd.utils.lockcheck import make_rlock
 
 
 class NeighborEntry(NamedTuple):
@@ -29,7 +30,7 @@ class Neighbors:
     def __init__(self, self_addr: str) -> None:
         self.self_addr = self_addr
         self.neis: Dict[str, NeighborEntry] = {}
-        self.neis_lock = threading.RLock()
+        self.neis_lock = make_rlock("Neighbors.neis_lock")
         self._on_change: list = []
 
     # -- transport hooks -------------------------------------------------

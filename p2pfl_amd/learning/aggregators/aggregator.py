@@ -29,6 +29,7 @@ from typing import Any, Dict, List, Optional, Tuple
 
 from p2pfl_amd.management.logger import logger
 from p2pfl_amd.settings import Settings
+from p2pfl_amd.utils.lockcheck import make_rlock
 
 
 class NoModelsToAggregateError(Exception):
@@ -44,7 +45,7 @@ class Aggregator:
         self._train_set: List[str] = []
         self._waiting_aggregated_model = False
         self._models: Dict[str, ModelEntry] = {}
-        self._lock = threading.RLock()
+        self._lock = make_rlock("Aggregator._lock")
         self._done = threading.Event()
         self._running = False
         self._partial_cache: Dict[frozenset, Tuple[Any, List[str], int]] = {}

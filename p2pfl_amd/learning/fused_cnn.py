@@ -26,12 +26,13 @@ from p2pfl_amd import ops
 from p2pfl_amd.learning.arena import FlatParams, ModuleArena
 from p2pfl_amd.learning.torch_learner import TorchLearner
 from p2pfl_amd.management.logger import logger
+from p2pfl_amd.utils.lockcheck import make_lock, make_rlock
 
 # Several learners (virtual peers on one GPU, each on its own node thread)
 # may capture epoch graphs concurrently: captures are serialised process-wide
 # and run in thread-local capture mode, so the other peers' kernels and
 # allocations on their own threads stay legal while one peer captures.
-_CAPTURE_LOCK = threading.Lock()
+_CAPTURE_LOCK = make_lock("FusedCNN._CAPTURE_LOCK")
 
 _NAMES = ("conv1.weight", "conv1.bias", "conv2.weight", "conv2.bias", "l1.weight", "l1.bias", "l2.weight", "l2.bias")
 FEAT, HID = 3136, 2048
@@ -185,7 +186,7 @@ class FusedCNNLearner(TorchLearner):
         self.engine = FusedCNNEngine(model, self.device, lr=lr, betas=betas, eps=eps, weight_decay=wd, arena=self.arena)
         self.use_graphs = use_graphs
         self._graphs: Dict[str, _EpochGraph] = {}
-        self._lock = threading.RLock()  # fit() -> _validate() re-enters
+        self._lock = make_rlock("FusedCNNLearner._lock")  # fit() -> _validate() re-enters
         self._stream = torch.cuda.Stream(self.device)
         self._dirty_shadows = False
 

@@ -18,12 +18,14 @@ from __future__ import annotations
 import threading
 from typing import Any, Dict, List, Optional
 
+from p2pfl_amd.utils.lockcheck import make_condition, make_lock
+
 
 class ChangeSignal:
     """Monotonic version counter with a condition variable."""
 
     def __init__(self) -> None:
-        self._cv = threading.Condition()
+        self._cv = make_condition("ChangeSignal._cv")
         self._version = 0
 
     @property
@@ -60,9 +62,9 @@ class NodeState:
         self.train_set: List[str] = []
         self.train_set_votes: Dict[str, Dict[str, int]] = {}
 
-        self.train_set_votes_lock = threading.Lock()
-        self.start_thread_lock = threading.Lock()
-        self.votes_cv = threading.Condition()
+        self.train_set_votes_lock = make_lock("NodeState.train_set_votes_lock")
+        self.start_thread_lock = make_lock("NodeState.start_thread_lock")
+        self.votes_cv = make_condition("NodeState.votes_cv")
         self.model_initialized = threading.Event()
         self.changed = ChangeSignal()
 

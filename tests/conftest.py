@@ -9,17 +9,41 @@ import pytest
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
+# Lock-order checking (race detection) is on for the whole suite unless the
+# caller sets P2PFL_LOCKCHECK=0; it must be enabled before any lock is built.
+os.environ.setdefault("P2PFL_LOCKCHECK", "1")
+
 from p2pfl_amd.settings import Settings  # noqa: E402
+from p2pfl_amd.utils import lockcheck  # noqa: E402
 from p2pfl_amd.utils import set_test_settings  # noqa: E402
 
 set_test_settings()
 Settings.LOG_LEVEL = "INFO"
 Settings.LOG_DIR = os.environ.get("P2PFL_TEST_LOG_DIR", "/tmp/p2pfl_amd_test_logs")
+if lockcheck.is_enabled():
+    # held for a whole epoch / graph capture / blocking RCCL send by design
+    lockcheck.enable(
+        hold_warn_s=10.0,
+        exempt={"FusedCNNLearner._lock", "FusedCNN._CAPTURE_LOCK", "DistDataPlane._send_lock"},
+    )
+
+
+@pytest.fixture(autouse=True)
+def _no_lock_order_violations(request):
+    """Fail a test during which the checker saw a potential deadlock."""
+    before = len(lockcheck.violations())
+    yield
+    if request.node.get_closest_marker("lockcheck_expected"):
+        return
+    new = lockcheck.violations()[before:]
+    if new:
+        pytest.fail("lock-order violations:\n" + "\n".join(str(v) for v in new), pytrace=False)
 
 
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs a real AMD GPU (MI355X) and the native extension")
     config.addinivalue_line("markers", "slow: long-running")
+    config.addinivalue_line("markers", "lockcheck_expected: the test provokes lock-order violations on purpose")
 
 
 def pytest_collection_modifyitems(config, items):
