@@ -83,6 +83,86 @@ void sgd_step(torch::Tensor p, torch::Tensor g, c10::optional<torch::Tensor> buf
   p2::sgd_step(p.data_ptr<float>(), g.data_ptr<float>(), b, opt_bf16(pbf, n), n, h, stream());
 }
 
+// ---- multi-tensor optimizer steps (mixed-precision learners) ----------------
+// tens: int64 [T, 3] (offset, numel, flags) on the GPU; chunks: int32 [C, 2]
+// (tensor, chunk) on the GPU; grads: one entry per tensor (None = skip).
+torch::Tensor grad_table(const std::vector<c10::optional<torch::Tensor>>& grads, const std::vector<int64_t>& numels,
+                         const std::vector<bool>& grad_bf16, const torch::Device& dev) {
+  const size_t T = grads.size();
+  TORCH_CHECK(numels.size() == T && grad_bf16.size() == T, "multi-tensor step: table size mismatch");
+  auto host = torch::empty({int64_t(T)}, torch::dtype(torch::kInt64)).pin_memory();
+  auto* hp = host.data_ptr<int64_t>();
+  for (size_t t = 0; t < T; ++t) {
+    hp[t] = 0;
+    if (!grads[t].has_value() || !grads[t]->defined()) continue;
+    const auto& g = *grads[t];
+    TORCH_CHECK(g.device() == dev && g.is_contiguous() && g.numel() == numels[t], "grad ", t,
+                " must be a contiguous GPU tensor of the parameter's size");
+    TORCH_CHECK(g.scalar_type() == (grad_bf16[t] ? torch::kBFloat16 : torch::kFloat32), "grad ", t,
+                " has an unexpected dtype");
+    TORCH_CHECK(reinterpret_cast<uintptr_t>(g.data_ptr()) % 16 == 0, "grad ", t, " must be 16-byte aligned");
+    hp[t] = int64_t(reinterpret_cast<uintptr_t>(g.data_ptr()));
+  }
+  return host.to(dev, /*non_blocking=*/true);
+}
+
+void check_tables(const torch::Tensor& tens, const torch::Tensor& chunks, const torch::Device& dev) {
+  TORCH_CHECK(tens.device() == dev && tens.scalar_type() == torch::kInt64 && tens.dim() == 2 && tens.size(1) == 3 &&
+                  tens.is_contiguous(),
+              "tensor table must be int64 [T, 3] on the arena's device");
+  TORCH_CHECK(chunks.device() == dev && chunks.scalar_type() == torch::kInt32 && chunks.dim() == 2 &&
+                  chunks.size(1) == 2 && chunks.is_contiguous(),
+              "chunk table must be int32 [C, 2] on the arena's device");
+}
+
+void adam_mt_step(torch::Tensor p, torch::Tensor m, torch::Tensor v, c10::optional<torch::Tensor> pbf,
+                  torch::Tensor tens, torch::Tensor chunks, std::vector<c10::optional<torch::Tensor>> grads,
+                  std::vector<int64_t> numels, std::vector<bool> grad_bf16, double lr, double b1, double b2, double eps,
+                  double wd, int64_t step, bool decoupled) {
+  for (auto* t : {&p, &m, &v}) check_f32(*t, "adam operand");
+  const int64_t n = p.numel();
+  TORCH_CHECK(m.numel() == n && v.numel() == n, "adam: size mismatch");
+  check_tables(tens, chunks, p.device());
+  TORCH_CHECK(tens.size(0) == int64_t(grads.size()), "adam: one gradient per tensor");
+  const c10::DeviceGuard guard(p.device());
+  auto gp = grad_table(grads, numels, grad_bf16, p.device());
+  p2::AdamParams h{};
+  h.lr = float(lr);
+  h.beta1 = float(b1);
+  h.beta2 = float(b2);
+  h.eps = float(eps);
+  h.weight_decay = float(wd);
+  h.step_size = float(lr / (1.0 - std::pow(b1, double(step))));
+  h.inv_sqrt_bc2 = float(1.0 / std::sqrt(1.0 - std::pow(b2, double(step))));
+  h.decoupled = decoupled ? 1 : 0;
+  p2::adam_mt_step(p.data_ptr<float>(), m.data_ptr<float>(), v.data_ptr<float>(), opt_bf16(pbf, n),
+                   reinterpret_cast<const p2::MTTensor*>(tens.data_ptr<int64_t>()),
+                   reinterpret_cast<const int2*>(chunks.data_ptr<int32_t>()), int(chunks.size(0)),
+                   reinterpret_cast<const uint64_t*>(gp.data_ptr<int64_t>()), h, stream());
+}
+
+void sgd_mt_step(torch::Tensor p, c10::optional<torch::Tensor> buf, c10::optional<torch::Tensor> pbf,
+                 torch::Tensor tens, torch::Tensor chunks, std::vector<c10::optional<torch::Tensor>> grads,
+                 std::vector<int64_t> numels, std::vector<bool> grad_bf16, double lr, double momentum,
+                 double dampening, double wd, bool nesterov, bool first_step) {
+  check_f32(p, "p");
+  const int64_t n = p.numel();
+  float* b = nullptr;
+  if (buf.has_value() && buf->defined()) {
+    check_f32(*buf, "buf");
+    TORCH_CHECK(buf->numel() == n, "sgd: buf size mismatch");
+    b = buf->data_ptr<float>();
+  }
+  check_tables(tens, chunks, p.device());
+  TORCH_CHECK(tens.size(0) == int64_t(grads.size()), "sgd: one gradient per tensor");
+  const c10::DeviceGuard guard(p.device());
+  auto gp = grad_table(grads, numels, grad_bf16, p.device());
+  p2::SgdParams h{float(lr), float(momentum), float(dampening), float(wd), nesterov ? 1 : 0, first_step ? 1 : 0};
+  p2::sgd_mt_step(p.data_ptr<float>(), b, opt_bf16(pbf, n), reinterpret_cast<const p2::MTTensor*>(tens.data_ptr<int64_t>()),
+                  reinterpret_cast<const int2*>(chunks.data_ptr<int32_t>()), int(chunks.size(0)),
+                  reinterpret_cast<const uint64_t*>(gp.data_ptr<int64_t>()), h, stream());
+}
+
 }  // namespace
 
 void register_cnn(pybind11::module& m);
@@ -93,6 +173,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("weighted_sum", &weighted_sum, "out = sum_i w_i * src_i (fp32 flat arenas)");
   m.def("adam_step", &adam_step, "fused whole-arena Adam/AdamW step");
   m.def("sgd_step", &sgd_step, "fused whole-arena SGD(+momentum/nesterov) step");
+  m.def("adam_mt_step", &adam_mt_step, "multi-tensor Adam/AdamW over per-tensor grads into flat fp32 state");
+  m.def("sgd_mt_step", &sgd_mt_step, "multi-tensor SGD over per-tensor grads into flat fp32 state");
   register_cnn(m);
   register_fused(m);
 }

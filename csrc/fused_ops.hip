@@ -355,6 +355,8 @@ static void ln_fwd_t(const void* x, const float* w, const float* b, void* y, flo
   T* yp = static_cast<T*>(y);
   if (C <= 512)
     hipLaunchKernelGGL((ln_fwd_kernel<T, 1>), grid, blk, 0, s, xp, w, b, yp, mean, rstd, N, C, eps);
+  else if (C <= 1024)
+    hipLaunchKernelGGL((ln_fwd_kernel<T, 2>), grid, blk, 0, s, xp, w, b, yp, mean, rstd, N, C, eps);
   else
     hipLaunchKernelGGL((ln_fwd_kernel<T, 4>), grid, blk, 0, s, xp, w, b, yp, mean, rstd, N, C, eps);
 }
@@ -368,8 +370,11 @@ void layer_norm_fwd(bool bf16, const void* x, const float* w, const float* b, vo
 }
 
 int layer_norm_bwd_blocks(int N) {
-  int g = (N + 63) / 64;  // >= 16 rows per wave keeps the partial count small
-  return g > 256 ? 256 : (g < 1 ? 1 : g);
+  // ~4 rows per wave: enough blocks to fill 256 CUs at ViT sizes (6304 rows ->
+  // 394 blocks; the previous 16 rows per wave gave 99 blocks, 42 us/call),
+  // while the [G, C] partials the column reduction reads stay a few MB.
+  int g = (N + 15) / 16;
+  return g > 1024 ? 1024 : (g < 1 ? 1 : g);
 }
 
 template <typename T>
@@ -383,6 +388,8 @@ static void ln_bwd_t(const void* dy, const void* x, const float* w, const float*
   T* dxp = static_cast<T*>(dx);
   if (C <= 512)
     hipLaunchKernelGGL((ln_bwd_kernel<T, 1>), grid, blk, lds, s, dyp, xp, w, mean, rstd, dxp, pdw, pdb, N, C);
+  else if (C <= 1024)
+    hipLaunchKernelGGL((ln_bwd_kernel<T, 2>), grid, blk, lds, s, dyp, xp, w, mean, rstd, dxp, pdw, pdb, N, C);
   else
     hipLaunchKernelGGL((ln_bwd_kernel<T, 4>), grid, blk, lds, s, dyp, xp, w, mean, rstd, dxp, pdw, pdb, N, C);
   hipLaunchKernelGGL(col_reduce_kernel, dim3((C + 63) / 64), blk, 0, s, pdw, dw, pdb, db, G, C);

@@ -26,4 +26,18 @@ struct SgdParams {
 };
 void sgd_step(float* p, const float* g, float* buf, uint16_t* p_bf16, int64_t n, const SgdParams& h, hipStream_t s);
 
+// Multi-tensor optimizer steps (mixed-precision learners, optim.hip).
+constexpr int kMTChunk = 4096;  // elements per block
+constexpr int kMTGradBf16 = 1;  // gradient tensor is bf16 (else fp32)
+constexpr int kMTShadow = 2;    // also write the bf16 shadow of the weight
+struct MTTensor {
+  int64_t off;  // element offset in the flat arenas
+  int64_t n;    // elements
+  int64_t flags;
+};
+void adam_mt_step(float* p, float* m, float* v, uint16_t* p_bf16, const MTTensor* tens, const int2* chunks,
+                  int n_chunks, const uint64_t* grad_ptrs, const AdamParams& h, hipStream_t s);
+void sgd_mt_step(float* p, float* buf, uint16_t* p_bf16, const MTTensor* tens, const int2* chunks, int n_chunks,
+                 const uint64_t* grad_ptrs, const SgdParams& h, hipStream_t s);
+
 }  // namespace p2

@@ -92,4 +92,126 @@ void sgd_step(float* p, const float* g, float* buf, uint16_t* pbf, int64_t n, co
   hipLaunchKernelGGL(sgd_kernel, dim3(stream_grid(n4, 256)), dim3(256), 0, s, p, g, buf, pbf, n4, h);
 }
 
+// ---------------------------------------------------------------------------
+// Multi-tensor variants for mixed-precision learners.  The module's matrix
+// weights are bf16 views of a shadow arena (the GEMMs read them directly, no
+// per-step cast kernels) and autograd leaves each gradient in its own tensor
+// (bf16 for bf16 weights, fp32 for the rest): no per-parameter grad
+// accumulate / zero-fill launches.  One launch updates every tensor: a static
+// chunk table maps each block to (tensor, start); the per-step table holds
+// the gradient pointers (null = no grad this step: the tensor is skipped, as
+// torch.optim does).  Master weights and state stay fp32 flat arenas, so
+// FedAvg / gossip / checkpoints are unchanged.
+// ---------------------------------------------------------------------------
+P2_DEVICE void load_grad4(const void* g, bool bf, int64_t i, float (&o)[4]) {
+  if (bf) {
+    const uint2 u = *reinterpret_cast<const uint2*>(static_cast<const uint16_t*>(g) + i);
+    o[0] = __uint_as_float(u.x << 16);
+    o[1] = __uint_as_float(u.x & 0xffff0000u);
+    o[2] = __uint_as_float(u.y << 16);
+    o[3] = __uint_as_float(u.y & 0xffff0000u);
+  } else {
+    const float4 f = *reinterpret_cast<const float4*>(static_cast<const float*>(g) + i);
+    o[0] = f.x; o[1] = f.y; o[2] = f.z; o[3] = f.w;
+  }
+}
+P2_DEVICE float load_grad1(const void* g, bool bf, int64_t i) {
+  return bf ? bf16_to_f32(static_cast<const uint16_t*>(g)[i]) : static_cast<const float*>(g)[i];
+}
+
+P2_DEVICE void adam_elem(float& p, float g, float& m, float& v, const AdamParams& h) {
+  if (h.weight_decay != 0.f) {
+    if (h.decoupled)
+      p *= (1.f - h.lr * h.weight_decay);
+    else
+      g = fmaf(h.weight_decay, p, g);
+  }
+  m = fmaf(h.beta1, m, (1.f - h.beta1) * g);
+  v = fmaf(h.beta2, v, (1.f - h.beta2) * g * g);
+  p = p - h.step_size * (m / (sqrtf(v) * h.inv_sqrt_bc2 + h.eps));
+}
+
+__global__ __launch_bounds__(256) void adam_mt_kernel(float* __restrict__ p, float* __restrict__ m,
+                                                      float* __restrict__ v, uint16_t* __restrict__ pbf,
+                                                      const MTTensor* __restrict__ tens, const int2* __restrict__ chunks,
+                                                      const uint64_t* __restrict__ gptr, AdamParams h) {
+  const int2 ch = chunks[blockIdx.x];
+  const void* g = reinterpret_cast<const void*>(gptr[ch.x]);
+  if (g == nullptr) return;
+  const MTTensor T = tens[ch.x];
+  const bool gbf = T.flags & kMTGradBf16, shadow = (T.flags & kMTShadow) && pbf;
+  const int64_t start = int64_t(ch.y) * kMTChunk;
+  const int64_t len = T.n - start < kMTChunk ? T.n - start : kMTChunk;
+  const int64_t len4 = len & ~int64_t(3);
+  float* P = p + T.off + start;
+  float* M = m + T.off + start;
+  float* V = v + T.off + start;
+  uint16_t* PB = shadow ? pbf + T.off + start : nullptr;
+  for (int64_t i = int64_t(threadIdx.x) * 4; i < len4; i += 256 * 4) {
+    float gg[4];
+    load_grad4(g, gbf, start + i, gg);
+    float4 pp = *reinterpret_cast<float4*>(P + i), mm = *reinterpret_cast<float4*>(M + i),
+           vv = *reinterpret_cast<float4*>(V + i);
+    adam_elem(pp.x, gg[0], mm.x, vv.x, h);
+    adam_elem(pp.y, gg[1], mm.y, vv.y, h);
+    adam_elem(pp.z, gg[2], mm.z, vv.z, h);
+    adam_elem(pp.w, gg[3], mm.w, vv.w, h);
+    *reinterpret_cast<float4*>(P + i) = pp;
+    *reinterpret_cast<float4*>(M + i) = mm;
+    *reinterpret_cast<float4*>(V + i) = vv;
+    if (PB) {
+      uint2 o;
+      o.x = pack_bf16x2(pp.x, pp.y);
+      o.y = pack_bf16x2(pp.z, pp.w);
+      *reinterpret_cast<uint2*>(PB + i) = o;
+    }
+  }
+  for (int64_t i = len4 + threadIdx.x; i < len; i += 256) {
+    adam_elem(P[i], load_grad1(g, gbf, start + i), M[i], V[i], h);
+    if (PB) PB[i] = f32_to_bf16(P[i]);
+  }
+}
+
+P2_DEVICE float sgd_elem(float& p, float g, float* b, const SgdParams& h) {
+  if (h.weight_decay != 0.f) g = fmaf(h.weight_decay, p, g);
+  if (b) {
+    *b = h.first_step ? g : fmaf(h.momentum, *b, (1.f - h.dampening) * g);
+    g = h.nesterov ? fmaf(h.momentum, *b, g) : *b;
+  }
+  p = fmaf(-h.lr, g, p);
+  return p;
+}
+
+__global__ __launch_bounds__(256) void sgd_mt_kernel(float* __restrict__ p, float* __restrict__ buf,
+                                                     uint16_t* __restrict__ pbf, const MTTensor* __restrict__ tens,
+                                                     const int2* __restrict__ chunks, const uint64_t* __restrict__ gptr,
+                                                     SgdParams h) {
+  const int2 ch = chunks[blockIdx.x];
+  const void* g = reinterpret_cast<const void*>(gptr[ch.x]);
+  if (g == nullptr) return;
+  const MTTensor T = tens[ch.x];
+  const bool gbf = T.flags & kMTGradBf16, shadow = (T.flags & kMTShadow) && pbf;
+  const int64_t start = int64_t(ch.y) * kMTChunk;
+  const int64_t len = T.n - start < kMTChunk ? T.n - start : kMTChunk;
+  float* P = p + T.off + start;
+  float* B = buf ? buf + T.off + start : nullptr;
+  uint16_t* PB = shadow ? pbf + T.off + start : nullptr;
+  for (int64_t i = threadIdx.x; i < len; i += 256) {
+    const float np = sgd_elem(P[i], load_grad1(g, gbf, start + i), B ? B + i : nullptr, h);
+    if (PB) PB[i] = f32_to_bf16(np);
+  }
+}
+
+void adam_mt_step(float* p, float* m, float* v, uint16_t* pbf, const MTTensor* tens, const int2* chunks,
+                  int n_chunks, const uint64_t* gptr, const AdamParams& h, hipStream_t s) {
+  if (n_chunks > 0)
+    hipLaunchKernelGGL(adam_mt_kernel, dim3(n_chunks), dim3(256), 0, s, p, m, v, pbf, tens, chunks, gptr, h);
+}
+
+void sgd_mt_step(float* p, float* buf, uint16_t* pbf, const MTTensor* tens, const int2* chunks, int n_chunks,
+                 const uint64_t* gptr, const SgdParams& h, hipStream_t s) {
+  if (n_chunks > 0)
+    hipLaunchKernelGGL(sgd_mt_kernel, dim3(n_chunks), dim3(256), 0, s, p, buf, pbf, tens, chunks, gptr, h);
+}
+
 }  // namespace p2

@@ -125,6 +125,8 @@ class DistDataPlane:
             cmd=msg.cmd,
         )
         with self._send_locks[dst]:
+            if self._stopped:
+                return "dist data plane stopped"
             err = send_header(hmsg)
             if err:
                 return err
@@ -137,17 +139,20 @@ class DistDataPlane:
         return None
 
     # -- receive -----------------------------------------------------------
-    def on_header(self, msg: WeightsMessage) -> None:
+    def on_header(self, msg: WeightsMessage) -> Optional[str]:
         header = json.loads(bytes(msg.weights[len(MAGIC):]).decode())
         src = int(header["src"])
         with self._lock:
+            if self._stopped:  # the sender then skips the data transfer
+                return "dist data plane stopped"
             q = self._recv_q.get(src)
             if q is None:
                 q = self._recv_q[src] = queue.Queue()
                 t = threading.Thread(target=self._recv_loop, args=(src, q), name=f"rccl-recv-{src}", daemon=True)
                 self._recv_threads[src] = t
                 t.start()
-        q.put((msg, header))
+            q.put((msg, header))
+        return None
 
     def _recv_loop(self, src: int, q: "queue.Queue") -> None:
         self._bind_device()
@@ -172,11 +177,23 @@ class DistDataPlane:
                 except Exception as e:  # a bad model must not kill the receive thread
                     logger.error(self.addr_of[self.rank], f"dist delivery failed: {e}")
 
-    def stop(self) -> None:
+    def stop(self, timeout: float = 10.0) -> None:
+        """Refuse new transfers, drain in-flight ones, end the receive threads.
+
+        After this returns no thread of this rank is inside a send/recv, so the
+        process group can be destroyed (a destroy racing an in-flight
+        point-to-point op aborts the process).
+        """
         self._stopped = True
+        for lk in self._send_locks.values():  # an in-flight send finishes first
+            if lk.acquire(timeout=timeout):
+                lk.release()
         with self._lock:
             for q in self._recv_q.values():
                 q.put(None)
+            threads = list(self._recv_threads.values())
+        for t in threads:
+            t.join(timeout)
 
 
 class DistServer(GrpcServer):
@@ -190,8 +207,7 @@ class DistServer(GrpcServer):
                 return "dist data plane not running"
             if msg.cmd not in self._commands:
                 return f"Unknown command: {msg.cmd}"
-            self.plane.on_header(msg)
-            return None
+            return self.plane.on_header(msg)
         return super().handle_weights(msg)
 
     def deliver_arena(self, msg: WeightsMessage) -> Optional[str]:

@@ -148,7 +148,14 @@ class ModuleArena:
     and restored by :meth:`sync_out`.
     """
 
-    def __init__(self, module: torch.nn.Module, device: Optional[torch.device] = None, grads: bool = False) -> None:
+    def __init__(
+        self,
+        module: torch.nn.Module,
+        device: Optional[torch.device] = None,
+        grads: bool = False,
+        compute_dtype: Optional[torch.dtype] = None,
+        fp32_names: Optional[Iterable[str]] = None,
+    ) -> None:
         sd = module.state_dict(keep_vars=True)
         if device is None:
             device = next(iter(sd.values())).device if sd else torch.device("cpu")
@@ -173,6 +180,27 @@ class ModuleArena:
                     p.grad = gviews[name]
         # mask of trainable elements (params, not buffers)
         self.param_names = [n for n, _ in module.named_parameters()]
+        # Mixed precision (GPU learners): the module's matrix weights become
+        # bf16 views of a shadow arena that the optimizer rewrites after every
+        # step, so GEMMs/convs read bf16 weights directly -- no autocast cast
+        # kernel per weight per forward, no cast-back kernel per gradient.
+        # The fp32 arena stays the master copy (FedAvg, gossip, checkpoints).
+        self.shadow: Optional[torch.Tensor] = None
+        self.shadow_names: Tuple[str, ...] = ()
+        if compute_dtype is not None:
+            if grads:
+                raise ValueError("mixed-precision arenas keep per-tensor grads (grads=False)")
+            keep = set(fp32_names) if fp32_names is not None else {n for n, p in module.named_parameters() if p.dim() < 2}
+            self.shadow = torch.empty(self.layout.numel, dtype=compute_dtype, device=device)
+            self.shadow.copy_(flat)
+            names = []
+            for name, p in module.named_parameters():
+                if name in keep:
+                    continue
+                off = self.layout.offsets[self.layout.names.index(name)]
+                p.data = self.shadow[off : off + p.numel()].view(p.shape)
+                names.append(name)
+            self.shadow_names = tuple(names)
 
     @property
     def flat(self) -> torch.Tensor:
@@ -184,9 +212,11 @@ class ModuleArena:
             self.params[name].copy_(t.reshape(self.params[name].shape).float())
 
     def sync_out(self) -> None:
-        """Copy averaged non-float buffers back to the module."""
+        """Copy averaged non-float buffers back to the module; refresh the bf16 shadow."""
         for name, t in self._int_buffers.items():
             t.copy_(self.params[name].reshape(t.shape).round().to(t.dtype))
+        if self.shadow is not None:
+            self.shadow.copy_(self.params.flat)
 
     def grads_bound(self) -> bool:
         if self.grads is None:

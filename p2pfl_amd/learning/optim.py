@@ -144,3 +144,109 @@ def fuse_optimizer(opt: torch.optim.Optimizer, arena: ModuleArena):
     if type(opt) is torch.optim.SGD:
         return ArenaSGD(arena, lr, g["momentum"], g["dampening"], g["weight_decay"], g["nesterov"])
     return None
+
+
+# ----------------------------------------------------------------------------
+# Multi-tensor optimizers for mixed-precision arenas (ModuleArena(compute_dtype=...))
+# ----------------------------------------------------------------------------
+class MTTables:
+    """Static per-tensor and per-chunk tables for the multi-tensor kernels.
+
+    ``tens`` int64 [T, 3] = (arena offset, numel, flags) with flags bit 0 =
+    bf16 gradient, bit 1 = write the bf16 shadow; ``chunks`` int32 [C, 2] =
+    (tensor, chunk index) -- one GPU block per 4096-element chunk.
+    """
+
+    CHUNK = 4096
+
+    def __init__(self, arena: ModuleArena) -> None:
+        lay = arena.layout
+        shadow = set(arena.shadow_names)
+        self.params = [p for _, p in arena.module.named_parameters()]
+        names = [n for n, _ in arena.module.named_parameters()]
+        self.table = []
+        chunks = []
+        for t, (name, p) in enumerate(zip(names, self.params)):
+            off = lay.offsets[lay.names.index(name)]
+            flags = (1 if p.dtype == torch.bfloat16 else 0) | (2 if name in shadow else 0)
+            self.table.append((off, p.numel(), flags))
+            chunks.extend((t, c) for c in range((p.numel() + self.CHUNK - 1) // self.CHUNK))
+        dev = arena.flat.device
+        self.numels = [n for _, n, _ in self.table]
+        self.grad_bf16 = [bool(f & 1) for _, _, f in self.table]
+        self.tens = torch.tensor(self.table, dtype=torch.int64, device=dev).reshape(-1, 3)
+        self.chunks = torch.tensor(chunks, dtype=torch.int32, device=dev).reshape(-1, 2)
+
+    def grads(self):
+        return [p.grad for p in self.params]
+
+
+class _MTOptimizer:
+    def __init__(self, arena: ModuleArena, lr: float, weight_decay: float) -> None:
+        self.arena = arena
+        self.lr = lr
+        self.weight_decay = weight_decay
+        self.t = 0
+        self.mt = MTTables(arena)
+
+    def zero_grad(self, set_to_none: bool = True) -> None:
+        # always None: autograd then hands over each new gradient without a
+        # zero-fill + accumulate kernel per parameter
+        for p in self.mt.params:
+            p.grad = None
+
+
+class MTAdam(_MTOptimizer):
+    def __init__(self, arena, lr=1e-3, betas=(0.9, 0.999), eps=1e-8, weight_decay=0.0, decoupled=False) -> None:
+        super().__init__(arena, lr, weight_decay)
+        self.beta1, self.beta2 = betas
+        self.eps = eps
+        self.decoupled = decoupled
+        self.m = torch.zeros_like(arena.flat)
+        self.v = torch.zeros_like(arena.flat)
+
+    def step(self) -> None:
+        self.t += 1
+        ops.adam_mt_step(
+            self.arena.flat, self.m, self.v, self.mt.grads(), self.mt,
+            lr=self.lr, beta1=self.beta1, beta2=self.beta2, eps=self.eps,
+            weight_decay=self.weight_decay, step=self.t, decoupled=self.decoupled, p_bf16=self.arena.shadow,
+        )
+
+
+class MTSGD(_MTOptimizer):
+    def __init__(self, arena, lr=1e-2, momentum=0.0, dampening=0.0, weight_decay=0.0, nesterov=False) -> None:
+        super().__init__(arena, lr, weight_decay)
+        self.momentum, self.dampening, self.nesterov = momentum, dampening, nesterov
+        self.buf: Optional[torch.Tensor] = torch.zeros_like(arena.flat) if momentum != 0 else None
+
+    def step(self) -> None:
+        self.t += 1
+        ops.sgd_mt_step(
+            self.arena.flat, self.buf, self.mt.grads(), self.mt,
+            lr=self.lr, momentum=self.momentum, dampening=self.dampening, weight_decay=self.weight_decay,
+            nesterov=self.nesterov, first_step=self.t == 1, p_bf16=self.arena.shadow,
+        )
+
+
+def fusable(opt: torch.optim.Optimizer, module: torch.nn.Module) -> bool:
+    """True if ``opt`` is a plain single-group Adam/AdamW/SGD over all of ``module``'s parameters."""
+    if len(opt.param_groups) != 1:
+        return False
+    g = opt.param_groups[0]
+    if {id(p) for p in g["params"]} != {id(p) for p in module.parameters()}:
+        return False
+    if g.get("maximize") or g.get("differentiable") or g.get("amsgrad"):
+        return False
+    return type(opt) in (torch.optim.Adam, torch.optim.AdamW, torch.optim.SGD)
+
+
+def fuse_optimizer_mt(opt: torch.optim.Optimizer, arena: ModuleArena):
+    """Multi-tensor equivalent of ``opt`` for a mixed-precision arena, or None."""
+    if not fusable(opt, arena.module):
+        return None
+    g = opt.param_groups[0]
+    lr = float(g["lr"]) if not isinstance(g["lr"], torch.Tensor) else float(g["lr"].item())
+    if type(opt) is torch.optim.SGD:
+        return MTSGD(arena, lr, g["momentum"], g["dampening"], g["weight_decay"], g["nesterov"])
+    return MTAdam(arena, lr, tuple(g["betas"]), g["eps"], g["weight_decay"], decoupled=type(opt) is torch.optim.AdamW)

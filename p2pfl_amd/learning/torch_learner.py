@@ -11,7 +11,11 @@ Replaces the Lightning ``Trainer`` with an explicit loop tuned for MI355X:
   (``ops.adam_step`` / ``ops.sgd_step``) instead of per-tensor launches;
 * data batches are produced on the device (no loader workers);
 * compute runs under bf16 autocast on the GPU (fp32 master weights and
-  optimizer state), fp32 on the CPU;
+  optimizer state), fp32 on the CPU.  On the GPU the matrix weights are bf16
+  views of a shadow arena rewritten by the optimizer kernel (``mixed``), and
+  gradients stay per-tensor (bf16 for bf16 weights) and are consumed by ONE
+  multi-tensor Adam/SGD launch -- no per-weight cast, zero-fill or
+  accumulate kernels in the step;
 * the optimizer is re-created on every :meth:`fit`, as Lightning does when a
   new ``Trainer`` is built per round (reference quirk Q23, kept).
 
@@ -52,6 +56,7 @@ class TorchLearner(NodeLearner):
         precision: Optional[str] = None,
         log_every_n_steps: int = 50,
         fused_optimizer: bool = True,
+        mixed: Optional[bool] = None,
     ) -> None:
         if Settings.TORCH_NUM_THREADS:
             torch.set_num_threads(Settings.TORCH_NUM_THREADS)
@@ -66,6 +71,8 @@ class TorchLearner(NodeLearner):
         self.precision = precision or ("bf16" if self.device.type == "cuda" else "fp32")
         self.log_every_n_steps = log_every_n_steps
         self.fused_optimizer = fused_optimizer
+        self._mixed_opt = mixed
+        self.mixed = False
         self._interrupt = threading.Event()
         self._step = 0
         self.model: Any = None
@@ -83,7 +90,23 @@ class TorchLearner(NodeLearner):
             self.arena = None
             return
         model.to(self.device)
-        self.arena = ModuleArena(model, device=self.device, grads=True)
+        self.mixed = self._want_mixed(model)
+        if self.mixed:
+            keep = model.fp32_parameter_names() if hasattr(model, "fp32_parameter_names") else None
+            self.arena = ModuleArena(model, device=self.device, compute_dtype=torch.bfloat16, fp32_names=keep)
+        else:
+            self.arena = ModuleArena(model, device=self.device, grads=True)
+
+    def _want_mixed(self, model: Any) -> bool:
+        """bf16 weight shadows + multi-tensor optimizer (GPU, bf16, fusable optimizer)."""
+        if self._mixed_opt is not None:
+            return bool(self._mixed_opt)
+        if not (self.device.type == "cuda" and self.precision == "bf16" and self.fused_optimizer and ops.available()):
+            return False
+        from p2pfl_amd.learning.optim import fusable
+
+        opt = model.configure_optimizers()
+        return fusable(opt[0] if isinstance(opt, (list, tuple)) else opt, model)
 
     def set_data(self, data: Any) -> None:
         self.data = data
@@ -171,14 +194,21 @@ class TorchLearner(NodeLearner):
         self.epochs = epochs
 
     def _autocast(self):
-        if self.precision == "bf16" and self.device.type == "cuda":
-            return torch.autocast(device_type="cuda", dtype=torch.bfloat16)
+        if self.precision == "bf16":
+            return torch.autocast(device_type=self.device.type, dtype=torch.bfloat16)
         return torch.autocast(device_type="cpu", enabled=False)
 
     def _make_optimizer(self):
         opt = self.model.configure_optimizers()
         if isinstance(opt, (list, tuple)):
             opt = opt[0]
+        if self.mixed:
+            from p2pfl_amd.learning.optim import fuse_optimizer_mt
+
+            fused = fuse_optimizer_mt(opt, self.arena)
+            if fused is None:  # bf16 weights must not be stepped by torch.optim
+                raise RuntimeError("mixed-precision learner needs a plain Adam/AdamW/SGD over all parameters")
+            return fused
         if not (self.fused_optimizer and self.device.type == "cuda" and self.arena is not None):
             return opt
         from p2pfl_amd.learning.optim import fuse_optimizer

@@ -142,6 +142,14 @@ class ViT(FLModule):
             return ops.softmax_xent(out, y)
         return nn.functional.cross_entropy(out, y)
 
+    def fp32_parameter_names(self) -> set:
+        """Parameters the fused kernels read in fp32 (LayerNorm affine, the bias of bias+GELU).
+
+        Every other weight (GEMM matrices, plain-linear biases, tokens) is a bf16
+        view of the learner's shadow arena under mixed precision.
+        """
+        return {n for n, _ in self.named_parameters() if "norm" in n or n.endswith("fc1.bias")}
+
     def configure_optimizers(self) -> torch.optim.Optimizer:
         return torch.optim.AdamW(self.parameters(), lr=self.lr_rate, weight_decay=self.weight_decay)
 

@@ -140,6 +140,46 @@ def sgd_step(p, g, buf, *, lr, momentum=0.0, dampening=0.0, weight_decay=0.0, ne
 
 
 # ----------------------------------------------------------------------------
+# multi-tensor optimizers (mixed-precision learners: per-tensor grads, flat state)
+# ----------------------------------------------------------------------------
+def _mt_reference(step_fn, p, states, pbf, table, grads):
+    for (off, n, flags), g in zip(table, grads):
+        if g is None:
+            continue
+        view = lambda t: t[off : off + n]  # noqa: E731
+        step_fn(view(p), g.reshape(-1).float(), *[view(s) if s is not None else None for s in states])
+        if pbf is not None and flags & 2:
+            view(pbf).copy_(view(p))
+
+
+def adam_mt_step(p, m, v, grads, mt, *, lr, beta1, beta2, eps, weight_decay, step, decoupled=False, p_bf16=None):
+    """Adam/AdamW for tensors whose grads live outside the arena (``mt``: :class:`~p2pfl_amd.learning.optim.MTTables`)."""
+    if not _gpu(p):
+        _mt_reference(
+            lambda pp, g, mm, vv: adam_step_reference(pp, g, mm, vv, lr, beta1, beta2, eps, weight_decay, step, decoupled),
+            p, (m, v), p_bf16, mt.table, grads,
+        )
+        return
+    ext().adam_mt_step(
+        p, m, v, p_bf16, mt.tens, mt.chunks, list(grads), mt.numels, mt.grad_bf16,
+        float(lr), float(beta1), float(beta2), float(eps), float(weight_decay), int(step), bool(decoupled),
+    )
+
+
+def sgd_mt_step(p, buf, grads, mt, *, lr, momentum=0.0, dampening=0.0, weight_decay=0.0, nesterov=False, first_step=False, p_bf16=None):
+    if not _gpu(p):
+        _mt_reference(
+            lambda pp, g, b: sgd_step_reference(pp, g, b, lr, momentum, dampening, weight_decay, nesterov, first_step),
+            p, (buf,), p_bf16, mt.table, grads,
+        )
+        return
+    ext().sgd_mt_step(
+        p, buf, p_bf16, mt.tens, mt.chunks, list(grads), mt.numels, mt.grad_bf16,
+        float(lr), float(momentum), float(dampening), float(weight_decay), bool(nesterov), bool(first_step),
+    )
+
+
+# ----------------------------------------------------------------------------
 # fused transformer / classifier ops (csrc/fused_ops.hip)
 # ----------------------------------------------------------------------------
 from p2pfl_amd.ops.fused import (  # noqa: E402

@@ -75,6 +75,7 @@ def main(out: str, model_name: str = "mlp", rounds: int = 2) -> None:
         dist.barrier()
     finally:
         node.stop()
+        dist.barrier()  # every rank's data plane drained before any group is destroyed
         dist.destroy_process_group()
 
 

@@ -252,3 +252,56 @@ def test_aggregator_lost_members():
     x.mark_lost(["c"])
     x.add_model(t(1), ["c"], 1)
     assert "c" in x.get_aggregated_models() and not x._lost
+
+
+def test_mixed_precision_learner_cpu():
+    """bf16 weight shadows + multi-tensor Adam (the GPU learner path) on the CPU reference ops."""
+    from p2pfl_amd.data import MnistFederatedDM
+
+    dm = MnistFederatedDM(sub_id=0, number_sub=40)
+    nl = TorchLearner(MLP(seed=1), dm, "mixed-test", 1, device="cpu", precision="bf16", mixed=True)
+    arena = nl.arena
+    assert nl.mixed and arena.shadow is not None and arena.grads is None
+    # matrix weights are bf16 views of the shadow; biases stay fp32 views of the master arena
+    for name, p in nl.model.named_parameters():
+        assert p.dtype == (torch.bfloat16 if p.dim() >= 2 else torch.float32), name
+    before = {k: v.clone() for k, v in nl.get_parameters().items()}
+    ev0 = nl.evaluate()["test_loss"]
+    nl.fit()
+    assert nl.evaluate()["test_loss"] < ev0
+    params = nl.get_parameters()
+    assert all(v.dtype == torch.float32 for v in params.values())
+    assert any(not torch.equal(before[k], v) for k, v in params.items())
+    for name in arena.shadow_names:  # shadow rewritten by every step
+        w = dict(nl.model.named_parameters())[name]
+        assert torch.equal(w.detach(), params[name].to(torch.bfloat16)), name
+    # set_parameters refreshes the shadow
+    nl.set_parameters(before)
+    w = dict(nl.model.named_parameters())[arena.shadow_names[0]]
+    assert torch.equal(w.detach(), before[arena.shadow_names[0]].to(torch.bfloat16))
+
+
+@pytest.mark.parametrize("opt_name", ["adam", "adamw", "sgd"])
+def test_multi_tensor_optimizer_matches_torch(opt_name):
+    """MTAdam/MTSGD over per-tensor grads == torch.optim on the same fp32 grads."""
+    from p2pfl_amd.learning.arena import ModuleArena
+    from p2pfl_amd.learning.optim import fuse_optimizer_mt
+
+    m1, m2 = MLP(seed=3), MLP(seed=3)
+    make = {
+        "adam": lambda ps: torch.optim.Adam(ps, lr=1e-2, weight_decay=1e-3),
+        "adamw": lambda ps: torch.optim.AdamW(ps, lr=1e-2, weight_decay=0.05),
+        "sgd": lambda ps: torch.optim.SGD(ps, lr=0.1, momentum=0.9, nesterov=True, weight_decay=1e-4),
+    }[opt_name]
+    arena = ModuleArena(m1, compute_dtype=torch.float32, fp32_names=[n for n, _ in m1.named_parameters()])
+    o1 = fuse_optimizer_mt(make(list(m1.parameters())), arena)
+    o2 = make(list(m2.parameters()))
+    torch.manual_seed(0)
+    for step in range(3):
+        x = torch.randn(16, 1, 28, 28)
+        for m, o in ((m1, o1), (m2, o2)):
+            o.zero_grad()
+            m.loss_fn(m(x), torch.arange(16) % 10).backward()
+            o.step()
+    for (k, a), b in zip(m1.state_dict().items(), m2.state_dict().values()):
+        assert torch.allclose(a, b, atol=1e-5, rtol=1e-4), k
