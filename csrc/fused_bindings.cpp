@@ -3,6 +3,9 @@
 #include <c10/hip/HIPStream.h>
 #include <torch/extension.h>
 
+#include <cmath>
+
+#include "attention.h"
 #include "fused_ops.h"
 
 namespace {
@@ -115,6 +118,59 @@ torch::Tensor xent_bwd(torch::Tensor z, torch::Tensor y, torch::Tensor lse, torc
   return dz;
 }
 
+// ---- fused attention over the QKV projection output --------------------------
+p2attn::AttnShape attn_shape(const torch::Tensor& qkv, int64_t heads) {
+  TORCH_CHECK(qkv.is_cuda() && qkv.is_contiguous() && qkv.scalar_type() == torch::kBFloat16 && qkv.dim() == 3,
+              "qkv must be a contiguous bf16 [B, T, 3C] GPU tensor");
+  TORCH_CHECK(reinterpret_cast<uintptr_t>(qkv.data_ptr()) % 16 == 0, "qkv must be 16-byte aligned");
+  const int64_t B = qkv.size(0), T = qkv.size(1), C3 = qkv.size(2);
+  TORCH_CHECK(C3 % 3 == 0 && heads > 0 && (C3 / 3) == heads * p2attn::kHeadDim, "qkv last dim must be 3 * heads * 64");
+  TORCH_CHECK(T >= 1 && T <= p2attn::kMaxT, "attention kernel supports 1..256 tokens");
+  TORCH_CHECK(B <= 65535 && heads <= 65535, "grid limits");
+  p2attn::AttnShape sh{};
+  sh.B = int(B);
+  sh.H = int(heads);
+  sh.T = int(T);
+  sh.C = int(C3 / 3);
+  sh.qkv_row = C3;
+  sh.qkv_batch = T * C3;
+  sh.o_row = sh.C;
+  sh.o_batch = T * sh.C;
+  sh.scale = float(1.0 / std::sqrt(double(p2attn::kHeadDim)));
+  return sh;
+}
+
+std::vector<torch::Tensor> attn_fwd(torch::Tensor qkv, int64_t heads) {
+  const c10::DeviceGuard g(qkv.device());
+  const auto sh = attn_shape(qkv, heads);
+  auto o = torch::empty({qkv.size(0), qkv.size(1), int64_t(sh.C)}, qkv.options());
+  auto lse = torch::empty({qkv.size(0), heads, qkv.size(1)}, qkv.options().dtype(torch::kFloat32));
+  if (sh.B > 0)
+    p2attn::attention_fwd(reinterpret_cast<const uint16_t*>(qkv.data_ptr()), reinterpret_cast<uint16_t*>(o.data_ptr()),
+                          lse.data_ptr<float>(), sh, stream());
+  return {o, lse};
+}
+
+torch::Tensor attn_bwd(torch::Tensor qkv, torch::Tensor o, torch::Tensor dout, torch::Tensor lse, int64_t heads) {
+  const c10::DeviceGuard g(qkv.device());
+  const auto sh = attn_shape(qkv, heads);
+  for (auto* t : {&o, &dout}) {
+    TORCH_CHECK(t->is_cuda() && t->is_contiguous() && t->scalar_type() == torch::kBFloat16 && t->dim() == 3 &&
+                    t->size(0) == sh.B && t->size(1) == sh.T && t->size(2) == sh.C,
+                "o / dout must be contiguous bf16 [B, T, C]");
+    TORCH_CHECK(reinterpret_cast<uintptr_t>(t->data_ptr()) % 16 == 0, "o / dout must be 16-byte aligned");
+  }
+  TORCH_CHECK(lse.is_cuda() && lse.is_contiguous() && lse.scalar_type() == torch::kFloat32 &&
+                  lse.numel() == int64_t(sh.B) * sh.H * sh.T,
+              "lse must be the forward's fp32 [B, H, T]");
+  auto dqkv = torch::empty_like(qkv);
+  if (sh.B > 0)
+    p2attn::attention_bwd(reinterpret_cast<const uint16_t*>(qkv.data_ptr()), reinterpret_cast<const uint16_t*>(o.data_ptr()),
+                          reinterpret_cast<const uint16_t*>(dout.data_ptr()), lse.data_ptr<float>(),
+                          reinterpret_cast<uint16_t*>(dqkv.data_ptr()), sh, stream());
+  return dqkv;
+}
+
 }  // namespace
 
 void register_fused(pybind11::module& m) {
@@ -125,4 +181,6 @@ void register_fused(pybind11::module& m) {
   f.def("bias_gelu_bwd", &bias_gelu_bwd);
   f.def("xent_fwd", &xent_fwd);
   f.def("xent_bwd", &xent_bwd);
+  f.def("attn_fwd", &attn_fwd, "fused MHSA forward over [B, T, 3C] qkv (head dim 64, T <= 256) -> (o, lse)");
+  f.def("attn_bwd", &attn_bwd, "fused MHSA backward -> dqkv [B, T, 3C]");
 }

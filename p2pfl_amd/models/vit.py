@@ -10,8 +10,9 @@ MLP 3072, 86.6 M parameters.
 On an AMD GPU with the native extension loaded, the fused ops come from
 :mod:`p2pfl_amd.ops` (hand-written HIP kernels): LayerNorm forward/backward,
 bias+GELU forward/backward and the softmax cross-entropy loss; the plain
-GEMMs are hipBLASLt (``torch.matmul``) and attention uses PyTorch's fused
-SDPA.  Optimiser: AdamW (fused over the arena by the learner).
+GEMMs are hipBLASLt (``torch.matmul``) and multi-head attention is the
+hand-written MFMA kernel of ``csrc/attention.hip`` (forward + two-pass
+backward, straight on the QKV projection layout).  Optimiser: AdamW (fused over the arena by the learner).
 """
 
 from __future__ import annotations
@@ -62,7 +63,11 @@ class Attention(nn.Module):
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
         B, T, C = x.shape
-        qkv = self.qkv(x).view(B, T, 3, self.heads, C // self.heads).permute(2, 0, 3, 1, 4)
+        qkv = self.qkv(x)
+        if _fused(qkv):
+            # HIP kernel on the [B, T, 3C] projection: no head permute / transpose copies
+            return self.proj(ops.attention_qkv(qkv, self.heads))
+        qkv = qkv.view(B, T, 3, self.heads, C // self.heads).permute(2, 0, 3, 1, 4)
         y = nn.functional.scaled_dot_product_attention(qkv[0], qkv[1], qkv[2])
         return self.proj(y.transpose(1, 2).reshape(B, T, C))
 

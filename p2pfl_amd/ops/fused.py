@@ -37,6 +37,15 @@ def softmax_xent_reference(z, y):
     return F.cross_entropy(z.float(), y)
 
 
+def attention_qkv_reference(qkv, heads):
+    """fp32 multi-head self-attention over a [B, T, 3C] QKV projection -> [B, T, C]."""
+    B, T, C3 = qkv.shape
+    C = C3 // 3
+    q, k, v = qkv.float().view(B, T, 3, heads, C // heads).permute(2, 0, 3, 1, 4)
+    y = F.scaled_dot_product_attention(q, k, v)
+    return y.transpose(1, 2).reshape(B, T, C)
+
+
 # -- LayerNorm ----------------------------------------------------------------
 class _LayerNorm(torch.autograd.Function):
     @staticmethod
@@ -114,3 +123,34 @@ def softmax_xent(logits: torch.Tensor, labels: torch.Tensor) -> torch.Tensor:
     if _native(logits) and logits.dim() == 2 and labels.dtype == torch.int64 and labels.is_cuda:
         return _SoftmaxXent.apply(logits, labels)
     return F.cross_entropy(logits, labels)
+
+
+# -- multi-head self-attention --------------------------------------------------------
+class _AttentionQKV(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, qkv, heads):
+        qkv = qkv.contiguous()
+        o, lse = _fx().attn_fwd(qkv, int(heads))
+        ctx.save_for_backward(qkv, o, lse)
+        ctx.heads = int(heads)
+        return o
+
+    @staticmethod
+    def backward(ctx, do):
+        qkv, o, lse = ctx.saved_tensors
+        return _fx().attn_bwd(qkv, o, do.to(o.dtype).contiguous(), lse, ctx.heads), None
+
+
+def attention_qkv(qkv: torch.Tensor, heads: int) -> torch.Tensor:
+    """softmax(q k^T / sqrt(d)) v for every head of a [B, T, 3C] QKV projection -> [B, T, C].
+
+    The HIP kernel (head dim 64, T <= 256, bf16) reads q/k/v straight out of
+    the projection and writes the proj GEMM's input layout; other shapes use
+    PyTorch SDPA.
+    """
+    B, T, C3 = qkv.shape
+    C = C3 // 3
+    if _native(qkv) and qkv.dtype == torch.bfloat16 and C == heads * 64 and T <= 256:
+        return _AttentionQKV.apply(qkv, heads)
+    q, k, v = qkv.view(B, T, 3, heads, C // heads).permute(2, 0, 3, 1, 4)
+    return F.scaled_dot_product_attention(q, k, v).transpose(1, 2).reshape(B, T, C)
