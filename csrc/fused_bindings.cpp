@@ -24,7 +24,8 @@ void check_f32(const torch::Tensor& t, int64_t n, const char* name) {
   TORCH_CHECK(t.numel() >= n, name, " too small");
 }
 
-std::vector<torch::Tensor> ln_fwd(torch::Tensor x, torch::Tensor w, torch::Tensor b, double eps) {
+std::vector<torch::Tensor> ln_fwd(torch::Tensor x, torch::Tensor w, torch::Tensor b, double eps,
+                                  c10::optional<torch::Tensor> residual) {
   const c10::DeviceGuard g(x.device());
   TORCH_CHECK(x.dim() == 2, "x must be [N, C]");
   const int64_t N = x.size(0), C = x.size(1);
@@ -32,17 +33,25 @@ std::vector<torch::Tensor> ln_fwd(torch::Tensor x, torch::Tensor w, torch::Tenso
   const bool bf = act_dtype(x, "x");
   check_f32(w, C, "weight");
   check_f32(b, C, "bias");
+  const bool has_res = residual.has_value() && residual->defined();
+  if (has_res) {
+    act_dtype(*residual, "residual");
+    TORCH_CHECK(residual->sizes() == x.sizes() && residual->scalar_type() == x.scalar_type(), "residual must match x");
+  }
   auto y = torch::empty_like(x);
+  auto sum = has_res ? torch::empty_like(x) : torch::Tensor();
   auto opt = x.options().dtype(torch::kFloat32);
   auto mean = torch::empty({N}, opt), rstd = torch::empty({N}, opt);
   if (N > 0)
-    p2fused::layer_norm_fwd(bf, x.data_ptr(), w.data_ptr<float>(), b.data_ptr<float>(), y.data_ptr(),
+    p2fused::layer_norm_fwd(bf, x.data_ptr(), has_res ? residual->data_ptr() : nullptr, w.data_ptr<float>(),
+                            b.data_ptr<float>(), y.data_ptr(), has_res ? sum.data_ptr() : nullptr,
                             mean.data_ptr<float>(), rstd.data_ptr<float>(), int(N), int(C), float(eps), stream());
+  if (has_res) return {y, mean, rstd, sum};
   return {y, mean, rstd};
 }
 
 std::vector<torch::Tensor> ln_bwd(torch::Tensor dy, torch::Tensor x, torch::Tensor w, torch::Tensor mean,
-                                  torch::Tensor rstd) {
+                                  torch::Tensor rstd, c10::optional<torch::Tensor> gsum) {
   const c10::DeviceGuard g(x.device());
   const int64_t N = x.size(0), C = x.size(1);
   TORCH_CHECK(dy.sizes() == x.sizes() && dy.scalar_type() == x.scalar_type(), "dy must match x");
@@ -51,17 +60,43 @@ std::vector<torch::Tensor> ln_bwd(torch::Tensor dy, torch::Tensor x, torch::Tens
   check_f32(w, C, "weight");
   check_f32(mean, N, "mean");
   check_f32(rstd, N, "rstd");
+  const bool has_gs = gsum.has_value() && gsum->defined();
+  if (has_gs) {
+    act_dtype(*gsum, "gsum");
+    TORCH_CHECK(gsum->sizes() == x.sizes() && gsum->scalar_type() == x.scalar_type(), "gsum must match x");
+  }
   auto dx = torch::empty_like(x);
   auto opt = x.options().dtype(torch::kFloat32);
-  auto dw = torch::zeros({C}, opt), db = torch::zeros({C}, opt);
+  auto dw = torch::empty({C}, opt), db = torch::empty({C}, opt);  // col_reduce writes every column
   if (N > 0) {
     const int G = p2fused::layer_norm_bwd_blocks(int(N));
     auto pdw = torch::empty({G, C}, opt), pdb = torch::empty({G, C}, opt);
     p2fused::layer_norm_bwd(bf, dy.data_ptr(), x.data_ptr(), w.data_ptr<float>(), mean.data_ptr<float>(),
-                            rstd.data_ptr<float>(), dx.data_ptr(), pdw.data_ptr<float>(), pdb.data_ptr<float>(),
-                            dw.data_ptr<float>(), db.data_ptr<float>(), int(N), int(C), stream());
+                            rstd.data_ptr<float>(), has_gs ? gsum->data_ptr() : nullptr, dx.data_ptr(),
+                            pdw.data_ptr<float>(), pdb.data_ptr<float>(), dw.data_ptr<float>(), db.data_ptr<float>(),
+                            int(N), int(C), stream());
+  } else {
+    dw.zero_();
+    db.zero_();
   }
   return {dx, dw, db};
+}
+
+torch::Tensor column_sum(torch::Tensor x) {
+  const c10::DeviceGuard g(x.device());
+  TORCH_CHECK(x.dim() == 2, "x must be [N, H]");
+  const int64_t N = x.size(0), H = x.size(1);
+  TORCH_CHECK(H % 8 == 0, "H must be a multiple of 8");
+  const bool bf = act_dtype(x, "x");
+  auto opt = x.options().dtype(torch::kFloat32);
+  auto out = torch::empty({H}, opt);
+  if (N > 0) {
+    auto part = torch::empty({p2fused::bias_gelu_bwd_splits(int(N)), H}, opt);
+    p2fused::column_sum(bf, x.data_ptr(), part.data_ptr<float>(), out.data_ptr<float>(), int(N), int(H), stream());
+  } else {
+    out.zero_();
+  }
+  return out;
 }
 
 torch::Tensor bias_gelu_fwd(torch::Tensor x, torch::Tensor b) {
@@ -83,11 +118,13 @@ std::vector<torch::Tensor> bias_gelu_bwd(torch::Tensor dy, torch::Tensor x, torc
   act_dtype(dy, "dy");
   check_f32(b, H, "bias");
   auto dx = torch::empty_like(x);
-  auto db = torch::zeros({H}, x.options().dtype(torch::kFloat32));
+  auto db = torch::empty({H}, x.options().dtype(torch::kFloat32));  // col_reduce writes every column
   if (N > 0) {
     auto pdb = torch::empty({p2fused::bias_gelu_bwd_splits(int(N)), H}, x.options().dtype(torch::kFloat32));
     p2fused::bias_gelu_bwd(bf, dy.data_ptr(), x.data_ptr(), b.data_ptr<float>(), dx.data_ptr(), pdb.data_ptr<float>(),
                            db.data_ptr<float>(), int(N), int(H), stream());
+  } else {
+    db.zero_();
   }
   return {dx, db};
 }
@@ -175,8 +212,11 @@ torch::Tensor attn_bwd(torch::Tensor qkv, torch::Tensor o, torch::Tensor dout, t
 
 void register_fused(pybind11::module& m) {
   auto f = m.def_submodule("fused", "fused LayerNorm / bias+GELU / softmax cross-entropy kernels");
-  f.def("ln_fwd", &ln_fwd);
-  f.def("ln_bwd", &ln_bwd);
+  f.def("ln_fwd", &ln_fwd, pybind11::arg("x"), pybind11::arg("w"), pybind11::arg("b"), pybind11::arg("eps"),
+        pybind11::arg("residual") = pybind11::none());
+  f.def("ln_bwd", &ln_bwd, pybind11::arg("dy"), pybind11::arg("x"), pybind11::arg("w"), pybind11::arg("mean"),
+        pybind11::arg("rstd"), pybind11::arg("gsum") = pybind11::none());
+  f.def("column_sum", &column_sum, "fp32 column sums of a [N, H] bf16/fp32 activation (linear bias gradient)");
   f.def("bias_gelu_fwd", &bias_gelu_fwd);
   f.def("bias_gelu_bwd", &bias_gelu_bwd);
   f.def("xent_fwd", &xent_fwd);

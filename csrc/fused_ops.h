@@ -8,18 +8,24 @@ namespace p2fused {
 
 constexpr int kMaxLnCols = 2048;  // row kept in registers (C % 8 == 0)
 
-void layer_norm_fwd(bool bf16, const void* x, const float* w, const float* b, void* y, float* mean, float* rstd,
-                    int N, int C, float eps, hipStream_t s);
+// residual (optional, nullptr = none): y = LN(x + residual), sum = x + residual (rounded to the activation dtype)
+void layer_norm_fwd(bool bf16, const void* x, const void* residual, const float* w, const float* b, void* y,
+                    void* sum, float* mean, float* rstd, int N, int C, float eps, hipStream_t s);
 // partial buffers: [layer_norm_bwd_blocks(N)][C] each
 int layer_norm_bwd_blocks(int N);
+// gsum (optional): gradient reaching the residual sum directly, added into dx
 void layer_norm_bwd(bool bf16, const void* dy, const void* x, const float* w, const float* mean, const float* rstd,
-                    void* dx, float* pdw, float* pdb, float* dw, float* db, int N, int C, hipStream_t s);
+                    const void* gsum, void* dx, float* pdw, float* pdb, float* dw, float* db, int N, int C,
+                    hipStream_t s);
 
 void bias_gelu_fwd(bool bf16, const void* x, const float* b, void* y, int64_t n, int H, hipStream_t s);
 // partial buffer: [bias_gelu_bwd_splits(N)][H]
 int bias_gelu_bwd_splits(int N);
 void bias_gelu_bwd(bool bf16, const void* dy, const void* x, const float* b, void* dx, float* pdb, float* db, int N,
                    int H, hipStream_t s);
+
+// out[c] = sum_r x[r][c] over an [N, H] activation (H % 8 == 0); partials [bias_gelu_bwd_splits(N)][H]
+void column_sum(bool bf16, const void* x, float* part, float* out, int N, int H, hipStream_t s);
 
 void xent_fwd(bool bf16, const void* z, const int64_t* y, float* loss, float* lse, int N, int K, hipStream_t s);
 void xent_bwd(bool bf16, const void* z, const int64_t* y, const float* lse, const float* gscale, void* dz, int N, int K,

@@ -49,6 +49,16 @@ struct Vec8<float> {
   }
 };
 P2_DEVICE void load8f(const float* p, float (&v)[8]) { Vec8<float>::load(p, v); }
+// round fp32 values to what a T tensor holds (bf16: RNE; fp32: identity)
+template <typename T>
+P2_DEVICE void round_to(float (&v)[8]);
+template <>
+P2_DEVICE void round_to<uint16_t>(float (&v)[8]) {
+#pragma unroll
+  for (int j = 0; j < 8; ++j) v[j] = bf16_to_f32(f32_to_bf16(v[j]));
+}
+template <>
+P2_DEVICE void round_to<float>(float (&)[8]) {}
 
 // ---------------------------------------------------------------------------
 // LayerNorm forward: y = (x - mean) * rstd * w + b over the last dim C.
@@ -57,8 +67,9 @@ P2_DEVICE void load8f(const float* p, float (&v)[8]) { Vec8<float>::load(p, v); 
 // cancellation).  Saves mean / rstd for the backward.
 // ---------------------------------------------------------------------------
 template <typename T, int K>
-__global__ __launch_bounds__(256) void ln_fwd_kernel(const T* __restrict__ x, const float* __restrict__ w,
-                                                     const float* __restrict__ b, T* __restrict__ y,
+__global__ __launch_bounds__(256) void ln_fwd_kernel(const T* __restrict__ x, const T* __restrict__ res,
+                                                     const float* __restrict__ w, const float* __restrict__ b,
+                                                     T* __restrict__ y, T* __restrict__ sum_out,
                                                      float* __restrict__ mean_out, float* __restrict__ rstd_out,
                                                      int N, int C, float eps) {
   const int lane = threadIdx.x & 63;
@@ -72,6 +83,14 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(const T* __restrict__ x, co
       const int c = (lane + 64 * k) * 8;
       if (c < C) {
         Vec8<T>::load(xr + c, v[k]);
+        if (res) {  // fused residual: s = x + r (rounded to T, as a separate add would store it)
+          float rv[8];
+          Vec8<T>::load(res + size_t(row) * C + c, rv);
+#pragma unroll
+          for (int j = 0; j < 8; ++j) v[k][j] += rv[j];
+          round_to<T>(v[k]);
+          Vec8<T>::store(sum_out + size_t(row) * C + c, v[k]);
+        }
 #pragma unroll
         for (int j = 0; j < 8; ++j) s += v[k][j];
       }
@@ -117,7 +136,8 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(const T* __restrict__ x, co
 template <typename T, int K>
 __global__ __launch_bounds__(256) void ln_bwd_kernel(const T* __restrict__ dy, const T* __restrict__ x,
                                                      const float* __restrict__ w, const float* __restrict__ mean_in,
-                                                     const float* __restrict__ rstd_in, T* __restrict__ dx,
+                                                     const float* __restrict__ rstd_in, const T* __restrict__ gs,
+                                                     T* __restrict__ dx,
                                                      float* __restrict__ part_dw, float* __restrict__ part_db, int N,
                                                      int C) {
   extern __shared__ float sred[];  // [2][C]
@@ -159,6 +179,12 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const T* __restrict__ dy, c
         float o[8];
 #pragma unroll
         for (int j = 0; j < 8; ++j) o[j] = rstd * (g[k][j] - m1 - xh[k][j] * m2);
+        if (gs) {  // fused residual branch: dx += gradient arriving at the sum directly
+          float gv[8];
+          Vec8<T>::load(gs + size_t(row) * C + c, gv);
+#pragma unroll
+          for (int j = 0; j < 8; ++j) o[j] += gv[j];
+        }
         Vec8<T>::store(dx + size_t(row) * C + c, o);
       }
     }
@@ -279,6 +305,32 @@ __global__ __launch_bounds__(256) void bias_gelu_bwd_kernel(const T* __restrict_
   }
 }
 
+// db[c] = sum_r dy[r][c] (bias gradient of a linear layer): same grid and
+// fixed-order partials as bias_gelu_bwd, without the GELU and the dx write.
+template <typename T>
+__global__ __launch_bounds__(256) void colsum_kernel(const T* __restrict__ dy, float* __restrict__ part, int N, int H) {
+  __shared__ float red[4][512];
+  const int lane = threadIdx.x & 63, ph = threadIdx.x >> 6;
+  const int c = (blockIdx.x * 64 + lane) * 8;
+  const int S = gridDim.y;
+  float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  if (c < H) {
+    for (int r = blockIdx.y * 4 + ph; r < N; r += 4 * S) {
+      float dv[8];
+      Vec8<T>::load(dy + size_t(r) * H + c, dv);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) acc[j] += dv[j];
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < 8; ++j) red[ph][lane * 8 + j] = acc[j];
+  __syncthreads();
+  for (int i = threadIdx.x; i < 512; i += 256) {
+    const int cc = blockIdx.x * 512 + i;
+    if (cc < H) part[size_t(blockIdx.y) * H + cc] = (red[0][i] + red[1][i]) + (red[2][i] + red[3][i]);
+  }
+}
+
 // ---------------------------------------------------------------------------
 // Softmax cross-entropy: loss_r = logsumexp(z_r) - z_r[y_r]; one wave per
 // row, online max/sum per lane then combined across the wave.
@@ -348,25 +400,27 @@ static int rows_grid(int N) {
 }
 
 template <typename T>
-static void ln_fwd_t(const void* x, const float* w, const float* b, void* y, float* mean, float* rstd, int N, int C,
-                     float eps, hipStream_t s) {
+static void ln_fwd_t(const void* x, const void* r, const float* w, const float* b, void* y, void* sum, float* mean,
+                     float* rstd, int N, int C, float eps, hipStream_t s) {
   const dim3 grid(rows_grid(N)), blk(256);
   const T* xp = static_cast<const T*>(x);
+  const T* rp = static_cast<const T*>(r);
   T* yp = static_cast<T*>(y);
+  T* sp = static_cast<T*>(sum);
   if (C <= 512)
-    hipLaunchKernelGGL((ln_fwd_kernel<T, 1>), grid, blk, 0, s, xp, w, b, yp, mean, rstd, N, C, eps);
+    hipLaunchKernelGGL((ln_fwd_kernel<T, 1>), grid, blk, 0, s, xp, rp, w, b, yp, sp, mean, rstd, N, C, eps);
   else if (C <= 1024)
-    hipLaunchKernelGGL((ln_fwd_kernel<T, 2>), grid, blk, 0, s, xp, w, b, yp, mean, rstd, N, C, eps);
+    hipLaunchKernelGGL((ln_fwd_kernel<T, 2>), grid, blk, 0, s, xp, rp, w, b, yp, sp, mean, rstd, N, C, eps);
   else
-    hipLaunchKernelGGL((ln_fwd_kernel<T, 4>), grid, blk, 0, s, xp, w, b, yp, mean, rstd, N, C, eps);
+    hipLaunchKernelGGL((ln_fwd_kernel<T, 4>), grid, blk, 0, s, xp, rp, w, b, yp, sp, mean, rstd, N, C, eps);
 }
 
-void layer_norm_fwd(bool bf16, const void* x, const float* w, const float* b, void* y, float* mean, float* rstd,
-                    int N, int C, float eps, hipStream_t s) {
+void layer_norm_fwd(bool bf16, const void* x, const void* residual, const float* w, const float* b, void* y,
+                    void* sum, float* mean, float* rstd, int N, int C, float eps, hipStream_t s) {
   if (bf16)
-    ln_fwd_t<uint16_t>(x, w, b, y, mean, rstd, N, C, eps, s);
+    ln_fwd_t<uint16_t>(x, residual, w, b, y, sum, mean, rstd, N, C, eps, s);
   else
-    ln_fwd_t<float>(x, w, b, y, mean, rstd, N, C, eps, s);
+    ln_fwd_t<float>(x, residual, w, b, y, sum, mean, rstd, N, C, eps, s);
 }
 
 int layer_norm_bwd_blocks(int N) {
@@ -378,8 +432,10 @@ int layer_norm_bwd_blocks(int N) {
 }
 
 template <typename T>
-static void ln_bwd_t(const void* dy, const void* x, const float* w, const float* mean, const float* rstd, void* dx,
-                     float* pdw, float* pdb, float* dw, float* db, int N, int C, hipStream_t s) {
+static void ln_bwd_t(const void* dy, const void* x, const float* w, const float* mean, const float* rstd,
+                     const void* gsum, void* dx, float* pdw, float* pdb, float* dw, float* db, int N, int C,
+                     hipStream_t s) {
+  const T* gp = static_cast<const T*>(gsum);
   const int G = layer_norm_bwd_blocks(N);
   const dim3 grid(G), blk(256);
   const size_t lds = size_t(2) * C * sizeof(float);
@@ -387,20 +443,21 @@ static void ln_bwd_t(const void* dy, const void* x, const float* w, const float*
   const T* xp = static_cast<const T*>(x);
   T* dxp = static_cast<T*>(dx);
   if (C <= 512)
-    hipLaunchKernelGGL((ln_bwd_kernel<T, 1>), grid, blk, lds, s, dyp, xp, w, mean, rstd, dxp, pdw, pdb, N, C);
+    hipLaunchKernelGGL((ln_bwd_kernel<T, 1>), grid, blk, lds, s, dyp, xp, w, mean, rstd, gp, dxp, pdw, pdb, N, C);
   else if (C <= 1024)
-    hipLaunchKernelGGL((ln_bwd_kernel<T, 2>), grid, blk, lds, s, dyp, xp, w, mean, rstd, dxp, pdw, pdb, N, C);
+    hipLaunchKernelGGL((ln_bwd_kernel<T, 2>), grid, blk, lds, s, dyp, xp, w, mean, rstd, gp, dxp, pdw, pdb, N, C);
   else
-    hipLaunchKernelGGL((ln_bwd_kernel<T, 4>), grid, blk, lds, s, dyp, xp, w, mean, rstd, dxp, pdw, pdb, N, C);
+    hipLaunchKernelGGL((ln_bwd_kernel<T, 4>), grid, blk, lds, s, dyp, xp, w, mean, rstd, gp, dxp, pdw, pdb, N, C);
   hipLaunchKernelGGL(col_reduce_kernel, dim3((C + 63) / 64), blk, 0, s, pdw, dw, pdb, db, G, C);
 }
 
 void layer_norm_bwd(bool bf16, const void* dy, const void* x, const float* w, const float* mean, const float* rstd,
-                    void* dx, float* pdw, float* pdb, float* dw, float* db, int N, int C, hipStream_t s) {
+                    const void* gsum, void* dx, float* pdw, float* pdb, float* dw, float* db, int N, int C,
+                    hipStream_t s) {
   if (bf16)
-    ln_bwd_t<uint16_t>(dy, x, w, mean, rstd, dx, pdw, pdb, dw, db, N, C, s);
+    ln_bwd_t<uint16_t>(dy, x, w, mean, rstd, gsum, dx, pdw, pdb, dw, db, N, C, s);
   else
-    ln_bwd_t<float>(dy, x, w, mean, rstd, dx, pdw, pdb, dw, db, N, C, s);
+    ln_bwd_t<float>(dy, x, w, mean, rstd, gsum, dx, pdw, pdb, dw, db, N, C, s);
 }
 
 void bias_gelu_fwd(bool bf16, const void* x, const float* b, void* y, int64_t n, int H, hipStream_t s) {
@@ -430,6 +487,16 @@ void bias_gelu_bwd(bool bf16, const void* dy, const void* x, const float* b, voi
     hipLaunchKernelGGL(bias_gelu_bwd_kernel<float>, grid, blk, 0, s, static_cast<const float*>(dy),
                        static_cast<const float*>(x), b, static_cast<float*>(dx), pdb, N, H);
   hipLaunchKernelGGL(col_reduce_kernel, dim3((H + 63) / 64), blk, 0, s, pdb, db, nullptr, nullptr, S, H);
+}
+
+void column_sum(bool bf16, const void* dy, float* part, float* out, int N, int H, hipStream_t s) {
+  const int S = bias_gelu_bwd_splits(N);
+  const dim3 grid((H + 511) / 512, S), blk(256);
+  if (bf16)
+    hipLaunchKernelGGL(colsum_kernel<uint16_t>, grid, blk, 0, s, static_cast<const uint16_t*>(dy), part, N, H);
+  else
+    hipLaunchKernelGGL(colsum_kernel<float>, grid, blk, 0, s, static_cast<const float*>(dy), part, N, H);
+  hipLaunchKernelGGL(col_reduce_kernel, dim3((H + 63) / 64), blk, 0, s, part, out, nullptr, nullptr, S, H);
 }
 
 void xent_fwd(bool bf16, const void* z, const int64_t* y, float* loss, float* lse, int N, int K, hipStream_t s) {

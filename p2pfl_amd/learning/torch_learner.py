@@ -68,6 +68,10 @@ class TorchLearner(NodeLearner):
             # Without it several ResNet shapes fall back to MIOpen's naive
             # kernels (77 % of a ResNet-18 round on MI355X).
             torch.backends.cudnn.benchmark = True
+            # pre-tuned hipBLASLt/rocBLAS GEMM selections (p2pfl_amd/tuning)
+            from p2pfl_amd.tuning import enable_tuned_gemms
+
+            enable_tuned_gemms()
         self.precision = precision or ("bf16" if self.device.type == "cuda" else "fp32")
         self.log_every_n_steps = log_every_n_steps
         self.fused_optimizer = fused_optimizer

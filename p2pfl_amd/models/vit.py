@@ -49,9 +49,8 @@ class Mlp(nn.Module):
     def forward(self, x: torch.Tensor) -> torch.Tensor:
         if _fused(x):
             h = ops.bias_gelu(torch.matmul(x, self.fc1.weight.t().to(x.dtype)), self.fc1.bias)
-        else:
-            h = nn.functional.gelu(self.fc1(x))
-        return self.fc2(h)
+            return ops.linear(h, self.fc2.weight, self.fc2.bias)
+        return self.fc2(nn.functional.gelu(self.fc1(x)))
 
 
 class Attention(nn.Module):
@@ -63,11 +62,11 @@ class Attention(nn.Module):
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
         B, T, C = x.shape
-        qkv = self.qkv(x)
-        if _fused(qkv):
+        if _fused(x):
             # HIP kernel on the [B, T, 3C] projection: no head permute / transpose copies
-            return self.proj(ops.attention_qkv(qkv, self.heads))
-        qkv = qkv.view(B, T, 3, self.heads, C // self.heads).permute(2, 0, 3, 1, 4)
+            qkv = ops.linear(x, self.qkv.weight, self.qkv.bias)
+            return ops.linear(ops.attention_qkv(qkv, self.heads), self.proj.weight, self.proj.bias)
+        qkv = self.qkv(x).view(B, T, 3, self.heads, C // self.heads).permute(2, 0, 3, 1, 4)
         y = nn.functional.scaled_dot_product_attention(qkv[0], qkv[1], qkv[2])
         return self.proj(y.transpose(1, 2).reshape(B, T, C))
 
@@ -125,8 +124,25 @@ class ViT(FLModule):
             x = x.float().mul_(1.0 / 255.0)
         x = self._patchify_embed(x)
         x = torch.cat([self.cls_token.expand(x.shape[0], -1, -1).to(x.dtype), x], dim=1) + self.pos_embed.to(x.dtype)
+        if _fused(x):
+            return ops.linear(self._encoder_fused(x)[:, 0], self.head.weight, self.head.bias)
         x = self.norm(self.blocks(x))
         return self.head(x[:, 0])
+
+    def _encoder_fused(self, h: torch.Tensor) -> torch.Tensor:
+        """The block stack with every residual add fused into the following LayerNorm.
+
+        ``h`` is the residual stream; ``add_layer_norm`` returns the new stream
+        and its normalisation (norm2 of the same block, or norm1 of the next /
+        the final norm), so no separate add kernel runs forward or backward.
+        """
+        blocks = list(self.blocks)
+        y = blocks[0].norm1(h)
+        for i, blk in enumerate(blocks):
+            h, y = ops.add_layer_norm(h, blk.attn(y), blk.norm2.weight, blk.norm2.bias, blk.norm2.eps)
+            nxt = blocks[i + 1].norm1 if i + 1 < len(blocks) else self.norm
+            h, y = ops.add_layer_norm(h, blk.mlp(y), nxt.weight, nxt.bias, nxt.eps)
+        return y
 
     def _patchify_embed(self, x: torch.Tensor) -> torch.Tensor:
         """Conv2d(C, D, P, stride=P) as patchify + one GEMM (identical math).
@@ -140,6 +156,8 @@ class ViT(FLModule):
         D, C, P, _ = w.shape
         B, _, H, W = x.shape
         patches = x.view(B, C, H // P, P, W // P, P).permute(0, 2, 4, 1, 3, 5).reshape(B, (H // P) * (W // P), C * P * P)
+        if _fused(patches):
+            return ops.linear(patches, w.view(D, C * P * P), self.patch_embed.bias)
         return nn.functional.linear(patches, w.view(D, C * P * P), self.patch_embed.bias)
 
     def loss_fn(self, out: torch.Tensor, y: torch.Tensor) -> torch.Tensor:

@@ -183,12 +183,15 @@ def sgd_mt_step(p, buf, grads, mt, *, lr, momentum=0.0, dampening=0.0, weight_de
 # fused transformer / classifier ops (csrc/fused_ops.hip)
 # ----------------------------------------------------------------------------
 from p2pfl_amd.ops.fused import (  # noqa: E402
+    add_layer_norm,
+    add_layer_norm_reference,
     attention_qkv,
     attention_qkv_reference,
     bias_gelu,
     bias_gelu_reference,
     layer_norm,
     layer_norm_reference,
+    linear,
     softmax_xent,
     softmax_xent_reference,
 )

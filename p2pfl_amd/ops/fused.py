@@ -80,6 +80,78 @@ def layer_norm(x: torch.Tensor, weight: torch.Tensor, bias: torch.Tensor, eps: f
     return F.layer_norm(x, (C,), weight, bias, eps)
 
 
+# -- residual add + LayerNorm -----------------------------------------------------
+class _AddLayerNorm(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, r, w, b, eps):
+        shape = x.shape
+        x2 = x.reshape(-1, shape[-1]).contiguous()
+        r2 = r.reshape(x2.shape).to(x2.dtype).contiguous()
+        y, mean, rstd, s = _fx().ln_fwd(x2, w.contiguous(), b.contiguous(), float(eps), r2)
+        ctx.save_for_backward(s, w, mean, rstd)
+        ctx.shape = shape
+        return s.view(shape), y.view(shape)
+
+    @staticmethod
+    def backward(ctx, gs, dy):
+        s, w, mean, rstd = ctx.saved_tensors
+        if dy is None:
+            dy = torch.zeros_like(s)
+        dy2 = dy.reshape(s.shape).to(s.dtype).contiguous()
+        gs2 = gs.reshape(s.shape).to(s.dtype).contiguous() if gs is not None else None
+        dx, dw, db = _fx().ln_bwd(dy2, s, w.contiguous(), mean, rstd, gs2)
+        dx = dx.view(ctx.shape)
+        return dx, dx, dw.to(w.dtype), db.to(w.dtype), None
+
+
+def add_layer_norm_reference(x, r, w, b, eps):
+    s = (x + r).to(x.dtype)
+    return s, F.layer_norm(s.float(), (x.shape[-1],), w.float(), b.float(), eps).to(x.dtype)
+
+
+def add_layer_norm(x: torch.Tensor, r: torch.Tensor, weight: torch.Tensor, bias: torch.Tensor, eps: float = 1e-5):
+    """``s = x + r; return s, LayerNorm(s)`` in one pass (one pass back: dx = dr = ds + LN'(dy))."""
+    C = x.shape[-1]
+    if _native(x) and r.shape == x.shape and weight.dtype == torch.float32 and C % 8 == 0 and C <= 2048:
+        return _AddLayerNorm.apply(x, r, weight, bias, eps)
+    s = x + r
+    return s, F.layer_norm(s, (C,), weight, bias, eps)
+
+
+# -- linear with a fused bias gradient -------------------------------------------------
+class _Linear(torch.autograd.Function):
+    @staticmethod
+    @torch.amp.custom_fwd(device_type="cuda", cast_inputs=torch.bfloat16)
+    def forward(ctx, x, w, b):
+        ctx.save_for_backward(x, w)
+        ctx.has_bias = b is not None
+        ctx.bias_dtype = b.dtype if b is not None else None
+        return F.linear(x, w, b)
+
+    @staticmethod
+    @torch.amp.custom_bwd(device_type="cuda")
+    def backward(ctx, dy):
+        x, w = ctx.saved_tensors
+        dy2 = dy.reshape(-1, dy.shape[-1])
+        if not dy2.is_contiguous():
+            dy2 = dy2.contiguous()
+        dx = dw = db = None
+        if ctx.needs_input_grad[0]:
+            dx = torch.mm(dy2, w).view(*dy.shape[:-1], w.shape[1])
+        if ctx.needs_input_grad[1]:
+            dw = torch.mm(dy2.t(), x.reshape(-1, x.shape[-1]))
+        if ctx.has_bias and ctx.needs_input_grad[2]:
+            db = _fx().column_sum(dy2).to(ctx.bias_dtype)  # one streaming pass, not a generic reduce
+        return dx, dw, db
+
+
+def linear(x: torch.Tensor, weight: torch.Tensor, bias=None) -> torch.Tensor:
+    """``F.linear`` whose backward computes the bias gradient with the column-sum kernel."""
+    if _native(x) and bias is not None and weight.shape[0] % 8 == 0:
+        return _Linear.apply(x, weight, bias)
+    return F.linear(x, weight, bias)
+
+
 # -- bias + GELU ----------------------------------------------------------------
 class _BiasGelu(torch.autograd.Function):
     @staticmethod

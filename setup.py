@@ -58,8 +58,19 @@ def hip_objects():
         return list(ex.map(_compile_one, srcs))
 
 
+def host_libs():
+    """Plain C ABI host libraries (no torch / HIP), loaded with ctypes."""
+    src = os.path.join(HERE, "csrc", "host", "wire_frame.cpp")
+    out = os.path.join(HERE, "p2pfl_amd", "_p2fa.so")
+    if not os.path.exists(out) or os.path.getmtime(out) < max(os.path.getmtime(src), os.path.getmtime(src[:-4] + ".h")):
+        cmd = ["g++", "-O2", "-std=c++17", "-fPIC", "-shared", "-Wall", "-Wextra", src, "-o", out]
+        print(" ".join(cmd), flush=True)
+        subprocess.check_call(cmd)
+
+
 class HipBuild(BuildExtension):
     def build_extensions(self):
+        host_libs()
         objs = hip_objects()
         for ext in self.extensions:
             ext.extra_objects = list(ext.extra_objects or []) + objs
@@ -70,6 +81,7 @@ setup(
     name="p2pfl_amd",
     version="0.1.0",
     packages=find_packages(include=["p2pfl_amd", "p2pfl_amd.*"]),
+    package_data={"p2pfl_amd.tuning": ["*.csv"], "p2pfl_amd": ["_p2fa.so"]},
     ext_modules=[
         CppExtension(
             "p2pfl_amd._C",

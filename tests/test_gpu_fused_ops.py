@@ -135,3 +135,43 @@ def test_attention_rejects_unsupported_shapes():
     # the Python entry point falls back to SDPA for such shapes
     y = ops.attention_qkv(torch.randn(1, 300, 3 * 64, device="cuda", dtype=torch.bfloat16), 1)
     assert y.shape == (1, 300, 64)
+
+
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
+@pytest.mark.parametrize("N,C", [(394, 768), (7, 192), (33, 1024)])
+def test_add_layer_norm_fwd_bwd(dtype, N, C):
+    """Fused residual add + LayerNorm vs separate add then fp32 LayerNorm."""
+    x = _inputs((N, C), dtype, 11).requires_grad_(True)
+    r = _inputs((N, C), dtype, 12).requires_grad_(True)
+    w = (torch.rand(C, device="cuda") + 0.5).requires_grad_(True)
+    b = torch.randn(C, device="cuda").requires_grad_(True)
+    s, y = ops.add_layer_norm(x, r, w, b, 1e-6)
+    xr, rr = x.detach().clone().requires_grad_(True), r.detach().clone().requires_grad_(True)
+    wr, br = w.detach().clone().requires_grad_(True), b.detach().clone().requires_grad_(True)
+    sr = (xr + rr).to(dtype)
+    yr = torch.nn.functional.layer_norm(sr.float(), (C,), wr, br, 1e-6)
+    tol = 2e-2 if dtype == torch.bfloat16 else 1e-4
+    torch.testing.assert_close(s, sr, atol=0, rtol=0)
+    torch.testing.assert_close(y.float(), yr, atol=tol * 4, rtol=tol)
+    gs, gy = _inputs((N, C), dtype, 13), _inputs((N, C), dtype, 14)
+    torch.autograd.backward([s, y], [gs, gy])
+    torch.autograd.backward([sr, yr], [gs, gy.float()])
+    for a, e in ((x.grad, xr.grad), (r.grad, rr.grad), (w.grad, wr.grad), (b.grad, br.grad)):
+        err = (a.float() - e.float()).abs().max().item() / max(e.float().abs().max().item(), 1e-6)
+        assert err < (3e-2 if dtype == torch.bfloat16 else 1e-4), err
+
+
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
+def test_linear_fused_bias_grad(dtype):
+    torch.manual_seed(5)
+    x = torch.randn(4, 197, 768, device="cuda", dtype=dtype, requires_grad=True)
+    w = (torch.randn(2304, 768, device="cuda") * 0.02).to(dtype).requires_grad_(True)
+    b = torch.randn(2304, device="cuda", dtype=dtype, requires_grad=True)
+    y = ops.linear(x, w, b)
+    ref = torch.nn.functional.linear(x.detach().float().requires_grad_(True), w.detach().float().requires_grad_(True), b.detach().float().requires_grad_(True))
+    torch.testing.assert_close(y.float(), ref, atol=5e-2, rtol=2e-2)
+    g = torch.randn_like(y)
+    y.backward(g)
+    col = g.float().reshape(-1, 2304).sum(0)
+    torch.testing.assert_close(b.grad.float(), col, atol=1e-1 if dtype == torch.bfloat16 else 1e-3, rtol=1e-2)
+    torch.testing.assert_close(ops.ext().fused.column_sum(g.reshape(-1, 2304).contiguous()), col, atol=1e-2, rtol=1e-4)
