@@ -232,7 +232,7 @@ def main() -> None:
         k = len(h)
         print(
             f"[bench rank {env.rank}] per-round phases (mean of {k}): evaluate {sum(x.eval_s for x in h) / k * 1e3:.2f} ms, "
-            f"fit {sum(x.fit_s for x in h) / k * 1e3:.2f} ms, fedavg+load {sum(x.agg_s for x in h) / k * 1e3:.2f} ms",
+            f"fit {sum(x.fit_s for x in h) / k * 1e3:.2f} ms, fedavg+load (+overlapped val) {sum(x.agg_s for x in h) / k * 1e3:.2f} ms",
             file=sys.stderr,
             flush=True,
         )

@@ -1,0 +1,440 @@
+// Fused BatchNorm (+ residual add) (+ ReLU) for MI355X (gfx950, wave64), on
+// channels-last activations viewed as [M, C] (M = N*H*W rows of C channels).
+//
+// What it replaces in a ResNet block (PyTorch-ROCm, NHWC bf16):
+//   forward   MIOpen BN training kernel(s) + residual add + ReLU     (3+ passes)
+//   backward  ReLU threshold_backward + MIOpen BN backward           (3+ passes)
+// Here, per BN:
+//   forward   stats (1 read of x)  -> finalize (C threads) -> apply (read x [+res], write y)
+//   backward  stats (read dy, y, x) -> finalize              -> apply (read dy, y, x, write dx [+dres])
+//
+// Column statistics: every thread owns 8 consecutive channels (one 16-B bf16
+// load per row), a 256-thread block covers `tpr` threads per row x `rp` row
+// phases, row splits go over gridDim.y.  Per-block sums are combined across
+// row phases in LDS in fixed order and written as [S, C] partials; the
+// finalize kernel reduces the S partials in fixed order.  No float atomics:
+// results are bitwise reproducible run to run.  Forward statistics use sums
+// shifted by the first row's value (x - x[0][c]) so the variance does not
+// cancel for activations with a large mean.
+#include "batchnorm.h"
+#include "common.h"
+
+namespace p2bn {
+using namespace p2;
+
+template <typename T>
+struct V8;
+template <>
+struct V8<uint16_t> {
+  static P2_DEVICE void load(const uint16_t* p, float (&v)[8]) {
+    const uint4 u = *reinterpret_cast<const uint4*>(p);
+    const uint32_t w[4] = {u.x, u.y, u.z, u.w};
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      v[2 * j] = __uint_as_float(w[j] << 16);
+      v[2 * j + 1] = __uint_as_float(w[j] & 0xffff0000u);
+    }
+  }
+  static P2_DEVICE void store(uint16_t* p, const float (&v)[8]) {
+    uint4 u;
+    u.x = pack_bf16x2(v[0], v[1]);
+    u.y = pack_bf16x2(v[2], v[3]);
+    u.z = pack_bf16x2(v[4], v[5]);
+    u.w = pack_bf16x2(v[6], v[7]);
+    *reinterpret_cast<uint4*>(p) = u;
+  }
+  static P2_DEVICE float one(const uint16_t* p) { return bf16_to_f32(*p); }
+};
+template <>
+struct V8<float> {
+  static P2_DEVICE void load(const float* p, float (&v)[8]) {
+    const float4 a = reinterpret_cast<const float4*>(p)[0], b = reinterpret_cast<const float4*>(p)[1];
+    v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w;
+    v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
+  }
+  static P2_DEVICE void store(float* p, const float (&v)[8]) {
+    reinterpret_cast<float4*>(p)[0] = make_float4(v[0], v[1], v[2], v[3]);
+    reinterpret_cast<float4*>(p)[1] = make_float4(v[4], v[5], v[6], v[7]);
+  }
+  static P2_DEVICE float one(const float* p) { return *p; }
+};
+P2_DEVICE void ld8f(const float* p, float (&v)[8]) { V8<float>::load(p, v); }
+
+constexpr int kThreads = 256;
+constexpr int kRedCols = kThreads * 8;  // LDS columns of one phase-reduction slab
+
+// ---------------------------------------------------------------------------
+// Block-level fixed-order reduction of two per-thread [8] accumulators over
+// the rp row phases, written as row blockIdx.y of the [S, C] partials a / b.
+// ---------------------------------------------------------------------------
+P2_DEVICE void phase_reduce_store(float (&s1)[8], float (&s2)[8], bool active, int tg, int ph, int tpr, int rp,
+                                  float* __restrict__ part, int C) {
+  __shared__ float red[2][kRedCols];
+  const int width = tpr * 8;  // columns of this block
+  if (active) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      red[0][ph * width + tg * 8 + j] = s1[j];
+      red[1][ph * width + tg * 8 + j] = s2[j];
+    }
+  }
+  __syncthreads();
+  const int S = gridDim.y;
+  for (int i = threadIdx.x; i < width; i += kThreads) {
+    const int c = blockIdx.x * width + i;
+    if (c >= C) continue;
+    float a = 0.f, b = 0.f;
+    for (int p = 0; p < rp; ++p) {
+      a += red[0][p * width + i];
+      b += red[1][p * width + i];
+    }
+    part[size_t(blockIdx.y) * C + c] = a;
+    part[size_t(S + blockIdx.y) * C + c] = b;
+  }
+}
+
+// forward statistics: sum (x - x0) and sum (x - x0)^2 per channel
+template <typename T>
+__global__ __launch_bounds__(kThreads) void bn_stats_kernel(const T* __restrict__ x, float* __restrict__ part, int M,
+                                                            int C, int tpr, int rp) {
+  const int tg = threadIdx.x % tpr, ph = threadIdx.x / tpr;
+  const int c = (blockIdx.x * tpr + tg) * 8;
+  const bool active = ph < rp && c < C;
+  float s1[8], s2[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) s1[j] = s2[j] = 0.f;
+  if (active) {
+    float sh[8];
+    V8<T>::load(x + c, sh);
+    const int step = rp * gridDim.y;
+    int r = blockIdx.y * rp + ph;
+    // two rows in flight per iteration
+    for (; r + step < M; r += 2 * step) {
+      float v0[8], v1[8];
+      V8<T>::load(x + size_t(r) * C + c, v0);
+      V8<T>::load(x + size_t(r + step) * C + c, v1);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const float d0 = v0[j] - sh[j], d1 = v1[j] - sh[j];
+        s1[j] += d0;
+        s2[j] = fmaf(d0, d0, s2[j]);
+        s1[j] += d1;
+        s2[j] = fmaf(d1, d1, s2[j]);
+      }
+    }
+    if (r < M) {
+      float v0[8];
+      V8<T>::load(x + size_t(r) * C + c, v0);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const float d0 = v0[j] - sh[j];
+        s1[j] += d0;
+        s2[j] = fmaf(d0, d0, s2[j]);
+      }
+    }
+  }
+  phase_reduce_store(s1, s2, active, tg, ph, tpr, rp, part, C);
+}
+
+// backward statistics: sum dz and sum dz * (x - mean) per channel
+template <typename T, bool RELU>
+__global__ __launch_bounds__(kThreads) void bn_bwd_stats_kernel(const T* __restrict__ dy, const T* __restrict__ y,
+                                                                const T* __restrict__ x,
+                                                                const float* __restrict__ mean,
+                                                                float* __restrict__ part, int M, int C, int tpr,
+                                                                int rp) {
+  const int tg = threadIdx.x % tpr, ph = threadIdx.x / tpr;
+  const int c = (blockIdx.x * tpr + tg) * 8;
+  const bool active = ph < rp && c < C;
+  float s1[8], s2[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) s1[j] = s2[j] = 0.f;
+  if (active) {
+    float mu[8];
+    ld8f(mean + c, mu);
+    const int step = rp * gridDim.y;
+    for (int r = blockIdx.y * rp + ph; r < M; r += step) {
+      const size_t e = size_t(r) * C + c;
+      float g[8], xv[8];
+      V8<T>::load(dy + e, g);
+      V8<T>::load(x + e, xv);
+      if (RELU) {
+        float yv[8];
+        V8<T>::load(y + e, yv);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) g[j] = yv[j] > 0.f ? g[j] : 0.f;
+      }
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        s1[j] += g[j];
+        s2[j] = fmaf(g[j], xv[j] - mu[j], s2[j]);
+      }
+    }
+  }
+  phase_reduce_store(s1, s2, active, tg, ph, tpr, rp, part, C);
+}
+
+// ---------------------------------------------------------------------------
+// Finalize: block = 64 channels x 4 partial-row phases, fixed-order sums.
+// ---------------------------------------------------------------------------
+P2_DEVICE void reduce_parts(const float* __restrict__ part, int S, int C, int c, float& a, float& b) {
+  __shared__ float red[2][4][64];
+  const int lane = threadIdx.x & 63, q = threadIdx.x >> 6;
+  float sa = 0.f, sb = 0.f;
+  if (c < C) {
+    for (int r0 = q; r0 < S; r0 += 4 * 4) {
+      float ta[4], tb[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int r = r0 + 4 * u;
+        ta[u] = r < S ? part[size_t(r) * C + c] : 0.f;
+        tb[u] = r < S ? part[size_t(S + r) * C + c] : 0.f;
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        sa += ta[u];
+        sb += tb[u];
+      }
+    }
+  }
+  red[0][q][lane] = sa;
+  red[1][q][lane] = sb;
+  __syncthreads();
+  a = (red[0][0][lane] + red[0][1][lane]) + (red[0][2][lane] + red[0][3][lane]);
+  b = (red[1][0][lane] + red[1][1][lane]) + (red[1][2][lane] + red[1][3][lane]);
+}
+
+template <typename T>
+__global__ __launch_bounds__(kThreads) void bn_finalize_fwd_kernel(
+    const float* __restrict__ part, int S, const T* __restrict__ x, const float* __restrict__ w,
+    const float* __restrict__ b, float* __restrict__ run_mean, float* __restrict__ run_var, int64_t* __restrict__ nbt,
+    float momentum, float eps, float* __restrict__ mean_out, float* __restrict__ rstd_out, float* __restrict__ coef,
+    int M, int C) {
+  const int c = blockIdx.x * 64 + (threadIdx.x & 63);
+  float s1, s2;
+  reduce_parts(part, S, C, c, s1, s2);
+  if (threadIdx.x >= 64 || c >= C) return;
+  const float inv_m = 1.f / float(M);
+  const float ms = s1 * inv_m;
+  const float var = fmaxf(s2 * inv_m - ms * ms, 0.f);
+  const float mu = V8<T>::one(x + c) + ms;
+  const float rs = rsqrtf(var + eps);
+  mean_out[c] = mu;
+  rstd_out[c] = rs;
+  const float sc = w[c] * rs;
+  coef[c] = sc;
+  coef[C + c] = b[c] - mu * sc;
+  if (run_mean) {
+    const float unb = M > 1 ? var * (float(M) / float(M - 1)) : var;
+    run_mean[c] = (1.f - momentum) * run_mean[c] + momentum * mu;
+    run_var[c] = (1.f - momentum) * run_var[c] + momentum * unb;
+  }
+  if (nbt && c == 0) nbt[0] += 1;
+}
+
+__global__ __launch_bounds__(kThreads) void bn_finalize_eval_kernel(const float* __restrict__ w,
+                                                                    const float* __restrict__ b,
+                                                                    const float* __restrict__ rm,
+                                                                    const float* __restrict__ rv, float eps,
+                                                                    float* __restrict__ coef, int C) {
+  const int c = blockIdx.x * kThreads + threadIdx.x;
+  if (c >= C) return;
+  const float sc = w[c] * rsqrtf(rv[c] + eps);
+  coef[c] = sc;
+  coef[C + c] = b[c] - rm[c] * sc;
+}
+
+// coef = [A | B | D]: dx = A dz + B (x - mean) + D;  dw = rstd * s2, db = s1
+__global__ __launch_bounds__(kThreads) void bn_finalize_bwd_kernel(const float* __restrict__ part, int S,
+                                                                   const float* __restrict__ w,
+                                                                   const float* __restrict__ rstd,
+                                                                   float* __restrict__ dw, float* __restrict__ db,
+                                                                   float* __restrict__ coef, int M, int C) {
+  const int c = blockIdx.x * 64 + (threadIdx.x & 63);
+  float s1, s2;
+  reduce_parts(part, S, C, c, s1, s2);
+  if (threadIdx.x >= 64 || c >= C) return;
+  const float rs = rstd[c], inv_m = 1.f / float(M);
+  const float A = w[c] * rs;
+  db[c] = s1;
+  dw[c] = s2 * rs;
+  coef[c] = A;
+  coef[C + c] = -A * rs * rs * s2 * inv_m;
+  coef[2 * C + c] = -A * s1 * inv_m;
+}
+
+// ---------------------------------------------------------------------------
+// Apply passes: 8 channels per thread, grid-stride over the [M, C] matrix.
+// ---------------------------------------------------------------------------
+template <typename T, bool RELU, bool RES>
+__global__ __launch_bounds__(kThreads) void bn_apply_fwd_kernel(const T* __restrict__ x, const T* __restrict__ res,
+                                                                const float* __restrict__ coef, T* __restrict__ y,
+                                                                int64_t n8, int C) {
+  for (int64_t i = blockIdx.x * int64_t(kThreads) + threadIdx.x; i < n8; i += int64_t(gridDim.x) * kThreads) {
+    const int64_t e = i * 8;
+    const int c = int(e % C);
+    float v[8], sc[8], sh[8];
+    V8<T>::load(x + e, v);
+    ld8f(coef + c, sc);
+    ld8f(coef + C + c, sh);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] = fmaf(v[j], sc[j], sh[j]);
+    if (RES) {
+      float r[8];
+      V8<T>::load(res + e, r);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[j] += r[j];
+    }
+    if (RELU) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[j] = fmaxf(v[j], 0.f);
+    }
+    V8<T>::store(y + e, v);
+  }
+}
+
+template <typename T, bool RELU, bool RES>
+__global__ __launch_bounds__(kThreads) void bn_apply_bwd_kernel(const T* __restrict__ dy, const T* __restrict__ y,
+                                                                const T* __restrict__ x,
+                                                                const float* __restrict__ mean,
+                                                                const float* __restrict__ coef, T* __restrict__ dx,
+                                                                T* __restrict__ dres, int64_t n8, int C) {
+  for (int64_t i = blockIdx.x * int64_t(kThreads) + threadIdx.x; i < n8; i += int64_t(gridDim.x) * kThreads) {
+    const int64_t e = i * 8;
+    const int c = int(e % C);
+    float g[8], xv[8], mu[8], A[8], B[8], D[8];
+    V8<T>::load(dy + e, g);
+    V8<T>::load(x + e, xv);
+    if (RELU) {
+      float yv[8];
+      V8<T>::load(y + e, yv);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) g[j] = yv[j] > 0.f ? g[j] : 0.f;
+    }
+    ld8f(mean + c, mu);
+    ld8f(coef + c, A);
+    ld8f(coef + C + c, B);
+    ld8f(coef + 2 * C + c, D);
+    if (RES) V8<T>::store(dres + e, g);
+    float o[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) o[j] = fmaf(A[j], g[j], fmaf(B[j], xv[j] - mu[j], D[j]));
+    V8<T>::store(dx + e, o);
+  }
+}
+
+// ---------------------------------------------------------------------------
+// launchers
+// ---------------------------------------------------------------------------
+BnPlan bn_plan(int M, int C) {
+  BnPlan p{};
+  const int groups = C / 8;
+  p.tpr = groups < kThreads ? groups : kThreads;
+  p.rp = kThreads / p.tpr;
+  p.gx = (groups + p.tpr - 1) / p.tpr;
+  // >= 4 rows per thread, <= 256 row splits, <= ~1024 blocks in total
+  int S = (M + 4 * p.rp - 1) / (4 * p.rp);
+  const int cap = 1024 / p.gx > 256 ? 256 : (1024 / p.gx < 1 ? 1 : 1024 / p.gx);
+  if (S > cap) S = cap;
+  p.S = S < 1 ? 1 : S;
+  return p;
+}
+
+template <typename T>
+static void fwd_train_t(const void* xv, const void* rv, const float* w, const float* b, float* rm, float* rvar,
+                        int64_t* nbt, float momentum, float eps, void* yv, float* mean, float* rstd, float* coef,
+                        float* part, int M, int C, bool relu, hipStream_t s) {
+  const T* x = static_cast<const T*>(xv);
+  const T* r = static_cast<const T*>(rv);
+  T* y = static_cast<T*>(yv);
+  const BnPlan p = bn_plan(M, C);
+  hipLaunchKernelGGL(bn_stats_kernel<T>, dim3(p.gx, p.S), dim3(kThreads), 0, s, x, part, M, C, p.tpr, p.rp);
+  hipLaunchKernelGGL(bn_finalize_fwd_kernel<T>, dim3((C + 63) / 64), dim3(kThreads), 0, s, part, p.S, x, w, b, rm,
+                     rvar, nbt, momentum, eps, mean, rstd, coef, M, C);
+  const int64_t n8 = int64_t(M) * C / 8;
+  const dim3 grid(stream_grid(n8, kThreads)), blk(kThreads);
+  if (relu && r)
+    hipLaunchKernelGGL((bn_apply_fwd_kernel<T, true, true>), grid, blk, 0, s, x, r, coef, y, n8, C);
+  else if (relu)
+    hipLaunchKernelGGL((bn_apply_fwd_kernel<T, true, false>), grid, blk, 0, s, x, r, coef, y, n8, C);
+  else if (r)
+    hipLaunchKernelGGL((bn_apply_fwd_kernel<T, false, true>), grid, blk, 0, s, x, r, coef, y, n8, C);
+  else
+    hipLaunchKernelGGL((bn_apply_fwd_kernel<T, false, false>), grid, blk, 0, s, x, r, coef, y, n8, C);
+}
+
+void bn_fwd_train(bool bf16, const void* x, const void* res, const float* w, const float* b, float* run_mean,
+                  float* run_var, int64_t* nbt, float momentum, float eps, void* y, float* mean, float* rstd,
+                  float* coef, float* part, int M, int C, bool relu, hipStream_t s) {
+  if (bf16)
+    fwd_train_t<uint16_t>(x, res, w, b, run_mean, run_var, nbt, momentum, eps, y, mean, rstd, coef, part, M, C, relu, s);
+  else
+    fwd_train_t<float>(x, res, w, b, run_mean, run_var, nbt, momentum, eps, y, mean, rstd, coef, part, M, C, relu, s);
+}
+
+template <typename T>
+static void fwd_eval_t(const void* xv, const void* rv, const float* w, const float* b, const float* rm,
+                       const float* rvar, float eps, void* yv, float* coef, int M, int C, bool relu, hipStream_t s) {
+  const T* x = static_cast<const T*>(xv);
+  const T* r = static_cast<const T*>(rv);
+  T* y = static_cast<T*>(yv);
+  hipLaunchKernelGGL(bn_finalize_eval_kernel, dim3((C + kThreads - 1) / kThreads), dim3(kThreads), 0, s, w, b, rm,
+                     rvar, eps, coef, C);
+  const int64_t n8 = int64_t(M) * C / 8;
+  const dim3 grid(stream_grid(n8, kThreads)), blk(kThreads);
+  if (relu && r)
+    hipLaunchKernelGGL((bn_apply_fwd_kernel<T, true, true>), grid, blk, 0, s, x, r, coef, y, n8, C);
+  else if (relu)
+    hipLaunchKernelGGL((bn_apply_fwd_kernel<T, true, false>), grid, blk, 0, s, x, r, coef, y, n8, C);
+  else if (r)
+    hipLaunchKernelGGL((bn_apply_fwd_kernel<T, false, true>), grid, blk, 0, s, x, r, coef, y, n8, C);
+  else
+    hipLaunchKernelGGL((bn_apply_fwd_kernel<T, false, false>), grid, blk, 0, s, x, r, coef, y, n8, C);
+}
+
+void bn_fwd_eval(bool bf16, const void* x, const void* res, const float* w, const float* b, const float* run_mean,
+                 const float* run_var, float eps, void* y, float* coef, int M, int C, bool relu, hipStream_t s) {
+  if (bf16)
+    fwd_eval_t<uint16_t>(x, res, w, b, run_mean, run_var, eps, y, coef, M, C, relu, s);
+  else
+    fwd_eval_t<float>(x, res, w, b, run_mean, run_var, eps, y, coef, M, C, relu, s);
+}
+
+template <typename T>
+static void bwd_t(const void* dyv, const void* yv, const void* xv, const float* w, const float* mean,
+                  const float* rstd, void* dxv, void* dresv, float* dw, float* db, float* coef, float* part, int M,
+                  int C, bool relu, hipStream_t s) {
+  const T* dy = static_cast<const T*>(dyv);
+  const T* y = static_cast<const T*>(yv);
+  const T* x = static_cast<const T*>(xv);
+  T* dx = static_cast<T*>(dxv);
+  T* dres = static_cast<T*>(dresv);
+  const BnPlan p = bn_plan(M, C);
+  const dim3 sgrid(p.gx, p.S), blk(kThreads);
+  if (relu)
+    hipLaunchKernelGGL((bn_bwd_stats_kernel<T, true>), sgrid, blk, 0, s, dy, y, x, mean, part, M, C, p.tpr, p.rp);
+  else
+    hipLaunchKernelGGL((bn_bwd_stats_kernel<T, false>), sgrid, blk, 0, s, dy, y, x, mean, part, M, C, p.tpr, p.rp);
+  hipLaunchKernelGGL(bn_finalize_bwd_kernel, dim3((C + 63) / 64), blk, 0, s, part, p.S, w, rstd, dw, db, coef, M, C);
+  const int64_t n8 = int64_t(M) * C / 8;
+  const dim3 grid(stream_grid(n8, kThreads));
+  if (relu && dres)
+    hipLaunchKernelGGL((bn_apply_bwd_kernel<T, true, true>), grid, blk, 0, s, dy, y, x, mean, coef, dx, dres, n8, C);
+  else if (relu)
+    hipLaunchKernelGGL((bn_apply_bwd_kernel<T, true, false>), grid, blk, 0, s, dy, y, x, mean, coef, dx, dres, n8, C);
+  else if (dres)
+    hipLaunchKernelGGL((bn_apply_bwd_kernel<T, false, true>), grid, blk, 0, s, dy, y, x, mean, coef, dx, dres, n8, C);
+  else
+    hipLaunchKernelGGL((bn_apply_bwd_kernel<T, false, false>), grid, blk, 0, s, dy, y, x, mean, coef, dx, dres, n8, C);
+}
+
+void bn_bwd(bool bf16, const void* dy, const void* y, const void* x, const float* w, const float* mean,
+            const float* rstd, void* dx, void* dres, float* dw, float* db, float* coef, float* part, int M, int C,
+            bool relu, hipStream_t s) {
+  if (bf16)
+    bwd_t<uint16_t>(dy, y, x, w, mean, rstd, dx, dres, dw, db, coef, part, M, C, relu, s);
+  else
+    bwd_t<float>(dy, y, x, w, mean, rstd, dx, dres, dw, db, coef, part, M, C, relu, s);
+}
+
+}  // namespace p2bn

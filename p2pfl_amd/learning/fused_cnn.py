@@ -279,7 +279,8 @@ class FusedCNNLearner(TorchLearner):
                     if (self._step - steps + j + 1) % every == 0:
                         self._log("train_loss", per_step[j], step=self._step - steps + j + 1)
                 self.last_train_loss = sum(float(st[j, 0]) for j in range(steps)) / n
-                self._validate()
+                if not (self.defer_final_validation and epoch == self.epochs - 1):
+                    self._validate()
 
     def _eval_pass(self, name: str, loader) -> Dict[str, float]:
         with self._lock:

@@ -79,6 +79,10 @@ class TorchLearner(NodeLearner):
         self.mixed = False
         self._interrupt = threading.Event()
         self._step = 0
+        # True: fit() skips the LAST epoch's validation pass and the caller runs
+        # validate() itself -- the round runner overlaps it with the FedAvg
+        # collective of the freshly trained weights (parallel/rounds.py)
+        self.defer_final_validation = False
         self.model: Any = None
         self.arena: Optional[ModuleArena] = None
         self.data: Any = None
@@ -246,7 +250,8 @@ class TorchLearner(NodeLearner):
                                 self._log(k, float(v), step=self._step)
                 if self.arena is not None and not self.arena.grads_bound():
                     self.arena.rebind_grads()
-                self._validate()
+                if not (self.defer_final_validation and _epoch == self.epochs - 1):
+                    self._validate()
         except Exception as e:
             logger.error(self._addr, f"Fit error: {e}")
             raise
@@ -265,6 +270,10 @@ class TorchLearner(NodeLearner):
                 sums[k] = sums.get(k, 0) + v * bs
             n += bs
         return {k: float(v) / max(1, n) for k, v in sums.items()}
+
+    def validate(self) -> None:
+        """The per-epoch validation pass (metrics to the local store)."""
+        self._validate()
 
     def _validate(self) -> None:
         loader = self.data.val_dataloader()

@@ -8,7 +8,9 @@ plus max-pool.  Inputs are uint8 images (the data modules keep datasets as
 uint8 on the device); normalisation to [0, 1] happens in ``forward``.
 
 Activations run channels-last on the GPU (MIOpen NHWC convolutions under
-bf16 autocast); weights stay NCHW views of the flat parameter arena.  Optimiser: SGD with momentum 0.9 and weight decay 5e-4 (fused
+bf16 autocast); weights stay NCHW views of the flat parameter arena.  Every
+``BatchNorm2d -> (+ shortcut) -> ReLU`` chain runs as the fused HIP kernel of
+``csrc/batchnorm.hip`` (:func:`~p2pfl_amd.ops.batchnorm.batch_norm_act`).  Optimiser: SGD with momentum 0.9 and weight decay 5e-4 (fused
 into one arena kernel by the learner), a standard federated CIFAR setup.
 """
 
@@ -21,9 +23,17 @@ import torch
 from torch import nn
 
 from p2pfl_amd.models.base import FLModule, seed_everything
+from p2pfl_amd.ops.batchnorm import batch_norm_act
 
 # NHWC activations on the GPU (P2PFL_CHANNELS_LAST=0 keeps NCHW)
 _CHANNELS_LAST = os.environ.get("P2PFL_CHANNELS_LAST", "1") != "0"
+
+
+def _shortcut(sc: nn.Module, x: torch.Tensor) -> torch.Tensor:
+    """Identity, or the projection conv + BN (no activation) through the fused BN kernel."""
+    if isinstance(sc, nn.Identity):
+        return x
+    return batch_norm_act(sc[0](x), sc[1], relu=False)
 
 
 class BasicBlock(nn.Module):
@@ -40,9 +50,8 @@ class BasicBlock(nn.Module):
             self.shortcut = nn.Sequential(nn.Conv2d(cin, cout, 1, stride, bias=False), nn.BatchNorm2d(cout))
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
-        out = torch.relu(self.bn1(self.conv1(x)))
-        out = self.bn2(self.conv2(out))
-        return torch.relu(out + self.shortcut(x))
+        out = batch_norm_act(self.conv1(x), self.bn1)
+        return batch_norm_act(self.conv2(out), self.bn2, residual=_shortcut(self.shortcut, x))
 
 
 class Bottleneck(nn.Module):
@@ -62,10 +71,9 @@ class Bottleneck(nn.Module):
             self.shortcut = nn.Sequential(nn.Conv2d(cin, cout, 1, stride, bias=False), nn.BatchNorm2d(cout))
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
-        out = torch.relu(self.bn1(self.conv1(x)))
-        out = torch.relu(self.bn2(self.conv2(out)))
-        out = self.bn3(self.conv3(out))
-        return torch.relu(out + self.shortcut(x))
+        out = batch_norm_act(self.conv1(x), self.bn1)
+        out = batch_norm_act(self.conv2(out), self.bn2)
+        return batch_norm_act(self.conv3(out), self.bn3, residual=_shortcut(self.shortcut, x))
 
 
 class ResNet(FLModule):
@@ -119,7 +127,9 @@ class ResNet(FLModule):
             x = x.float().mul_(1.0 / 255.0)
         if x.is_cuda and _CHANNELS_LAST:
             x = x.contiguous(memory_format=torch.channels_last)
-        x = self.stem(x)
+        x = batch_norm_act(self.stem[0](x), self.stem[1])
+        if len(self.stem) > 3:
+            x = self.stem[3](x)
         x = self.layer4(self.layer3(self.layer2(self.layer1(x))))
         x = torch.flatten(nn.functional.adaptive_avg_pool2d(x, 1), 1)
         return self.fc(x)

@@ -1,0 +1,107 @@
+"""Fused BatchNorm (+ residual add) (+ ReLU) on channels-last activations (``csrc/batchnorm.hip``).
+
+ResNet blocks (BASELINE.json configs 3 and 5) spend their non-convolution time
+in ``BatchNorm2d -> (+ shortcut) -> ReLU``: three elementwise-class passes
+forward and three backward on PyTorch-ROCm.  :func:`batch_norm_act` runs the
+whole chain as one column-statistics pass plus one apply pass in each
+direction, reading the NHWC activation as an ``[N*H*W, C]`` matrix.
+
+Semantics equal ``act(F.batch_norm(x, ...) + residual)``: biased batch
+variance for normalisation, unbiased variance and ``momentum`` for the running
+statistics, ``num_batches_tracked`` incremented on the device.  Eval mode
+uses the running statistics.  CPU tensors, NCHW-contiguous tensors, channel
+counts not divisible by 8 and ``momentum=None`` use the plain PyTorch chain.
+"""
+
+from __future__ import annotations
+
+from typing import Optional
+
+import torch
+import torch.nn.functional as F
+from torch import nn
+
+
+def _bx():
+    from p2pfl_amd.ops import ext
+
+    return ext().bn
+
+
+def _nhwc_2d(t: torch.Tensor) -> torch.Tensor:
+    """[N, C, H, W] channels-last tensor -> its [N*H*W, C] storage view."""
+    return t.permute(0, 2, 3, 1).reshape(-1, t.shape[1])
+
+
+def _from_2d(t2: torch.Tensor, shape) -> torch.Tensor:
+    n, c, h, w = shape
+    return t2.view(n, h, w, c).permute(0, 3, 1, 2)
+
+
+def batch_norm_act_reference(x, weight, bias, running_mean, running_var, training, momentum, eps, residual=None, relu=True):
+    """Plain PyTorch definition (also the CPU / fallback path)."""
+    y = F.batch_norm(x, running_mean, running_var, weight, bias, training, momentum, eps)
+    if residual is not None:
+        y = y + residual
+    return torch.relu(y) if relu else y
+
+
+class _BatchNormAct(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, weight, bias, residual, running_mean, running_var, nbt, momentum, eps, relu):
+        shape = x.shape
+        x2 = _nhwc_2d(x)
+        r2 = _nhwc_2d(residual.to(x.dtype)) if residual is not None else None
+        y2, mean, rstd = _bx().fwd_train(x2, weight, bias, r2, running_mean, running_var, nbt, float(momentum), float(eps), bool(relu))
+        ctx.save_for_backward(x2, y2, weight, mean, rstd)
+        ctx.shape, ctx.relu, ctx.has_res = shape, bool(relu), residual is not None
+        ctx.res_dtype = residual.dtype if residual is not None else None
+        return _from_2d(y2, shape)
+
+    @staticmethod
+    def backward(ctx, dy):
+        x2, y2, weight, mean, rstd = ctx.saved_tensors
+        dy = dy.to(x2.dtype)
+        if not dy.is_contiguous(memory_format=torch.channels_last):
+            dy = dy.contiguous(memory_format=torch.channels_last)
+        out = _bx().bwd(_nhwc_2d(dy), y2, x2, weight, mean, rstd, ctx.relu, ctx.has_res and ctx.needs_input_grad[3])
+        dx = _from_2d(out[0], ctx.shape)
+        dres = _from_2d(out[3], ctx.shape).to(ctx.res_dtype) if len(out) > 3 else None
+        return dx, out[1].to(weight.dtype), out[2].to(weight.dtype), dres, None, None, None, None, None, None
+
+
+def _native_ok(x: torch.Tensor, bn: nn.BatchNorm2d, residual: Optional[torch.Tensor]) -> bool:
+    from p2pfl_amd.ops import _gpu
+
+    if not (_gpu(x) and x.dim() == 4 and x.dtype in (torch.bfloat16, torch.float32)):
+        return False
+    if not x.is_contiguous(memory_format=torch.channels_last) or x.shape[1] % 8 or x.numel() == 0:
+        return False
+    if not bn.affine or bn.weight.dtype != torch.float32 or bn.bias.dtype != torch.float32:
+        return False
+    if residual is not None and (residual.shape != x.shape or not residual.is_contiguous(memory_format=torch.channels_last)):
+        return False
+    # 16-byte aligned rows of 8 channels
+    return x.data_ptr() % 16 == 0 and (residual is None or residual.data_ptr() % 16 == 0)
+
+
+def batch_norm_act(x: torch.Tensor, bn: nn.BatchNorm2d, residual: Optional[torch.Tensor] = None, relu: bool = True) -> torch.Tensor:
+    """``act(bn(x) [+ residual])`` for a ``BatchNorm2d`` module, fused on MI355X."""
+    training = bn.training or not bn.track_running_stats
+    if not _native_ok(x, bn, residual) or (training and bn.momentum is None):
+        y = bn(x)
+        if residual is not None:
+            y = y + residual
+        return torch.relu(y) if relu else y
+    if training:
+        track = bn.training and bn.track_running_stats
+        rm = bn.running_mean if track else None
+        rv = bn.running_var if track else None
+        nbt = bn.num_batches_tracked if track and bn.num_batches_tracked is not None else None
+        return _BatchNormAct.apply(x, bn.weight, bn.bias, residual, rm, rv, nbt, bn.momentum, bn.eps, relu)
+    if torch.is_grad_enabled() and (x.requires_grad or bn.weight.requires_grad):
+        # eval-mode BN with autograd (rare): PyTorch chain
+        return batch_norm_act_reference(x, bn.weight, bn.bias, bn.running_mean, bn.running_var, False, 0.0, bn.eps, residual, relu)
+    r2 = _nhwc_2d(residual.to(x.dtype)) if residual is not None else None
+    y2 = _bx().fwd_eval(_nhwc_2d(x), bn.weight, bn.bias, r2, bn.running_mean, bn.running_var, float(bn.eps), bool(relu))
+    return _from_2d(y2, x.shape)

@@ -83,6 +83,26 @@ class CollectiveFedAvg:
             dist.all_reduce(flat[s : s + self.bucket_elems])
         return flat
 
+    def aggregate_async(self, flat: torch.Tensor, weight: float, total: Optional[float] = None) -> "PendingFedAvg":
+        """Start ``sum_ranks (w_rank / W) * flat_rank`` on a SNAPSHOT of ``flat``; returns a handle.
+
+        The scaled snapshot is made by one kernel on the current (compute)
+        stream; the bucketed all-reduces are issued with ``async_op=True`` so
+        RCCL runs them on its own HIP stream, ordered after the snapshot but
+        concurrent with whatever the compute stream does next (the round
+        runner's validation pass).  ``flat`` itself stays untouched and
+        readable meanwhile.  ``handle.wait()`` orders the current stream after
+        the collective (no host block on RCCL) and returns the aggregate.
+        """
+        if self.env.world_size == 1:
+            return PendingFedAvg(flat, [])
+        if total is None:
+            total = self.total_weight(weight)
+        scale = float(weight) / total if total > 0 else 1.0 / self.env.world_size
+        snap = flat * scale
+        works = [dist.all_reduce(snap[s : s + self.bucket_elems], async_op=True) for s in range(0, snap.numel(), self.bucket_elems)]
+        return PendingFedAvg(snap, works)
+
     def barrier(self) -> None:
         if self.env.world_size > 1:
             dist.barrier()
@@ -101,3 +121,17 @@ class CollectiveFedAvg:
         out = [torch.zeros_like(t) for _ in range(self.env.world_size)]
         dist.all_gather(out, t)
         return [float(x.item()) for x in out]
+
+
+class PendingFedAvg:
+    """An in-flight :meth:`CollectiveFedAvg.aggregate_async`."""
+
+    def __init__(self, result: torch.Tensor, works: list) -> None:
+        self.result = result
+        self._works = works
+
+    def wait(self) -> torch.Tensor:
+        for w in self._works:
+            w.wait()
+        self._works = []
+        return self.result

@@ -1,0 +1,158 @@
+"""Fused BatchNorm(+residual)(+ReLU) HIP kernels vs fp32 PyTorch (MI355X only)."""
+
+from __future__ import annotations
+
+import pytest
+import torch
+from torch import nn
+
+from p2pfl_amd import ops
+from p2pfl_amd.ops.batchnorm import batch_norm_act, batch_norm_act_reference
+
+pytestmark = pytest.mark.gpu
+
+
+def _cl(t):
+    return t.contiguous(memory_format=torch.channels_last)
+
+
+def _bn(C, seed):
+    g = torch.Generator(device="cuda").manual_seed(seed)
+    bn = nn.BatchNorm2d(C).cuda()
+    with torch.no_grad():
+        bn.weight.copy_(torch.rand(C, device="cuda", generator=g) + 0.5)
+        bn.bias.copy_(torch.randn(C, device="cuda", generator=g))
+        bn.running_mean.copy_(torch.randn(C, device="cuda", generator=g) * 0.1)
+        bn.running_var.copy_(torch.rand(C, device="cuda", generator=g) + 0.5)
+    return bn
+
+
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
+@pytest.mark.parametrize("shape", [(32, 64, 32, 32), (8, 512, 4, 4), (3, 96, 5, 7), (2, 2048, 2, 2), (2, 8, 1, 1)])
+@pytest.mark.parametrize("residual,relu", [(False, True), (True, True), (False, False)])
+def test_batch_norm_act_train(dtype, shape, residual, relu):
+    ops.ext()
+    g = torch.Generator(device="cuda").manual_seed(sum(shape))
+    C = shape[1]
+    x = _cl(torch.randn(*shape, device="cuda", generator=g) * 3 + 1.5).to(dtype).requires_grad_(True)
+    r = _cl(torch.randn(*shape, device="cuda", generator=g)).to(dtype).requires_grad_(True) if residual else None
+    bn = _bn(C, 7)
+    ref = _bn(C, 7)
+    y = batch_norm_act(x, bn, r, relu)
+    assert y.dtype == dtype and y.shape == x.shape and y.is_contiguous(memory_format=torch.channels_last)
+    xr = x.detach().float().requires_grad_(True)
+    rr = r.detach().float().requires_grad_(True) if residual else None
+    yr = batch_norm_act_reference(xr, ref.weight, ref.bias, ref.running_mean, ref.running_var, True, 0.1, ref.eps, rr, relu)
+    tol = dict(atol=3e-2, rtol=2e-2) if dtype == torch.bfloat16 else dict(atol=1e-4, rtol=1e-4)
+    torch.testing.assert_close(y.float(), yr, **tol)
+    # running statistics (unbiased variance) and the batch counter
+    torch.testing.assert_close(bn.running_mean, ref.running_mean, atol=1e-5, rtol=1e-4)
+    torch.testing.assert_close(bn.running_var, ref.running_var, atol=1e-5, rtol=1e-4)
+    assert int(bn.num_batches_tracked) == 1
+    # backward
+    dy = _cl(torch.randn(*shape, device="cuda", generator=g)).to(dtype)
+    y.backward(dy)
+    yr.backward(dy.float())
+    M = x.numel() // C
+    grads = [(x.grad, xr.grad, "dx"), (bn.weight.grad, ref.weight.grad, "dw"), (bn.bias.grad, ref.bias.grad, "db")]
+    if residual:
+        grads.append((r.grad, rr.grad, "dres"))
+    for a, e, name in grads:
+        err = (a.float() - e.float()).abs().max().item() / max(e.float().abs().max().item(), 1e-6)
+        lim = (3e-2 if dtype == torch.bfloat16 else 1e-4) * (1 if name in ("dx", "dres") else max(1.0, (M / 4096) ** 0.5))
+        assert err < lim, (name, err)
+
+
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
+@pytest.mark.parametrize("residual", [False, True])
+def test_batch_norm_act_eval(dtype, residual):
+    g = torch.Generator(device="cuda").manual_seed(3)
+    shape = (4, 128, 8, 8)
+    x = _cl(torch.randn(*shape, device="cuda", generator=g)).to(dtype)
+    r = _cl(torch.randn(*shape, device="cuda", generator=g)).to(dtype) if residual else None
+    bn = _bn(128, 9).eval()
+    with torch.no_grad():
+        y = batch_norm_act(x, bn, r)
+        yr = batch_norm_act_reference(x.float(), bn.weight, bn.bias, bn.running_mean, bn.running_var, False, 0.0, bn.eps, r.float() if residual else None)
+    torch.testing.assert_close(y.float(), yr, **(dict(atol=3e-2, rtol=2e-2) if dtype == torch.bfloat16 else dict(atol=1e-5, rtol=1e-5)))
+
+
+def test_batch_norm_is_deterministic():
+    g = torch.Generator(device="cuda").manual_seed(5)
+    x = _cl(torch.randn(16, 256, 16, 16, device="cuda", generator=g)).to(torch.bfloat16)
+    dy = _cl(torch.randn(16, 256, 16, 16, device="cuda", generator=g)).to(torch.bfloat16)
+    outs = []
+    for _ in range(2):
+        bn = _bn(256, 1)
+        xi = x.clone().requires_grad_(True)
+        y = batch_norm_act(xi, bn)
+        y.backward(dy)
+        outs.append((y, xi.grad, bn.weight.grad, bn.bias.grad, bn.running_var.clone()))
+    for a, b in zip(*outs):
+        assert torch.equal(a, b)
+
+
+def test_batch_norm_large_mean_no_cancellation():
+    """Shifted sums keep the variance exact for activations far from zero."""
+    g = torch.Generator(device="cuda").manual_seed(11)
+    x = _cl(torch.randn(8, 64, 16, 16, device="cuda", generator=g) * 0.01 + 300.0)
+    bn = _bn(64, 2)
+    ref = _bn(64, 2)
+    y = batch_norm_act(x, bn, relu=False)
+    yr = batch_norm_act_reference(x.double(), ref.weight.double(), ref.bias.double(), ref.running_mean.double(), ref.running_var.double(), True, 0.1, ref.eps, None, False)
+    torch.testing.assert_close(y.double(), yr, atol=2e-3, rtol=1e-3)
+
+
+def test_resnet18_uses_fused_bn_and_trains():
+    from p2pfl_amd.models.resnet import ResNet18
+
+    torch.manual_seed(0)
+    m = ResNet18(seed=0).cuda()
+    x = torch.randint(0, 255, (16, 3, 32, 32), dtype=torch.uint8, device="cuda")
+    y = torch.randint(0, 10, (16,), device="cuda")
+    calls = {"n": 0}
+    real = ops.ext().bn.fwd_train
+    import p2pfl_amd.ops.batchnorm as bnmod
+
+    orig = bnmod._bx
+
+    def spy():
+        b = orig()
+
+        class W:
+            def fwd_train(self, *a, **k):
+                calls["n"] += 1
+                return real(*a, **k)
+
+            def __getattr__(self, k):
+                return getattr(b, k)
+
+        return W()
+
+    bnmod._bx = spy
+    try:
+        opt = torch.optim.SGD(m.parameters(), lr=0.05, momentum=0.9)
+        losses = []
+        for _ in range(15):
+            opt.zero_grad()
+            with torch.autocast("cuda", dtype=torch.bfloat16):
+                loss = torch.nn.functional.cross_entropy(m(x), y)
+            loss.backward()
+            opt.step()
+            losses.append(float(loss))
+    finally:
+        bnmod._bx = orig
+    assert calls["n"] == 15 * 20, calls  # stem + 16 block BNs + 3 projection BNs per step
+    assert losses[-1] < 0.5 * losses[0], losses
+    # eval forward agrees with the PyTorch chain
+    m.eval()
+    import os
+
+    with torch.no_grad(), torch.autocast("cuda", dtype=torch.bfloat16):
+        a = m(x).float()
+        os.environ["P2PFL_FORCE_TORCH_OPS"] = "1"
+        try:
+            b = m(x).float()
+        finally:
+            del os.environ["P2PFL_FORCE_TORCH_OPS"]
+    torch.testing.assert_close(a, b, atol=0.15, rtol=0.05)
