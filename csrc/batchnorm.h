@@ -17,14 +17,14 @@ BnPlan bn_plan(int M, int C);
 
 // Training forward: batch statistics (biased variance, shifted sums), running
 // stats update (unbiased variance, PyTorch momentum convention), then
-//   y = act(x * scale + shift [+ res])      scale = w * rstd, shift = b - mean * scale
-// part: [2, S, C] fp32; coef: [2, C] fp32 scratch; mean / rstd: [C] (saved for backward).
+//   y = act((x - mean) * scale + b [+ res])      scale = w * rstd
+// part: [2, S, C] fp32; coef: [3, C] fp32 scratch; mean / rstd: [C] (saved for backward).
 // run_mean / run_var / nbt may be null (no running statistics).
 void bn_fwd_train(bool bf16, const void* x, const void* res, const float* w, const float* b, float* run_mean,
                   float* run_var, int64_t* nbt, float momentum, float eps, void* y, float* mean, float* rstd,
                   float* coef, float* part, int M, int C, bool relu, hipStream_t s);
 
-// Inference forward with running statistics; coef: [2, C] scratch.
+// Inference forward with running statistics; coef: [3, C] scratch.
 void bn_fwd_eval(bool bf16, const void* x, const void* res, const float* w, const float* b, const float* run_mean,
                  const float* run_var, float eps, void* y, float* coef, int M, int C, bool relu, hipStream_t s);
 

@@ -221,9 +221,9 @@ __global__ __launch_bounds__(kThreads) void bn_finalize_fwd_kernel(
   const float rs = rsqrtf(var + eps);
   mean_out[c] = mu;
   rstd_out[c] = rs;
-  const float sc = w[c] * rs;
-  coef[c] = sc;
-  coef[C + c] = b[c] - mu * sc;
+  coef[c] = mu;
+  coef[C + c] = w[c] * rs;
+  coef[2 * C + c] = b[c];
   if (run_mean) {
     const float unb = M > 1 ? var * (float(M) / float(M - 1)) : var;
     run_mean[c] = (1.f - momentum) * run_mean[c] + momentum * mu;
@@ -239,9 +239,9 @@ __global__ __launch_bounds__(kThreads) void bn_finalize_eval_kernel(const float*
                                                                     float* __restrict__ coef, int C) {
   const int c = blockIdx.x * kThreads + threadIdx.x;
   if (c >= C) return;
-  const float sc = w[c] * rsqrtf(rv[c] + eps);
-  coef[c] = sc;
-  coef[C + c] = b[c] - rm[c] * sc;
+  coef[c] = rm[c];
+  coef[C + c] = w[c] * rsqrtf(rv[c] + eps);
+  coef[2 * C + c] = b[c];
 }
 
 // coef = [A | B | D]: dx = A dz + B (x - mean) + D;  dw = rstd * s2, db = s1
@@ -273,12 +273,13 @@ __global__ __launch_bounds__(kThreads) void bn_apply_fwd_kernel(const T* __restr
   for (int64_t i = blockIdx.x * int64_t(kThreads) + threadIdx.x; i < n8; i += int64_t(gridDim.x) * kThreads) {
     const int64_t e = i * 8;
     const int c = int(e % C);
-    float v[8], sc[8], sh[8];
+    float v[8], mu[8], sc[8], bb[8];
     V8<T>::load(x + e, v);
-    ld8f(coef + c, sc);
-    ld8f(coef + C + c, sh);
+    ld8f(coef + c, mu);
+    ld8f(coef + C + c, sc);
+    ld8f(coef + 2 * C + c, bb);
 #pragma unroll
-    for (int j = 0; j < 8; ++j) v[j] = fmaf(v[j], sc[j], sh[j]);
+    for (int j = 0; j < 8; ++j) v[j] = fmaf(v[j] - mu[j], sc[j], bb[j]);
     if (RES) {
       float r[8];
       V8<T>::load(res + e, r);

@@ -65,7 +65,7 @@ std::vector<torch::Tensor> bn_fwd_train(torch::Tensor x, torch::Tensor w, torch:
   }
   auto y = torch::empty_like(x);
   auto opt = x.options().dtype(torch::kFloat32);
-  auto mean = torch::empty({C}, opt), rstd = torch::empty({C}, opt), coef = torch::empty({2, C}, opt);
+  auto mean = torch::empty({C}, opt), rstd = torch::empty({C}, opt), coef = torch::empty({3, C}, opt);
   const auto plan = p2bn::bn_plan(int(M), int(C));
   auto part = torch::empty({2, plan.S, C}, opt);
   p2bn::bn_fwd_train(bf, x.data_ptr(), rp, f32(w, C, x, "weight"), f32(b, C, x, "bias"), rm, rv, nbt, float(momentum),
@@ -86,7 +86,7 @@ torch::Tensor bn_fwd_eval(torch::Tensor x, torch::Tensor w, torch::Tensor b, c10
     rp = residual->data_ptr();
   }
   auto y = torch::empty_like(x);
-  auto coef = torch::empty({2, C}, x.options().dtype(torch::kFloat32));
+  auto coef = torch::empty({3, C}, x.options().dtype(torch::kFloat32));
   p2bn::bn_fwd_eval(bf, x.data_ptr(), rp, f32(w, C, x, "weight"), f32(b, C, x, "bias"),
                     f32(running_mean, C, x, "running_mean"), f32(running_var, C, x, "running_var"), float(eps),
                     y.data_ptr(), coef.data_ptr<float>(), int(M), int(C), relu, stream());

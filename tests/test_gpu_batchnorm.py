@@ -58,7 +58,8 @@ def test_batch_norm_act_train(dtype, shape, residual, relu):
     if residual:
         grads.append((r.grad, rr.grad, "dres"))
     for a, e, name in grads:
-        err = (a.float() - e.float()).abs().max().item() / max(e.float().abs().max().item(), 1e-6)
+        # relative to the gradient scale (dy ~ N(0, 1)); M = 2 makes dx ~ 0 exactly
+        err = (a.float() - e.float()).abs().max().item() / max(e.float().abs().max().item(), 1.0)
         lim = (3e-2 if dtype == torch.bfloat16 else 1e-4) * (1 if name in ("dx", "dres") else max(1.0, (M / 4096) ** 0.5))
         assert err < lim, (name, err)
 
