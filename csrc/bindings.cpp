@@ -115,17 +115,33 @@ void check_tables(const torch::Tensor& tens, const torch::Tensor& chunks, const 
               "chunk table must be int32 [C, 2] on the arena's device");
 }
 
+// gtab (optional): a persistent device table of gradient addresses (int64 [T])
+// used instead of `grads` -- for steps captured in a HIP graph, whose gradient
+// buffers have fixed addresses filled in after capture.
+torch::Tensor grad_ptrs(const c10::optional<torch::Tensor>& gtab, const std::vector<c10::optional<torch::Tensor>>& grads,
+                        const std::vector<int64_t>& numels, const std::vector<bool>& grad_bf16,
+                        const torch::Tensor& tens, const torch::Device& dev) {
+  if (gtab.has_value() && gtab->defined()) {
+    TORCH_CHECK(gtab->device() == dev && gtab->scalar_type() == torch::kInt64 && gtab->is_contiguous() &&
+                    gtab->numel() == tens.size(0),
+                "gtab must be a contiguous int64 [T] tensor on the arena's device");
+    return *gtab;
+  }
+  TORCH_CHECK(tens.size(0) == int64_t(grads.size()), "multi-tensor step: one gradient per tensor");
+  return grad_table(grads, numels, grad_bf16, dev);
+}
+
 void adam_mt_step(torch::Tensor p, torch::Tensor m, torch::Tensor v, c10::optional<torch::Tensor> pbf,
                   torch::Tensor tens, torch::Tensor chunks, std::vector<c10::optional<torch::Tensor>> grads,
                   std::vector<int64_t> numels, std::vector<bool> grad_bf16, double lr, double b1, double b2, double eps,
-                  double wd, int64_t step, bool decoupled) {
+                  double wd, int64_t step, bool decoupled, c10::optional<torch::Tensor> gtab,
+                  c10::optional<torch::Tensor> t_dev) {
   for (auto* t : {&p, &m, &v}) check_f32(*t, "adam operand");
   const int64_t n = p.numel();
   TORCH_CHECK(m.numel() == n && v.numel() == n, "adam: size mismatch");
   check_tables(tens, chunks, p.device());
-  TORCH_CHECK(tens.size(0) == int64_t(grads.size()), "adam: one gradient per tensor");
   const c10::DeviceGuard guard(p.device());
-  auto gp = grad_table(grads, numels, grad_bf16, p.device());
+  auto gp = grad_ptrs(gtab, grads, numels, grad_bf16, tens, p.device());
   p2::AdamParams h{};
   h.lr = float(lr);
   h.beta1 = float(b1);
@@ -135,6 +151,11 @@ void adam_mt_step(torch::Tensor p, torch::Tensor m, torch::Tensor v, c10::option
   h.step_size = float(lr / (1.0 - std::pow(b1, double(step))));
   h.inv_sqrt_bc2 = float(1.0 / std::sqrt(1.0 - std::pow(b2, double(step))));
   h.decoupled = decoupled ? 1 : 0;
+  if (t_dev.has_value() && t_dev->defined()) {
+    TORCH_CHECK(t_dev->device() == p.device() && t_dev->scalar_type() == torch::kInt32 && t_dev->numel() == 1,
+                "t_dev must be an int32 [1] tensor on the arena's device");
+    h.t_dev = t_dev->data_ptr<int32_t>();
+  }
   p2::adam_mt_step(p.data_ptr<float>(), m.data_ptr<float>(), v.data_ptr<float>(), opt_bf16(pbf, n),
                    reinterpret_cast<const p2::MTTensor*>(tens.data_ptr<int64_t>()),
                    reinterpret_cast<const int2*>(chunks.data_ptr<int32_t>()), int(chunks.size(0)),
@@ -144,7 +165,7 @@ void adam_mt_step(torch::Tensor p, torch::Tensor m, torch::Tensor v, c10::option
 void sgd_mt_step(torch::Tensor p, c10::optional<torch::Tensor> buf, c10::optional<torch::Tensor> pbf,
                  torch::Tensor tens, torch::Tensor chunks, std::vector<c10::optional<torch::Tensor>> grads,
                  std::vector<int64_t> numels, std::vector<bool> grad_bf16, double lr, double momentum,
-                 double dampening, double wd, bool nesterov, bool first_step) {
+                 double dampening, double wd, bool nesterov, bool first_step, c10::optional<torch::Tensor> gtab) {
   check_f32(p, "p");
   const int64_t n = p.numel();
   float* b = nullptr;
@@ -154,9 +175,8 @@ void sgd_mt_step(torch::Tensor p, c10::optional<torch::Tensor> buf, c10::optiona
     b = buf->data_ptr<float>();
   }
   check_tables(tens, chunks, p.device());
-  TORCH_CHECK(tens.size(0) == int64_t(grads.size()), "sgd: one gradient per tensor");
   const c10::DeviceGuard guard(p.device());
-  auto gp = grad_table(grads, numels, grad_bf16, p.device());
+  auto gp = grad_ptrs(gtab, grads, numels, grad_bf16, tens, p.device());
   p2::SgdParams h{float(lr), float(momentum), float(dampening), float(wd), nesterov ? 1 : 0, first_step ? 1 : 0};
   p2::sgd_mt_step(p.data_ptr<float>(), b, opt_bf16(pbf, n), reinterpret_cast<const p2::MTTensor*>(tens.data_ptr<int64_t>()),
                   reinterpret_cast<const int2*>(chunks.data_ptr<int32_t>()), int(chunks.size(0)),
@@ -174,8 +194,17 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("weighted_sum", &weighted_sum, "out = sum_i w_i * src_i (fp32 flat arenas)");
   m.def("adam_step", &adam_step, "fused whole-arena Adam/AdamW step");
   m.def("sgd_step", &sgd_step, "fused whole-arena SGD(+momentum/nesterov) step");
-  m.def("adam_mt_step", &adam_mt_step, "multi-tensor Adam/AdamW over per-tensor grads into flat fp32 state");
-  m.def("sgd_mt_step", &sgd_mt_step, "multi-tensor SGD over per-tensor grads into flat fp32 state");
+  m.def("adam_mt_step", &adam_mt_step, "multi-tensor Adam/AdamW over per-tensor grads into flat fp32 state",
+        pybind11::arg("p"), pybind11::arg("m"), pybind11::arg("v"), pybind11::arg("pbf"), pybind11::arg("tens"),
+        pybind11::arg("chunks"), pybind11::arg("grads"), pybind11::arg("numels"), pybind11::arg("grad_bf16"),
+        pybind11::arg("lr"), pybind11::arg("beta1"), pybind11::arg("beta2"), pybind11::arg("eps"),
+        pybind11::arg("weight_decay"), pybind11::arg("step"), pybind11::arg("decoupled"),
+        pybind11::arg("gtab") = pybind11::none(), pybind11::arg("t_dev") = pybind11::none());
+  m.def("sgd_mt_step", &sgd_mt_step, "multi-tensor SGD over per-tensor grads into flat fp32 state", pybind11::arg("p"),
+        pybind11::arg("buf"), pybind11::arg("pbf"), pybind11::arg("tens"), pybind11::arg("chunks"),
+        pybind11::arg("grads"), pybind11::arg("numels"), pybind11::arg("grad_bf16"), pybind11::arg("lr"),
+        pybind11::arg("momentum"), pybind11::arg("dampening"), pybind11::arg("weight_decay"),
+        pybind11::arg("nesterov"), pybind11::arg("first_step"), pybind11::arg("gtab") = pybind11::none());
   register_cnn(m);
   register_fused(m);
   register_bn(m);

@@ -16,6 +16,9 @@ struct AdamParams {
   float step_size;     // lr / (1 - beta1^t)
   float inv_sqrt_bc2;  // 1 / sqrt(1 - beta2^t)
   int decoupled;
+  // multi-tensor kernel only: when set, t = *t_dev and the two bias
+  // corrections above are computed on the device (graph-replayable steps)
+  const int* t_dev;
 };
 void adam_step(float* p, const float* g, float* m, float* v, uint16_t* p_bf16, int64_t n, const AdamParams& h,
                hipStream_t s);

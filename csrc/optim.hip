@@ -135,6 +135,11 @@ __global__ __launch_bounds__(256) void adam_mt_kernel(float* __restrict__ p, flo
                                                       float* __restrict__ v, uint16_t* __restrict__ pbf,
                                                       const MTTensor* __restrict__ tens, const int2* __restrict__ chunks,
                                                       const uint64_t* __restrict__ gptr, AdamParams h) {
+  if (h.t_dev) {
+    const float t = float(*h.t_dev);
+    h.step_size = h.lr / (1.f - powf(h.beta1, t));
+    h.inv_sqrt_bc2 = rsqrtf(1.f - powf(h.beta2, t));
+  }
   const int2 ch = chunks[blockIdx.x];
   const void* g = reinterpret_cast<const void*>(gptr[ch.x]);
   if (g == nullptr) return;

@@ -180,14 +180,40 @@ class MTTables:
     def grads(self):
         return [p.grad for p in self.params]
 
+    def fill_grad_table(self, gtab: torch.Tensor) -> None:
+        """Write the current gradients' addresses into the persistent device table ``gtab``."""
+        ptrs = [p.grad.data_ptr() if p.grad is not None else 0 for p in self.params]
+        gtab.copy_(torch.tensor(ptrs, dtype=torch.int64))
+
 
 class _MTOptimizer:
+    """Base of the multi-tensor optimizers.
+
+    ``step()`` is the eager path (gradient addresses gathered per call);
+    ``step_graph(gtab)`` reads them from a persistent device table and keeps
+    every step-dependent scalar on the device, so it can be captured once in
+    a HIP graph and replayed (:mod:`p2pfl_amd.learning.step_graph`).
+    ``reset()`` returns the optimizer to its freshly-constructed state while
+    keeping its buffers' addresses (a captured graph stays valid).
+    """
+
     def __init__(self, arena: ModuleArena, lr: float, weight_decay: float) -> None:
         self.arena = arena
         self.lr = lr
         self.weight_decay = weight_decay
         self.t = 0
         self.mt = MTTables(arena)
+
+    def config(self) -> tuple:
+        return (type(self).__name__, self.lr, self.weight_decay)
+
+    def state_tensors(self) -> list:
+        return []
+
+    def reset(self) -> None:
+        self.t = 0
+        for t in self.state_tensors():
+            t.zero_()
 
     def zero_grad(self, set_to_none: bool = True) -> None:
         # always None: autograd then hands over each new gradient without a
@@ -204,6 +230,13 @@ class MTAdam(_MTOptimizer):
         self.decoupled = decoupled
         self.m = torch.zeros_like(arena.flat)
         self.v = torch.zeros_like(arena.flat)
+        self.t_dev = torch.zeros(1, dtype=torch.int32, device=arena.flat.device)
+
+    def config(self) -> tuple:
+        return super().config() + (self.beta1, self.beta2, self.eps, self.decoupled)
+
+    def state_tensors(self) -> list:
+        return [self.m, self.v, self.t_dev]
 
     def step(self) -> None:
         self.t += 1
@@ -211,6 +244,18 @@ class MTAdam(_MTOptimizer):
             self.arena.flat, self.m, self.v, self.mt.grads(), self.mt,
             lr=self.lr, beta1=self.beta1, beta2=self.beta2, eps=self.eps,
             weight_decay=self.weight_decay, step=self.t, decoupled=self.decoupled, p_bf16=self.arena.shadow,
+        )
+        if self.arena.flat.is_cuda:
+            self.t_dev.fill_(self.t)
+
+    def step_graph(self, gtab: torch.Tensor) -> None:
+        """Graph-capturable step: t_dev += 1 on the device, bias corrections from it."""
+        self.t_dev.add_(1)
+        ops.adam_mt_step(
+            self.arena.flat, self.m, self.v, [], self.mt,
+            lr=self.lr, beta1=self.beta1, beta2=self.beta2, eps=self.eps,
+            weight_decay=self.weight_decay, step=1, decoupled=self.decoupled, p_bf16=self.arena.shadow,
+            gtab=gtab, t_dev=self.t_dev,
         )
 
 
@@ -220,12 +265,26 @@ class MTSGD(_MTOptimizer):
         self.momentum, self.dampening, self.nesterov = momentum, dampening, nesterov
         self.buf: Optional[torch.Tensor] = torch.zeros_like(arena.flat) if momentum != 0 else None
 
+    def config(self) -> tuple:
+        return super().config() + (self.momentum, self.dampening, self.nesterov)
+
+    def state_tensors(self) -> list:
+        return [self.buf] if self.buf is not None else []
+
     def step(self) -> None:
         self.t += 1
         ops.sgd_mt_step(
             self.arena.flat, self.buf, self.mt.grads(), self.mt,
             lr=self.lr, momentum=self.momentum, dampening=self.dampening, weight_decay=self.weight_decay,
             nesterov=self.nesterov, first_step=self.t == 1, p_bf16=self.arena.shadow,
+        )
+
+    def step_graph(self, gtab: torch.Tensor) -> None:
+        """Graph-capturable step for t >= 2 (the first step, which seeds the momentum buffer, runs eagerly)."""
+        ops.sgd_mt_step(
+            self.arena.flat, self.buf, [], self.mt,
+            lr=self.lr, momentum=self.momentum, dampening=self.dampening, weight_decay=self.weight_decay,
+            nesterov=self.nesterov, first_step=False, p_bf16=self.arena.shadow, gtab=gtab,
         )
 
 

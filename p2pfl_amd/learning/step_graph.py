@@ -1,0 +1,112 @@
+"""One training step captured as a HIP graph (mixed-precision torch learners).
+
+A ResNet / ViT training step on PyTorch-ROCm is a few hundred kernel launches
+(convolutions / GEMMs, the fused BatchNorm or LayerNorm kernels, autograd's
+bookkeeping, the multi-tensor optimizer).  At the federated batch size (32)
+most of them run for a few microseconds, so the step is bound by host-side
+launch work, not by the GPU.  :class:`TrainStepGraph` records the whole step
+ONCE -- batch gather from the device-resident shard, forward under bf16
+autocast, backward, fused optimizer -- and then replays it with a single
+``hipGraphLaunch`` per step.  Only the batch's sample indices change between
+replays (one 256-byte device copy into the graph's static index buffer).
+
+Semantics are those of the eager loop: same batches in the same order, the
+same optimizer math (the optimizer's step count and bias corrections live on
+the device, see :class:`~p2pfl_amd.learning.optim.MTAdam`), BatchNorm running
+statistics updated inside the graph.  The first step of every ``fit`` (which
+seeds SGD momentum) and a short last batch run eagerly.
+"""
+
+from __future__ import annotations
+
+from typing import Any, Optional, Tuple
+
+import torch
+
+from p2pfl_amd.utils.lockcheck import make_lock
+
+# virtual peers (one node thread each) may capture concurrently: serialise
+# captures process-wide, capture in thread-local mode (other threads' work stays legal)
+_CAPTURE_LOCK = make_lock("StepGraph._CAPTURE_LOCK")
+
+
+def graphable_loader(loader: Any) -> bool:
+    return all(hasattr(loader, a) for a in ("x", "y", "permutation", "normalize", "batch_size")) and loader.x.is_cuda
+
+
+class TrainStepGraph:
+    def __init__(self, learner: Any, opt: Any, loader: Any) -> None:
+        self.learner = learner
+        self.opt = opt
+        self.loader = loader
+        self.B = int(loader.batch_size)
+        dev = learner.device
+        self.key = self.make_key(learner, opt, loader)
+        self.idx = torch.zeros(self.B, dtype=torch.int64, device=dev)
+        self.gtab = torch.zeros(len(opt.mt.params), dtype=torch.int64, device=dev)
+        self.stream = torch.cuda.Stream(dev)
+        self.graph: Optional[torch.cuda.CUDAGraph] = None
+        self.loss: Optional[torch.Tensor] = None
+
+    @staticmethod
+    def make_key(learner: Any, opt: Any, loader: Any) -> Tuple:
+        return (id(opt), opt.config(), int(loader.batch_size), loader.x.data_ptr(), loader.y.data_ptr(),
+                learner.arena.flat.data_ptr(), id(learner.model))
+
+    # -- body ---------------------------------------------------------------
+    def _body(self, graph: bool) -> torch.Tensor:
+        ld, model, opt = self.loader, self.learner.model, self.opt
+        x = ld.x.index_select(0, self.idx)
+        if ld.normalize:
+            x = x.float().div_(255.0)
+        y = ld.y.index_select(0, self.idx)
+        for p in opt.mt.params:
+            p.grad = None
+        with torch.autocast(device_type="cuda", dtype=torch.bfloat16, cache_enabled=False):
+            loss = model.training_step((x, y), 0)
+        loss.backward()
+        if graph:
+            opt.step_graph(self.gtab)
+        else:
+            opt.step()
+        model.pop_logged()
+        return loss.detach()
+
+    def capture(self, idx: torch.Tensor) -> None:
+        """Warm up and capture; parameters, optimizer and BN state are restored afterwards."""
+        learner, opt = self.learner, self.opt
+        arena = learner.arena
+        cur = torch.cuda.current_stream(learner.device)
+        with _CAPTURE_LOCK:
+            torch.cuda.synchronize(learner.device)
+            keep = [arena.flat, arena.shadow] + opt.state_tensors()
+            saved = [t.clone() for t in keep if t is not None]
+            ints = {k: v.clone() for k, v in getattr(arena, "_int_buffers", {}).items()}
+            t_host = opt.t
+            self.idx.copy_(idx)
+            self.stream.wait_stream(cur)
+            with torch.cuda.stream(self.stream):
+                self._body(graph=False)  # lazy inits (workspaces, solver choices) outside the capture
+            self.stream.synchronize()
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g, stream=self.stream, capture_error_mode="thread_local"):
+                self.loss = self._body(graph=True)
+            torch.cuda.synchronize(learner.device)
+            opt.mt.fill_grad_table(self.gtab)  # the graph's gradient buffers, fixed for every replay
+            for dst, src in zip([t for t in keep if t is not None], saved):
+                dst.copy_(src)
+            for k, v in ints.items():
+                arena._int_buffers[k].copy_(v)
+            opt.t = t_host
+            for p in opt.mt.params:  # eager steps allocate their own gradients
+                p.grad = None
+            torch.cuda.synchronize(learner.device)
+        self.graph = g
+
+    def run(self, idx: torch.Tensor) -> torch.Tensor:
+        """One training step on the samples ``idx`` (len == batch size)."""
+        self.idx.copy_(idx, non_blocking=True)
+        assert self.graph is not None
+        self.graph.replay()
+        self.opt.t += 1
+        return self.loss

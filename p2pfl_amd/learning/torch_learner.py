@@ -26,6 +26,7 @@ store, exactly where the reference's ``FederatedLogger`` put them.
 
 from __future__ import annotations
 
+import os
 import threading
 from collections import OrderedDict
 from typing import Any, Dict, Mapping, Optional, Tuple
@@ -57,6 +58,7 @@ class TorchLearner(NodeLearner):
         log_every_n_steps: int = 50,
         fused_optimizer: bool = True,
         mixed: Optional[bool] = None,
+        use_step_graphs: bool = True,
     ) -> None:
         if Settings.TORCH_NUM_THREADS:
             torch.set_num_threads(Settings.TORCH_NUM_THREADS)
@@ -83,6 +85,10 @@ class TorchLearner(NodeLearner):
         # validate() itself -- the round runner overlaps it with the FedAvg
         # collective of the freshly trained weights (parallel/rounds.py)
         self.defer_final_validation = False
+        # HIP-graph replay of the training step (mixed precision, device-resident data)
+        self.use_step_graphs = use_step_graphs and os.environ.get("P2PFL_STEP_GRAPHS", "1") != "0"
+        self._mt_opt: Any = None
+        self._step_graph: Any = None
         self.model: Any = None
         self.arena: Optional[ModuleArena] = None
         self.data: Any = None
@@ -216,6 +222,13 @@ class TorchLearner(NodeLearner):
             fused = fuse_optimizer_mt(opt, self.arena)
             if fused is None:  # bf16 weights must not be stepped by torch.optim
                 raise RuntimeError("mixed-precision learner needs a plain Adam/AdamW/SGD over all parameters")
+            prev = self._mt_opt
+            if prev is not None and prev.arena is self.arena and prev.config() == fused.config():
+                # same optimizer re-created: reset the persistent one instead
+                # (identical state, and a captured step graph stays valid)
+                prev.reset()
+                return prev
+            self._mt_opt = fused
             return fused
         if not (self.fused_optimizer and self.device.type == "cuda" and self.arena is not None):
             return opt
@@ -235,8 +248,16 @@ class TorchLearner(NodeLearner):
             model = self.model
             for _epoch in range(self.epochs):
                 model.train()
+                loader = self.data.train_dataloader()
+                if self._graph_ok(opt, loader):
+                    with logger.span(self._addr, "train_epoch"):
+                        if not self._fit_epoch_graph(opt, loader):
+                            return
+                    if not (self.defer_final_validation and _epoch == self.epochs - 1):
+                        self._validate()
+                    continue
                 with logger.span(self._addr, "train_epoch"):
-                    for i, batch in enumerate(self.data.train_dataloader()):
+                    for i, batch in enumerate(loader):
                         if self._interrupt.is_set():
                             return
                         opt.zero_grad(set_to_none=False)
@@ -255,6 +276,50 @@ class TorchLearner(NodeLearner):
         except Exception as e:
             logger.error(self._addr, f"Fit error: {e}")
             raise
+
+    def _graph_ok(self, opt: Any, loader: Any) -> bool:
+        if not (self.use_step_graphs and self.mixed and self.device.type == "cuda" and hasattr(opt, "step_graph")):
+            return False
+        from p2pfl_amd.learning.step_graph import graphable_loader
+
+        return graphable_loader(loader)
+
+    def _fit_epoch_graph(self, opt: Any, loader: Any) -> bool:
+        """One epoch with full batches replayed from a captured step graph; False if interrupted."""
+        from p2pfl_amd.learning.step_graph import TrainStepGraph
+
+        model = self.model
+        B, n = int(loader.batch_size), len(loader.dataset)
+        perm = loader.permutation()  # the same batch order as iterating the loader
+        key = TrainStepGraph.make_key(self, opt, loader)
+        for i, s in enumerate(range(0, n, B)):
+            if self._interrupt.is_set():
+                return False
+            idx = perm[s : s + B]
+            if idx.numel() == B and opt.t >= 1:
+                sg = self._step_graph
+                if sg is None or sg.key != key:
+                    sg = self._step_graph = TrainStepGraph(self, opt, loader)
+                    sg.capture(idx)
+                logged = {"train_loss": sg.run(idx)}
+            else:  # first step (seeds optimizer state) and a short last batch
+                x = loader.x.index_select(0, idx)
+                if loader.normalize:
+                    x = x.float().div_(255.0)
+                opt.zero_grad(set_to_none=True)
+                with self._autocast():
+                    loss = model.training_step((x, loader.y.index_select(0, idx)), i)
+                loss.backward()
+                opt.step()
+                # drop this step's autograd graph now: its AccumulateGrad nodes
+                # (bound to this stream) must not survive into a graph capture
+                del loss
+                logged = model.pop_logged()
+            self._step += 1
+            if self.log_every_n_steps and self._step % self.log_every_n_steps == 0:
+                for k, v in logged.items():
+                    self._log(k, float(v), step=self._step)
+        return True
 
     @torch.no_grad()
     def _run_eval(self, loader, hook) -> Dict[str, float]:

@@ -152,8 +152,13 @@ def _mt_reference(step_fn, p, states, pbf, table, grads):
             view(pbf).copy_(view(p))
 
 
-def adam_mt_step(p, m, v, grads, mt, *, lr, beta1, beta2, eps, weight_decay, step, decoupled=False, p_bf16=None):
-    """Adam/AdamW for tensors whose grads live outside the arena (``mt``: :class:`~p2pfl_amd.learning.optim.MTTables`)."""
+def adam_mt_step(p, m, v, grads, mt, *, lr, beta1, beta2, eps, weight_decay, step, decoupled=False, p_bf16=None, gtab=None, t_dev=None):
+    """Adam/AdamW for tensors whose grads live outside the arena (``mt``: :class:`~p2pfl_amd.learning.optim.MTTables`).
+
+    ``gtab`` (device int64 [T]) replaces ``grads`` by a persistent table of
+    gradient addresses and ``t_dev`` (device int32 [1]) supplies the step
+    count: together they make the launch replayable inside a HIP graph.
+    """
     if not _gpu(p):
         _mt_reference(
             lambda pp, g, mm, vv: adam_step_reference(pp, g, mm, vv, lr, beta1, beta2, eps, weight_decay, step, decoupled),
@@ -162,11 +167,11 @@ def adam_mt_step(p, m, v, grads, mt, *, lr, beta1, beta2, eps, weight_decay, ste
         return
     ext().adam_mt_step(
         p, m, v, p_bf16, mt.tens, mt.chunks, list(grads), mt.numels, mt.grad_bf16,
-        float(lr), float(beta1), float(beta2), float(eps), float(weight_decay), int(step), bool(decoupled),
+        float(lr), float(beta1), float(beta2), float(eps), float(weight_decay), int(step), bool(decoupled), gtab, t_dev,
     )
 
 
-def sgd_mt_step(p, buf, grads, mt, *, lr, momentum=0.0, dampening=0.0, weight_decay=0.0, nesterov=False, first_step=False, p_bf16=None):
+def sgd_mt_step(p, buf, grads, mt, *, lr, momentum=0.0, dampening=0.0, weight_decay=0.0, nesterov=False, first_step=False, p_bf16=None, gtab=None):
     if not _gpu(p):
         _mt_reference(
             lambda pp, g, b: sgd_step_reference(pp, g, b, lr, momentum, dampening, weight_decay, nesterov, first_step),
@@ -175,7 +180,7 @@ def sgd_mt_step(p, buf, grads, mt, *, lr, momentum=0.0, dampening=0.0, weight_de
         return
     ext().sgd_mt_step(
         p, buf, p_bf16, mt.tens, mt.chunks, list(grads), mt.numels, mt.grad_bf16,
-        float(lr), float(momentum), float(dampening), float(weight_decay), bool(nesterov), bool(first_step),
+        float(lr), float(momentum), float(dampening), float(weight_decay), bool(nesterov), bool(first_step), gtab,
     )
 
 
