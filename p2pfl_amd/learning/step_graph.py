@@ -110,3 +110,71 @@ class TrainStepGraph:
         self.graph.replay()
         self.opt.t += 1
         return self.loss
+
+
+class EvalStepGraph:
+    """HIP graph of one evaluation step: batch gather, forward, the model's
+    eval hook (loss / metric), and per-metric sums accumulated on the device.
+
+    A pass replays it once per full batch and reads the sums back once at
+    the end (one host sync per pass instead of one per logged value).
+    """
+
+    def __init__(self, learner: Any, loader: Any, hook: Any) -> None:
+        self.learner = learner
+        self.loader = loader
+        self.hook = hook
+        self.B = int(loader.batch_size)
+        dev = learner.device
+        self.key = self.make_key(learner, loader, hook)
+        self.idx = torch.zeros(self.B, dtype=torch.int64, device=dev)
+        self.keys: list = []
+        self.sums: Optional[torch.Tensor] = None
+        self.stream = torch.cuda.Stream(dev)
+        self.graph: Optional[torch.cuda.CUDAGraph] = None
+
+    @staticmethod
+    def make_key(learner: Any, loader: Any, hook: Any) -> Tuple:
+        return (getattr(hook, "__name__", str(hook)), int(loader.batch_size), loader.x.data_ptr(), loader.y.data_ptr(),
+                learner.arena.flat.data_ptr(), id(learner.model))
+
+    def batch(self, idx: torch.Tensor):
+        ld = self.loader
+        x = ld.x.index_select(0, idx)
+        if ld.normalize:
+            x = x.float().div_(255.0)
+        return x, ld.y.index_select(0, idx)
+
+    def step(self, idx: torch.Tensor, weight: float, cache: bool = True) -> None:
+        """Eager evaluation of one batch, accumulated into the sums (also the captured body)."""
+        with torch.autocast(device_type="cuda", dtype=torch.bfloat16, cache_enabled=cache):
+            self.hook(self.batch(idx), 0)
+        logged = self.learner.model.pop_logged()
+        if not self.keys:
+            self.keys = sorted(logged)
+            self.sums = torch.zeros(len(self.keys), dtype=torch.float32, device=self.learner.device)
+        for j, k in enumerate(self.keys):
+            v = logged[k]
+            v = v.float() if isinstance(v, torch.Tensor) else torch.tensor(float(v), device=self.learner.device)
+            self.sums[j : j + 1].add_(v.reshape(1) * weight)
+
+    @torch.no_grad()
+    def capture(self, idx: torch.Tensor) -> None:
+        learner = self.learner
+        cur = torch.cuda.current_stream(learner.device)
+        with _CAPTURE_LOCK:
+            self.idx.copy_(idx)
+            self.stream.wait_stream(cur)
+            with torch.cuda.stream(self.stream):
+                self.step(self.idx, float(self.B), cache=False)  # warm-up, creates the sums
+            self.stream.synchronize()
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g, stream=self.stream, capture_error_mode="thread_local"):
+                self.step(self.idx, float(self.B), cache=False)
+            torch.cuda.synchronize(learner.device)
+        self.graph = g
+
+    def run(self, idx: torch.Tensor) -> None:
+        self.idx.copy_(idx, non_blocking=True)
+        assert self.graph is not None
+        self.graph.replay()

@@ -89,6 +89,7 @@ class TorchLearner(NodeLearner):
         self.use_step_graphs = use_step_graphs and os.environ.get("P2PFL_STEP_GRAPHS", "1") != "0"
         self._mt_opt: Any = None
         self._step_graph: Any = None
+        self._eval_graphs: Dict[str, Any] = {}
         self.model: Any = None
         self.arena: Optional[ModuleArena] = None
         self.data: Any = None
@@ -324,6 +325,8 @@ class TorchLearner(NodeLearner):
     @torch.no_grad()
     def _run_eval(self, loader, hook) -> Dict[str, float]:
         self.model.eval()
+        if self._eval_graph_ok(loader):
+            return self._run_eval_graph(loader, hook)
         sums: Dict[str, torch.Tensor] = {}
         n = 0
         for i, (x, y) in enumerate(loader):
@@ -339,6 +342,35 @@ class TorchLearner(NodeLearner):
     def validate(self) -> None:
         """The per-epoch validation pass (metrics to the local store)."""
         self._validate()
+
+    def _eval_graph_ok(self, loader: Any) -> bool:
+        if not (self.use_step_graphs and self.mixed and self.device.type == "cuda"):
+            return False
+        from p2pfl_amd.learning.step_graph import graphable_loader
+
+        return graphable_loader(loader) and len(loader.dataset) >= loader.batch_size
+
+    def _run_eval_graph(self, loader: Any, hook: Any) -> Dict[str, float]:
+        """Full batches replay a captured evaluation graph; sums stay on the device."""
+        from p2pfl_amd.learning.step_graph import EvalStepGraph
+
+        B, n = int(loader.batch_size), len(loader.dataset)
+        name = getattr(hook, "__name__", str(hook))
+        key = EvalStepGraph.make_key(self, loader, hook)
+        eg = self._eval_graphs.get(name)
+        perm = loader.permutation()
+        if eg is None or eg.key != key:
+            eg = self._eval_graphs[name] = EvalStepGraph(self, loader, hook)
+            eg.capture(perm[:B])
+        eg.sums.zero_()
+        for s in range(0, n, B):
+            idx = perm[s : s + B]
+            if idx.numel() == B:
+                eg.run(idx)
+            else:
+                eg.step(idx, float(idx.numel()))
+        vals = eg.sums.tolist()
+        return {k: v / max(1, n) for k, v in zip(eg.keys, vals)}
 
     def _validate(self) -> None:
         loader = self.data.val_dataloader()
