@@ -22,6 +22,10 @@ import torch.nn.functional as F
 from torch import nn
 
 
+# host-side counters of the extra passes the backward had to insert
+STATS = {"dy_cast": 0, "dy_relayout": 0}
+
+
 def _bx():
     from p2pfl_amd.ops import ext
 
@@ -61,8 +65,11 @@ class _BatchNormAct(torch.autograd.Function):
     @staticmethod
     def backward(ctx, dy):
         x2, y2, weight, mean, rstd = ctx.saved_tensors
-        dy = dy.to(x2.dtype)
+        if dy.dtype != x2.dtype:
+            STATS["dy_cast"] += 1
+            dy = dy.to(x2.dtype)
         if not dy.is_contiguous(memory_format=torch.channels_last):
+            STATS["dy_relayout"] += 1
             dy = dy.contiguous(memory_format=torch.channels_last)
         out = _bx().bwd(_nhwc_2d(dy), y2, x2, weight, mean, rstd, ctx.relu, ctx.has_res and ctx.needs_input_grad[3])
         dx = _from_2d(out[0], ctx.shape)
