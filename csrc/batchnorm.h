@@ -24,7 +24,8 @@ void bn_fwd_train(bool bf16, const void* x, const void* res, const float* w, con
                   float* run_var, int64_t* nbt, float momentum, float eps, void* y, float* mean, float* rstd,
                   float* coef, float* part, int M, int C, bool relu, hipStream_t s);
 
-// Inference forward with running statistics; coef: [3, C] scratch.
+// Inference forward with running statistics (one launch; coef unused, kept for
+// the call signature).  w, b, run_mean, run_var must be 16-byte aligned.
 void bn_fwd_eval(bool bf16, const void* x, const void* res, const float* w, const float* b, const float* run_mean,
                  const float* run_var, float eps, void* y, float* coef, int M, int C, bool relu, hipStream_t s);
 

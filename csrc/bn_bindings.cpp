@@ -85,6 +85,8 @@ torch::Tensor bn_fwd_eval(torch::Tensor x, torch::Tensor w, torch::Tensor b, c10
     act(*residual, x, "residual");
     rp = residual->data_ptr();
   }
+  for (const auto* t : {&w, &b, &running_mean, &running_var})
+    TORCH_CHECK(reinterpret_cast<uintptr_t>(t->data_ptr()) % 16 == 0, "eval BN parameters must be 16-byte aligned");
   auto y = torch::empty_like(x);
   auto coef = torch::empty({3, C}, x.options().dtype(torch::kFloat32));
   p2bn::bn_fwd_eval(bf, x.data_ptr(), rp, f32(w, C, x, "weight"), f32(b, C, x, "bias"),

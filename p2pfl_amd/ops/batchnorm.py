@@ -109,6 +109,8 @@ def batch_norm_act(x: torch.Tensor, bn: nn.BatchNorm2d, residual: Optional[torch
     if torch.is_grad_enabled() and (x.requires_grad or bn.weight.requires_grad):
         # eval-mode BN with autograd (rare): PyTorch chain
         return batch_norm_act_reference(x, bn.weight, bn.bias, bn.running_mean, bn.running_var, False, 0.0, bn.eps, residual, relu)
+    if any(t.data_ptr() % 16 for t in (bn.weight, bn.bias, bn.running_mean, bn.running_var)):
+        return batch_norm_act_reference(x, bn.weight, bn.bias, bn.running_mean, bn.running_var, False, 0.0, bn.eps, residual, relu)
     r2 = _nhwc_2d(residual.to(x.dtype)) if residual is not None else None
     y2 = _bx().fwd_eval(_nhwc_2d(x), bn.weight, bn.bias, r2, bn.running_mean, bn.running_var, float(bn.eps), bool(relu))
     return _from_2d(y2, x.shape)
