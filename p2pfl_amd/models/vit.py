@@ -48,7 +48,7 @@ class Mlp(nn.Module):
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
         if _fused(x):
-            h = ops.bias_gelu(torch.matmul(x, self.fc1.weight.t().to(x.dtype)), self.fc1.bias)
+            h = ops.bias_gelu(ops.linear(x, self.fc1.weight), self.fc1.bias)
             return ops.linear(h, self.fc2.weight, self.fc2.bias)
         return self.fc2(nn.functional.gelu(self.fc1(x)))
 

@@ -175,3 +175,23 @@ def test_linear_fused_bias_grad(dtype):
     col = g.float().reshape(-1, 2304).sum(0)
     torch.testing.assert_close(b.grad.float(), col, atol=1e-1 if dtype == torch.bfloat16 else 1e-3, rtol=1e-2)
     torch.testing.assert_close(ops.ext().fused.column_sum(g.reshape(-1, 2304).contiguous()), col, atol=1e-2, rtol=1e-4)
+
+
+@pytest.mark.parametrize("N,K", [(768, 768), (2304, 768), (768, 3072)])
+def test_linear_split_k_weight_grad(N, K):
+    """ViT-sized weight gradients take the split-K bmm path; compare with an fp32 reference."""
+    from p2pfl_amd.ops.fused import _wgrad_splits
+
+    M = 32 * 197
+    assert _wgrad_splits(M, N, K) > 1
+    torch.manual_seed(N + K)
+    x = torch.randn(M, K, device="cuda", dtype=torch.bfloat16, requires_grad=True)
+    w = (torch.randn(N, K, device="cuda") * 0.02).to(torch.bfloat16).requires_grad_(True)
+    b = torch.zeros(N, device="cuda", requires_grad=True)
+    with torch.autocast("cuda", dtype=torch.bfloat16):
+        y = ops.linear(x, w, b)
+    g = torch.randn_like(y)
+    y.backward(g)
+    ref = g.float().t() @ x.detach().float()
+    err = (w.grad.float() - ref).abs().max().item() / ref.abs().max().item()
+    assert w.grad.dtype == torch.bfloat16 and err < 1e-2, err
