@@ -209,45 +209,49 @@ void route_fc2(const uint16_t* dH, const uint16_t* w1t, const uint8_t* am2, int 
 //    dW1[n][k] = sum_b dH[b][n] * A1[b][k]  (K = batch).  Grid (25, 64):
 //    block = 32 rows of n x 128 columns of k, one 32x32 tile per wave.  The
 //    batch-major dH / A1 tiles are transposed through LDS (so no transposed
-//    copies live in HBM); the gradient tile never leaves registers: each lane
-//    updates W1/m/v for its 16 elements (coalesced 128-B rows), writes the
-//    bf16 shadow, and stages the bf16 tile in LDS so W1^T is written as 64-B
-//    row segments.
+//    copies live in HBM).  The gradient tile never leaves the chip: it goes
+//    from the MFMA accumulators through LDS into a row-major layout where
+//    every lane owns 4 consecutive k of one row, so W1 / m / v move as 16-B
+//    accesses (issued before the staging, so their latency overlaps it) and
+//    the bf16 shadow as 8-B stores; W1^T is written as 16-B row segments from
+//    a transposed bf16 tile.  (The accumulator-layout epilogue it replaces did
+//    4-B / 2-B accesses: 37.0 -> 35.1 us per call, bitwise-identical results,
+//    tools/lab/fc1_lab.hip.)
 // ---------------------------------------------------------------------------
 template <int MR>
-__global__ __launch_bounds__(256) void fc1_wgrad_adam_kernel(const uint16_t* __restrict__ dH,
-                                                             const uint16_t* __restrict__ a1,
-                                                             float* __restrict__ p, float* __restrict__ m,
-                                                             float* __restrict__ v, float* __restrict__ gdump,
-                                                             uint16_t* __restrict__ w1bf,
-                                                             uint16_t* __restrict__ w1tbf, Offsets off,
-                                                             const int* __restrict__ adam_t, int t_off, AdamCfg cfg) {
-  constexpr int P = MR + 8;  // padded batch pitch (16-B aligned rows, bank spread)
-  __shared__ __attribute__((aligned(16))) uint16_t sdh[32][P];    // [n][b]
-  __shared__ __attribute__((aligned(16))) uint16_t sa1[128][P];   // [k][b]
-  __shared__ __attribute__((aligned(16))) uint16_t tr[128][40];   // bf16 W1 tile for the W1^T write
+__global__ __launch_bounds__(256) void fc1_wgrad_adam_kernel(const uint16_t* __restrict__ dH, const uint16_t* __restrict__ a1,
+                                               float* __restrict__ p, float* __restrict__ m, float* __restrict__ v,
+                                               float* __restrict__ gdump, uint16_t* __restrict__ w1bf,
+                                               uint16_t* __restrict__ w1tbf, Offsets off,
+                                               const int* __restrict__ adam_t, int t_off, AdamCfg cfg) {
+  constexpr int P = MR + 8;
+  constexpr int GP = 132;  // fp32 pitch of the gradient tile
+  constexpr int kStage = (32 + 128) * P * 2;
+  constexpr int kGrad = 32 * GP * 4;
+  __shared__ __attribute__((aligned(16))) char smem[kStage > kGrad ? kStage : kGrad];
+  __shared__ __attribute__((aligned(16))) uint16_t tr[128][40];
+  uint16_t(*sdh)[P] = reinterpret_cast<uint16_t(*)[P]>(smem);
+  uint16_t(*sa1)[P] = reinterpret_cast<uint16_t(*)[P]>(smem + 32 * P * 2);
+  float(*gt)[GP] = reinterpret_cast<float(*)[GP]>(smem);
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, r = lane & 31, h = lane >> 5;
   const int n0 = blockIdx.y * 32;
   const int kb = blockIdx.x * 128;
-  const int k0 = kb + wave * 32;
-  const bool valid = k0 < kFeat;
-  // This lane's 16 Adam elements: all 48 fp32 loads (W1, m, v) are issued
-  // first, so their latency overlaps the staging and the MFMA (one memory
-  // round trip per lane instead of one per element).
+  // this thread's Adam elements: row nl, k = kb + kq + 32 j + [0, 4)
+  const int nl = tid >> 3, kq = (tid & 7) * 4;
   float* pw = p + off.l1w;
   float* mw = m + off.l1w;
   float* vw = v + off.l1w;
-  float pr[16], mr[16], vr[16];
-  if (valid) {
+  float4 pr[4], mr[4], vr[4];
 #pragma unroll
-    for (int i = 0; i < 16; ++i) {
-      const int64_t e = int64_t(n0 + acc_row_b(i, h)) * kFeat + k0 + r;
-      pr[i] = pw[e];
-      mr[i] = mw[e];
-      vr[i] = vw[e];
+  for (int j = 0; j < 4; ++j) {
+    const int k = kb + kq + 32 * j;
+    if (k < kFeat) {
+      const int64_t e = int64_t(n0 + nl) * kFeat + k;
+      pr[j] = *reinterpret_cast<const float4*>(pw + e);
+      mr[j] = *reinterpret_cast<const float4*>(mw + e);
+      vr[j] = *reinterpret_cast<const float4*>(vw + e);
     }
   }
-  // stage and transpose: dH[b][n0..n0+31] -> sdh[n][b];  A1[b][kb..kb+127] -> sa1[k][b]
   for (int i = tid; i < MR * 4; i += 256) {
     const int b = i >> 2, q = i & 3;
     const uint4 u = reinterpret_cast<const uint4*>(dH + size_t(b) * kHid + n0)[q];
@@ -265,6 +269,14 @@ __global__ __launch_bounds__(256) void fc1_wgrad_adam_kernel(const uint16_t* __r
     for (int j = 0; j < 8; ++j) sa1[q * 8 + j][b] = e[j];
   }
   __syncthreads();
+  const AdamScal s = adam_scal(cfg, adam_t, t_off);
+  if (blockIdx.x == 0 && wave == 0 && lane < 32) {  // FC1 bias (reads sdh before the tile reuses it)
+    const int n = n0 + lane;
+    float g = 0.f;
+    for (int b = 0; b < MR; ++b) g += bf16_to_f32(sdh[lane][b]);
+    if (gdump) gdump[off.l1b + n] = g;
+    adam_apply(p, m, v, off.l1b + n, g, cfg, s);
+  }
   f32x16 acc = {};
 #pragma unroll
   for (int ks = 0; ks < MR / 16; ++ks) {
@@ -272,21 +284,34 @@ __global__ __launch_bounds__(256) void fc1_wgrad_adam_kernel(const uint16_t* __r
     const uint4 b = *reinterpret_cast<const uint4*>(&sa1[wave * 32 + r][ks * 16 + 8 * h]);
     acc = mfma32b(a, b, acc);
   }
-  const AdamScal s = adam_scal(cfg, adam_t, t_off);
-  if (valid) {
+  __syncthreads();  // staging dead -> gradient tile
 #pragma unroll
-    for (int i = 0; i < 16; ++i) {
-      const int nl = acc_row_b(i, h);
-      const int64_t e = int64_t(n0 + nl) * kFeat + k0 + r;
-      if (gdump) gdump[off.l1w + e] = acc[i];
-      adam_regs(pr[i], mr[i], vr[i], acc[i], cfg, s);
-      pw[e] = pr[i];
-      mw[e] = mr[i];
-      vw[e] = vr[i];
-      const uint16_t hb = f32_to_bf16(pr[i]);
-      w1bf[e] = hb;
-      tr[wave * 32 + r][nl] = hb;
-    }
+  for (int i = 0; i < 16; ++i) gt[acc_row_b(i, h)][wave * 32 + r] = acc[i];
+  __syncthreads();
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int kl = kq + 32 * j, k = kb + kl;
+    if (k >= kFeat) continue;
+    const float4 g = *reinterpret_cast<const float4*>(&gt[nl][kl]);
+    const int64_t e = int64_t(n0 + nl) * kFeat + k;
+    if (gdump) *reinterpret_cast<float4*>(gdump + off.l1w + e) = g;
+    adam_regs(pr[j].x, mr[j].x, vr[j].x, g.x, cfg, s);
+    adam_regs(pr[j].y, mr[j].y, vr[j].y, g.y, cfg, s);
+    adam_regs(pr[j].z, mr[j].z, vr[j].z, g.z, cfg, s);
+    adam_regs(pr[j].w, mr[j].w, vr[j].w, g.w, cfg, s);
+    *reinterpret_cast<float4*>(pw + e) = pr[j];
+    *reinterpret_cast<float4*>(mw + e) = mr[j];
+    *reinterpret_cast<float4*>(vw + e) = vr[j];
+    const uint16_t b0 = f32_to_bf16(pr[j].x), b1 = f32_to_bf16(pr[j].y), b2 = f32_to_bf16(pr[j].z),
+                   b3 = f32_to_bf16(pr[j].w);
+    uint2 o;
+    o.x = uint32_t(b0) | (uint32_t(b1) << 16);
+    o.y = uint32_t(b2) | (uint32_t(b3) << 16);
+    *reinterpret_cast<uint2*>(w1bf + e) = o;
+    tr[kl][nl] = b0;
+    tr[kl + 1][nl] = b1;
+    tr[kl + 2][nl] = b2;
+    tr[kl + 3][nl] = b3;
   }
   __syncthreads();
   for (int j = tid; j < 128 * 4; j += 256) {
@@ -294,13 +319,6 @@ __global__ __launch_bounds__(256) void fc1_wgrad_adam_kernel(const uint16_t* __r
     const int k = kb + kl;
     if (k < kFeat)
       *reinterpret_cast<uint4*>(w1tbf + size_t(k) * kHid + n0 + q * 8) = *reinterpret_cast<const uint4*>(&tr[kl][q * 8]);
-  }
-  if (blockIdx.x == 0 && wave == 0 && lane < 32) {
-    const int n = n0 + lane;
-    float g = 0.f;
-    for (int b = 0; b < MR; ++b) g += bf16_to_f32(sdh[lane][b]);
-    if (gdump) gdump[off.l1b + n] = g;
-    adam_apply(p, m, v, off.l1b + n, g, cfg, s);
   }
 }
 
