@@ -207,17 +207,21 @@ class FusedCNNLearner(TorchLearner):
         B = loader.batch_size
         plan = self._plan(n, B)
         key = (name, n, B, loader.x.data_ptr(), loader.y.data_ptr())
+        from p2pfl_amd.learning.step_graph import GATE
+
         g = self._graphs.get(name)
         if g is None or g.key != key:
-            g = self._capture(name, loader, plan, train, key)
+            with GATE.exclusive():  # no other learner's GPU work during the capture
+                g = self._capture(name, loader, plan, train, key)
             self._graphs[name] = g
-        if perm is not None:
-            g.perm.copy_(perm, non_blocking=True)
-        g.stats.zero_()
-        if g.graph is not None:
-            g.graph.replay()
-        else:
-            self._enqueue(loader, plan, train, g.perm, g.stats)
+        with GATE.shared():
+            if perm is not None:
+                g.perm.copy_(perm, non_blocking=True)
+            g.stats.zero_()
+            if g.graph is not None:
+                g.graph.replay()
+            else:
+                self._enqueue(loader, plan, train, g.perm, g.stats)
         return g.stats
 
     def _enqueue(self, loader, plan, train, perm, stats) -> None:

@@ -19,6 +19,8 @@ seeds SGD momentum) and a short last batch run eagerly.
 
 from __future__ import annotations
 
+import threading
+from contextlib import contextmanager
 from typing import Any, Optional, Tuple
 
 import torch
@@ -28,6 +30,52 @@ from p2pfl_amd.utils.lockcheck import make_lock
 # virtual peers (one node thread each) may capture concurrently: serialise
 # captures process-wide, capture in thread-local mode (other threads' work stays legal)
 _CAPTURE_LOCK = make_lock("StepGraph._CAPTURE_LOCK")
+
+
+class DeviceGate:
+    """Shared/exclusive gate of the GPU work of the learners of one process.
+
+    Virtual peers train concurrently, one node thread each.  A HIP-graph
+    capture must not overlap another peer's eager work (its autograd
+    backward runs on the engine's shared device thread, its library calls
+    may synchronise), so every learner step runs under ``shared()`` and every
+    capture under ``exclusive()``; neither is ever taken while holding the
+    other, so the gate cannot deadlock.
+    """
+
+    def __init__(self) -> None:
+        self._cv = threading.Condition()
+        self._shared = 0
+        self._excl = False
+
+    @contextmanager
+    def shared(self):
+        with self._cv:
+            while self._excl:
+                self._cv.wait()
+            self._shared += 1
+        try:
+            yield
+        finally:
+            with self._cv:
+                self._shared -= 1
+                self._cv.notify_all()
+
+    @contextmanager
+    def exclusive(self):
+        with self._cv:
+            while self._excl or self._shared:
+                self._cv.wait()
+            self._excl = True
+        try:
+            yield
+        finally:
+            with self._cv:
+                self._excl = False
+                self._cv.notify_all()
+
+
+GATE = DeviceGate()
 
 
 def graphable_loader(loader: Any) -> bool:
@@ -77,7 +125,7 @@ class TrainStepGraph:
         learner, opt = self.learner, self.opt
         arena = learner.arena
         cur = torch.cuda.current_stream(learner.device)
-        with _CAPTURE_LOCK:
+        with GATE.exclusive(), _CAPTURE_LOCK:
             torch.cuda.synchronize(learner.device)
             keep = [arena.flat, arena.shadow] + opt.state_tensors()
             saved = [t.clone() for t in keep if t is not None]
@@ -162,7 +210,7 @@ class EvalStepGraph:
     def capture(self, idx: torch.Tensor) -> None:
         learner = self.learner
         cur = torch.cuda.current_stream(learner.device)
-        with _CAPTURE_LOCK:
+        with GATE.exclusive(), _CAPTURE_LOCK:
             self.idx.copy_(idx)
             self.stream.wait_stream(cur)
             with torch.cuda.stream(self.stream):

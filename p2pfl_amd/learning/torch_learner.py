@@ -27,6 +27,7 @@ store, exactly where the reference's ``FederatedLogger`` put them.
 from __future__ import annotations
 
 import os
+import contextlib
 import threading
 from collections import OrderedDict
 from typing import Any, Dict, Mapping, Optional, Tuple
@@ -261,11 +262,13 @@ class TorchLearner(NodeLearner):
                     for i, batch in enumerate(loader):
                         if self._interrupt.is_set():
                             return
-                        opt.zero_grad(set_to_none=False)
-                        with self._autocast():
-                            loss = model.training_step(batch, i)
-                        loss.backward()
-                        opt.step()
+                        with self._gate():
+                            opt.zero_grad(set_to_none=False)
+                            with self._autocast():
+                                loss = model.training_step(batch, i)
+                            loss.backward()
+                            opt.step()
+                            del loss
                         self._step += 1
                         if self.log_every_n_steps and self._step % self.log_every_n_steps == 0:
                             for k, v in model.pop_logged().items():
@@ -277,6 +280,14 @@ class TorchLearner(NodeLearner):
         except Exception as e:
             logger.error(self._addr, f"Fit error: {e}")
             raise
+
+    def _gate(self):
+        """Shared hold of the process's GPU gate around one step / eval pass (see step_graph.DeviceGate)."""
+        if self.device.type != "cuda":
+            return contextlib.nullcontext()
+        from p2pfl_amd.learning.step_graph import GATE
+
+        return GATE.shared()
 
     def _graph_ok(self, opt: Any, loader: Any) -> bool:
         if not (self.use_step_graphs and self.mixed and self.device.type == "cuda" and hasattr(opt, "step_graph")):
@@ -301,21 +312,23 @@ class TorchLearner(NodeLearner):
                 sg = self._step_graph
                 if sg is None or sg.key != key:
                     sg = self._step_graph = TrainStepGraph(self, opt, loader)
-                    sg.capture(idx)
-                logged = {"train_loss": sg.run(idx)}
+                    sg.capture(idx)  # takes the gate exclusively
+                with self._gate():
+                    logged = {"train_loss": sg.run(idx)}
             else:  # first step (seeds optimizer state) and a short last batch
-                x = loader.x.index_select(0, idx)
-                if loader.normalize:
-                    x = x.float().div_(255.0)
-                opt.zero_grad(set_to_none=True)
-                with self._autocast():
-                    loss = model.training_step((x, loader.y.index_select(0, idx)), i)
-                loss.backward()
-                opt.step()
-                # drop this step's autograd graph now: its AccumulateGrad nodes
-                # (bound to this stream) must not survive into a graph capture
-                del loss
-                logged = model.pop_logged()
+                with self._gate():
+                    x = loader.x.index_select(0, idx)
+                    if loader.normalize:
+                        x = x.float().div_(255.0)
+                    opt.zero_grad(set_to_none=True)
+                    with self._autocast():
+                        loss = model.training_step((x, loader.y.index_select(0, idx)), i)
+                    loss.backward()
+                    opt.step()
+                    # drop this step's autograd graph now: its AccumulateGrad nodes
+                    # (bound to this stream) must not survive into a graph capture
+                    del loss
+                    logged = model.pop_logged()
             self._step += 1
             if self.log_every_n_steps and self._step % self.log_every_n_steps == 0:
                 for k, v in logged.items():
@@ -327,6 +340,10 @@ class TorchLearner(NodeLearner):
         self.model.eval()
         if self._eval_graph_ok(loader):
             return self._run_eval_graph(loader, hook)
+        with self._gate():
+            return self._run_eval_eager(loader, hook)
+
+    def _run_eval_eager(self, loader, hook) -> Dict[str, float]:
         sums: Dict[str, torch.Tensor] = {}
         n = 0
         for i, (x, y) in enumerate(loader):
@@ -361,15 +378,16 @@ class TorchLearner(NodeLearner):
         perm = loader.permutation()
         if eg is None or eg.key != key:
             eg = self._eval_graphs[name] = EvalStepGraph(self, loader, hook)
-            eg.capture(perm[:B])
-        eg.sums.zero_()
-        for s in range(0, n, B):
-            idx = perm[s : s + B]
-            if idx.numel() == B:
-                eg.run(idx)
-            else:
-                eg.step(idx, float(idx.numel()))
-        vals = eg.sums.tolist()
+            eg.capture(perm[:B])  # takes the gate exclusively
+        with self._gate():
+            eg.sums.zero_()
+            for s in range(0, n, B):
+                idx = perm[s : s + B]
+                if idx.numel() == B:
+                    eg.run(idx)
+                else:
+                    eg.step(idx, float(idx.numel()))
+            vals = eg.sums.tolist()
         return {k: v / max(1, n) for k, v in zip(eg.keys, vals)}
 
     def _validate(self) -> None:
