@@ -212,21 +212,24 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const T* __restrict__ dy, c
 }
 
 // out[c] = sum_r part[r][c] (fixed order), for one or two partial arrays.
-// Block = 64 columns x 4 row phases; each thread keeps 8 independent loads in
-// flight, the 4 phase partials are combined in LDS in fixed order.
+// Block = 16 columns x 16 row phases; each thread keeps 8 rows x 2 arrays of
+// loads in flight, so R <= 384 partial rows take <= 3 rounds of memory
+// latency (the previous 64 x 4 split needed up to 13: 6.7 us per call at
+// the ViT sizes); the 16 phase partials are combined in LDS in fixed order.
+constexpr int kCrCols = 16, kCrPh = 256 / kCrCols;
 __global__ __launch_bounds__(256) void col_reduce_kernel(const float* __restrict__ a, float* __restrict__ oa,
                                                          const float* __restrict__ b, float* __restrict__ ob, int R,
                                                          int C) {
-  __shared__ float red[2][4][64];
-  const int lane = threadIdx.x & 63, q = threadIdx.x >> 6;
-  const int c = blockIdx.x * 64 + lane;
+  __shared__ float red[2][kCrPh][kCrCols];
+  const int cl = threadIdx.x % kCrCols, q = threadIdx.x / kCrCols;
+  const int c = blockIdx.x * kCrCols + cl;
   float sa = 0.f, sb = 0.f;
   if (c < C) {
-    for (int r0 = q; r0 < R; r0 += 4 * 8) {
+    for (int r0 = q; r0 < R; r0 += kCrPh * 8) {
       float ta[8], tb[8];
 #pragma unroll
       for (int u = 0; u < 8; ++u) {
-        const int r = r0 + 4 * u;
+        const int r = r0 + kCrPh * u;
         ta[u] = r < R ? a[size_t(r) * C + c] : 0.f;
         tb[u] = (b && r < R) ? b[size_t(r) * C + c] : 0.f;
       }
@@ -237,12 +240,18 @@ __global__ __launch_bounds__(256) void col_reduce_kernel(const float* __restrict
       }
     }
   }
-  red[0][q][lane] = sa;
-  red[1][q][lane] = sb;
+  red[0][q][cl] = sa;
+  red[1][q][cl] = sb;
   __syncthreads();
   if (q == 0 && c < C) {
-    oa[c] = (red[0][0][lane] + red[0][1][lane]) + (red[0][2][lane] + red[0][3][lane]);
-    if (b) ob[c] = (red[1][0][lane] + red[1][1][lane]) + (red[1][2][lane] + red[1][3][lane]);
+    float xa = 0.f, xb = 0.f;
+#pragma unroll
+    for (int p = 0; p < kCrPh; ++p) {
+      xa += red[0][p][cl];
+      xb += red[1][p][cl];
+    }
+    oa[c] = xa;
+    if (b) ob[c] = xb;
   }
 }
 
@@ -448,7 +457,7 @@ static void ln_bwd_t(const void* dy, const void* x, const float* w, const float*
     hipLaunchKernelGGL((ln_bwd_kernel<T, 2>), grid, blk, lds, s, dyp, xp, w, mean, rstd, gp, dxp, pdw, pdb, N, C);
   else
     hipLaunchKernelGGL((ln_bwd_kernel<T, 4>), grid, blk, lds, s, dyp, xp, w, mean, rstd, gp, dxp, pdw, pdb, N, C);
-  hipLaunchKernelGGL(col_reduce_kernel, dim3((C + 63) / 64), blk, 0, s, pdw, dw, pdb, db, G, C);
+  hipLaunchKernelGGL(col_reduce_kernel, dim3((C + kCrCols - 1) / kCrCols), blk, 0, s, pdw, dw, pdb, db, G, C);
 }
 
 void layer_norm_bwd(bool bf16, const void* dy, const void* x, const float* w, const float* mean, const float* rstd,
@@ -486,7 +495,7 @@ void bias_gelu_bwd(bool bf16, const void* dy, const void* x, const float* b, voi
   else
     hipLaunchKernelGGL(bias_gelu_bwd_kernel<float>, grid, blk, 0, s, static_cast<const float*>(dy),
                        static_cast<const float*>(x), b, static_cast<float*>(dx), pdb, N, H);
-  hipLaunchKernelGGL(col_reduce_kernel, dim3((H + 63) / 64), blk, 0, s, pdb, db, nullptr, nullptr, S, H);
+  hipLaunchKernelGGL(col_reduce_kernel, dim3((H + kCrCols - 1) / kCrCols), blk, 0, s, pdb, db, nullptr, nullptr, S, H);
 }
 
 void column_sum(bool bf16, const void* dy, float* part, float* out, int N, int H, hipStream_t s) {
@@ -496,7 +505,7 @@ void column_sum(bool bf16, const void* dy, float* part, float* out, int N, int H
     hipLaunchKernelGGL(colsum_kernel<uint16_t>, grid, blk, 0, s, static_cast<const uint16_t*>(dy), part, N, H);
   else
     hipLaunchKernelGGL(colsum_kernel<float>, grid, blk, 0, s, static_cast<const float*>(dy), part, N, H);
-  hipLaunchKernelGGL(col_reduce_kernel, dim3((H + 63) / 64), blk, 0, s, part, out, nullptr, nullptr, S, H);
+  hipLaunchKernelGGL(col_reduce_kernel, dim3((H + kCrCols - 1) / kCrCols), blk, 0, s, part, out, nullptr, nullptr, S, H);
 }
 
 void xent_fwd(bool bf16, const void* z, const int64_t* y, float* loss, float* lse, int N, int K, hipStream_t s) {
