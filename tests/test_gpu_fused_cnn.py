@@ -197,3 +197,22 @@ def test_three_fused_peers_in_one_process():
     finally:
         for n in nodes:
             n.stop()
+
+
+def test_evaluate_matches_torch_reference():
+    """Evaluation runs 64-sample forward launches; loss / accuracy equal an fp32 PyTorch pass over the set."""
+    from p2pfl_amd.data import MnistFederatedDM
+    from p2pfl_amd.learning.fused_cnn import FusedCNNLearner
+    from p2pfl_amd.models import CNN
+
+    torch.manual_seed(3)
+    ln = FusedCNNLearner(CNN(seed=3), MnistFederatedDM(sub_id=0, number_sub=40, batch_size=32), "p", 1)
+    ln.fit()
+    res = ln.evaluate()
+    ld = ln.data.test_dataloader()
+    with torch.no_grad():
+        logits = ln.model(ld.x.float() / 255.0)
+        loss = torch.nn.functional.cross_entropy(logits, ld.y).item()
+        acc = (logits.argmax(1) == ld.y).float().mean().item()
+    assert abs(res["test_loss"] - loss) < 3e-2 * max(1.0, loss), (res, loss)
+    assert abs(res["test_metric"] - acc) <= 2.0 / len(ld.dataset) + 1e-6, (res, acc)
