@@ -87,17 +87,21 @@ void sgd_step(torch::Tensor p, torch::Tensor g, c10::optional<torch::Tensor> buf
 // tens: int64 [T, 3] (offset, numel, flags) on the GPU; chunks: int32 [C, 2]
 // (tensor, chunk) on the GPU; grads: one entry per tensor (None = skip).
 torch::Tensor grad_table(const std::vector<c10::optional<torch::Tensor>>& grads, const std::vector<int64_t>& numels,
-                         const std::vector<bool>& grad_bf16, const torch::Device& dev) {
+                         const std::vector<bool>& grad_bf16, const std::vector<bool>& grad_cl, const torch::Device& dev) {
   const size_t T = grads.size();
-  TORCH_CHECK(numels.size() == T && grad_bf16.size() == T, "multi-tensor step: table size mismatch");
+  TORCH_CHECK(numels.size() == T && grad_bf16.size() == T && grad_cl.size() == T,
+              "multi-tensor step: table size mismatch");
   auto host = torch::empty({int64_t(T)}, torch::dtype(torch::kInt64)).pin_memory();
   auto* hp = host.data_ptr<int64_t>();
   for (size_t t = 0; t < T; ++t) {
     hp[t] = 0;
     if (!grads[t].has_value() || !grads[t]->defined()) continue;
     const auto& g = *grads[t];
-    TORCH_CHECK(g.device() == dev && g.is_contiguous() && g.numel() == numels[t], "grad ", t,
-                " must be a contiguous GPU tensor of the parameter's size");
+    // channels-last tensors (flag bit 2): the gradient arrives in the
+    // weight's (O, kh, kw, I) memory order
+    const bool dense = grad_cl[t] ? (g.dim() == 4 && g.is_contiguous(at::MemoryFormat::ChannelsLast)) : g.is_contiguous();
+    TORCH_CHECK(g.device() == dev && dense && g.numel() == numels[t], "grad ", t,
+                " must be a dense GPU tensor of the parameter's size and layout");
     TORCH_CHECK(g.scalar_type() == (grad_bf16[t] ? torch::kBFloat16 : torch::kFloat32), "grad ", t,
                 " has an unexpected dtype");
     TORCH_CHECK(reinterpret_cast<uintptr_t>(g.data_ptr()) % 16 == 0, "grad ", t, " must be 16-byte aligned");
@@ -120,7 +124,7 @@ void check_tables(const torch::Tensor& tens, const torch::Tensor& chunks, const 
 // buffers have fixed addresses filled in after capture.
 torch::Tensor grad_ptrs(const c10::optional<torch::Tensor>& gtab, const std::vector<c10::optional<torch::Tensor>>& grads,
                         const std::vector<int64_t>& numels, const std::vector<bool>& grad_bf16,
-                        const torch::Tensor& tens, const torch::Device& dev) {
+                        const std::vector<bool>& grad_cl, const torch::Tensor& tens, const torch::Device& dev) {
   if (gtab.has_value() && gtab->defined()) {
     TORCH_CHECK(gtab->device() == dev && gtab->scalar_type() == torch::kInt64 && gtab->is_contiguous() &&
                     gtab->numel() == tens.size(0),
@@ -128,12 +132,13 @@ torch::Tensor grad_ptrs(const c10::optional<torch::Tensor>& gtab, const std::vec
     return *gtab;
   }
   TORCH_CHECK(tens.size(0) == int64_t(grads.size()), "multi-tensor step: one gradient per tensor");
-  return grad_table(grads, numels, grad_bf16, dev);
+  return grad_table(grads, numels, grad_bf16, grad_cl, dev);
 }
 
 void adam_mt_step(torch::Tensor p, torch::Tensor m, torch::Tensor v, c10::optional<torch::Tensor> pbf,
                   torch::Tensor tens, torch::Tensor chunks, std::vector<c10::optional<torch::Tensor>> grads,
-                  std::vector<int64_t> numels, std::vector<bool> grad_bf16, double lr, double b1, double b2, double eps,
+                  std::vector<int64_t> numels, std::vector<bool> grad_bf16, std::vector<bool> grad_cl, double lr,
+                  double b1, double b2, double eps,
                   double wd, int64_t step, bool decoupled, c10::optional<torch::Tensor> gtab,
                   c10::optional<torch::Tensor> t_dev) {
   for (auto* t : {&p, &m, &v}) check_f32(*t, "adam operand");
@@ -141,7 +146,7 @@ void adam_mt_step(torch::Tensor p, torch::Tensor m, torch::Tensor v, c10::option
   TORCH_CHECK(m.numel() == n && v.numel() == n, "adam: size mismatch");
   check_tables(tens, chunks, p.device());
   const c10::DeviceGuard guard(p.device());
-  auto gp = grad_ptrs(gtab, grads, numels, grad_bf16, tens, p.device());
+  auto gp = grad_ptrs(gtab, grads, numels, grad_bf16, grad_cl, tens, p.device());
   p2::AdamParams h{};
   h.lr = float(lr);
   h.beta1 = float(b1);
@@ -164,7 +169,8 @@ void adam_mt_step(torch::Tensor p, torch::Tensor m, torch::Tensor v, c10::option
 
 void sgd_mt_step(torch::Tensor p, c10::optional<torch::Tensor> buf, c10::optional<torch::Tensor> pbf,
                  torch::Tensor tens, torch::Tensor chunks, std::vector<c10::optional<torch::Tensor>> grads,
-                 std::vector<int64_t> numels, std::vector<bool> grad_bf16, double lr, double momentum,
+                 std::vector<int64_t> numels, std::vector<bool> grad_bf16, std::vector<bool> grad_cl, double lr,
+                 double momentum,
                  double dampening, double wd, bool nesterov, bool first_step, c10::optional<torch::Tensor> gtab) {
   check_f32(p, "p");
   const int64_t n = p.numel();
@@ -176,7 +182,7 @@ void sgd_mt_step(torch::Tensor p, c10::optional<torch::Tensor> buf, c10::optiona
   }
   check_tables(tens, chunks, p.device());
   const c10::DeviceGuard guard(p.device());
-  auto gp = grad_ptrs(gtab, grads, numels, grad_bf16, tens, p.device());
+  auto gp = grad_ptrs(gtab, grads, numels, grad_bf16, grad_cl, tens, p.device());
   p2::SgdParams h{float(lr), float(momentum), float(dampening), float(wd), nesterov ? 1 : 0, first_step ? 1 : 0};
   p2::sgd_mt_step(p.data_ptr<float>(), b, opt_bf16(pbf, n), reinterpret_cast<const p2::MTTensor*>(tens.data_ptr<int64_t>()),
                   reinterpret_cast<const int2*>(chunks.data_ptr<int32_t>()), int(chunks.size(0)),
@@ -196,13 +202,13 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("sgd_step", &sgd_step, "fused whole-arena SGD(+momentum/nesterov) step");
   m.def("adam_mt_step", &adam_mt_step, "multi-tensor Adam/AdamW over per-tensor grads into flat fp32 state",
         pybind11::arg("p"), pybind11::arg("m"), pybind11::arg("v"), pybind11::arg("pbf"), pybind11::arg("tens"),
-        pybind11::arg("chunks"), pybind11::arg("grads"), pybind11::arg("numels"), pybind11::arg("grad_bf16"),
+        pybind11::arg("chunks"), pybind11::arg("grads"), pybind11::arg("numels"), pybind11::arg("grad_bf16"), pybind11::arg("grad_cl"),
         pybind11::arg("lr"), pybind11::arg("beta1"), pybind11::arg("beta2"), pybind11::arg("eps"),
         pybind11::arg("weight_decay"), pybind11::arg("step"), pybind11::arg("decoupled"),
         pybind11::arg("gtab") = pybind11::none(), pybind11::arg("t_dev") = pybind11::none());
   m.def("sgd_mt_step", &sgd_mt_step, "multi-tensor SGD over per-tensor grads into flat fp32 state", pybind11::arg("p"),
         pybind11::arg("buf"), pybind11::arg("pbf"), pybind11::arg("tens"), pybind11::arg("chunks"),
-        pybind11::arg("grads"), pybind11::arg("numels"), pybind11::arg("grad_bf16"), pybind11::arg("lr"),
+        pybind11::arg("grads"), pybind11::arg("numels"), pybind11::arg("grad_bf16"), pybind11::arg("grad_cl"), pybind11::arg("lr"),
         pybind11::arg("momentum"), pybind11::arg("dampening"), pybind11::arg("weight_decay"),
         pybind11::arg("nesterov"), pybind11::arg("first_step"), pybind11::arg("gtab") = pybind11::none());
   register_cnn(m);

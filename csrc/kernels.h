@@ -33,6 +33,8 @@ void sgd_step(float* p, const float* g, float* buf, uint16_t* p_bf16, int64_t n,
 constexpr int kMTChunk = 4096;  // elements per block
 constexpr int kMTGradBf16 = 1;  // gradient tensor is bf16 (else fp32)
 constexpr int kMTShadow = 2;    // also write the bf16 shadow of the weight
+constexpr int kMTPermCL = 4;    // grad + shadow in channels-last (O, kh, kw, I) order; fp32 state OIHW.
+                                // flags bits 8..31 = I, bits 32..55 = kh * kw
 struct MTTensor {
   int64_t off;  // element offset in the flat arenas
   int64_t n;    // elements

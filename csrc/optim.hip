@@ -119,6 +119,15 @@ P2_DEVICE float load_grad1(const void* g, bool bf, int64_t i) {
   return bf ? bf16_to_f32(static_cast<const uint16_t*>(g)[i]) : static_cast<const float*>(g)[i];
 }
 
+// Memory position, in a channels-last (O, kh, kw, I) tensor, of logical
+// OIHW element ``i``.  32-bit math: one tensor stays below 2^31 elements.
+P2_DEVICE uint32_t cl_index(uint32_t i, uint32_t C, uint32_t HW) {
+  const uint32_t per_o = C * HW, o = i / per_o, r = i - o * per_o, c = r / HW, s = r - c * HW;
+  return o * per_o + s * C + c;
+}
+P2_DEVICE uint32_t cl_c(int64_t flags) { return uint32_t((flags >> 8) & 0xFFFFFF); }
+P2_DEVICE uint32_t cl_hw(int64_t flags) { return uint32_t((flags >> 32) & 0xFFFFFF); }
+
 P2_DEVICE void adam_elem(float& p, float g, float& m, float& v, const AdamParams& h) {
   if (h.weight_decay != 0.f) {
     if (h.decoupled)
@@ -152,6 +161,19 @@ __global__ __launch_bounds__(256) void adam_mt_kernel(float* __restrict__ p, flo
   float* M = m + T.off + start;
   float* V = v + T.off + start;
   uint16_t* PB = shadow ? pbf + T.off + start : nullptr;
+  if (T.flags & kMTPermCL) {
+    // fp32 state in logical (coalesced) order; the bf16 gradient and shadow
+    // are gathered / scattered at their channels-last positions (the whole
+    // slab of an output channel is L2-resident while its block runs)
+    const uint32_t C = cl_c(T.flags), HW = cl_hw(T.flags);
+    uint16_t* SB = shadow ? pbf + T.off : nullptr;
+    for (int64_t i = threadIdx.x; i < len; i += 256) {
+      const uint32_t j = cl_index(uint32_t(start + i), C, HW);
+      adam_elem(P[i], load_grad1(g, gbf, j), M[i], V[i], h);
+      if (SB) SB[j] = f32_to_bf16(P[i]);
+    }
+    return;
+  }
   for (int64_t i = int64_t(threadIdx.x) * 4; i < len4; i += 256 * 4) {
     float gg[4];
     load_grad4(g, gbf, start + i, gg);
@@ -201,6 +223,16 @@ __global__ __launch_bounds__(256) void sgd_mt_kernel(float* __restrict__ p, floa
   float* P = p + T.off + start;
   float* B = buf ? buf + T.off + start : nullptr;
   uint16_t* PB = shadow ? pbf + T.off + start : nullptr;
+  if (T.flags & kMTPermCL) {  // see adam_mt_kernel
+    const uint32_t C = cl_c(T.flags), HW = cl_hw(T.flags);
+    uint16_t* SB = shadow ? pbf + T.off : nullptr;
+    for (int64_t i = threadIdx.x; i < len; i += 256) {
+      const uint32_t j = cl_index(uint32_t(start + i), C, HW);
+      const float np = sgd_elem(P[i], load_grad1(g, gbf, j), B ? B + i : nullptr, h);
+      if (SB) SB[j] = f32_to_bf16(np);
+    }
+    return;
+  }
   for (int64_t i = threadIdx.x; i < len; i += 256) {
     const float np = sgd_elem(P[i], load_grad1(g, gbf, start + i), B ? B + i : nullptr, h);
     if (PB) PB[i] = f32_to_bf16(np);

@@ -155,6 +155,7 @@ class ModuleArena:
         grads: bool = False,
         compute_dtype: Optional[torch.dtype] = None,
         fp32_names: Optional[Iterable[str]] = None,
+        channels_last_names: Optional[Iterable[str]] = None,
     ) -> None:
         sd = module.state_dict(keep_vars=True)
         if device is None:
@@ -187,24 +188,49 @@ class ModuleArena:
         # The fp32 arena stays the master copy (FedAvg, gossip, checkpoints).
         self.shadow: Optional[torch.Tensor] = None
         self.shadow_names: Tuple[str, ...] = ()
+        self.shadow_cl: Dict[str, Tuple[int, Tuple[int, ...]]] = {}
         if compute_dtype is not None:
             if grads:
                 raise ValueError("mixed-precision arenas keep per-tensor grads (grads=False)")
             keep = set(fp32_names) if fp32_names is not None else {n for n, p in module.named_parameters() if p.dim() < 2}
+            # Conv weights named in ``channels_last_names`` get a channels-last
+            # (O, kh, kw, I) shadow region: with NHWC activations MIOpen then
+            # reads the weight as is and returns its gradient in the same
+            # layout, instead of a relayout copy of every conv weight per
+            # forward/backward and of every weight gradient per step.  The
+            # fp32 master (wire, FedAvg, checkpoints) keeps the OIHW order;
+            # the multi-tensor optimizer maps between the two.
+            cl = set(channels_last_names or ())
             self.shadow = torch.empty(self.layout.numel, dtype=compute_dtype, device=device)
-            self.shadow.copy_(flat)
             names = []
             for name, p in module.named_parameters():
                 if name in keep:
                     continue
                 off = self.layout.offsets[self.layout.names.index(name)]
-                p.data = self.shadow[off : off + p.numel()].view(p.shape)
+                region = self.shadow[off : off + p.numel()]
+                if name in cl and p.dim() == 4 and p.shape[2] * p.shape[3] > 1:
+                    o, i, kh, kw = p.shape
+                    self.shadow_cl[name] = (off, tuple(p.shape))
+                    p.data = region.view(o, kh, kw, i).permute(0, 3, 1, 2)
+                else:
+                    p.data = region.view(p.shape)
                 names.append(name)
             self.shadow_names = tuple(names)
+            self.refresh_shadow()
 
     @property
     def flat(self) -> torch.Tensor:
         return self.params.flat
+
+    def refresh_shadow(self) -> None:
+        """Rewrite the compute-dtype shadow from the fp32 master (channels-last regions permuted)."""
+        if self.shadow is None:
+            return
+        flat = self.params.flat
+        self.shadow.copy_(flat)
+        for off, (o, i, kh, kw) in self.shadow_cl.values():
+            n = o * i * kh * kw
+            self.shadow[off : off + n].view(o, kh, kw, i).copy_(flat[off : off + n].view(o, i, kh, kw).permute(0, 2, 3, 1))
 
     def sync_in(self) -> None:
         """Mirror non-float buffers into the arena (before sending / aggregating)."""
@@ -216,7 +242,7 @@ class ModuleArena:
         for name, t in self._int_buffers.items():
             t.copy_(self.params[name].reshape(t.shape).round().to(t.dtype))
         if self.shadow is not None:
-            self.shadow.copy_(self.params.flat)
+            self.refresh_shadow()
 
     def grads_bound(self) -> bool:
         if self.grads is None:

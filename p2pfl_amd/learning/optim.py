@@ -153,7 +153,9 @@ class MTTables:
     """Static per-tensor and per-chunk tables for the multi-tensor kernels.
 
     ``tens`` int64 [T, 3] = (arena offset, numel, flags) with flags bit 0 =
-    bf16 gradient, bit 1 = write the bf16 shadow; ``chunks`` int32 [C, 2] =
+    bf16 gradient, bit 1 = write the bf16 shadow, bit 2 = gradient and shadow
+    are channels-last (O, kh, kw, I) with I in bits 8..31 and kh*kw in bits
+    32..55 (the fp32 state stays OIHW); ``chunks`` int32 [C, 2] =
     (tensor, chunk index) -- one GPU block per 4096-element chunk.
     """
 
@@ -169,11 +171,15 @@ class MTTables:
         for t, (name, p) in enumerate(zip(names, self.params)):
             off = lay.offsets[lay.names.index(name)]
             flags = (1 if p.dtype == torch.bfloat16 else 0) | (2 if name in shadow else 0)
+            if name in arena.shadow_cl:
+                o, i, kh, kw = arena.shadow_cl[name][1]
+                flags |= 4 | (i << 8) | ((kh * kw) << 32)
             self.table.append((off, p.numel(), flags))
             chunks.extend((t, c) for c in range((p.numel() + self.CHUNK - 1) // self.CHUNK))
         dev = arena.flat.device
         self.numels = [n for _, n, _ in self.table]
         self.grad_bf16 = [bool(f & 1) for _, _, f in self.table]
+        self.grad_cl = [bool(f & 4) for _, _, f in self.table]
         self.tens = torch.tensor(self.table, dtype=torch.int64, device=dev).reshape(-1, 3)
         self.chunks = torch.tensor(chunks, dtype=torch.int32, device=dev).reshape(-1, 2)
 
@@ -182,6 +188,9 @@ class MTTables:
 
     def fill_grad_table(self, gtab: torch.Tensor) -> None:
         """Write the current gradients' addresses into the persistent device table ``gtab``."""
+        for p, cl in zip(self.params, self.grad_cl):
+            if p.grad is not None and not p.grad.is_contiguous(memory_format=torch.channels_last if cl else torch.contiguous_format):
+                raise RuntimeError(f"gradient of shape {tuple(p.grad.shape)} is not in its parameter's layout")
         ptrs = [p.grad.data_ptr() if p.grad is not None else 0 for p in self.params]
         gtab.copy_(torch.tensor(ptrs, dtype=torch.int64))
 

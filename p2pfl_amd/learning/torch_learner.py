@@ -109,7 +109,8 @@ class TorchLearner(NodeLearner):
         self.mixed = self._want_mixed(model)
         if self.mixed:
             keep = model.fp32_parameter_names() if hasattr(model, "fp32_parameter_names") else None
-            self.arena = ModuleArena(model, device=self.device, compute_dtype=torch.bfloat16, fp32_names=keep)
+            cl = model.channels_last_parameter_names() if hasattr(model, "channels_last_parameter_names") else None
+            self.arena = ModuleArena(model, device=self.device, compute_dtype=torch.bfloat16, fp32_names=keep, channels_last_names=cl)
         else:
             self.arena = ModuleArena(model, device=self.device, grads=True)
 

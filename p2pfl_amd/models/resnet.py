@@ -134,6 +134,12 @@ class ResNet(FLModule):
         x = torch.flatten(nn.functional.adaptive_avg_pool2d(x, 1), 1)
         return self.fc(x)
 
+    def channels_last_parameter_names(self) -> List[str]:
+        """Spatial conv weights a mixed-precision arena keeps in channels-last order (NHWC activations)."""
+        if not _CHANNELS_LAST:
+            return []
+        return [n for n, p in self.named_parameters() if p.dim() == 4 and p.shape[2] * p.shape[3] > 1]
+
     def configure_optimizers(self) -> torch.optim.Optimizer:
         return torch.optim.SGD(self.parameters(), lr=self.lr_rate, momentum=self.momentum, weight_decay=self.weight_decay)
 

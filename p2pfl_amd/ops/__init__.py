@@ -149,7 +149,11 @@ def _mt_reference(step_fn, p, states, pbf, table, grads):
         view = lambda t: t[off : off + n]  # noqa: E731
         step_fn(view(p), g.reshape(-1).float(), *[view(s) if s is not None else None for s in states])
         if pbf is not None and flags & 2:
-            view(pbf).copy_(view(p))
+            if flags & 4:  # channels-last shadow region
+                i, hw = (flags >> 8) & 0xFFFFFF, (flags >> 32) & 0xFFFFFF
+                view(pbf).view(-1, hw, i).copy_(view(p).view(-1, i, hw).transpose(1, 2))
+            else:
+                view(pbf).copy_(view(p))
 
 
 def adam_mt_step(p, m, v, grads, mt, *, lr, beta1, beta2, eps, weight_decay, step, decoupled=False, p_bf16=None, gtab=None, t_dev=None):
@@ -166,7 +170,7 @@ def adam_mt_step(p, m, v, grads, mt, *, lr, beta1, beta2, eps, weight_decay, ste
         )
         return
     ext().adam_mt_step(
-        p, m, v, p_bf16, mt.tens, mt.chunks, list(grads), mt.numels, mt.grad_bf16,
+        p, m, v, p_bf16, mt.tens, mt.chunks, list(grads), mt.numels, mt.grad_bf16, mt.grad_cl,
         float(lr), float(beta1), float(beta2), float(eps), float(weight_decay), int(step), bool(decoupled), gtab, t_dev,
     )
 
@@ -179,7 +183,7 @@ def sgd_mt_step(p, buf, grads, mt, *, lr, momentum=0.0, dampening=0.0, weight_de
         )
         return
     ext().sgd_mt_step(
-        p, buf, p_bf16, mt.tens, mt.chunks, list(grads), mt.numels, mt.grad_bf16,
+        p, buf, p_bf16, mt.tens, mt.chunks, list(grads), mt.numels, mt.grad_bf16, mt.grad_cl,
         float(lr), float(momentum), float(dampening), float(weight_decay), bool(nesterov), bool(first_step), gtab,
     )
 

@@ -77,15 +77,20 @@ def test_fedavg_uses_kernel_on_gpu():
 class _Tables:
     """Minimal MTTables stand-in: tensors at 64-aligned offsets of one arena."""
 
-    def __init__(self, sizes, bf16_flags, dev):
+    def __init__(self, sizes, bf16_flags, dev, cl=None):
         self.table, chunks, off = [], [], 0
+        cl = cl or [None] * len(sizes)
         for t, (n, bf) in enumerate(zip(sizes, bf16_flags)):
-            self.table.append((off, n, (1 if bf else 0) | (2 if bf else 0)))
+            flags = (1 if bf else 0) | (2 if bf else 0)
+            if cl[t] is not None:  # (in_channels, kh*kw): channels-last grad + shadow
+                flags |= 4 | (cl[t][0] << 8) | (cl[t][1] << 32)
+            self.table.append((off, n, flags))
             chunks.extend((t, c) for c in range((n + 4095) // 4096))
             off = (off + n + 63) // 64 * 64
         self.numel = max(off, 64)
         self.numels = list(sizes)
         self.grad_bf16 = list(bf16_flags)
+        self.grad_cl = [c is not None for c in cl]
         self.tens = torch.tensor(self.table, dtype=torch.int64, device=dev).reshape(-1, 3)
         self.chunks = torch.tensor(chunks, dtype=torch.int32, device=dev).reshape(-1, 2)
 
@@ -176,3 +181,46 @@ def test_gpu_learner_uses_mixed_precision(model):
         assert torch.equal(w.detach(), params[name].to(torch.bfloat16)), name
     if model != "resnet18":  # ResNet eval on a Dirichlet shard after 1 epoch is noisy
         assert nl.evaluate()["test_loss"] < ev0
+
+
+@pytest.mark.parametrize("opt", ["adam", "sgd"])
+def test_multi_tensor_channels_last(opt):
+    """Conv weights with channels-last grads/shadows: fp32 state in OIHW order, shadow written at OHWI positions."""
+    shapes = [(64, 32, 3, 3), (10, 7), (128, 64, 5, 5), (16, 3, 7, 7)]
+    cl = [(s[1], s[2] * s[3]) if len(s) == 4 else None for s in shapes]
+    sizes = [int(torch.Size(s).numel()) for s in shapes]
+    mt = _Tables(sizes, [True] * len(shapes), "cuda", cl=cl)
+    torch.manual_seed(5)
+    p = torch.randn(mt.numel, device="cuda")
+    st = [torch.zeros_like(p), torch.zeros_like(p)]
+    shadow = torch.zeros(mt.numel, device="cuda", dtype=torch.bfloat16)
+    p_ref, st_ref, s_ref = p.clone(), [t.clone() for t in st], shadow.clone()
+    for step in range(1, 4):
+        grads = []
+        for s in shapes:
+            g = torch.randn(s, device="cuda").to(torch.bfloat16)
+            grads.append(g.contiguous(memory_format=torch.channels_last) if len(s) == 4 else g)
+        if opt == "adam":
+            kw = dict(lr=1e-3, beta1=0.9, beta2=0.999, eps=1e-8, weight_decay=0.01, step=step)
+            ops.adam_mt_step(p, st[0], st[1], grads, mt, p_bf16=shadow, **kw)
+            ops._mt_reference(
+                lambda pp, g, mm, vv: ops.adam_step_reference(pp, g, mm, vv, 1e-3, 0.9, 0.999, 1e-8, 0.01, step, False),
+                p_ref, tuple(st_ref), s_ref, mt.table, grads,
+            )
+        else:
+            kw = dict(lr=0.05, momentum=0.9, dampening=0.0, weight_decay=5e-4, nesterov=False, first_step=step == 1)
+            ops.sgd_mt_step(p, st[0], grads, mt, p_bf16=shadow, **kw)
+            ops._mt_reference(
+                lambda pp, g, b: ops.sgd_step_reference(pp, g, b, 0.05, 0.9, 0.0, 5e-4, False, step == 1),
+                p_ref, (st_ref[0],), s_ref, mt.table, grads,
+            )
+    torch.testing.assert_close(p, p_ref, atol=1e-6, rtol=1e-5)
+    for (off, n, _), s in zip(mt.table, shapes):
+        want = p[off:off + n].view(s).to(torch.bfloat16)
+        got = shadow[off:off + n]
+        if len(s) == 4:  # channels-last region: memory order (O, kh, kw, I)
+            got = got.view(s[0], s[2], s[3], s[1]).permute(0, 3, 1, 2)
+        assert torch.equal(got.reshape(s), want)
+    with pytest.raises(RuntimeError):  # an OIHW-contiguous gradient is rejected for a channels-last tensor
+        bad = [g.contiguous() for g in grads]
+        ops.sgd_mt_step(p, st[0], bad, mt, lr=0.05, momentum=0.9, p_bf16=shadow)

@@ -110,3 +110,29 @@ def test_step_graph_resnet18_trains_like_eager():
     # both fit the shard; the graph run lands where the eager one does
     assert lg < first and le < first, (first, le, lg)
     assert abs(le - lg) < 0.5 * max(le, lg, 0.1), (first, le, lg)
+
+
+def test_resnet_channels_last_weight_shadows():
+    """ResNet spatial conv weights are channels-last bf16 shadows; MIOpen hands back channels-last grads, and
+    after graph-replayed steps every shadow equals its fp32 OIHW master rounded to bf16."""
+    from p2pfl_amd.learning.torch_learner import TorchLearner
+    from p2pfl_amd.models.resnet import ResNet18
+
+    torch.manual_seed(0)
+    ln = TorchLearner(ResNet18(seed=0, lr_rate=0.01), _cifar(), "p", 1, device=torch.device("cuda", 0), use_step_graphs=True)
+    arena = ln.arena
+    named = dict(ln.model.named_parameters())
+    assert arena.shadow_cl and all(named[n].is_contiguous(memory_format=torch.channels_last) for n in arena.shadow_cl)
+    # one eager backward: the conv weight grads arrive in the weights' own layout (no relayout copy)
+    x, y = next(iter(ln.data.train_dataloader()))
+    with torch.autocast("cuda", dtype=torch.bfloat16):
+        torch.nn.functional.cross_entropy(ln.model(x.cuda()), y.cuda()).backward()
+    for n in arena.shadow_cl:
+        g = named[n].grad
+        assert g is not None and g.dtype == torch.bfloat16 and g.is_contiguous(memory_format=torch.channels_last), n
+        named[n].grad = None
+    ln.model.zero_grad(set_to_none=True)
+    ln.fit()
+    torch.cuda.synchronize()
+    for n in arena.shadow_names:
+        assert torch.equal(named[n].detach(), arena.params[n].to(torch.bfloat16)), n

@@ -305,3 +305,44 @@ def test_multi_tensor_optimizer_matches_torch(opt_name):
             o.step()
     for (k, a), b in zip(m1.state_dict().items(), m2.state_dict().values()):
         assert torch.allclose(a, b, atol=1e-5, rtol=1e-4), k
+
+
+@pytest.mark.parametrize("opt_name", ["adam", "sgd"])
+def test_channels_last_shadow_optimizer_matches_torch(opt_name):
+    """Conv weights with a channels-last shadow: grads arrive NHWC-ordered, master/state stay OIHW, results == torch.optim."""
+    from p2pfl_amd.learning.arena import ModuleArena
+    from p2pfl_amd.learning.optim import fuse_optimizer_mt
+
+    def net():
+        torch.manual_seed(11)
+        return torch.nn.Sequential(torch.nn.Conv2d(3, 8, 3, padding=1), torch.nn.ReLU(), torch.nn.Conv2d(8, 4, 1),
+                                   torch.nn.Flatten(), torch.nn.Linear(4 * 6 * 6, 5))
+
+    m1, m2 = net(), net()
+    make = {
+        "adam": lambda ps: torch.optim.Adam(ps, lr=1e-2, weight_decay=1e-3),
+        "sgd": lambda ps: torch.optim.SGD(ps, lr=0.1, momentum=0.9, weight_decay=5e-4),
+    }[opt_name]
+    keep = [n for n, p in m1.named_parameters() if p.dim() < 2]
+    arena = ModuleArena(m1, compute_dtype=torch.float32, fp32_names=keep, channels_last_names=["0.weight", "2.weight"])
+    assert set(arena.shadow_cl) == {"0.weight"}  # 1x1 kernels need no permutation
+    w0 = m1[0].weight
+    assert w0.is_contiguous(memory_format=torch.channels_last) and not w0.is_contiguous()
+    o1 = fuse_optimizer_mt(make(list(m1.parameters())), arena)
+    assert o1.mt.grad_cl == [n == "0.weight" for n, _ in m1.named_parameters()]
+    o2 = make(list(m2.parameters()))
+    torch.manual_seed(0)
+    for _ in range(3):
+        x = torch.randn(8, 3, 6, 6).contiguous(memory_format=torch.channels_last)
+        y = torch.arange(8) % 5
+        for m, o in ((m1, o1), (m2, o2)):
+            o.zero_grad()
+            torch.nn.functional.cross_entropy(m(x), y).backward()
+            o.step()
+    for (k, a), b in zip(m1.state_dict().items(), m2.state_dict().values()):
+        assert torch.allclose(a, b, atol=1e-5, rtol=1e-4), k
+    master = arena.params["0.weight"]
+    assert torch.equal(w0.detach(), master)  # shadow (NHWC memory) == master (OIHW) element-wise
+    arena.params.flat.mul_(0.5)
+    arena.refresh_shadow()
+    assert torch.equal(w0.detach(), master)

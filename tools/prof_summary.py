@@ -36,7 +36,7 @@ def main() -> None:
     print(f"{hdr}: kernel time {tot / 1e6:.2f} ms over {sum(v[0] for v in agg.values())} launches\n")
     print("| kernel | calls | total ms | avg us | % |\n|---|---:|---:|---:|---:|")
     for name, (n, ns) in sorted(agg.items(), key=lambda kv: -kv[1][1])[:top]:
-        print(f"| `{name[:72]}` | {n} | {ns / 1e6:.3f} | {ns / n / 1e3:.2f} | {100 * ns / tot:.1f} |")
+        print(f"| `{name[:150]}` | {n} | {ns / 1e6:.3f} | {ns / n / 1e3:.2f} | {100 * ns / tot:.1f} |")
 
 
 if __name__ == "__main__":
