@@ -43,14 +43,14 @@ __global__ __launch_bounds__(256) void conv1_fwd_kernel(const uint8_t* __restric
                                                         const float* __restrict__ w1, const float* __restrict__ b1,
                                                         uint16_t* __restrict__ p1, uint8_t* __restrict__ am1,
                                                         uint16_t* __restrict__ p1s) {
-  __shared__ float img[32][33];
+  __shared__ float img[8][33];  // padded input rows 4q .. 4q+7 (all this block's windows read)
   __shared__ uint16_t sv[kC1][2][16];  // pooled values [oc][row][px], cols 14/15 zero
   __shared__ __attribute__((aligned(16))) uint8_t sa[28][kC1];  // argmax codes [pos][oc]
   const int b = blockIdx.y, q = blockIdx.x, tid = threadIdx.x;
   const int64_t row = idx ? idx[b] : b;
   const uint8_t* src = x + row * (kImg * kImg);
-  for (int i = tid; i < 32 * 32; i += 256) {
-    const int yy = i >> 5, xx = i & 31, sy = yy - 2, sx = xx - 2;
+  {
+    const int i = tid, yy = i >> 5, xx = i & 31, sy = 4 * q + yy - 2, sx = xx - 2;
     float v = 0.f;
     if (sy >= 0 && sy < kImg && sx >= 0 && sx < kImg) v = float(src[sy * kImg + sx]) * (1.f / 255.f);
     img[yy][xx] = v;
@@ -63,12 +63,12 @@ __global__ __launch_bounds__(256) void conv1_fwd_kernel(const uint8_t* __restric
   if (tid < kC1 * 2 * 2) sv[tid >> 2][(tid >> 1) & 1][14 + (tid & 1)] = 0;
   __syncthreads();
   for (int k = tid >> 5; k < 28; k += 8) {
-    const int rr = k / 14, px = k % 14, py = 2 * q + rr;
+    const int rr = k / 14, px = k % 14;
     float win[6][6];
 #pragma unroll
     for (int i = 0; i < 6; ++i)
 #pragma unroll
-      for (int j = 0; j < 6; ++j) win[i][j] = img[2 * py + i][2 * px + j];
+      for (int j = 0; j < 6; ++j) win[i][j] = img[2 * rr + i][2 * px + j];
     float best = -3.4e38f;
     int arg = 0;
 #pragma unroll

@@ -82,17 +82,33 @@ std::vector<torch::Tensor> ln_bwd(torch::Tensor dy, torch::Tensor x, torch::Tens
   return {dx, dw, db};
 }
 
-torch::Tensor column_sum(torch::Tensor x) {
+torch::Tensor split_sum_bf16(torch::Tensor parts) {
+  const c10::DeviceGuard g(parts.device());
+  TORCH_CHECK(parts.is_cuda() && parts.scalar_type() == torch::kBFloat16 && parts.is_contiguous() && parts.dim() >= 2,
+              "parts must be a contiguous bf16 [S, ...] GPU tensor");
+  const int64_t S = parts.size(0), n = parts.numel() / std::max<int64_t>(S, 1);
+  TORCH_CHECK(S >= 1 && n % 8 == 0, "split_sum_bf16: S >= 1 and a multiple-of-8 slice required");
+  TORCH_CHECK(reinterpret_cast<uintptr_t>(parts.data_ptr()) % 16 == 0, "parts must be 16-byte aligned");
+  auto out = torch::empty(parts.sizes().slice(1), parts.options());
+  if (n > 0)
+    p2fused::split_sum_bf16(reinterpret_cast<const uint16_t*>(parts.data_ptr<at::BFloat16>()),
+                            reinterpret_cast<uint16_t*>(out.data_ptr<at::BFloat16>()), n, int(S), stream());
+  return out;
+}
+
+torch::Tensor column_sum(torch::Tensor x, bool bf16_out) {
   const c10::DeviceGuard g(x.device());
   TORCH_CHECK(x.dim() == 2, "x must be [N, H]");
   const int64_t N = x.size(0), H = x.size(1);
   TORCH_CHECK(H % 8 == 0, "H must be a multiple of 8");
   const bool bf = act_dtype(x, "x");
   auto opt = x.options().dtype(torch::kFloat32);
-  auto out = torch::empty({H}, opt);
+  auto out = torch::empty({H}, bf16_out ? x.options().dtype(torch::kBFloat16) : opt);
   if (N > 0) {
     auto part = torch::empty({p2fused::bias_gelu_bwd_splits(int(N)), H}, opt);
-    p2fused::column_sum(bf, x.data_ptr(), part.data_ptr<float>(), out.data_ptr<float>(), int(N), int(H), stream());
+    p2fused::column_sum(bf, x.data_ptr(), part.data_ptr<float>(), bf16_out ? nullptr : out.data_ptr<float>(),
+                        bf16_out ? reinterpret_cast<uint16_t*>(out.data_ptr<at::BFloat16>()) : nullptr, int(N), int(H),
+                        stream());
   } else {
     out.zero_();
   }
@@ -216,7 +232,9 @@ void register_fused(pybind11::module& m) {
         pybind11::arg("residual") = pybind11::none());
   f.def("ln_bwd", &ln_bwd, pybind11::arg("dy"), pybind11::arg("x"), pybind11::arg("w"), pybind11::arg("mean"),
         pybind11::arg("rstd"), pybind11::arg("gsum") = pybind11::none());
-  f.def("column_sum", &column_sum, "fp32 column sums of a [N, H] bf16/fp32 activation (linear bias gradient)");
+  f.def("column_sum", &column_sum, "column sums of a [N, H] bf16/fp32 activation (linear bias gradient), fp32 or bf16 out",
+        pybind11::arg("x"), pybind11::arg("bf16_out") = false);
+  f.def("split_sum_bf16", &split_sum_bf16, "bf16 sum over dim 0 of [S, ...] bf16 partials, fp32 accumulation");
   f.def("bias_gelu_fwd", &bias_gelu_fwd);
   f.def("bias_gelu_bwd", &bias_gelu_bwd);
   f.def("xent_fwd", &xent_fwd);

@@ -25,7 +25,11 @@ void bias_gelu_bwd(bool bf16, const void* dy, const void* x, const float* b, voi
                    int H, hipStream_t s);
 
 // out[c] = sum_r x[r][c] over an [N, H] activation (H % 8 == 0); partials [bias_gelu_bwd_splits(N)][H]
-void column_sum(bool bf16, const void* x, float* part, float* out, int N, int H, hipStream_t s);
+// (out_bf != nullptr: the result is written as bf16 to out_bf instead of out)
+void column_sum(bool bf16, const void* x, float* part, float* out, uint16_t* out_bf, int N, int H, hipStream_t s);
+
+// out[i] = bf16(sum_s parts[s][i]) over S bf16 partial arrays of n elements (n % 8 == 0)
+void split_sum_bf16(const uint16_t* parts, uint16_t* out, int64_t n, int S, hipStream_t s);
 
 void xent_fwd(bool bf16, const void* z, const int64_t* y, float* loss, float* lse, int N, int K, hipStream_t s);
 void xent_bwd(bool bf16, const void* z, const int64_t* y, const float* lse, const float* gscale, void* dz, int N, int K,

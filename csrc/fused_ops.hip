@@ -219,7 +219,7 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const T* __restrict__ dy, c
 constexpr int kCrCols = 16, kCrPh = 256 / kCrCols;
 __global__ __launch_bounds__(256) void col_reduce_kernel(const float* __restrict__ a, float* __restrict__ oa,
                                                          const float* __restrict__ b, float* __restrict__ ob, int R,
-                                                         int C) {
+                                                         int C, uint16_t* __restrict__ oa_bf = nullptr) {
   __shared__ float red[2][kCrPh][kCrCols];
   const int cl = threadIdx.x % kCrCols, q = threadIdx.x / kCrCols;
   const int c = blockIdx.x * kCrCols + cl;
@@ -250,7 +250,10 @@ __global__ __launch_bounds__(256) void col_reduce_kernel(const float* __restrict
       xa += red[0][p][cl];
       xb += red[1][p][cl];
     }
-    oa[c] = xa;
+    if (oa_bf)  // bf16 result (a bf16 parameter's gradient): no separate cast kernel
+      oa_bf[c] = f32_to_bf16(xa);
+    else
+      oa[c] = xa;
     if (b) ob[c] = xb;
   }
 }
@@ -498,14 +501,48 @@ void bias_gelu_bwd(bool bf16, const void* dy, const void* x, const float* b, voi
   hipLaunchKernelGGL(col_reduce_kernel, dim3((H + kCrCols - 1) / kCrCols), blk, 0, s, pdb, db, nullptr, nullptr, S, H);
 }
 
-void column_sum(bool bf16, const void* dy, float* part, float* out, int N, int H, hipStream_t s) {
+void column_sum(bool bf16, const void* dy, float* part, float* out, uint16_t* out_bf, int N, int H, hipStream_t s) {
   const int S = bias_gelu_bwd_splits(N);
   const dim3 grid((H + 511) / 512, S), blk(256);
   if (bf16)
     hipLaunchKernelGGL(colsum_kernel<uint16_t>, grid, blk, 0, s, static_cast<const uint16_t*>(dy), part, N, H);
   else
     hipLaunchKernelGGL(colsum_kernel<float>, grid, blk, 0, s, static_cast<const float*>(dy), part, N, H);
-  hipLaunchKernelGGL(col_reduce_kernel, dim3((H + kCrCols - 1) / kCrCols), blk, 0, s, part, out, nullptr, nullptr, S, H);
+  hipLaunchKernelGGL(col_reduce_kernel, dim3((H + kCrCols - 1) / kCrCols), blk, 0, s, part, out, nullptr, nullptr, S, H,
+                     out_bf);
+}
+
+// ---------------------------------------------------------------------------
+// out[i] = bf16(sum_s parts[s][i]), fp32 accumulation in fixed s order: the
+// reduction of split-K weight-gradient partials (one pass; replaces a generic
+// reduce kernel + a float->bf16 cast kernel).  n % 8 == 0, 16-B accesses.
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void split_sum_bf16_kernel(const uint16_t* __restrict__ parts,
+                                                             uint16_t* __restrict__ out, int64_t n8, int S) {
+  const int64_t stride = int64_t(gridDim.x) * blockDim.x;
+  for (int64_t i = int64_t(blockIdx.x) * blockDim.x + threadIdx.x; i < n8; i += stride) {
+    float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    for (int sp = 0; sp < S; ++sp) {
+      const uint4 u = reinterpret_cast<const uint4*>(parts + size_t(sp) * size_t(n8) * 8)[i];
+      const uint32_t w[4] = {u.x, u.y, u.z, u.w};
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        acc[2 * k] += __uint_as_float(w[k] << 16);
+        acc[2 * k + 1] += __uint_as_float(w[k] & 0xffff0000u);
+      }
+    }
+    uint4 o;
+    o.x = pack_bf16x2(acc[0], acc[1]);
+    o.y = pack_bf16x2(acc[2], acc[3]);
+    o.z = pack_bf16x2(acc[4], acc[5]);
+    o.w = pack_bf16x2(acc[6], acc[7]);
+    reinterpret_cast<uint4*>(out)[i] = o;
+  }
+}
+
+void split_sum_bf16(const uint16_t* parts, uint16_t* out, int64_t n, int S, hipStream_t s) {
+  const int64_t n8 = n / 8;
+  hipLaunchKernelGGL(split_sum_bf16_kernel, dim3(stream_grid(n8, 256)), dim3(256), 0, s, parts, out, n8, S);
 }
 
 void xent_fwd(bool bf16, const void* z, const int64_t* y, float* loss, float* lse, int N, int K, hipStream_t s) {

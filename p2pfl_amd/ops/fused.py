@@ -143,6 +143,8 @@ def _wgrad(dy2: torch.Tensor, x2: torch.Tensor) -> torch.Tensor:
     if s == 1:
         return torch.mm(dy2.t(), x2)
     part = torch.bmm(dy2.view(s, M // s, N).transpose(1, 2), x2.contiguous().view(s, M // s, K))
+    if part.dtype == torch.bfloat16 and (N * K) % 8 == 0:
+        return _fx().split_sum_bf16(part)  # one pass, fp32 accumulation, bf16 out
     return part.sum(0, dtype=torch.float32).to(dy2.dtype)
 
 
@@ -169,7 +171,8 @@ class _Linear(torch.autograd.Function):
         if ctx.needs_input_grad[1]:
             dw = _wgrad(dy2, x.reshape(-1, x.shape[-1]))
         if ctx.has_bias and ctx.needs_input_grad[2]:
-            db = _fx().column_sum(dy2).to(ctx.bias_dtype)  # one streaming pass, not a generic reduce
+            # one streaming pass, not a generic reduce; a bf16 bias gets its bf16 gradient directly
+            db = _fx().column_sum(dy2, ctx.bias_dtype == torch.bfloat16).to(ctx.bias_dtype)
         return dx, dw, db
 
 

@@ -195,3 +195,20 @@ def test_linear_split_k_weight_grad(N, K):
     ref = g.float().t() @ x.detach().float()
     err = (w.grad.float() - ref).abs().max().item() / ref.abs().max().item()
     assert w.grad.dtype == torch.bfloat16 and err < 1e-2, err
+
+
+def test_split_sum_and_bf16_column_sum():
+    """Split-K partial reduction and the bf16-out column sum == fp32 PyTorch sums rounded to bf16."""
+    torch.manual_seed(4)
+    for S, shape in ((2, (768, 2304)), (4, (3072, 768)), (3, (8, 40))):
+        parts = torch.randn(S, *shape, device="cuda").to(torch.bfloat16)
+        want = parts.float().sum(0).to(torch.bfloat16)
+        got = ops.ext().fused.split_sum_bf16(parts)
+        assert got.shape == want.shape and got.dtype == torch.bfloat16
+        torch.testing.assert_close(got.float(), want.float(), atol=0, rtol=1e-2)
+        assert (got != want).float().mean() < 1e-3  # fp32 summation order only
+    g = torch.randn(6304, 768, device="cuda").to(torch.bfloat16)
+    f32 = ops.ext().fused.column_sum(g)
+    b16 = ops.ext().fused.column_sum(g, True)
+    assert b16.dtype == torch.bfloat16 and torch.equal(b16, f32.to(torch.bfloat16))
+    torch.testing.assert_close(f32, g.float().sum(0), atol=1e-2, rtol=1e-4)
