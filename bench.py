@@ -1,35 +1,41 @@
-"""Headline benchmark: MNIST-CNN FedAvg rounds, one federated peer per GPU.
+"""Headline benchmark: MNIST-CNN FedAvg rounds, one federated peer (Node) per GPU.
 
 Metric (BASELINE.json): wall-clock per round + samples/s per peer, MNIST-CNN
 FedAvg at 1/2/4/8 peers.  ``value`` is the whole-job aggregate training
 throughput (train samples/s summed over peers); ``ms_per_step`` is the
 wall-clock of one federated round.
 
-Per-peer round (weak scaling -- fixed per-peer work as N grows), matching the
-reference example ``p2pfl/examples/mnist.py`` shard (``MnistFederatedDM(sub_id,
-number_sub=20)``): 2,700 train / 300 val / 500 test MNIST-shaped samples,
-batch 32, the reference CNN (6.5 M params), Adam lr 1e-3 re-created per round,
-1 local epoch:
+What runs (default ``--aggregation gossip``): every rank is a full p2pfl
+:class:`~p2pfl_amd.node.Node` driven through the reference's stage machine
+(``Node.set_start_learning`` -> StartLearning -> VoteTrainSet -> Train ->
+GossipModel -> RoundFinished, reference ``node.py:297-364``) on the xGMI
+transport: control messages on the node-local bus, model pushes as RCCL
+point-to-point transfers over xGMI (epoch-grouped, k-way link-parallel
+fan-out), FedAvg of the received arenas by the hand-written HIP
+``weighted_sum`` kernel.  Each round per peer (weak scaling, fixed per-peer
+work): evaluate(test) -> fit(1 epoch + val) -> push partial aggregates to the
+train set -> FedAvg -> models_ready / diffusion.  Full-mesh deployment
+settings: train set = all peers, fan-out ``GOSSIP_MODELS_PER_ROUND = N-1``
+(one push per xGMI link), ``TTL = 1`` (every peer is a direct neighbour, so
+flooding adds no reachability); everything else is the reference default.
 
-    evaluate(test) -> fit(1 epoch + val) -> FedAvg over all peers (RCCL) -> load
+Timing: rounds run autonomously in each node's learning thread; a round hook
+synchronises the GPU and takes a barrier across ranks after round W (start)
+and after round W+K (end); the MAX over ranks of the bracketed time is
+reported.
 
-Implementations (``--impl``):
-  fused      hand-written HIP/CDNA4 CNN step (MFMA GEMMs, fused epilogues,
-             fused Adam), HIP-graph-captured; flat-arena FedAvg   [default]
-  torch      PyTorch-ROCm autograd (bf16 autocast) + fused arena Adam kernel
-  reference  reference-equivalent path: fp32 eager PyTorch, torch.optim.Adam,
-             double-forward eval, pickle encode/decode of the model and a
-             per-layer FedAvg loop (what p2pfl's Lightning learner executes),
-             used to measure the baseline on the same MI355X.
+Per-peer round work matches the reference example shard
+(``MnistFederatedDM(sub_id, number_sub=20)``): 2,700 train / 300 val / 500
+test MNIST-shaped samples, batch 32, the reference CNN (6.5 M params), Adam
+1e-3 re-created per round, 1 local epoch.
 
-Other BASELINE.json configurations (``--model``, PyTorch-ROCm path with the
-fused arena optimiser and, for ViT, the fused LayerNorm/GELU/xent kernels):
-  resnet18   CIFAR-10-shaped, non-IID Dirichlet(0.5) shards, SGD-momentum (config 3)
-  resnet50   CIFAR-10-shaped, Dirichlet shards (config 5's model)
-  vit_b16    ImageNet-shaped 224x224 (197 tokens), AdamW (config 4)
+Other modes: ``--aggregation allreduce`` (round-1 data-path runner: one
+weighted RCCL all-reduce instead of the protocol), ``--impl reference``
+(reference-equivalent fp32 eager path, used for the measured baseline),
+``--model resnet18|resnet50|vit_b16`` (BASELINE configs 3-5).
 
-Run:  python bench.py --gpus 1 --steps 3 --warmup 1
-      python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
+Launch: ``python bench.py --gpus N`` starts N worker processes itself (the
+launcher never touches the GPU); under ``torchrun`` each process is one rank.
 """
 
 from __future__ import annotations
@@ -38,8 +44,12 @@ import argparse
 import json
 import os
 import pickle
+import signal
+import socket
+import subprocess
 import sys
 import time
+import uuid
 
 sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 
@@ -47,14 +57,313 @@ import torch  # noqa: E402
 
 from p2pfl_amd.data import MnistFederatedDM  # noqa: E402
 from p2pfl_amd.models import CNN  # noqa: E402
-from p2pfl_amd.parallel import CollectiveFedAvg, init_distributed  # noqa: E402
-from p2pfl_amd.parallel.rounds import FederatedRoundRunner  # noqa: E402
 
 # Reference-equivalent baseline, measured (not published -- the reference
-# publishes no timing): `python bench.py --impl reference` on one MI355X,
-# 99.6 ms per round = 27,120.7 train samples/s per peer.
-# vs_baseline compares per-peer throughput (value / n_gpus) with it.
+# publishes no timing): `python bench.py --impl reference --aggregation
+# allreduce` on one MI355X, 99.6 ms per round = 27,120.7 train samples/s per
+# peer.  vs_baseline compares per-peer throughput with it; it is
+# context, not a published comparison (the reference's own control plane
+# sleeps >= 2 s per round on top of that work).
 BASELINE_SAMPLES_PER_SEC_PER_PEER = 27120.7
+
+
+# ----------------------------------------------------------------------------
+# configs
+# ----------------------------------------------------------------------------
+def build_config(args, rank):
+    """(model, data module, model description, data description) for ``--model``."""
+    if args.model == "cnn":
+        ns = args.number_sub or 20
+        data = MnistFederatedDM(sub_id=rank % ns, number_sub=ns, batch_size=args.batch)
+        return (
+            CNN(seed=1234),
+            data,
+            "MNIST-CNN (p2pfl CNN: conv5x5 32/64 + FC 3136-2048-10, 6.5M params), Adam 1e-3",
+            "synthetic MNIST-shaped (uint8 1x28x28, 10 classes), random-init weights",
+        )
+    if args.model in ("resnet18", "resnet50"):
+        from p2pfl_amd.data import Cifar10FederatedDM
+        from p2pfl_amd.models.resnet import ResNet18, ResNet50
+
+        ns = args.number_sub or 40
+        data = Cifar10FederatedDM(sub_id=rank % ns, number_sub=ns, batch_size=args.batch, partitioner="dirichlet", alpha=0.5)
+        make = ResNet18 if args.model == "resnet18" else ResNet50
+        n = "ResNet-18 (11.2M params)" if args.model == "resnet18" else "ResNet-50 (23.5M params)"
+        return (
+            make(num_classes=10, seed=1234),
+            data,
+            f"{n}, CIFAR stem, SGD(0.05, momentum 0.9, wd 5e-4)",
+            "synthetic CIFAR-10-shaped (uint8 3x32x32), Dirichlet(0.5) non-IID shards, random-init weights",
+        )
+    if args.model == "vit_b16":
+        from p2pfl_amd.data import ImageNetFederatedDM
+        from p2pfl_amd.models.vit import ViT_B16
+
+        ns = args.number_sub or 1
+        data = ImageNetFederatedDM(sub_id=rank % ns, number_sub=ns, batch_size=args.batch, n_train=1024, seed=rank)
+        return (
+            ViT_B16(num_classes=1000, seed=1234),
+            data,
+            "ViT-B/16 (86.6M params, 197 tokens), AdamW(3e-4, wd 0.05)",
+            "synthetic ImageNet-shaped (uint8 3x224x224, 1000 classes), random-init weights",
+        )
+    raise ValueError(args.model)
+
+
+def learner_class(args):
+    if args.impl == "fused" and args.model == "cnn":
+        from p2pfl_amd.learning.fused_cnn import FusedCNNLearner
+
+        return FusedCNNLearner
+    from p2pfl_amd.learning.torch_learner import TorchLearner
+
+    return TorchLearner
+
+
+def _sync(dev: torch.device) -> None:
+    if dev.type == "cuda":
+        torch.cuda.synchronize(dev)
+
+
+# ----------------------------------------------------------------------------
+# launcher (parent process: never touches the GPU)
+# ----------------------------------------------------------------------------
+def _free_port() -> int:
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch(args, argv) -> int:
+    """Start one worker process per GPU; return the first failing exit code."""
+    import torch.distributed as dist
+
+    n = args.gpus
+    port = _free_port()
+    # the job's c10d store lives here, so it survives any worker's death
+    store = dist.TCPStore("127.0.0.1", port, n, True, wait_for_workers=False)  # noqa: F841
+    job = uuid.uuid4().hex[:8]
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), TORCHELASTIC_USE_AGENT_STORE="True",
+                   TORCHELASTIC_RESTART_COUNT="0", P2PFL_JOB_ID=job)
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + argv, env=env, start_new_session=True))
+    rc = 0
+    deadline = time.monotonic() + args.watchdog + 60
+    try:
+        while True:
+            codes = [p.poll() for p in procs]
+            bad = [c for c in codes if c not in (None, 0)]
+            if bad:
+                rc = bad[0]
+                break
+            if all(c == 0 for c in codes):
+                break
+            if time.monotonic() > deadline:
+                print("[bench] launcher watchdog: workers did not finish", file=sys.stderr, flush=True)
+                rc = 124
+                break
+            time.sleep(0.05)
+    finally:
+        for p in procs:
+            if p.poll() is None:
+                try:
+                    os.killpg(p.pid, signal.SIGTERM)
+                except OSError:
+                    pass
+        for p in procs:
+            try:
+                p.wait(timeout=20)
+            except subprocess.TimeoutExpired:
+                try:
+                    os.killpg(p.pid, signal.SIGKILL)
+                except OSError:
+                    pass
+    return rc
+
+
+# ----------------------------------------------------------------------------
+# worker: full-stack Node per rank, gossip over the xGMI transport
+# ----------------------------------------------------------------------------
+class _Env:
+    def __init__(self) -> None:
+        self.world = int(os.environ.get("WORLD_SIZE", "1"))
+        self.rank = int(os.environ.get("RANK", "0"))
+        self.local = int(os.environ.get("LOCAL_RANK", "0"))
+        if torch.cuda.is_available():
+            idx = self.local % torch.cuda.device_count()
+            torch.cuda.set_device(idx)
+            self.device = torch.device("cuda", idx)
+        else:
+            self.device = torch.device("cpu")
+        import torch.distributed as dist
+
+        if self.world > 1:
+            os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+            dist.init_process_group("gloo", rank=self.rank, world_size=self.world)
+            self.store = dist.distributed_c10d._get_default_store()
+        else:
+            self.store = dist.HashStore()
+
+    def barrier(self) -> None:
+        if self.world > 1:
+            import torch.distributed as dist
+
+            dist.barrier()
+
+    def max(self, v: float) -> float:
+        if self.world == 1:
+            return v
+        import torch.distributed as dist
+
+        t = torch.tensor([v], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        return float(t.item())
+
+    def sum(self, v: float) -> float:
+        if self.world == 1:
+            return v
+        import torch.distributed as dist
+
+        t = torch.tensor([v], dtype=torch.float64)
+        dist.all_reduce(t)
+        return float(t.item())
+
+    def close(self) -> None:
+        if self.world > 1:
+            import torch.distributed as dist
+
+            dist.destroy_process_group()
+
+
+def run_gossip(args, env: _Env) -> dict:
+    from p2pfl_amd.communication.xgmi import XgmiJob
+    from p2pfl_amd.management.logger import logger
+    from p2pfl_amd.node import Node
+    from p2pfl_amd.settings import Settings
+
+    N, W, K = env.world, args.warmup, args.steps
+    Settings.LOG_LEVEL = os.environ.get("P2PFL_BENCH_LOG_LEVEL", "WARNING")
+    Settings.TRAIN_SET_SIZE = N
+    Settings.GOSSIP_MODELS_PER_ROUND = max(1, N - 1)
+    Settings.TTL = 1
+    Settings.WIRE_DTYPE = args.wire_dtype
+    job = XgmiJob(env.rank, N, env.store, device=env.device, prefix=f"p2pfl/{os.environ.get('P2PFL_JOB_ID', 'bench')}")
+    torch.manual_seed(1234)  # identical init on every peer (the initiator's model wins anyway)
+    model, data, desc, data_desc = build_config(args, env.rank)
+    node = Node(model, data, protocol=job.protocol, learner=learner_class(args), device=env.device)
+    marks = {}
+
+    def hook(state) -> None:
+        r = state.round
+        if r in (W, W + K):
+            _sync(env.device)
+            env.barrier()
+            marks[r] = time.perf_counter()
+
+    node.round_hooks.append(hook)
+    node.start()
+    try:
+        # full mesh: rank i handshakes with every lower rank
+        addrs = {}
+        for r in range(N):
+            a = env.store.get(f"{job.prefix}/addr/{r}")
+            addrs[r] = a.decode() if isinstance(a, (bytes, bytearray)) else a
+        for r in range(env.rank):
+            if not node.connect(addrs[r]):
+                raise RuntimeError(f"rank {env.rank} could not connect to rank {r}")
+        t_end = time.monotonic() + 120
+        while len(node.get_neighbors(only_direct=True)) < N - 1:
+            if time.monotonic() > t_end:
+                raise TimeoutError("full mesh did not form")
+            time.sleep(0.01)
+        plane = node._communication_protocol.plane
+        if plane is not None and not plane.ready.wait(180):
+            raise TimeoutError("data plane did not come up")
+        if plane is not None and plane.failed:
+            raise RuntimeError(plane.failed)
+        env.barrier()
+        t_start = time.perf_counter()
+        if W == 0:
+            marks[0] = t_start
+        if env.rank == 0:
+            node.set_start_learning(rounds=W + K, epochs=args.epochs)
+        t_end = time.monotonic() + args.watchdog
+        while node._learning_thread is None:
+            if time.monotonic() > t_end:
+                raise TimeoutError("learning never started")
+            time.sleep(0.001)
+        if not node.wait_learning(timeout=args.watchdog):
+            raise TimeoutError("learning did not finish")
+        if W + K not in marks or W not in marks:
+            raise RuntimeError(f"round marks missing: {sorted(marks)} (learning stopped early?)")
+        elapsed = env.max(marks[W + K] - marks[W])
+        # per-round phase breakdown from the tracer (this rank, timed rounds)
+        sp = lambda name: [s for s in logger.tracer.spans(node.addr, name) if s.start >= marks[W]]  # noqa: E731
+        ph = {k: sum(s.duration for s in sp(k)) / max(1, K) * 1e3 for k in ("evaluate", "fit", "wait_aggregation", "aggregate")}
+        pushes = logger.tracer.counters(node.addr)
+        stats = dict(plane.stats) if plane is not None else {}
+        print(
+            f"[bench rank {env.rank}] per-round (mean of {K}): " + ", ".join(f"{k} {v:.2f} ms" for k, v in ph.items())
+            + f"; data plane: {stats.get('sent', 0)} sends / {stats.get('received', 0)} recvs / "
+            f"{stats.get('groups', 0)} groups, {stats.get('nacked', 0)} declined; xgmi bytes sent "
+            f"{pushes.get('xgmi_bytes_sent', 0) / 1e6:.1f} MB",
+            file=sys.stderr, flush=True,
+        )
+        n_train = len(data.train_dataloader().dataset)
+        n_val = len(data.val_dataloader().dataset)
+        n_test = len(data.test_dataloader().dataset)
+        per_peer_total = env.sum(n_train * args.epochs * K / elapsed)
+        env.barrier()
+    finally:
+        node.stop()
+    return {
+        "elapsed": elapsed, "desc": desc, "data_desc": data_desc, "n_train": n_train, "n_val": n_val, "n_test": n_test,
+        "total": per_peer_total, "parallelism": "gossip-p2p", "transport": f"xgmi/{job.backend}",
+    }
+
+
+def run_allreduce(args, env: _Env) -> dict:
+    """Round-1 data-path runner: weighted RCCL all-reduce of the arenas (no protocol)."""
+    from p2pfl_amd.parallel import CollectiveFedAvg, DistEnv
+    from p2pfl_amd.parallel.rounds import FederatedRoundRunner
+
+    if env.world > 1 and env.device.type == "cuda":
+        import torch.distributed as dist
+
+        dist.destroy_process_group()
+        dist.init_process_group("nccl", rank=env.rank, world_size=env.world, device_id=env.device)
+    denv = DistEnv(env.rank, env.world, env.local, env.device)
+    torch.manual_seed(1234)
+    model, data, desc, data_desc = build_config(args, env.rank)
+    fed = CollectiveFedAvg(denv)
+    if args.impl == "reference":
+        learner = ReferenceEquivalentLearner(model, data, env.device)
+        weight = float(learner.get_num_samples()[0])
+        run = lambda: reference_round(learner, denv, weight)  # noqa: E731
+    else:
+        learner = learner_class(args)(model, data, f"peer{env.rank}", args.epochs, device=env.device)
+        runner = FederatedRoundRunner(learner, fed, name=f"peer{env.rank}")
+        run = lambda: runner.run_round().seconds  # noqa: E731
+    for i in range(args.warmup):
+        t = run()
+        print(f"[bench rank {env.rank}] warmup round {i}: {t * 1e3:.2f} ms", file=sys.stderr, flush=True)
+    fed.barrier()
+    _sync(env.device)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        run()
+    _sync(env.device)
+    fed.barrier()
+    elapsed = fed.max_over_ranks(time.perf_counter() - t0)
+    n_train = len(data.train_dataloader().dataset)
+    per_peer = n_train * args.epochs * args.steps / elapsed
+    return {
+        "elapsed": elapsed, "desc": desc, "data_desc": data_desc, "n_train": n_train,
+        "n_val": len(data.val_dataloader().dataset), "n_test": len(data.test_dataloader().dataset),
+        "total": per_peer * env.world, "parallelism": f"fedavg-allreduce-dp{env.world}", "transport": "rccl-allreduce",
+    }
 
 
 class ReferenceEquivalentLearner:
@@ -80,9 +389,6 @@ class ReferenceEquivalentLearner:
                 n += len(y)
         return tot / max(n, 1)
 
-    def evaluate(self):
-        return {"test_loss": self._eval(self.data.test_dataloader())}
-
     def fit(self):
         self.model.train()
         opt = torch.optim.Adam(self.model.parameters(), lr=1e-3)
@@ -94,7 +400,7 @@ class ReferenceEquivalentLearner:
         self._eval(self.data.val_dataloader())
 
     def get_parameters(self):
-        # reference encode: .cpu().numpy() + pickle; decode: pickle.loads + torch.tensor
+        # reference encode: .cpu().numpy() + pickle; decode: pickle.loads + torch.tensor (own data, trusted)
         blob = pickle.dumps([v.cpu().numpy() for v in self.model.state_dict().values()])
         arrays = pickle.loads(blob)
         self._keys = list(self.model.state_dict().keys())
@@ -104,78 +410,29 @@ class ReferenceEquivalentLearner:
         self.model.load_state_dict(dict(zip(self._keys, params)))
 
 
-def reference_round(learner, env, weight, total):
+def reference_round(learner, env, weight):
     import torch.distributed as dist
 
     t0 = time.perf_counter()
-    learner.evaluate()
+    learner._eval(learner.data.test_dataloader())
     learner.fit()
     params = learner.get_parameters()
-    # per-layer FedAvg over all peers' models (reference fedavg.py:49-58)
     gathered = [params]
     if env.world_size > 1:
-        gathered = []
-        for r in range(env.world_size):
-            gathered.append([p.clone() for p in params])
+        gathered = [[None] * len(params) for _ in range(env.world_size)]
         for i, p in enumerate(params):
             outs = [torch.empty_like(p) for _ in range(env.world_size)]
             dist.all_gather(outs, p)
             for r in range(env.world_size):
                 gathered[r][i] = outs[r]
     accum = [torch.zeros_like(p) for p in params]
-    for model in gathered:
+    for model in gathered:  # per-layer FedAvg loop (reference fedavg.py:49-58)
         for i, layer in enumerate(model):
             accum[i] = accum[i] + layer * weight
     accum = [a / (weight * len(gathered)) for a in accum]
     learner.set_parameters(accum)
-    _sync()
+    _sync(env.device)
     return time.perf_counter() - t0
-
-
-def build_config(args, env):
-    """(model, data module, model description, data description) for ``--model``."""
-    sub = env.rank
-    if args.model == "cnn":
-        ns = args.number_sub or 20
-        data = MnistFederatedDM(sub_id=sub % ns, number_sub=ns, batch_size=args.batch)
-        return (
-            CNN(seed=1234),
-            data,
-            "MNIST-CNN (p2pfl CNN: conv5x5 32/64 + FC 3136-2048-10, 6.5M params), Adam 1e-3",
-            "synthetic MNIST-shaped (uint8 1x28x28, 10 classes), random-init weights",
-        )
-    if args.model in ("resnet18", "resnet50"):
-        from p2pfl_amd.data import Cifar10FederatedDM
-        from p2pfl_amd.models.resnet import ResNet18, ResNet50
-
-        ns = args.number_sub or 40
-        data = Cifar10FederatedDM(sub_id=sub % ns, number_sub=ns, batch_size=args.batch, partitioner="dirichlet", alpha=0.5)
-        make = ResNet18 if args.model == "resnet18" else ResNet50
-        n = "ResNet-18 (11.2M params)" if args.model == "resnet18" else "ResNet-50 (23.5M params)"
-        return (
-            make(num_classes=10, seed=1234),
-            data,
-            f"{n}, CIFAR stem, SGD(0.05, momentum 0.9, wd 5e-4)",
-            "synthetic CIFAR-10-shaped (uint8 3x32x32), Dirichlet(0.5) non-IID shards, random-init weights",
-        )
-    if args.model == "vit_b16":
-        from p2pfl_amd.data import ImageNetFederatedDM
-        from p2pfl_amd.models.vit import ViT_B16
-
-        ns = args.number_sub or 1
-        data = ImageNetFederatedDM(sub_id=sub % ns, number_sub=ns, batch_size=args.batch, n_train=1024, seed=sub)
-        return (
-            ViT_B16(num_classes=1000, seed=1234),
-            data,
-            "ViT-B/16 (86.6M params, 197 tokens), AdamW(3e-4, wd 0.05)",
-            "synthetic ImageNet-shaped (uint8 3x224x224, 1000 classes), random-init weights",
-        )
-    raise ValueError(args.model)
-
-
-def _sync() -> None:
-    if torch.cuda.is_available():
-        torch.cuda.synchronize()
 
 
 def main() -> None:
@@ -183,94 +440,64 @@ def main() -> None:
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=3, help="timed federated rounds")
     ap.add_argument("--warmup", type=int, default=1, help="untimed federated rounds")
+    ap.add_argument("--aggregation", choices=["gossip", "allreduce"], default="gossip")
     ap.add_argument("--impl", choices=["fused", "torch", "reference"], default="fused")
     ap.add_argument("--model", choices=["cnn", "resnet18", "resnet50", "vit_b16"], default="cnn")
     ap.add_argument("--epochs", type=int, default=1)
     ap.add_argument("--number-sub", type=int, default=None, help="shards of the dataset (default per model)")
     ap.add_argument("--batch", type=int, default=32)
+    ap.add_argument("--wire-dtype", choices=["fp32", "bf16"], default="fp32", help="model arenas on the xGMI data plane")
     ap.add_argument("--watchdog", type=float, default=900, help="dump stacks and exit if the run hangs")
-    args = ap.parse_args()
+    argv = sys.argv[1:]
+    args = ap.parse_args(argv)
+    if args.impl == "reference":
+        args.aggregation = "allreduce"
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(launch(args, argv))
+
     import faulthandler
 
     faulthandler.dump_traceback_later(args.watchdog, exit=True)
-
-    env = init_distributed()
-    assert env.world_size == args.gpus, f"--gpus {args.gpus} but WORLD_SIZE={env.world_size}"
-    dev = env.device
-    torch.manual_seed(1234)  # identical init on every peer (the initiator's model)
-    model, data, desc, data_desc = build_config(args, env)
-    fed = CollectiveFedAvg(env)
-
-    if args.impl == "reference":
-        learner = ReferenceEquivalentLearner(model, data, dev)
-        weight = float(learner.get_num_samples()[0])
-        total = fed.total_weight(weight)
-        run = lambda: reference_round(learner, env, weight, total)  # noqa: E731
-    else:
-        if args.impl == "fused" and args.model == "cnn":
-            from p2pfl_amd.learning.fused_cnn import FusedCNNLearner as L
-        else:
-            from p2pfl_amd.learning.torch_learner import TorchLearner as L
-        learner = L(model, data, f"peer{env.rank}", args.epochs, device=dev)
-        runner = FederatedRoundRunner(learner, fed, name=f"peer{env.rank}")
-        run = lambda: runner.run_round().seconds  # noqa: E731
-
-    for i in range(args.warmup):
-        t = run()
-        print(f"[bench rank {env.rank}] warmup round {i}: {t * 1e3:.2f} ms", file=sys.stderr, flush=True)
-    fed.barrier()
-    _sync()
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        run()
-    _sync()
-    fed.barrier()
-    elapsed = fed.max_over_ranks(time.perf_counter() - t0)
-
-    if args.impl != "reference" and runner.history:
-        h = runner.history[-args.steps:]
-        k = len(h)
-        print(
-            f"[bench rank {env.rank}] per-round phases (mean of {k}): evaluate {sum(x.eval_s for x in h) / k * 1e3:.2f} ms, "
-            f"fit {sum(x.fit_s for x in h) / k * 1e3:.2f} ms, fedavg+load (+overlapped val) {sum(x.agg_s for x in h) / k * 1e3:.2f} ms",
-            file=sys.stderr,
-            flush=True,
-        )
-    n_train = len(data.train_dataloader().dataset)
-    ms_per_round = elapsed / args.steps * 1e3
-    per_peer = n_train * args.epochs * args.steps / elapsed
-    total = per_peer * env.world_size
-    if env.is_main:
-        base = BASELINE_SAMPLES_PER_SEC_PER_PEER
+    env = _Env()
+    if env.world != args.gpus:
+        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={env.world}")
+    res = run_gossip(args, env) if args.aggregation == "gossip" else run_allreduce(args, env)
+    ms_per_round = res["elapsed"] / args.steps * 1e3
+    total = res["total"]
+    per_peer = total / env.world
+    if env.rank == 0:
         print(
             json.dumps(
                 {
                     "metric": "train samples/s (aggregate over peers); wall-clock per FedAvg round in ms_per_step",
                     "value": round(total, 1),
                     "unit": "samples/s",
-                    "n_gpus": env.world_size,
+                    "n_gpus": env.world,
                     "steps": args.steps,
                     "warmup": args.warmup,
                     "ms_per_step": round(ms_per_round, 3),
                     "samples_per_sec_per_peer": round(per_peer, 1),
                     "higher_is_better": True,
                     "scaling": "weak",
-                    "vs_baseline": (round(per_peer / base, 3) if (base and args.model == "cnn") else None),
-                    "dtype": "bf16" if (args.impl != "reference" and dev.type == "cuda") else "fp32",
-                    "data": data_desc,
+                    "vs_baseline": (round(per_peer / BASELINE_SAMPLES_PER_SEC_PER_PEER, 3) if args.model == "cnn" else None),
+                    "dtype": "bf16" if (args.impl != "reference" and env.device.type == "cuda") else "fp32",
+                    "data": res["data_desc"],
                     "impl": args.impl if (args.model == "cnn" or args.impl != "fused") else "torch",
+                    "transport": res["transport"],
+                    "wire_dtype": args.wire_dtype,
                     "config": {
-                        "model": desc,
-                        "global_batch": args.batch * env.world_size,
+                        "model": res["desc"],
+                        "global_batch": args.batch * env.world,
                         "seq_len": 197 if args.model == "vit_b16" else None,
-                        "per_peer_round": f"{n_train} train + {len(data.val_dataloader().dataset)} val + "
-                        f"{len(data.test_dataloader().dataset)} test samples, {args.epochs} epoch",
-                        "parallelism": f"fedavg-dp{env.world_size}",
+                        "per_peer_round": f"{res['n_train']} train + {res['n_val']} val + {res['n_test']} test samples, "
+                        f"{args.epochs} epoch",
+                        "parallelism": res["parallelism"],
                     },
                 }
             ),
             flush=True,
         )
+    env.close()
 
 
 if __name__ == "__main__":

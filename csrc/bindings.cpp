@@ -194,6 +194,7 @@ void sgd_mt_step(torch::Tensor p, c10::optional<torch::Tensor> buf, c10::optiona
 void register_cnn(pybind11::module& m);
 void register_fused(pybind11::module& m);
 void register_bn(pybind11::module& m);
+void register_rccl(pybind11::module& m);
 
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.doc() = "p2pfl_amd native HIP/CDNA4 kernels (gfx950)";
@@ -214,4 +215,5 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   register_cnn(m);
   register_fused(m);
   register_bn(m);
+  register_rccl(m);
 }

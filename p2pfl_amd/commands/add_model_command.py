@@ -25,6 +25,20 @@ class AddModelCommand(Command):
     def get_name() -> str:
         return "add_model"
 
+    def precheck(self, source: str, round: int, contributors: List[str], weight: int) -> Optional[str]:
+        """Why this payload would be ignored (None: it would be used), evaluated
+        before the transfer (the receive path of the reference decoded every
+        payload first: ``add_model_command.py:79-83``)."""
+        if self.state.round is None or self.state.learner is None:
+            return "learning not running"
+        if round != self.state.round:
+            return f"late round ({round} != {self.state.round})"
+        if len(self.state.train_set) == 0:
+            return "no train set"
+        if not self.aggregator.would_accept(list(contributors)):
+            return "model not needed"
+        return None
+
     def execute(
         self,
         source: str,

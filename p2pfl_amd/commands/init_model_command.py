@@ -28,6 +28,17 @@ class InitModelCommand(Command):
     def get_name() -> str:
         return "init_model"
 
+    def precheck(self, source: str, round: int, contributors: List[str], weight: int) -> Optional[str]:
+        """Why this payload would be ignored (None: it would be used) -- lets a
+        data-plane transport decline a transfer before any byte moves."""
+        if self.state.learner is None:
+            return "learner not ready"
+        if round != self.state.round:
+            return f"late round ({round} != {self.state.round})"
+        if self.state.model_initialized.is_set():
+            return "model already initialized"
+        return None
+
     def execute(
         self,
         source: str,

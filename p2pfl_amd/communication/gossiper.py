@@ -132,13 +132,29 @@ class Gossiper(threading.Thread):
         period: float,
         create_connection: bool,
         wakeup: Any = None,
+        peer_status_fn: Optional[Callable[[str], Any]] = None,
     ) -> None:
+        """Push models until no candidate is left.
+
+        A candidate is (re)sent a model when it has never been sent one, when
+        ITS status (``peer_status_fn(n)``: what it reported having) changed
+        since the last send to it, or when a full ``period`` passed -- other
+        peers' reports waking the loop never cause duplicate multi-MB pushes
+        to a peer whose own state did not move.  Without ``peer_status_fn`` a
+        node-wide state change counts as the candidate's change.
+        """
         n_equal = max(1, Settings.GOSSIP_EXIT_ON_X_EQUAL_ROUNDS)
         last_status: Optional[str] = None
         equal_count = 0
         last_counted = 0.0
-        last_sent: Dict[str, Tuple[int, float]] = {}
+        last_sent: Dict[str, Tuple[Any, float]] = {}
         version = wakeup.version if wakeup is not None else 0
+
+        def token(n: str) -> Any:
+            if peer_status_fn is not None:
+                return repr(peer_status_fn(n))
+            return wakeup.version if wakeup is not None else version
+
         while True:
             t0 = time.monotonic()
             if early_stopping_fn() or self._terminate.is_set():
@@ -162,16 +178,17 @@ class Gossiper(threading.Thread):
             due = [
                 n
                 for n in neis
-                if n not in last_sent or last_sent[n][0] != version or (t0 - last_sent[n][1]) >= period * 0.999
+                if n not in last_sent or last_sent[n][0] != token(n) or (t0 - last_sent[n][1]) >= period * 0.999
             ]
             for nei in random.sample(due, min(Settings.GOSSIP_MODELS_PER_ROUND, len(due))):
+                tok = token(nei)
                 model = model_fn(nei)
                 if model is None:
                     continue
                 logger.debug(self._self_addr, f"Gossiping model to {nei}.")
                 with logger.span(self._self_addr, "gossip_send", cmd=getattr(model, "cmd", "?"), to=nei):
                     self._client.send(nei, model, create_connection=create_connection)
-                last_sent[nei] = (wakeup.version if wakeup is not None else version, time.monotonic())
+                last_sent[nei] = (tok, time.monotonic())
             # wait for a state change or the rest of the period
             remaining = max(0.0, period - (time.monotonic() - t0))
             if wakeup is not None:

@@ -74,6 +74,7 @@ class CommunicationProtocol(ABC):
         period: Optional[float] = None,
         create_connection: bool = False,
         wakeup: Any = None,
+        peer_status_fn: Optional[Callable[[str], Any]] = None,
     ) -> None: ...
 
     # -- optional capability (new) ---------------------------------------
@@ -161,6 +162,7 @@ class BaseCommunicationProtocol(CommunicationProtocol):
         period: Optional[float] = None,
         create_connection: bool = False,
         wakeup: Any = None,
+        peer_status_fn: Optional[Callable[[str], Any]] = None,
     ) -> None:
         self._gossiper.gossip_weights(
             early_stopping_fn,
@@ -170,4 +172,5 @@ class BaseCommunicationProtocol(CommunicationProtocol):
             Settings.GOSSIP_MODELS_PERIOD if period is None else period,
             create_connection,
             wakeup,
+            peer_status_fn,
         )

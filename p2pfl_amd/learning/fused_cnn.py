@@ -224,6 +224,9 @@ class FusedCNNLearner(TorchLearner):
 
     # -- parameters: keep the bf16 shadows in sync -------------------------
     def set_parameters(self, params) -> None:
+        if isinstance(params, FlatParams) and params.flat.data_ptr() == self.engine.params.data_ptr():
+            self._arena_changed()
+            return  # the arena itself: weights and bf16 shadows are already current
         super().set_parameters(params)
         with torch.cuda.stream(torch.cuda.current_stream(self.device)):
             self.engine.pack_shadows()
@@ -293,6 +296,7 @@ class FusedCNNLearner(TorchLearner):
         if self.epochs <= 0 or self.model is None:
             return
         self._interrupt.clear()
+        self._arena_changed()
         with self._lock:
             self.engine.reset_optimizer()  # Adam re-created per fit (reference quirk Q23)
             loader = self.data.train_dataloader()

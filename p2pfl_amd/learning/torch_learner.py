@@ -89,6 +89,8 @@ class TorchLearner(NodeLearner):
         # HIP-graph replay of the training step (mixed precision, device-resident data)
         self.use_step_graphs = use_step_graphs and os.environ.get("P2PFL_STEP_GRAPHS", "1") != "0"
         self._mt_opt: Any = None
+        self._arena_version = 0
+        self._snapshot: Optional[Tuple[int, FlatParams]] = None
         self._step_graph: Any = None
         self._eval_graphs: Dict[str, Any] = {}
         self.model: Any = None
@@ -143,8 +145,11 @@ class TorchLearner(NodeLearner):
 
     def set_parameters(self, params: Mapping[str, torch.Tensor]) -> None:
         assert self.arena is not None
+        self._arena_changed()
+        own = self.arena.params
+        if isinstance(params, FlatParams) and params.flat.data_ptr() == own.flat.data_ptr():
+            return  # the arena itself (e.g. a one-member aggregate): nothing to copy
         try:
-            own = self.arena.params
             if isinstance(params, FlatParams) and params.layout.compatible(own.layout):
                 own.flat.copy_(params.flat, non_blocking=True)
             else:
@@ -167,13 +172,29 @@ class TorchLearner(NodeLearner):
         return encode_params(params)
 
     def snapshot_parameters(self, params: Optional[Mapping[str, torch.Tensor]] = None) -> FlatParams:
+        """Immutable device payload for gossip.
+
+        Only the LIVE arena changes under a payload (training, set_parameters),
+        so only it is copied -- once per arena version, shared by every
+        neighbour and gossip iteration until the arena changes.  Aggregates and
+        received models are fresh buffers nobody mutates: they go out as is.
+        """
         if params is None:
             params = self.get_parameters()
         if isinstance(params, FlatParams):
-            return params.clone()
+            if self.arena is None or params.flat.data_ptr() != self.arena.flat.data_ptr():
+                return params
+            snap = self._snapshot
+            if snap is None or snap[0] != self._arena_version:
+                snap = self._snapshot = (self._arena_version, params.clone())
+            return snap[1]
         from p2pfl_amd.learning.arena import flatten
 
         return flatten(params, device=self.device)
+
+    def _arena_changed(self) -> None:
+        self._arena_version += 1
+        self._snapshot = None
 
     def decode_parameters(self, data: Any) -> FlatParams:
         assert self.arena is not None
@@ -246,6 +267,7 @@ class TorchLearner(NodeLearner):
         if self.epochs <= 0 or self.model is None:
             return
         self._interrupt.clear()
+        self._arena_changed()
         try:
             opt = self._make_optimizer()
             model = self.model

@@ -53,6 +53,15 @@ class Tracer:
                 if len(self._spans) < self.max_spans:
                     self._spans.append(sp)
 
+    def record(self, node: str, name: str, start: float, duration: float, **attrs: Any) -> None:
+        """Add a span measured by the caller (``start`` on the ``perf_counter`` clock)."""
+        if not self.enabled:
+            return
+        sp = Span(node, name, start, duration, threading.current_thread().name, dict(attrs))
+        with self._lock:
+            if len(self._spans) < self.max_spans:
+                self._spans.append(sp)
+
     def count(self, node: str, key: str, value: float = 1.0) -> None:
         with self._lock:
             self._counters[node][key] += value

@@ -79,6 +79,10 @@ class Node:
         self.state.simulation = simulation
         self.learning_workflow = LearningWorkflow()
         self._learning_thread: Optional[threading.Thread] = None
+        # callables run by the learning thread at every round boundary
+        # (after the round counter moved on): hook(state).  New; used by the
+        # benchmark to bracket its timed rounds with barriers.
+        self.round_hooks: list = []
 
         self._communication_protocol.add_command(
             [
@@ -175,8 +179,8 @@ class Node:
     # ------------------------------------------------------------------
     def _start_learning_thread(self, rounds: int, epochs: int) -> None:
         t = threading.Thread(target=self._start_learning, args=(rounds, epochs), name=f"learning_thread-{self.addr}", daemon=True)
-        self._learning_thread = t
         t.start()
+        self._learning_thread = t  # published only once joinable
 
     def set_start_learning(self, rounds: int = 1, epochs: int = 1) -> None:
         self.assert_running(True)
@@ -216,6 +220,7 @@ class Node:
                 aggregator=self.aggregator,
                 learner_class=self.learner_class,
                 learner_kwargs=self.learner_kwargs,
+                round_hooks=self.round_hooks,
             )
         except Exception as e:
             logger.error(self.addr, f"Error: {e}")

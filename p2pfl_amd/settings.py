@@ -67,6 +67,10 @@ class Settings:
     GRPC_MAX_MESSAGE_BYTES: int = 1 << 30
     """gRPC send/receive limit (the reference kept gRPC's 4 MiB default,
     which the 26 MB MNIST CNN exceeds: reference quirk Q6)."""
+    WIRE_DTYPE: str = "fp32"
+    """Element type of model arenas on the xGMI data plane: ``"fp32"`` (the
+    reference's numerics) or ``"bf16"`` (half the bytes per link; receivers
+    average bf16 inputs in fp32)."""
     TORCH_NUM_THREADS: int | None = None
     """If set, ``torch.set_num_threads`` value used by the learners
     (the reference hard-codes 1: ``lightning_learner.py:38``)."""

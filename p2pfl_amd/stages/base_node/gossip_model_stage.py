@@ -77,4 +77,11 @@ class GossipModelStage(Stage):
                 1,
             )
 
-        protocol.gossip_weights(lambda: state.round is None, candidates, candidates, model_fn, wakeup=state.changed)
+        protocol.gossip_weights(
+            lambda: state.round is None,
+            candidates,
+            candidates,
+            model_fn,
+            wakeup=state.changed,
+            peer_status_fn=lambda n: state.nei_status.get(n),
+        )

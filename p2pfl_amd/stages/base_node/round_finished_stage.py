@@ -33,6 +33,8 @@ class RoundFinishedStage(Stage):
         _auto_checkpoint(state)
         state.increase_round()
         logger.round_finished(state.addr)
+        for hook in kwargs.get("round_hooks") or ():
+            hook(state)
         logger.info(state.addr, f"Round {state.round} of {state.total_rounds} finished.")
         if state.round is None or state.total_rounds is None:
             raise Exception("Round or total rounds not set.")

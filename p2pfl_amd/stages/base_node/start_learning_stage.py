@@ -73,4 +73,11 @@ class StartLearningStage(Stage):
                 1,
             )
 
-        protocol.gossip_weights(lambda: state.round is None, candidates, candidates, model_fn, wakeup=state.changed)
+        protocol.gossip_weights(
+            lambda: state.round is None,
+            candidates,
+            candidates,
+            model_fn,
+            wakeup=state.changed,
+            peer_status_fn=lambda n: n in state.nei_status,
+        )

@@ -87,5 +87,11 @@ class TrainStage(Stage):
             )
 
         protocol.gossip_weights(
-            lambda: state.round is None, candidates, status, model_fn, create_connection=True, wakeup=state.changed
+            lambda: state.round is None,
+            candidates,
+            status,
+            model_fn,
+            create_connection=True,
+            wakeup=state.changed,
+            peer_status_fn=peer_has,
         )

@@ -17,11 +17,15 @@ import sys
 from concurrent.futures import ThreadPoolExecutor
 
 from setuptools import find_packages, setup
+import torch
 from torch.utils.cpp_extension import BuildExtension, CppExtension
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 ROCM = os.environ.get("ROCM_PATH", "/opt/rocm")
 ARCH = os.environ.get("PYTORCH_ROCM_ARCH", "gfx950")
+# RCCL: link the copy PyTorch ships (same soname, already loaded by torch), so
+# the data plane and torch.distributed share one library instance.
+TORCH_LIB = os.path.join(os.path.dirname(torch.__file__), "lib")
 OBJ_DIR = os.path.join(HERE, "build", "hipobj")
 HIP_FLAGS = [
     "-O3",
@@ -88,8 +92,9 @@ setup(
             sorted(glob.glob(os.path.join("csrc", "*.cpp"))),
             include_dirs=[os.path.join(HERE, "csrc"), os.path.join(ROCM, "include")],
             define_macros=[("__HIP_PLATFORM_AMD__", "1"), ("USE_ROCM", "1")],
-            library_dirs=[os.path.join(ROCM, "lib")],
-            libraries=["amdhip64", "c10_hip", "torch_hip"],
+            library_dirs=[TORCH_LIB, os.path.join(ROCM, "lib")],
+            libraries=["amdhip64", "c10_hip", "torch_hip", "rccl"],
+            extra_link_args=["-Wl,-rpath," + TORCH_LIB],
             extra_compile_args=["-O3", "-std=c++17"],
         )
     ],

@@ -24,7 +24,7 @@ if lockcheck.is_enabled():
     # held for a whole epoch / graph capture / blocking RCCL send by design
     lockcheck.enable(
         hold_warn_s=10.0,
-        exempt={"FusedCNNLearner._lock", "FusedCNN._CAPTURE_LOCK", "DistDataPlane._send_lock"},
+        exempt={"FusedCNNLearner._lock", "FusedCNN._CAPTURE_LOCK"},
     )
 
 
@@ -57,12 +57,17 @@ def pytest_collection_modifyitems(config, items):
             item.add_marker(skip)
 
 
-@pytest.fixture(params=["memory", "grpc"])
+@pytest.fixture(params=["memory", "grpc", "xgmi"])
 def protocol(request):
     if request.param == "memory":
         from p2pfl_amd.communication.memory import InMemoryCommunicationProtocol
 
         return InMemoryCommunicationProtocol
+    if request.param == "xgmi":
+        # node-local control bus + data plane on the strict RCCL-semantics simulator
+        from p2pfl_amd.communication.xgmi import XgmiSimNetwork
+
+        return XgmiSimNetwork().protocol
     from p2pfl_amd.communication.grpc import GrpcCommunicationProtocol
 
     return GrpcCommunicationProtocol

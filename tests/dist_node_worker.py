@@ -1,10 +1,11 @@
-"""Worker for tests/test_dist_protocol.py: one federated Node per torch.distributed rank.
+"""Worker for tests/test_dist_protocol.py: one federated Node per process on the xGMI transport.
 
-Run as ``python -m torch.distributed.run --nproc-per-node N tests/dist_node_worker.py OUT_JSON``
-(or spawned by the test).  Each rank builds a Node on the dist transport
-(gRPC control plane + torch.distributed weights data plane), ranks > 0
-connect to rank 0, rank 0 starts a 2-round experiment, and every rank
-reports its final parameters' checksum and its data-plane byte counters.
+Run as ``python -m torch.distributed.run --nproc-per-node N tests/dist_node_worker.py OUT_JSON [mlp|cnn]``.
+Each rank builds a Node on :class:`~p2pfl_amd.communication.xgmi.XgmiCommunicationProtocol`
+(node-local control bus + point-to-point data plane: RCCL with one GPU per
+rank, gloo otherwise -- ``P2PFL_XGMI_BACKEND`` overrides), ranks > 0 connect to
+rank 0, rank 0 starts a 2-round experiment, and every rank reports its final
+parameters' checksum and its data-plane byte counters.
 """
 
 from __future__ import annotations
@@ -21,29 +22,33 @@ import torch.distributed as dist  # noqa: E402
 
 
 def main(out: str, model_name: str = "mlp", rounds: int = 2) -> None:
-    from p2pfl_amd.communication.dist import DistCommunicationProtocol
+    from p2pfl_amd.communication.xgmi import XgmiJob
     from p2pfl_amd.data import MnistFederatedDM
+    from p2pfl_amd.learning.fused_cnn import auto_learner
     from p2pfl_amd.management.logger import logger
     from p2pfl_amd.models import CNN, MLP
     from p2pfl_amd.node import Node
-    from p2pfl_amd.parallel import init_distributed
     from p2pfl_amd.settings import Settings
     from p2pfl_amd.utils import set_test_settings
 
-    env = init_distributed()
+    rank, world = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
+    local = int(os.environ.get("LOCAL_RANK", rank))
+    dev = torch.device("cuda", local % torch.cuda.device_count()) if torch.cuda.is_available() else torch.device("cpu")
+    if dev.type == "cuda":
+        torch.cuda.set_device(dev)
+    dist.init_process_group("gloo")
+    store = dist.distributed_c10d._get_default_store()
     set_test_settings()
     Settings.LOG_LEVEL = "INFO"
-    rank, world = env.rank, env.world_size
+    job = XgmiJob(rank, world, store, device=dev, backend=os.environ.get("P2PFL_XGMI_BACKEND", "auto"))
     model = MLP(seed=rank) if model_name == "mlp" else CNN(seed=rank)
-    from p2pfl_amd.learning.fused_cnn import auto_learner
-
-    node = Node(model, MnistFederatedDM(sub_id=rank, number_sub=2 * world), protocol=DistCommunicationProtocol,
-                learner=auto_learner, device=env.device)
+    node = Node(model, MnistFederatedDM(sub_id=rank, number_sub=2 * world), protocol=job.protocol,
+                learner=auto_learner, device=dev)
     node.start()
     try:
-        addrs = node._communication_protocol.peer_addresses()
+        addr0 = store.get(f"{job.prefix}/addr/0").decode()
         if rank > 0:
-            assert node.connect(addrs[0])
+            assert node.connect(addr0)
         t0 = time.time()
         while len(node.get_neighbors(only_direct=False)) < world - 1:
             if time.time() - t0 > 60:
@@ -53,29 +58,28 @@ def main(out: str, model_name: str = "mlp", rounds: int = 2) -> None:
         if rank == 0:
             node.set_start_learning(rounds=rounds, epochs=1)
         t0 = time.time()
-        while node.state.learner is None or node._learning_thread is None:
+        while node._learning_thread is None:
             if time.time() - t0 > 120:
                 raise TimeoutError("learning never started")
             time.sleep(0.05)
         assert node.wait_learning(timeout=600), "learning did not finish"
         flat = node.state.learner.get_parameters().flat.detach().float().cpu()
-        counters = logger.tracer.counters(node.addr)
         rec = {
             "rank": rank,
             "sum": float(flat.double().sum()),
             "abs": float(flat.double().abs().sum()),
             "metrics": node.state.learner.evaluate(),
-            "counters": counters,
+            "counters": logger.tracer.counters(node.addr),
+            "transport": f"xgmi/{job.backend}",
         }
         objs = [None] * world
         dist.all_gather_object(objs, rec)
         if rank == 0:
             with open(out, "w") as f:
                 json.dump(objs, f)
-        dist.barrier()
+        dist.barrier()  # nobody stops while a peer may still push
     finally:
         node.stop()
-        dist.barrier()  # every rank's data plane drained before any group is destroyed
         dist.destroy_process_group()
 
 

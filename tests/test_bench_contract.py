@@ -1,4 +1,5 @@
-"""bench.py driver contract on the CPU: one JSON line; the N>1 path under torchrun (gloo)."""
+"""bench.py driver contract on the CPU: one JSON line, for N=1, for N=2 self-launched
+(no torchrun: bench.py starts its own worker processes) and for N=2 under torchrun."""
 
 from __future__ import annotations
 
@@ -31,10 +32,11 @@ def _json_lines(out: str):
 
 
 @pytest.mark.timeout(600)
-@pytest.mark.parametrize("world", [1, 2])
-def test_bench_json_line(world):
-    args = ["bench.py", "--gpus", str(world), "--steps", "1", "--warmup", "1", "--impl", "torch", "--number-sub", "200"]
-    if world == 1:
+@pytest.mark.parametrize("world,launcher", [(1, "self"), (2, "self"), (2, "torchrun")])
+def test_bench_json_line(world, launcher):
+    args = ["bench.py", "--gpus", str(world), "--steps", "1", "--warmup", "1", "--impl", "torch", "--number-sub", "200",
+            "--watchdog", "300"]
+    if launcher == "self":
         cmd = [sys.executable] + args
     else:
         cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={world}",
@@ -46,7 +48,17 @@ def test_bench_json_line(world):
     rec = lines[0]
     assert KEYS <= set(rec)
     assert rec["n_gpus"] == world and rec["steps"] == 1 and rec["scaling"] == "weak"
-    assert rec["config"]["parallelism"] == f"fedavg-dp{world}"
+    assert rec["config"]["parallelism"] == "gossip-p2p"  # full Node stack, gossip over the xGMI transport
     assert rec["value"] > 0 and rec["ms_per_step"] > 0
     # whole-job aggregate: value = per-peer throughput x peers
     assert abs(rec["value"] - rec["samples_per_sec_per_peer"] * world) <= 1e-3 * rec["value"] + 0.2
+
+
+@pytest.mark.timeout(600)
+def test_bench_allreduce_mode_still_available():
+    cmd = [sys.executable, "bench.py", "--gpus", "1", "--steps", "1", "--warmup", "1", "--impl", "torch",
+           "--number-sub", "200", "--aggregation", "allreduce"]
+    r = subprocess.run(cmd, cwd=ROOT, env=_env(), capture_output=True, text=True, timeout=560)
+    assert r.returncode == 0, r.stderr[-3000:]
+    rec = _json_lines(r.stdout)[0]
+    assert rec["config"]["parallelism"] == "fedavg-allreduce-dp1"
