@@ -12,70 +12,95 @@
 namespace p2 {
 
 struct WSumArgs {
-  const float* src[kMaxInputs];
+  const void* src[kMaxInputs];
   float w[kMaxInputs];
 };
 
+// Four consecutive elements of input k as fp32: a 16-byte fp32 load or an
+// 8-byte bf16 load widened in registers (a bf16 arena costs half the bytes).
+P2_DEVICE f32x4 load4(const void* base, int64_t i, bool bf16) {
+  if (bf16) {
+    const uint2 r = __builtin_bit_cast(uint2, __builtin_nontemporal_load(reinterpret_cast<const u32x2*>(base) + i));
+    return f32x4{__uint_as_float(r.x << 16), __uint_as_float(r.x & 0xffff0000u), __uint_as_float(r.y << 16),
+                 __uint_as_float(r.y & 0xffff0000u)};
+  }
+  return __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(base) + i);
+}
+
+// bf16_mask bit k: input k is bf16 (else fp32).  The mask is uniform across
+// the grid, so the per-input dtype test never diverges.
 template <int K>
-__global__ __launch_bounds__(256) void wsum_kernel(WSumArgs a, float* __restrict__ out, int64_t n4,
-                                                   int accumulate) {
+__global__ __launch_bounds__(256) void wsum_kernel(WSumArgs a, uint32_t bf16_mask, void* __restrict__ out, int out_bf16,
+                                                   int64_t n4, int accumulate) {
   const int64_t stride = int64_t(gridDim.x) * blockDim.x;
   for (int64_t i = int64_t(blockIdx.x) * blockDim.x + threadIdx.x; i < n4; i += stride) {
     f32x4 acc = accumulate ? reinterpret_cast<const f32x4*>(out)[i] : f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-    for (int k = 0; k < K; ++k) {
-      const f32x4 v = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(a.src[k]) + i);
-      acc += a.w[k] * v;
+    for (int k = 0; k < K; ++k) acc += a.w[k] * load4(a.src[k], i, (bf16_mask >> k) & 1u);
+    if (out_bf16) {
+      reinterpret_cast<uint2*>(out)[i] = uint2{pack_bf16x2(acc[0], acc[1]), pack_bf16x2(acc[2], acc[3])};
+    } else {
+      reinterpret_cast<f32x4*>(out)[i] = acc;
     }
-    reinterpret_cast<f32x4*>(out)[i] = acc;
   }
 }
 
-__global__ void wsum_tail(WSumArgs a, int k, float* out, int64_t start, int64_t n, int accumulate) {
+__global__ void wsum_tail(WSumArgs a, uint32_t bf16_mask, int k, void* out, int out_bf16, int64_t start, int64_t n,
+                          int accumulate) {
   int64_t i = start + blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
-  float acc = accumulate ? out[i] : 0.f;
-  for (int j = 0; j < k; ++j) acc = fmaf(a.w[j], a.src[j][i], acc);
-  out[i] = acc;
+  float acc = accumulate ? reinterpret_cast<const float*>(out)[i] : 0.f;
+  for (int j = 0; j < k; ++j) {
+    const float v = ((bf16_mask >> j) & 1u) ? bf16_to_f32(reinterpret_cast<const uint16_t*>(a.src[j])[i])
+                                            : reinterpret_cast<const float*>(a.src[j])[i];
+    acc = fmaf(a.w[j], v, acc);
+  }
+  if (out_bf16)
+    reinterpret_cast<uint16_t*>(out)[i] = f32_to_bf16(acc);
+  else
+    reinterpret_cast<float*>(out)[i] = acc;
 }
 
 template <int K>
-static void launch_k(const WSumArgs& a, float* out, int64_t n4, int acc, hipStream_t s) {
-  hipLaunchKernelGGL(wsum_kernel<K>, dim3(stream_grid(n4, 256)), dim3(256), 0, s, a, out, n4, acc);
+static void launch_k(const WSumArgs& a, uint32_t mask, void* out, int out_bf16, int64_t n4, int acc, hipStream_t s) {
+  hipLaunchKernelGGL(wsum_kernel<K>, dim3(stream_grid(n4, 256)), dim3(256), 0, s, a, mask, out, out_bf16, n4, acc);
 }
 
-void weighted_sum(const float* const* srcs, const float* weights, int k, float* out, int64_t n,
-                  hipStream_t stream) {
+void weighted_sum(const void* const* srcs, const int* src_bf16, const float* weights, int k, void* out, int out_bf16,
+                  int64_t n, hipStream_t stream) {
   int done = 0;
   while (done < k) {
     const int kk = (k - done) < kMaxInputs ? (k - done) : kMaxInputs;
     WSumArgs a{};
+    uint32_t mask = 0;
     for (int j = 0; j < kk; ++j) {
       a.src[j] = srcs[done + j];
       a.w[j] = weights[done + j];
+      if (src_bf16[done + j]) mask |= 1u << j;
     }
-    const int acc = done > 0;
+    const int acc = done > 0;  // chunks after the first accumulate (fp32 output only; checked by the caller)
     const int64_t n4 = n / 4;
     switch (kk) {
-      case 1: launch_k<1>(a, out, n4, acc, stream); break;
-      case 2: launch_k<2>(a, out, n4, acc, stream); break;
-      case 3: launch_k<3>(a, out, n4, acc, stream); break;
-      case 4: launch_k<4>(a, out, n4, acc, stream); break;
-      case 5: launch_k<5>(a, out, n4, acc, stream); break;
-      case 6: launch_k<6>(a, out, n4, acc, stream); break;
-      case 7: launch_k<7>(a, out, n4, acc, stream); break;
-      case 8: launch_k<8>(a, out, n4, acc, stream); break;
-      case 9: launch_k<9>(a, out, n4, acc, stream); break;
-      case 10: launch_k<10>(a, out, n4, acc, stream); break;
-      case 11: launch_k<11>(a, out, n4, acc, stream); break;
-      case 12: launch_k<12>(a, out, n4, acc, stream); break;
-      case 13: launch_k<13>(a, out, n4, acc, stream); break;
-      case 14: launch_k<14>(a, out, n4, acc, stream); break;
-      case 15: launch_k<15>(a, out, n4, acc, stream); break;
-      default: launch_k<16>(a, out, n4, acc, stream); break;
+      case 1: launch_k<1>(a, mask, out, out_bf16, n4, acc, stream); break;
+      case 2: launch_k<2>(a, mask, out, out_bf16, n4, acc, stream); break;
+      case 3: launch_k<3>(a, mask, out, out_bf16, n4, acc, stream); break;
+      case 4: launch_k<4>(a, mask, out, out_bf16, n4, acc, stream); break;
+      case 5: launch_k<5>(a, mask, out, out_bf16, n4, acc, stream); break;
+      case 6: launch_k<6>(a, mask, out, out_bf16, n4, acc, stream); break;
+      case 7: launch_k<7>(a, mask, out, out_bf16, n4, acc, stream); break;
+      case 8: launch_k<8>(a, mask, out, out_bf16, n4, acc, stream); break;
+      case 9: launch_k<9>(a, mask, out, out_bf16, n4, acc, stream); break;
+      case 10: launch_k<10>(a, mask, out, out_bf16, n4, acc, stream); break;
+      case 11: launch_k<11>(a, mask, out, out_bf16, n4, acc, stream); break;
+      case 12: launch_k<12>(a, mask, out, out_bf16, n4, acc, stream); break;
+      case 13: launch_k<13>(a, mask, out, out_bf16, n4, acc, stream); break;
+      case 14: launch_k<14>(a, mask, out, out_bf16, n4, acc, stream); break;
+      case 15: launch_k<15>(a, mask, out, out_bf16, n4, acc, stream); break;
+      default: launch_k<16>(a, mask, out, out_bf16, n4, acc, stream); break;
     }
     const int64_t tail = n - n4 * 4;
-    if (tail > 0) hipLaunchKernelGGL(wsum_tail, dim3(1), dim3(64), 0, stream, a, kk, out, n4 * 4, n, acc);
+    if (tail > 0)
+      hipLaunchKernelGGL(wsum_tail, dim3(1), dim3(64), 0, stream, a, mask, kk, out, out_bf16, n4 * 4, n, acc);
     done += kk;
   }
 }

@@ -22,21 +22,33 @@ void check_f32(const torch::Tensor& t, const char* name) {
   TORCH_CHECK(reinterpret_cast<uintptr_t>(t.data_ptr()) % 16 == 0, name, " must be 16-byte aligned");
 }
 
+void check_arena(const torch::Tensor& t, const char* name) {
+  TORCH_CHECK(t.is_cuda(), name, " must be a GPU tensor");
+  TORCH_CHECK(t.scalar_type() == torch::kFloat32 || t.scalar_type() == torch::kBFloat16, name, " must be float32 or bfloat16");
+  TORCH_CHECK(t.is_contiguous(), name, " must be contiguous");
+  TORCH_CHECK(reinterpret_cast<uintptr_t>(t.data_ptr()) % 16 == 0, name, " must be 16-byte aligned");
+}
+
 void weighted_sum(std::vector<torch::Tensor> srcs, std::vector<double> weights, torch::Tensor out) {
   TORCH_CHECK(!srcs.empty() && srcs.size() == weights.size(), "weighted_sum: bad inputs");
-  check_f32(out, "out");
+  check_arena(out, "out");
+  const bool out_bf16 = out.scalar_type() == torch::kBFloat16;
+  TORCH_CHECK(!out_bf16 || srcs.size() <= size_t(p2::kMaxInputs), "weighted_sum: bf16 output supports at most ",
+              p2::kMaxInputs, " inputs");
   const c10::DeviceGuard guard(out.device());
   const int64_t n = out.numel();
-  std::vector<const float*> ptrs;
+  std::vector<const void*> ptrs;
+  std::vector<int> bf;
   std::vector<float> w;
   for (size_t i = 0; i < srcs.size(); ++i) {
-    check_f32(srcs[i], "src");
+    check_arena(srcs[i], "src");
     TORCH_CHECK(srcs[i].numel() == n, "weighted_sum: size mismatch");
     TORCH_CHECK(srcs[i].device() == out.device(), "weighted_sum: device mismatch");
-    ptrs.push_back(srcs[i].data_ptr<float>());
+    ptrs.push_back(srcs[i].data_ptr());
+    bf.push_back(srcs[i].scalar_type() == torch::kBFloat16 ? 1 : 0);
     w.push_back(float(weights[i]));
   }
-  p2::weighted_sum(ptrs.data(), w.data(), int(ptrs.size()), out.data_ptr<float>(), n, stream());
+  p2::weighted_sum(ptrs.data(), bf.data(), w.data(), int(ptrs.size()), out.data_ptr(), out_bf16 ? 1 : 0, n, stream());
 }
 
 uint16_t* opt_bf16(const c10::optional<torch::Tensor>& t, int64_t n) {
@@ -198,7 +210,7 @@ void register_rccl(pybind11::module& m);
 
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.doc() = "p2pfl_amd native HIP/CDNA4 kernels (gfx950)";
-  m.def("weighted_sum", &weighted_sum, "out = sum_i w_i * src_i (fp32 flat arenas)");
+  m.def("weighted_sum", &weighted_sum, "out = sum_i w_i * src_i (flat arenas, fp32/bf16 in, fp32/bf16 out)");
   m.def("adam_step", &adam_step, "fused whole-arena Adam/AdamW step");
   m.def("sgd_step", &sgd_step, "fused whole-arena SGD(+momentum/nesterov) step");
   m.def("adam_mt_step", &adam_mt_step, "multi-tensor Adam/AdamW over per-tensor grads into flat fp32 state",

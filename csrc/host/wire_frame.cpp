@@ -95,17 +95,8 @@ int p2fa_validate(const uint8_t* buf, size_t len, p2fa_frame* out) {
   const uint32_t version = rd32(buf + 4);
   const uint64_t hlen = rd32(buf + 8);
   const uint64_t n = len;
-  if (version == 1) {
-    if (hlen > n - kPrefixV1) return P2FA_BAD_HEADER_LEN;
-    const uint64_t start = align_up(kPrefixV1 + hlen);
-    out->version = 1;
-    out->header_off = kPrefixV1;
-    out->header_len = hlen;
-    out->payload_off = start < n ? start : n;
-    out->payload_len = n - out->payload_off;
-    out->crc = 0;
-    return P2FA_OK;
-  }
+  // v1 frames (no payload checksum) are refused: nothing emits them any more,
+  // and accepting them would let a corrupted version field skip the CRC check
   if (version != 2) return P2FA_BAD_VERSION;
   if (n < kPrefixV2) return P2FA_TOO_SHORT;
   if (hlen > n - kPrefixV2) return P2FA_BAD_HEADER_LEN;

@@ -8,8 +8,10 @@ namespace p2 {
 
 constexpr int kMaxInputs = 16;
 
-// out[i] = sum_j weights[j] * srcs[j][i]   (fp32; k may exceed kMaxInputs)
-void weighted_sum(const float* const* srcs, const float* weights, int k, float* out, int64_t n, hipStream_t s);
+// out[i] = sum_j weights[j] * srcs[j][i]; each src fp32 or bf16 (src_bf16[j]),
+// out fp32 or bf16, fp32 accumulation; k may exceed kMaxInputs (fp32 out only).
+void weighted_sum(const void* const* srcs, const int* src_bf16, const float* weights, int k, void* out, int out_bf16,
+                  int64_t n, hipStream_t s);
 
 struct AdamParams {
   float lr, beta1, beta2, eps, weight_decay;

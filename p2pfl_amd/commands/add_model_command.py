@@ -6,6 +6,7 @@ announces the new contributor set with ``models_aggregated``.
 
 from __future__ import annotations
 
+import time
 from typing import Any, Callable, List, Optional
 
 from p2pfl_amd.commands.command import Command
@@ -35,9 +36,37 @@ class AddModelCommand(Command):
             return f"late round ({round} != {self.state.round})"
         if len(self.state.train_set) == 0:
             return "no train set"
-        if not self.aggregator.would_accept(list(contributors)):
+        if not self.aggregator.would_accept(list(contributors)) and not self._probe_uncovered(list(contributors)):
             return "model not needed"
         return None
+
+    def _probe_uncovered(self, contributors: List[str]) -> bool:
+        """A waiting node is offered an aggregate that lacks train-set members it
+        still believes alive (the sender already lost them; this node has not
+        noticed yet -- e.g. no heartbeat timeout so far).  Probe those members
+        right away: an unreachable one is dropped from the neighbour table and
+        marked lost, and the offer is re-evaluated.  True if it is acceptable now.
+
+        Without this, the diffusion loop of the sender can give up (stall exit)
+        before this node's heartbeat timeout fires, and the node then waits for
+        AGGREGATION_TIMEOUT.
+        """
+        missing = self.aggregator.uncovered(contributors)
+        if not missing:
+            return False
+        proto = self.communication_protocol
+        known = proto.get_neighbors(only_direct=False)
+        gone = [m for m in missing if m not in known]
+        for m in missing:
+            if m in known:
+                # a failed send removes the neighbour; the node's neighbour
+                # listener then marks it lost in the aggregator
+                proto.send(m, proto.build_msg("beat", [str(time.time())]), create_connection=True)
+                if m not in proto.get_neighbors(only_direct=False):
+                    gone.append(m)
+        if gone:
+            self.aggregator.mark_lost(gone)
+        return self.aggregator.would_accept(contributors)
 
     def execute(
         self,
@@ -64,10 +93,13 @@ class AddModelCommand(Command):
             return
         try:
             # cheap pre-check: skip decoding models the aggregator would reject
-            if not self.aggregator.would_accept(list(contributors)):
+            if not self.aggregator.would_accept(list(contributors)) and not self._probe_uncovered(list(contributors)):
                 logger.debug(self.state.addr, f"Model from {contributors} not needed; skipped decode.")
                 return
-            models_added = self.aggregator.add_model(learner.decode_parameters(weights), list(contributors), weight)
+            params = learner.decode_parameters(weights)
+            models_added = self.aggregator.add_model(params, list(contributors), weight)
+            if not models_added and self._probe_uncovered(list(contributors)):
+                models_added = self.aggregator.add_model(params, list(contributors), weight)
             if models_added:
                 self.state.changed.bump()
                 self.communication_protocol.broadcast(

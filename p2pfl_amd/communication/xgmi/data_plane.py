@@ -389,6 +389,8 @@ class XgmiDataPlane:
         self._alloc_stream: Any = None
         # set by the transport: tell the other members to join generation g
         self.on_rebuild: Optional[Callable[[int], None]] = None
+        # generation-0 backend every rank switches to if the primary fails on any
+        self.fallback: Optional[Callable[[int, List[int]], Backend]] = None
 
     # ------------------------------------------------------------------
     # lifecycle
@@ -402,7 +404,7 @@ class XgmiDataPlane:
 
     def _init(self) -> None:
         try:
-            backend = self._make_backend(0, list(self.members))
+            backend = self._agreed_backend()
             with self._cv:
                 self._backend = backend
                 self._alloc_stream = getattr(backend, "stream", None)
@@ -415,6 +417,36 @@ class XgmiDataPlane:
             self.failed = f"data plane init failed: {e}"
             logger.error(self.name, self.failed)
             self.ready.set()
+
+    def _agreed_backend(self) -> Backend:
+        """Generation 0's backend; with a fallback, every rank switches together.
+
+        Each rank reports whether its primary backend (RCCL) came up; if any
+        rank failed, all of them build the fallback (gloo through host memory)
+        instead -- a federation that runs slower rather than one that cannot
+        move models at all.
+        """
+        members = list(self.members)
+        try:
+            backend, err = self._make_backend(0, members), None
+        except Exception as e:  # noqa: BLE001
+            backend, err = None, e
+        if self.fallback is None or self._store is None or self.world == 1:
+            if backend is None:
+                raise err  # type: ignore[misc]
+            return backend
+        keys = [f"{self._prefix}/g0/ok/{r}" for r in members]
+        self._store.set(keys[members.index(self.rank)], "1" if backend is not None else "0")
+        self._store.wait(keys, datetime.timedelta(seconds=self.group_timeout * 2))
+        if all(bytes(self._store.get(k)) == b"1" for k in keys):
+            return backend  # type: ignore[return-value]
+        logger.warning(self.name, f"xgmi data plane: primary backend failed on some rank ({err}); using the fallback")
+        if backend is not None:
+            try:
+                backend.abort()
+            except Exception:
+                pass
+        return self.fallback(0, members)
 
     def _preconnect(self) -> None:
         """Epoch 0: exchange one element with every member (opens every xGMI

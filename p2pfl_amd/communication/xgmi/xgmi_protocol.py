@@ -150,6 +150,11 @@ class XgmiJob:
                 ack_timeout=self.ack_timeout, group_timeout=self.group_timeout, rebuild_grace=self.rebuild_grace,
                 name=name, preconnect=self.backend == "rccl",
             )
+            if self.backend == "rccl":
+                # gloo staged through host memory if RCCL cannot come up on every rank
+                self.plane.fallback = make_backend_factory(
+                    "gloo", self.rank, self.store, f"{self.prefix}/plane", self.device, None, self.group_timeout
+                )
             plane = self.plane
         plane.start()
         return plane

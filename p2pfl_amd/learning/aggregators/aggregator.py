@@ -118,6 +118,17 @@ class Aggregator:
             if self._complete_locked():
                 self._done.set()
 
+    def mark_alive(self, nodes: List[str]) -> None:
+        """Train-set members back in the neighbour table (a heartbeat stall, not a
+        crash): wait for their models again -- unless the aggregation already
+        completed without them, which stays final."""
+        with self._lock:
+            back = set(nodes) & self._lost
+            if not back or self._done.is_set():
+                return
+            self._lost -= back
+            logger.info(self.node_name, f"Train-set members back: {sorted(back)}; waiting for their models again")
+
     def _complete_locked(self) -> bool:
         if self._waiting_aggregated_model:
             return bool(self._models)
@@ -128,6 +139,17 @@ class Aggregator:
         """A diffused model is final if it covers every live train-set member."""
         c = set(contributors)
         return c <= set(self._train_set) and (set(self._train_set) - self._lost) <= c
+
+    def uncovered(self, contributors: List[str]) -> List[str]:
+        """Live train-set members a full aggregate with these contributors lacks
+        (what keeps a waiting node from accepting it)."""
+        with self._lock:
+            if not self._waiting_aggregated_model or self._models:
+                return []
+            c = set(contributors)
+            if not c <= set(self._train_set):
+                return []
+            return [n for n in self._train_set if n not in c and n not in self._lost]
 
     def would_accept(self, contributors: List[str]) -> bool:
         """Pure version of :meth:`add_model`'s acceptance test."""

@@ -82,6 +82,10 @@ class TorchLearner(NodeLearner):
         self.mixed = False
         self._interrupt = threading.Event()
         self._step = 0
+        from p2pfl_amd.learning.federated_logger import FederatedLogger
+
+        # per-step metric sink (reference: the Lightning logger plugged into the Trainer)
+        self.metrics_logger = FederatedLogger(self_addr)
         # True: fit() skips the LAST epoch's validation pass and the caller runs
         # validate() itself -- the round runner overlaps it with the FedAvg
         # collective of the freshly trained weights (parallel/rounds.py)
@@ -216,6 +220,14 @@ class TorchLearner(NodeLearner):
             if not params.layout.compatible(own.layout):
                 raise ModelNotMatchingError("payload layout does not match the local model")
             return FlatParams.from_flat(params.flat, own.layout)
+        if isinstance(params, list):
+            # the reference's positional [ndarray, ...] (state_dict order); its
+            # zip() silently truncated on a count mismatch (quirk Q17): checked here
+            if len(params) != len(own) or any(
+                tuple(a.shape) != tuple(b.shape) for a, b in zip(params, own.values())
+            ):
+                raise ModelNotMatchingError("reference payload does not match the local model")
+            params = OrderedDict(zip(own.keys(), params))
         # generic dict payload: validate then re-home
         if len(params) != len(own) or any(tuple(a.shape) != tuple(b.shape) for a, b in zip(params.values(), own.values())):
             raise ModelNotMatchingError("payload tensors do not match the local model")
@@ -430,8 +442,14 @@ class TorchLearner(NodeLearner):
         return results
 
     def _log(self, key: str, value: float, step=None) -> None:
+        """Per-step metrics go through the FederatedLogger adapter (as the
+        reference's Trainer logger did, ``lightning_logger.py:54-57``); round
+        metrics (no step) straight to the global store."""
         try:
-            logger.log_metric(self._addr, key, value, step=step)
+            if step is not None:
+                self.metrics_logger.log_metrics({key: value}, step)
+            else:
+                logger.log_metric(self._addr, key, value)
         except Exception:
             pass  # learner used outside a registered node (benchmarks, unit tests)
 

@@ -16,7 +16,12 @@ interpreted: bounds of every length field and the CRC32C of the payload, so a
 truncated or corrupted model is rejected instead of being averaged into the
 federation.  That library is what the host sanitizer test fuzzes under
 ASan/UBSan (``tests/test_native_sanitizers.py``).  Without the library the
-same checks run in Python.  v1 frames (no checksum) still decode.
+same checks run in Python.  v1 frames (no checksum) are refused.
+
+Interoperability with stock reference peers: :mod:`p2pfl_amd.learning.refpickle`
+reads and writes the reference's ``pickle.dumps([ndarray, ...])`` payload with
+an allow-listed, non-executing unpickler; :func:`decode_params` recognises it
+by its pickle protocol header.
 
 Header: ``{"kind": "flat", "layout": ParamLayout}`` for arena payloads (one
 contiguous fp32 block -- one device-to-host copy to encode, one host-to-device
@@ -142,12 +147,7 @@ def _validate(mv: memoryview):
     if bytes(mv[:4]) != MAGIC:
         raise DecodingParamsError(_ERRORS[2])
     version, hlen = struct.unpack("<II", mv[4:12])
-    if version == 1:
-        if hlen > n - 12:
-            raise DecodingParamsError(_ERRORS[4])
-        start = min(-(-(12 + hlen) // _ALIGN) * _ALIGN, n)
-        return 1, bytes(mv[12 : 12 + hlen]), mv[start:]
-    if version != 2:
+    if version != 2:  # v1 (no checksum) is refused, like the native validator
         raise DecodingParamsError(_ERRORS[3])
     if n < _PREFIX:
         raise DecodingParamsError(_ERRORS[1])
@@ -195,6 +195,14 @@ def _tensor_bytes(t: torch.Tensor) -> bytes:
 
 
 def encode_params(params: Mapping[str, torch.Tensor]) -> bytes:
+    """This codec's frame; with ``Settings.WIRE_FORMAT == "reference"`` the
+    reference's pickled array list instead (for federating with stock p2pfl peers)."""
+    from p2pfl_amd.settings import Settings
+
+    if Settings.WIRE_FORMAT == "reference":
+        from p2pfl_amd.learning.refpickle import encode_reference_payload
+
+        return encode_reference_payload(params)
     if isinstance(params, FlatParams):
         return _pack({"kind": "flat", "layout": params.layout.to_json()}, _tensor_bytes(params.flat[: params.layout.numel]))
     entries, blobs, off = [], [], 0
@@ -206,7 +214,13 @@ def encode_params(params: Mapping[str, torch.Tensor]) -> bytes:
     return _pack({"kind": "dict", "tensors": entries}, b"".join(blobs))
 
 
-def decode_params(data: Union[bytes, bytearray, memoryview]) -> Union[FlatParams, "OrderedDict[str, torch.Tensor]"]:
+def decode_params(data: Union[bytes, bytearray, memoryview]) -> Union[FlatParams, "OrderedDict[str, torch.Tensor]", list]:
+    """Decode a payload: this codec's frame, or (a list of tensors) the
+    reference's pickled ``[ndarray, ...]`` read by the allow-listed decoder."""
+    from p2pfl_amd.learning import refpickle
+
+    if refpickle.looks_like_pickle(data):
+        return refpickle.decode_reference_payload(data)
     try:
         mv = memoryview(data).cast("B")
         _version, hbytes, body = _validate(mv)

@@ -111,6 +111,9 @@ class Node:
             lost = [n for n in train_set if n not in live]
             if lost:
                 self.aggregator.mark_lost(lost)
+            back = [n for n in train_set if n in live]
+            if back:
+                self.aggregator.mark_alive(back)
 
     # ------------------------------------------------------------------
     # neighbourhood

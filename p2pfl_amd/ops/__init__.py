@@ -68,26 +68,45 @@ def weighted_average_reference(flats: Sequence[torch.Tensor], weights: Sequence[
 
 
 def weighted_average(
-    flats: Sequence[torch.Tensor], weights: Sequence[float], out: Optional[torch.Tensor] = None
+    flats: Sequence[torch.Tensor],
+    weights: Sequence[float],
+    out: Optional[torch.Tensor] = None,
+    out_dtype: torch.dtype = torch.float32,
 ) -> torch.Tensor:
-    """``sum_i w_i * flats[i] / sum_i w_i`` in fp32 (one fused kernel on GPU)."""
+    """``sum_i w_i * flats[i] / sum_i w_i`` with fp32 accumulation (one fused kernel on GPU).
+
+    Inputs may be fp32 or bf16 arenas in any mix (bf16 ones come from peers on
+    the bf16 wire option) -- the kernel widens them in registers, no
+    conversion pass; the result is fp32 (default) or bf16.
+    """
     if len(flats) == 0:
         raise ValueError("no inputs")
     n = flats[0].numel()
     for f in flats:
         if f.numel() != n:
             raise ValueError("inputs differ in size")
+    if out is not None:
+        out_dtype = out.dtype
     if not _gpu(flats[0]):
         res = weighted_average_reference(flats, weights)
         if out is not None:
             out.copy_(res)
             return out
-        return res
+        return res.to(out_dtype)
     dev = flats[0].device
-    srcs = [f if (f.device == dev and f.dtype == torch.float32 and f.is_contiguous()) else f.to(dev, torch.float32).contiguous() for f in flats]
+    ok = (torch.float32, torch.bfloat16)
+    srcs = [f if (f.device == dev and f.dtype in ok and f.is_contiguous() and f.data_ptr() % 16 == 0)
+            else f.to(dev, torch.float32).contiguous() for f in flats]
+    w = normalized_weights(weights)
+    if out_dtype == torch.bfloat16 and len(srcs) > 16:
+        res = weighted_average(srcs, w)  # fp32 partial sums, then one cast
+        if out is None:
+            return res.to(torch.bfloat16)
+        out.copy_(res)
+        return out
     if out is None:
-        out = torch.empty(n, dtype=torch.float32, device=dev)
-    ext().weighted_sum(srcs, normalized_weights(weights), out)
+        out = torch.empty(n, dtype=out_dtype, device=dev)
+    ext().weighted_sum(srcs, w, out)
     return out
 
 

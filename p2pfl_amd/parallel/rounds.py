@@ -1,4 +1,7 @@
-"""Federated round runner for one-peer-per-GPU jobs.
+"""Federated round runner for one-peer-per-GPU jobs (``bench.py --aggregation allreduce``).
+
+The default benchmark path is the full Node stage machine over the xGMI
+transport; this runner is the comparison point without the protocol.
 
 One round = the reference's per-round work for an all-train network
 (``TrainStage`` -> ``GossipModelStage`` -> ``RoundFinishedStage``):
@@ -58,9 +61,7 @@ class FederatedRoundRunner:
 
     def run_round(self, evaluate: bool = True) -> RoundStats:
         t0 = time.perf_counter()
-        metrics = self.learner.evaluate_fast() if (evaluate and hasattr(self.learner, "evaluate_fast")) else (
-            self.learner.evaluate() if evaluate else {}
-        )
+        metrics = self.learner.evaluate() if evaluate else {}
         t1 = time.perf_counter()
         overlap = self.overlap_validation and hasattr(self.learner, "validate") and getattr(self.learner, "epochs", 0) > 0
         if overlap:

@@ -67,6 +67,11 @@ class Settings:
     GRPC_MAX_MESSAGE_BYTES: int = 1 << 30
     """gRPC send/receive limit (the reference kept gRPC's 4 MiB default,
     which the 26 MB MNIST CNN exceeds: reference quirk Q6)."""
+    WIRE_FORMAT: str = "p2fa"
+    """Byte encoding of weights on host transports (gRPC): ``"p2fa"`` (framed,
+    checksummed, never executes anything) or ``"reference"`` (the reference's
+    ``pickle.dumps([ndarray, ...])``, to federate with stock p2pfl peers; it is
+    always *read* with an allow-listed non-executing decoder)."""
     WIRE_DTYPE: str = "fp32"
     """Element type of model arenas on the xGMI data plane: ``"fp32"`` (the
     reference's numerics) or ``"bf16"`` (half the bytes per link; receivers

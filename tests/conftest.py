@@ -18,7 +18,7 @@ from p2pfl_amd.utils import lockcheck  # noqa: E402
 from p2pfl_amd.utils import set_test_settings  # noqa: E402
 
 set_test_settings()
-Settings.LOG_LEVEL = "INFO"
+Settings.LOG_LEVEL = os.environ.get("P2PFL_TEST_LOG_LEVEL", "INFO")
 Settings.LOG_DIR = os.environ.get("P2PFL_TEST_LOG_DIR", "/tmp/p2pfl_amd_test_logs")
 if lockcheck.is_enabled():
     # held for a whole epoch / graph capture / blocking RCCL send by design

@@ -84,13 +84,13 @@ int main(int argc, char** argv) {
     if (junk.size() >= 4 && rng() % 2) memcpy(junk.data(), "P2FA", 4);
     validate_exact(junk, junk.size(), &fr);
   }
-  // v1 frames still validate (no checksum)
+  // v1 frames (no checksum) are refused
   std::vector<uint8_t> v1(64 + 8, 0);
   memcpy(v1.data(), "P2FA", 4);
   const uint32_t one = 1, h = 3;
   memcpy(v1.data() + 4, &one, 4);
   memcpy(v1.data() + 8, &h, 4);
-  CHECK(validate_exact(v1, v1.size(), &fr) == P2FA_OK && fr.version == 1 && fr.payload_off == 64);
+  CHECK(validate_exact(v1, v1.size(), &fr) == P2FA_BAD_VERSION);
   printf("fuzz_wire: %d iterations, %d failures\n", iters, fails);
   return fails ? 1 : 0;
 }

@@ -26,6 +26,29 @@ def test_weighted_sum(k, n):
     torch.testing.assert_close(out, ref, atol=1e-5, rtol=1e-5)
 
 
+@pytest.mark.parametrize("in_dtypes", ["f32", "bf16", "mixed"])
+@pytest.mark.parametrize("out_dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("k,n", [(1, 4096 + 3), (3, 6_497_216), (8, 1 << 20), (21, 777)])
+def test_weighted_sum_dtypes(in_dtypes, out_dtype, k, n):
+    """bf16 arenas (bf16 wire option) are averaged directly: fp32 accumulation,
+    fp32 or bf16 result, against an fp64 reference of the same (bf16-valued) inputs."""
+    g = torch.Generator(device="cuda").manual_seed(k + n % 11)
+    flats = []
+    for i in range(k):
+        f = torch.randn(n, device="cuda", generator=g)
+        if in_dtypes == "bf16" or (in_dtypes == "mixed" and i % 2):
+            f = f.to(torch.bfloat16)
+        flats.append(f)
+    weights = [float(i % 4 + 1) for i in range(k)]
+    out = ops.weighted_average(flats, weights, out_dtype=out_dtype)
+    assert out.dtype == out_dtype
+    ref = ops.weighted_average_reference([f.double() for f in flats], weights)
+    if out_dtype == torch.bfloat16:
+        torch.testing.assert_close(out, ref.to(torch.bfloat16), atol=1e-2, rtol=8e-3)
+    else:
+        torch.testing.assert_close(out, ref.float(), atol=1e-5, rtol=1e-5)
+
+
 @pytest.mark.parametrize("decoupled,wd", [(False, 0.0), (False, 0.01), (True, 0.1)])
 def test_adam_step(decoupled, wd):
     n = 1 << 20

@@ -137,9 +137,12 @@ def test_wire_codec_roundtrip_and_safety():
     flat = flatten(OrderedDict(x=torch.randn(10), y=torch.randn(3, 3)))
     back = decode_params(encode_params(flat))
     assert isinstance(back, FlatParams) and torch.equal(back.flat, flat.flat) and back.layout == flat.layout
-    # a pickle payload (what the reference sends) is refused, never unpickled
+    # a pickle payload (what the reference sends) is read by the allow-listed
+    # decoder (numeric arrays only); anything executable is refused, never run
+    got = decode_params(pickle.dumps([torch.arange(3.0).numpy()]))
+    assert isinstance(got, list) and torch.equal(got[0], torch.arange(3.0))
     with pytest.raises(DecodingParamsError):
-        decode_params(pickle.dumps([torch.zeros(2).numpy()]))
+        decode_params(pickle.dumps([print]))
     with pytest.raises(DecodingParamsError):
         decode_params(encode_params(flat)[:-8])
 

@@ -212,3 +212,39 @@ def test_rank_killed_mid_transfer_survivors_finish():
     assert rec["stats"].get("rebuilds", 0) >= 1  # the stuck receive forced a new communicator
     # the survivors ended with the same model
     assert abs(rec["sums"][0] - rec["sums"][1]) < 1e-3 * max(1.0, abs(rec["sums"][0]))
+
+
+def test_primary_backend_failure_on_one_rank_switches_every_rank_to_fallback():
+    import torch.distributed as dist
+
+    from p2pfl_amd.communication.xgmi.data_plane import SimBackend
+
+    fabric, store = SimFabric(), dist.HashStore()
+
+    def primary(rank):
+        def make(gen, members):
+            if rank == 1:
+                raise RuntimeError("no RCCL here")
+            return SimBackend(SimFabric(), members, rank)  # a fabric nobody else uses
+        return make
+
+    planes = []
+    for r in range(2):
+        p = XgmiDataPlane(r, 2, primary(r), store=store, prefix="fb", preconnect=False, group_timeout=10)
+        p.fallback = make_backend_factory("sim", r, store, "fb", torch.device("cpu"), fabric)
+        planes.append(p)
+    for p in planes:
+        p.start()
+    try:
+        for p in planes:
+            assert p.ready.wait(10) and p.failed is None
+            assert p._backend.fabric is fabric  # both on the agreed fallback
+        got = threading.Event()
+        t = torch.arange(8.0)
+        hdr = planes[0].propose(1, t, lambda ok, reason, evict: None)
+        e, _ = planes[1].accept(0, hdr, lambda buf, reason: (got.set() if buf is not None and torch.equal(buf, t) else None))
+        planes[0].on_ack(hdr["seq"], e, hdr["gen"])
+        assert got.wait(10)
+    finally:
+        for p in planes:
+            p.stop()
