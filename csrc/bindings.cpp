@@ -207,6 +207,7 @@ void register_cnn(pybind11::module& m);
 void register_fused(pybind11::module& m);
 void register_bn(pybind11::module& m);
 void register_rccl(pybind11::module& m);
+void register_gemm(pybind11::module& m);
 
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.doc() = "p2pfl_amd native HIP/CDNA4 kernels (gfx950)";
@@ -228,4 +229,5 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   register_fused(m);
   register_bn(m);
   register_rccl(m);
+  register_gemm(m);
 }

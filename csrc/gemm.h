@@ -1,0 +1,35 @@
+// Host launch API of the hand-written MFMA GEMM (csrc/gemm.hip).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace p2 {
+
+// C[M][N] = sum_k A(m, k) * B(n, k) over bf16 operands, fp32 accumulation.
+//   A(m, k) = a[m * lda + k] when a_kmajor, else a[k * lda + m]
+//   B(n, k) = b[n * ldb + k] when b_kmajor, else b[k * ldb + n]
+// (nn.Linear forward: A = x [M][K], B = W [N][K], both k-major; dgrad:
+//  B = W read n-major; wgrad: both operands m/n-major.)
+// Epilogue, in order: + bias[n] (fp32 or bf16), GELU (writes the
+// pre-activation to `z` if given), + residual[m][n] (bf16); C is bf16 or
+// fp32.  With splits > 1 every K-slice writes its raw fp32 partial to
+// c + slice * M * N instead (no epilogue; reduce afterwards).
+struct GemmParams {
+  const uint16_t* a;
+  const uint16_t* b;
+  void* c;
+  int64_t lda, ldb, ldc;
+  int M, N, K;
+  int a_kmajor, b_kmajor;
+  int c_bf16;
+  const void* bias;
+  int bias_bf16;
+  int gelu;
+  uint16_t* z;  // GELU pre-activation output (bf16, ldc), optional
+  const uint16_t* residual;  // bf16 [M][ldc], optional
+  int splits;
+};
+
+void gemm_bf16(const GemmParams& p, hipStream_t s);
+
+}  // namespace p2

@@ -1,0 +1,92 @@
+// PyTorch bindings of the hand-written MFMA GEMM (p2pfl_amd._C.gemm).
+// Shapes, strides, dtypes and alignment are validated on the host before the
+// launch: a mismatched call is a Python exception, never a GPU fault.
+#include <torch/extension.h>
+#include <c10/core/DeviceGuard.h>
+#include <c10/hip/HIPStream.h>
+
+#include "gemm.h"
+
+namespace {
+
+void check_bf16_2d(const torch::Tensor& t, const char* name) {
+  TORCH_CHECK(t.is_cuda() && t.scalar_type() == torch::kBFloat16, name, " must be a bf16 GPU tensor");
+  TORCH_CHECK(t.dim() == 2 && t.stride(1) == 1, name, " must be 2-D with unit column stride");
+  TORCH_CHECK(t.stride(0) % 8 == 0 && reinterpret_cast<uintptr_t>(t.data_ptr()) % 16 == 0, name,
+              " rows must be 16-byte aligned");
+}
+
+// a: [M, K] (a_kmajor) or [K, M];  b: [N, K] (b_kmajor) or [K, N];  out: [M, N] bf16/fp32,
+// or [splits, M, N] fp32 when splits > 1.
+void gemm(torch::Tensor a, torch::Tensor b, bool a_kmajor, bool b_kmajor, torch::Tensor out,
+          c10::optional<torch::Tensor> bias, bool gelu, c10::optional<torch::Tensor> z,
+          c10::optional<torch::Tensor> residual, int64_t splits) {
+  check_bf16_2d(a, "a");
+  check_bf16_2d(b, "b");
+  const int64_t M = a_kmajor ? a.size(0) : a.size(1), K = a_kmajor ? a.size(1) : a.size(0);
+  const int64_t N = b_kmajor ? b.size(0) : b.size(1), Kb = b_kmajor ? b.size(1) : b.size(0);
+  TORCH_CHECK(K == Kb, "gemm: reduction sizes differ (", K, " vs ", Kb, ")");
+  TORCH_CHECK(M >= 1 && N >= 8 && K >= 8, "gemm: degenerate shape");
+  TORCH_CHECK(K % 8 == 0 && N % 8 == 0, "gemm: K and N must be multiples of 8");
+  TORCH_CHECK(a_kmajor || M % 8 == 0, "gemm: an m-major A needs M % 8 == 0");
+  TORCH_CHECK(M < (int64_t(1) << 31) && N < (int64_t(1) << 31) && K < (int64_t(1) << 31), "gemm: size overflow");
+  TORCH_CHECK(a.device() == b.device() && out.device() == a.device(), "gemm: device mismatch");
+  TORCH_CHECK(splits >= 1 && splits <= 64, "gemm: 1 <= splits <= 64");
+  p2::GemmParams p{};
+  p.a = reinterpret_cast<const uint16_t*>(a.data_ptr());
+  p.b = reinterpret_cast<const uint16_t*>(b.data_ptr());
+  p.lda = a.stride(0);
+  p.ldb = b.stride(0);
+  p.M = int(M);
+  p.N = int(N);
+  p.K = int(K);
+  p.a_kmajor = a_kmajor;
+  p.b_kmajor = b_kmajor;
+  p.splits = int(splits);
+  if (splits > 1) {
+    TORCH_CHECK(out.scalar_type() == torch::kFloat32 && out.is_contiguous() && out.numel() == splits * M * N,
+                "gemm: split-K output must be a contiguous fp32 [splits, M, N] tensor");
+    TORCH_CHECK(!bias.has_value() && !gelu && !residual.has_value(), "gemm: no epilogue with split-K");
+    p.ldc = N;
+  } else {
+    TORCH_CHECK(out.dim() == 2 && out.size(0) == M && out.size(1) == N && out.stride(1) == 1, "gemm: out must be [M, N]");
+    TORCH_CHECK(out.scalar_type() == torch::kBFloat16 || out.scalar_type() == torch::kFloat32, "gemm: out bf16 or fp32");
+    TORCH_CHECK(out.stride(0) % 4 == 0 && reinterpret_cast<uintptr_t>(out.data_ptr()) % 16 == 0, "gemm: out alignment");
+    p.ldc = out.stride(0);
+  }
+  p.c = out.data_ptr();
+  p.c_bf16 = out.scalar_type() == torch::kBFloat16;
+  if (bias.has_value() && bias->defined()) {
+    TORCH_CHECK(bias->is_cuda() && bias->is_contiguous() && bias->numel() == N &&
+                    (bias->scalar_type() == torch::kFloat32 || bias->scalar_type() == torch::kBFloat16),
+                "gemm: bias must be a contiguous fp32/bf16 [N] tensor");
+    p.bias = bias->data_ptr();
+    p.bias_bf16 = bias->scalar_type() == torch::kBFloat16;
+  }
+  p.gelu = gelu;
+  if (z.has_value() && z->defined()) {
+    TORCH_CHECK(gelu, "gemm: z (pre-activation) only with gelu");
+    TORCH_CHECK(z->scalar_type() == torch::kBFloat16 && z->dim() == 2 && z->size(0) == M && z->size(1) == N &&
+                    z->stride(0) == p.ldc && z->stride(1) == 1,
+                "gemm: z must be bf16 [M, N] with out's row stride");
+    p.z = reinterpret_cast<uint16_t*>(z->data_ptr());
+  }
+  if (residual.has_value() && residual->defined()) {
+    TORCH_CHECK(residual->scalar_type() == torch::kBFloat16 && residual->dim() == 2 && residual->size(0) == M &&
+                    residual->size(1) == N && residual->stride(0) == p.ldc && residual->stride(1) == 1,
+                "gemm: residual must be bf16 [M, N] with out's row stride");
+    p.residual = reinterpret_cast<const uint16_t*>(residual->data_ptr());
+  }
+  const c10::DeviceGuard guard(a.device());
+  p2::gemm_bf16(p, c10::hip::getCurrentHIPStream().stream());
+}
+
+}  // namespace
+
+void register_gemm(pybind11::module& m) {
+  m.def("gemm", &gemm, "bf16 MFMA GEMM with fused bias/GELU/residual epilogue and split-K",
+        pybind11::arg("a"), pybind11::arg("b"), pybind11::arg("a_kmajor"), pybind11::arg("b_kmajor"),
+        pybind11::arg("out"), pybind11::arg("bias") = pybind11::none(), pybind11::arg("gelu") = false,
+        pybind11::arg("z") = pybind11::none(), pybind11::arg("residual") = pybind11::none(),
+        pybind11::arg("splits") = 1);
+}

@@ -26,6 +26,14 @@ class MLP(FLModule):
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
         x = x.reshape(x.shape[0], -1)
+        if x.is_cuda:
+            from p2pfl_amd import ops
+
+            if ops.available():
+                # 784->256 and 256->128 on the hand-written MFMA GEMM (bias in its epilogue)
+                x = torch.relu(ops.linear(x, self.l1.weight, self.l1.bias))
+                x = torch.relu(ops.linear(x, self.l2.weight, self.l2.bias))
+                return torch.log_softmax(self.l3(x), dim=1)
         x = torch.relu(self.l1(x))
         x = torch.relu(self.l2(x))
         return torch.log_softmax(self.l3(x), dim=1)

@@ -48,7 +48,7 @@ class Mlp(nn.Module):
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
         if _fused(x):
-            h = ops.bias_gelu(ops.linear(x, self.fc1.weight), self.fc1.bias)
+            h = ops.linear_gelu(x, self.fc1.weight, self.fc1.bias)  # bias + GELU in the GEMM epilogue
             return ops.linear(h, self.fc2.weight, self.fc2.bias)
         return self.fc2(nn.functional.gelu(self.fc1(x)))
 

@@ -219,7 +219,8 @@ from p2pfl_amd.ops.fused import (  # noqa: E402
     bias_gelu_reference,
     layer_norm,
     layer_norm_reference,
-    linear,
     softmax_xent,
     softmax_xent_reference,
 )
+from p2pfl_amd.ops.fused import linear as linear_blas  # noqa: E402,F401  (hipBLASLt comparison path)
+from p2pfl_amd.ops.gemm import gemm, gemm_reference, linear, linear_gelu  # noqa: E402,F401

@@ -1,0 +1,198 @@
+"""Linear layers on the hand-written MFMA GEMM (``csrc/gemm.hip``).
+
+:func:`gemm` exposes the kernel: ``C = A . B^T`` over bf16 operands with fp32
+accumulation, each operand given in its natural memory layout (k-major or
+m/n-major, so nothing is transposed in memory), an epilogue with bias, GELU
+(+ pre-activation) and residual add, and split-K into fp32 slabs reduced by
+the FedAvg weighted-sum kernel (fp32 accumulation, bf16 out).
+
+:func:`linear` / :func:`linear_gelu` are ``nn.Linear`` (and ``gelu(nn.Linear)``)
+with all three products -- forward, input gradient, weight gradient -- on
+that kernel; the bias gradient is the column-sum kernel.  Reference shapes:
+``/root/reference/p2pfl/learning/pytorch/mnist_examples/models/mlp.py:53-69``
+and the ViT-B/16 of BASELINE config 4.
+"""
+
+from __future__ import annotations
+
+from typing import Optional, Tuple
+
+import torch
+import torch.nn.functional as F
+
+
+def _C():
+    from p2pfl_amd.ops import ext
+
+    return ext()
+
+
+def gemm_reference(a, b, a_kmajor=True, b_kmajor=True, bias=None, gelu=False, residual=None):
+    A = a.float() if a_kmajor else a.float().t()
+    B = b.float() if b_kmajor else b.float().t()
+    c = A @ B.t()
+    if bias is not None:
+        c = c + bias.float()
+    z = c
+    if gelu:
+        c = F.gelu(c)
+    if residual is not None:
+        c = c + residual.float()
+    return c, z
+
+
+def splits_for(M: int, N: int, K: int) -> int:
+    """Split-K factor so that a small M x N grid still covers the 256 CUs."""
+    tiles = -(-M // 128) * -(-N // 128)
+    s = 1
+    while tiles * s < 256 and K // (s * 2) >= 512 and s < 16:
+        s *= 2
+    return s
+
+
+def gemm(
+    a: torch.Tensor,
+    b: torch.Tensor,
+    a_kmajor: bool = True,
+    b_kmajor: bool = True,
+    out_dtype: torch.dtype = torch.bfloat16,
+    bias: Optional[torch.Tensor] = None,
+    gelu: bool = False,
+    want_z: bool = False,
+    residual: Optional[torch.Tensor] = None,
+    splits: int = 1,
+    out: Optional[torch.Tensor] = None,
+) -> Tuple[torch.Tensor, Optional[torch.Tensor]]:
+    """``(C, z)`` with ``C[m, n] = sum_k A(m, k) B(n, k)`` (+ epilogue).
+
+    ``a`` is [M, K] if ``a_kmajor`` else [K, M]; ``b`` is [N, K] if
+    ``b_kmajor`` else [K, N].  ``z`` is the GELU pre-activation (``want_z``).
+    With ``splits > 1`` the K-slices' fp32 partials are summed into ``C``.
+    """
+    M = a.shape[0] if a_kmajor else a.shape[1]
+    N = b.shape[0] if b_kmajor else b.shape[1]
+    dev = a.device
+    if splits > 1:
+        if bias is not None or gelu or residual is not None:
+            raise ValueError("split-K GEMM has no epilogue")
+        slabs = torch.empty((splits, M, N), dtype=torch.float32, device=dev)
+        _C().gemm(a, b, a_kmajor, b_kmajor, slabs, None, False, None, None, splits)
+        out = torch.empty((M, N), dtype=out_dtype, device=dev) if out is None else out
+        _sum_slabs(slabs, out)
+        return out, None
+    if out is None:
+        out = torch.empty((M, N), dtype=out_dtype, device=dev)
+    z = torch.empty((M, N), dtype=torch.bfloat16, device=dev) if (gelu and want_z) else None
+    _C().gemm(a, b, a_kmajor, b_kmajor, out, bias, gelu, z, residual, 1)
+    return out, z
+
+
+def _sum_slabs(slabs: torch.Tensor, out: torch.Tensor) -> None:
+    """out = sum over dim 0 of the fp32 split-K slabs: one pass of the weighted-sum
+    kernel (unit weights, fp32 accumulation, bf16/fp32 out)."""
+    s = slabs.shape[0]
+    _C().weighted_sum(list(slabs.view(s, -1)), [1.0] * s, out.view(-1))
+
+
+def _wgrad(dy2: torch.Tensor, x2: torch.Tensor, dtype: torch.dtype) -> torch.Tensor:
+    """dW[n, k] = sum_m dy[m, n] x[m, k]: both operands m-major, split over m."""
+    M, N = dy2.shape
+    K = x2.shape[1]
+    s = splits_for(N, K, M)
+    if s == 1:
+        return gemm(dy2, x2, a_kmajor=False, b_kmajor=False, out_dtype=dtype)[0]
+    return gemm(dy2, x2, a_kmajor=False, b_kmajor=False, out_dtype=dtype, splits=s)[0]
+
+
+def _bias_grad(dy2: torch.Tensor, dtype: torch.dtype) -> torch.Tensor:
+    from p2pfl_amd.ops.fused import _fx
+
+    return _fx().column_sum(dy2, dtype == torch.bfloat16).to(dtype)
+
+
+def _rows(x: torch.Tensor) -> torch.Tensor:
+    x2 = x.reshape(-1, x.shape[-1])
+    if x2.stride(-1) != 1 or x2.stride(0) % 8 or x2.data_ptr() % 16:
+        x2 = x2.contiguous()
+    return x2
+
+
+class _LinearMFMA(torch.autograd.Function):
+    @staticmethod
+    @torch.amp.custom_fwd(device_type="cuda", cast_inputs=torch.bfloat16)
+    def forward(ctx, x, w, b):
+        x2 = _rows(x.to(torch.bfloat16))
+        wc = w.to(torch.bfloat16).contiguous()
+        y, _ = gemm(x2, wc, bias=b)
+        ctx.save_for_backward(x2, wc)
+        ctx.w_dtype = w.dtype
+        ctx.b_dtype = b.dtype if b is not None else None
+        ctx.xshape = x.shape
+        return y.view(*x.shape[:-1], w.shape[0])
+
+    @staticmethod
+    @torch.amp.custom_bwd(device_type="cuda")
+    def backward(ctx, dy):
+        x2, w = ctx.saved_tensors
+        dy2 = _rows(dy.to(torch.bfloat16))
+        dx = dw = db = None
+        if ctx.needs_input_grad[0]:
+            dx = gemm(dy2, w, a_kmajor=True, b_kmajor=False)[0].view(ctx.xshape)
+        if ctx.needs_input_grad[1]:
+            dw = _wgrad(dy2, x2, ctx.w_dtype)
+        if ctx.b_dtype is not None and ctx.needs_input_grad[2]:
+            db = _bias_grad(dy2, ctx.b_dtype)
+        return dx, dw, db
+
+
+class _LinearGeluMFMA(torch.autograd.Function):
+    """h = gelu(x W^T + b): bias and GELU in the GEMM epilogue, which also keeps
+    the pre-activation for the backward pass (no separate bias-GELU pass)."""
+
+    @staticmethod
+    @torch.amp.custom_fwd(device_type="cuda", cast_inputs=torch.bfloat16)
+    def forward(ctx, x, w, b):
+        x2 = _rows(x.to(torch.bfloat16))
+        wc = w.to(torch.bfloat16).contiguous()
+        h, z = gemm(x2, wc, bias=b, gelu=True, want_z=True)
+        ctx.save_for_backward(x2, wc, z)
+        ctx.w_dtype = w.dtype
+        ctx.b_dtype = b.dtype
+        ctx.xshape = x.shape
+        return h.view(*x.shape[:-1], w.shape[0])
+
+    @staticmethod
+    @torch.amp.custom_bwd(device_type="cuda")
+    def backward(ctx, dh):
+        from p2pfl_amd.ops.fused import _fx
+
+        x2, w, z = ctx.saved_tensors
+        dh2 = _rows(dh.to(torch.bfloat16))
+        zero = torch.zeros(z.shape[1], dtype=torch.float32, device=z.device)
+        dz, db = _fx().bias_gelu_bwd(dh2, z, zero)  # dz = dh * gelu'(z), db = column sums of dz
+        dx = dw = None
+        if ctx.needs_input_grad[0]:
+            dx = gemm(dz, w, a_kmajor=True, b_kmajor=False)[0].view(ctx.xshape)
+        if ctx.needs_input_grad[1]:
+            dw = _wgrad(dz, x2, ctx.w_dtype)
+        return dx, dw, db.to(ctx.b_dtype) if ctx.needs_input_grad[2] else None
+
+
+def _ok(x: torch.Tensor, w: torch.Tensor) -> bool:
+    from p2pfl_amd.ops import _gpu
+
+    return _gpu(x) and x.dtype in (torch.bfloat16, torch.float32) and w.shape[0] % 8 == 0 and w.shape[1] % 8 == 0
+
+
+def linear(x: torch.Tensor, weight: torch.Tensor, bias: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """``F.linear`` with forward, input gradient and weight gradient on the MFMA GEMM."""
+    if _ok(x, weight):
+        return _LinearMFMA.apply(x, weight, bias)
+    return F.linear(x, weight, bias)
+
+
+def linear_gelu(x: torch.Tensor, weight: torch.Tensor, bias: torch.Tensor) -> torch.Tensor:
+    """``gelu(F.linear(x, weight, bias))`` (exact erf GELU), fused epilogue."""
+    if _ok(x, weight):
+        return _LinearGeluMFMA.apply(x, weight, bias)
+    return F.gelu(F.linear(x, weight, bias))

@@ -1,0 +1,102 @@
+"""Hand-written MFMA GEMM (csrc/gemm.hip) vs an fp32 PyTorch reference on the same bf16 operands."""
+
+from __future__ import annotations
+
+import pytest
+import torch
+import torch.nn.functional as F
+
+from p2pfl_amd import ops
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(autouse=True)
+def _require_ext():
+    ops.ext()
+
+
+def _operands(M, N, K, a_kmajor, b_kmajor, seed=0):
+    g = torch.Generator(device="cuda").manual_seed(seed)
+    A = torch.randn(M, K, device="cuda", generator=g).to(torch.bfloat16)
+    B = torch.randn(N, K, device="cuda", generator=g).to(torch.bfloat16)
+    a = A if a_kmajor else A.t().contiguous()
+    b = B if b_kmajor else B.t().contiguous()
+    return a, b
+
+
+@pytest.mark.parametrize("a_kmajor,b_kmajor", [(True, True), (True, False), (False, True), (False, False)])
+@pytest.mark.parametrize("M,N,K", [(128, 128, 64), (256, 384, 192), (200, 136, 200), (6304 // 8, 768, 768), (72, 1000, 96)])
+def test_gemm_layouts_vs_fp32(a_kmajor, b_kmajor, M, N, K):
+    """Every operand layout; ragged M (row clamping), N (masked stores) and K (zeroed tail)."""
+    if not a_kmajor and M % 8:
+        pytest.skip("m-major A needs M % 8 == 0")
+    a, b = _operands(M, N, K, a_kmajor, b_kmajor, seed=M + N + K)
+    out, _ = ops.gemm(a, b, a_kmajor, b_kmajor, out_dtype=torch.float32)
+    ref, _ = ops.gemm_reference(a, b, a_kmajor, b_kmajor)
+    torch.testing.assert_close(out, ref, atol=2e-3, rtol=1e-4)
+
+
+def test_gemm_asymmetric_exact_integers():
+    """Small integer operands: exact in bf16 and fp32, so any mis-mapped lane/row shows as an exact mismatch."""
+    M, N, K = 160, 96, 128
+    A = torch.randint(-3, 4, (M, K), device="cuda").to(torch.bfloat16)
+    B = (torch.arange(N * K, device="cuda").view(N, K) % 7 - 3).to(torch.bfloat16)  # asymmetric
+    for ak, bk in [(True, True), (True, False), (False, True), (False, False)]:
+        a = A if ak else A.t().contiguous()
+        b = B if bk else B.t().contiguous()
+        out, _ = ops.gemm(a, b, ak, bk, out_dtype=torch.float32)
+        assert torch.equal(out, A.float() @ B.float().t()), (ak, bk)
+
+
+@pytest.mark.parametrize("splits", [2, 4, 8])
+def test_gemm_split_k(splits):
+    M, N, K = 256, 320, 6304  # the weight-gradient shape class: reduction over token rows, ragged K
+    a, b = _operands(M, N, K, False, False, seed=splits)
+    out, _ = ops.gemm(a, b, False, False, out_dtype=torch.float32, splits=splits)
+    ref, _ = ops.gemm_reference(a, b, False, False)
+    torch.testing.assert_close(out, ref, atol=5e-3, rtol=1e-4)
+
+
+@pytest.mark.parametrize("bias_dtype", [torch.float32, torch.bfloat16])
+def test_gemm_epilogue_bias_gelu_residual(bias_dtype):
+    M, N, K = 300, 256, 128
+    a, b = _operands(M, N, K, True, True, seed=3)
+    bias = torch.randn(N, device="cuda").to(bias_dtype)
+    res = torch.randn(M, N, device="cuda").to(torch.bfloat16)
+    out, z = ops.gemm(a, b, bias=bias, gelu=True, want_z=True, residual=res, out_dtype=torch.float32)
+    ref, zref = ops.gemm_reference(a, b, bias=bias, gelu=True, residual=res)
+    torch.testing.assert_close(out, ref, atol=2e-3, rtol=1e-4)
+    torch.testing.assert_close(z.float(), zref, atol=3e-2, rtol=8e-3)  # z is stored in bf16
+
+
+@pytest.mark.parametrize("gelu", [False, True])
+def test_linear_autograd_vs_fp32(gelu):
+    torch.manual_seed(0)
+    x = torch.randn(4, 197, 768, device="cuda").to(torch.bfloat16).requires_grad_()
+    w = (torch.randn(512, 768, device="cuda") * 0.03).to(torch.bfloat16).requires_grad_()
+    bias = torch.randn(512, device="cuda").requires_grad_()
+    y = ops.linear_gelu(x, w, bias) if gelu else ops.linear(x, w, bias)
+    g = torch.randn_like(y)
+    y.backward(g)
+    xr, wr, br = (t.detach().float().requires_grad_() for t in (x, w, bias))
+    yr = F.linear(xr, wr, br)
+    if gelu:
+        yr = F.gelu(yr)
+    yr.backward(g.float())
+    torch.testing.assert_close(y.float(), yr, atol=3e-2, rtol=2e-2)
+    torch.testing.assert_close(x.grad.float(), xr.grad, atol=3e-2, rtol=2e-2)
+    torch.testing.assert_close(w.grad.float(), wr.grad, atol=1e-1, rtol=2e-2)
+    torch.testing.assert_close(bias.grad, br.grad, atol=1e-1, rtol=2e-2)
+
+
+def test_vit_block_mlp_uses_native_gemm():
+    from p2pfl_amd.models.vit import Mlp
+
+    torch.manual_seed(0)
+    m = Mlp(768, 3072).cuda()
+    x = torch.randn(2, 197, 768, device="cuda")
+    with torch.autocast("cuda", dtype=torch.bfloat16):
+        y = m(x)
+    ref = m.fc2(F.gelu(m.fc1(x)))
+    torch.testing.assert_close(y.float(), ref, atol=5e-2, rtol=5e-2)
