@@ -20,14 +20,16 @@ void check_bf16_2d(const torch::Tensor& t, const char* name) {
 // or [splits, M, N] fp32 when splits > 1.
 void gemm(torch::Tensor a, torch::Tensor b, bool a_kmajor, bool b_kmajor, torch::Tensor out,
           c10::optional<torch::Tensor> bias, bool gelu, c10::optional<torch::Tensor> z,
-          c10::optional<torch::Tensor> residual, int64_t splits) {
+          c10::optional<torch::Tensor> residual, int64_t splits, int64_t variant) {
   check_bf16_2d(a, "a");
   check_bf16_2d(b, "b");
   const int64_t M = a_kmajor ? a.size(0) : a.size(1), K = a_kmajor ? a.size(1) : a.size(0);
   const int64_t N = b_kmajor ? b.size(0) : b.size(1), Kb = b_kmajor ? b.size(1) : b.size(0);
   TORCH_CHECK(K == Kb, "gemm: reduction sizes differ (", K, " vs ", Kb, ")");
   TORCH_CHECK(M >= 1 && N >= 8 && K >= 8, "gemm: degenerate shape");
-  TORCH_CHECK(K % 8 == 0 && N % 8 == 0, "gemm: K and N must be multiples of 8");
+  TORCH_CHECK(N % 8 == 0, "gemm: N must be a multiple of 8 (M=", M, " N=", N, " K=", K, ")");
+  TORCH_CHECK((!a_kmajor && !b_kmajor) || K % 8 == 0, "gemm: a k-major operand needs K % 8 == 0 (M=", M, " N=", N,
+              " K=", K, ")");
   TORCH_CHECK(a_kmajor || M % 8 == 0, "gemm: an m-major A needs M % 8 == 0");
   TORCH_CHECK(M < (int64_t(1) << 31) && N < (int64_t(1) << 31) && K < (int64_t(1) << 31), "gemm: size overflow");
   TORCH_CHECK(a.device() == b.device() && out.device() == a.device(), "gemm: device mismatch");
@@ -43,6 +45,7 @@ void gemm(torch::Tensor a, torch::Tensor b, bool a_kmajor, bool b_kmajor, torch:
   p.a_kmajor = a_kmajor;
   p.b_kmajor = b_kmajor;
   p.splits = int(splits);
+  p.variant = int(variant);
   if (splits > 1) {
     TORCH_CHECK(out.scalar_type() == torch::kFloat32 && out.is_contiguous() && out.numel() == splits * M * N,
                 "gemm: split-K output must be a contiguous fp32 [splits, M, N] tensor");
@@ -88,5 +91,5 @@ void register_gemm(pybind11::module& m) {
         pybind11::arg("a"), pybind11::arg("b"), pybind11::arg("a_kmajor"), pybind11::arg("b_kmajor"),
         pybind11::arg("out"), pybind11::arg("bias") = pybind11::none(), pybind11::arg("gelu") = false,
         pybind11::arg("z") = pybind11::none(), pybind11::arg("residual") = pybind11::none(),
-        pybind11::arg("splits") = 1);
+        pybind11::arg("splits") = 1, pybind11::arg("variant") = 0);
 }

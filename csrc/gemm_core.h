@@ -1,0 +1,234 @@
+// MFMA GEMM core shared by the Linear GEMM (gemm.hip) and the implicit-GEMM
+// convolutions (conv.hip): C[M][N] = sum_k A(m, k) B(n, k), bf16 operands,
+// fp32 accumulation, gfx950 v_mfma_f32_32x32x16_bf16.
+//
+// The operands come through LOADER policies: a loader maps one 16-byte chunk
+// of an operand tile to a global address, so the same pipeline serves plain
+// matrices and the gathers of an implicit-GEMM convolution (im2col rows,
+// transposed-convolution taps).  A k-major loader returns 8 consecutive k of
+// one row (m or n); an mn-major loader 8 consecutive m / n of one k.  Any
+// element outside the operand (rows past M / N, k past K, zero padding of a
+// convolution) points at a 16-byte zero page, so tails need no masking.
+//
+// Pipeline (see gemm.hip for the full rationale): 128 x 128 tile per 256-thread
+// workgroup, 4 waves as 2 x 2 (64 x 64 each, 2 x 2 MFMA tiles), BK = 64,
+// global_load_lds into a double buffer (next tile's DMA issued before the
+// current tile's MFMAs, one vmcnt(0) + barrier per K-tile), XOR-swizzled LDS
+// images (ds_read_b128 for k-major, ds_read_b64_tr_b16 transpose reads for
+// mn-major), XCD-aware tile order, split-K into fp32 slabs.
+#pragma once
+#include "common.h"
+#include "gemm.h"
+
+namespace p2gemm {
+using namespace p2;
+
+typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
+typedef short s16x4 __attribute__((ext_vector_type(4)));
+
+constexpr int BM = 128, BN = 128, BK = 64, NT = 256;
+constexpr int TILE = BM * BK * 2;  // bytes per operand tile (16 KB)
+
+// 16 zero bytes every out-of-operand chunk is loaded from
+extern __device__ __attribute__((aligned(16))) uint16_t g_zero16[8];
+
+P2_DEVICE f32x16 mfma(uint4 a, uint4 b, f32x16 c) {
+  return __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8_t, a), __builtin_bit_cast(bf16x8_t, b), c,
+                                                  0, 0, 0);
+}
+
+P2_DEVICE int swz_k(int row) { return (row >> 1) & 7; }                       // k-major: 8 chunks / 128-B row
+P2_DEVICE int swz_mn(int row) { return ((row & 3) << 2) | ((row >> 2) & 3); }  // mn-major: 16 chunks / 256-B row
+
+// ---- plain matrix loaders ------------------------------------------------------
+struct PlainK {  // element (r, k) at g[r * ld + k]
+  static constexpr bool KMAJ = true;
+  const uint16_t* g;
+  int64_t ld;
+  int nrows, K;
+  P2_DEVICE const void* src(int r, int k) const {
+    return (r < nrows && k < K) ? static_cast<const void*>(g + r * ld + k) : static_cast<const void*>(g_zero16);
+  }
+};
+struct PlainMN {  // element (r, k) at g[k * ld + r]
+  static constexpr bool KMAJ = false;
+  const uint16_t* g;
+  int64_t ld;
+  int nrows, K;
+  P2_DEVICE const void* src(int k, int r) const {
+    return (r < nrows && k < K) ? static_cast<const void*>(g + k * ld + r) : static_cast<const void*>(g_zero16);
+  }
+};
+
+// Issue the DMA of one operand tile (rows r0.. of the M or N dimension,
+// reduction indices k0..k0+63) into `lds`; every lane moves 16 B four times.
+template <class L>
+P2_DEVICE void stage(const L& ld, int r0, int k0, char* lds, int tid) {
+  const int wave = tid >> 6;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int cid = i * NT + tid;
+    char* dst = lds + (i * NT + wave * 64) * 16;  // wave-uniform; lane L writes dst + 16 L
+    const void* src;
+    if constexpr (L::KMAJ) {
+      const int row = cid >> 3, c = (cid & 7) ^ swz_k(row);
+      src = ld.src(r0 + row, k0 + 8 * c);
+    } else {
+      const int row = cid >> 4, ch = (cid & 15) ^ swz_mn(row);
+      src = ld.src(k0 + row, r0 + 8 * ch);
+    }
+    __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
+                                     (__attribute__((address_space(3))) void*)dst, 16, 0, 0);
+  }
+}
+
+// Fragment of a 32-row block (rows rb..rb+31 of the tile) for k-substep ks:
+// lane l holds element (rb + (l & 31), 16 ks + 8 (l >> 5) + j), j = 0..7.
+template <bool KMAJ>
+P2_DEVICE uint4 frag(const char* lds, int rb, int ks, int lane) {
+  if constexpr (KMAJ) {
+    const int row = rb + (lane & 31), c = 2 * ks + (lane >> 5);
+    return *reinterpret_cast<const uint4*>(lds + row * 128 + ((c ^ swz_k(row)) << 4));
+  } else {
+    const int g = lane >> 4, i = lane & 15, q = i >> 2, p = i & 3;
+    const int col = rb + 16 * (g & 1) + 4 * p;  // this lane supplies 4 columns of row q
+    const int ch = col >> 3, sub = (col & 7) * 2;
+    uint4 out;
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+      const int row = 16 * ks + 8 * (g >> 1) + 4 * t + q;
+      const char* addr = lds + row * 256 + ((ch ^ swz_mn(row)) << 4) + sub;
+      const s16x4 v = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4*)(addr));
+      const uint2 u = __builtin_bit_cast(uint2, v);
+      if (t == 0) {
+        out.x = u.x;
+        out.y = u.y;
+      } else {
+        out.z = u.x;
+        out.w = u.y;
+      }
+    }
+    return out;
+  }
+}
+
+P2_DEVICE float gelu_f(float z) { return 0.5f * z * (1.f + erff(z * 0.70710678118654752f)); }
+
+// XCD-aware bijective remap of a linear workgroup id (blocks sharing an XCD get consecutive ids).
+P2_DEVICE int xcd_remap(int orig, int nwg) {
+  const int xcd = orig % 8, q = nwg / 8, r = nwg % 8;
+  return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + orig / 8;
+}
+
+// The whole kernel body.  `p` carries M/N/K, split-K and the epilogue.
+template <class LA, class LB>
+P2_DEVICE void gemm_body(const GemmParams& p, const LA& la, const LB& lb, int tiles_m, int tiles_n, char* smem) {
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave >> 1, wn = wave & 1;
+  const int bid = (p.variant & 4) ? int(blockIdx.x) : xcd_remap(blockIdx.x, gridDim.x);
+  const int tiles = tiles_m * tiles_n;
+  const int split = bid / tiles, t = bid % tiles;
+  // consecutive tiles share the B panel (variant bit 1: the A panel)
+  const int tm = (p.variant & 2) ? t / tiles_n : t % tiles_m, tn = (p.variant & 2) ? t % tiles_n : t / tiles_m;
+  const int m0 = tm * BM, n0 = tn * BN;
+  int kper = (p.K + p.splits - 1) / p.splits;
+  kper = (kper + BK - 1) / BK * BK;
+  const int kb = split * kper, ke = min(p.K, kb + kper);
+  const int nt = ke > kb ? (ke - kb + BK - 1) / BK : 0;
+
+  f32x16 acc[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.f;
+
+  if (nt > 0) {
+    stage(la, m0, kb, smem, tid);
+    stage(lb, n0, kb, smem + TILE, tid);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+  }
+  for (int it = 0; it < nt; ++it) {
+    const int cur = it & 1;
+    const char* sa = smem + cur * 2 * TILE;
+    const char* sb = sa + TILE;
+    if (it + 1 < nt) {
+      char* na = smem + (cur ^ 1) * 2 * TILE;
+      stage(la, m0, kb + (it + 1) * BK, na, tid);
+      stage(lb, n0, kb + (it + 1) * BK, na + TILE, tid);
+    }
+#pragma unroll
+    for (int ks = 0; ks < BK / 16; ++ks) {
+      uint4 fa[2], fb[2];
+#pragma unroll
+      for (int i = 0; i < 2; ++i) fa[i] = frag<LA::KMAJ>(sa, wm * 64 + i * 32, ks, lane);
+#pragma unroll
+      for (int j = 0; j < 2; ++j) fb[j] = frag<LB::KMAJ>(sb, wn * 64 + j * 32, ks, lane);
+      if (p.variant & 1) __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) acc[i][j] = mfma(fb[j], fa[i], acc[i][j]);
+      if (p.variant & 1) __builtin_amdgcn_s_setprio(0);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+  }
+
+  // ---- epilogue: lane holds C[m][n0 + ... + 8 g + 4 h + e] for its m
+  const int h = lane >> 5;
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int m = m0 + wm * 64 + i * 32 + (lane & 31);
+    if (m >= p.M) continue;
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const int n = n0 + wn * 64 + j * 32 + 8 * g + 4 * h;
+        if (n >= p.N) continue;  // N is a multiple of 8: a group is all in or all out
+        float v[4] = {acc[i][j][4 * g], acc[i][j][4 * g + 1], acc[i][j][4 * g + 2], acc[i][j][4 * g + 3]};
+        if (p.splits > 1) {
+          float* slab = reinterpret_cast<float*>(p.c) + int64_t(split) * p.M * p.N + int64_t(m) * p.N + n;
+          *reinterpret_cast<f32x4*>(slab) = f32x4{v[0], v[1], v[2], v[3]};
+          continue;
+        }
+        if (p.bias) {
+#pragma unroll
+          for (int e = 0; e < 4; ++e)
+            v[e] += p.bias_bf16 ? bf16_to_f32(reinterpret_cast<const uint16_t*>(p.bias)[n + e])
+                                : reinterpret_cast<const float*>(p.bias)[n + e];
+        }
+        const int64_t off = int64_t(m) * p.ldc + n;
+        if (p.gelu) {
+          if (p.z) *reinterpret_cast<uint2*>(p.z + off) = uint2{pack_bf16x2(v[0], v[1]), pack_bf16x2(v[2], v[3])};
+#pragma unroll
+          for (int e = 0; e < 4; ++e) v[e] = gelu_f(v[e]);
+        }
+        if (p.residual) {
+          const uint2 rr = *reinterpret_cast<const uint2*>(p.residual + off);
+          v[0] += __uint_as_float(rr.x << 16);
+          v[1] += __uint_as_float(rr.x & 0xffff0000u);
+          v[2] += __uint_as_float(rr.y << 16);
+          v[3] += __uint_as_float(rr.y & 0xffff0000u);
+        }
+        if (p.c_bf16) {
+          *reinterpret_cast<uint2*>(reinterpret_cast<uint16_t*>(p.c) + off) =
+              uint2{pack_bf16x2(v[0], v[1]), pack_bf16x2(v[2], v[3])};
+        } else {
+          *reinterpret_cast<f32x4*>(reinterpret_cast<float*>(p.c) + off) = f32x4{v[0], v[1], v[2], v[3]};
+        }
+      }
+    }
+  }
+}
+
+inline int gemm_grid(const GemmParams& p, int& tiles_m, int& tiles_n) {
+  tiles_m = (p.M + BM - 1) / BM;
+  tiles_n = (p.N + BN - 1) / BN;
+  return tiles_m * tiles_n * (p.splits > 1 ? p.splits : 1);
+}
+
+}  // namespace p2gemm

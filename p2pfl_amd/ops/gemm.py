@@ -50,6 +50,27 @@ def splits_for(M: int, N: int, K: int) -> int:
     return s
 
 
+def supported(M: int, N: int, K: int, a_kmajor: bool, b_kmajor: bool) -> bool:
+    """Shapes the kernel takes (checked again, loudly, by the native binding)."""
+    if N % 8 or M < 1 or K < 8:
+        return False
+    if (a_kmajor or b_kmajor) and K % 8:
+        return False
+    return a_kmajor or M % 8 == 0
+
+
+def _product(a, b, a_kmajor, b_kmajor, dtype, splits=1):
+    """One Linear product on the MFMA kernel, or torch for shapes it does not take."""
+    M = a.shape[0] if a_kmajor else a.shape[1]
+    N = b.shape[0] if b_kmajor else b.shape[1]
+    K = a.shape[1] if a_kmajor else a.shape[0]
+    if supported(M, N, K, a_kmajor, b_kmajor):
+        return gemm(a, b, a_kmajor, b_kmajor, out_dtype=dtype, splits=splits)[0]
+    A = a if a_kmajor else a.t()
+    B = b if b_kmajor else b.t()
+    return (A @ B.t()).to(dtype)
+
+
 def gemm(
     a: torch.Tensor,
     b: torch.Tensor,
@@ -98,10 +119,7 @@ def _wgrad(dy2: torch.Tensor, x2: torch.Tensor, dtype: torch.dtype) -> torch.Ten
     """dW[n, k] = sum_m dy[m, n] x[m, k]: both operands m-major, split over m."""
     M, N = dy2.shape
     K = x2.shape[1]
-    s = splits_for(N, K, M)
-    if s == 1:
-        return gemm(dy2, x2, a_kmajor=False, b_kmajor=False, out_dtype=dtype)[0]
-    return gemm(dy2, x2, a_kmajor=False, b_kmajor=False, out_dtype=dtype, splits=s)[0]
+    return _product(dy2, x2, False, False, dtype, splits_for(N, K, M))
 
 
 def _bias_grad(dy2: torch.Tensor, dtype: torch.dtype) -> torch.Tensor:
@@ -137,7 +155,7 @@ class _LinearMFMA(torch.autograd.Function):
         dy2 = _rows(dy.to(torch.bfloat16))
         dx = dw = db = None
         if ctx.needs_input_grad[0]:
-            dx = gemm(dy2, w, a_kmajor=True, b_kmajor=False)[0].view(ctx.xshape)
+            dx = _product(dy2, w, True, False, torch.bfloat16).view(ctx.xshape)
         if ctx.needs_input_grad[1]:
             dw = _wgrad(dy2, x2, ctx.w_dtype)
         if ctx.b_dtype is not None and ctx.needs_input_grad[2]:
@@ -172,7 +190,7 @@ class _LinearGeluMFMA(torch.autograd.Function):
         dz, db = _fx().bias_gelu_bwd(dh2, z, zero)  # dz = dh * gelu'(z), db = column sums of dz
         dx = dw = None
         if ctx.needs_input_grad[0]:
-            dx = gemm(dz, w, a_kmajor=True, b_kmajor=False)[0].view(ctx.xshape)
+            dx = _product(dz, w, True, False, torch.bfloat16).view(ctx.xshape)
         if ctx.needs_input_grad[1]:
             dw = _wgrad(dz, x2, ctx.w_dtype)
         return dx, dw, db.to(ctx.b_dtype) if ctx.needs_input_grad[2] else None
@@ -181,7 +199,7 @@ class _LinearGeluMFMA(torch.autograd.Function):
 def _ok(x: torch.Tensor, w: torch.Tensor) -> bool:
     from p2pfl_amd.ops import _gpu
 
-    return _gpu(x) and x.dtype in (torch.bfloat16, torch.float32) and w.shape[0] % 8 == 0 and w.shape[1] % 8 == 0
+    return _gpu(x) and x.dtype in (torch.bfloat16, torch.float32) and w.shape[0] % 8 == 0 and w.shape[1] % 8 == 0 and x.shape[-1] == w.shape[1]
 
 
 def linear(x: torch.Tensor, weight: torch.Tensor, bias: Optional[torch.Tensor] = None) -> torch.Tensor:
