@@ -28,7 +28,7 @@ struct GemmParams {
   uint16_t* z;  // GELU pre-activation output (bf16, ldc), optional
   const uint16_t* residual;  // bf16 [M][ldc], optional
   int splits;
-  int variant;  // tuning experiments: bit0 setprio around MFMAs, bit1 A-panel tile order, bit2 no XCD remap
+  int variant;  // tuning experiments: bit0 setprio around MFMAs, bit1 A-panel tile order, bit2 no XCD remap, bit3 single LDS buffer (4 workgroups / CU)
 };
 
 void gemm_bf16(const GemmParams& p, hipStream_t s);

@@ -37,17 +37,20 @@ namespace p2gemm {
 
 __device__ __attribute__((aligned(16))) uint16_t g_zero16[8] = {0, 0, 0, 0, 0, 0, 0, 0};
 
-template <class LA, class LB>
+template <int NBUF, class LA, class LB>
 __global__ __launch_bounds__(NT, 2) void gemm_kernel(GemmParams p, LA la, LB lb, int tiles_m, int tiles_n) {
-  __shared__ __attribute__((aligned(16))) char smem[4 * TILE];  // [buf][A | B]
-  gemm_body(p, la, lb, tiles_m, tiles_n, smem);
+  __shared__ __attribute__((aligned(16))) char smem[NBUF * 2 * TILE];  // [buf][A | B]
+  gemm_body<NBUF>(p, la, lb, tiles_m, tiles_n, smem);
 }
 
 template <class LA, class LB>
 static void launch(const GemmParams& p, const LA& la, const LB& lb, hipStream_t s) {
   int tm, tn;
   const int grid = gemm_grid(p, tm, tn);
-  hipLaunchKernelGGL((gemm_kernel<LA, LB>), dim3(grid), dim3(NT), 0, s, p, la, lb, tm, tn);
+  if (p.variant & 8)
+    hipLaunchKernelGGL((gemm_kernel<1, LA, LB>), dim3(grid), dim3(NT), 0, s, p, la, lb, tm, tn);
+  else
+    hipLaunchKernelGGL((gemm_kernel<2, LA, LB>), dim3(grid), dim3(NT), 0, s, p, la, lb, tm, tn);
 }
 
 }  // namespace p2gemm

@@ -40,14 +40,45 @@ P2_DEVICE f32x16 mfma(uint4 a, uint4 b, f32x16 c) {
 P2_DEVICE int swz_k(int row) { return (row >> 1) & 7; }                       // k-major: 8 chunks / 128-B row
 P2_DEVICE int swz_mn(int row) { return ((row & 3) << 2) | ((row >> 2) & 3); }  // mn-major: 16 chunks / 256-B row
 
-// ---- plain matrix loaders ------------------------------------------------------
+// ---- loader protocol -----------------------------------------------------------
+// A loader is a small struct passed by value into the kernel.  `prep(r0, tid)`
+// runs once per workgroup and returns the lane's state: within one operand
+// tile a lane always moves the same four chunks (i = 0..3), whose row (k-major)
+// or column (mn-major) coordinate does not change along K, so everything that
+// depends on it is decoded once.  `src(st, i, k0, tid)` returns the global
+// address of chunk i of the K-tile starting at k0 (or g_zero16).
+//
+// Chunk geometry (cid = 256 i + tid):
+//   k-major : row = 32 i + (tid >> 3), k = k0 + 8 ((tid & 7) ^ ((tid >> 4) & 7))
+//   mn-major: k = k0 + 16 i + (tid >> 4),
+//             col = 8 ((tid & 15) ^ (((tid >> 4) & 3) << 2 | (tid >> 6) & 3))
+// (the XOR terms are swz_k / swz_mn of the LDS row, which do not depend on i).
+P2_DEVICE int kmaj_row(int i, int tid) { return 32 * i + (tid >> 3); }
+P2_DEVICE int kmaj_k(int tid) { return 8 * ((tid & 7) ^ ((tid >> 4) & 7)); }
+P2_DEVICE int mnmaj_k(int i, int tid) { return 16 * i + (tid >> 4); }
+P2_DEVICE int mnmaj_col(int tid) { return 8 * ((tid & 15) ^ ((((tid >> 4) & 3) << 2) | ((tid >> 6) & 3))); }
+
 struct PlainK {  // element (r, k) at g[r * ld + k]
   static constexpr bool KMAJ = true;
   const uint16_t* g;
   int64_t ld;
   int nrows, K;
-  P2_DEVICE const void* src(int r, int k) const {
-    return (r < nrows && k < K) ? static_cast<const void*>(g + r * ld + k) : static_cast<const void*>(g_zero16);
+  struct St {
+    const uint16_t* row[4];
+    int kk;
+  };
+  P2_DEVICE St prep(int r0, int tid) const {
+    St st;
+    st.kk = kmaj_k(tid);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int r = r0 + kmaj_row(i, tid);
+      st.row[i] = r < nrows ? g + r * ld + st.kk : nullptr;
+    }
+    return st;
+  }
+  P2_DEVICE const void* src(const St& st, int i, int k0, int) const {
+    return (st.row[i] && k0 + st.kk < K) ? static_cast<const void*>(st.row[i] + k0) : static_cast<const void*>(g_zero16);
   }
 };
 struct PlainMN {  // element (r, k) at g[k * ld + r]
@@ -55,29 +86,30 @@ struct PlainMN {  // element (r, k) at g[k * ld + r]
   const uint16_t* g;
   int64_t ld;
   int nrows, K;
-  P2_DEVICE const void* src(int k, int r) const {
-    return (r < nrows && k < K) ? static_cast<const void*>(g + k * ld + r) : static_cast<const void*>(g_zero16);
+  struct St {
+    const uint16_t* col;
+    int kr;
+  };
+  P2_DEVICE St prep(int r0, int tid) const {
+    const int c = r0 + mnmaj_col(tid);
+    return St{c < nrows ? g + c : nullptr, tid >> 4};
+  }
+  P2_DEVICE const void* src(const St& st, int i, int k0, int) const {
+    const int k = k0 + 16 * i + st.kr;
+    return (st.col && k < K) ? static_cast<const void*>(st.col + k * ld) : static_cast<const void*>(g_zero16);
   }
 };
 
-// Issue the DMA of one operand tile (rows r0.. of the M or N dimension,
-// reduction indices k0..k0+63) into `lds`; every lane moves 16 B four times.
+// Issue the DMA of one operand tile (K-tile starting at k0) into `lds`; every
+// lane moves 16 B four times.  The LDS image is lane-linear per wave; the
+// swizzle lives in the chunk -> source-address mapping above.
 template <class L>
-P2_DEVICE void stage(const L& ld, int r0, int k0, char* lds, int tid) {
+P2_DEVICE void stage(const L& ld, const typename L::St& st, int k0, char* lds, int tid) {
   const int wave = tid >> 6;
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
-    const int cid = i * NT + tid;
     char* dst = lds + (i * NT + wave * 64) * 16;  // wave-uniform; lane L writes dst + 16 L
-    const void* src;
-    if constexpr (L::KMAJ) {
-      const int row = cid >> 3, c = (cid & 7) ^ swz_k(row);
-      src = ld.src(r0 + row, k0 + 8 * c);
-    } else {
-      const int row = cid >> 4, ch = (cid & 15) ^ swz_mn(row);
-      src = ld.src(k0 + row, r0 + 8 * ch);
-    }
-    __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
+    __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)ld.src(st, i, k0, tid),
                                      (__attribute__((address_space(3))) void*)dst, 16, 0, 0);
   }
 }
@@ -121,7 +153,7 @@ P2_DEVICE int xcd_remap(int orig, int nwg) {
 }
 
 // The whole kernel body.  `p` carries M/N/K, split-K and the epilogue.
-template <class LA, class LB>
+template <int NBUF, class LA, class LB>
 P2_DEVICE void gemm_body(const GemmParams& p, const LA& la, const LB& lb, int tiles_m, int tiles_n, char* smem) {
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave >> 1, wn = wave & 1;
@@ -144,20 +176,31 @@ P2_DEVICE void gemm_body(const GemmParams& p, const LA& la, const LB& lb, int ti
 #pragma unroll
       for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.f;
 
-  if (nt > 0) {
-    stage(la, m0, kb, smem, tid);
-    stage(lb, n0, kb, smem + TILE, tid);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
+  const typename LA::St sta = la.prep(m0, tid);
+  const typename LB::St stb = lb.prep(n0, tid);
+  if constexpr (NBUF == 2) {
+    if (nt > 0) {
+      stage(la, sta, kb, smem, tid);
+      stage(lb, stb, kb, smem + TILE, tid);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+    }
   }
   for (int it = 0; it < nt; ++it) {
-    const int cur = it & 1;
+    const int cur = NBUF == 2 ? (it & 1) : 0;
     const char* sa = smem + cur * 2 * TILE;
     const char* sb = sa + TILE;
-    if (it + 1 < nt) {
-      char* na = smem + (cur ^ 1) * 2 * TILE;
-      stage(la, m0, kb + (it + 1) * BK, na, tid);
-      stage(lb, n0, kb + (it + 1) * BK, na + TILE, tid);
+    if constexpr (NBUF == 2) {
+      if (it + 1 < nt) {  // next K-tile's DMA overlaps this tile's MFMAs
+        char* na = smem + (cur ^ 1) * 2 * TILE;
+        stage(la, sta, kb + (it + 1) * BK, na, tid);
+        stage(lb, stb, kb + (it + 1) * BK, na + TILE, tid);
+      }
+    } else {  // one buffer: latency hidden by the other resident workgroups
+      stage(la, sta, kb + it * BK, smem, tid);
+      stage(lb, stb, kb + it * BK, smem + TILE, tid);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
     }
 #pragma unroll
     for (int ks = 0; ks < BK / 16; ++ks) {
@@ -173,7 +216,7 @@ P2_DEVICE void gemm_body(const GemmParams& p, const LA& la, const LB& lb, int ti
         for (int j = 0; j < 2; ++j) acc[i][j] = mfma(fb[j], fa[i], acc[i][j]);
       if (p.variant & 1) __builtin_amdgcn_s_setprio(0);
     }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if constexpr (NBUF == 2) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
   }
 

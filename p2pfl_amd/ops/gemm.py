@@ -15,6 +15,8 @@ and the ViT-B/16 of BASELINE config 4.
 
 from __future__ import annotations
 
+import os
+
 from typing import Optional, Tuple
 
 import torch
@@ -71,6 +73,19 @@ def _product(a, b, a_kmajor, b_kmajor, dtype, splits=1):
     return (A @ B.t()).to(dtype)
 
 
+# Kernel schedule per product (csrc/gemm.h variant bits; measured on the ViT
+# shapes, profiles/r2_gemm_variants.md): forward / input-gradient products run
+# the single-LDS-buffer schedule (4 workgroups per CU hide the DMA latency)
+# with A-panel tile order; the split-K weight gradient keeps the double buffer.
+_VARIANT_ENV = os.environ.get("P2PFL_GEMM_VARIANT")
+
+
+def _variant(a_kmajor: bool, splits: int) -> int:
+    if _VARIANT_ENV is not None:
+        return int(_VARIANT_ENV)
+    return 2 if (splits > 1 or not a_kmajor) else 10
+
+
 def gemm(
     a: torch.Tensor,
     b: torch.Tensor,
@@ -97,14 +112,14 @@ def gemm(
         if bias is not None or gelu or residual is not None:
             raise ValueError("split-K GEMM has no epilogue")
         slabs = torch.empty((splits, M, N), dtype=torch.float32, device=dev)
-        _C().gemm(a, b, a_kmajor, b_kmajor, slabs, None, False, None, None, splits)
+        _C().gemm(a, b, a_kmajor, b_kmajor, slabs, None, False, None, None, splits, _variant(a_kmajor, splits))
         out = torch.empty((M, N), dtype=out_dtype, device=dev) if out is None else out
         _sum_slabs(slabs, out)
         return out, None
     if out is None:
         out = torch.empty((M, N), dtype=out_dtype, device=dev)
     z = torch.empty((M, N), dtype=torch.bfloat16, device=dev) if (gelu and want_z) else None
-    _C().gemm(a, b, a_kmajor, b_kmajor, out, bias, gelu, z, residual, 1)
+    _C().gemm(a, b, a_kmajor, b_kmajor, out, bias, gelu, z, residual, 1, _variant(a_kmajor, 1))
     return out, z
 
 

@@ -86,7 +86,9 @@ def test_linear_autograd_vs_fp32(gelu):
     yr.backward(g.float())
     torch.testing.assert_close(y.float(), yr, atol=3e-2, rtol=2e-2)
     torch.testing.assert_close(x.grad.float(), xr.grad, atol=3e-2, rtol=2e-2)
-    torch.testing.assert_close(w.grad.float(), wr.grad, atol=1e-1, rtol=2e-2)
+    # dW reduces over 788 rows of a bf16 dZ (rounded GELU backward): judge it on its scale
+    scale = wr.grad.abs().max().item()
+    torch.testing.assert_close(w.grad.float(), wr.grad, atol=1e-2 * scale, rtol=2e-2)
     torch.testing.assert_close(bias.grad, br.grad, atol=1e-1, rtol=2e-2)
 
 
