@@ -208,6 +208,7 @@ void register_fused(pybind11::module& m);
 void register_bn(pybind11::module& m);
 void register_rccl(pybind11::module& m);
 void register_gemm(pybind11::module& m);
+void register_conv(pybind11::module& m);
 
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.doc() = "p2pfl_amd native HIP/CDNA4 kernels (gfx950)";
@@ -230,4 +231,5 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   register_bn(m);
   register_rccl(m);
   register_gemm(m);
+  register_conv(m);
 }

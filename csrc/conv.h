@@ -1,0 +1,41 @@
+// Host launch API of the implicit-GEMM convolutions (csrc/conv.hip).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "gemm.h"
+
+namespace p2 {
+
+// NHWC activations, (O, kh, kw, C) weights, bf16.  Output spatial size
+// OH = (H + 2 pad - dil (kh - 1) - 1) / stride + 1 (same for W).
+struct ConvShape {
+  int N, H, W, C;  // input
+  int O, OH, OW;   // output
+  int kh, kw, stride, pad, dil;
+};
+
+// y[N*OH*OW][O] = conv(x, w)                                    (C % 64 == 0, O % 8 == 0)
+// dx[N*H*W][C] = conv_transpose(dy, w)                           (O % 64 == 0, C % 8 == 0, stride 1 or 2)
+// splits == 1: bf16 output; splits > 1 without counters: fp32 slabs [splits][rows][cols]
+// at the output pointer (reduce with slab_sum); with counters (one zeroed int per 128x128
+// output tile) the slabs go to `ws` and the launch reduces them into the bf16 output itself.
+struct SplitK {
+  int splits = 1;
+  float* ws = nullptr;
+  int* counters = nullptr;
+};
+void conv_fwd(const ConvShape& s, const uint16_t* x, const uint16_t* w, void* y, const SplitK& k, int variant,
+              hipStream_t st);
+void conv_dgrad(const ConvShape& s, const uint16_t* dy, const uint16_t* w, void* dx, const SplitK& k, int variant,
+                hipStream_t st);
+// dw[O][kh*kw*C] = sum over output pixels of dy (x) im2col(x)    (O % 8 == 0, C % 8 == 0)
+// splits == 1: written as bf16 (out_bf16) or fp32; splits > 1: fp32 slabs
+// [splits][O][kh*kw*C] at `out` (reduce with slab_sum).
+void conv_wgrad(const ConvShape& s, const uint16_t* dy, const uint16_t* x, void* out, int out_bf16, const SplitK& k,
+                int variant, hipStream_t st);
+
+// out[i] = sum_s slabs[s][i] (fp32 in; bf16 or fp32 out), n % 4 == 0.
+void slab_sum(const float* slabs, int splits, int64_t n, void* out, int out_bf16, hipStream_t st);
+
+}  // namespace p2

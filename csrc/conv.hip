@@ -1,0 +1,261 @@
+// Implicit-GEMM convolutions for the ResNet family (gfx950), NHWC bf16.
+//
+// All three products of a convolution run on the MFMA GEMM core of
+// gemm_core.h; only the operand LOADERS differ, so no im2col matrix is ever
+// materialised and no tensor is transposed in memory:
+//
+//   forward   Y[m = (n, oh, ow)][o]        = sum_{k = (ky, kx, c)} X~(m, k) W[o][k]
+//   dgrad    dX[m = (n, ih, iw)][c]        = sum_{k = (ky, kx, o)} dY~(m, k) W[o][ky][kx][c]
+//   wgrad    dW[o][(ky, kx, c)]            = sum_{k = (n, oh, ow)} dY[k][o] X~(k, (ky, kx, c))
+//
+// X~ / dY~ are gathers: every 16-byte chunk of an operand tile is 8
+// consecutive channels of one pixel, located by the loader; padding taps,
+// stride holes and tails resolve to the shared zero page.  Per K-tile the
+// forward/dgrad gathers need a single (ky, kx) (C resp. O % 64 == 0), so the
+// tap decode is a wave-uniform scalar computation and a lane only adds its
+// precomputed pixel offset.  The weight gradient decodes output pixels per
+// chunk with multiply-high division.
+//
+// Layouts match the learner's channels-last weight shadows (arena.py):
+// weights are (O, kh, kw, C), so dW is written straight into the gradient
+// layout the multi-tensor optimizer consumes.
+//
+// The reference trains convolutions through torch.nn.Conv2d
+// (/root/reference/p2pfl/learning/pytorch/mnist_examples/models/cnn.py:55-62);
+// the ResNet targets are BASELINE.json configs 3 and 5.
+#include "conv.h"
+#include "gemm_core.h"
+
+namespace p2gemm {
+
+struct FastDiv {  // n / d for 0 <= n < 2^31 as (umulhi(n, mul) + n) >> shift
+  uint32_t d, mul, shift;
+};
+inline FastDiv make_fastdiv(uint32_t d) {
+  uint32_t l = 0;
+  while ((uint64_t(1) << l) < d) ++l;
+  const uint64_t mul = ((uint64_t(1) << 32) * ((uint64_t(1) << l) - d)) / d + 1;
+  return FastDiv{d, uint32_t(mul), l};
+}
+P2_DEVICE int fdiv(int n, const FastDiv& f) { return int((__umulhi(uint32_t(n), f.mul) + uint32_t(n)) >> f.shift); }
+
+constexpr int kOff = -(1 << 28);  // pixel coordinate that fails every bounds check
+
+// ---- forward: A = im2col(X), k-major, k = (ky, kx, c) ------------------------------
+struct ConvFwdA {
+  static constexpr bool KMAJ = true;
+  const uint16_t* x;
+  FastDiv ohw, ow;
+  int M, H, W, C, stride, pad, dil, kw;
+  struct St {
+    int64_t base[4];  // element offset of X[n][ih0][iw0][kk]
+    int ih0[4], iw0[4];
+    int kk;
+  };
+  P2_DEVICE St prep(int r0, int tid) const {
+    St st;
+    st.kk = kmaj_k(tid);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int m = r0 + kmaj_row(i, tid);
+      const int n = fdiv(m, ohw), r = m - n * int(ohw.d);
+      const int oh = fdiv(r, ow), owi = r - oh * int(ow.d);
+      st.ih0[i] = m < M ? oh * stride - pad : kOff;
+      st.iw0[i] = owi * stride - pad;
+      st.base[i] = ((int64_t(n) * H + st.ih0[i]) * W + st.iw0[i]) * C + st.kk;
+    }
+    return st;
+  }
+  P2_DEVICE const void* src(const St& st, int i, int k0, int) const {
+    const int tap = k0 / C, cb = k0 - tap * C;  // wave-uniform
+    const int ky = tap / kw, kx = tap - ky * kw;
+    const int ih = st.ih0[i] + ky * dil, iw = st.iw0[i] + kx * dil;
+    const bool ok = unsigned(ih) < unsigned(H) && unsigned(iw) < unsigned(W);
+    return ok ? static_cast<const void*>(x + st.base[i] + (int64_t(ky * dil) * W + kx * dil) * C + cb)
+              : static_cast<const void*>(g_zero16);
+  }
+};
+
+// ---- dgrad: A = transposed-conv gather of dY, k-major, k = (ky, kx, o) -------------
+struct ConvDgradA {
+  static constexpr bool KMAJ = true;
+  const uint16_t* dy;
+  FastDiv hw, w;
+  int M, OH, OW, O, stride, pad, dil, kw;
+  struct St {
+    int64_t nbase[4];  // element offset of dY[n][0][0][kk]
+    int thp[4], twp[4];  // ih + pad, iw + pad
+    int kk;
+  };
+  P2_DEVICE St prep(int r0, int tid) const {
+    St st;
+    st.kk = kmaj_k(tid);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int m = r0 + kmaj_row(i, tid);
+      const int n = fdiv(m, hw), r = m - n * int(hw.d);
+      const int ih = fdiv(r, w), iw = r - ih * int(w.d);
+      st.thp[i] = m < M ? ih + pad : kOff;
+      st.twp[i] = iw + pad;
+      st.nbase[i] = int64_t(n) * OH * OW * O + st.kk;
+    }
+    return st;
+  }
+  P2_DEVICE const void* src(const St& st, int i, int k0, int) const {
+    const int tap = k0 / O, ob = k0 - tap * O;  // wave-uniform
+    const int ky = tap / kw, kx = tap - ky * kw;
+    int oh = st.thp[i] - ky * dil, ow = st.twp[i] - kx * dil;
+    bool ok = oh >= 0 && ow >= 0;
+    if (stride == 2) {
+      ok = ok && !((oh | ow) & 1);
+      oh >>= 1;
+      ow >>= 1;
+    }
+    ok = ok && oh < OH && ow < OW;
+    return ok ? static_cast<const void*>(dy + st.nbase[i] + (int64_t(oh) * OW + ow) * O + ob)
+              : static_cast<const void*>(g_zero16);
+  }
+};
+
+// ---- dgrad: B = W[o][ky][kx][c] read c-contiguous, mn-major, k = (ky, kx, o) -------
+struct ConvDgradB {
+  static constexpr bool KMAJ = false;
+  const uint16_t* w;
+  int C, O, T;  // T = kh * kw
+  struct St {
+    const uint16_t* col;
+    int kr;
+  };
+  P2_DEVICE St prep(int r0, int tid) const {
+    const int c = r0 + mnmaj_col(tid);
+    return St{c < C ? w + c : nullptr, tid >> 4};
+  }
+  P2_DEVICE const void* src(const St& st, int i, int k0, int) const {
+    const int tap = k0 / O, ob = k0 - tap * O;  // wave-uniform
+    const int o = ob + 16 * i + st.kr;
+    return st.col ? static_cast<const void*>(st.col + (int64_t(o) * T + tap) * C) : static_cast<const void*>(g_zero16);
+  }
+};
+
+// ---- wgrad: B = im2col(X) read c-contiguous, mn-major, cols = (ky, kx, c), k = pixel
+struct ConvWgradB {
+  static constexpr bool KMAJ = false;
+  const uint16_t* x;
+  FastDiv ohw, ow, c_div;
+  int M, H, W, C, stride, pad, dil, kw, ncols;
+  struct St {
+    int kyd, kxd, c, kr;
+  };
+  P2_DEVICE St prep(int r0, int tid) const {
+    const int col = r0 + mnmaj_col(tid);
+    const int tap = fdiv(col, c_div), c = col - tap * C;
+    const int ky = tap / kw, kx = tap - ky * kw;
+    return St{col < ncols ? ky * dil - pad : kOff, kx * dil - pad, c, tid >> 4};
+  }
+  P2_DEVICE const void* src(const St& st, int i, int k0, int) const {
+    const int m = k0 + 16 * i + st.kr;
+    const int n = fdiv(m, ohw), r = m - n * int(ohw.d);
+    const int oh = fdiv(r, ow), owi = r - oh * int(ow.d);
+    const int ih = oh * stride + st.kyd, iw = owi * stride + st.kxd;
+    const bool ok = m < M && unsigned(ih) < unsigned(H) && unsigned(iw) < unsigned(W);
+    return ok ? static_cast<const void*>(x + ((int64_t(n) * H + ih) * W + iw) * C + st.c)
+              : static_cast<const void*>(g_zero16);
+  }
+};
+
+template <int NBUF, class LA, class LB>
+__global__ __launch_bounds__(NT, 2) void conv_kernel(GemmParams p, LA la, LB lb, int tiles_m, int tiles_n) {
+  __shared__ __attribute__((aligned(16))) char smem[NBUF * 2 * TILE];
+  gemm_body<NBUF>(p, la, lb, tiles_m, tiles_n, smem);
+}
+
+template <class LA, class LB>
+static void launch(const GemmParams& p, const LA& la, const LB& lb, hipStream_t s) {
+  int tm, tn;
+  const int grid = gemm_grid(p, tm, tn);
+  if (p.variant & 8)
+    hipLaunchKernelGGL((conv_kernel<1, LA, LB>), dim3(grid), dim3(NT), 0, s, p, la, lb, tm, tn);
+  else
+    hipLaunchKernelGGL((conv_kernel<2, LA, LB>), dim3(grid), dim3(NT), 0, s, p, la, lb, tm, tn);
+}
+
+static GemmParams base_params(int M, int N, int K, void* c, int64_t ldc, int c_bf16, const p2::SplitK& k,
+                              int variant) {
+  const int splits = k.splits;
+  GemmParams p{};
+  p.ws = k.ws;
+  p.counters = splits > 1 ? k.counters : nullptr;
+  p.M = M;
+  p.N = N;
+  p.K = K;
+  p.c = c;
+  p.ldc = ldc;
+  p.c_bf16 = c_bf16;
+  p.splits = splits < 1 ? 1 : splits;
+  p.variant = variant;
+  return p;
+}
+
+// One float4 column per thread, slices summed 8 loads at a time (independent
+// loads in flight); 64-thread blocks so even a small gradient spreads over the CUs.
+__global__ __launch_bounds__(64) void slab_sum_kernel(const float* __restrict__ slabs, int splits, int64_t n4,
+                                                       void* out, int out_bf16) {
+  const int64_t i = blockIdx.x * int64_t(64) + threadIdx.x;
+  if (i >= n4) return;
+  const f32x4* src = reinterpret_cast<const f32x4*>(slabs) + i;
+  f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+  int s = 0;
+  for (; s + 8 <= splits; s += 8) {
+    f32x4 v[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) v[u] = src[(s + u) * n4];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) acc += v[u];
+  }
+  for (; s < splits; ++s) acc += src[s * n4];
+  if (out_bf16)
+    reinterpret_cast<uint2*>(out)[i] = uint2{pack_bf16x2(acc[0], acc[1]), pack_bf16x2(acc[2], acc[3])};
+  else
+    reinterpret_cast<f32x4*>(out)[i] = acc;
+}
+
+}  // namespace p2gemm
+
+namespace p2 {
+
+void conv_fwd(const ConvShape& s, const uint16_t* x, const uint16_t* w, void* y, const SplitK& k, int variant,
+              hipStream_t st) {
+  using namespace p2gemm;
+  const int M = s.N * s.OH * s.OW, K = s.kh * s.kw * s.C;
+  const GemmParams p = base_params(M, s.O, K, y, s.O, k.splits <= 1 || k.counters, k, variant);
+  const ConvFwdA la{x, make_fastdiv(s.OH * s.OW), make_fastdiv(s.OW), M, s.H, s.W, s.C, s.stride, s.pad, s.dil, s.kw};
+  launch(p, la, PlainK{w, K, s.O, K}, st);
+}
+
+void conv_dgrad(const ConvShape& s, const uint16_t* dy, const uint16_t* w, void* dx, const SplitK& k, int variant,
+                hipStream_t st) {
+  using namespace p2gemm;
+  const int M = s.N * s.H * s.W, K = s.kh * s.kw * s.O;
+  const GemmParams p = base_params(M, s.C, K, dx, s.C, k.splits <= 1 || k.counters, k, variant);
+  const ConvDgradA la{dy, make_fastdiv(s.H * s.W), make_fastdiv(s.W), M, s.OH, s.OW, s.O, s.stride, s.pad, s.dil, s.kw};
+  launch(p, la, ConvDgradB{w, s.C, s.O, s.kh * s.kw}, st);
+}
+
+void conv_wgrad(const ConvShape& s, const uint16_t* dy, const uint16_t* x, void* out, int out_bf16, const SplitK& k,
+                int variant, hipStream_t st) {
+  using namespace p2gemm;
+  const int npix = s.N * s.OH * s.OW, ncols = s.kh * s.kw * s.C;
+  const GemmParams p =
+      base_params(s.O, ncols, npix, out, ncols, (k.splits > 1 && !k.counters) ? 0 : out_bf16, k, variant);
+  const ConvWgradB lb{x,   make_fastdiv(s.OH * s.OW), make_fastdiv(s.OW), make_fastdiv(s.C), npix, s.H, s.W, s.C,
+                      s.stride, s.pad, s.dil, s.kw, ncols};
+  launch(p, PlainMN{dy, s.O, s.O, npix}, lb, st);
+}
+
+void slab_sum(const float* slabs, int splits, int64_t n, void* out, int out_bf16, hipStream_t st) {
+  const int64_t n4 = n / 4;
+  hipLaunchKernelGGL(p2gemm::slab_sum_kernel, dim3(int((n4 + 63) / 64)), dim3(64), 0, st, slabs, splits, n4, out,
+                     out_bf16);
+}
+
+}  // namespace p2

@@ -1,0 +1,176 @@
+// PyTorch bindings of the implicit-GEMM convolutions (p2pfl_amd._C.conv_*).
+// Every shape / layout / alignment assumption of csrc/conv.hip is checked here
+// before the launch, so a bad call is a Python exception, never a GPU fault.
+#include <torch/extension.h>
+#include <c10/core/DeviceGuard.h>
+#include <c10/hip/HIPStream.h>
+
+#include "conv.h"
+
+namespace {
+
+void check_nhwc(const torch::Tensor& t, const char* name) {
+  TORCH_CHECK(t.is_cuda() && t.scalar_type() == torch::kBFloat16, name, " must be a bf16 GPU tensor");
+  TORCH_CHECK(t.dim() == 4 && t.is_contiguous(), name, " must be a contiguous 4-D (NHWC / OHWC) tensor");
+  TORCH_CHECK(reinterpret_cast<uintptr_t>(t.data_ptr()) % 16 == 0, name, " must be 16-byte aligned");
+}
+
+int out_size(int in, int k, int stride, int pad, int dil) { return (in + 2 * pad - dil * (k - 1) - 1) / stride + 1; }
+
+p2::ConvShape make_shape(int64_t N, int64_t H, int64_t W, int64_t C, int64_t O, int64_t kh, int64_t kw, int64_t stride,
+                         int64_t pad, int64_t dil) {
+  TORCH_CHECK(stride >= 1 && stride <= 2 && pad >= 0 && dil >= 1, "conv: stride 1/2, pad >= 0, dilation >= 1");
+  TORCH_CHECK(N * H * W < (int64_t(1) << 31) && kh * kw * std::max(C, O) < (int64_t(1) << 31), "conv: size overflow");
+  p2::ConvShape s{};
+  s.N = int(N);
+  s.H = int(H);
+  s.W = int(W);
+  s.C = int(C);
+  s.O = int(O);
+  s.kh = int(kh);
+  s.kw = int(kw);
+  s.stride = int(stride);
+  s.pad = int(pad);
+  s.dil = int(dil);
+  s.OH = out_size(s.H, s.kh, s.stride, s.pad, s.dil);
+  s.OW = out_size(s.W, s.kw, s.stride, s.pad, s.dil);
+  TORCH_CHECK(s.OH >= 1 && s.OW >= 1, "conv: empty output");
+  return s;
+}
+
+hipStream_t stream_of(const torch::Tensor& t) { return c10::hip::getCurrentHIPStream(t.device().index()).stream(); }
+
+// Split-K configuration: without `counters`, splits > 1 writes fp32 slabs to the output
+// tensor itself; with `counters` (int32, one per 128 x 128 output tile, all zero) the slabs
+// go to `ws` (fp32, splits * rows * cols) and the launch reduces them itself.
+p2::SplitK make_splitk(int64_t splits, const c10::optional<torch::Tensor>& ws, const c10::optional<torch::Tensor>& counters,
+                       int64_t rows, int64_t cols, const torch::Tensor& like, const char* who) {
+  TORCH_CHECK(splits >= 1 && splits <= 128, who, ": 1 <= splits <= 128");
+  p2::SplitK k;
+  k.splits = int(splits);
+  const bool have_cnt = counters.has_value() && counters->defined();
+  if (have_cnt) {
+    TORCH_CHECK(splits > 1, who, ": counters only with splits > 1");
+    const int64_t tiles = ((rows + 127) / 128) * ((cols + 127) / 128);
+    TORCH_CHECK(counters->is_cuda() && counters->scalar_type() == torch::kInt32 && counters->is_contiguous() &&
+                    counters->numel() >= tiles && counters->device() == like.device(),
+                who, ": counters must be a contiguous int32 GPU tensor with >= ", tiles, " entries");
+    TORCH_CHECK(ws.has_value() && ws->defined(), who, ": counters need a workspace");
+    TORCH_CHECK(ws->is_cuda() && ws->scalar_type() == torch::kFloat32 && ws->is_contiguous() &&
+                    ws->numel() >= splits * rows * cols && reinterpret_cast<uintptr_t>(ws->data_ptr()) % 16 == 0 &&
+                    ws->device() == like.device(),
+                who, ": workspace must be contiguous fp32 with splits * rows * cols elements");
+    k.counters = counters->data_ptr<int>();
+    k.ws = ws->data_ptr<float>();
+  }
+  return k;
+}
+
+// The output of conv_fwd / conv_dgrad: bf16 NHWC [n, h, w, c], or raw fp32 slabs
+// (contiguous, splits * n*h*w*c elements) for a split-K launch without counters.
+void check_out(const torch::Tensor& out, const p2::SplitK& k, int n, int h, int w, int c, const char* who) {
+  if (k.splits == 1 || k.counters) {
+    check_nhwc(out, "out");
+    TORCH_CHECK(out.size(0) == n && out.size(1) == h && out.size(2) == w && out.size(3) == c, who, ": out shape");
+  } else {
+    TORCH_CHECK(out.is_cuda() && out.scalar_type() == torch::kFloat32 && out.is_contiguous() &&
+                    out.numel() == int64_t(k.splits) * n * h * w * c && reinterpret_cast<uintptr_t>(out.data_ptr()) % 16 == 0,
+                who, ": split-K out must be contiguous fp32 with splits * rows * cols elements");
+  }
+}
+
+using OptT = c10::optional<torch::Tensor>;
+
+// x [N, H, W, C], w [O, kh, kw, C]  ->  y [N, OH, OW, O]
+void conv_fwd(torch::Tensor x, torch::Tensor w, int64_t stride, int64_t pad, int64_t dil, torch::Tensor y,
+              int64_t splits, int64_t variant, OptT ws, OptT counters) {
+  check_nhwc(x, "x");
+  check_nhwc(w, "w");
+  TORCH_CHECK(w.size(3) == x.size(3), "conv_fwd: channel mismatch");
+  const auto s = make_shape(x.size(0), x.size(1), x.size(2), x.size(3), w.size(0), w.size(1), w.size(2), stride, pad, dil);
+  TORCH_CHECK(s.C % 64 == 0 && s.O % 8 == 0, "conv_fwd: needs C % 64 == 0 and O % 8 == 0 (C=", s.C, " O=", s.O, ")");
+  const auto k = make_splitk(splits, ws, counters, int64_t(s.N) * s.OH * s.OW, s.O, x, "conv_fwd");
+  check_out(y, k, s.N, s.OH, s.OW, s.O, "conv_fwd");
+  TORCH_CHECK(x.device() == w.device() && y.device() == x.device(), "conv_fwd: device mismatch");
+  const c10::DeviceGuard g(x.device());
+  p2::conv_fwd(s, reinterpret_cast<const uint16_t*>(x.data_ptr()), reinterpret_cast<const uint16_t*>(w.data_ptr()),
+               y.data_ptr(), k, int(variant), stream_of(x));
+}
+
+// dy [N, OH, OW, O], w [O, kh, kw, C]  ->  dx [N, H, W, C]  (dx_shape = (N, H, W, C), dx may hold slabs)
+void conv_dgrad(torch::Tensor dy, torch::Tensor w, int64_t stride, int64_t pad, int64_t dil, torch::Tensor dx,
+                std::vector<int64_t> dx_shape, int64_t splits, int64_t variant, OptT ws, OptT counters) {
+  check_nhwc(dy, "dy");
+  check_nhwc(w, "w");
+  TORCH_CHECK(dx_shape.size() == 4, "conv_dgrad: dx_shape is (N, H, W, C)");
+  const auto s =
+      make_shape(dx_shape[0], dx_shape[1], dx_shape[2], dx_shape[3], w.size(0), w.size(1), w.size(2), stride, pad, dil);
+  TORCH_CHECK(w.size(3) == s.C, "conv_dgrad: channel mismatch");
+  TORCH_CHECK(s.O % 64 == 0 && s.C % 8 == 0, "conv_dgrad: needs O % 64 == 0 and C % 8 == 0 (C=", s.C, " O=", s.O, ")");
+  TORCH_CHECK(dy.size(0) == s.N && dy.size(1) == s.OH && dy.size(2) == s.OW && dy.size(3) == s.O, "conv_dgrad: dy shape");
+  const auto k = make_splitk(splits, ws, counters, int64_t(s.N) * s.H * s.W, s.C, dy, "conv_dgrad");
+  check_out(dx, k, s.N, s.H, s.W, s.C, "conv_dgrad");
+  TORCH_CHECK(dy.device() == w.device() && dx.device() == dy.device(), "conv_dgrad: device mismatch");
+  const c10::DeviceGuard g(dy.device());
+  p2::conv_dgrad(s, reinterpret_cast<const uint16_t*>(dy.data_ptr()), reinterpret_cast<const uint16_t*>(w.data_ptr()),
+                 dx.data_ptr(), k, int(variant), stream_of(dy));
+}
+
+// dy [N, OH, OW, O], x [N, H, W, C]  ->  out: [O, kh, kw, C] bf16/fp32, or raw fp32 slabs
+// [splits, O*kh*kw*C] for a split-K launch without counters
+void conv_wgrad(torch::Tensor dy, torch::Tensor x, int64_t kh, int64_t kw, int64_t stride, int64_t pad, int64_t dil,
+                torch::Tensor out, int64_t splits, int64_t variant, OptT ws, OptT counters) {
+  check_nhwc(dy, "dy");
+  check_nhwc(x, "x");
+  const auto s = make_shape(x.size(0), x.size(1), x.size(2), x.size(3), dy.size(3), kh, kw, stride, pad, dil);
+  TORCH_CHECK(s.O % 8 == 0 && s.C % 8 == 0, "conv_wgrad: needs O % 8 == 0 and C % 8 == 0");
+  TORCH_CHECK(dy.size(0) == s.N && dy.size(1) == s.OH && dy.size(2) == s.OW, "conv_wgrad: dy shape");
+  TORCH_CHECK(out.is_cuda() && out.is_contiguous() && reinterpret_cast<uintptr_t>(out.data_ptr()) % 16 == 0,
+              "conv_wgrad: out must be contiguous and 16-byte aligned");
+  const int64_t n = int64_t(s.O) * kh * kw * s.C;
+  const auto k = make_splitk(splits, ws, counters, s.O, kh * kw * s.C, x, "conv_wgrad");
+  int out_bf16 = 0;
+  if (k.splits > 1 && !k.counters) {
+    TORCH_CHECK(out.scalar_type() == torch::kFloat32 && out.numel() == splits * n, "conv_wgrad: split-K out must be fp32 [splits, n]");
+  } else {
+    TORCH_CHECK(out.numel() == n && (out.scalar_type() == torch::kFloat32 || out.scalar_type() == torch::kBFloat16),
+                "conv_wgrad: out must be [O, kh, kw, C] bf16/fp32");
+    out_bf16 = out.scalar_type() == torch::kBFloat16;
+  }
+  TORCH_CHECK(dy.device() == x.device() && out.device() == x.device(), "conv_wgrad: device mismatch");
+  const c10::DeviceGuard g(x.device());
+  p2::conv_wgrad(s, reinterpret_cast<const uint16_t*>(dy.data_ptr()), reinterpret_cast<const uint16_t*>(x.data_ptr()),
+                 out.data_ptr(), out_bf16, k, int(variant), stream_of(x));
+}
+
+// out = sum over dim 0 of fp32 slabs [S, n]
+void slab_sum(torch::Tensor slabs, torch::Tensor out) {
+  TORCH_CHECK(slabs.is_cuda() && slabs.scalar_type() == torch::kFloat32 && slabs.dim() == 2 && slabs.is_contiguous(),
+              "slab_sum: slabs must be contiguous fp32 [S, n]");
+  const int64_t n = slabs.size(1);
+  TORCH_CHECK(n % 4 == 0 && out.is_cuda() && out.is_contiguous() && out.numel() == n &&
+                  (out.scalar_type() == torch::kFloat32 || out.scalar_type() == torch::kBFloat16),
+              "slab_sum: out must be contiguous fp32/bf16 with n % 4 == 0 elements");
+  TORCH_CHECK(reinterpret_cast<uintptr_t>(out.data_ptr()) % 16 == 0 && reinterpret_cast<uintptr_t>(slabs.data_ptr()) % 16 == 0,
+              "slab_sum: alignment");
+  TORCH_CHECK(slabs.size(0) >= 1 && slabs.device() == out.device(), "slab_sum: bad slabs");
+  const c10::DeviceGuard g(out.device());
+  p2::slab_sum(slabs.data_ptr<float>(), int(slabs.size(0)), n, out.data_ptr(), out.scalar_type() == torch::kBFloat16,
+               stream_of(out));
+}
+
+}  // namespace
+
+void register_conv(pybind11::module& m) {
+  using pybind11::arg;
+  m.def("conv_fwd", &conv_fwd, "implicit-GEMM conv forward (NHWC bf16)", arg("x"), arg("w"), arg("stride"), arg("pad"),
+        arg("dil"), arg("y"), arg("splits") = 1, arg("variant") = 10, arg("ws") = pybind11::none(),
+        arg("counters") = pybind11::none());
+  m.def("conv_dgrad", &conv_dgrad, "implicit-GEMM conv input gradient", arg("dy"), arg("w"), arg("stride"), arg("pad"),
+        arg("dil"), arg("dx"), arg("dx_shape"), arg("splits") = 1, arg("variant") = 10, arg("ws") = pybind11::none(),
+        arg("counters") = pybind11::none());
+  m.def("conv_wgrad", &conv_wgrad, "implicit-GEMM conv weight gradient", arg("dy"), arg("x"), arg("kh"), arg("kw"),
+        arg("stride"), arg("pad"), arg("dil"), arg("out"), arg("splits") = 1, arg("variant") = 2,
+        arg("ws") = pybind11::none(), arg("counters") = pybind11::none());
+  m.def("slab_sum", &slab_sum, "sum of fp32 split-K slabs", arg("slabs"), arg("out"));
+}

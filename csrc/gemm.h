@@ -13,7 +13,11 @@ namespace p2 {
 // Epilogue, in order: + bias[n] (fp32 or bf16), GELU (writes the
 // pre-activation to `z` if given), + residual[m][n] (bf16); C is bf16 or
 // fp32.  With splits > 1 every K-slice writes its raw fp32 partial to
-// c + slice * M * N instead (no epilogue; reduce afterwards).
+// c + slice * M * N instead (no epilogue; reduce afterwards) -- or, when
+// `counters` is given, to the workspace `ws` ([splits][M][N] fp32), and the
+// last slice to finish a tile reduces the tile in the same launch and runs
+// the epilogue into c.  `counters` holds one int per output tile, zero
+// before the launch; the kernel leaves it zero again.
 struct GemmParams {
   const uint16_t* a;
   const uint16_t* b;
@@ -28,6 +32,8 @@ struct GemmParams {
   uint16_t* z;  // GELU pre-activation output (bf16, ldc), optional
   const uint16_t* residual;  // bf16 [M][ldc], optional
   int splits;
+  float* ws;      // split-K workspace for the in-launch reduction
+  int* counters;  // per-tile arrival counters (see above), or null
   int variant;  // tuning experiments: bit0 setprio around MFMAs, bit1 A-panel tile order, bit2 no XCD remap, bit3 single LDS buffer (4 workgroups / CU)
 };
 

@@ -35,8 +35,6 @@
 
 namespace p2gemm {
 
-__device__ __attribute__((aligned(16))) uint16_t g_zero16[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-
 template <int NBUF, class LA, class LB>
 __global__ __launch_bounds__(NT, 2) void gemm_kernel(GemmParams p, LA la, LB lb, int tiles_m, int tiles_n) {
   __shared__ __attribute__((aligned(16))) char smem[NBUF * 2 * TILE];  // [buf][A | B]

@@ -20,7 +20,8 @@ void check_bf16_2d(const torch::Tensor& t, const char* name) {
 // or [splits, M, N] fp32 when splits > 1.
 void gemm(torch::Tensor a, torch::Tensor b, bool a_kmajor, bool b_kmajor, torch::Tensor out,
           c10::optional<torch::Tensor> bias, bool gelu, c10::optional<torch::Tensor> z,
-          c10::optional<torch::Tensor> residual, int64_t splits, int64_t variant) {
+          c10::optional<torch::Tensor> residual, int64_t splits, int64_t variant, c10::optional<torch::Tensor> ws,
+          c10::optional<torch::Tensor> counters) {
   check_bf16_2d(a, "a");
   check_bf16_2d(b, "b");
   const int64_t M = a_kmajor ? a.size(0) : a.size(1), K = a_kmajor ? a.size(1) : a.size(0);
@@ -46,7 +47,21 @@ void gemm(torch::Tensor a, torch::Tensor b, bool a_kmajor, bool b_kmajor, torch:
   p.b_kmajor = b_kmajor;
   p.splits = int(splits);
   p.variant = int(variant);
-  if (splits > 1) {
+  const bool in_launch = counters.has_value() && counters->defined();
+  if (in_launch) {  // split-K reduced inside the launch: slabs in ws, epilogue into out
+    TORCH_CHECK(splits > 1, "gemm: counters only with splits > 1");
+    const int64_t tiles = ((M + 127) / 128) * ((N + 127) / 128);
+    TORCH_CHECK(counters->is_cuda() && counters->scalar_type() == torch::kInt32 && counters->is_contiguous() &&
+                    counters->numel() >= tiles && counters->device() == a.device(),
+                "gemm: counters must be a contiguous int32 GPU tensor with one entry per 128x128 tile");
+    TORCH_CHECK(ws.has_value() && ws->defined() && ws->is_cuda() && ws->scalar_type() == torch::kFloat32 &&
+                    ws->is_contiguous() && ws->numel() >= splits * M * N && ws->device() == a.device() &&
+                    reinterpret_cast<uintptr_t>(ws->data_ptr()) % 16 == 0,
+                "gemm: split-K workspace must be contiguous fp32 with splits * M * N elements");
+    p.ws = ws->data_ptr<float>();
+    p.counters = counters->data_ptr<int>();
+  }
+  if (splits > 1 && !in_launch) {
     TORCH_CHECK(out.scalar_type() == torch::kFloat32 && out.is_contiguous() && out.numel() == splits * M * N,
                 "gemm: split-K output must be a contiguous fp32 [splits, M, N] tensor");
     TORCH_CHECK(!bias.has_value() && !gelu && !residual.has_value(), "gemm: no epilogue with split-K");
@@ -91,5 +106,6 @@ void register_gemm(pybind11::module& m) {
         pybind11::arg("a"), pybind11::arg("b"), pybind11::arg("a_kmajor"), pybind11::arg("b_kmajor"),
         pybind11::arg("out"), pybind11::arg("bias") = pybind11::none(), pybind11::arg("gelu") = false,
         pybind11::arg("z") = pybind11::none(), pybind11::arg("residual") = pybind11::none(),
-        pybind11::arg("splits") = 1, pybind11::arg("variant") = 0);
+        pybind11::arg("splits") = 1, pybind11::arg("variant") = 0, pybind11::arg("ws") = pybind11::none(),
+        pybind11::arg("counters") = pybind11::none());
 }

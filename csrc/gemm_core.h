@@ -29,8 +29,8 @@ typedef short s16x4 __attribute__((ext_vector_type(4)));
 constexpr int BM = 128, BN = 128, BK = 64, NT = 256;
 constexpr int TILE = BM * BK * 2;  // bytes per operand tile (16 KB)
 
-// 16 zero bytes every out-of-operand chunk is loaded from
-extern __device__ __attribute__((aligned(16))) uint16_t g_zero16[8];
+// 16 zero bytes every out-of-operand chunk is loaded from (one copy per translation unit)
+static __device__ __attribute__((aligned(16))) uint16_t g_zero16[8] = {0, 0, 0, 0, 0, 0, 0, 0};
 
 P2_DEVICE f32x16 mfma(uint4 a, uint4 b, f32x16 c) {
   return __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8_t, a), __builtin_bit_cast(bf16x8_t, b), c,
@@ -220,52 +220,108 @@ P2_DEVICE void gemm_body(const GemmParams& p, const LA& la, const LB& lb, int ti
     __syncthreads();
   }
 
-  // ---- epilogue: lane holds C[m][n0 + ... + 8 g + 4 h + e] for its m
+  // ---- epilogue: lane holds C[m][n0 + wn*64 + j*32 + 8 g + 4 h + e] for its m
   const int h = lane >> 5;
+  auto row_of = [&](int i) { return m0 + wm * 64 + i * 32 + (lane & 31); };
+  auto col_of = [&](int j, int g) { return n0 + wn * 64 + j * 32 + 8 * g + 4 * h; };
+  // bias, GELU (+ pre-activation), residual, store of C[m][n..n+3]
+  auto finish = [&](int m, int n, float v0, float v1, float v2, float v3) {
+    float v[4] = {v0, v1, v2, v3};
+    if (p.bias) {
 #pragma unroll
-  for (int i = 0; i < 2; ++i) {
-    const int m = m0 + wm * 64 + i * 32 + (lane & 31);
-    if (m >= p.M) continue;
+      for (int e = 0; e < 4; ++e)
+        v[e] += p.bias_bf16 ? bf16_to_f32(reinterpret_cast<const uint16_t*>(p.bias)[n + e])
+                            : reinterpret_cast<const float*>(p.bias)[n + e];
+    }
+    const int64_t off = int64_t(m) * p.ldc + n;
+    if (p.gelu) {
+      if (p.z) *reinterpret_cast<uint2*>(p.z + off) = uint2{pack_bf16x2(v[0], v[1]), pack_bf16x2(v[2], v[3])};
 #pragma unroll
-    for (int j = 0; j < 2; ++j) {
+      for (int e = 0; e < 4; ++e) v[e] = gelu_f(v[e]);
+    }
+    if (p.residual) {
+      const uint2 rr = *reinterpret_cast<const uint2*>(p.residual + off);
+      v[0] += __uint_as_float(rr.x << 16);
+      v[1] += __uint_as_float(rr.x & 0xffff0000u);
+      v[2] += __uint_as_float(rr.y << 16);
+      v[3] += __uint_as_float(rr.y & 0xffff0000u);
+    }
+    if (p.c_bf16) {
+      *reinterpret_cast<uint2*>(reinterpret_cast<uint16_t*>(p.c) + off) =
+          uint2{pack_bf16x2(v[0], v[1]), pack_bf16x2(v[2], v[3])};
+    } else {
+      *reinterpret_cast<f32x4*>(reinterpret_cast<float*>(p.c) + off) = f32x4{v[0], v[1], v[2], v[3]};
+    }
+  };
+  if (p.splits > 1) {
+    // every K-slice writes its raw fp32 partial tile (N % 8 == 0: a group is all in or all out)
+    float* slabs = p.counters ? p.ws : reinterpret_cast<float*>(p.c);
+    const int64_t mn = int64_t(p.M) * p.N;
 #pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        const int n = n0 + wn * 64 + j * 32 + 8 * g + 4 * h;
-        if (n >= p.N) continue;  // N is a multiple of 8: a group is all in or all out
-        float v[4] = {acc[i][j][4 * g], acc[i][j][4 * g + 1], acc[i][j][4 * g + 2], acc[i][j][4 * g + 3]};
-        if (p.splits > 1) {
-          float* slab = reinterpret_cast<float*>(p.c) + int64_t(split) * p.M * p.N + int64_t(m) * p.N + n;
-          *reinterpret_cast<f32x4*>(slab) = f32x4{v[0], v[1], v[2], v[3]};
-          continue;
-        }
-        if (p.bias) {
+    for (int i = 0; i < 2; ++i)
 #pragma unroll
-          for (int e = 0; e < 4; ++e)
-            v[e] += p.bias_bf16 ? bf16_to_f32(reinterpret_cast<const uint16_t*>(p.bias)[n + e])
-                                : reinterpret_cast<const float*>(p.bias)[n + e];
-        }
-        const int64_t off = int64_t(m) * p.ldc + n;
-        if (p.gelu) {
-          if (p.z) *reinterpret_cast<uint2*>(p.z + off) = uint2{pack_bf16x2(v[0], v[1]), pack_bf16x2(v[2], v[3])};
+      for (int j = 0; j < 2; ++j)
 #pragma unroll
-          for (int e = 0; e < 4; ++e) v[e] = gelu_f(v[e]);
+        for (int g = 0; g < 4; ++g) {
+          const int m = row_of(i), n = col_of(j, g);
+          if (m < p.M && n < p.N)
+            *reinterpret_cast<f32x4*>(slabs + split * mn + int64_t(m) * p.N + n) =
+                f32x4{acc[i][j][4 * g], acc[i][j][4 * g + 1], acc[i][j][4 * g + 2], acc[i][j][4 * g + 3]};
         }
-        if (p.residual) {
-          const uint2 rr = *reinterpret_cast<const uint2*>(p.residual + off);
-          v[0] += __uint_as_float(rr.x << 16);
-          v[1] += __uint_as_float(rr.x & 0xffff0000u);
-          v[2] += __uint_as_float(rr.y << 16);
-          v[3] += __uint_as_float(rr.y & 0xffff0000u);
-        }
-        if (p.c_bf16) {
-          *reinterpret_cast<uint2*>(reinterpret_cast<uint16_t*>(p.c) + off) =
-              uint2{pack_bf16x2(v[0], v[1]), pack_bf16x2(v[2], v[3])};
-        } else {
-          *reinterpret_cast<f32x4*>(reinterpret_cast<float*>(p.c) + off) = f32x4{v[0], v[1], v[2], v[3]};
-        }
+    if (!p.counters) return;
+    // In-launch reduction: the slice that arrives last at this tile's counter
+    // sums the other slices' slabs and runs the epilogue (agent-scope release
+    // before the ticket, acquire after it; the counter is reset for the next
+    // launch, so the zero-initialised counter array is reusable).
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    int* flag = reinterpret_cast<int*>(smem);
+    if (tid == 0) {
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      const int old = __hip_atomic_fetch_add(p.counters + t, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      flag[0] = old == p.splits - 1;
+    }
+    __syncthreads();
+    if (!flag[0]) return;
+    if (tid == 0) {
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __hip_atomic_store(p.counters + t, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    __syncthreads();
+    // sum all slices from the workspace (own slab included: acc is dead here,
+    // which keeps the register budget of the main loop); the 16 groups of a
+    // lane are independent loads, so each slice costs one memory round trip
+    f32x4 sum[16];
+#pragma unroll
+    for (int q = 0; q < 16; ++q) sum[q] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int s2 = 0; s2 < p.splits; ++s2) {
+      const float* base = slabs + s2 * mn;
+#pragma unroll
+      for (int q = 0; q < 16; ++q) {
+        const int i = q >> 3, j = (q >> 2) & 1, g = q & 3;
+        const int m = row_of(i), n = col_of(j, g);
+        if (m < p.M && n < p.N) sum[q] += *reinterpret_cast<const f32x4*>(base + int64_t(m) * p.N + n);
       }
     }
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+      const int i = q >> 3, j = (q >> 2) & 1, g = q & 3;
+      const int m = row_of(i), n = col_of(j, g);
+      if (m < p.M && n < p.N) finish(m, n, sum[q][0], sum[q][1], sum[q][2], sum[q][3]);
+    }
+    return;
   }
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const int m = row_of(i), n = col_of(j, g);
+        if (m < p.M && n < p.N) finish(m, n, acc[i][j][4 * g], acc[i][j][4 * g + 1], acc[i][j][4 * g + 2], acc[i][j][4 * g + 3]);
+      }
 }
 
 inline int gemm_grid(const GemmParams& p, int& tiles_m, int& tiles_n) {

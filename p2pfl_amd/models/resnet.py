@@ -7,8 +7,11 @@ without max-pool for 32x32 inputs, ``stem="imagenet"`` the 7x7/stride-2 stem
 plus max-pool.  Inputs are uint8 images (the data modules keep datasets as
 uint8 on the device); normalisation to [0, 1] happens in ``forward``.
 
-Activations run channels-last on the GPU (MIOpen NHWC convolutions under
-bf16 autocast); weights stay NCHW views of the flat parameter arena.  Every
+Activations run channels-last on the GPU.  Every convolution but the
+3-channel stem runs on the hand-written implicit-GEMM MFMA kernels
+(``csrc/conv.hip`` via :func:`~p2pfl_amd.ops.conv.conv2d`: forward, input
+and weight gradient) reading the learner's channels-last bf16 weight shadow;
+the stem (and any shape those kernels do not take) uses ``F.conv2d``.  Every
 ``BatchNorm2d -> (+ shortcut) -> ReLU`` chain runs as the fused HIP kernel of
 ``csrc/batchnorm.hip`` (:func:`~p2pfl_amd.ops.batchnorm.batch_norm_act`).  Optimiser: SGD with momentum 0.9 and weight decay 5e-4 (fused
 into one arena kernel by the learner), a standard federated CIFAR setup.
@@ -24,6 +27,7 @@ from torch import nn
 
 from p2pfl_amd.models.base import FLModule, seed_everything
 from p2pfl_amd.ops.batchnorm import batch_norm_act
+from p2pfl_amd.ops.conv import conv2d
 
 # NHWC activations on the GPU (P2PFL_CHANNELS_LAST=0 keeps NCHW)
 _CHANNELS_LAST = os.environ.get("P2PFL_CHANNELS_LAST", "1") != "0"
@@ -33,7 +37,7 @@ def _shortcut(sc: nn.Module, x: torch.Tensor) -> torch.Tensor:
     """Identity, or the projection conv + BN (no activation) through the fused BN kernel."""
     if isinstance(sc, nn.Identity):
         return x
-    return batch_norm_act(sc[0](x), sc[1], relu=False)
+    return batch_norm_act(conv2d(x, sc[0]), sc[1], relu=False)
 
 
 class BasicBlock(nn.Module):
@@ -50,8 +54,8 @@ class BasicBlock(nn.Module):
             self.shortcut = nn.Sequential(nn.Conv2d(cin, cout, 1, stride, bias=False), nn.BatchNorm2d(cout))
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
-        out = batch_norm_act(self.conv1(x), self.bn1)
-        return batch_norm_act(self.conv2(out), self.bn2, residual=_shortcut(self.shortcut, x))
+        out = batch_norm_act(conv2d(x, self.conv1), self.bn1)
+        return batch_norm_act(conv2d(out, self.conv2), self.bn2, residual=_shortcut(self.shortcut, x))
 
 
 class Bottleneck(nn.Module):
@@ -71,9 +75,9 @@ class Bottleneck(nn.Module):
             self.shortcut = nn.Sequential(nn.Conv2d(cin, cout, 1, stride, bias=False), nn.BatchNorm2d(cout))
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
-        out = batch_norm_act(self.conv1(x), self.bn1)
-        out = batch_norm_act(self.conv2(out), self.bn2)
-        return batch_norm_act(self.conv3(out), self.bn3, residual=_shortcut(self.shortcut, x))
+        out = batch_norm_act(conv2d(x, self.conv1), self.bn1)
+        out = batch_norm_act(conv2d(out, self.conv2), self.bn2)
+        return batch_norm_act(conv2d(out, self.conv3), self.bn3, residual=_shortcut(self.shortcut, x))
 
 
 class ResNet(FLModule):
@@ -127,7 +131,7 @@ class ResNet(FLModule):
             x = x.float().mul_(1.0 / 255.0)
         if x.is_cuda and _CHANNELS_LAST:
             x = x.contiguous(memory_format=torch.channels_last)
-        x = batch_norm_act(self.stem[0](x), self.stem[1])
+        x = batch_norm_act(conv2d(x, self.stem[0]), self.stem[1])
         if len(self.stem) > 3:
             x = self.stem[3](x)
         x = self.layer4(self.layer3(self.layer2(self.layer1(x))))

@@ -224,3 +224,4 @@ from p2pfl_amd.ops.fused import (  # noqa: E402
 )
 from p2pfl_amd.ops.fused import linear as linear_blas  # noqa: E402,F401  (hipBLASLt comparison path)
 from p2pfl_amd.ops.gemm import gemm, gemm_reference, linear, linear_gelu  # noqa: E402,F401
+from p2pfl_amd.ops.conv import conv2d  # noqa: E402,F401

@@ -1,0 +1,178 @@
+"""Implicit-GEMM 2-D convolution on the MFMA core (``csrc/conv.hip``).
+
+:func:`conv2d` runs a ``nn.Conv2d`` (no bias, groups 1) whose activations are
+channels-last bf16 and whose weight is a channels-last bf16 view (the
+learner's mixed-precision shadow arena, ``arena.py``) on the hand-written
+kernels: forward, input gradient and weight gradient are one launch each
+(a split-K launch reduces its K-slices itself: ``ops/splitk.py``).  The weight gradient
+comes back in the weight's own (O, kh, kw, C) layout, so autograd hands it to
+the optimizer without a relayout copy.
+
+Anything the kernels do not take -- CPU tensors, fp32 weights, channel
+counts that are not multiples of 64 on the reduction side (the 3-channel
+stem), groups, asymmetric stride/padding -- runs ``F.conv2d``.  The
+reference trains its convolutions through torch.nn.Conv2d
+(/root/reference/p2pfl/learning/pytorch/mnist_examples/models/cnn.py:55-62).
+"""
+
+from __future__ import annotations
+
+import os
+from typing import Tuple
+
+import torch
+import torch.nn.functional as F
+from torch import nn
+
+from p2pfl_amd.ops.splitk import IN_LAUNCH_MAX_SPLITS, counters, tiles_of
+
+# counters a test can read to prove the native path ran
+STATS = {"native_fwd": 0, "torch_fwd": 0}
+
+_DISABLED = os.environ.get("P2PFL_NATIVE_CONV", "1") == "0"
+# csrc/gemm.h variant bits per product (single LDS buffer for the gathers, double buffer for split-K wgrad)
+_V_FWD = int(os.environ.get("P2PFL_CONV_VARIANT_FWD", "10"))
+_V_DGRAD = int(os.environ.get("P2PFL_CONV_VARIANT_DGRAD", "10"))
+_V_WGRAD = int(os.environ.get("P2PFL_CONV_VARIANT_WGRAD", "2"))
+
+
+def _C():
+    from p2pfl_amd.ops import ext
+
+    return ext()
+
+
+def _sym(v) -> int:
+    if isinstance(v, (tuple, list)):
+        if len(set(v)) != 1:
+            return -1
+        return int(v[0])
+    return int(v)
+
+
+def out_hw(h: int, w: int, k: Tuple[int, int], stride: int, pad: int, dil: int) -> Tuple[int, int]:
+    return (h + 2 * pad - dil * (k[0] - 1) - 1) // stride + 1, (w + 2 * pad - dil * (k[1] - 1) - 1) // stride + 1
+
+
+def wgrad_splits(O: int, ncols: int, npix: int) -> int:
+    """Split the pixel reduction of a weight gradient until ~2 workgroups per CU."""
+    tiles = -(-O // 128) * -(-ncols // 128)
+    s = 1
+    while tiles * s < 512 and npix // (s * 2) >= 512 and s < 64:
+        s *= 2
+    return s
+
+
+def mn_splits(M: int, N: int, K: int) -> int:
+    """Split-K for a forward / input-gradient product whose output has few 128x128 tiles
+    (the 8x8 and 4x4 stages of a CIFAR ResNet): aim at one workgroup per CU, >= 256 deep."""
+    tiles = -(-M // 128) * -(-N // 128)
+    s = 1
+    while tiles * s < 256 and K // (s * 2) >= 256 and s < 16:
+        s *= 2
+    return s
+
+
+def _run_split(launch, rows: int, cols: int, s: int, out: torch.Tensor) -> None:
+    """``launch(target, splits, ws, counters)`` producing ``out``: directly, split-K reduced
+    in the launch, or split-K into fp32 slabs reduced by one ``slab_sum``."""
+    if s == 1:
+        launch(out, 1, None, None)
+        return
+    ws = torch.empty(s * rows * cols, dtype=torch.float32, device=out.device)
+    if s <= IN_LAUNCH_MAX_SPLITS:
+        launch(out, s, ws, counters(tiles_of(rows, cols), out.device))
+        return
+    launch(ws, s, None, None)
+    _C().slab_sum(ws.view(s, rows * cols), out.view(-1))
+
+
+def native_ok(x: torch.Tensor, conv: nn.Conv2d) -> bool:
+    from p2pfl_amd.ops import _gpu
+
+    if _DISABLED or not _gpu(x) or x.dim() != 4:
+        return False
+    w = conv.weight
+    if w.dtype != torch.bfloat16 or conv.bias is not None or conv.groups != 1 or conv.padding_mode != "zeros":
+        return False
+    if isinstance(conv.padding, str):
+        return False
+    stride, pad, dil = _sym(conv.stride), _sym(conv.padding), _sym(conv.dilation)
+    if stride not in (1, 2) or pad < 0 or dil < 1:
+        return False
+    O, C = w.shape[0], w.shape[1]
+    if C % 64 or O % 64:
+        return False
+    if not w.permute(0, 2, 3, 1).is_contiguous() or w.data_ptr() % 16:
+        return False
+    return x.shape[1] == C and x.is_contiguous(memory_format=torch.channels_last)
+
+
+class _Conv2dNHWC(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, w, stride, pad, dil):
+        if x.dtype != torch.bfloat16:
+            x = x.to(torch.bfloat16)
+        x4 = x.permute(0, 2, 3, 1)
+        if not x4.is_contiguous() or x4.data_ptr() % 16:
+            x4 = x4.contiguous()
+        w4 = w.permute(0, 2, 3, 1)
+        N, H, W_, C = x4.shape
+        O, kh, kw = w4.shape[0], w4.shape[1], w4.shape[2]
+        OH, OW = out_hw(H, W_, (kh, kw), stride, pad, dil)
+        y4 = torch.empty((N, OH, OW, O), dtype=torch.bfloat16, device=x.device)
+        rows = N * OH * OW
+        _run_split(
+            lambda o, s, ws, cnt: _C().conv_fwd(x4, w4, stride, pad, dil, o, s, _V_FWD, ws, cnt),
+            rows, O, mn_splits(rows, O, kh * kw * C), y4,
+        )
+        ctx.save_for_backward(x4, w)
+        ctx.cfg = (stride, pad, dil)
+        return y4.permute(0, 3, 1, 2)
+
+    @staticmethod
+    def backward(ctx, dy):
+        x4, w = ctx.saved_tensors
+        stride, pad, dil = ctx.cfg
+        if dy.dtype != torch.bfloat16:
+            dy = dy.to(torch.bfloat16)
+        dy4 = dy.permute(0, 2, 3, 1)
+        if not dy4.is_contiguous() or dy4.data_ptr() % 16:
+            dy4 = dy4.contiguous()
+        w4 = w.permute(0, 2, 3, 1)
+        C = _C()
+        dx = dw = None
+        if ctx.needs_input_grad[0]:
+            dx4 = torch.empty(x4.shape, dtype=torch.bfloat16, device=x4.device)
+            shape = list(x4.shape)
+            O, kh, kw = w4.shape[0], w4.shape[1], w4.shape[2]
+            rows = shape[0] * shape[1] * shape[2]
+            _run_split(
+                lambda o, s, ws, cnt: C.conv_dgrad(dy4, w4, stride, pad, dil, o, shape, s, _V_DGRAD, ws, cnt),
+                rows, shape[3], mn_splits(rows, shape[3], kh * kw * O), dx4,
+            )
+            dx = dx4.permute(0, 3, 1, 2)
+        if ctx.needs_input_grad[1]:
+            O, kh, kw, Cin = w4.shape
+            npix = dy4.shape[0] * dy4.shape[1] * dy4.shape[2]
+            dw4 = torch.empty((O, kh, kw, Cin), dtype=w.dtype, device=w.device)
+            _run_split(
+                lambda o, s, ws, cnt: C.conv_wgrad(dy4, x4, kh, kw, stride, pad, dil, o, s, _V_WGRAD, ws, cnt),
+                O, kh * kw * Cin, wgrad_splits(O, kh * kw * Cin, npix), dw4,
+            )
+            dw = dw4.permute(0, 3, 1, 2)
+        return dx, dw, None, None, None
+
+
+def conv2d(x: torch.Tensor, conv: nn.Conv2d) -> torch.Tensor:
+    """``conv(x)`` on the implicit-GEMM kernels when :func:`native_ok`, else ``F.conv2d``."""
+    if native_ok(x, conv):
+        STATS["native_fwd"] += 1
+        return _Conv2dNHWC.apply(x, conv.weight, _sym(conv.stride), _sym(conv.padding), _sym(conv.dilation))
+    STATS["torch_fwd"] += 1
+    return conv(x)
+
+
+def conv2d_reference(x: torch.Tensor, w: torch.Tensor, stride: int, pad: int, dil: int) -> torch.Tensor:
+    """fp32 definition used by the numerics tests."""
+    return F.conv2d(x.float(), w.float(), None, stride, pad, dil)

@@ -22,6 +22,8 @@ from typing import Optional, Tuple
 import torch
 import torch.nn.functional as F
 
+from p2pfl_amd.ops.splitk import IN_LAUNCH_MAX_SPLITS, counters, tiles_of
+
 
 def _C():
     from p2pfl_amd.ops import ext
@@ -103,31 +105,31 @@ def gemm(
 
     ``a`` is [M, K] if ``a_kmajor`` else [K, M]; ``b`` is [N, K] if
     ``b_kmajor`` else [K, N].  ``z`` is the GELU pre-activation (``want_z``).
-    With ``splits > 1`` the K-slices' fp32 partials are summed into ``C``.
+    With ``splits > 1`` the K-slices' fp32 partials are summed inside the
+    launch by the last slice to finish each tile (``ops/splitk.py``).
     """
     M = a.shape[0] if a_kmajor else a.shape[1]
     N = b.shape[0] if b_kmajor else b.shape[1]
     dev = a.device
     if splits > 1:
+        if out is None:
+            out = torch.empty((M, N), dtype=out_dtype, device=dev)
+        z = torch.empty((M, N), dtype=torch.bfloat16, device=dev) if (gelu and want_z) else None
+        ws = torch.empty(splits * M * N, dtype=torch.float32, device=dev)
+        v = _variant(a_kmajor, splits)
+        if splits <= IN_LAUNCH_MAX_SPLITS:  # the last slice of each tile reduces it in the launch
+            _C().gemm(a, b, a_kmajor, b_kmajor, out, bias, gelu, z, residual, splits, v, ws, counters(tiles_of(M, N), dev))
+            return out, z
         if bias is not None or gelu or residual is not None:
-            raise ValueError("split-K GEMM has no epilogue")
-        slabs = torch.empty((splits, M, N), dtype=torch.float32, device=dev)
-        _C().gemm(a, b, a_kmajor, b_kmajor, slabs, None, False, None, None, splits, _variant(a_kmajor, splits))
-        out = torch.empty((M, N), dtype=out_dtype, device=dev) if out is None else out
-        _sum_slabs(slabs, out)
-        return out, None
+            raise ValueError("a split-K GEMM with more than 4 slices has no epilogue")
+        _C().gemm(a, b, a_kmajor, b_kmajor, ws, None, False, None, None, splits, v)
+        _C().slab_sum(ws.view(splits, M * N), out.view(-1))
+        return out, z
     if out is None:
         out = torch.empty((M, N), dtype=out_dtype, device=dev)
     z = torch.empty((M, N), dtype=torch.bfloat16, device=dev) if (gelu and want_z) else None
     _C().gemm(a, b, a_kmajor, b_kmajor, out, bias, gelu, z, residual, 1, _variant(a_kmajor, 1))
     return out, z
-
-
-def _sum_slabs(slabs: torch.Tensor, out: torch.Tensor) -> None:
-    """out = sum over dim 0 of the fp32 split-K slabs: one pass of the weighted-sum
-    kernel (unit weights, fp32 accumulation, bf16/fp32 out)."""
-    s = slabs.shape[0]
-    _C().weighted_sum(list(slabs.view(s, -1)), [1.0] * s, out.view(-1))
 
 
 def _wgrad(dy2: torch.Tensor, x2: torch.Tensor, dtype: torch.dtype) -> torch.Tensor:

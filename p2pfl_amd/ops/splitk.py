@@ -1,0 +1,45 @@
+"""Tile-arrival counters for split-K launches that reduce inside the kernel.
+
+A split-K GEMM / convolution launch with counters (``csrc/gemm_core.h``)
+needs one int per 128 x 128 output tile, zero when the launch starts; the
+last K-slice to reach a tile reduces it and resets the counter, so the
+array is zero again when the kernel ends.  Launches on one stream are
+serialised, so a per-stream ring of counters is enough: each call takes the
+next free slice, and calls captured into a HIP graph keep distinct slices
+(the graph's capture stream has its own ring) -- two graphs replayed
+concurrently on different streams never share a counter.
+"""
+
+from __future__ import annotations
+
+from typing import Dict, List, Tuple
+
+import torch
+
+# Up to this many K-slices the last-arriving slice reduces a tile inside the
+# launch (<= 256 KB of partials per tile); beyond it one wide slab reduction
+# (csrc/conv.hip slab_sum) over the whole chip is faster than one workgroup
+# reading every slice of its tile.
+IN_LAUNCH_MAX_SPLITS = 4
+RING = 1 << 18  # counters per stream (1 MiB)
+_RINGS: Dict[Tuple[int, int], List] = {}
+
+
+def counters(tiles: int, device: torch.device) -> torch.Tensor:
+    """A zeroed int32 slice of ``tiles`` counters for one launch on the current stream."""
+    if tiles > RING:
+        raise ValueError(f"split-K launch with {tiles} tiles exceeds the counter ring")
+    stream = torch.cuda.current_stream(device)
+    key = (stream.device_index, stream.cuda_stream)
+    ring = _RINGS.get(key)
+    if ring is None:
+        ring = _RINGS[key] = [torch.zeros(RING, dtype=torch.int32, device=device), 0]
+    if ring[1] + tiles > RING:
+        ring[1] = 0
+    off = ring[1]
+    ring[1] += (tiles + 15) // 16 * 16
+    return ring[0][off : off + tiles]
+
+
+def tiles_of(rows: int, cols: int) -> int:
+    return -(-rows // 128) * -(-cols // 128)

@@ -1,0 +1,184 @@
+"""Implicit-GEMM convolutions (csrc/conv.hip) vs an fp32 PyTorch reference on the same bf16 operands."""
+
+from __future__ import annotations
+
+import pytest
+import torch
+import torch.nn.functional as F
+from torch import nn
+
+from p2pfl_amd import ops
+from p2pfl_amd.ops import conv as conv_ops
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(autouse=True)
+def _require_ext():
+    ops.ext()
+
+
+def _operands(N, C, H, W, O, k, seed, integer=False):
+    g = torch.Generator(device="cuda").manual_seed(seed)
+    if integer:  # exact in bf16 and fp32: any mis-addressed tap shows as an exact mismatch
+        x = torch.randint(-2, 3, (N, C, H, W), device="cuda", generator=g).float()
+        w = torch.randint(-2, 3, (O, C, k, k), device="cuda", generator=g).float()
+    else:
+        x = torch.randn(N, C, H, W, device="cuda", generator=g)
+        w = torch.randn(O, C, k, k, device="cuda", generator=g) / (C * k * k) ** 0.5
+    xb = x.to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    wb = w.to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    return xb, wb
+
+
+CASES = [
+    # N, C, H, W, O, k, stride, pad, dil
+    (2, 64, 8, 8, 64, 3, 1, 1, 1),
+    (2, 64, 8, 8, 128, 3, 2, 1, 1),
+    (3, 128, 7, 5, 64, 3, 1, 1, 1),
+    (2, 64, 9, 9, 128, 1, 2, 0, 1),
+    (2, 128, 6, 6, 64, 1, 1, 0, 1),
+    (1, 64, 10, 10, 64, 3, 1, 2, 2),
+    (4, 64, 32, 32, 64, 3, 1, 1, 1),
+    (2, 256, 4, 4, 512, 3, 2, 1, 1),
+]
+
+
+def _ref(x, w, s, p, d):
+    return F.conv2d(x.float(), w.float(), None, s, p, d)
+
+
+@pytest.mark.parametrize("N,C,H,W,O,k,s,p,d", CASES)
+def test_conv_fwd_exact_integers(N, C, H, W, O, k, s, p, d):
+    x, w = _operands(N, C, H, W, O, k, seed=N + C + H + O, integer=True)
+    y4 = torch.empty((N,) + conv_ops.out_hw(H, W, (k, k), s, p, d) + (O,), dtype=torch.bfloat16, device="cuda")
+    ops.ext().conv_fwd(x.permute(0, 2, 3, 1), w.permute(0, 2, 3, 1), s, p, d, y4, 1)
+    ref = _ref(x, w, s, p, d)
+    # integer sums up to |k*k*C*4| <= 256 per term class: exact in fp32, and bf16 output holds them when |y| <= 256
+    torch.testing.assert_close(y4.permute(0, 3, 1, 2).float(), ref.to(torch.bfloat16).float(), atol=0, rtol=0)
+
+
+@pytest.mark.parametrize("N,C,H,W,O,k,s,p,d", CASES)
+def test_conv_autograd_vs_fp32(N, C, H, W, O, k, s, p, d):
+    x, w = _operands(N, C, H, W, O, k, seed=7 * N + C + W + k)
+    conv = nn.Conv2d(C, O, k, s, p, d, bias=False).cuda()
+    conv.weight.data = w  # bf16 channels-last view, as the mixed-precision arena provides
+    xg = x.clone().requires_grad_()
+    before = conv_ops.STATS["native_fwd"]
+    y = ops.conv2d(xg, conv)
+    assert conv_ops.STATS["native_fwd"] == before + 1, "native path not taken"
+    g = torch.randn(y.shape, device="cuda").to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    y.backward(g)
+    xr = x.float().requires_grad_()
+    wr = w.float().requires_grad_()
+    yr = _ref(xr, wr, s, p, d)
+    yr.backward(g.float())
+    torch.testing.assert_close(y.float(), yr, atol=3e-2, rtol=2e-2)
+    torch.testing.assert_close(xg.grad.float(), xr.grad, atol=3e-2, rtol=2e-2)
+    scale = wr.grad.abs().max().item()
+    torch.testing.assert_close(conv.weight.grad.float(), wr.grad, atol=1e-2 * scale, rtol=2e-2)
+    # gradient keeps the weight's channels-last layout (no relayout copy for the optimizer)
+    assert conv.weight.grad.permute(0, 2, 3, 1).is_contiguous()
+
+
+@pytest.mark.parametrize("splits", [2, 16])
+def test_conv_fwd_dgrad_split_k(splits):
+    N, C, H, W, O, k = 2, 128, 4, 4, 256, 3
+    x, w = _operands(N, C, H, W, O, k, seed=splits, integer=True)
+    x4, w4 = x.permute(0, 2, 3, 1), w.permute(0, 2, 3, 1)
+    slabs = torch.empty(splits, N * H * W * O, device="cuda")
+    ops.ext().conv_fwd(x4, w4, 1, 1, 1, slabs, splits)
+    ref = _ref(x, w, 1, 1, 1)
+    torch.testing.assert_close(slabs.sum(0).view(N, H, W, O).permute(0, 3, 1, 2), ref, atol=0, rtol=0)
+    dy = torch.randint(-2, 3, (N, O, H, W), device="cuda").to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    slabs = torch.empty(splits, N * H * W * C, device="cuda")
+    ops.ext().conv_dgrad(dy.permute(0, 2, 3, 1), w4, 1, 1, 1, slabs, [N, H, W, C], splits)
+    xr = x.float().requires_grad_()
+    _ref(xr, w, 1, 1, 1).backward(dy.float())
+    torch.testing.assert_close(slabs.sum(0).view(N, H, W, C).permute(0, 3, 1, 2), xr.grad, atol=0, rtol=0)
+
+
+@pytest.mark.parametrize("splits", [2, 8, 32])
+def test_conv_split_k_in_launch_reduction(splits):
+    """Split-K reduced by the last-arriving slice: equals the slab sum, and the counters end at zero."""
+    from p2pfl_amd.ops.splitk import tiles_of
+
+    N, C, H, W, O, k = 4, 128, 8, 8, 256, 3
+    x, w = _operands(N, C, H, W, O, k, seed=3 * splits, integer=True)
+    x4, w4 = x.permute(0, 2, 3, 1), w.permute(0, 2, 3, 1)
+    rows = N * H * W
+    cnt = torch.zeros(tiles_of(rows, O), dtype=torch.int32, device="cuda")
+    ws = torch.empty(splits * rows * O, device="cuda")
+    y4 = torch.empty(N, H, W, O, device="cuda", dtype=torch.bfloat16)
+    for _ in range(3):  # counters are reusable launch after launch
+        ops.ext().conv_fwd(x4, w4, 1, 1, 1, y4, splits, 10, ws, cnt)
+        ref = _ref(x, w, 1, 1, 1)
+        torch.testing.assert_close(y4.permute(0, 3, 1, 2).float(), ref.to(torch.bfloat16).float(), atol=0, rtol=0)
+        assert int(cnt.abs().sum()) == 0
+    dy = torch.randint(-2, 3, (N, O, H, W), device="cuda").to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    dx4 = torch.empty(N, H, W, C, device="cuda", dtype=torch.bfloat16)
+    cnt = torch.zeros(tiles_of(rows, C), dtype=torch.int32, device="cuda")
+    ops.ext().conv_dgrad(dy.permute(0, 2, 3, 1), w4, 1, 1, 1, dx4, [N, H, W, C], splits, 10, ws, cnt)
+    xr = x.float().requires_grad_()
+    wr = w.float().requires_grad_()
+    _ref(xr, wr, 1, 1, 1).backward(dy.float())
+    torch.testing.assert_close(dx4.permute(0, 3, 1, 2).float(), xr.grad.to(torch.bfloat16).float(), atol=0, rtol=0)
+    dw4 = torch.empty(O, k, k, C, device="cuda", dtype=torch.float32)
+    cnt = torch.zeros(tiles_of(O, k * k * C), dtype=torch.int32, device="cuda")
+    ws = torch.empty(splits * O * k * k * C, device="cuda")
+    ops.ext().conv_wgrad(dy.permute(0, 2, 3, 1), x4, k, k, 1, 1, 1, dw4, splits, 2, ws, cnt)
+    torch.testing.assert_close(dw4, wr.grad.permute(0, 2, 3, 1), atol=0, rtol=0)
+    assert int(cnt.abs().sum()) == 0
+
+
+@pytest.mark.parametrize("splits", [1, 2, 8, 64])
+def test_conv_wgrad_split_k(splits):
+    N, C, H, W, O, k = 8, 64, 16, 16, 64, 3
+    x, w = _operands(N, C, H, W, O, k, seed=splits)
+    dy = torch.randn(N, O, H, W, device="cuda").to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    n = O * k * k * C
+    out = torch.empty((splits, n) if splits > 1 else (O, k, k, C), dtype=torch.float32, device="cuda")
+    ops.ext().conv_wgrad(dy.permute(0, 2, 3, 1), x.permute(0, 2, 3, 1), k, k, 1, 1, 1, out, splits)
+    dw = out.sum(0) if splits > 1 else out.view(-1)
+    xr = x.float().requires_grad_()
+    wr = w.float().requires_grad_()
+    _ref(xr, wr, 1, 1, 1).backward(dy.float())
+    torch.testing.assert_close(dw.view(O, k, k, C), wr.grad.permute(0, 2, 3, 1), atol=5e-3 * wr.grad.abs().max().item(), rtol=1e-3)
+
+
+def test_slab_sum():
+    slabs = torch.randn(5, 4096, device="cuda")
+    out = torch.empty(4096, device="cuda", dtype=torch.bfloat16)
+    ops.ext().slab_sum(slabs, out)
+    torch.testing.assert_close(out.float(), slabs.sum(0).to(torch.bfloat16).float(), atol=1e-2, rtol=1e-2)
+
+
+def test_conv_rejects_bad_shapes():
+    x = torch.zeros(1, 8, 8, 48, device="cuda", dtype=torch.bfloat16)  # C % 64 != 0
+    w = torch.zeros(64, 3, 3, 48, device="cuda", dtype=torch.bfloat16)
+    y = torch.empty(1, 8, 8, 64, device="cuda", dtype=torch.bfloat16)
+    with pytest.raises(RuntimeError):
+        ops.ext().conv_fwd(x, w, 1, 1, 1, y, 1)
+
+
+def test_resnet18_block_runs_native_convs():
+    """A ResNet-18 train step through the learner's mixed-precision arena takes the native conv path."""
+    from p2pfl_amd.learning.arena import ModuleArena
+    from p2pfl_amd.models.resnet import ResNet18
+
+    torch.manual_seed(0)
+    model = ResNet18(num_classes=10).cuda()
+    arena = ModuleArena(model, device=torch.device("cuda"), compute_dtype=torch.bfloat16,
+                        channels_last_names=model.channels_last_parameter_names())
+    x = torch.randint(0, 255, (8, 3, 32, 32), device="cuda", dtype=torch.uint8)
+    before = dict(conv_ops.STATS)
+    with torch.autocast("cuda", dtype=torch.bfloat16):
+        loss = model(x).float().logsumexp(1).mean()
+    loss.backward()
+    assert conv_ops.STATS["native_fwd"] - before["native_fwd"] >= 19  # all but the stem
+    assert conv_ops.STATS["torch_fwd"] - before["torch_fwd"] == 1  # the 3-channel stem
+    assert torch.isfinite(loss)
+    assert arena.shadow is not None
+    for name, p in model.named_parameters():
+        if p.dim() == 4:
+            assert p.grad is not None and torch.isfinite(p.grad).all(), name

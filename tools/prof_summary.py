@@ -1,43 +1,44 @@
-"""Summarise rocprofv3 CSV output as a markdown table.
+"""Summarise a rocprofv3 --kernel-trace --stats output directory into markdown and drop the raw trace.
 
-    python tools/prof_summary.py <kernel_stats.csv> [top]
-    python tools/prof_summary.py <kernel_trace.csv> [top] --tail-ms T   # only kernels in the last T ms
-                                                                         # of the trace (steady state, no warmup)
+    python tools/prof_summary.py gpurun_out/<dir> [--keep-trace] [--top 30]
+
+Writes <dir>.md: kernel-time table (top N by total time), launch count,
+total kernel time, and the busy window of the trace; removes
+run_kernel_trace.csv unless --keep-trace (traces of whole benchmarks exceed
+the gpurun copy-back limit).
 """
+import argparse
 import csv
-import sys
-from collections import defaultdict
+import os
 
-
-def main() -> None:
-    args = [a for a in sys.argv[1:] if not a.startswith("--")]
-    tail = None
-    if "--tail-ms" in sys.argv:
-        tail = float(sys.argv[sys.argv.index("--tail-ms") + 1])
-        args = [a for a in args if a != sys.argv[sys.argv.index("--tail-ms") + 1]]
-    path, top = args[0], int(args[1]) if len(args) > 1 else 20
-    rows = list(csv.DictReader(open(path)))
-    agg = defaultdict(lambda: [0, 0.0])
-    if "Start_Timestamp" in rows[0]:
-        end = max(int(r["End_Timestamp"]) for r in rows)
-        lo = end - tail * 1e6 if tail else 0
-        sel = [r for r in rows if int(r["Start_Timestamp"]) >= lo]
-        for r in sel:
-            a = agg[r["Kernel_Name"]]
-            a[0] += 1
-            a[1] += int(r["End_Timestamp"]) - int(r["Start_Timestamp"])
-        span = (end - min(int(r["Start_Timestamp"]) for r in sel)) / 1e6 if sel else 0.0
-        hdr = f"window: last {tail} ms of the trace (wall span {span:.2f} ms)" if tail else "whole trace"
-    else:
-        for r in rows:
-            agg[r["Name"]] = [int(r["Calls"]), float(r["TotalDurationNs"])]
-        hdr = "whole run (rocprofv3 --stats)"
-    tot = sum(v[1] for v in agg.values())
-    print(f"{hdr}: kernel time {tot / 1e6:.2f} ms over {sum(v[0] for v in agg.values())} launches\n")
-    print("| kernel | calls | total ms | avg us | % |\n|---|---:|---:|---:|---:|")
-    for name, (n, ns) in sorted(agg.items(), key=lambda kv: -kv[1][1])[:top]:
-        print(f"| `{name[:150]}` | {n} | {ns / 1e6:.3f} | {ns / n / 1e3:.2f} | {100 * ns / tot:.1f} |")
-
-
-if __name__ == "__main__":
-    main()
+ap = argparse.ArgumentParser()
+ap.add_argument("dir")
+ap.add_argument("--keep-trace", action="store_true")
+ap.add_argument("--top", type=int, default=30)
+args = ap.parse_args()
+d = args.dir.rstrip("/")
+stats = list(csv.DictReader(open(os.path.join(d, "run_kernel_stats.csv"))))
+tot = sum(float(r["TotalDurationNs"]) for r in stats)
+calls = sum(int(r["Calls"]) for r in stats)
+lines = [f"# rocprofv3 kernel stats: {os.path.basename(d)}", "",
+         f"total kernel time {tot / 1e6:.2f} ms over {calls} launches", ""]
+trace = os.path.join(d, "run_kernel_trace.csv")
+if os.path.exists(trace):
+    t0 = t1 = None
+    for r in csv.DictReader(open(trace)):
+        s, e = int(r["Start_Timestamp"]), int(r["End_Timestamp"])
+        t0 = s if t0 is None else min(t0, s)
+        t1 = e if t1 is None else max(t1, e)
+    if t0 is not None:
+        lines += [f"trace span {(t1 - t0) / 1e6:.1f} ms", ""]
+lines += ["| kernel | calls | total ms | avg us | % |", "|---|---:|---:|---:|---:|"]
+for r in stats[: args.top]:
+    name = r["Name"].replace("|", "/")
+    if len(name) > 150:
+        name = name[:150] + "..."
+    lines.append(f"| `{name}` | {r['Calls']} | {float(r['TotalDurationNs']) / 1e6:.3f} | "
+                 f"{float(r['AverageNs']) / 1e3:.2f} | {float(r['TotalDurationNs']) / tot * 100:.1f} |")
+open(d + ".md", "w").write("\n".join(lines) + "\n")
+print("\n".join(lines[:40]))
+if os.path.exists(trace) and not args.keep_trace:
+    os.remove(trace)
