@@ -72,7 +72,7 @@ struct ConvFwdA {
     const int ih = st.ih0[i] + ky * dil, iw = st.iw0[i] + kx * dil;
     const bool ok = unsigned(ih) < unsigned(H) && unsigned(iw) < unsigned(W);
     return ok ? static_cast<const void*>(x + st.base[i] + (int64_t(ky * dil) * W + kx * dil) * C + cb)
-              : static_cast<const void*>(g_zero16);
+              : zero_chunk();
   }
 };
 
@@ -113,7 +113,7 @@ struct ConvDgradA {
     }
     ok = ok && oh < OH && ow < OW;
     return ok ? static_cast<const void*>(dy + st.nbase[i] + (int64_t(oh) * OW + ow) * O + ob)
-              : static_cast<const void*>(g_zero16);
+              : zero_chunk();
   }
 };
 
@@ -133,7 +133,7 @@ struct ConvDgradB {
   P2_DEVICE const void* src(const St& st, int i, int k0, int) const {
     const int tap = k0 / O, ob = k0 - tap * O;  // wave-uniform
     const int o = ob + 16 * i + st.kr;
-    return st.col ? static_cast<const void*>(st.col + (int64_t(o) * T + tap) * C) : static_cast<const void*>(g_zero16);
+    return st.col ? static_cast<const void*>(st.col + (int64_t(o) * T + tap) * C) : zero_chunk();
   }
 };
 
@@ -159,12 +159,12 @@ struct ConvWgradB {
     const int ih = oh * stride + st.kyd, iw = owi * stride + st.kxd;
     const bool ok = m < M && unsigned(ih) < unsigned(H) && unsigned(iw) < unsigned(W);
     return ok ? static_cast<const void*>(x + ((int64_t(n) * H + ih) * W + iw) * C + st.c)
-              : static_cast<const void*>(g_zero16);
+              : zero_chunk();
   }
 };
 
 template <int NBUF, class LA, class LB>
-__global__ __launch_bounds__(NT, 2) void conv_kernel(GemmParams p, LA la, LB lb, int tiles_m, int tiles_n) {
+__global__ __launch_bounds__(NT, NBUF == 1 ? 3 : 2) void conv_kernel(GemmParams p, LA la, LB lb, int tiles_m, int tiles_n) {
   __shared__ __attribute__((aligned(16))) char smem[NBUF * 2 * TILE];
   gemm_body<NBUF>(p, la, lb, tiles_m, tiles_n, smem);
 }

@@ -36,7 +36,7 @@
 namespace p2gemm {
 
 template <int NBUF, class LA, class LB>
-__global__ __launch_bounds__(NT, 2) void gemm_kernel(GemmParams p, LA la, LB lb, int tiles_m, int tiles_n) {
+__global__ __launch_bounds__(NT, NBUF == 1 ? 4 : 2) void gemm_kernel(GemmParams p, LA la, LB lb, int tiles_m, int tiles_n) {
   __shared__ __attribute__((aligned(16))) char smem[NBUF * 2 * TILE];  // [buf][A | B]
   gemm_body<NBUF>(p, la, lb, tiles_m, tiles_n, smem);
 }

@@ -25,8 +25,10 @@ def main() -> None:
     ap = argparse.ArgumentParser()
     ap.add_argument("--batch", type=int, default=32)
     ap.add_argument("--out", default=None)
+    ap.add_argument("--variants", default="10,10,2", help="csrc/gemm.h variant bits for fwd,dgrad,wgrad")
     args = ap.parse_args()
     C_ = ops.ext()
+    vf, vd, vw = (int(v) for v in args.variants.split(","))
     N = args.batch
     bf = torch.bfloat16
     # (name, C, H, O, k, stride, pad, count in ResNet-18)
@@ -55,9 +57,9 @@ def main() -> None:
         dw4 = torch.empty(O, k, k, C, device="cuda", dtype=bf)
         sf, sd, sw = mn_splits(N * OH * OW, O, k * k * C), mn_splits(N * H * H, C, k * k * O), wgrad_splits(O, k * k * C, N * OH * OW)
         mine = [
-            timeit(lambda: _run_split(lambda o, sp, ws, cnt: C_.conv_fwd(x4, w4, s, p, 1, o, sp, 10, ws, cnt), N * OH * OW, O, sf, y4)),
-            timeit(lambda: _run_split(lambda o, sp, ws, cnt: C_.conv_dgrad(dy4, w4, s, p, 1, o, [N, H, H, C], sp, 10, ws, cnt), N * H * H, C, sd, dx4)),
-            timeit(lambda: _run_split(lambda o, sp, ws, cnt: C_.conv_wgrad(dy4, x4, k, k, s, p, 1, o, sp, 2, ws, cnt), O, k * k * C, sw, dw4)),
+            timeit(lambda: _run_split(lambda o, sp, ws, cnt: C_.conv_fwd(x4, w4, s, p, 1, o, sp, vf, ws, cnt), N * OH * OW, O, sf, y4)),
+            timeit(lambda: _run_split(lambda o, sp, ws, cnt: C_.conv_dgrad(dy4, w4, s, p, 1, o, [N, H, H, C], sp, vd, ws, cnt), N * H * H, C, sd, dx4)),
+            timeit(lambda: _run_split(lambda o, sp, ws, cnt: C_.conv_wgrad(dy4, x4, k, k, s, p, 1, o, sp, vw, ws, cnt), O, k * k * C, sw, dw4)),
         ]
         xr = x.clone().requires_grad_()
         wr = w.clone().requires_grad_()

@@ -15,6 +15,7 @@ ap = argparse.ArgumentParser()
 ap.add_argument("dir")
 ap.add_argument("--keep-trace", action="store_true")
 ap.add_argument("--top", type=int, default=30)
+ap.add_argument("--window-ms", type=float, default=0.0, help="also tabulate the last N ms of the trace (steady state)")
 args = ap.parse_args()
 d = args.dir.rstrip("/")
 stats = list(csv.DictReader(open(os.path.join(d, "run_kernel_stats.csv"))))
@@ -31,6 +32,25 @@ if os.path.exists(trace):
         t1 = e if t1 is None else max(t1, e)
     if t0 is not None:
         lines += [f"trace span {(t1 - t0) / 1e6:.1f} ms", ""]
+    if args.window_ms > 0 and t1 is not None:
+        lo = t1 - int(args.window_ms * 1e6)
+        agg = {}
+        for r in csv.DictReader(open(trace)):
+            s_, e_ = int(r["Start_Timestamp"]), int(r["End_Timestamp"])
+            if s_ < lo:
+                continue
+            key = (r["Kernel_Name"], r["Grid_Size_X"])
+            agg.setdefault(key, []).append((e_ - s_) / 1e3)
+        wt = sum(sum(v) for v in agg.values())
+        lines += [f"## steady-state window: last {args.window_ms:.0f} ms -- kernel time {wt / 1e3:.2f} ms, "
+                  f"{sum(len(v) for v in agg.values())} launches", "",
+                  "| kernel | grid | calls | total ms | median us |", "|---|---:|---:|---:|---:|"]
+        for (name, grid), v in sorted(agg.items(), key=lambda kv: -sum(kv[1]))[: args.top * 2]:
+            v.sort()
+            nm = name.replace("|", "/")
+            nm = nm[:110] + "..." if len(nm) > 110 else nm
+            lines.append(f"| `{nm}` | {grid} | {len(v)} | {sum(v) / 1e3:.3f} | {v[len(v) // 2]:.2f} |")
+        lines.append("")
 lines += ["| kernel | calls | total ms | avg us | % |", "|---|---:|---:|---:|---:|"]
 for r in stats[: args.top]:
     name = r["Name"].replace("|", "/")
