@@ -90,6 +90,13 @@ void conv_adam(const float* wslab1, const float* wslab2, const float* gb, int B,
                float* gdump, uint16_t* w2r, uint16_t* w2q, Offsets off, const int* adam_t, int t_off, AdamCfg cfg,
                hipStream_t s);
 
+// conv_adam and fc1_wgrad_adam in one launch (run after conv2_bwd): the conv
+// reduction + Adam blocks hide behind the HBM-bound FC1 Adam stream.
+void fc1_conv_adam(const uint16_t* dH, const uint16_t* a1, int mrows, const float* wslab1, const float* wslab2,
+                   const float* gb, int B, float* params, float* m, float* v, float* gdump, uint16_t* w1bf,
+                   uint16_t* w1tbf, uint16_t* w2r, uint16_t* w2q, Offsets off, const int* adam_t, int t_off,
+                   AdamCfg cfg, hipStream_t s);
+
 // Standalone packing of the bf16 shadows from fp32 params (after set_parameters).
 void pack_shadows(const float* params, Offsets off, uint16_t* w2r, uint16_t* w2q, uint16_t* w1bf, uint16_t* w1tbf,
                   hipStream_t s);

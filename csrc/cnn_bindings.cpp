@@ -184,6 +184,30 @@ void k_conv_adam(torch::Tensor wslab1, torch::Tensor wslab2, torch::Tensor gb, i
                    ptr<int>(adam_t, torch::kInt32, 1, "adam_t", 4), int(t_off), cfg(lr, b1, b2, eps, wd), stream());
 }
 
+void k_fc1_conv_adam(torch::Tensor dH, torch::Tensor a1, int64_t mrows, torch::Tensor wslab1, torch::Tensor wslab2,
+                     torch::Tensor gb, int64_t B, torch::Tensor params, torch::Tensor m, torch::Tensor v,
+                     c10::optional<torch::Tensor> gdump, torch::Tensor w1bf, torch::Tensor w1tbf, torch::Tensor w2r,
+                     torch::Tensor w2q, std::vector<int64_t> off, torch::Tensor adam_t, int64_t t_off, double lr,
+                     double b1, double b2, double eps, double wd) {
+  const c10::DeviceGuard g(params.device());
+  check_batch(int(B), int(mrows));
+  Offsets o = offsets(off);
+  const int64_t n = params_end(o);
+  p2cnn::fc1_conv_adam(
+      reinterpret_cast<uint16_t*>(ptr<at::BFloat16>(dH, torch::kBFloat16, mrows * 2048, "dH")),
+      reinterpret_cast<uint16_t*>(ptr<at::BFloat16>(a1, torch::kBFloat16, mrows * 3136, "a1")), int(mrows),
+      ptr<float>(wslab1, torch::kFloat32, B * p2cnn::kDgTiles * p2cnn::kSlab1, "wslab1"),
+      ptr<float>(wslab2, torch::kFloat32, p2cnn::wgrad_groups(int(B)) * int64_t(p2cnn::kSlab2), "wslab2"),
+      ptr<float>(gb, torch::kFloat32, B * 3136, "gb"), int(B), ptr<float>(params, torch::kFloat32, n, "params"),
+      ptr<float>(m, torch::kFloat32, n, "m"), ptr<float>(v, torch::kFloat32, n, "v"),
+      optr<float>(gdump, torch::kFloat32, n, "gdump"),
+      reinterpret_cast<uint16_t*>(ptr<at::BFloat16>(w1bf, torch::kBFloat16, 2048 * 3136, "w1bf")),
+      reinterpret_cast<uint16_t*>(ptr<at::BFloat16>(w1tbf, torch::kBFloat16, 2048 * 3136, "w1tbf")),
+      reinterpret_cast<uint16_t*>(ptr<at::BFloat16>(w2r, torch::kBFloat16, 51200, "w2r")),
+      reinterpret_cast<uint16_t*>(ptr<at::BFloat16>(w2q, torch::kBFloat16, 51200, "w2q")), o,
+      ptr<int>(adam_t, torch::kInt32, 1, "adam_t", 4), int(t_off), cfg(lr, b1, b2, eps, wd), stream());
+}
+
 void k_pack_shadows(torch::Tensor params, std::vector<int64_t> off, torch::Tensor w2r, torch::Tensor w2q,
                     torch::Tensor w1bf, torch::Tensor w1tbf) {
   const c10::DeviceGuard g(params.device());
@@ -213,5 +237,6 @@ void register_cnn(pybind11::module& m) {
   c.def("fc1_wgrad_adam", &k_fc1_wgrad_adam);
   c.def("conv2_bwd", &k_conv2_bwd);
   c.def("conv_adam", &k_conv_adam);
+  c.def("fc1_conv_adam", &k_fc1_conv_adam);
   c.def("pack_shadows", &k_pack_shadows);
 }

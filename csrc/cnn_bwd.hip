@@ -219,23 +219,30 @@ void route_fc2(const uint16_t* dH, const uint16_t* w1t, const uint8_t* am2, int 
 //    tools/lab/fc1_lab.hip.)
 // ---------------------------------------------------------------------------
 template <int MR>
-__global__ __launch_bounds__(256) void fc1_wgrad_adam_kernel(const uint16_t* __restrict__ dH, const uint16_t* __restrict__ a1,
-                                               float* __restrict__ p, float* __restrict__ m, float* __restrict__ v,
-                                               float* __restrict__ gdump, uint16_t* __restrict__ w1bf,
-                                               uint16_t* __restrict__ w1tbf, Offsets off,
-                                               const int* __restrict__ adam_t, int t_off, AdamCfg cfg) {
-  constexpr int P = MR + 8;
-  constexpr int GP = 132;  // fp32 pitch of the gradient tile
-  constexpr int kStage = (32 + 128) * P * 2;
-  constexpr int kGrad = 32 * GP * 4;
-  __shared__ __attribute__((aligned(16))) char smem[kStage > kGrad ? kStage : kGrad];
-  __shared__ __attribute__((aligned(16))) uint16_t tr[128][40];
+struct Fc1Lds {
+  static constexpr int P = MR + 8;
+  static constexpr int GP = 132;  // fp32 pitch of the gradient tile
+  static constexpr int kStage = (32 + 128) * P * 2;
+  static constexpr int kGrad = 32 * GP * 4;
+  static constexpr int kMain = kStage > kGrad ? kStage : kGrad;
+  static constexpr int kBytes = kMain + 128 * 40 * 2;  // + the transposed bf16 tile
+};
+
+template <int MR>
+P2_DEVICE void fc1_wgrad_adam_body(int bx, int by, const uint16_t* __restrict__ dH, const uint16_t* __restrict__ a1,
+                                   float* __restrict__ p, float* __restrict__ m, float* __restrict__ v,
+                                   float* __restrict__ gdump, uint16_t* __restrict__ w1bf,
+                                   uint16_t* __restrict__ w1tbf, const Offsets& off,
+                                   const int* __restrict__ adam_t, int t_off, const AdamCfg& cfg, char* smem) {
+  constexpr int P = Fc1Lds<MR>::P;
+  constexpr int GP = Fc1Lds<MR>::GP;
+  uint16_t(*tr)[40] = reinterpret_cast<uint16_t(*)[40]>(smem + Fc1Lds<MR>::kMain);
   uint16_t(*sdh)[P] = reinterpret_cast<uint16_t(*)[P]>(smem);
   uint16_t(*sa1)[P] = reinterpret_cast<uint16_t(*)[P]>(smem + 32 * P * 2);
   float(*gt)[GP] = reinterpret_cast<float(*)[GP]>(smem);
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, r = lane & 31, h = lane >> 5;
-  const int n0 = blockIdx.y * 32;
-  const int kb = blockIdx.x * 128;
+  const int n0 = by * 32;
+  const int kb = bx * 128;
   // this thread's Adam elements: row nl, k = kb + kq + 32 j + [0, 4)
   const int nl = tid >> 3, kq = (tid & 7) * 4;
   float* pw = p + off.l1w;
@@ -270,7 +277,7 @@ __global__ __launch_bounds__(256) void fc1_wgrad_adam_kernel(const uint16_t* __r
   }
   __syncthreads();
   const AdamScal s = adam_scal(cfg, adam_t, t_off);
-  if (blockIdx.x == 0 && wave == 0 && lane < 32) {  // FC1 bias (reads sdh before the tile reuses it)
+  if (bx == 0 && wave == 0 && lane < 32) {  // FC1 bias (reads sdh before the tile reuses it)
     const int n = n0 + lane;
     float g = 0.f;
     for (int b = 0; b < MR; ++b) g += bf16_to_f32(sdh[lane][b]);
@@ -320,6 +327,17 @@ __global__ __launch_bounds__(256) void fc1_wgrad_adam_kernel(const uint16_t* __r
     if (k < kFeat)
       *reinterpret_cast<uint4*>(w1tbf + size_t(k) * kHid + n0 + q * 8) = *reinterpret_cast<const uint4*>(&tr[kl][q * 8]);
   }
+}
+
+template <int MR>
+__global__ __launch_bounds__(256) void fc1_wgrad_adam_kernel(const uint16_t* __restrict__ dH, const uint16_t* __restrict__ a1,
+                                                             float* __restrict__ p, float* __restrict__ m,
+                                                             float* __restrict__ v, float* __restrict__ gdump,
+                                                             uint16_t* __restrict__ w1bf, uint16_t* __restrict__ w1tbf,
+                                                             Offsets off, const int* __restrict__ adam_t, int t_off,
+                                                             AdamCfg cfg) {
+  __shared__ __attribute__((aligned(16))) char smem[Fc1Lds<MR>::kBytes];
+  fc1_wgrad_adam_body<MR>(blockIdx.x, blockIdx.y, dH, a1, p, m, v, gdump, w1bf, w1tbf, off, adam_t, t_off, cfg, smem);
 }
 
 void fc1_wgrad_adam(const uint16_t* dH, const uint16_t* a1, int mrows, float* params, float* m, float* v,
@@ -570,18 +588,19 @@ void conv2_bwd(const uint16_t* dc2m, const uint16_t* p1s, const uint8_t* am1, co
 // ---------------------------------------------------------------------------
 constexpr int kC1Blocks = kSlab1 / 16;  // 52
 
-__global__ __launch_bounds__(256) void conv_adam_kernel(const float* __restrict__ ws1, const float* __restrict__ ws2,
-                                                        const float* __restrict__ gb, int B, float* __restrict__ p,
-                                                        float* __restrict__ m, float* __restrict__ v,
-                                                        float* __restrict__ gdump, uint16_t* __restrict__ w2r,
-                                                        uint16_t* __restrict__ w2q, Offsets off,
-                                                        const int* __restrict__ adam_t, int t_off, AdamCfg cfg) {
-  __shared__ float g2[kTaps][kC1 + 1];
-  __shared__ float red[256];
+constexpr int kConvAdamLds = (kTaps * (kC1 + 1) + 256) * 4;
+
+P2_DEVICE void conv_adam_body(int blk, const float* __restrict__ ws1, const float* __restrict__ ws2,
+                              const float* __restrict__ gb, int B, float* __restrict__ p, float* __restrict__ m,
+                              float* __restrict__ v, float* __restrict__ gdump, uint16_t* __restrict__ w2r,
+                              uint16_t* __restrict__ w2q, const Offsets& off, const int* __restrict__ adam_t, int t_off,
+                              const AdamCfg& cfg, char* smem) {
+  float(*g2)[kC1 + 1] = reinterpret_cast<float(*)[kC1 + 1]>(smem);
+  float* red = reinterpret_cast<float*>(smem + kTaps * (kC1 + 1) * 4);
   const int tid = threadIdx.x;
   const AdamScal sc = adam_scal(cfg, adam_t, t_off);
-  if (blockIdx.x < kC2) {
-    const int oc = blockIdx.x, ng = wgrad_groups(B);
+  if (blk < kC2) {
+    const int oc = blk, ng = wgrad_groups(B);
     // Adam state of this thread's (up to 4) weights and the bias: loaded first,
     // independent of the reductions below
     float pr[4], mr[4], vr[4];
@@ -660,7 +679,7 @@ __global__ __launch_bounds__(256) void conv_adam_kernel(const float* __restrict_
       v[off.c2b + oc] = vb;
     }
   } else {
-    const int j = (blockIdx.x - kC2) * 16 + (tid & 15), q = tid >> 4;  // 16 row splits
+    const int j = (blk - kC2) * 16 + (tid & 15), q = tid >> 4;  // 16 row splits
     const int rows = B * kDgTiles;
     const int64_t e = j < kC1 * kTaps ? off.c1w + j : off.c1b + (j - kC1 * kTaps);
     float pe = 0.f, me = 0.f, ve = 0.f;
@@ -693,6 +712,55 @@ __global__ __launch_bounds__(256) void conv_adam_kernel(const float* __restrict_
       v[e] = ve;
     }
   }
+}
+
+__global__ __launch_bounds__(256) void conv_adam_kernel(const float* __restrict__ ws1, const float* __restrict__ ws2,
+                                                        const float* __restrict__ gb, int B, float* __restrict__ p,
+                                                        float* __restrict__ m, float* __restrict__ v,
+                                                        float* __restrict__ gdump, uint16_t* __restrict__ w2r,
+                                                        uint16_t* __restrict__ w2q, Offsets off,
+                                                        const int* __restrict__ adam_t, int t_off, AdamCfg cfg) {
+  __shared__ __attribute__((aligned(16))) char smem[kConvAdamLds];
+  conv_adam_body(blockIdx.x, ws1, ws2, gb, B, p, m, v, gdump, w2r, w2q, off, adam_t, t_off, cfg, smem);
+}
+
+// ---------------------------------------------------------------------------
+// 7+10 in one launch (after conv2_bwd): the 116 conv-parameter blocks first,
+// then the 1600 FC1 weight-gradient + Adam blocks.  The FC1 part streams the
+// 6.4M-parameter Adam state (HBM-bound, ~28 B per parameter); the conv part is
+// a latency-bound reduction -- sharing the launch hides the latter behind the
+// former instead of paying a kernel boundary and its tail.
+// ---------------------------------------------------------------------------
+template <int MR>
+__global__ __launch_bounds__(256) void fc1_conv_adam_kernel(
+    const uint16_t* __restrict__ dH, const uint16_t* __restrict__ a1, const float* __restrict__ ws1,
+    const float* __restrict__ ws2, const float* __restrict__ gb, int B, float* __restrict__ p, float* __restrict__ m,
+    float* __restrict__ v, float* __restrict__ gdump, uint16_t* __restrict__ w1bf, uint16_t* __restrict__ w1tbf,
+    uint16_t* __restrict__ w2r, uint16_t* __restrict__ w2q, Offsets off, const int* __restrict__ adam_t, int t_off,
+    AdamCfg cfg) {
+  constexpr int kLds = Fc1Lds<MR>::kBytes > kConvAdamLds ? Fc1Lds<MR>::kBytes : kConvAdamLds;
+  __shared__ __attribute__((aligned(16))) char smem[kLds];
+  constexpr int kCA = kC2 + kC1Blocks, kBx = (kFeat + 127) / 128;
+  const int j = blockIdx.x;
+  if (j < kCA) {
+    conv_adam_body(j, ws1, ws2, gb, B, p, m, v, gdump, w2r, w2q, off, adam_t, t_off, cfg, smem);
+    return;
+  }
+  const int f = j - kCA;
+  fc1_wgrad_adam_body<MR>(f % kBx, f / kBx, dH, a1, p, m, v, gdump, w1bf, w1tbf, off, adam_t, t_off, cfg, smem);
+}
+
+void fc1_conv_adam(const uint16_t* dH, const uint16_t* a1, int mrows, const float* wslab1, const float* wslab2,
+                   const float* gb, int B, float* params, float* m, float* v, float* gdump, uint16_t* w1bf,
+                   uint16_t* w1tbf, uint16_t* w2r, uint16_t* w2q, Offsets off, const int* adam_t, int t_off,
+                   AdamCfg cfg, hipStream_t s) {
+  const dim3 grid(kC2 + kC1Blocks + ((kFeat + 127) / 128) * (kHid / 32));
+  if (mrows == 32)
+    hipLaunchKernelGGL(fc1_conv_adam_kernel<32>, grid, dim3(256), 0, s, dH, a1, wslab1, wslab2, gb, B, params, m, v,
+                       gdump, w1bf, w1tbf, w2r, w2q, off, adam_t, t_off, cfg);
+  else
+    hipLaunchKernelGGL(fc1_conv_adam_kernel<64>, grid, dim3(256), 0, s, dH, a1, wslab1, wslab2, gb, B, params, m, v,
+                       gdump, w1bf, w1tbf, w2r, w2q, off, adam_t, t_off, cfg);
 }
 
 void conv_adam(const float* wslab1, const float* wslab2, const float* gb, int B, float* params, float* m, float* v,

@@ -16,6 +16,8 @@ a GPU by :func:`auto_learner`.
 
 from __future__ import annotations
 
+import os
+
 import math
 import threading
 from typing import Any, Dict, List, Optional, Tuple
@@ -34,6 +36,8 @@ from p2pfl_amd.utils.lockcheck import make_lock, make_rlock
 # allocations on their own threads stay legal while one peer captures.
 _CAPTURE_LOCK = make_lock("FusedCNN._CAPTURE_LOCK")
 
+# conv_adam folded into the FC1 Adam launch (P2PFL_CNN_MERGED_ADAM=0: separate launches)
+_MERGED_ADAM = os.environ.get("P2PFL_CNN_MERGED_ADAM", "1") != "0"
 _NAMES = ("conv1.weight", "conv1.bias", "conv2.weight", "conv2.bias", "l1.weight", "l1.bias", "l2.weight", "l2.bias")
 FEAT, HID = 3136, 2048
 
@@ -133,7 +137,9 @@ class FusedCNNEngine:
         (route blocks first, then the FC1 Adam stream; W1^T ping-ponged so the
         two roles need no ordering) was also measured: 50.8 us vs 12.6 + 33.8 us
         separately. The 512-thread blocks and the union LDS lower the FC1
-        role's occupancy more than the overlap hides.
+        role's occupancy more than the overlap hides.  The conv-parameter Adam
+        (256-thread blocks, 4 KB of LDS) does share the FC1 launch
+        (``fc1_conv_adam``): it adds nothing to the FC1 role's footprint.
         """
         if B > self.mrows:
             raise ValueError(f"batch {B} > engine capacity {self.mrows}")
@@ -141,6 +147,13 @@ class FusedCNNEngine:
         self.forward(x, labels, idx, B, stats, True)
         C.route_fc2(self.dH, self.w1tbf, self.am2, M, B, self.dc2m, self.gb, self.dlogits, self.H,
                     self.params, self.m, self.v, self.gdump, self.off, self.adam_t, t_off, *a)
+        if _MERGED_ADAM:
+            # conv backward first, then ONE launch for the conv-parameter Adam
+            # (latency-bound) and the FC1 wgrad + Adam stream (HBM-bound)
+            C.conv2_bwd(self.dc2m, self.p1s, self.am1, self.w2q, x, idx, self.wslab1, self.wslab2, B)
+            C.fc1_conv_adam(self.dH, self.a1, M, self.wslab1, self.wslab2, self.gb, B, self.params, self.m, self.v,
+                            self.gdump, self.w1bf, self.w1tbf, self.w2r, self.w2q, self.off, self.adam_t, t_off, *a)
+            return
         C.fc1_wgrad_adam(self.dH, self.a1, M, self.params, self.m, self.v, self.gdump, self.w1bf, self.w1tbf, self.off, self.adam_t, t_off, *a)
         C.conv2_bwd(self.dc2m, self.p1s, self.am1, self.w2q, x, idx, self.wslab1, self.wslab2, B)
         C.conv_adam(self.wslab1, self.wslab2, self.gb, B, self.params, self.m, self.v, self.gdump, self.w2r, self.w2q, self.off, self.adam_t, t_off, *a)
