@@ -25,6 +25,9 @@ def main(argv=None) -> None:
     p.add_argument("--model", choices=["resnet50", "resnet18", "mlp"], default="resnet50")
     p.add_argument("--number-sub", type=int, default=64, help="dataset shards (per-peer data = 1/number-sub)")
     p.add_argument("--fast", action="store_true", help="test settings (short heartbeats)")
+    p.add_argument("--overlap", choices=["on", "off"], default="on",
+                   help="on: background diffusion (Settings.ASYNC_DIFFUSION) + per-node HIP streams; "
+                        "off: the reference's blocking diffusion, all peers on the default stream")
     args = p.parse_args(argv)
 
     from p2pfl_amd.communication.memory import InMemoryCommunicationProtocol
@@ -36,6 +39,8 @@ def main(argv=None) -> None:
     if args.fast:
         set_test_settings()
     Settings.LOG_LEVEL = "WARNING"
+    Settings.ASYNC_DIFFUSION = args.overlap == "on"
+    Settings.NODE_STREAMS = args.overlap == "on"
     Settings.TRAIN_SET_SIZE = max(2, args.peers // 2)
     Settings.GOSSIP_MODELS_PER_ROUND = 2
     dev = torch.device("cuda" if torch.cuda.is_available() else "cpu")
@@ -84,6 +89,7 @@ def main(argv=None) -> None:
     print(json.dumps({
         "scenario": "ring topology, train set K/2, 1 train-set peer dropped mid-round",
         "peers": args.peers, "model": args.model, "device": str(dev), "dropped": victim.addr if victim else None,
+        "overlap": args.overlap,
         "round_ms": rounds, "total_s": round(total, 2), "survivors_equal_models": True, "test_accuracy": acc,
     }), flush=True)
 

@@ -308,6 +308,10 @@ class FusedCNNLearner(TorchLearner):
     def fit(self) -> None:
         if self.epochs <= 0 or self.model is None:
             return
+        with self._on_stream():
+            self._fit_fused()
+
+    def _fit_fused(self) -> None:
         self._interrupt.clear()
         self._arena_changed()
         with self._lock:
@@ -351,7 +355,7 @@ class FusedCNNLearner(TorchLearner):
     def evaluate(self) -> Dict[str, float]:
         if self.epochs <= 0 or self.model is None:
             return {}
-        with logger.span(self._addr, "evaluate"):
+        with logger.span(self._addr, "evaluate"), self._on_stream():
             r = self._eval_pass("test", self.data.test_dataloader())
         results = {"test_loss": r["loss"], "test_metric": r["metric"]}
         for k, v in results.items():

@@ -95,6 +95,12 @@ class TorchLearner(NodeLearner):
         self._mt_opt: Any = None
         self._arena_version = 0
         self._snapshot: Optional[Tuple[int, FlatParams]] = None
+        # this node's compute stream (Settings.NODE_STREAMS): virtual peers in
+        # one process train concurrently, and their training overlaps the
+        # aggregation / transport work left on the default stream
+        self._compute_stream: Optional[torch.cuda.Stream] = None
+        if self.device.type == "cuda" and Settings.NODE_STREAMS:
+            self._compute_stream = torch.cuda.Stream(self.device)
         self._step_graph: Any = None
         self._eval_graphs: Dict[str, Any] = {}
         self.model: Any = None
@@ -147,7 +153,27 @@ class TorchLearner(NodeLearner):
         self.arena.sync_in()
         return self.arena.params
 
+    @contextlib.contextmanager
+    def _on_stream(self):
+        """Run a block on this learner's compute stream: ordered after work the
+        caller already enqueued on its stream, and complete (host-synchronised)
+        when the block returns, so every other stream may read the result."""
+        cs = self._compute_stream
+        if cs is None or torch.cuda.current_stream(self.device) == cs:
+            yield
+            return
+        cs.wait_stream(torch.cuda.current_stream(self.device))
+        try:
+            with torch.cuda.stream(cs):
+                yield
+        finally:
+            cs.synchronize()
+
     def set_parameters(self, params: Mapping[str, torch.Tensor]) -> None:
+        with self._on_stream():
+            self._set_parameters(params)
+
+    def _set_parameters(self, params: Mapping[str, torch.Tensor]) -> None:
         assert self.arena is not None
         self._arena_changed()
         own = self.arena.params
@@ -278,6 +304,10 @@ class TorchLearner(NodeLearner):
     def fit(self) -> None:
         if self.epochs <= 0 or self.model is None:
             return
+        with self._on_stream():
+            self._fit()
+
+    def _fit(self) -> None:
         self._interrupt.clear()
         self._arena_changed()
         try:
@@ -393,7 +423,8 @@ class TorchLearner(NodeLearner):
 
     def validate(self) -> None:
         """The per-epoch validation pass (metrics to the local store)."""
-        self._validate()
+        with self._on_stream():
+            self._validate()
 
     def _eval_graph_ok(self, loader: Any) -> bool:
         if not (self.use_step_graphs and self.mixed and self.device.type == "cuda"):
@@ -435,7 +466,7 @@ class TorchLearner(NodeLearner):
     def evaluate(self) -> Dict[str, float]:
         if self.epochs <= 0 or self.model is None:
             return {}
-        with logger.span(self._addr, "evaluate"):
+        with logger.span(self._addr, "evaluate"), self._on_stream():
             results = self._run_eval(self.data.test_dataloader(), self.model.test_step)
         for k, v in results.items():
             self._log(k, v)

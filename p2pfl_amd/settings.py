@@ -47,6 +47,18 @@ class Settings:
     """Model gossip stops after this many identical status snapshots."""
 
     # ---- training --------------------------------------------------------
+    ASYNC_DIFFUSION: bool = False
+    """Diffuse a round's aggregated model in the background while the next
+    round trains (new; the reference blocks in ``GossipModelStage`` until every
+    direct neighbour has the model).  One immutable device snapshot of the
+    aggregate is pushed to every lagging neighbour; a newer round's diffusion
+    supersedes an older one."""
+
+    NODE_STREAMS: bool = True
+    """GPU learners train / evaluate on their own HIP stream (virtual peers in
+    one process then overlap each other and the aggregation / transport work
+    left on the default stream)."""
+
     TRAIN_SET_SIZE: int = 4
     """Number of nodes elected to train each experiment."""
     VOTE_TIMEOUT: float = 60

@@ -1,16 +1,22 @@
 """GossipModelStage (reference ``stages/base_node/gossip_model_stage.py:34-132``).
 
 Wait for the aggregation, load it, announce ``models_ready``, then diffuse the
-full model to direct neighbours that are still behind this round.
+full model to direct neighbours that are still behind this round -- inline
+(reference behaviour), or with ``Settings.ASYNC_DIFFUSION`` on a background
+diffusion thread that keeps pushing ONE device snapshot of the round's
+aggregate while the node already trains the next round (the compute of round
+r+1 overlaps the communication of round r).
 """
 
 from __future__ import annotations
 
+import threading
 from typing import Any, List, Optional, Type
 
 from p2pfl_amd.commands.add_model_command import AddModelCommand
 from p2pfl_amd.commands.models_ready_command import ModelsReadyCommand
 from p2pfl_amd.management.logger import logger
+from p2pfl_amd.settings import Settings
 from p2pfl_amd.stages.base_node.common import model_payload
 from p2pfl_amd.stages.stage import Stage
 from p2pfl_amd.stages.stage_factory import StageFactory
@@ -54,10 +60,13 @@ class GossipModelStage(Stage):
 
     @staticmethod
     def _gossip_model_diffusion(state: Any, protocol: Any, aggregator: Any) -> None:
-        logger.info(state.addr, "Gossiping aggregated model.")
         fixed_round = state.round
         if fixed_round is None:
             return
+        if Settings.ASYNC_DIFFUSION:
+            Diffusion.start(state, protocol, aggregator, fixed_round)
+            return
+        logger.info(state.addr, "Gossiping aggregated model.")
 
         def candidates() -> List[str]:
             return [
@@ -85,3 +94,66 @@ class GossipModelStage(Stage):
             wakeup=state.changed,
             peer_status_fn=lambda n: state.nei_status.get(n),
         )
+
+
+class Diffusion:
+    """Background diffusion of one round's aggregate (``Settings.ASYNC_DIFFUSION``).
+
+    The payload and the contributor list are captured ONCE when the round's
+    aggregate is loaded -- before the next round touches the live arena or
+    clears the aggregator -- so every lagging neighbour receives the same
+    immutable snapshot, however long it takes to catch up.  The thread ends
+    when no direct neighbour is behind ``round`` any more, when the node stops
+    or leaves the experiment, or when a newer round's diffusion starts.
+    """
+
+    def __init__(self, state: Any, protocol: Any, rnd: int, message: Any) -> None:
+        self.state, self.protocol, self.round, self.message = state, protocol, rnd, message
+        self.cancelled = threading.Event()
+        self.thread = threading.Thread(target=self._run, name=f"diffusion-{state.addr}-r{rnd}", daemon=True)
+
+    @staticmethod
+    def start(state: Any, protocol: Any, aggregator: Any, rnd: int) -> "Diffusion":
+        payload = model_payload(state, protocol)  # device snapshot (or encoded bytes), taken now
+        contributors = list(aggregator.get_aggregated_models())
+
+        def message() -> Any:  # a fresh envelope per push, all around the same payload
+            return protocol.build_weights(AddModelCommand.get_name(), rnd, payload, contributors, 1)
+
+        d = Diffusion(state, protocol, rnd, message)
+        prev = getattr(state, "diffusion", None)
+        if prev is not None:
+            prev.cancelled.set()  # a newer aggregate supersedes the older one
+        state.diffusion = d
+        logger.info(state.addr, f"Gossiping aggregated model of round {rnd} in the background.")
+        d.thread.start()
+        return d
+
+    def _candidates(self) -> List[str]:
+        st = self.state
+        return [
+            n
+            for n in self.protocol.get_neighbors(only_direct=True)
+            if n in st.nei_status and st.nei_status[n] < self.round
+        ]
+
+    def _stop(self) -> bool:
+        st = self.state
+        return self.cancelled.is_set() or st.round is None or st.round < self.round
+
+    def _run(self) -> None:
+        try:
+            with logger.span(self.state.addr, "async_diffusion", round=self.round):
+                self.protocol.gossip_weights(
+                    self._stop,
+                    self._candidates,
+                    self._candidates,
+                    lambda _n: self.message(),
+                    wakeup=self.state.changed,
+                    peer_status_fn=lambda n: self.state.nei_status.get(n),
+                )
+        except Exception as e:  # a transport failure must not take the node down
+            logger.warning(self.state.addr, f"background diffusion of round {self.round} failed: {e}")
+
+    def join(self, timeout: Optional[float] = None) -> None:
+        self.thread.join(timeout)

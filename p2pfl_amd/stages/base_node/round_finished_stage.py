@@ -40,6 +40,12 @@ class RoundFinishedStage(Stage):
             raise Exception("Round or total rounds not set.")
         if state.round < state.total_rounds:
             return StageFactory.get_stage("TrainStage")
+        # last round: a background diffusion (Settings.ASYNC_DIFFUSION) must
+        # reach the lagging neighbours before the experiment state is reset
+        diffusion = getattr(state, "diffusion", None)
+        if diffusion is not None:
+            diffusion.join()
+            state.diffusion = None
         evaluate_and_share(state, communication_protocol)
         # experiment over: reset per-experiment peer bookkeeping so a new
         # experiment re-gossips the initial model (the reference kept stale
