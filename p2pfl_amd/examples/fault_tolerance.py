@@ -25,9 +25,10 @@ def main(argv=None) -> None:
     p.add_argument("--model", choices=["resnet50", "resnet18", "mlp"], default="resnet50")
     p.add_argument("--number-sub", type=int, default=64, help="dataset shards (per-peer data = 1/number-sub)")
     p.add_argument("--fast", action="store_true", help="test settings (short heartbeats)")
-    p.add_argument("--overlap", choices=["on", "off"], default="on",
+    p.add_argument("--overlap", choices=["on", "off", "async", "streams"], default="on",
                    help="on: background diffusion (Settings.ASYNC_DIFFUSION) + per-node HIP streams; "
-                        "off: the reference's blocking diffusion, all peers on the default stream")
+                        "off: the reference's blocking diffusion, all peers on the default stream; "
+                        "async / streams: only one of the two")
     args = p.parse_args(argv)
 
     from p2pfl_amd.communication.memory import InMemoryCommunicationProtocol
@@ -39,8 +40,8 @@ def main(argv=None) -> None:
     if args.fast:
         set_test_settings()
     Settings.LOG_LEVEL = "WARNING"
-    Settings.ASYNC_DIFFUSION = args.overlap == "on"
-    Settings.NODE_STREAMS = args.overlap == "on"
+    Settings.ASYNC_DIFFUSION = args.overlap in ("on", "async")
+    Settings.NODE_STREAMS = args.overlap in ("on", "streams")
     Settings.TRAIN_SET_SIZE = max(2, args.peers // 2)
     Settings.GOSSIP_MODELS_PER_ROUND = 2
     dev = torch.device("cuda" if torch.cuda.is_available() else "cpu")

@@ -25,7 +25,10 @@ class FedAvg(Aggregator):
     def aggregate(self, models: Dict[str, Tuple[Any, int]]) -> FlatParams:
         if len(models) == 0:
             raise NoModelsToAggregateError(f"({self.node_name}) Trying to aggregate models when there is no models")
-        entries = list(models.values())
+        # fixed summation order (by contributor key), so every node that
+        # aggregates the same models gets the bitwise-same result whatever
+        # order they arrived in
+        entries = [models[k] for k in sorted(models)]
         ref = entries[-1][0]
         device = next(iter(ref.values())).device if len(ref) else torch.device("cpu")
         flats: List[FlatParams] = [flatten(m, device=device) for m, _ in entries]

@@ -103,8 +103,10 @@ class Diffusion:
     aggregate is loaded -- before the next round touches the live arena or
     clears the aggregator -- so every lagging neighbour receives the same
     immutable snapshot, however long it takes to catch up.  The thread ends
-    when no direct neighbour is behind ``round`` any more, when the node stops
-    or leaves the experiment, or when a newer round's diffusion starts.
+    when no direct neighbour is behind ``round`` any more (or their status
+    stops moving, ``GOSSIP_EXIT_ON_X_EQUAL_ROUNDS``), or when the node stops
+    or leaves the experiment.  Diffusions of consecutive rounds may run side
+    by side.
     """
 
     def __init__(self, state: Any, protocol: Any, rnd: int, message: Any) -> None:
@@ -121,10 +123,10 @@ class Diffusion:
             return protocol.build_weights(AddModelCommand.get_name(), rnd, payload, contributors, 1)
 
         d = Diffusion(state, protocol, rnd, message)
-        prev = getattr(state, "diffusion", None)
-        if prev is not None:
-            prev.cancelled.set()  # a newer aggregate supersedes the older one
-        state.diffusion = d
+        # an older round's diffusion keeps running: a neighbour still at that
+        # round needs THAT aggregate (it ignores newer-round models)
+        live = [x for x in getattr(state, "diffusions", []) if x.thread.is_alive()]
+        state.diffusions = live + [d]
         logger.info(state.addr, f"Gossiping aggregated model of round {rnd} in the background.")
         d.thread.start()
         return d

@@ -42,10 +42,9 @@ class RoundFinishedStage(Stage):
             return StageFactory.get_stage("TrainStage")
         # last round: a background diffusion (Settings.ASYNC_DIFFUSION) must
         # reach the lagging neighbours before the experiment state is reset
-        diffusion = getattr(state, "diffusion", None)
-        if diffusion is not None:
+        for diffusion in getattr(state, "diffusions", []):
             diffusion.join()
-            state.diffusion = None
+        state.diffusions = []
         evaluate_and_share(state, communication_protocol)
         # experiment over: reset per-experiment peer bookkeeping so a new
         # experiment re-gossips the initial model (the reference kept stale

@@ -46,8 +46,7 @@ def test_async_diffusion_chain_non_trainers(protocol, async_settings):
         check_equal_models(nodes, atol=1e-5)
         # every background diffusion has ended with the experiment
         for nd in nodes:
-            d = getattr(nd.state, "diffusion", None)
-            assert d is None or not d.thread.is_alive()
+            assert all(not d.thread.is_alive() for d in getattr(nd.state, "diffusions", []))
     finally:
         for nd in nodes:
             nd.stop()
