@@ -80,7 +80,16 @@ def main(argv=None) -> None:
         survivors = [n for n in nodes if n is not victim]
         wait_4_results(survivors, timeout=1800)
         total = time.perf_counter() - t0
-        check_equal_models(survivors)
+        try:
+            check_equal_models(survivors)
+        except AssertionError as e:
+            ref = survivors[0].state.learner.get_parameters().flat
+            for s_ in survivors:
+                d = float((s_.state.learner.get_parameters().flat - ref).abs().max())
+                rounds_done = len(logger.tracer.spans(s_.addr, "stage:RoundFinishedStage"))
+                print(f"  {s_.addr}: max|diff| vs {survivors[0].addr} = {d:.3g}, rounds finished {rounds_done}, "
+                      f"train_set member: {s_.addr in survivors[0].state.train_set}", flush=True)
+            raise e
         ends = sorted(s.start + s.duration for s in logger.tracer.spans(survivors[0].addr, "stage:RoundFinishedStage"))
         rounds = [round((b - a) * 1e3, 1) for a, b in zip([t0] + ends, ends)]
         acc = survivors[0].state.learner.evaluate()["test_metric"]

@@ -213,16 +213,25 @@ class _LinearGeluMFMA(torch.autograd.Function):
         return dx, dw, db.to(ctx.b_dtype) if ctx.needs_input_grad[2] else None
 
 
+# P2PFL_NATIVE_GEMM=0 routes Linear layers to the hipBLASLt path
+# (ops.linear_blas) instead -- the A/B switch the ViT measurements use.
+_NATIVE = os.environ.get("P2PFL_NATIVE_GEMM", "1") != "0"
+
+
 def _ok(x: torch.Tensor, w: torch.Tensor) -> bool:
     from p2pfl_amd.ops import _gpu
 
-    return _gpu(x) and x.dtype in (torch.bfloat16, torch.float32) and w.shape[0] % 8 == 0 and w.shape[1] % 8 == 0 and x.shape[-1] == w.shape[1]
+    return _NATIVE and _gpu(x) and x.dtype in (torch.bfloat16, torch.float32) and w.shape[0] % 8 == 0 and w.shape[1] % 8 == 0 and x.shape[-1] == w.shape[1]
 
 
 def linear(x: torch.Tensor, weight: torch.Tensor, bias: Optional[torch.Tensor] = None) -> torch.Tensor:
     """``F.linear`` with forward, input gradient and weight gradient on the MFMA GEMM."""
     if _ok(x, weight):
         return _LinearMFMA.apply(x, weight, bias)
+    if not _NATIVE and x.is_cuda:
+        from p2pfl_amd.ops.fused import linear as linear_blas
+
+        return linear_blas(x, weight, bias)
     return F.linear(x, weight, bias)
 
 
@@ -230,4 +239,8 @@ def linear_gelu(x: torch.Tensor, weight: torch.Tensor, bias: torch.Tensor) -> to
     """``gelu(F.linear(x, weight, bias))`` (exact erf GELU), fused epilogue."""
     if _ok(x, weight):
         return _LinearGeluMFMA.apply(x, weight, bias)
+    if not _NATIVE and x.is_cuda:
+        from p2pfl_amd.ops.fused import bias_gelu, linear as linear_blas
+
+        return bias_gelu(linear_blas(x, weight, None), bias)
     return F.gelu(F.linear(x, weight, bias))

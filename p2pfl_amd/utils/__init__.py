@@ -68,7 +68,10 @@ def check_equal_models(nodes: List[Any], atol: float = 1e-1) -> None:
             first = {k: v.detach().float().cpu().numpy().copy() for k, v in params.items()}
             continue
         for layer, ref in first.items():
-            assert np.allclose(ref, params[layer].detach().float().cpu().numpy(), atol=atol), layer
+            cur = params[layer].detach().float().cpu().numpy()
+            if not np.allclose(ref, cur, atol=atol):
+                diff = float(np.abs(ref - cur).max())
+                raise AssertionError(f"{layer}: {nodes[0].addr} vs {node.addr} differ (max |diff| {diff:.3g})")
 
 
 def to_numpy(t: torch.Tensor) -> np.ndarray:
