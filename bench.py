@@ -311,6 +311,12 @@ def run_gossip(args, env: _Env) -> dict:
             f"{pushes.get('xgmi_bytes_sent', 0) / 1e6:.1f} MB",
             file=sys.stderr, flush=True,
         )
+        from p2pfl_amd.ops import autotune
+
+        if env.rank == 0 and autotune.choices():
+            n_nat = sum(1 for v, _ in autotune.choices().values() if v == "native")
+            print(f"[bench rank 0] kernel choice per shape (native vs library, ms): {n_nat}/{len(autotune.choices())} native\n"
+                  + autotune.summary(), file=sys.stderr, flush=True)
         n_train = len(data.train_dataloader().dataset)
         n_val = len(data.val_dataloader().dataset)
         n_test = len(data.test_dataloader().dataset)

@@ -10,7 +10,10 @@ the optimizer without a relayout copy.
 
 Anything the kernels do not take -- CPU tensors, fp32 weights, channel
 counts that are not multiples of 64 on the reduction side (the 3-channel
-stem), groups, asymmetric stride/padding -- runs ``F.conv2d``.  The
+stem), groups, asymmetric stride/padding -- runs ``F.conv2d``.  Where both
+can run, the first eager call of each layer shape times native vs MIOpen
+and keeps the faster (``ops/autotune.py``; ``P2PFL_NATIVE_CONV=1/0`` forces
+one side).  The
 reference trains its convolutions through torch.nn.Conv2d
 (/root/reference/p2pfl/learning/pytorch/mnist_examples/models/cnn.py:55-62).
 """
@@ -24,12 +27,14 @@ import torch
 import torch.nn.functional as F
 from torch import nn
 
+from p2pfl_amd.ops import autotune
 from p2pfl_amd.ops.splitk import IN_LAUNCH_MAX_SPLITS, counters, tiles_of
 
 # counters a test can read to prove the native path ran
 STATS = {"native_fwd": 0, "torch_fwd": 0}
 
-_DISABLED = os.environ.get("P2PFL_NATIVE_CONV", "1") == "0"
+# "native" | "library" | "auto" (measured per shape, ops/autotune.py); env P2PFL_NATIVE_CONV
+_POLICY = autotune.policy("P2PFL_NATIVE_CONV")
 # csrc/gemm.h variant bits per product (single LDS buffer for the gathers, double buffer for split-K wgrad)
 _V_FWD = int(os.environ.get("P2PFL_CONV_VARIANT_FWD", "10"))
 _V_DGRAD = int(os.environ.get("P2PFL_CONV_VARIANT_DGRAD", "10"))
@@ -90,7 +95,7 @@ def _run_split(launch, rows: int, cols: int, s: int, out: torch.Tensor) -> None:
 def native_ok(x: torch.Tensor, conv: nn.Conv2d) -> bool:
     from p2pfl_amd.ops import _gpu
 
-    if _DISABLED or not _gpu(x) or x.dim() != 4:
+    if not _gpu(x) or x.dim() != 4:
         return False
     w = conv.weight
     if w.dtype != torch.bfloat16 or conv.bias is not None or conv.groups != 1 or conv.padding_mode != "zeros":
@@ -164,9 +169,41 @@ class _Conv2dNHWC(torch.autograd.Function):
         return dx, dw, None, None, None
 
 
+def _native_faster(x: torch.Tensor, conv: nn.Conv2d) -> bool:
+    """Time native vs MIOpen for this layer shape once (forward, plus both
+    gradients when autograd will need them) and remember the winner."""
+    w = conv.weight
+    stride, pad, dil = _sym(conv.stride), _sym(conv.padding), _sym(conv.dilation)
+    grad = torch.is_grad_enabled() and (x.requires_grad or w.requires_grad)
+    key = ("conv2d", tuple(x.shape), tuple(w.shape), stride, pad, dil, grad)
+    if key in autotune._CHOICE:
+        return autotune._CHOICE[key] == "native"
+    xb = x.detach().to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    wd = w.detach()
+    OH, OW = out_hw(x.shape[2], x.shape[3], (w.shape[2], w.shape[3]), stride, pad, dil)
+    dy = torch.randn(x.shape[0], w.shape[0], OH, OW, device=x.device).to(torch.bfloat16)
+    dy = dy.contiguous(memory_format=torch.channels_last)
+
+    def native():
+        with torch.enable_grad():
+            xr = xb.requires_grad_(grad)
+            wr = wd.detach().requires_grad_(grad)
+            y = _Conv2dNHWC.apply(xr, wr, stride, pad, dil)
+            if grad:
+                torch.autograd.backward(y, dy)
+
+    def library():
+        F.conv2d(xb, wd, None, stride, pad, dil)
+        if grad:
+            torch.ops.aten.convolution_backward(dy, xb, wd, None, [stride] * 2, [pad] * 2, [dil] * 2, False, [0, 0],
+                                                1, [True, True, False])
+
+    return autotune.choose(key, [("native", native), ("library", library)]) == "native"
+
+
 def conv2d(x: torch.Tensor, conv: nn.Conv2d) -> torch.Tensor:
-    """``conv(x)`` on the implicit-GEMM kernels when :func:`native_ok`, else ``F.conv2d``."""
-    if native_ok(x, conv):
+    """``conv(x)`` on the implicit-GEMM kernels or MIOpen (``_POLICY``; "auto" = measured per shape)."""
+    if native_ok(x, conv) and _POLICY != "library" and (_POLICY == "native" or _native_faster(x, conv)):
         STATS["native_fwd"] += 1
         return _Conv2dNHWC.apply(x, conv.weight, _sym(conv.stride), _sym(conv.padding), _sym(conv.dilation))
     STATS["torch_fwd"] += 1

@@ -22,6 +22,7 @@ from typing import Optional, Tuple
 import torch
 import torch.nn.functional as F
 
+from p2pfl_amd.ops import autotune
 from p2pfl_amd.ops.splitk import IN_LAUNCH_MAX_SPLITS, counters, tiles_of
 
 
@@ -213,22 +214,65 @@ class _LinearGeluMFMA(torch.autograd.Function):
         return dx, dw, db.to(ctx.b_dtype) if ctx.needs_input_grad[2] else None
 
 
-# P2PFL_NATIVE_GEMM=0 routes Linear layers to the hipBLASLt path
-# (ops.linear_blas) instead -- the A/B switch the ViT measurements use.
-_NATIVE = os.environ.get("P2PFL_NATIVE_GEMM", "1") != "0"
+# "native" | "library" | "auto" (measured per shape, ops/autotune.py); env P2PFL_NATIVE_GEMM.
+# The library side is hipBLASLt (ops.linear_blas) plus the fused bias+GELU kernel.
+_POLICY = autotune.policy("P2PFL_NATIVE_GEMM")
+
+
+def _native_faster(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor], gelu: bool) -> bool:
+    """Time this Linear shape once on both paths (forward, plus the input and
+    weight gradients when autograd needs them) and remember the winner."""
+    grad = torch.is_grad_enabled() and (x.requires_grad or w.requires_grad)
+    M = x.numel() // x.shape[-1]
+    N, K = w.shape
+    key = ("linear", M, N, K, bool(gelu), bias is not None, grad)
+    if key in autotune._CHOICE:
+        return autotune._CHOICE[key] == "native"
+    from p2pfl_amd.ops.fused import bias_gelu, linear as linear_blas
+
+    x2 = x.detach().reshape(M, K).to(torch.bfloat16)
+    wd = w.detach().to(torch.bfloat16)
+    bd = bias.detach() if bias is not None else None
+    dy = torch.randn(M, N, device=x.device).to(torch.bfloat16)
+
+    def native():
+        if gelu:
+            gemm(x2, wd, bias=bd, gelu=True, want_z=grad)
+        else:
+            gemm(x2, wd, bias=bd)
+        if grad:
+            _product(dy, wd, True, False, torch.bfloat16)
+            _wgrad(dy, x2, torch.bfloat16)
+
+    def library():
+        if gelu:
+            bias_gelu(linear_blas(x2, wd, None), bd)
+        else:
+            linear_blas(x2, wd, bd)
+        if grad:
+            dy @ wd
+            dy.t() @ x2
+
+    return autotune.choose(key, [("native", native), ("library", library)]) == "native"
+
+
+def _use_native(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor], gelu: bool) -> bool:
+    if _POLICY == "library" or not _ok(x, w):
+        return False
+    return _POLICY == "native" or _native_faster(x, w, bias, gelu)
 
 
 def _ok(x: torch.Tensor, w: torch.Tensor) -> bool:
     from p2pfl_amd.ops import _gpu
 
-    return _NATIVE and _gpu(x) and x.dtype in (torch.bfloat16, torch.float32) and w.shape[0] % 8 == 0 and w.shape[1] % 8 == 0 and x.shape[-1] == w.shape[1]
+    return _gpu(x) and x.dtype in (torch.bfloat16, torch.float32) and w.shape[0] % 8 == 0 and w.shape[1] % 8 == 0 and x.shape[-1] == w.shape[1]
 
 
 def linear(x: torch.Tensor, weight: torch.Tensor, bias: Optional[torch.Tensor] = None) -> torch.Tensor:
     """``F.linear`` with forward, input gradient and weight gradient on the MFMA GEMM."""
-    if _ok(x, weight):
+    if _use_native(x, weight, bias, False):
         return _LinearMFMA.apply(x, weight, bias)
-    if not _NATIVE and x.is_cuda:
+    if x.is_cuda:
         from p2pfl_amd.ops.fused import linear as linear_blas
 
         return linear_blas(x, weight, bias)
@@ -237,9 +281,9 @@ def linear(x: torch.Tensor, weight: torch.Tensor, bias: Optional[torch.Tensor] =
 
 def linear_gelu(x: torch.Tensor, weight: torch.Tensor, bias: torch.Tensor) -> torch.Tensor:
     """``gelu(F.linear(x, weight, bias))`` (exact erf GELU), fused epilogue."""
-    if _ok(x, weight):
+    if _use_native(x, weight, bias, True):
         return _LinearGeluMFMA.apply(x, weight, bias)
-    if not _NATIVE and x.is_cuda:
+    if x.is_cuda:
         from p2pfl_amd.ops.fused import bias_gelu, linear as linear_blas
 
         return bias_gelu(linear_blas(x, weight, None), bias)

@@ -14,8 +14,10 @@ pytestmark = pytest.mark.gpu
 
 
 @pytest.fixture(autouse=True)
-def _require_ext():
+def _require_ext(monkeypatch):
     ops.ext()
+    # these tests exercise the hand-written kernels: no per-shape library choice
+    monkeypatch.setattr(conv_ops, "_POLICY", "native")
 
 
 def _operands(N, C, H, W, O, k, seed, integer=False):
@@ -182,3 +184,25 @@ def test_resnet18_block_runs_native_convs():
     for name, p in model.named_parameters():
         if p.dim() == 4:
             assert p.grad is not None and torch.isfinite(p.grad).all(), name
+
+
+def test_autotune_picks_and_caches_a_path(monkeypatch):
+    """Policy "auto": the first call of a shape times native vs MIOpen, later calls reuse the choice."""
+    from p2pfl_amd.ops import autotune
+
+    monkeypatch.setattr(conv_ops, "_POLICY", "auto")
+    autotune.reset()
+    x, w = _operands(2, 64, 8, 8, 64, 3, seed=11)
+    conv = nn.Conv2d(64, 64, 3, 1, 1, bias=False).cuda()
+    conv.weight.data = w
+    xg = x.clone().requires_grad_()
+    y = ops.conv2d(xg, conv)
+    y.float().sum().backward()
+    decided = autotune.choices()
+    assert len(decided) == 1
+    (choice, times), = decided.values()
+    assert choice in ("native", "library") and set(times) == {"native", "library"}
+    ref = _ref(x, w, 1, 1, 1)
+    torch.testing.assert_close(y.float(), ref, atol=3e-2, rtol=2e-2)
+    ops.conv2d(x.clone().requires_grad_(), conv)
+    assert len(autotune.choices()) == 1  # cached

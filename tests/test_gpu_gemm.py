@@ -7,13 +7,18 @@ import torch
 import torch.nn.functional as F
 
 from p2pfl_amd import ops
+import importlib
+
+gemm_mod = importlib.import_module("p2pfl_amd.ops.gemm")
 
 pytestmark = pytest.mark.gpu
 
 
 @pytest.fixture(autouse=True)
-def _require_ext():
+def _require_ext(monkeypatch):
     ops.ext()
+    # these tests exercise the hand-written kernels: no per-shape library choice
+    monkeypatch.setattr(gemm_mod, "_POLICY", "native")
 
 
 def _operands(M, N, K, a_kmajor, b_kmajor, seed=0):
