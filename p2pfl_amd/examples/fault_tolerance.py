@@ -25,6 +25,7 @@ def main(argv=None) -> None:
     p.add_argument("--model", choices=["resnet50", "resnet18", "mlp"], default="resnet50")
     p.add_argument("--number-sub", type=int, default=64, help="dataset shards (per-peer data = 1/number-sub)")
     p.add_argument("--fast", action="store_true", help="test settings (short heartbeats)")
+    p.add_argument("--lr", type=float, default=None, help="override the ResNet SGD learning rate (default 0.05)")
     p.add_argument("--overlap", choices=["on", "off", "async", "streams"], default="on",
                    help="on: background diffusion (Settings.ASYNC_DIFFUSION) + per-node HIP streams; "
                         "off: the reference's blocking diffusion, all peers on the default stream; "
@@ -55,8 +56,9 @@ def main(argv=None) -> None:
         from p2pfl_amd.models.resnet import ResNet18, ResNet50
 
         net = ResNet50 if args.model == "resnet50" else ResNet18
+        kw = {} if args.lr is None else {"lr_rate": args.lr}
         make = lambda i: (  # noqa: E731
-            net(seed=1234),
+            net(seed=1234, **kw),
             Cifar10FederatedDM(sub_id=i, number_sub=args.number_sub, partitioner="dirichlet", alpha=0.5),
         )
     nodes = []
