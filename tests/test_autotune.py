@@ -1,0 +1,48 @@
+"""Kernel-choice policy (p2pfl_amd/ops/autotune.py) and split-K helpers, CPU side."""
+
+from __future__ import annotations
+
+import pytest
+
+from p2pfl_amd.ops import autotune
+from p2pfl_amd.ops.splitk import IN_LAUNCH_MAX_SPLITS, tiles_of
+
+
+@pytest.mark.parametrize("val,expect", [("1", "native"), ("native", "native"), ("0", "library"), ("off", "library"),
+                                        ("auto", "auto"), ("", "auto"), ("bogus", "auto")])
+def test_policy_parsing(monkeypatch, val, expect):
+    monkeypatch.setenv("P2PFL_TEST_POLICY", val)
+    assert autotune.policy("P2PFL_TEST_POLICY") == expect
+
+
+def test_policy_default_is_auto(monkeypatch):
+    monkeypatch.delenv("P2PFL_TEST_POLICY", raising=False)
+    assert autotune.policy("P2PFL_TEST_POLICY") == "auto"
+
+
+def test_cached_choice_is_reused_without_timing():
+    autotune.reset()
+    autotune._CHOICE[("k",)] = "library"
+    calls = []
+    assert autotune.choose(("k",), [("native", lambda: calls.append(1)), ("library", lambda: calls.append(2))]) == "library"
+    assert calls == []
+    assert "library" in autotune.summary() or autotune.summary() == "('k',): library ()"
+    autotune.reset()
+    assert autotune.choices() == {}
+
+
+def test_split_k_helpers():
+    assert tiles_of(128, 128) == 1 and tiles_of(129, 128) == 2 and tiles_of(6304, 768) == 50 * 6
+    assert 1 < IN_LAUNCH_MAX_SPLITS <= 8
+
+
+def test_conv_split_choices():
+    from p2pfl_amd.ops.conv import mn_splits, out_hw, wgrad_splits
+
+    assert out_hw(32, 32, (3, 3), 1, 1, 1) == (32, 32)
+    assert out_hw(32, 32, (3, 3), 2, 1, 1) == (16, 16)
+    assert out_hw(9, 9, (1, 1), 2, 0, 1) == (5, 5)
+    # big output grids need no split, small ones are split until ~1 WG per CU
+    assert mn_splits(32768, 64, 576) == 1
+    assert mn_splits(512, 512, 4608) == 16
+    assert wgrad_splits(64, 576, 32768) >= 16
