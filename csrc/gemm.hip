@@ -7,7 +7,9 @@
 // ever transposed in memory:
 //
 // * 128 x 128 output tile per 256-thread workgroup, 4 waves as 2 x 2, each
-//   wave 64 x 64 = 2 x 2 tiles of v_mfma_f32_32x32x16_bf16, BK = 64;
+//   wave 64 x 64 = 2 x 2 tiles of v_mfma_f32_32x32x16_bf16, BK = 64; or
+//   (variant bit 6) 256 x 256 per 512-thread workgroup, 8 waves as 2 x 4,
+//   each 128 x 64 -- half the operand bytes per FLOP, for large products;
 // * the pipeline itself lives in gemm_core.h (shared with the implicit-GEMM
 //   convolutions of conv.hip); this file instantiates it with plain loaders;
 // * operands go HBM -> LDS with global_load_lds (16 B per lane, no VGPR
@@ -37,14 +39,27 @@ namespace p2gemm {
 
 template <int NBUF, class LA, class LB>
 __global__ __launch_bounds__(NT, NBUF == 1 ? 4 : 2) void gemm_kernel(GemmParams p, LA la, LB lb, int tiles_m, int tiles_n) {
-  __shared__ __attribute__((aligned(16))) char smem[NBUF * 2 * TILE];  // [buf][A | B]
-  gemm_body<NBUF>(p, la, lb, tiles_m, tiles_n, smem);
+  __shared__ __attribute__((aligned(16))) char smem[NBUF * Tile128::STAGE];  // [buf][A | B]
+  gemm_body<Tile128, NBUF>(p, la, lb, tiles_m, tiles_n, smem);
+}
+
+// 256 x 256 tile, 8 waves, one workgroup per CU (128 KB of LDS, up to 256
+// registers per lane at two waves per SIMD).
+template <class LA, class LB>
+__global__ __launch_bounds__(Tile256::NT) void gemm256_kernel(GemmParams p, LA la, LB lb, int tiles_m, int tiles_n) {
+  __shared__ __attribute__((aligned(16))) char smem[2 * Tile256::STAGE];
+  gemm_body<Tile256, 2>(p, la, lb, tiles_m, tiles_n, smem);
 }
 
 template <class LA, class LB>
 static void launch(const GemmParams& p, const LA& la, const LB& lb, hipStream_t s) {
   int tm, tn;
-  const int grid = gemm_grid(p, tm, tn);
+  if (p.variant & 64) {
+    const int grid = gemm_grid<Tile256>(p, tm, tn);
+    hipLaunchKernelGGL((gemm256_kernel<LA, LB>), dim3(grid), dim3(Tile256::NT), 0, s, p, la, lb, tm, tn);
+    return;
+  }
+  const int grid = gemm_grid<Tile128>(p, tm, tn);
   if (p.variant & 8)
     hipLaunchKernelGGL((gemm_kernel<1, LA, LB>), dim3(grid), dim3(NT), 0, s, p, la, lb, tm, tn);
   else

@@ -27,7 +27,30 @@ typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
 typedef short s16x4 __attribute__((ext_vector_type(4)));
 
 constexpr int BM = 128, BN = 128, BK = 64, NT = 256;
-constexpr int TILE = BM * BK * 2;  // bytes per operand tile (16 KB)
+constexpr int TILE = BM * BK * 2;  // bytes per 128-row operand half-tile (16 KB)
+
+// Output tile shape.  Operands are staged as 128-row halves (TILE bytes each,
+// the loader geometry above: 256 threads x 4 chunks); a workgroup of NT
+// threads is GROUPS = NT / 256 staging groups, group g filling the halves
+// h = g, g + GROUPS, ... of A and of B.  Waves are WAVES_M x WAVES_N, each
+// owning FM x FN 32 x 32 MFMA tiles.
+//   Tile128: 128 x 128, 4 waves (2 x 2), 64 x 64 per wave -- up to 4
+//            workgroups per CU (single-buffer schedule), the small-grid shape;
+//   Tile256: 256 x 256, 8 waves (2 x 4), 128 x 64 per wave, 128 accumulator
+//            registers, one workgroup per CU: half the L2 -> LDS bytes per
+//            FLOP of Tile128, for the large products.
+template <int BM_, int BN_, int WAVES_M_, int WAVES_N_>
+struct TileCfg {
+  static constexpr int BM = BM_, BN = BN_, WAVES_M = WAVES_M_, WAVES_N = WAVES_N_;
+  static constexpr int NT = 64 * WAVES_M * WAVES_N;
+  static constexpr int GROUPS = NT / 256;
+  static constexpr int HA = BM / 128, HB = BN / 128;  // operand halves
+  static constexpr int FM = BM / WAVES_M / 32, FN = BN / WAVES_N / 32;
+  static constexpr int STAGE = (HA + HB) * TILE;  // bytes per pipeline stage
+  static_assert(NT % 256 == 0 && HA % GROUPS == 0 && HB % GROUPS == 0, "staging groups must split the halves");
+};
+using Tile128 = TileCfg<128, 128, 2, 2>;
+using Tile256 = TileCfg<256, 256, 2, 4>;
 
 // Zero page for out-of-operand chunks (one copy per translation unit).  It is
 // 64 KB, not 16 B: a tile whose rows or taps fall outside the operand sends
@@ -110,15 +133,33 @@ struct PlainMN {  // element (r, k) at g[k * ld + r]
 // Issue the DMA of one operand tile (K-tile starting at k0) into `lds`; every
 // lane moves 16 B four times.  The LDS image is lane-linear per wave; the
 // swizzle lives in the chunk -> source-address mapping above.
+//
+// The load is issued from inline asm, not __builtin_amdgcn_global_load_lds:
+// hipcc cannot tell which LDS bytes a builtin DMA writes, so it drains every
+// outstanding DMA (s_waitcnt vmcnt(0)) before the next ds_read -- including
+// the prefetch of the OTHER buffer, issued just before this K-tile's
+// fragment reads, which serialised the double buffer.  Hidden in asm, the
+// DMA is waited for only where the pipeline says so: the explicit
+// vmcnt(0) + barrier ahead of the buffer's first read.
+P2_DEVICE void dma16(const void* gsrc, char* lds_dst) {
+  const uint32_t m0v = __builtin_amdgcn_readfirstlane(uint32_t(reinterpret_cast<uintptr_t>(lds_dst)));
+  uint32_t keep;
+  asm volatile(
+      "s_mov_b32 %0, m0\n\t"
+      "s_mov_b32 m0, %2\n\t"
+      "s_nop 0\n\t"
+      "global_load_lds_dwordx4 %1, off\n\t"
+      "s_mov_b32 m0, %0"
+      : "=&s"(keep)
+      : "v"(gsrc), "s"(m0v)
+      : "memory");
+}
+
 template <class L>
 P2_DEVICE void stage(const L& ld, const typename L::St& st, int k0, char* lds, int tid) {
   const int wave = tid >> 6;
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    char* dst = lds + (i * NT + wave * 64) * 16;  // wave-uniform; lane L writes dst + 16 L
-    __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)ld.src(st, i, k0, tid),
-                                     (__attribute__((address_space(3))) void*)dst, 16, 0, 0);
-  }
+  for (int i = 0; i < 4; ++i) dma16(ld.src(st, i, k0, tid), lds + (i * NT + wave * 64) * 16);  // lane L writes dst + 16 L
 }
 
 // Fragment of a 32-row block (rows rb..rb+31 of the tile) for k-substep ks:
@@ -160,99 +201,162 @@ P2_DEVICE int xcd_remap(int orig, int nwg) {
 }
 
 // The whole kernel body.  `p` carries M/N/K, split-K and the epilogue.
-template <int NBUF, class LA, class LB>
+template <class CFG, int NBUF, class LA, class LB>
 P2_DEVICE void gemm_body(const GemmParams& p, const LA& la, const LB& lb, int tiles_m, int tiles_n, char* smem) {
+  constexpr int FM = CFG::FM, FN = CFG::FN, HA = CFG::HA, HB = CFG::HB, G = CFG::GROUPS;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int wm = wave >> 1, wn = wave & 1;
+  const int wm = wave / CFG::WAVES_N, wn = wave % CFG::WAVES_N;
+  const int grp = tid >> 8, gt = tid & 255;  // staging group, thread within it
   const int bid = (p.variant & 4) ? int(blockIdx.x) : xcd_remap(blockIdx.x, gridDim.x);
   const int tiles = tiles_m * tiles_n;
   const int split = bid / tiles, t = bid % tiles;
-  // consecutive tiles share the B panel (variant bit 1: the A panel)
-  const int tm = (p.variant & 2) ? t / tiles_n : t % tiles_m, tn = (p.variant & 2) ? t % tiles_n : t / tiles_m;
-  const int m0 = tm * BM, n0 = tn * BN;
+  // Tile order: the workgroups resident on one XCD at a time are a run of
+  // consecutive ids (xcd_remap), and that XCD's L2 serves them only the
+  // operand panels they share.  Grouped order (default) walks GROUP_M tile
+  // rows before moving one tile column, so a run of R resident tiles covers
+  // about GROUP_M x R / GROUP_M tiles: 8 A + 4 B panels for Tile256's 32 per
+  // XCD, where a single-row run reads 1 A + 32 B panels (measured at 8192^3:
+  // L2 hit rate 48 % -> the bound on the K loop).  Variant bit 8: legacy
+  // panel order, consecutive tiles sharing the B panel (bit 1: the A panel).
+  int tm, tn;
+  if (p.variant & 256) {
+    tm = (p.variant & 2) ? t / tiles_n : t % tiles_m;
+    tn = (p.variant & 2) ? t % tiles_n : t / tiles_m;
+  } else {
+    constexpr int GROUP_M = 8;
+    const int per_group = GROUP_M * tiles_n, g0 = (t / per_group) * GROUP_M;
+    const int gsize = min(tiles_m - g0, GROUP_M), r = t % per_group;
+    tm = g0 + r % gsize;
+    tn = r / gsize;
+  }
+  const int m0 = tm * CFG::BM, n0 = tn * CFG::BN;
   int kper = (p.K + p.splits - 1) / p.splits;
   kper = (kper + BK - 1) / BK * BK;
   const int kb = split * kper, ke = min(p.K, kb + kper);
   const int nt = (ke > kb && !(p.variant & 32)) ? (ke - kb + BK - 1) / BK : 0;  // bit 5: skip the K loop (timing probe)
 
-  f32x16 acc[2][2];
+  f32x16 acc[FM][FN];
 #pragma unroll
-  for (int i = 0; i < 2; ++i)
+  for (int i = 0; i < FM; ++i)
 #pragma unroll
-    for (int j = 0; j < 2; ++j)
+    for (int j = 0; j < FN; ++j)
 #pragma unroll
       for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.f;
 
-  const typename LA::St sta = la.prep(m0, tid);
-  const typename LB::St stb = lb.prep(n0, tid);
+  // loader state of the halves this thread's group stages
+  typename LA::St sta[HA / G];
+  typename LB::St stb[HB / G];
+#pragma unroll
+  for (int q = 0; q < HA / G; ++q) sta[q] = la.prep(m0 + 128 * (grp + G * q), gt);
+#pragma unroll
+  for (int q = 0; q < HB / G; ++q) stb[q] = lb.prep(n0 + 128 * (grp + G * q), gt);
+  auto stage_all = [&](int k0, char* dst) {
+#pragma unroll
+    for (int q = 0; q < HA / G; ++q) stage(la, sta[q], k0, dst + (grp + G * q) * TILE, gt);
+#pragma unroll
+    for (int q = 0; q < HB / G; ++q) stage(lb, stb[q], k0, dst + (HA + grp + G * q) * TILE, gt);
+  };
+  // chunk c (0..3) of every half this group stages: stage_all split in four
+  auto stage_chunk = [&](int c, int k0, char* dst) {
+    const int wo = (c * NT + (gt >> 6) * 64) * 16;
+#pragma unroll
+    for (int q = 0; q < HA / G; ++q) dma16(la.src(sta[q], c, k0, gt), dst + (grp + G * q) * TILE + wo);
+#pragma unroll
+    for (int q = 0; q < HB / G; ++q) dma16(lb.src(stb[q], c, k0, gt), dst + (HA + grp + G * q) * TILE + wo);
+  };
+  // where the next K-tile's DMA is issued (variant bits 9-10): 0 before this
+  // K-tile's first fragment reads, 1 right after them, 2 spread over the four
+  // k-substeps (one chunk each)
+  const int dma_mode = (p.variant >> 9) & 3;
+  // fragment rows: wave (wm, wn) owns A rows wm * 32 FM + 32 i, B rows wn * 32 FN + 32 j
+  auto frag_a = [&](const char* s, int i, int ks) {
+    const int r = wm * 32 * FM + 32 * i;
+    return frag<LA::KMAJ>(s + (r >> 7) * TILE, r & 127, ks, lane);
+  };
+  auto frag_b = [&](const char* s, int j, int ks) {
+    const int r = wn * 32 * FN + 32 * j;
+    return frag<LB::KMAJ>(s + (HA + (r >> 7)) * TILE, r & 127, ks, lane);
+  };
   if constexpr (NBUF == 2) {
     if (nt > 0) {
-      stage(la, sta, kb, smem, tid);
-      stage(lb, stb, kb, smem + TILE, tid);
+      stage_all(kb, smem);
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __syncthreads();
     }
   }
-  for (int it = 0; it < nt; ++it) {
-    const int cur = NBUF == 2 ? (it & 1) : 0;
-    const char* sa = smem + cur * 2 * TILE;
-    const char* sb = sa + TILE;
-    if constexpr (NBUF == 2) {
-      if (it + 1 < nt) {  // next K-tile's DMA overlaps this tile's MFMAs
-        char* na = smem + (cur ^ 1) * 2 * TILE;
-        stage(la, sta, kb + (it + 1) * BK, na, tid);
-        stage(lb, stb, kb + (it + 1) * BK, na + TILE, tid);
-      }
-    } else {  // one buffer: latency hidden by the other resident workgroups
-      stage(la, sta, kb + it * BK, smem, tid);
-      stage(lb, stb, kb + it * BK, smem + TILE, tid);
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __syncthreads();
-    }
-    // fragments of sub-step ks + 1 are read from LDS while the MFMAs of ks run
-    // (one block per CU is common for the small convolution / split-K grids,
-    // where the LDS read latency is otherwise exposed four times per K-tile)
-    uint4 fa[2][2], fb[2][2];
+  // One K-tile: MFMAs over the LDS image at `s`; fragments of sub-step ks + 1
+  // are read from LDS while the MFMAs of ks run (one block per CU is common
+  // for the small convolution / split-K grids, where the LDS read latency is
+  // otherwise exposed four times per K-tile).
+  auto compute = [&](const char* s, int k_next, char* dst) {  // k_next < 0: no DMA
+    if (k_next >= 0 && dma_mode == 0) stage_all(k_next, dst);
+    uint4 fa[2][FM], fb[2][FN];
 #pragma unroll
-    for (int i = 0; i < 2; ++i) fa[0][i] = frag<LA::KMAJ>(sa, wm * 64 + i * 32, 0, lane);
+    for (int i = 0; i < FM; ++i) fa[0][i] = frag_a(s, i, 0);
 #pragma unroll
-    for (int j = 0; j < 2; ++j) fb[0][j] = frag<LB::KMAJ>(sb, wn * 64 + j * 32, 0, lane);
+    for (int j = 0; j < FN; ++j) fb[0][j] = frag_b(s, j, 0);
+    if (k_next >= 0 && dma_mode == 1) stage_all(k_next, dst);
 #pragma unroll
     for (int ks = 0; ks < BK / 16; ++ks) {
       const int cb = ks & 1;
+      if (k_next >= 0 && dma_mode >= 2) stage_chunk(ks, k_next, dst);
       if (ks + 1 < BK / 16) {
 #pragma unroll
-        for (int i = 0; i < 2; ++i) fa[cb ^ 1][i] = frag<LA::KMAJ>(sa, wm * 64 + i * 32, ks + 1, lane);
+        for (int i = 0; i < FM; ++i) fa[cb ^ 1][i] = frag_a(s, i, ks + 1);
 #pragma unroll
-        for (int j = 0; j < 2; ++j) fb[cb ^ 1][j] = frag<LB::KMAJ>(sb, wn * 64 + j * 32, ks + 1, lane);
+        for (int j = 0; j < FN; ++j) fb[cb ^ 1][j] = frag_b(s, j, ks + 1);
       }
       if (p.variant & 1) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
-      for (int i = 0; i < 2; ++i)
+      for (int i = 0; i < FM; ++i)
 #pragma unroll
-        for (int j = 0; j < 2; ++j) acc[i][j] = mfma(fb[cb][j], fa[cb][i], acc[i][j]);
+        for (int j = 0; j < FN; ++j) acc[i][j] = mfma(fb[cb][j], fa[cb][i], acc[i][j]);
       if (p.variant & 1) __builtin_amdgcn_s_setprio(0);
     }
-    if constexpr (NBUF == 2) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
+  };
+  if constexpr (NBUF == 2) {
+    // Two K-tiles per iteration so both LDS buffers sit at constant offsets:
+    // the compiler can then tell the DMA into one buffer from the ds_reads of
+    // the other and does not drain the in-flight prefetch (vmcnt(0)) before
+    // every K-tile's first fragment read -- with a runtime buffer index it
+    // did, which serialised load and compute.
+    const bool dma = !(p.variant & 128);  // bit 7: no DMA after the prologue (timing probe: compute only)
+    for (int it = 0; it < nt; it += 2) {
+      compute(smem, (dma && it + 1 < nt) ? kb + (it + 1) * BK : -1, smem + CFG::STAGE);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      if (it + 1 < nt) {
+        compute(smem + CFG::STAGE, (dma && it + 2 < nt) ? kb + (it + 2) * BK : -1, smem);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+      }
+    }
+  } else {  // one buffer: latency hidden by the other resident workgroups
+    for (int it = 0; it < nt; ++it) {
+      stage_all(kb + it * BK, smem);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      compute(smem, -1, smem);
+      __syncthreads();
+    }
   }
 
-  // ---- epilogue: lane holds C[m][n0 + wn*64 + j*32 + 8 g + 4 h + e] for its m
+  // ---- epilogue: lane holds C[m][n0 + wn*32FN + j*32 + 8 g + 4 h + e] for its m
   if (p.variant & 16) {  // bit 4: no stores (timing probe); keep acc alive
-    if (acc[0][0][0] == 12345.f && acc[1][1][15] == -1.f) reinterpret_cast<float*>(p.c)[0] = 0.f;
+    if (acc[0][0][0] == 12345.f && acc[FM - 1][FN - 1][15] == -1.f) reinterpret_cast<float*>(p.c)[0] = 0.f;
     return;
   }
   const int h = lane >> 5;
-  auto row_of = [&](int i) { return m0 + wm * 64 + i * 32 + (lane & 31); };
-  auto col_of = [&](int j, int g) { return n0 + wn * 64 + j * 32 + 8 * g + 4 * h; };
+  auto row_of = [&](int i) { return m0 + wm * 32 * FM + i * 32 + (lane & 31); };
+  auto col_of = [&](int j, int g) { return n0 + wn * 32 * FN + j * 32 + 8 * g + 4 * h; };
   if (p.splits > 1) {
     // every K-slice writes its raw fp32 partial tile (N % 8 == 0: a group is all in or all out)
     float* slabs = p.counters ? p.ws : reinterpret_cast<float*>(p.c);
     const int64_t mn = int64_t(p.M) * p.N;
 #pragma unroll
-    for (int i = 0; i < 2; ++i)
+    for (int i = 0; i < FM; ++i)
 #pragma unroll
-      for (int j = 0; j < 2; ++j)
+      for (int j = 0; j < FN; ++j)
 #pragma unroll
         for (int g = 0; g < 4; ++g) {
           const int m = row_of(i), n = col_of(j, g);
@@ -285,17 +389,17 @@ P2_DEVICE void gemm_body(const GemmParams& p, const LA& la, const LB& lb, int ti
     // acc := sum of all slices (own slab included); the 16 groups of a lane are
     // independent loads, so each slice costs one memory round trip
 #pragma unroll
-    for (int i = 0; i < 2; ++i)
+    for (int i = 0; i < FM; ++i)
 #pragma unroll
-      for (int j = 0; j < 2; ++j)
+      for (int j = 0; j < FN; ++j)
 #pragma unroll
         for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.f;
     for (int s2 = 0; s2 < p.splits; ++s2) {
       const float* base = slabs + s2 * mn;
 #pragma unroll
-      for (int i = 0; i < 2; ++i)
+      for (int i = 0; i < FM; ++i)
 #pragma unroll
-        for (int j = 0; j < 2; ++j)
+        for (int j = 0; j < FN; ++j)
 #pragma unroll
           for (int g = 0; g < 4; ++g) {
             const int m = row_of(i), n = col_of(j, g);
@@ -309,9 +413,9 @@ P2_DEVICE void gemm_body(const GemmParams& p, const LA& la, const LB& lb, int ti
   }
   // bias, GELU (+ pre-activation, stored directly), residual: in place on acc
 #pragma unroll
-  for (int i = 0; i < 2; ++i)
+  for (int i = 0; i < FM; ++i)
 #pragma unroll
-    for (int j = 0; j < 2; ++j)
+    for (int j = 0; j < FN; ++j)
 #pragma unroll
       for (int g = 0; g < 4; ++g) {
         const int m = row_of(i), n = col_of(j, g);
@@ -344,22 +448,25 @@ P2_DEVICE void gemm_body(const GemmParams& p, const LA& la, const LB& lb, int ti
   if (!p.c_bf16) return;
   // bf16 C goes out through LDS: a lane's 4-column groups sit on 32 different
   // rows, so direct 8-byte stores scatter over 32 rows per instruction; staged
-  // through a padded [64][128] image (272-byte rows: 2-way bank conflicts at
-  // most), each thread then stores whole 16-byte row chunks, a wave writing 4
-  // contiguous 256-byte row segments per instruction.  Two halves of 64 rows
-  // (17 KB) fit the single-buffer LDS of the 4-workgroup/CU schedule.
-  constexpr int LROW = 272;
+  // through a padded [32 FM][BN] image (rows padded by 16 B: 2-way bank
+  // conflicts at most), each thread then stores whole 16-byte row chunks, a
+  // wave writing contiguous row segments per instruction.  One pass per wave
+  // row (32 FM rows), so the image fits the single-buffer LDS of the
+  // 4-workgroup/CU Tile128 schedule (17 KB) and Tile256's 128 KB (68 KB).
+  constexpr int LROW = CFG::BN * 2 + 16, ROWS = 32 * FM, CPR = CFG::BN / 8;
+  static_assert(ROWS * LROW <= NBUF * CFG::STAGE, "epilogue image must fit the pipeline LDS");
+  static_assert((ROWS * CPR) % CFG::NT == 0, "whole chunks per thread");
 #pragma unroll
-  for (int half = 0; half < 2; ++half) {
-    __syncthreads();  // LDS free: main loop (or previous half) done
+  for (int half = 0; half < CFG::WAVES_M; ++half) {
+    __syncthreads();  // LDS free: main loop (or previous pass) done
     if (wm == half) {
 #pragma unroll
-      for (int i = 0; i < 2; ++i)
+      for (int i = 0; i < FM; ++i)
 #pragma unroll
-        for (int j = 0; j < 2; ++j)
+        for (int j = 0; j < FN; ++j)
 #pragma unroll
           for (int g = 0; g < 4; ++g) {
-            const int r = i * 32 + (lane & 31), c = wn * 64 + j * 32 + 8 * g + 4 * h;
+            const int r = i * 32 + (lane & 31), c = wn * 32 * FN + j * 32 + 8 * g + 4 * h;
             *reinterpret_cast<uint2*>(smem + r * LROW + c * 2) =
                 uint2{pack_bf16x2(acc[i][j][4 * g], acc[i][j][4 * g + 1]),
                       pack_bf16x2(acc[i][j][4 * g + 2], acc[i][j][4 * g + 3])};
@@ -367,9 +474,9 @@ P2_DEVICE void gemm_body(const GemmParams& p, const LA& la, const LB& lb, int ti
     }
     __syncthreads();
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const int chunk = q * NT + tid, r = chunk >> 4, c = chunk & 15;
-      const int m = m0 + half * 64 + r, n = n0 + c * 8;
+    for (int q = 0; q < ROWS * CPR / CFG::NT; ++q) {
+      const int chunk = q * CFG::NT + tid, r = chunk / CPR, c = chunk % CPR;
+      const int m = m0 + half * ROWS + r, n = n0 + c * 8;
       if (m < p.M && n < p.N)
         *reinterpret_cast<uint4*>(reinterpret_cast<uint16_t*>(p.c) + int64_t(m) * p.ldc + n) =
             *reinterpret_cast<const uint4*>(smem + r * LROW + c * 16);
@@ -377,9 +484,10 @@ P2_DEVICE void gemm_body(const GemmParams& p, const LA& la, const LB& lb, int ti
   }
 }
 
+template <class CFG>
 inline int gemm_grid(const GemmParams& p, int& tiles_m, int& tiles_n) {
-  tiles_m = (p.M + BM - 1) / BM;
-  tiles_n = (p.N + BN - 1) / BN;
+  tiles_m = (p.M + CFG::BM - 1) / CFG::BM;
+  tiles_n = (p.N + CFG::BN - 1) / CFG::BN;
   return tiles_m * tiles_n * (p.splits > 1 ? p.splits : 1);
 }
 

@@ -1,12 +1,21 @@
-"""Run one GEMM shape repeatedly (for rocprofv3 counter collection)."""
-import os, sys
+"""Run one square GEMM configuration a few times (for rocprofv3 counter passes): gemm_one.py N VARIANT [lib]."""
+import os
+import sys
+
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
-import torch
-from p2pfl_amd import ops
-M, N, K = (int(v) for v in (sys.argv[1:4] if len(sys.argv) > 3 else (6304, 768, 3072)))
-x = torch.randn(M, K, device="cuda").to(torch.bfloat16)
-w = torch.randn(N, K, device="cuda").to(torch.bfloat16)
-for _ in range(20):
-    ops.gemm(x, w)
+import torch  # noqa: E402
+
+from p2pfl_amd import ops  # noqa: E402
+
+n, v = int(sys.argv[1]), int(sys.argv[2])
+C = ops.ext()
+a = (torch.rand(n, n, device="cuda") * 2 - 1).to(torch.bfloat16)
+b = (torch.rand(n, n, device="cuda") * 2 - 1).to(torch.bfloat16)
+o = torch.empty(n, n, device="cuda", dtype=torch.bfloat16)
+for _ in range(5):
+    if len(sys.argv) > 3:
+        torch.matmul(a, b.t(), out=o)
+    else:
+        C.gemm(a, b, True, True, o, None, False, None, None, 1, v)
 torch.cuda.synchronize()
-print("done", M, N, K)
+print("ok", flush=True)

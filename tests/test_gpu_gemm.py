@@ -107,3 +107,54 @@ def test_vit_block_mlp_uses_native_gemm():
         y = m(x)
     ref = m.fc2(F.gelu(m.fc1(x)))
     torch.testing.assert_close(y.float(), ref, atol=5e-2, rtol=5e-2)
+
+
+# ---- 256 x 256 tile (variant bit 6: 8 waves, 128 x 64 per wave) -------------------------
+@pytest.mark.parametrize("variant", [64, 66])
+@pytest.mark.parametrize("a_kmajor,b_kmajor", [(True, True), (True, False), (False, True), (False, False)])
+@pytest.mark.parametrize("M,N,K", [(256, 256, 64), (600, 520, 200), (1000, 768, 768), (72, 1000, 96)])
+def test_gemm256_layouts_vs_fp32(monkeypatch, variant, a_kmajor, b_kmajor, M, N, K):
+    """Every operand layout on the wide tile; ragged M / N / K and a grid smaller than one tile."""
+    monkeypatch.setattr(gemm_mod, "_VARIANT_ENV", str(variant))
+    a, b = _operands(M, N, K, a_kmajor, b_kmajor, seed=M + N + K + variant)
+    out, _ = ops.gemm(a, b, a_kmajor, b_kmajor, out_dtype=torch.float32)
+    ref, _ = ops.gemm_reference(a, b, a_kmajor, b_kmajor)
+    torch.testing.assert_close(out, ref, atol=2e-3, rtol=1e-4)
+
+
+def test_gemm256_exact_integers(monkeypatch):
+    monkeypatch.setattr(gemm_mod, "_VARIANT_ENV", "64")
+    M, N, K = 520, 392, 256
+    A = torch.randint(-3, 4, (M, K), device="cuda").to(torch.bfloat16)
+    B = (torch.arange(N * K, device="cuda").view(N, K) % 7 - 3).to(torch.bfloat16)
+    for ak, bk in [(True, True), (True, False), (False, True), (False, False)]:
+        a = A if ak else A.t().contiguous()
+        b = B if bk else B.t().contiguous()
+        out, _ = ops.gemm(a, b, ak, bk, out_dtype=torch.float32)
+        assert torch.equal(out, A.float() @ B.float().t()), (ak, bk)
+        outb, _ = ops.gemm(a, b, ak, bk, out_dtype=torch.bfloat16)  # LDS-staged bf16 epilogue
+        assert torch.equal(outb, (A.float() @ B.float().t()).to(torch.bfloat16)), (ak, bk)
+
+
+@pytest.mark.parametrize("splits", [2, 4, 8])
+def test_gemm256_split_k(monkeypatch, splits):
+    monkeypatch.setattr(gemm_mod, "_VARIANT_ENV", "66")
+    M, N, K = 512, 768, 6304
+    a, b = _operands(M, N, K, False, False, seed=splits)
+    out, _ = ops.gemm(a, b, False, False, out_dtype=torch.bfloat16, splits=splits)
+    ref, _ = ops.gemm_reference(a, b, False, False)
+    torch.testing.assert_close(out.float(), ref, atol=0.5, rtol=1e-2)
+
+
+def test_gemm256_epilogue_bias_gelu_residual(monkeypatch):
+    monkeypatch.setattr(gemm_mod, "_VARIANT_ENV", "64")
+    M, N, K = 700, 512, 192
+    a, b = _operands(M, N, K, True, True, seed=5)
+    bias = torch.randn(N, device="cuda")
+    res = torch.randn(M, N, device="cuda").to(torch.bfloat16)
+    out, z = ops.gemm(a, b, bias=bias, gelu=True, want_z=True, residual=res, out_dtype=torch.float32)
+    ref, zref = ops.gemm_reference(a, b, bias=bias, gelu=True, residual=res)
+    torch.testing.assert_close(out, ref, atol=2e-3, rtol=1e-4)
+    torch.testing.assert_close(z.float(), zref, atol=3e-2, rtol=8e-3)
+    outb, _ = ops.gemm(a, b, bias=bias, gelu=True, residual=res, out_dtype=torch.bfloat16)
+    torch.testing.assert_close(outb.float(), ref, atol=5e-2, rtol=1e-2)
