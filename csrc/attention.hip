@@ -33,6 +33,7 @@
 //   dS = P * (dP - rowsum(dO * O)).
 #include "attention.h"
 #include "common.h"
+#include <stdlib.h>
 
 namespace p2attn {
 using namespace p2;
@@ -54,7 +55,10 @@ P2_DEVICE float ex2(float x) { return __builtin_amdgcn_exp2f(x); }
 
 constexpr int kD = 64;
 constexpr int kSP = 260;  // LDS image row length (elements): 520 B rows -> conflict-free 8-B reads
-constexpr int kThreads = 512;  // 8 waves: one block covers all (<= 8) 32-token tiles of a (batch, head)
+// W waves per block, a block per 32 W tokens of a (batch, head).  W = 8 covers
+// ViT's 197 tokens in one block (2 x 12 x 32 = 384 blocks = 1.5 per CU, so half
+// the CUs run two); W = 4 splits them (768 blocks = 3 per CU, the K/V or Q
+// images staged twice).  Chosen per launch (attention_waves()).
 constexpr float kLog2e = 1.4426950408889634f;
 
 P2_DEVICE f32x16 mfma(uint4 a, uint4 b, f32x16 c) {
@@ -92,6 +96,7 @@ P2_DEVICE uint4 lds_frag(const uint16_t* img, int row, int t0) {
 // global loads, then 8 dword LDS writes of (src[t][d], src[t+1][d]) --
 // consecutive lanes take consecutive token pairs, so the writes of a wave
 // hit distinct banks.  All of a thread's loads are issued before any write.
+template <int kThreads>
 P2_DEVICE void stage_transposed(uint16_t* img, const uint16_t* src, int64_t rs, int T, int Tp) {
   constexpr int kItems = (kMaxT / 2) * 8 / kThreads;  // per thread, upper bound
   const int half = Tp >> 1;
@@ -137,9 +142,10 @@ P2_DEVICE float dot64(const uint16_t* a, const uint16_t* b) {
 }
 
 // ---------------------------------------------------------------------------
-// forward.  Grid (1, H, B), 8 waves: wave w owns queries [32 w, +32).  lse2 = log2-domain log-sum-exp of the scaled scores.
+// forward.  Grid (T / 128, H, B), 4 waves: wave w owns queries [32 (4 x + w), +32).  lse2 = log2-domain log-sum-exp of the scaled scores.
 // ---------------------------------------------------------------------------
-__global__ __launch_bounds__(kThreads) void attn_fwd_kernel(const uint16_t* __restrict__ qkv, uint16_t* __restrict__ o,
+template <int kWaves>
+__global__ __launch_bounds__(64 * kWaves) void attn_fwd_kernel(const uint16_t* __restrict__ qkv, uint16_t* __restrict__ o,
                                                        float* __restrict__ lse2, AttnShape sh) {
   __shared__ __attribute__((aligned(16))) uint16_t vt[kD * kSP];
   const int b = blockIdx.z, hd = blockIdx.y, T = sh.T;
@@ -148,10 +154,10 @@ __global__ __launch_bounds__(kThreads) void attn_fwd_kernel(const uint16_t* __re
   const uint16_t* K = Q + sh.C;
   const uint16_t* V = Q + 2 * sh.C;
   const int nkt = (T + 31) >> 5;
-  stage_transposed(vt, V, rs, T, nkt * 32);
+  stage_transposed<64 * kWaves>(vt, V, rs, T, nkt * 32);
   __syncthreads();
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, r = lane & 31, h = lane >> 5;
-  const int q0 = (blockIdx.x * 8 + wave) * 32;
+  const int q0 = (blockIdx.x * kWaves + wave) * 32;
   if (q0 >= T) return;  // no barrier below
   const bool qv = q0 + r < T;
   uint4 qf[4];
@@ -226,10 +232,11 @@ __global__ __launch_bounds__(kThreads) void attn_fwd_kernel(const uint16_t* __re
 }
 
 // ---------------------------------------------------------------------------
-// backward pass 1: dK, dV.  Grid (1, H, B), wave w owns keys [32 w, +32)
+// backward pass 1: dK, dV.  Grid (T / 128, H, B), wave w owns keys [32 (4 x + w), +32)
 // and loops over all query tiles (next tile's Q / dO rows prefetched).
 // ---------------------------------------------------------------------------
-__global__ __launch_bounds__(kThreads) void attn_bwd_dkdv_kernel(const uint16_t* __restrict__ qkv,
+template <int kWaves>
+__global__ __launch_bounds__(64 * kWaves) void attn_bwd_dkdv_kernel(const uint16_t* __restrict__ qkv,
                                                             const uint16_t* __restrict__ o,
                                                             const uint16_t* __restrict__ dout,
                                                             const float* __restrict__ lse2,
@@ -246,8 +253,8 @@ __global__ __launch_bounds__(kThreads) void attn_bwd_dkdv_kernel(const uint16_t*
   const uint16_t* DO = dout + b * sh.o_batch + hd * kD;
   const float* L = lse2 + (int64_t(b) * sh.H + hd) * T;
   const int nqt = (T + 31) >> 5, Tp = nqt * 32;
-  stage_transposed(qtl, Q, rs, T, Tp);
-  stage_transposed(dotl, DO, sh.o_row, T, Tp);
+  stage_transposed<64 * kWaves>(qtl, Q, rs, T, Tp);
+  stage_transposed<64 * kWaves>(dotl, DO, sh.o_row, T, Tp);
   for (int t = threadIdx.x; t < Tp; t += blockDim.x) {
     const bool ok = t < T;
     s_lse[t] = ok ? L[t] : INFINITY;  // padded queries: P = exp2(-inf) = 0
@@ -255,7 +262,7 @@ __global__ __launch_bounds__(kThreads) void attn_bwd_dkdv_kernel(const uint16_t*
   }
   __syncthreads();
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, r = lane & 31, h = lane >> 5;
-  const int k0 = (blockIdx.x * 8 + wave) * 32;
+  const int k0 = (blockIdx.x * kWaves + wave) * 32;
   if (k0 >= T) return;
   const bool kv = k0 + r < T;
   uint4 kf[4], vf[4];
@@ -325,10 +332,11 @@ __global__ __launch_bounds__(kThreads) void attn_bwd_dkdv_kernel(const uint16_t*
 }
 
 // ---------------------------------------------------------------------------
-// backward pass 2: dQ.  Grid (1, H, B), wave w owns queries [32 w, +32)
+// backward pass 2: dQ.  Grid (T / 128, H, B), wave w owns queries [32 (4 x + w), +32)
 // and loops over all key tiles (next tile's K / V rows prefetched).
 // ---------------------------------------------------------------------------
-__global__ __launch_bounds__(kThreads) void attn_bwd_dq_kernel(const uint16_t* __restrict__ qkv,
+template <int kWaves>
+__global__ __launch_bounds__(64 * kWaves) void attn_bwd_dq_kernel(const uint16_t* __restrict__ qkv,
                                                           const uint16_t* __restrict__ o,
                                                           const uint16_t* __restrict__ dout,
                                                           const float* __restrict__ lse2, uint16_t* __restrict__ dqkv,
@@ -342,10 +350,10 @@ __global__ __launch_bounds__(kThreads) void attn_bwd_dq_kernel(const uint16_t* _
   const uint16_t* O = o + b * sh.o_batch + hd * kD;
   const uint16_t* DO = dout + b * sh.o_batch + hd * kD;
   const int nkt = (T + 31) >> 5;
-  stage_transposed(ktl, K, rs, T, nkt * 32);
+  stage_transposed<64 * kWaves>(ktl, K, rs, T, nkt * 32);
   __syncthreads();
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, r = lane & 31, h = lane >> 5;
-  const int q0 = (blockIdx.x * 8 + wave) * 32;
+  const int q0 = (blockIdx.x * kWaves + wave) * 32;
   if (q0 >= T) return;
   const int qq = q0 + r;
   const bool qv = qq < T;
@@ -429,16 +437,36 @@ __global__ __launch_bounds__(kThreads) void attn_bwd_dq_kernel(const uint16_t* _
 // ---------------------------------------------------------------------------
 // launchers
 // ---------------------------------------------------------------------------
-static dim3 grid_of(const AttnShape& sh) { return dim3((sh.T + 255) / 256, sh.H, sh.B); }
+template <int W>
+static dim3 grid_of(const AttnShape& sh) { return dim3((sh.T + 32 * W - 1) / (32 * W), sh.H, sh.B); }
+
+// 8-wave blocks unless P2PFL_ATTN_WAVES=4 (A/B switch, read once; measured at
+// the ViT shape: fwd 21.8 vs 23.7 us, fwd+bwd 118 vs 121 us -- the kernels are
+// VALU-bound, the 1.5-blocks-per-CU imbalance costs less than staging twice)
+static int attention_waves() {
+  static const int w = [] {
+    const char* e = getenv("P2PFL_ATTN_WAVES");
+    return (e && atoi(e) == 4) ? 4 : 8;
+  }();
+  return w;
+}
 
 void attention_fwd(const uint16_t* qkv, uint16_t* o, float* lse2, const AttnShape& sh, hipStream_t s) {
-  hipLaunchKernelGGL(attn_fwd_kernel, grid_of(sh), dim3(kThreads), 0, s, qkv, o, lse2, sh);
+  if (attention_waves() == 8)
+    hipLaunchKernelGGL(attn_fwd_kernel<8>, grid_of<8>(sh), dim3(512), 0, s, qkv, o, lse2, sh);
+  else
+    hipLaunchKernelGGL(attn_fwd_kernel<4>, grid_of<4>(sh), dim3(256), 0, s, qkv, o, lse2, sh);
 }
 
 void attention_bwd(const uint16_t* qkv, const uint16_t* o, const uint16_t* dout, const float* lse2, uint16_t* dqkv,
                    const AttnShape& sh, hipStream_t s) {
-  hipLaunchKernelGGL(attn_bwd_dkdv_kernel, grid_of(sh), dim3(kThreads), 0, s, qkv, o, dout, lse2, dqkv, sh);
-  hipLaunchKernelGGL(attn_bwd_dq_kernel, grid_of(sh), dim3(kThreads), 0, s, qkv, o, dout, lse2, dqkv, sh);
+  if (attention_waves() == 8) {
+    hipLaunchKernelGGL(attn_bwd_dkdv_kernel<8>, grid_of<8>(sh), dim3(512), 0, s, qkv, o, dout, lse2, dqkv, sh);
+    hipLaunchKernelGGL(attn_bwd_dq_kernel<8>, grid_of<8>(sh), dim3(512), 0, s, qkv, o, dout, lse2, dqkv, sh);
+  } else {
+    hipLaunchKernelGGL(attn_bwd_dkdv_kernel<4>, grid_of<4>(sh), dim3(256), 0, s, qkv, o, dout, lse2, dqkv, sh);
+    hipLaunchKernelGGL(attn_bwd_dq_kernel<4>, grid_of<4>(sh), dim3(256), 0, s, qkv, o, dout, lse2, dqkv, sh);
+  }
 }
 
 }  // namespace p2attn

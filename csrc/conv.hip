@@ -165,7 +165,7 @@ struct ConvWgradB {
 
 template <int NBUF, class LA, class LB>
 __global__ __launch_bounds__(NT, NBUF == 1 ? 3 : 2) void conv_kernel(GemmParams p, LA la, LB lb, int tiles_m, int tiles_n) {
-  __shared__ __attribute__((aligned(16))) char smem[NBUF * Tile128::STAGE];
+  __shared__ __attribute__((aligned(16))) char smem[smem_bytes<Tile128, NBUF>()];
   gemm_body<Tile128, NBUF>(p, la, lb, tiles_m, tiles_n, smem);
 }
 

@@ -39,15 +39,15 @@ namespace p2gemm {
 
 template <int NBUF, class LA, class LB>
 __global__ __launch_bounds__(NT, NBUF == 1 ? 4 : 2) void gemm_kernel(GemmParams p, LA la, LB lb, int tiles_m, int tiles_n) {
-  __shared__ __attribute__((aligned(16))) char smem[NBUF * Tile128::STAGE];  // [buf][A | B]
+  __shared__ __attribute__((aligned(16))) char smem[smem_bytes<Tile128, NBUF>()];  // [buf][A | B]
   gemm_body<Tile128, NBUF>(p, la, lb, tiles_m, tiles_n, smem);
 }
 
-// 256 x 256 tile, 8 waves, one workgroup per CU (128 KB of LDS, up to 256
+// 256 x 256 tile, 8 waves, one workgroup per CU (132 KB of LDS, up to 256
 // registers per lane at two waves per SIMD).
 template <class LA, class LB>
 __global__ __launch_bounds__(Tile256::NT) void gemm256_kernel(GemmParams p, LA la, LB lb, int tiles_m, int tiles_n) {
-  __shared__ __attribute__((aligned(16))) char smem[2 * Tile256::STAGE];
+  __shared__ __attribute__((aligned(16))) char smem[smem_bytes<Tile256, 2>()];
   gemm_body<Tile256, 2>(p, la, lb, tiles_m, tiles_n, smem);
 }
 

@@ -200,6 +200,15 @@ P2_DEVICE int xcd_remap(int orig, int nwg) {
   return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + orig / 8;
 }
 
+// LDS bytes a kernel of this shape declares: the pipeline stages, and for the
+// 8-wave tile at least the whole bf16 output tile (padded rows), so its
+// epilogue stages C in one pass (132 KB; still one workgroup per CU).
+template <class CFG, int NBUF>
+constexpr int smem_bytes() {
+  constexpr int pipe = NBUF * CFG::STAGE, epi = CFG::BM * (CFG::BN * 2 + 16);
+  return (CFG::NT >= 512 && epi > pipe) ? epi : pipe;
+}
+
 // The whole kernel body.  `p` carries M/N/K, split-K and the epilogue.
 template <class CFG, int NBUF, class LA, class LB>
 P2_DEVICE void gemm_body(const GemmParams& p, const LA& la, const LB& lb, int tiles_m, int tiles_n, char* smem) {
@@ -453,20 +462,25 @@ P2_DEVICE void gemm_body(const GemmParams& p, const LA& la, const LB& lb, int ti
   // wave writing contiguous row segments per instruction.  One pass per wave
   // row (32 FM rows), so the image fits the single-buffer LDS of the
   // 4-workgroup/CU Tile128 schedule (17 KB) and Tile256's 128 KB (68 KB).
-  constexpr int LROW = CFG::BN * 2 + 16, ROWS = 32 * FM, CPR = CFG::BN / 8;
-  static_assert(ROWS * LROW <= NBUF * CFG::STAGE, "epilogue image must fit the pipeline LDS");
+  constexpr int LROW = CFG::BN * 2 + 16, CPR = CFG::BN / 8;
+  // one pass over the whole tile when the kernel's LDS holds its image
+  // (smem_bytes), else one pass per wave row
+  constexpr bool ONE = CFG::BM * LROW <= smem_bytes<CFG, NBUF>();
+  constexpr int PASSES = ONE ? 1 : CFG::WAVES_M, ROWS = CFG::BM / PASSES;
+  static_assert(ROWS * LROW <= smem_bytes<CFG, NBUF>(), "epilogue image must fit the kernel's LDS");
   static_assert((ROWS * CPR) % CFG::NT == 0, "whole chunks per thread");
 #pragma unroll
-  for (int half = 0; half < CFG::WAVES_M; ++half) {
+  for (int pass = 0; pass < PASSES; ++pass) {
     __syncthreads();  // LDS free: main loop (or previous pass) done
-    if (wm == half) {
+    if (ONE || wm == pass) {
+      const int rbase = ONE ? wm * 32 * FM : 0;
 #pragma unroll
       for (int i = 0; i < FM; ++i)
 #pragma unroll
         for (int j = 0; j < FN; ++j)
 #pragma unroll
           for (int g = 0; g < 4; ++g) {
-            const int r = i * 32 + (lane & 31), c = wn * 32 * FN + j * 32 + 8 * g + 4 * h;
+            const int r = rbase + i * 32 + (lane & 31), c = wn * 32 * FN + j * 32 + 8 * g + 4 * h;
             *reinterpret_cast<uint2*>(smem + r * LROW + c * 2) =
                 uint2{pack_bf16x2(acc[i][j][4 * g], acc[i][j][4 * g + 1]),
                       pack_bf16x2(acc[i][j][4 * g + 2], acc[i][j][4 * g + 3])};
@@ -476,7 +490,7 @@ P2_DEVICE void gemm_body(const GemmParams& p, const LA& la, const LB& lb, int ti
 #pragma unroll
     for (int q = 0; q < ROWS * CPR / CFG::NT; ++q) {
       const int chunk = q * CFG::NT + tid, r = chunk / CPR, c = chunk % CPR;
-      const int m = m0 + half * ROWS + r, n = n0 + c * 8;
+      const int m = m0 + pass * ROWS + r, n = n0 + c * 8;
       if (m < p.M && n < p.N)
         *reinterpret_cast<uint4*>(reinterpret_cast<uint16_t*>(p.c) + int64_t(m) * p.ldc + n) =
             *reinterpret_cast<const uint4*>(smem + r * LROW + c * 16);

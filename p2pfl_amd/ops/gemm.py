@@ -83,9 +83,13 @@ def _product(a, b, a_kmajor, b_kmajor, dtype, splits=1):
 _VARIANT_ENV = os.environ.get("P2PFL_GEMM_VARIANT")
 
 
-def _variant(a_kmajor: bool, splits: int) -> int:
+def _variant(a_kmajor: bool, splits: int, M: int = 0, N: int = 0, K: int = 0) -> int:
     if _VARIANT_ENV is not None:
         return int(_VARIANT_ENV)
+    if splits == 1 and M * N >= 4096 * 4096 and K >= 2048:
+        # large products: the 256 x 256 8-wave tile (half the operand bytes
+        # per FLOP; profiles/r2_gemm_256.md), grouped XCD-local tile order
+        return 64
     return 2 if (splits > 1 or not a_kmajor) else 10
 
 
@@ -111,6 +115,7 @@ def gemm(
     """
     M = a.shape[0] if a_kmajor else a.shape[1]
     N = b.shape[0] if b_kmajor else b.shape[1]
+    K = a.shape[1] if a_kmajor else a.shape[0]
     dev = a.device
     if splits > 1:
         if out is None:
@@ -129,7 +134,7 @@ def gemm(
     if out is None:
         out = torch.empty((M, N), dtype=out_dtype, device=dev)
     z = torch.empty((M, N), dtype=torch.bfloat16, device=dev) if (gelu and want_z) else None
-    _C().gemm(a, b, a_kmajor, b_kmajor, out, bias, gelu, z, residual, 1, _variant(a_kmajor, 1))
+    _C().gemm(a, b, a_kmajor, b_kmajor, out, bias, gelu, z, residual, 1, _variant(a_kmajor, 1, M, N, K))
     return out, z
 
 
@@ -233,6 +238,7 @@ def _native_faster(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor
     x2 = x.detach().reshape(M, K).to(torch.bfloat16)
     wd = w.detach().to(torch.bfloat16)
     bd = bias.detach() if bias is not None else None
+    bd16 = bd.to(torch.bfloat16) if bd is not None else None  # the library path outside autocast needs one dtype
     dy = torch.randn(M, N, device=x.device).to(torch.bfloat16)
 
     def native():
@@ -248,7 +254,7 @@ def _native_faster(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor
         if gelu:
             bias_gelu(linear_blas(x2, wd, None), bd)
         else:
-            linear_blas(x2, wd, bd)
+            linear_blas(x2, wd, bd16)
         if grad:
             dy @ wd
             dy.t() @ x2

@@ -1,39 +1,24 @@
-"""Fused attention kernel vs PyTorch SDPA at the ViT-B/16 shape (B=32, T=197, H=12, d=64)."""
-import sys
+"""Fused attention fwd / fwd+bwd at the ViT-B/16 shape (B 32, T 197, 12 heads x 64): us per call.
+Run twice with P2PFL_ATTN_WAVES=4 / 8 to compare block shapes."""
 import os
+import sys
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import torch  # noqa: E402
-import torch.nn.functional as F  # noqa: E402
 
 from p2pfl_amd import ops  # noqa: E402
+from p2pfl_amd.ops.fused import attention_qkv  # noqa: E402
+from scripts.gemm_bench import timeit  # noqa: E402
 
-
-def sdpa(qkv, H):
-    B, T, C3 = qkv.shape
-    C = C3 // 3
-    q, k, v = qkv.view(B, T, 3, H, C // H).permute(2, 0, 3, 1, 4)
-    return F.scaled_dot_product_attention(q, k, v).transpose(1, 2).reshape(B, T, C)
-
-
-def timeit(fn, iters=50):
-    for _ in range(5):
-        fn()
-    torch.cuda.synchronize()
-    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    s.record()
-    for _ in range(iters):
-        fn()
-    e.record()
-    torch.cuda.synchronize()
-    return s.elapsed_time(e) / iters * 1e3
-
-
+ops.ext()
 B, T, H = 32, 197, 12
-qkv = torch.randn(B, T, 3 * 64 * H, device="cuda", dtype=torch.bfloat16, requires_grad=True)
-g = torch.randn(B, T, 64 * H, device="cuda", dtype=torch.bfloat16)
-for name, f in (("fused", lambda: ops.attention_qkv(qkv, H)), ("sdpa", lambda: sdpa(qkv, H))):
-    with torch.no_grad():
-        tf = timeit(f)
-    tb = timeit(lambda: f().backward(g))
-    print(f"{name:6s} fwd {tf:7.1f} us   fwd+bwd {tb:7.1f} us", flush=True)
+qkv = torch.randn(B, T, 3 * H * 64, device="cuda").to(torch.bfloat16).requires_grad_()
+g = torch.randn(B, T, H * 64, device="cuda").to(torch.bfloat16)
+fwd = timeit(lambda: attention_qkv(qkv.detach(), H), iters=50)
+def fb():
+    o = attention_qkv(qkv, H)
+    o.backward(g)
+both = timeit(fb, iters=50)
+fl = 4 * B * H * T * T * 64
+print(f"waves={os.environ.get('P2PFL_ATTN_WAVES', '4')}: fwd {fwd * 1e6:.1f} us ({fl / fwd / 1e12:.0f} TF/s), "
+      f"fwd+bwd {both * 1e6:.1f} us ({3.5 * fl / both / 1e12:.0f} TF/s)", flush=True)
