@@ -302,6 +302,14 @@ def run_gossip(args, env: _Env) -> dict:
         # per-round phase breakdown from the tracer (this rank, timed rounds)
         sp = lambda name: [s for s in logger.tracer.spans(node.addr, name) if s.start >= marks[W]]  # noqa: E731
         ph = {k: sum(s.duration for s in sp(k)) / max(1, K) * 1e3 for k in ("evaluate", "fit", "wait_aggregation", "aggregate")}
+        if os.environ.get("P2PFL_BENCH_SPANS"):
+            tot: dict = {}
+            for s in logger.tracer.spans(node.addr):
+                if s.start >= marks[W]:
+                    tot[s.name] = tot.get(s.name, 0.0) + s.duration
+            print(f"[bench rank {env.rank}] all spans, ms per round: "
+                  + ", ".join(f"{k} {v / max(1, K) * 1e3:.2f}" for k, v in sorted(tot.items(), key=lambda kv: -kv[1])),
+                  file=sys.stderr, flush=True)
         pushes = logger.tracer.counters(node.addr)
         stats = dict(plane.stats) if plane is not None else {}
         print(

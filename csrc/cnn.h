@@ -75,10 +75,10 @@ void fc1_wgrad_adam(const uint16_t* dH, const uint16_t* a1, int mrows, float* pa
 // backward fused into the epilogue -> dC2 map [B][64][14x16] (all 4 window
 // positions written, so no clearing; cols 14/15 stay zero from allocation) and
 // the fp32 alive-masked dA1 [B][3136] (conv2 bias terms); plus, in extra
-// blocks, the FC2 weight/bias gradient with Adam.
+// blocks (with_fc2), the FC2 weight/bias gradient with Adam.
 void route_fc2(const uint16_t* dH, const uint16_t* w1t, const uint8_t* am2, int mrows, int B, uint16_t* dc2m,
                float* gb, const float* dlogits, const uint16_t* H, float* params, float* m, float* v, float* gdump,
-               Offsets off, const int* adam_t, int t_off, AdamCfg cfg, hipStream_t s);
+               Offsets off, const int* adam_t, int t_off, AdamCfg cfg, bool with_fc2, hipStream_t s);
 
 // One launch: conv2 input gradient + pool1/ReLU backward + conv1 weight
 // gradient (-> wslab1 [B][7][832]) and conv2 weight gradient
@@ -91,11 +91,13 @@ void conv_adam(const float* wslab1, const float* wslab2, const float* gb, int B,
                hipStream_t s);
 
 // conv_adam and fc1_wgrad_adam in one launch (run after conv2_bwd): the conv
-// reduction + Adam blocks hide behind the HBM-bound FC1 Adam stream.
+// reduction + Adam blocks hide behind the HBM-bound FC1 Adam stream.  With
+// dlogits / H non-null the FC2 gradient + Adam blocks join the launch too
+// (then route_fc2 runs with with_fc2 = false).
 void fc1_conv_adam(const uint16_t* dH, const uint16_t* a1, int mrows, const float* wslab1, const float* wslab2,
                    const float* gb, int B, float* params, float* m, float* v, float* gdump, uint16_t* w1bf,
                    uint16_t* w1tbf, uint16_t* w2r, uint16_t* w2q, Offsets off, const int* adam_t, int t_off,
-                   AdamCfg cfg, hipStream_t s);
+                   AdamCfg cfg, const float* dlogits, const uint16_t* H, hipStream_t s);
 
 // Standalone packing of the bf16 shadows from fp32 params (after set_parameters).
 void pack_shadows(const float* params, Offsets off, uint16_t* w2r, uint16_t* w2q, uint16_t* w1bf, uint16_t* w1tbf,

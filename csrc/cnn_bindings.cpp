@@ -132,7 +132,8 @@ void k_fc1_wgrad_adam(torch::Tensor dH, torch::Tensor a1, int64_t mrows, torch::
 void k_route_fc2(torch::Tensor dH, torch::Tensor w1tbf, torch::Tensor am2, int64_t mrows, int64_t B,
                  torch::Tensor dc2m, torch::Tensor gb, torch::Tensor dlogits, torch::Tensor H, torch::Tensor params,
                  torch::Tensor m, torch::Tensor v, c10::optional<torch::Tensor> gdump, std::vector<int64_t> off,
-                 torch::Tensor adam_t, int64_t t_off, double lr, double b1, double b2, double eps, double wd) {
+                 torch::Tensor adam_t, int64_t t_off, double lr, double b1, double b2, double eps, double wd,
+                 bool with_fc2) {
   const c10::DeviceGuard g(dH.device());
   check_batch(int(B), int(mrows));
   Offsets o = offsets(off);
@@ -146,7 +147,8 @@ void k_route_fc2(torch::Tensor dH, torch::Tensor w1tbf, torch::Tensor am2, int64
                    reinterpret_cast<uint16_t*>(ptr<at::BFloat16>(H, torch::kBFloat16, B * 2048, "H")),
                    ptr<float>(params, torch::kFloat32, n, "params"), ptr<float>(m, torch::kFloat32, n, "m"),
                    ptr<float>(v, torch::kFloat32, n, "v"), optr<float>(gdump, torch::kFloat32, n, "gdump"), o,
-                   ptr<int>(adam_t, torch::kInt32, 1, "adam_t", 4), int(t_off), cfg(lr, b1, b2, eps, wd), stream());
+                   ptr<int>(adam_t, torch::kInt32, 1, "adam_t", 4), int(t_off), cfg(lr, b1, b2, eps, wd), with_fc2,
+                   stream());
 }
 
 void k_conv2_bwd(torch::Tensor dc2m, torch::Tensor p1s, torch::Tensor am1, torch::Tensor w2q, torch::Tensor x,
@@ -188,9 +190,11 @@ void k_fc1_conv_adam(torch::Tensor dH, torch::Tensor a1, int64_t mrows, torch::T
                      torch::Tensor gb, int64_t B, torch::Tensor params, torch::Tensor m, torch::Tensor v,
                      c10::optional<torch::Tensor> gdump, torch::Tensor w1bf, torch::Tensor w1tbf, torch::Tensor w2r,
                      torch::Tensor w2q, std::vector<int64_t> off, torch::Tensor adam_t, int64_t t_off, double lr,
-                     double b1, double b2, double eps, double wd) {
+                     double b1, double b2, double eps, double wd, c10::optional<torch::Tensor> dlogits,
+                     c10::optional<torch::Tensor> H) {
   const c10::DeviceGuard g(params.device());
   check_batch(int(B), int(mrows));
+  TORCH_CHECK(dlogits.has_value() == H.has_value(), "fc1_conv_adam: pass both dlogits and H or neither");
   Offsets o = offsets(off);
   const int64_t n = params_end(o);
   p2cnn::fc1_conv_adam(
@@ -205,7 +209,9 @@ void k_fc1_conv_adam(torch::Tensor dH, torch::Tensor a1, int64_t mrows, torch::T
       reinterpret_cast<uint16_t*>(ptr<at::BFloat16>(w1tbf, torch::kBFloat16, 2048 * 3136, "w1tbf")),
       reinterpret_cast<uint16_t*>(ptr<at::BFloat16>(w2r, torch::kBFloat16, 51200, "w2r")),
       reinterpret_cast<uint16_t*>(ptr<at::BFloat16>(w2q, torch::kBFloat16, 51200, "w2q")), o,
-      ptr<int>(adam_t, torch::kInt32, 1, "adam_t", 4), int(t_off), cfg(lr, b1, b2, eps, wd), stream());
+      ptr<int>(adam_t, torch::kInt32, 1, "adam_t", 4), int(t_off), cfg(lr, b1, b2, eps, wd),
+      optr<float>(dlogits, torch::kFloat32, B * 10, "dlogits"),
+      reinterpret_cast<const uint16_t*>(optr<at::BFloat16>(H, torch::kBFloat16, B * 2048, "H")), stream());
 }
 
 void k_pack_shadows(torch::Tensor params, std::vector<int64_t> off, torch::Tensor w2r, torch::Tensor w2q,
@@ -233,10 +239,17 @@ void register_cnn(pybind11::module& m) {
   c.def("conv2_fwd", &k_conv2_fwd);
   c.def("gemm_skinny", &k_gemm_skinny);
   c.def("head", &k_head);
-  c.def("route_fc2", &k_route_fc2);
+  c.def("route_fc2", &k_route_fc2, pybind11::arg("dH"), pybind11::arg("w1tbf"), pybind11::arg("am2"), pybind11::arg("mrows"), pybind11::arg("B"),
+        pybind11::arg("dc2m"), pybind11::arg("gb"), pybind11::arg("dlogits"), pybind11::arg("H"), pybind11::arg("params"), pybind11::arg("m"), pybind11::arg("v"),
+        pybind11::arg("gdump"), pybind11::arg("off"), pybind11::arg("adam_t"), pybind11::arg("t_off"), pybind11::arg("lr"), pybind11::arg("b1"),
+        pybind11::arg("b2"), pybind11::arg("eps"), pybind11::arg("wd"), pybind11::arg("with_fc2") = true);
   c.def("fc1_wgrad_adam", &k_fc1_wgrad_adam);
   c.def("conv2_bwd", &k_conv2_bwd);
   c.def("conv_adam", &k_conv_adam);
-  c.def("fc1_conv_adam", &k_fc1_conv_adam);
+  c.def("fc1_conv_adam", &k_fc1_conv_adam, pybind11::arg("dH"), pybind11::arg("a1"), pybind11::arg("mrows"), pybind11::arg("wslab1"),
+        pybind11::arg("wslab2"), pybind11::arg("gb"), pybind11::arg("B"), pybind11::arg("params"), pybind11::arg("m"), pybind11::arg("v"), pybind11::arg("gdump"),
+        pybind11::arg("w1bf"), pybind11::arg("w1tbf"), pybind11::arg("w2r"), pybind11::arg("w2q"), pybind11::arg("off"), pybind11::arg("adam_t"),
+        pybind11::arg("t_off"), pybind11::arg("lr"), pybind11::arg("b1"), pybind11::arg("b2"), pybind11::arg("eps"), pybind11::arg("wd"),
+        pybind11::arg("dlogits") = pybind11::none(), pybind11::arg("H") = pybind11::none());
   c.def("pack_shadows", &k_pack_shadows);
 }

@@ -79,13 +79,14 @@ P2_DEVICE float adam_apply(float* __restrict__ p, float* __restrict__ m, float* 
 //    parameter: dW2[c][k] = sum_b dlogits[b][c] H[b][k].
 // ---------------------------------------------------------------------------
 constexpr int kRouteBlocks = kFeat / 32;                       // 98
-constexpr int kFc2Blocks = (kCls * kHid + kCls + 511) / 512;   // 41
+constexpr int kFc2Blocks = (kCls * kHid + kCls + 511) / 512;   // 41 (512-thread blocks)
 
+template <int TPB>
 P2_DEVICE void fc2_role(int blk, const float* __restrict__ dlogits, const uint16_t* __restrict__ H, int B,
                         float* __restrict__ p, float* __restrict__ m, float* __restrict__ v,
                         float* __restrict__ gdump, const Offsets& off, const int* __restrict__ adam_t, int t_off,
                         const AdamCfg& cfg) {
-  const int e = blk * 512 + threadIdx.x;
+  const int e = blk * TPB + threadIdx.x;
   const int nW = kCls * kHid;
   if (e >= nW + kCls) return;
   const int64_t pi = e < nW ? off.l2w + e : off.l2b + (e - nW);
@@ -123,13 +124,14 @@ __global__ __launch_bounds__(512) void route_fc2_kernel(const uint16_t* __restri
                                                         float* __restrict__ m, float* __restrict__ v,
                                                         float* __restrict__ gdump, Offsets off,
                                                         const int* __restrict__ adam_t, int t_off, AdamCfg cfg) {
-  if (blockIdx.x >= kRouteBlocks) {
-    fc2_role(blockIdx.x - kRouteBlocks, dlogits, H, B, p, m, v, gdump, off, adam_t, t_off, cfg);
+  const int bid = blockIdx.x;
+  if (bid >= kRouteBlocks) {
+    fc2_role<512>(bid - kRouteBlocks, dlogits, H, B, p, m, v, gdump, off, adam_t, t_off, cfg);
     return;
   }
   __shared__ float red[8 * MT * 1024];
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, r = lane & 31, h = lane >> 5;
-  const int n0 = blockIdx.x * 32;
+  const int n0 = bid * 32;
   constexpr int K = kHid, NG = K / 64;
   // argmax codes of this thread's epilogue elements (independent of the GEMM)
   uint8_t acode[2 * MT];
@@ -194,8 +196,8 @@ __global__ __launch_bounds__(512) void route_fc2_kernel(const uint16_t* __restri
 
 void route_fc2(const uint16_t* dH, const uint16_t* w1t, const uint8_t* am2, int mrows, int B, uint16_t* dc2m,
                float* gb, const float* dlogits, const uint16_t* H, float* params, float* m, float* v, float* gdump,
-               Offsets off, const int* adam_t, int t_off, AdamCfg cfg, hipStream_t s) {
-  const dim3 grid(kRouteBlocks + kFc2Blocks);
+               Offsets off, const int* adam_t, int t_off, AdamCfg cfg, bool with_fc2, hipStream_t s) {
+  const dim3 grid(kRouteBlocks + (with_fc2 ? kFc2Blocks : 0));
   if (mrows == 32)
     hipLaunchKernelGGL(route_fc2_kernel<1>, grid, dim3(512), 0, s, dH, w1t, am2, B, dc2m, gb, dlogits, H, params, m,
                        v, gdump, off, adam_t, t_off, cfg);
@@ -725,23 +727,33 @@ __global__ __launch_bounds__(256) void conv_adam_kernel(const float* __restrict_
 }
 
 // ---------------------------------------------------------------------------
-// 7+10 in one launch (after conv2_bwd): the 116 conv-parameter blocks first,
-// then the 1600 FC1 weight-gradient + Adam blocks.  The FC1 part streams the
-// 6.4M-parameter Adam state (HBM-bound, ~28 B per parameter); the conv part is
-// a latency-bound reduction -- sharing the launch hides the latter behind the
-// former instead of paying a kernel boundary and its tail.
+// 7+10 in one launch (after conv2_bwd): optionally the 81 FC2 Adam blocks,
+// then the 116 conv-parameter blocks, then the 1600 FC1 weight-gradient + Adam
+// blocks.  The FC1 part streams the 6.4M-parameter Adam state (HBM-bound, ~28
+// B per parameter); the FC2 and conv parts are latency-bound reductions --
+// sharing the launch hides them behind the stream instead of paying a kernel
+// boundary and their tails.  (The FC2 role used to share route_fc2's launch:
+// there the two roles did not overlap -- 11.8 us together vs 6.7 us for the
+// dA1 blocks alone and 7.4 us for the FC2 blocks alone, scripts/kbench.py.)
 // ---------------------------------------------------------------------------
+constexpr int kFc2Blocks256 = (kCls * kHid + kCls + 255) / 256;  // 81
+
 template <int MR>
 __global__ __launch_bounds__(256) void fc1_conv_adam_kernel(
     const uint16_t* __restrict__ dH, const uint16_t* __restrict__ a1, const float* __restrict__ ws1,
     const float* __restrict__ ws2, const float* __restrict__ gb, int B, float* __restrict__ p, float* __restrict__ m,
     float* __restrict__ v, float* __restrict__ gdump, uint16_t* __restrict__ w1bf, uint16_t* __restrict__ w1tbf,
     uint16_t* __restrict__ w2r, uint16_t* __restrict__ w2q, Offsets off, const int* __restrict__ adam_t, int t_off,
-    AdamCfg cfg) {
+    AdamCfg cfg, const float* __restrict__ dlogits, const uint16_t* __restrict__ H, int nf2) {
   constexpr int kLds = Fc1Lds<MR>::kBytes > kConvAdamLds ? Fc1Lds<MR>::kBytes : kConvAdamLds;
   __shared__ __attribute__((aligned(16))) char smem[kLds];
   constexpr int kCA = kC2 + kC1Blocks, kBx = (kFeat + 127) / 128;
-  const int j = blockIdx.x;
+  int j = blockIdx.x;
+  if (j < nf2) {
+    fc2_role<256>(j, dlogits, H, B, p, m, v, gdump, off, adam_t, t_off, cfg);
+    return;
+  }
+  j -= nf2;
   if (j < kCA) {
     conv_adam_body(j, ws1, ws2, gb, B, p, m, v, gdump, w2r, w2q, off, adam_t, t_off, cfg, smem);
     return;
@@ -753,14 +765,15 @@ __global__ __launch_bounds__(256) void fc1_conv_adam_kernel(
 void fc1_conv_adam(const uint16_t* dH, const uint16_t* a1, int mrows, const float* wslab1, const float* wslab2,
                    const float* gb, int B, float* params, float* m, float* v, float* gdump, uint16_t* w1bf,
                    uint16_t* w1tbf, uint16_t* w2r, uint16_t* w2q, Offsets off, const int* adam_t, int t_off,
-                   AdamCfg cfg, hipStream_t s) {
-  const dim3 grid(kC2 + kC1Blocks + ((kFeat + 127) / 128) * (kHid / 32));
+                   AdamCfg cfg, const float* dlogits, const uint16_t* H, hipStream_t s) {
+  const int nf2 = dlogits ? kFc2Blocks256 : 0;
+  const dim3 grid(nf2 + kC2 + kC1Blocks + ((kFeat + 127) / 128) * (kHid / 32));
   if (mrows == 32)
     hipLaunchKernelGGL(fc1_conv_adam_kernel<32>, grid, dim3(256), 0, s, dH, a1, wslab1, wslab2, gb, B, params, m, v,
-                       gdump, w1bf, w1tbf, w2r, w2q, off, adam_t, t_off, cfg);
+                       gdump, w1bf, w1tbf, w2r, w2q, off, adam_t, t_off, cfg, dlogits, H, nf2);
   else
     hipLaunchKernelGGL(fc1_conv_adam_kernel<64>, grid, dim3(256), 0, s, dH, a1, wslab1, wslab2, gb, B, params, m, v,
-                       gdump, w1bf, w1tbf, w2r, w2q, off, adam_t, t_off, cfg);
+                       gdump, w1bf, w1tbf, w2r, w2q, off, adam_t, t_off, cfg, dlogits, H, nf2);
 }
 
 void conv_adam(const float* wslab1, const float* wslab2, const float* gb, int B, float* params, float* m, float* v,

@@ -133,6 +133,9 @@ class FusedCNNEngine:
         side stream (overlapping the latency-bound conv backward) was measured
         on MI355X at 146 us/step vs 119 us serial: each cross-queue edge of a
         HIP graph costs more than the overlap saves at this granularity.
+        The FC2 gradient + Adam blocks ride in that same launch rather than in
+        route_fc2's: sharing route_fc2's launch they did not overlap with the
+        dA1 blocks (11.8 us together vs 6.7 + 7.4 us alone, scripts/kbench.py).
         Fusing route_fc2 and fc1_wgrad_adam horizontally into one launch
         (route blocks first, then the FC1 Adam stream; W1^T ping-ponged so the
         two roles need no ordering) was also measured: 50.8 us vs 12.6 + 33.8 us
@@ -145,15 +148,19 @@ class FusedCNNEngine:
             raise ValueError(f"batch {B} > engine capacity {self.mrows}")
         C, M, a = self.C, self.mrows, self._adam()
         self.forward(x, labels, idx, B, stats, True)
-        C.route_fc2(self.dH, self.w1tbf, self.am2, M, B, self.dc2m, self.gb, self.dlogits, self.H,
-                    self.params, self.m, self.v, self.gdump, self.off, self.adam_t, t_off, *a)
         if _MERGED_ADAM:
-            # conv backward first, then ONE launch for the conv-parameter Adam
-            # (latency-bound) and the FC1 wgrad + Adam stream (HBM-bound)
+            # dA1 routing alone, the conv backward, then ONE launch for the
+            # FC2 and conv-parameter Adam (latency-bound) and the FC1 wgrad +
+            # Adam stream (HBM-bound)
+            C.route_fc2(self.dH, self.w1tbf, self.am2, M, B, self.dc2m, self.gb, self.dlogits, self.H,
+                        self.params, self.m, self.v, self.gdump, self.off, self.adam_t, t_off, *a, False)
             C.conv2_bwd(self.dc2m, self.p1s, self.am1, self.w2q, x, idx, self.wslab1, self.wslab2, B)
             C.fc1_conv_adam(self.dH, self.a1, M, self.wslab1, self.wslab2, self.gb, B, self.params, self.m, self.v,
-                            self.gdump, self.w1bf, self.w1tbf, self.w2r, self.w2q, self.off, self.adam_t, t_off, *a)
+                            self.gdump, self.w1bf, self.w1tbf, self.w2r, self.w2q, self.off, self.adam_t, t_off, *a,
+                            self.dlogits, self.H)
             return
+        C.route_fc2(self.dH, self.w1tbf, self.am2, M, B, self.dc2m, self.gb, self.dlogits, self.H,
+                    self.params, self.m, self.v, self.gdump, self.off, self.adam_t, t_off, *a)
         C.fc1_wgrad_adam(self.dH, self.a1, M, self.params, self.m, self.v, self.gdump, self.w1bf, self.w1tbf, self.off, self.adam_t, t_off, *a)
         C.conv2_bwd(self.dc2m, self.p1s, self.am1, self.w2q, x, idx, self.wslab1, self.wslab2, B)
         C.conv_adam(self.wslab1, self.wslab2, self.gb, B, self.params, self.m, self.v, self.gdump, self.w2r, self.w2q, self.off, self.adam_t, t_off, *a)

@@ -51,6 +51,9 @@ def main() -> None:
         "gemm_fc1": lambda: C.gemm_skinny(eng.a1, eng.w1bf, eng.slabs1, M, 2048, 3136, eng.S1),
         "head": lambda: C.head(eng.slabs1, eng.S1, M, eng.params, eng.off, y, None, B, True, eng.H, eng.dH, eng.dlogits, stats),
         "route_fc2": lambda: C.route_fc2(eng.dH, eng.w1tbf, eng.am2, M, B, eng.dc2m, eng.gb, eng.dlogits, eng.H, P, Mm, V, None, eng.off, eng.adam_t, 1, *a),
+        "route_dA1_only": lambda: C.route_fc2(eng.dH, eng.w1tbf, eng.am2, M, B, eng.dc2m, eng.gb, eng.dlogits, eng.H, P, Mm, V, None, eng.off, eng.adam_t, 1, *a, False),
+        "fc1_conv_adam": lambda: C.fc1_conv_adam(eng.dH, eng.a1, M, eng.wslab1, eng.wslab2, eng.gb, B, P, Mm, V, None, eng.w1bf, eng.w1tbf, eng.w2r, eng.w2q, eng.off, eng.adam_t, 1, *a),
+        "fc2_fc1_conv_adam": lambda: C.fc1_conv_adam(eng.dH, eng.a1, M, eng.wslab1, eng.wslab2, eng.gb, B, P, Mm, V, None, eng.w1bf, eng.w1tbf, eng.w2r, eng.w2q, eng.off, eng.adam_t, 1, *a, eng.dlogits, eng.H),
         "fc1_wgrad_adam": lambda: C.fc1_wgrad_adam(eng.dH, eng.a1, M, P, Mm, V, None, eng.w1bf, eng.w1tbf, eng.off, eng.adam_t, 1, *a),
         "conv2_bwd": lambda: C.conv2_bwd(eng.dc2m, eng.p1s, eng.am1, eng.w2q, x, None, eng.wslab1, eng.wslab2, B),
         "conv_adam": lambda: C.conv_adam(eng.wslab1, eng.wslab2, eng.gb, B, P, Mm, V, None, eng.w2r, eng.w2q, eng.off, eng.adam_t, 1, *a),
@@ -90,7 +93,7 @@ def main() -> None:
         torch.cuda.synchronize()
         res["step_graph"] = round(e0.elapsed_time(e1) * 1000.0 / 100, 2)
     if not only:
-        res["sum_isolated"] = round(sum(v for k, v in res.items() if not k.startswith("step_graph")), 2)
+        res["sum_isolated"] = round(sum(v for k, v in res.items() if k in ("conv1_fwd", "conv2_fwd", "gemm_fc1", "head", "route_dA1_only", "conv2_bwd", "fc2_fc1_conv_adam")), 2)
     print(json.dumps({"us_per_kernel": res, "batch": B}))
 
 
