@@ -112,7 +112,7 @@ AdamCfg cfg(double lr, double b1, double b2, double eps, double wd) {
 }
 
 void k_fc1_wgrad_adam(torch::Tensor dH, torch::Tensor a1, int64_t mrows, torch::Tensor params, torch::Tensor m,
-                      torch::Tensor v, c10::optional<torch::Tensor> gdump, torch::Tensor w1bf, torch::Tensor w1tbf,
+                      torch::Tensor v, c10::optional<torch::Tensor> gdump, torch::Tensor w1bf, c10::optional<torch::Tensor> w1tbf,
                       std::vector<int64_t> off, torch::Tensor adam_t, int64_t t_off, double lr, double b1, double b2,
                       double eps, double wd) {
   const c10::DeviceGuard g(params.device());
@@ -125,21 +125,23 @@ void k_fc1_wgrad_adam(torch::Tensor dH, torch::Tensor a1, int64_t mrows, torch::
                         ptr<float>(m, torch::kFloat32, n, "m"), ptr<float>(v, torch::kFloat32, n, "v"),
                         optr<float>(gdump, torch::kFloat32, n, "gdump"),
                         reinterpret_cast<uint16_t*>(ptr<at::BFloat16>(w1bf, torch::kBFloat16, 2048 * 3136, "w1bf")),
-                        reinterpret_cast<uint16_t*>(ptr<at::BFloat16>(w1tbf, torch::kBFloat16, 2048 * 3136, "w1tbf")),
+                        reinterpret_cast<uint16_t*>(optr<at::BFloat16>(w1tbf, torch::kBFloat16, 2048 * 3136, "w1tbf")),
                         o, ptr<int>(adam_t, torch::kInt32, 1, "adam_t", 4), int(t_off), cfg(lr, b1, b2, eps, wd), stream());
 }
 
-void k_route_fc2(torch::Tensor dH, torch::Tensor w1tbf, torch::Tensor am2, int64_t mrows, int64_t B,
+void k_route_fc2(torch::Tensor dH, torch::Tensor w1, torch::Tensor am2, int64_t mrows, int64_t B,
                  torch::Tensor dc2m, torch::Tensor gb, torch::Tensor dlogits, torch::Tensor H, torch::Tensor params,
                  torch::Tensor m, torch::Tensor v, c10::optional<torch::Tensor> gdump, std::vector<int64_t> off,
                  torch::Tensor adam_t, int64_t t_off, double lr, double b1, double b2, double eps, double wd,
-                 bool with_fc2) {
+                 bool with_fc2, bool row_major) {
   const c10::DeviceGuard g(dH.device());
   check_batch(int(B), int(mrows));
   Offsets o = offsets(off);
   const int64_t n = params_end(o);
-  p2cnn::route_fc2(reinterpret_cast<uint16_t*>(ptr<at::BFloat16>(dH, torch::kBFloat16, mrows * 2048, "dH")),
-                   reinterpret_cast<uint16_t*>(ptr<at::BFloat16>(w1tbf, torch::kBFloat16, 2048 * 3136, "w1tbf")),
+  // row_major: w1 is the forward shadow W1 [2048][3136]; else the W1^T shadow [3136][2048]
+  (row_major ? p2cnn::route_fc2_rm : p2cnn::route_fc2)(
+                   reinterpret_cast<uint16_t*>(ptr<at::BFloat16>(dH, torch::kBFloat16, mrows * 2048, "dH")),
+                   reinterpret_cast<uint16_t*>(ptr<at::BFloat16>(w1, torch::kBFloat16, 2048 * 3136, "w1")),
                    ptr<uint8_t>(am2, torch::kUInt8, B * 3136, "am2"), int(mrows), int(B),
                    reinterpret_cast<uint16_t*>(ptr<at::BFloat16>(dc2m, torch::kBFloat16, B * 64 * 224, "dc2m")),
                    ptr<float>(gb, torch::kFloat32, B * 3136, "gb"),
@@ -188,7 +190,7 @@ void k_conv_adam(torch::Tensor wslab1, torch::Tensor wslab2, torch::Tensor gb, i
 
 void k_fc1_conv_adam(torch::Tensor dH, torch::Tensor a1, int64_t mrows, torch::Tensor wslab1, torch::Tensor wslab2,
                      torch::Tensor gb, int64_t B, torch::Tensor params, torch::Tensor m, torch::Tensor v,
-                     c10::optional<torch::Tensor> gdump, torch::Tensor w1bf, torch::Tensor w1tbf, torch::Tensor w2r,
+                     c10::optional<torch::Tensor> gdump, torch::Tensor w1bf, c10::optional<torch::Tensor> w1tbf, torch::Tensor w2r,
                      torch::Tensor w2q, std::vector<int64_t> off, torch::Tensor adam_t, int64_t t_off, double lr,
                      double b1, double b2, double eps, double wd, c10::optional<torch::Tensor> dlogits,
                      c10::optional<torch::Tensor> H) {
@@ -206,7 +208,7 @@ void k_fc1_conv_adam(torch::Tensor dH, torch::Tensor a1, int64_t mrows, torch::T
       ptr<float>(m, torch::kFloat32, n, "m"), ptr<float>(v, torch::kFloat32, n, "v"),
       optr<float>(gdump, torch::kFloat32, n, "gdump"),
       reinterpret_cast<uint16_t*>(ptr<at::BFloat16>(w1bf, torch::kBFloat16, 2048 * 3136, "w1bf")),
-      reinterpret_cast<uint16_t*>(ptr<at::BFloat16>(w1tbf, torch::kBFloat16, 2048 * 3136, "w1tbf")),
+      reinterpret_cast<uint16_t*>(optr<at::BFloat16>(w1tbf, torch::kBFloat16, 2048 * 3136, "w1tbf")),
       reinterpret_cast<uint16_t*>(ptr<at::BFloat16>(w2r, torch::kBFloat16, 51200, "w2r")),
       reinterpret_cast<uint16_t*>(ptr<at::BFloat16>(w2q, torch::kBFloat16, 51200, "w2q")), o,
       ptr<int>(adam_t, torch::kInt32, 1, "adam_t", 4), int(t_off), cfg(lr, b1, b2, eps, wd),
@@ -215,14 +217,14 @@ void k_fc1_conv_adam(torch::Tensor dH, torch::Tensor a1, int64_t mrows, torch::T
 }
 
 void k_pack_shadows(torch::Tensor params, std::vector<int64_t> off, torch::Tensor w2r, torch::Tensor w2q,
-                    torch::Tensor w1bf, torch::Tensor w1tbf) {
+                    torch::Tensor w1bf, c10::optional<torch::Tensor> w1tbf) {
   const c10::DeviceGuard g(params.device());
   Offsets o = offsets(off);
   p2cnn::pack_shadows(ptr<float>(params, torch::kFloat32, params_end(o), "params"), o,
                       reinterpret_cast<uint16_t*>(ptr<at::BFloat16>(w2r, torch::kBFloat16, 51200, "w2r")),
                       reinterpret_cast<uint16_t*>(ptr<at::BFloat16>(w2q, torch::kBFloat16, 51200, "w2q")),
                       reinterpret_cast<uint16_t*>(ptr<at::BFloat16>(w1bf, torch::kBFloat16, 2048 * 3136, "w1bf")),
-                      reinterpret_cast<uint16_t*>(ptr<at::BFloat16>(w1tbf, torch::kBFloat16, 2048 * 3136, "w1tbf")),
+                      reinterpret_cast<uint16_t*>(optr<at::BFloat16>(w1tbf, torch::kBFloat16, 2048 * 3136, "w1tbf")),
                       stream());
 }
 
@@ -239,10 +241,10 @@ void register_cnn(pybind11::module& m) {
   c.def("conv2_fwd", &k_conv2_fwd);
   c.def("gemm_skinny", &k_gemm_skinny);
   c.def("head", &k_head);
-  c.def("route_fc2", &k_route_fc2, pybind11::arg("dH"), pybind11::arg("w1tbf"), pybind11::arg("am2"), pybind11::arg("mrows"), pybind11::arg("B"),
+  c.def("route_fc2", &k_route_fc2, pybind11::arg("dH"), pybind11::arg("w1"), pybind11::arg("am2"), pybind11::arg("mrows"), pybind11::arg("B"),
         pybind11::arg("dc2m"), pybind11::arg("gb"), pybind11::arg("dlogits"), pybind11::arg("H"), pybind11::arg("params"), pybind11::arg("m"), pybind11::arg("v"),
         pybind11::arg("gdump"), pybind11::arg("off"), pybind11::arg("adam_t"), pybind11::arg("t_off"), pybind11::arg("lr"), pybind11::arg("b1"),
-        pybind11::arg("b2"), pybind11::arg("eps"), pybind11::arg("wd"), pybind11::arg("with_fc2") = true);
+        pybind11::arg("b2"), pybind11::arg("eps"), pybind11::arg("wd"), pybind11::arg("with_fc2") = true, pybind11::arg("row_major") = false);
   c.def("fc1_wgrad_adam", &k_fc1_wgrad_adam);
   c.def("conv2_bwd", &k_conv2_bwd);
   c.def("conv_adam", &k_conv_adam);

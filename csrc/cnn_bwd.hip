@@ -17,6 +17,7 @@ namespace p2cnn {
 using namespace p2;
 
 typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
+typedef short s16x4 __attribute__((ext_vector_type(4)));
 P2_DEVICE f32x16 mfma32b(uint4 a, uint4 b, f32x16 c) {
   return __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8_t, a), __builtin_bit_cast(bf16x8_t, b), c,
                                                   0, 0, 0);
@@ -194,6 +195,147 @@ __global__ __launch_bounds__(512) void route_fc2_kernel(const uint16_t* __restri
   }
 }
 
+// Same dA1 routing, reading the row-major FC1 weight W1 [2048][3136] (the
+// forward operand) instead of a transposed W1^T shadow, so the FC1 Adam
+// stream no longer writes 12.8 MB of W1^T per step.  Each wave DMAs its 256 K
+// rows of the block's 32 feature columns (64 B per row) into LDS, and reads
+// the B fragments back with ds_read_b64_tr_b16: per 16-lane group 4 rows x 16
+// columns delivered column-major.  Same k permutation as the W1^T kernel
+// (lane half h, sub-step q -> physical k = k0 + 32 h + 8 q + j), so the A
+// fragments (dH rows) are unchanged.  A 32-lane half reads 4 rows x 64 B =
+// 256 contiguous bytes: conflict-free.  128 KB of LDS: one block per CU (98
+// blocks), the reduction buffer aliases the tile after the MFMAs.
+constexpr int kRouteRmLds = kHid * 64;  // 131072 B
+
+// Workgroups are dispatched round-robin over the 8 XCDs; renumber so that
+// consecutive logical blocks share an XCD (and its L2): route_rm's blocks 2j
+// and 2j+1 read the two 64-B halves of the same 128-B lines of W1.
+P2_DEVICE int xcd_local(int orig, int nwg) {
+  const int xcd = orig % 8, q = nwg / 8, r = nwg % 8;
+  return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + orig / 8;
+}
+
+template <int MT>
+__global__ __launch_bounds__(512) void route_rm_kernel(const uint16_t* __restrict__ dH,
+                                                       const uint16_t* __restrict__ w1,
+                                                       const uint8_t* __restrict__ am2, int B,
+                                                       uint16_t* __restrict__ dc2m, float* __restrict__ gb,
+                                                       const float* __restrict__ dlogits,
+                                                       const uint16_t* __restrict__ H, float* __restrict__ p,
+                                                       float* __restrict__ m, float* __restrict__ v,
+                                                       float* __restrict__ gdump, Offsets off,
+                                                       const int* __restrict__ adam_t, int t_off, AdamCfg cfg) {
+  if (int(blockIdx.x) >= kRouteBlocks) {
+    fc2_role<512>(blockIdx.x - kRouteBlocks, dlogits, H, B, p, m, v, gdump, off, adam_t, t_off, cfg);
+    return;
+  }
+  const int bid = xcd_local(blockIdx.x, kRouteBlocks);
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  static_assert(8 * MT * 1024 * 4 <= kRouteRmLds, "reduction buffer must fit the tile");
+  float* red = reinterpret_cast<float*>(smem);
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, r = lane & 31, h = lane >> 5;
+  const int n0 = bid * 32;
+  constexpr int K = kHid, NG = K / 64, NGW = NG / 8;
+  uint8_t acode[2 * MT];
+#pragma unroll
+  for (int q = 0; q < 2 * MT; ++q) {
+    const int e = tid + 512 * q;
+    const int b = (e >> 10) * 32 + acc_row_b((e >> 6) & 15, (e & 63) >> 5);
+    acode[q] = b < B ? am2[size_t(b) * kFeat + n0 + (e & 31)] : uint8_t(4);
+  }
+  // W1 rows of this wave's k-groups -> LDS [k][32 features] (64-B rows): one
+  // wave instruction = 16 rows x 4 lanes x 16 B
+#pragma unroll
+  for (int gi = 0; gi < NGW; ++gi) {
+    const int k0 = (wave + 8 * gi) * 64;
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      const int row = k0 + 16 * c + (lane >> 2);
+      __builtin_amdgcn_global_load_lds(
+          (const __attribute__((address_space(1))) void*)(w1 + size_t(row) * kFeat + n0 + (lane & 3) * 8),
+          (__attribute__((address_space(3))) void*)(smem + (k0 + 16 * c) * 64), 16, 0, 0);
+    }
+  }
+  uint4 aq[NGW][MT][4];
+#pragma unroll
+  for (int gi = 0; gi < NGW; ++gi) {
+    const int k0 = (wave + 8 * gi) * 64;
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+        aq[gi][mt][q] = reinterpret_cast<const uint4*>(dH + size_t(mt * 32 + r) * K + 32 * h + k0)[q];
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  f32x16 acc[MT];
+#pragma unroll
+  for (int mt = 0; mt < MT; ++mt) acc[mt] = f32x16{};
+  const int g = lane >> 4, qq = (lane >> 2) & 3, col = 16 * (g & 1) + 4 * (lane & 3);
+#pragma unroll
+  for (int gi = 0; gi < NGW; ++gi) {
+    const int k0 = (wave + 8 * gi) * 64;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      uint4 bq;
+#pragma unroll
+      for (int t = 0; t < 2; ++t) {
+        const int row = k0 + 32 * (g >> 1) + 8 * q + 4 * t + qq;
+        const s16x4 w = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+            (__attribute__((address_space(3))) s16x4*)(smem + row * 64 + col * 2));
+        const uint2 u = __builtin_bit_cast(uint2, w);
+        if (t == 0) {
+          bq.x = u.x;
+          bq.y = u.y;
+        } else {
+          bq.z = u.x;
+          bq.w = u.y;
+        }
+      }
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt) acc[mt] = mfma32b(aq[gi][mt][q], bq, acc[mt]);
+    }
+  }
+  __syncthreads();  // tile dead -> reduction buffer
+#pragma unroll
+  for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+    for (int i = 0; i < 16; ++i) red[((wave * MT + mt) * 16 + i) * 64 + lane] = acc[mt][i];
+  __syncthreads();
+#pragma unroll
+  for (int q = 0; q < 2 * MT; ++q) {
+    const int e = tid + 512 * q;
+    float gsum = 0.f;
+#pragma unroll
+    for (int w = 0; w < 8; ++w) gsum += red[w * MT * 1024 + e];
+    const int mt = e >> 10, i = (e >> 6) & 15, ln = e & 63;
+    const int b = mt * 32 + acc_row_b(i, ln >> 5), feat = n0 + (ln & 31);
+    if (b >= B) continue;
+    const uint8_t a = acode[q];
+    const int oc = feat / 49, pp = feat % 49, py = pp / 7, px = pp % 7;
+    gb[size_t(b) * kFeat + feat] = a < 4 ? gsum : 0.f;
+    const uint16_t gv = f32_to_bf16(gsum);
+    uint16_t* row = dc2m + (size_t(b) * kC2 + oc) * 224 + (2 * py) * 16 + 2 * px;
+    const uint32_t top = (a == 0 ? gv : 0u) | (uint32_t(a == 1 ? gv : 0u) << 16);
+    const uint32_t bot = (a == 2 ? gv : 0u) | (uint32_t(a == 3 ? gv : 0u) << 16);
+    *reinterpret_cast<uint32_t*>(row) = top;
+    *reinterpret_cast<uint32_t*>(row + 16) = bot;
+  }
+}
+
+void route_fc2_rm(const uint16_t* dH, const uint16_t* w1, const uint8_t* am2, int mrows, int B, uint16_t* dc2m,
+                  float* gb, const float* dlogits, const uint16_t* H, float* params, float* m, float* v,
+                  float* gdump, Offsets off, const int* adam_t, int t_off, AdamCfg cfg, bool with_fc2,
+                  hipStream_t s) {
+  const dim3 grid(kRouteBlocks + (with_fc2 ? kFc2Blocks : 0));
+  if (mrows == 32)
+    hipLaunchKernelGGL(route_rm_kernel<1>, grid, dim3(512), kRouteRmLds, s, dH, w1, am2, B, dc2m, gb, dlogits, H,
+                       params, m, v, gdump, off, adam_t, t_off, cfg);
+  else
+    hipLaunchKernelGGL(route_rm_kernel<2>, grid, dim3(512), kRouteRmLds, s, dH, w1, am2, B, dc2m, gb, dlogits, H,
+                       params, m, v, gdump, off, adam_t, t_off, cfg);
+}
+
 void route_fc2(const uint16_t* dH, const uint16_t* w1t, const uint8_t* am2, int mrows, int B, uint16_t* dc2m,
                float* gb, const float* dlogits, const uint16_t* H, float* params, float* m, float* v, float* gdump,
                Offsets off, const int* adam_t, int t_off, AdamCfg cfg, bool with_fc2, hipStream_t s) {
@@ -317,11 +459,13 @@ P2_DEVICE void fc1_wgrad_adam_body(int bx, int by, const uint16_t* __restrict__ 
     o.x = uint32_t(b0) | (uint32_t(b1) << 16);
     o.y = uint32_t(b2) | (uint32_t(b3) << 16);
     *reinterpret_cast<uint2*>(w1bf + e) = o;
+    if (!w1tbf) continue;
     tr[kl][nl] = b0;
     tr[kl + 1][nl] = b1;
     tr[kl + 2][nl] = b2;
     tr[kl + 3][nl] = b3;
   }
+  if (!w1tbf) return;  // row-major dA1 routing: no W1^T shadow
   __syncthreads();
   for (int j = tid; j < 128 * 4; j += 256) {
     const int kl = j >> 2, q = j & 3;
@@ -791,6 +935,10 @@ void init_attributes() {
   init_fwd_attributes();
   P2_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(conv2_bwd_kernel),
                                hipFuncAttributeMaxDynamicSharedMemorySize, kDgLds));
+  P2_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(route_rm_kernel<1>),
+                               hipFuncAttributeMaxDynamicSharedMemorySize, kRouteRmLds));
+  P2_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(route_rm_kernel<2>),
+                               hipFuncAttributeMaxDynamicSharedMemorySize, kRouteRmLds));
 }
 
 }  // namespace p2cnn

@@ -442,7 +442,7 @@ __global__ __launch_bounds__(256) void pack_shadows_kernel(const float* __restri
       const int n = int(j / kFeat), k = int(j % kFeat);
       const uint16_t v = f32_to_bf16(params[off.l1w + j]);
       w1bf[j] = v;
-      w1tbf[size_t(k) * kHid + n] = v;
+      if (w1tbf) w1tbf[size_t(k) * kHid + n] = v;
     }
   }
 }

@@ -38,6 +38,10 @@ _CAPTURE_LOCK = make_lock("FusedCNN._CAPTURE_LOCK")
 
 # conv_adam folded into the FC1 Adam launch (P2PFL_CNN_MERGED_ADAM=0: separate launches)
 _MERGED_ADAM = os.environ.get("P2PFL_CNN_MERGED_ADAM", "1") != "0"
+# dA1 routing reads the row-major W1 shadow through LDS transpose reads (no
+# W1^T shadow, 12.8 MB less written per step by the FC1 Adam stream); "0"
+# selects the W1^T-shadow kernel.
+_ROUTE_RM = os.environ.get("P2PFL_CNN_ROUTE_RM", "1") != "0"
 _NAMES = ("conv1.weight", "conv1.bias", "conv2.weight", "conv2.bias", "l1.weight", "l1.bias", "l2.weight", "l2.bias")
 FEAT, HID = 3136, 2048
 
@@ -79,7 +83,9 @@ class FusedCNNEngine:
         self.adam_t = torch.zeros(1, dtype=torch.int32, device=dev)
         # bf16 weight shadows in kernel-friendly layouts
         self.w2r, self.w2q = z(51200, dt=bf), z(51200, dt=bf)
-        self.w1bf, self.w1tbf = z(HID * FEAT, dt=bf), z(HID * FEAT, dt=bf)
+        self.route_rm = _ROUTE_RM
+        self.w1bf = z(HID * FEAT, dt=bf)
+        self.w1tbf = None if self.route_rm else z(HID * FEAT, dt=bf)
         # activations / workspaces (sized for mrows samples)
         M = mrows
         self.p1, self.am1 = z(M * 196 * 32, dt=bf), z(M * 196 * 32, dt=torch.uint8)
@@ -100,6 +106,11 @@ class FusedCNNEngine:
     @property
     def params(self) -> torch.Tensor:
         return self.arena.flat
+
+    @property
+    def w1_route(self) -> torch.Tensor:
+        """The W1 operand of the dA1 routing kernel (row-major W1, or the W1^T shadow)."""
+        return self.w1bf if self.route_rm else self.w1tbf
 
     def pack_shadows(self) -> None:
         """Refresh the bf16 weight copies after the fp32 parameters changed externally."""
@@ -152,15 +163,15 @@ class FusedCNNEngine:
             # dA1 routing alone, the conv backward, then ONE launch for the
             # FC2 and conv-parameter Adam (latency-bound) and the FC1 wgrad +
             # Adam stream (HBM-bound)
-            C.route_fc2(self.dH, self.w1tbf, self.am2, M, B, self.dc2m, self.gb, self.dlogits, self.H,
-                        self.params, self.m, self.v, self.gdump, self.off, self.adam_t, t_off, *a, False)
+            C.route_fc2(self.dH, self.w1_route, self.am2, M, B, self.dc2m, self.gb, self.dlogits, self.H,
+                        self.params, self.m, self.v, self.gdump, self.off, self.adam_t, t_off, *a, False, self.route_rm)
             C.conv2_bwd(self.dc2m, self.p1s, self.am1, self.w2q, x, idx, self.wslab1, self.wslab2, B)
             C.fc1_conv_adam(self.dH, self.a1, M, self.wslab1, self.wslab2, self.gb, B, self.params, self.m, self.v,
                             self.gdump, self.w1bf, self.w1tbf, self.w2r, self.w2q, self.off, self.adam_t, t_off, *a,
                             self.dlogits, self.H)
             return
-        C.route_fc2(self.dH, self.w1tbf, self.am2, M, B, self.dc2m, self.gb, self.dlogits, self.H,
-                    self.params, self.m, self.v, self.gdump, self.off, self.adam_t, t_off, *a)
+        C.route_fc2(self.dH, self.w1_route, self.am2, M, B, self.dc2m, self.gb, self.dlogits, self.H,
+                    self.params, self.m, self.v, self.gdump, self.off, self.adam_t, t_off, *a, True, self.route_rm)
         C.fc1_wgrad_adam(self.dH, self.a1, M, self.params, self.m, self.v, self.gdump, self.w1bf, self.w1tbf, self.off, self.adam_t, t_off, *a)
         C.conv2_bwd(self.dc2m, self.p1s, self.am1, self.w2q, x, idx, self.wslab1, self.wslab2, B)
         C.conv_adam(self.wslab1, self.wslab2, self.gb, B, self.params, self.m, self.v, self.gdump, self.w2r, self.w2q, self.off, self.adam_t, t_off, *a)

@@ -146,8 +146,8 @@ def test_head_and_fc2_wgrad(eng):
     before = eng.params.clone()
     eng.adam_t.fill_(1)
     m_save, v_save = eng.m.clone(), eng.v.clone()
-    eng.C.route_fc2(eng.dH, eng.w1tbf, eng.am2, 32, B, eng.dc2m, eng.gb, eng.dlogits, eng.H,
-                    eng.params, eng.m, eng.v, eng.gdump, eng.off, eng.adam_t, 0, *eng._adam())
+    eng.C.route_fc2(eng.dH, eng.w1_route, eng.am2, 32, B, eng.dc2m, eng.gb, eng.dlogits, eng.H,
+                    eng.params, eng.m, eng.v, eng.gdump, eng.off, eng.adam_t, 0, *eng._adam(), row_major=eng.route_rm)
     torch.cuda.synchronize()
     gw = eng.gdump[eng.off[6] : eng.off[6] + 20480].view(10, 2048)
     gb = eng.gdump[eng.off[7] : eng.off[7] + 10]
@@ -183,7 +183,8 @@ def test_fc1_wgrad_adam(eng):
     # bf16 shadows are the updated weights, in both layouts
     W = eng.params[o : o + 2048 * 3136].view(2048, 3136)
     assert torch.equal(eng.w1bf.view(2048, 3136), W.to(torch.bfloat16))
-    assert torch.equal(eng.w1tbf.view(3136, 2048), W.t().to(torch.bfloat16))
+    if eng.w1tbf is not None:
+        assert torch.equal(eng.w1tbf.view(3136, 2048), W.t().to(torch.bfloat16))
     eng.params.copy_(before)
     eng.m.copy_(m0)
     eng.v.copy_(v0)
@@ -191,24 +192,29 @@ def test_fc1_wgrad_adam(eng):
     eng.pack_shadows()
 
 
-def _route(eng, seed):
+def _route(eng, seed, row_major=None):
     """Random dH through route_fc2 (dA1 = dH W1, pool2/ReLU backward) into the dC2 map.
 
     The launch's FC2-Adam blocks update scratch copies, not the engine's weights.
+    ``row_major`` picks the kernel reading W1 (LDS transpose reads) or a W1^T
+    shadow (built here when the engine keeps none); default: the engine's.
     """
     g = torch.Generator(device="cuda").manual_seed(seed)
     dh = (torch.randn(32, 2048, device="cuda", generator=g) * 1e-2).to(torch.bfloat16)
     P, Mm, V = eng.params.clone(), eng.m.clone(), eng.v.clone()
-    eng.C.route_fc2(dh, eng.w1tbf, eng.am2, 32, B, eng.dc2m, eng.gb, eng.dlogits, eng.H,
-                    P, Mm, V, None, eng.off, eng.adam_t, 1, *eng._adam())
+    rm = eng.route_rm if row_major is None else row_major
+    w1 = eng.w1bf if rm else eng.w1bf.view(2048, 3136).t().contiguous()
+    eng.C.route_fc2(dh, w1, eng.am2, 32, B, eng.dc2m, eng.gb, eng.dlogits, eng.H,
+                    P, Mm, V, None, eng.off, eng.adam_t, 1, *eng._adam(), row_major=rm)
     torch.cuda.synchronize()
     return dh
 
 
-def test_gemm_da1_route(eng):
+@pytest.mark.parametrize("row_major", [True, False])
+def test_gemm_da1_route(eng, row_major):
     x = _x(6)
     _forward(eng, x)
-    dh = _route(eng, 21)
+    dh = _route(eng, 21, row_major)
     w1 = _bf(_p(eng, "l1.weight"))
     da1 = dh.float() @ w1  # [32, 3136]
     am2 = eng.am2.view(-1, 3136)[:B]
@@ -256,7 +262,7 @@ def test_conv2_bwd_partial_batch(eng, Bp):
     dh = (torch.randn(32, 2048, device="cuda", generator=g) * 1e-2).to(torch.bfloat16)
     dh[Bp:] = 0
     P, Mm, V = eng.params.clone(), eng.m.clone(), eng.v.clone()
-    eng.C.route_fc2(dh, eng.w1tbf, eng.am2, 32, Bp, eng.dc2m, eng.gb, eng.dlogits, eng.H, P, Mm, V, None, eng.off, eng.adam_t, 1, *eng._adam())
+    eng.C.route_fc2(dh, eng.w1_route, eng.am2, 32, Bp, eng.dc2m, eng.gb, eng.dlogits, eng.H, P, Mm, V, None, eng.off, eng.adam_t, 1, *eng._adam(), row_major=eng.route_rm)
     eng.C.conv2_bwd(eng.dc2m, eng.p1s, eng.am1, eng.w2q, x.reshape(-1, 784), None, eng.wslab1, eng.wslab2, Bp)
     torch.cuda.synchronize()
     dc2 = eng.dc2m.view(-1, 64, 14, 16)[:Bp, :, :, :14].float()
