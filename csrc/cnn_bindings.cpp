@@ -254,4 +254,6 @@ void register_cnn(pybind11::module& m) {
         pybind11::arg("t_off"), pybind11::arg("lr"), pybind11::arg("b1"), pybind11::arg("b2"), pybind11::arg("eps"), pybind11::arg("wd"),
         pybind11::arg("dlogits") = pybind11::none(), pybind11::arg("H") = pybind11::none());
   c.def("pack_shadows", &k_pack_shadows);
+  c.def("wgrad_groups", [](int64_t B) { return int64_t(p2cnn::wgrad_groups(int(B))); },
+        "conv2 weight-gradient partial slabs (of 51200 floats) written for a batch of B");
 }

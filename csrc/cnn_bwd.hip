@@ -10,6 +10,8 @@
 // reproducible -- required because Adam amplifies last-bit differences in
 // near-zero gradients.  Adam's step count is (*adam_t + t_off): a device base
 // plus an offset baked into each launch, so a whole epoch is one HIP graph.
+#include <cstdlib>
+
 #include "cnn.h"
 #include "common.h"
 
@@ -704,9 +706,9 @@ __global__ __launch_bounds__(256) void conv2_bwd_kernel(const uint16_t* __restri
                                                         const uint16_t* __restrict__ w2q,
                                                         const uint8_t* __restrict__ xds,
                                                         const int64_t* __restrict__ idx, float* __restrict__ wslab1,
-                                                        float* __restrict__ wslab2, int B) {
+                                                        float* __restrict__ wslab2, int B, int first_block) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  const int j = blockIdx.x, nd = 2 * B;
+  const int j = blockIdx.x + first_block, nd = 2 * B;
   if (j < nd) {
     conv2_dgrad_block(j & 1, j >> 1, dc2m, am1, w2q, xds, idx, wslab1, smem);
   } else {
@@ -717,9 +719,22 @@ __global__ __launch_bounds__(256) void conv2_bwd_kernel(const uint16_t* __restri
 
 void conv2_bwd(const uint16_t* dc2m, const uint16_t* p1s, const uint8_t* am1, const uint16_t* w2q, const uint8_t* x,
                const int64_t* idx, float* wslab1, float* wslab2, int B, hipStream_t s) {
-  const int blocks = 2 * B + (kTaps * wgrad_groups(B) + 3) / 4;
+  // P2CNN_CONV2BWD_ROLES (measurement knob, read once): 1 = dgrad blocks
+  // only, 2 = wgrad blocks only; unset = both (the product).  Measured
+  // (scripts/kbench.py, B = 32): dgrad 7.3 us, wgrad 13.1 us, both 12.5 us.
+  // One-image wgrad waves (kWgG = 1) cut the wgrad role to 5.7 us, but its 200
+  // blocks plus the 64 dgrad blocks no longer fit one block per CU (the
+  // launch's 143 KB LDS), and neither spare dgrad waves nor 8-wave blocks
+  // (1 image per dgrad block) beat 13.9 us inside the step's HIP graph.
+  static const int roles = [] {
+    const char* e = getenv("P2CNN_CONV2BWD_ROLES");
+    return e ? atoi(e) : 3;
+  }();
+  const int nd = 2 * B, nw = (kTaps * wgrad_groups(B) + 3) / 4;
+  const int first = roles == 2 ? nd : 0;
+  const int blocks = roles == 1 ? nd : roles == 2 ? nw : nd + nw;
   hipLaunchKernelGGL(conv2_bwd_kernel, dim3(blocks), dim3(256), kDgLds, s, dc2m, p1s, am1, w2q, x, idx, wslab1, wslab2,
-                     B);
+                     B, first);
 }
 
 // ---------------------------------------------------------------------------

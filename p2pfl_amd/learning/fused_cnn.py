@@ -97,7 +97,7 @@ class FusedCNNEngine:
         self.dlogits = z(M * 10)
         # dC2 map written by route_fc2 (its padding columns stay zero from here on)
         self.dc2m, self.gb = z(M * 64 * 224, dt=bf), z(M * FEAT)
-        self.wslab1, self.wslab2 = z(M * 7 * 832), z(((M + 1) // 2) * 51200)
+        self.wslab1, self.wslab2 = z(M * 7 * 832), z(self.C.wgrad_groups(M) * 51200)
         self.stats = z(2)
         self.gdump: Optional[torch.Tensor] = None
         self.pack_shadows()
