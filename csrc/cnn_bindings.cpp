@@ -42,7 +42,8 @@ int64_t params_end(const Offsets& o) {
 }
 
 void check_batch(int B, int mrows) {
-  TORCH_CHECK(mrows == 32 || mrows == 64, "mrows must be 32 or 64");
+  // 128-row launches exist for the forward-only (evaluation) kernels
+  TORCH_CHECK(mrows == 32 || mrows == 64 || mrows == 128, "mrows must be 32, 64 or 128");
   TORCH_CHECK(B >= 1 && B <= mrows, "batch ", B, " exceeds mrows ", mrows);
 }
 
@@ -56,7 +57,8 @@ const int64_t* idx_ptr(const c10::optional<torch::Tensor>& idx, int B) {
 void k_conv1_fwd(torch::Tensor x, c10::optional<torch::Tensor> idx, torch::Tensor params, std::vector<int64_t> off,
                  torch::Tensor p1, torch::Tensor am1, c10::optional<torch::Tensor> p1s, int64_t B) {
   const c10::DeviceGuard g(params.device());
-  TORCH_CHECK(B >= 1 && B <= 64, "bad batch");
+  // training launches (P1s wanted) hold <= 64 images; evaluation launches <= 128
+  TORCH_CHECK(B >= 1 && B <= (p1s.has_value() && p1s->defined() ? 64 : 128), "bad batch");
   Offsets o = offsets(off);
   TORCH_CHECK(x.numel() % 784 == 0, "x must be [N,1,28,28] uint8");
   if (!idx.has_value()) TORCH_CHECK(x.numel() / 784 >= B, "x has fewer than B rows");
@@ -83,8 +85,8 @@ void k_conv2_fwd(torch::Tensor p1, torch::Tensor w2r, torch::Tensor params, std:
 void k_gemm_skinny(torch::Tensor A, torch::Tensor Bt, torch::Tensor slabs, int64_t mrows, int64_t N, int64_t K,
                    int64_t S) {
   const c10::DeviceGuard g(A.device());
-  TORCH_CHECK(mrows == 32 || mrows == 64, "mrows must be 32 or 64");
   TORCH_CHECK(N % 32 == 0 && K % 64 == 0 && S >= 1, "gemm_skinny: N%32, K%64 required");
+  TORCH_CHECK(mrows == 32 || mrows == 64 || mrows == 128, "gemm_skinny: mrows must be 32, 64 or 128");
   p2cnn::gemm_skinny(reinterpret_cast<uint16_t*>(ptr<at::BFloat16>(A, torch::kBFloat16, mrows * K, "A")),
                      reinterpret_cast<uint16_t*>(ptr<at::BFloat16>(Bt, torch::kBFloat16, N * K, "Bt")),
                      ptr<float>(slabs, torch::kFloat32, S * mrows * N, "slabs"), int(mrows), int(N), int(K), int(S),
@@ -136,6 +138,7 @@ void k_route_fc2(torch::Tensor dH, torch::Tensor w1, torch::Tensor am2, int64_t 
                  bool with_fc2, bool row_major) {
   const c10::DeviceGuard g(dH.device());
   check_batch(int(B), int(mrows));
+  TORCH_CHECK(mrows <= 64, "route_fc2: mrows must be 32 or 64");
   Offsets o = offsets(off);
   const int64_t n = params_end(o);
   // row_major: w1 is the forward shadow W1 [2048][3136]; else the W1^T shadow [3136][2048]
@@ -196,6 +199,7 @@ void k_fc1_conv_adam(torch::Tensor dH, torch::Tensor a1, int64_t mrows, torch::T
                      c10::optional<torch::Tensor> H) {
   const c10::DeviceGuard g(params.device());
   check_batch(int(B), int(mrows));
+  TORCH_CHECK(mrows <= 64, "fc1_conv_adam: mrows must be 32 or 64");
   TORCH_CHECK(dlogits.has_value() == H.has_value(), "fc1_conv_adam: pass both dlogits and H or neither");
   Offsets o = offsets(off);
   const int64_t n = params_end(o);

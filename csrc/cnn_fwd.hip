@@ -218,7 +218,7 @@ void conv2_fwd(const uint16_t* p1, const uint16_t* w2r, const float* params, Off
 
 // ---------------------------------------------------------------------------
 // 4/7. Skinny GEMM  slabs[s][m][n] = sum_{k in split s} A[m][k] * Bt[n][k]
-//    (M = mrows = 32*MT rows, N multiple of 32, K multiple of 64).  Block =
+//    (M = mrows = 32*MT rows, MT = 1, 2, 4; N multiple of 32, K multiple of 64).  Block =
 //    32 output columns x one K split; its 4 waves take interleaved 64-wide K
 //    groups.  Each lane streams 64 contiguous bytes of an A row and of a Bt row
 //    per group (the two half-waves cover a full 128-B line), and the group's
@@ -230,7 +230,8 @@ template <int MT>
 __global__ __launch_bounds__(256) void gemm_skinny_kernel(const uint16_t* __restrict__ A,
                                                           const uint16_t* __restrict__ Bt, float* __restrict__ slabs,
                                                           int N, int K, int S) {
-  __shared__ float red[4 * MT * 16 * 64];
+  constexpr int RT = MT < 2 ? MT : 2;  // row tiles reduced per LDS pass (<= 32 KB)
+  __shared__ float red[4 * RT * 16 * 64];
   const int nt = blockIdx.x, sp = blockIdx.y, tid = threadIdx.x;
   const int wave = tid >> 6, lane = tid & 63, r = lane & 31, h = lane >> 5;
   const int n0 = nt * 32;
@@ -274,17 +275,21 @@ __global__ __launch_bounds__(256) void gemm_skinny_kernel(const uint16_t* __rest
       }
     }
   }
-#pragma unroll
-  for (int mt = 0; mt < MT; ++mt)
-#pragma unroll
-    for (int i = 0; i < 16; ++i) red[((wave * MT + mt) * 16 + i) * 64 + lane] = acc[mt][i];
-  __syncthreads();
   const int mrows = MT * 32;
-  for (int e = tid; e < MT * 1024; e += 256) {
-    const float sum = red[e] + red[MT * 1024 + e] + red[2 * MT * 1024 + e] + red[3 * MT * 1024 + e];
-    const int mt = e >> 10, i = (e >> 6) & 15, ln = e & 63;
-    const int row = mt * 32 + acc_row(i, ln >> 5), col = ln & 31;
-    slabs[(size_t(sp) * mrows + row) * N + n0 + col] = sum;
+#pragma unroll
+  for (int m0 = 0; m0 < MT; m0 += RT) {
+    if (m0) __syncthreads();  // previous pass's reads done
+#pragma unroll
+    for (int mt = 0; mt < RT; ++mt)
+#pragma unroll
+      for (int i = 0; i < 16; ++i) red[((wave * RT + mt) * 16 + i) * 64 + lane] = acc[m0 + mt][i];
+    __syncthreads();
+    for (int e = tid; e < RT * 1024; e += 256) {
+      const float sum = red[e] + red[RT * 1024 + e] + red[2 * RT * 1024 + e] + red[3 * RT * 1024 + e];
+      const int mt = m0 + (e >> 10), i = (e >> 6) & 15, ln = e & 63;
+      const int row = mt * 32 + acc_row(i, ln >> 5), col = ln & 31;
+      slabs[(size_t(sp) * mrows + row) * N + n0 + col] = sum;
+    }
   }
 }
 
@@ -292,8 +297,10 @@ void gemm_skinny(const uint16_t* A, const uint16_t* Bt, float* slabs, int mrows,
   const dim3 grid(N / 32, S);
   if (mrows == 32)
     hipLaunchKernelGGL(gemm_skinny_kernel<1>, grid, dim3(256), 0, s, A, Bt, slabs, N, K, S);
-  else
+  else if (mrows == 64)
     hipLaunchKernelGGL(gemm_skinny_kernel<2>, grid, dim3(256), 0, s, A, Bt, slabs, N, K, S);
+  else
+    hipLaunchKernelGGL(gemm_skinny_kernel<4>, grid, dim3(256), 0, s, A, Bt, slabs, N, K, S);
 }
 
 // ---------------------------------------------------------------------------

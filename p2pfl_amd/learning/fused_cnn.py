@@ -190,17 +190,17 @@ class FusedCNNEngine:
 
 
 class _EvalForward:
-    """Forward-only view of a :class:`FusedCNNEngine` at 64 samples per launch.
+    """Forward-only view of a :class:`FusedCNNEngine` at 128 samples per launch.
 
     Evaluation has no optimizer step between batches, so it runs the same
     forward kernels (reading the engine's fp32 parameters and bf16 shadows)
-    on 64-sample batches: half the launches per pass, and the FC1 GEMM --
-    bound by streaming its 12.8 MB weight -- costs about the same per launch
-    at 64 rows as at 32.  Per-sample losses and predictions do not depend on
-    how the set is batched.
+    on 128-sample batches: a quarter of the launches per pass, and the FC1
+    GEMM -- bound by streaming its 12.8 MB weight -- costs little more per
+    launch at 128 rows than at 32.  Per-sample losses and predictions do not
+    depend on how the set is batched.
     """
 
-    MROWS = 64
+    MROWS = 128
 
     def __init__(self, eng: FusedCNNEngine) -> None:
         self.eng = eng

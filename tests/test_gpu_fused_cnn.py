@@ -200,7 +200,7 @@ def test_three_fused_peers_in_one_process():
 
 
 def test_evaluate_matches_torch_reference():
-    """Evaluation runs 64-sample forward launches; loss / accuracy equal an fp32 PyTorch pass over the set."""
+    """Evaluation runs 128-sample forward launches; loss / accuracy equal an fp32 PyTorch pass over the set."""
     from p2pfl_amd.data import MnistFederatedDM
     from p2pfl_amd.learning.fused_cnn import FusedCNNLearner
     from p2pfl_amd.models import CNN
