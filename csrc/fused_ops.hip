@@ -62,11 +62,14 @@ P2_DEVICE void round_to<float>(float (&)[8]) {}
 
 // ---------------------------------------------------------------------------
 // LayerNorm forward: y = (x - mean) * rstd * w + b over the last dim C.
-// One wave per row; the row (C <= 512 * K elements, C <= 2048) stays in registers
-// between the mean and the variance pass (two-pass variance: no
-// cancellation).  Saves mean / rstd for the backward.
+// One wave per row, R rows per wave with every row's loads issued before the
+// first reduction (one memory round trip for R rows instead of R: one row per
+// wave left the ViT-sized call latency-bound at ~1.4 TB/s).  The rows
+// (C <= 512 * K elements, C <= 2048) stay in registers between the mean and
+// the variance pass (two-pass variance: no cancellation).  Saves mean / rstd
+// for the backward.
 // ---------------------------------------------------------------------------
-template <typename T, int K>
+template <typename T, int K, int R, bool RES>
 __global__ __launch_bounds__(256) void ln_fwd_kernel(const T* __restrict__ x, const T* __restrict__ res,
                                                      const float* __restrict__ w, const float* __restrict__ b,
                                                      T* __restrict__ y, T* __restrict__ sum_out,
@@ -74,55 +77,81 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(const T* __restrict__ x, co
                                                      int N, int C, float eps) {
   const int lane = threadIdx.x & 63;
   const int nw = gridDim.x * 4;
-  for (int row = blockIdx.x * 4 + (threadIdx.x >> 6); row < N; row += nw) {
-    const T* xr = x + size_t(row) * C;
-    float v[K][8];
-    float s = 0.f;
+  // affine parameters are the same for every row: loaded once
+  // Loads are unconditional (column clamped to a valid chunk, unused values
+  // masked at use; residual presence is a template parameter): a load under
+  // a branch gets its own s_waitcnt vmcnt(0), which serialised the rows.
+  float wv[K][8], bv[K][8];
 #pragma unroll
-    for (int k = 0; k < K; ++k) {
-      const int c = (lane + 64 * k) * 8;
-      if (c < C) {
-        Vec8<T>::load(xr + c, v[k]);
-        if (res) {  // fused residual: s = x + r (rounded to T, as a separate add would store it)
-          float rv[8];
-          Vec8<T>::load(res + size_t(row) * C + c, rv);
+  for (int k = 0; k < K; ++k) {
+    const int c = (lane + 64 * k) * 8, cc = c < C ? c : 0;
+    load8f(w + cc, wv[k]);
+    load8f(b + cc, bv[k]);
+  }
+  for (int row0 = (blockIdx.x * 4 + (threadIdx.x >> 6)) * R; row0 < N; row0 += nw * R) {
+    float v[R][K][8], rv[R][K][8];
 #pragma unroll
-          for (int j = 0; j < 8; ++j) v[k][j] += rv[j];
-          round_to<T>(v[k]);
-          Vec8<T>::store(sum_out + size_t(row) * C + c, v[k]);
-        }
+    for (int q = 0; q < R; ++q) {
+      const int row = row0 + q < N ? row0 + q : N - 1;  // clamped: duplicates are not stored
 #pragma unroll
-        for (int j = 0; j < 8; ++j) s += v[k][j];
+      for (int k = 0; k < K; ++k) {
+        const int c = (lane + 64 * k) * 8, cc = c < C ? c : 0;
+        Vec8<T>::load(x + size_t(row) * C + cc, v[q][k]);
+        if constexpr (RES) Vec8<T>::load(res + size_t(row) * C + cc, rv[q][k]);
       }
     }
-    const float mean = wave_sum(s) / float(C);
-    float q = 0.f;
+    if constexpr (RES) {  // fused residual: s = x + r (rounded to T, as a separate add would store it)
 #pragma unroll
-    for (int k = 0; k < K; ++k) {
-      const int c = (lane + 64 * k) * 8;
-      if (c < C)
+      for (int q = 0; q < R; ++q)
 #pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          const float d = v[k][j] - mean;
-          q = fmaf(d, d, q);
+        for (int k = 0; k < K; ++k) {
+#pragma unroll
+          for (int j = 0; j < 8; ++j) v[q][k][j] += rv[q][k][j];
+          round_to<T>(v[q][k]);
         }
     }
-    const float rstd = rsqrtf(wave_sum(q) / float(C) + eps);
 #pragma unroll
-    for (int k = 0; k < K; ++k) {
-      const int c = (lane + 64 * k) * 8;
-      if (c < C) {
-        float wv[8], bv[8], o[8];
-        load8f(w + c, wv);
-        load8f(b + c, bv);
+    for (int q = 0; q < R; ++q) {
+      const int row = row0 + q;
+      float s = 0.f;
 #pragma unroll
-        for (int j = 0; j < 8; ++j) o[j] = fmaf((v[k][j] - mean) * rstd, wv[j], bv[j]);
-        Vec8<T>::store(y + size_t(row) * C + c, o);
+      for (int k = 0; k < K; ++k) {
+        const int c = (lane + 64 * k) * 8;
+        if (c < C) {
+          if constexpr (RES)
+            if (row < N) Vec8<T>::store(sum_out + size_t(row) * C + c, v[q][k]);
+#pragma unroll
+          for (int j = 0; j < 8; ++j) s += v[q][k][j];
+        }
       }
-    }
-    if (lane == 0) {
-      mean_out[row] = mean;
-      rstd_out[row] = rstd;
+      const float mean = wave_sum(s) / float(C);
+      float sq = 0.f;
+#pragma unroll
+      for (int k = 0; k < K; ++k) {
+        const int c = (lane + 64 * k) * 8;
+        if (c < C)
+#pragma unroll
+          for (int j = 0; j < 8; ++j) {
+            const float d = v[q][k][j] - mean;
+            sq = fmaf(d, d, sq);
+          }
+      }
+      const float rstd = rsqrtf(wave_sum(sq) / float(C) + eps);
+      if (row >= N) continue;
+#pragma unroll
+      for (int k = 0; k < K; ++k) {
+        const int c = (lane + 64 * k) * 8;
+        if (c < C) {
+          float o[8];
+#pragma unroll
+          for (int j = 0; j < 8; ++j) o[j] = fmaf((v[q][k][j] - mean) * rstd, wv[k][j], bv[k][j]);
+          Vec8<T>::store(y + size_t(row) * C + c, o);
+        }
+      }
+      if (lane == 0) {
+        mean_out[row] = mean;
+        rstd_out[row] = rstd;
+      }
     }
   }
 }
@@ -133,7 +162,7 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(const T* __restrict__ x, co
 // and per-block partial column sums of dy * xhat (dgamma) and dy (dbeta),
 // combined across the block's 4 waves in fixed order through LDS.
 // ---------------------------------------------------------------------------
-template <typename T, int K>
+template <typename T, int K, bool GS>
 __global__ __launch_bounds__(256) void ln_bwd_kernel(const T* __restrict__ dy, const T* __restrict__ x,
                                                      const float* __restrict__ w, const float* __restrict__ mean_in,
                                                      const float* __restrict__ rstd_in, const T* __restrict__ gs,
@@ -141,6 +170,7 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const T* __restrict__ dy, c
                                                      float* __restrict__ part_dw, float* __restrict__ part_db, int N,
                                                      int C) {
   extern __shared__ float sred[];  // [2][C]
+  constexpr int R = 2;  // rows per wave whose loads are in flight together
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int nw = gridDim.x * 4;
   float adw[K][8], adb[K][8];
@@ -148,44 +178,66 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const T* __restrict__ dy, c
   for (int k = 0; k < K; ++k)
 #pragma unroll
     for (int j = 0; j < 8; ++j) adw[k][j] = adb[k][j] = 0.f;
-  for (int row = blockIdx.x * 4 + wave; row < N; row += nw) {
-    const float mean = mean_in[row], rstd = rstd_in[row];
-    float xh[K][8], g[K][8];
-    float s1 = 0.f, s2 = 0.f;
+  // Loads are unconditional (columns clamped to a valid chunk, unused values
+  // masked at use; the residual branch is a template parameter): a load
+  // under a branch gets its own s_waitcnt vmcnt(0), serialising the row.
+  float wk[K][8];  // same for every row: loaded once
 #pragma unroll
-    for (int k = 0; k < K; ++k) {
-      const int c = (lane + 64 * k) * 8;
-      if (c < C) {
-        float xv[8], dv[8], wv[8];
-        Vec8<T>::load(x + size_t(row) * C + c, xv);
-        Vec8<T>::load(dy + size_t(row) * C + c, dv);
-        load8f(w + c, wv);
+  for (int k = 0; k < K; ++k) {
+    const int c = (lane + 64 * k) * 8;
+    load8f(w + (c < C ? c : 0), wk[k]);
+  }
+  for (int row0 = (blockIdx.x * 4 + wave) * R; row0 < N; row0 += nw * R) {
+    float xv[R][K][8], dv[R][K][8], gv[R][K][8], mean[R], rstd[R];
 #pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          xh[k][j] = (xv[j] - mean) * rstd;
-          g[k][j] = dv[j] * wv[j];
-          s1 += g[k][j];
-          s2 = fmaf(g[k][j], xh[k][j], s2);
-          adw[k][j] = fmaf(dv[j], xh[k][j], adw[k][j]);
-          adb[k][j] += dv[j];
-        }
+    for (int q = 0; q < R; ++q) {
+      const int row = row0 + q < N ? row0 + q : N - 1;  // clamped: duplicates add nothing, store nothing
+      mean[q] = mean_in[row];
+      rstd[q] = rstd_in[row];
+#pragma unroll
+      for (int k = 0; k < K; ++k) {
+        const int c = (lane + 64 * k) * 8, cc = c < C ? c : 0;
+        Vec8<T>::load(x + size_t(row) * C + cc, xv[q][k]);
+        Vec8<T>::load(dy + size_t(row) * C + cc, dv[q][k]);
+        if constexpr (GS) Vec8<T>::load(gs + size_t(row) * C + cc, gv[q][k]);
       }
     }
-    const float m1 = wave_sum(s1) / float(C), m2 = wave_sum(s2) / float(C);
 #pragma unroll
-    for (int k = 0; k < K; ++k) {
-      const int c = (lane + 64 * k) * 8;
-      if (c < C) {
-        float o[8];
+    for (int q = 0; q < R; ++q) {
+      const int row = row0 + q;
+      const bool live = row < N;
+      float xh[K][8], g[K][8];
+      float s1 = 0.f, s2 = 0.f;
 #pragma unroll
-        for (int j = 0; j < 8; ++j) o[j] = rstd * (g[k][j] - m1 - xh[k][j] * m2);
-        if (gs) {  // fused residual branch: dx += gradient arriving at the sum directly
-          float gv[8];
-          Vec8<T>::load(gs + size_t(row) * C + c, gv);
+      for (int k = 0; k < K; ++k) {
+        const int c = (lane + 64 * k) * 8;
+        if (c < C && live) {
 #pragma unroll
-          for (int j = 0; j < 8; ++j) o[j] += gv[j];
+          for (int j = 0; j < 8; ++j) {
+            xh[k][j] = (xv[q][k][j] - mean[q]) * rstd[q];
+            g[k][j] = dv[q][k][j] * wk[k][j];
+            s1 += g[k][j];
+            s2 = fmaf(g[k][j], xh[k][j], s2);
+            adw[k][j] = fmaf(dv[q][k][j], xh[k][j], adw[k][j]);
+            adb[k][j] += dv[q][k][j];
+          }
         }
-        Vec8<T>::store(dx + size_t(row) * C + c, o);
+      }
+      const float m1 = wave_sum(s1) / float(C), m2 = wave_sum(s2) / float(C);
+      if (!live) continue;
+#pragma unroll
+      for (int k = 0; k < K; ++k) {
+        const int c = (lane + 64 * k) * 8;
+        if (c < C) {
+          float o[8];
+#pragma unroll
+          for (int j = 0; j < 8; ++j) o[j] = rstd[q] * (g[k][j] - m1 - xh[k][j] * m2);
+          if constexpr (GS) {  // fused residual branch: dx += gradient arriving at the sum directly
+#pragma unroll
+            for (int j = 0; j < 8; ++j) o[j] += gv[q][k][j];
+          }
+          Vec8<T>::store(dx + size_t(row) * C + c, o);
+        }
       }
     }
   }
@@ -414,17 +466,35 @@ static int rows_grid(int N) {
 template <typename T>
 static void ln_fwd_t(const void* x, const void* r, const float* w, const float* b, void* y, void* sum, float* mean,
                      float* rstd, int N, int C, float eps, hipStream_t s) {
-  const dim3 grid(rows_grid(N)), blk(256);
+  // Rows per wave: R = 4 (all loads of 4 rows in flight, 394 blocks at ViT's
+  // 6304 rows) measured 14.3 us per residual call in the ViT graph vs ~12 us
+  // with one row per wave (1576 blocks): the per-row reductions of a wave
+  // run serially, so more waves beat deeper per-wave batches here.  Kept
+  // selectable; the default is one row per wave.
+  constexpr int R = 4;
+  const bool multi = false;
+  const dim3 grid(multi ? (N + 4 * R - 1) / (4 * R) : rows_grid(N)), blk(256);
   const T* xp = static_cast<const T*>(x);
   const T* rp = static_cast<const T*>(r);
   T* yp = static_cast<T*>(y);
   T* sp = static_cast<T*>(sum);
-  if (C <= 512)
-    hipLaunchKernelGGL((ln_fwd_kernel<T, 1>), grid, blk, 0, s, xp, rp, w, b, yp, sp, mean, rstd, N, C, eps);
-  else if (C <= 1024)
-    hipLaunchKernelGGL((ln_fwd_kernel<T, 2>), grid, blk, 0, s, xp, rp, w, b, yp, sp, mean, rstd, N, C, eps);
-  else
-    hipLaunchKernelGGL((ln_fwd_kernel<T, 4>), grid, blk, 0, s, xp, rp, w, b, yp, sp, mean, rstd, N, C, eps);
+#define P2_LN_FWD(KK, RR)                                                                                    \
+  do {                                                                                                      \
+    if (rp)                                                                                                 \
+      hipLaunchKernelGGL((ln_fwd_kernel<T, KK, RR, true>), grid, blk, 0, s, xp, rp, w, b, yp, sp, mean, rstd, N, C, \
+                         eps);                                                                              \
+    else                                                                                                    \
+      hipLaunchKernelGGL((ln_fwd_kernel<T, KK, RR, false>), grid, blk, 0, s, xp, rp, w, b, yp, sp, mean, rstd, N, \
+                         C, eps);                                                                           \
+  } while (0)
+  if (C <= 512) {
+    if (multi) P2_LN_FWD(1, R); else P2_LN_FWD(1, 1);
+  } else if (C <= 1024) {
+    if (multi) P2_LN_FWD(2, R); else P2_LN_FWD(2, 1);
+  } else {
+    if (multi) P2_LN_FWD(4, 2); else P2_LN_FWD(4, 1);
+  }
+#undef P2_LN_FWD
 }
 
 void layer_norm_fwd(bool bf16, const void* x, const void* residual, const float* w, const float* b, void* y,
@@ -454,12 +524,22 @@ static void ln_bwd_t(const void* dy, const void* x, const float* w, const float*
   const T* dyp = static_cast<const T*>(dy);
   const T* xp = static_cast<const T*>(x);
   T* dxp = static_cast<T*>(dx);
+#define P2_LN_BWD(KK)                                                                                            \
+  do {                                                                                                          \
+    if (gp)                                                                                                     \
+      hipLaunchKernelGGL((ln_bwd_kernel<T, KK, true>), grid, blk, lds, s, dyp, xp, w, mean, rstd, gp, dxp, pdw, pdb, N, \
+                         C);                                                                                    \
+    else                                                                                                        \
+      hipLaunchKernelGGL((ln_bwd_kernel<T, KK, false>), grid, blk, lds, s, dyp, xp, w, mean, rstd, gp, dxp, pdw, pdb, \
+                         N, C);                                                                                 \
+  } while (0)
   if (C <= 512)
-    hipLaunchKernelGGL((ln_bwd_kernel<T, 1>), grid, blk, lds, s, dyp, xp, w, mean, rstd, gp, dxp, pdw, pdb, N, C);
+    P2_LN_BWD(1);
   else if (C <= 1024)
-    hipLaunchKernelGGL((ln_bwd_kernel<T, 2>), grid, blk, lds, s, dyp, xp, w, mean, rstd, gp, dxp, pdw, pdb, N, C);
+    P2_LN_BWD(2);
   else
-    hipLaunchKernelGGL((ln_bwd_kernel<T, 4>), grid, blk, lds, s, dyp, xp, w, mean, rstd, gp, dxp, pdw, pdb, N, C);
+    P2_LN_BWD(4);
+#undef P2_LN_BWD
   hipLaunchKernelGGL(col_reduce_kernel, dim3((C + kCrCols - 1) / kCrCols), blk, 0, s, pdw, dw, pdb, db, G, C);
 }
 
