@@ -321,15 +321,23 @@ P2_DEVICE float gelu_grad(float z) {
 template <typename T>
 __global__ __launch_bounds__(256) void bias_gelu_fwd_kernel(const T* __restrict__ x, const float* __restrict__ b,
                                                             T* __restrict__ y, int64_t n8, int H) {
-  for (int64_t i = blockIdx.x * int64_t(256) + threadIdx.x; i < n8; i += int64_t(gridDim.x) * 256) {
-    const int64_t e = i * 8;
-    const int c = int(e % H);
-    float v[8], bv[8];
-    Vec8<T>::load(x + e, v);
-    load8f(b + c, bv);
+  // two chunks per iteration, both loads issued before the (erf-heavy) math,
+  // so each thread keeps a second chunk in flight while it computes
+  const int64_t stride = int64_t(gridDim.x) * 256;
+  for (int64_t i = blockIdx.x * int64_t(256) + threadIdx.x; i < n8; i += 2 * stride) {
+    const int64_t i1 = i + stride < n8 ? i + stride : i;
+    const int64_t e0 = i * 8, e1 = i1 * 8;
+    float v[2][8], bv[2][8];
+    Vec8<T>::load(x + e0, v[0]);
+    Vec8<T>::load(x + e1, v[1]);
+    load8f(b + int(e0 % H), bv[0]);
+    load8f(b + int(e1 % H), bv[1]);
 #pragma unroll
-    for (int j = 0; j < 8; ++j) v[j] = gelu_f(v[j] + bv[j]);
-    Vec8<T>::store(y + e, v);
+    for (int u = 0; u < 2; ++u)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[u][j] = gelu_f(v[u][j] + bv[u][j]);
+    Vec8<T>::store(y + e0, v[0]);
+    if (i1 != i) Vec8<T>::store(y + e1, v[1]);
   }
 }
 
@@ -348,16 +356,30 @@ __global__ __launch_bounds__(256) void bias_gelu_bwd_kernel(const T* __restrict_
   if (c < H) {
     float bv[8];
     load8f(b + c, bv);
-    for (int r = blockIdx.y * 4 + ph; r < N; r += 4 * S) {
-      float xv[8], dv[8], o[8];
-      Vec8<T>::load(x + size_t(r) * H + c, xv);
-      Vec8<T>::load(dy + size_t(r) * H + c, dv);
+    // two rows per iteration, all four loads issued before the math (the
+    // rows of a thread are otherwise one serial load -> compute chain)
+    for (int r = blockIdx.y * 4 + ph; r < N; r += 8 * S) {
+      const int r1 = r + 4 * S;
+      const bool two = r1 < N;
+      const int rr1 = two ? r1 : r;
+      float xv[2][8], dv[2][8];
+      Vec8<T>::load(x + size_t(r) * H + c, xv[0]);
+      Vec8<T>::load(dy + size_t(r) * H + c, dv[0]);
+      Vec8<T>::load(x + size_t(rr1) * H + c, xv[1]);
+      Vec8<T>::load(dy + size_t(rr1) * H + c, dv[1]);
+      float o[2][8];
 #pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        o[j] = dv[j] * gelu_grad(xv[j] + bv[j]);
-        acc[j] += o[j];
+      for (int u = 0; u < 2; ++u)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) o[u][j] = dv[u][j] * gelu_grad(xv[u][j] + bv[j]);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) acc[j] += o[0][j];
+      Vec8<T>::store(dx + size_t(r) * H + c, o[0]);
+      if (two) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) acc[j] += o[1][j];
+        Vec8<T>::store(dx + size_t(r1) * H + c, o[1]);
       }
-      Vec8<T>::store(dx + size_t(r) * H + c, o);
     }
   }
 #pragma unroll
