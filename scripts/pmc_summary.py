@@ -1,0 +1,95 @@
+"""Summarise rocprofv3 ``--pmc`` runs per kernel (median over dispatches).
+
+Each pass directory holds ``*counter_collection.csv`` (and, when the pass ran
+with ``--kernel-trace``, ``*kernel_trace.csv``).  Counters of one dispatch are
+summed over dimensions; durations come from the kernel trace of the same pass
+(joined on the dispatch id).  Derived columns:
+
+* ``HBM GB/s``   = (2 * FETCH_SIZE + WRITE_SIZE) [KB] / duration -- on gfx950
+  FETCH_SIZE tallies a wide coalesced read at half its bytes
+  (MI355X_MICROARCH.md, rocprofv3 section), so it is doubled; Infinity-Cache
+  hits are counted too, so this is memory-side traffic, not strictly HBM.
+* ``MFMA busy``  = SQ_VALU_MFMA_BUSY_CYCLES / (GRBM_GUI_ACTIVE / 8 * CUs) --
+  matrix-core busy cycles over the kernel's cycles on every CU
+  (GRBM_GUI_ACTIVE is summed over the 8 XCDs).
+
+    python scripts/pmc_summary.py gpurun_out/pmc_fetch gpurun_out/pmc_write gpurun_out/pmc_sq [--md]
+"""
+
+from __future__ import annotations
+
+import csv
+import glob
+import os
+import statistics
+import sys
+from collections import defaultdict
+
+CUS = 256
+
+
+def _short(name: str) -> str:
+    return name.replace("void ", "").split("(")[0].replace("p2cnn::", "")[:48]
+
+
+def load(d: str):
+    """-> {kernel: {counter: [values per dispatch]}}, {kernel: [durations ns]}"""
+    vals: dict = defaultdict(lambda: defaultdict(lambda: defaultdict(float)))
+    names: dict = {}
+    for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
+        for r in csv.DictReader(open(f)):
+            did = r.get("Dispatch_Id") or r.get("Correlation_Id")
+            names[did] = r["Kernel_Name"]
+            vals[did][r["Counter_Name"]]["v"] += float(r["Counter_Value"])
+    durs: dict = {}
+    for f in glob.glob(os.path.join(d, "**", "*kernel_trace.csv"), recursive=True):
+        for r in csv.DictReader(open(f)):
+            did = r.get("Dispatch_Id") or r.get("Correlation_Id")
+            durs[did] = float(r["End_Timestamp"]) - float(r["Start_Timestamp"])
+    per_k: dict = defaultdict(lambda: defaultdict(list))
+    per_d: dict = defaultdict(list)
+    for did, cs in vals.items():
+        k = _short(names[did])
+        for c, acc in cs.items():
+            per_k[k][c].append(acc["v"])
+        if did in durs:
+            per_d[k].append(durs[did])
+    return per_k, per_d
+
+
+def main() -> None:
+    dirs = [a for a in sys.argv[1:] if not a.startswith("--")]
+    md = "--md" in sys.argv
+    counters: dict = defaultdict(dict)
+    durs: dict = defaultdict(list)
+    for d in dirs:
+        pk, pd = load(d)
+        for k, cs in pk.items():
+            for c, v in cs.items():
+                counters[k][c] = statistics.median(v)
+        for k, v in pd.items():
+            durs[k] += v
+    cols = sorted({c for cs in counters.values() for c in cs})
+    head = ["kernel", "dur us"] + cols + ["HBM GB/s", "MFMA busy"]
+    rows = []
+    for k, cs in counters.items():
+        du = statistics.median(durs[k]) / 1e3 if durs.get(k) else float("nan")
+        kb = 2.0 * cs.get("FETCH_SIZE", 0.0) + cs.get("WRITE_SIZE", 0.0)
+        gbs = kb * 1e3 / (du * 1e3) if du == du and du > 0 else float("nan")  # KB/us -> GB/s
+        mb = cs.get("SQ_VALU_MFMA_BUSY_CYCLES")
+        gui = cs.get("GRBM_GUI_ACTIVE")
+        mf = mb / (gui / 8.0 * CUS) if mb is not None and gui else float("nan")
+        rows.append([k, f"{du:.2f}"] + [f"{cs.get(c, float('nan')):.4g}" for c in cols] + [f"{gbs:.0f}", f"{mf:.1%}"])
+    rows.sort(key=lambda r: -float(r[1]) if r[1] != "nan" else 0)
+    if md:
+        print("| " + " | ".join(head) + " |")
+        print("|" + "---|" * len(head))
+        for r in rows:
+            print("| `" + r[0] + "` | " + " | ".join(r[1:]) + " |")
+    else:
+        for r in rows:
+            print("  ".join(r))
+
+
+if __name__ == "__main__":
+    main()
