@@ -257,6 +257,31 @@ def test_aggregator_lost_members():
     assert "c" in x.get_aggregated_models() and not x._lost
 
 
+def test_aggregator_heartbeat_stall_member_comes_back():
+    """A trainer evicted by a heartbeat stall (not a crash) that reappears before the
+    aggregation completes is waited for again; once complete, the aggregate stays final."""
+    t = lambda v: {"w": torch.full((4,), float(v))}  # noqa: E731
+    agg = FedAvg("a")
+    agg.set_nodes_to_aggregate(["a", "b", "c"])
+    agg.add_model(t(1), ["a"], 1)
+    agg.mark_lost(["c"])  # heartbeat timeout while c is still training
+    agg.mark_alive(["c"])  # c's heartbeat is seen again
+    agg.add_model(t(3), ["b"], 1)
+    assert not agg._done.is_set()  # still waiting for c
+    agg.add_model(t(5), ["c"], 1)
+    assert torch.allclose(agg.wait_and_get_aggregation(timeout=0.1)["w"], torch.full((4,), 3.0))
+    # completed without the member: a late reappearance does not reopen the round
+    agg.clear()
+    agg.set_nodes_to_aggregate(["a", "b", "c"])
+    agg.add_model(t(1), ["a"], 1)
+    agg.add_model(t(3), ["b"], 1)
+    agg.mark_lost(["c"])
+    assert agg._done.is_set()
+    agg.mark_alive(["c"])
+    assert agg._done.is_set() and "c" in agg._lost
+    assert torch.allclose(agg.wait_and_get_aggregation(timeout=0.1)["w"], torch.full((4,), 2.0))
+
+
 def test_mixed_precision_learner_cpu():
     """bf16 weight shadows + multi-tensor Adam (the GPU learner path) on the CPU reference ops."""
     from p2pfl_amd.data import MnistFederatedDM
