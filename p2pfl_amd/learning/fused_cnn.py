@@ -342,25 +342,26 @@ class FusedCNNLearner(TorchLearner):
                 self.engine.adam_t.fill_(epoch * steps)  # Adam step base for this epoch's graph
                 with logger.span(self._addr, "train_epoch"):
                     stats = self._run("train", loader, True, loader.permutation())
-                    st = stats.cpu()
-                steps = st.shape[0]
+                    # one host copy, then plain floats: per-element tensor
+                    # indexing costs microseconds each, x steps, while the GPU idles
+                    loss_sums = [row[0] for row in stats.cpu().tolist()]
+                steps = len(loss_sums)
                 self._step += steps
                 bs = loader.batch_size
                 n = len(loader.dataset)
-                per_step = [float(st[j, 0]) / min(bs, n - j * bs) for j in range(steps)]
                 every = max(1, self.log_every_n_steps)
                 for j in range(steps):
                     if (self._step - steps + j + 1) % every == 0:
-                        self._log("train_loss", per_step[j], step=self._step - steps + j + 1)
-                self.last_train_loss = sum(float(st[j, 0]) for j in range(steps)) / n
+                        self._log("train_loss", loss_sums[j] / min(bs, n - j * bs), step=self._step - steps + j + 1)
+                self.last_train_loss = sum(loss_sums) / n
                 if not (self.defer_final_validation and epoch == self.epochs - 1):
                     self._validate()
 
     def _eval_pass(self, name: str, loader) -> Dict[str, float]:
         with self._lock:
-            st = self._run(name, loader, False, None).cpu()
+            loss, correct = self._run(name, loader, False, None)[0, :2].tolist()
         n = max(1, len(loader.dataset))
-        return {"loss": float(st[0, 0]) / n, "metric": float(st[0, 1]) / n}
+        return {"loss": loss / n, "metric": correct / n}
 
     def _validate(self) -> None:
         loader = self.data.val_dataloader()
