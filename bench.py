@@ -148,6 +148,11 @@ def launch(args, argv) -> int:
         env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
                    MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), TORCHELASTIC_USE_AGENT_STORE="True",
                    TORCHELASTIC_RESTART_COUNT="0", P2PFL_JOB_ID=job)
+        if os.environ.get("P2PFL_RCCL_SPLIT_HOSTS") == "1":
+            # one-GPU rehearsal of the multi-rank RCCL path: RCCL rejects two
+            # ranks on one device unless each looks like its own host, so the
+            # ranks talk over RCCL's socket transport (loopback), not xGMI
+            env.update(NCCL_HOSTID=f"p2pfl-{job}-r{r}", NCCL_SOCKET_IFNAME="lo", NCCL_IB_DISABLE="1")
         procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + argv, env=env, start_new_session=True))
     rc = 0
     deadline = time.monotonic() + args.watchdog + 60
@@ -249,14 +254,20 @@ def run_gossip(args, env: _Env) -> dict:
     Settings.GOSSIP_MODELS_PER_ROUND = max(1, N - 1)
     Settings.TTL = 1
     Settings.WIRE_DTYPE = args.wire_dtype
-    job = XgmiJob(env.rank, N, env.store, device=env.device, prefix=f"p2pfl/{os.environ.get('P2PFL_JOB_ID', 'bench')}")
+    # node addresses are machine-wide bus names: unique per job (self-launched
+    # jobs carry P2PFL_JOB_ID, torchrun jobs their rendezvous port)
+    job_id = os.environ.get("P2PFL_JOB_ID") or f"tr{os.environ.get('MASTER_PORT', '0')}-{os.getppid()}"
+    job = XgmiJob(env.rank, N, env.store, device=env.device, backend=args.plane_backend, allow_fallback=args.allow_fallback,
+                  prefix=f"p2pfl/{job_id}", job_id=job_id)
     torch.manual_seed(1234)  # identical init on every peer (the initiator's model wins anyway)
     model, data, desc, data_desc = build_config(args, env.rank)
     node = Node(model, data, protocol=job.protocol, learner=learner_class(args), device=env.device)
     marks = {}
+    round_ends = {}
 
     def hook(state) -> None:
         r = state.round
+        round_ends[r] = time.perf_counter()
         if r in (W, W + K):
             _sync(env.device)
             env.barrier()
@@ -283,8 +294,11 @@ def run_gossip(args, env: _Env) -> dict:
             raise TimeoutError("data plane did not come up")
         if plane is not None and plane.failed:
             raise RuntimeError(plane.failed)
+        # the backend the ranks actually agreed on (a fallback is reported, never hidden)
+        backend_used = plane.backend_name if plane is not None else job.backend
         env.barrier()
         t_start = time.perf_counter()
+        round_ends.setdefault(0, t_start)
         if W == 0:
             marks[0] = t_start
         if env.rank == 0:
@@ -310,6 +324,8 @@ def run_gossip(args, env: _Env) -> dict:
             print(f"[bench rank {env.rank}] all spans, ms per round: "
                   + ", ".join(f"{k} {v / max(1, K) * 1e3:.2f}" for k, v in sorted(tot.items(), key=lambda kv: -kv[1])),
                   file=sys.stderr, flush=True)
+        if N > 1 or os.environ.get("P2PFL_BENCH_SPANS"):
+            _print_round_breakdown(env.rank, node.addr, logger.tracer, round_ends, W, K)
         pushes = logger.tracer.counters(node.addr)
         stats = dict(plane.stats) if plane is not None else {}
         print(
@@ -334,8 +350,39 @@ def run_gossip(args, env: _Env) -> dict:
         node.stop()
     return {
         "elapsed": elapsed, "desc": desc, "data_desc": data_desc, "n_train": n_train, "n_val": n_val, "n_test": n_test,
-        "total": per_peer_total, "parallelism": "gossip-p2p", "transport": f"xgmi/{job.backend}",
+        "total": per_peer_total, "parallelism": "gossip-p2p",
+        "transport": f"xgmi/{backend_used}" + ("+split-hosts-rehearsal" if os.environ.get("NCCL_HOSTID") else ""),
     }
+
+
+def _print_round_breakdown(rank, addr, tracer, round_ends, W, K) -> None:
+    """Per-rank, per-round spans of the timed rounds (stderr): where a round's
+    wall-clock went -- training, the pushes' propose->ack latency and group
+    transfer times, bytes per link, the wait for the other peers' models, FedAvg."""
+    rounds = [r for r in range(W + 1, W + K + 1) if r in round_ends and r - 1 in round_ends]
+    spans = [s for s in tracer.spans(addr)]
+    for r in rounds:
+        t0, t1 = round_ends[r - 1], round_ends[r]
+        inr = [s for s in spans if t0 <= s.start < t1]
+
+        def tot(name):
+            return sum(s.duration for s in inr if s.name == name) * 1e3
+
+        acks = [s.duration * 1e3 for s in inr if s.name == "xgmi_ack"]
+        groups = [s for s in inr if s.name == "xgmi_group"]
+        gbytes = sum(int(s.attrs.get("nbytes", 0)) for s in groups)
+        print(
+            f"[bench rank {rank}] round {r}: wall {(t1 - t0) * 1e3:.2f} ms | fit {tot('fit'):.2f} evaluate {tot('evaluate'):.2f} "
+            f"wait_aggregation {tot('wait_aggregation'):.2f} aggregate {tot('aggregate'):.2f} | pushes: "
+            f"ack {('%.3f' % (sum(acks) / len(acks))) if acks else '-'} ms mean over {len(acks)}, "
+            f"{len(groups)} groups {sum(s.duration for s in groups) * 1e3:.2f} ms total "
+            f"(max {max((s.duration for s in groups), default=0) * 1e3:.2f}), {gbytes / 1e6:.1f} MB moved",
+            file=sys.stderr, flush=True,
+        )
+    links = {k.split("/", 1)[1]: v for k, v in tracer.counters(addr).items() if k.startswith("link_tx_bytes/")}
+    if links:
+        print(f"[bench rank {rank}] bytes sent per link over the run: "
+              + ", ".join(f"->{p} {v / 1e6:.1f} MB" for p, v in sorted(links.items())), file=sys.stderr, flush=True)
 
 
 def run_allreduce(args, env: _Env) -> dict:
@@ -462,6 +509,11 @@ def main() -> None:
     ap.add_argument("--batch", type=int, default=32)
     ap.add_argument("--wire-dtype", choices=["fp32", "bf16"], default="fp32", help="model arenas on the xGMI data plane")
     ap.add_argument("--watchdog", type=float, default=900, help="dump stacks and exit if the run hangs")
+    ap.add_argument("--plane-backend", choices=["auto", "rccl", "gloo"], default="auto",
+                    help="xGMI data-plane backend (auto: rccl on GPUs, gloo on CPUs)")
+    ap.add_argument("--allow-fallback", action="store_true",
+                    help="let the data plane degrade from RCCL to host-staged gloo instead of failing (the JSON "
+                         "'transport' then says xgmi/gloo)")
     argv = sys.argv[1:]
     args = ap.parse_args(argv)
     if args.impl == "reference":

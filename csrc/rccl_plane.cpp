@@ -104,10 +104,18 @@ class RcclPlane {
   // ops: (kind, peer, tensor) with kind 0 = send, 1 = recv.  The comm stream
   // first waits on every stream in `after` (the producers of the send
   // buffers / previous users of the receive buffers).  Returns a group id.
+  //
+  // Lock discipline (no host mutex is ever held while the GIL is taken back):
+  // argument checks run under the GIL only; the RCCL group is enqueued with
+  // the GIL released under issue_mu_ (one group at a time on the
+  // communicator) and comm_mu_ (shared; abort takes it exclusively), both of
+  // which are dropped before the GIL is re-acquired; the group's bookkeeping
+  // entry is added afterwards under a short mu_ section.  wait/query/release
+  // take mu_ with the GIL held, so holding mu_ across a GIL re-acquire would
+  // be a lock-order inversion (issuer: mu_ -> GIL, completer: GIL -> mu_).
   int64_t issue(const std::vector<std::tuple<int64_t, int64_t, torch::Tensor>>& ops, const std::vector<int64_t>& after,
                 double timeout_s) {
-    std::lock_guard<std::mutex> lk(mu_);
-    TORCH_CHECK(comm_ != nullptr, "RcclPlane: communicator aborted/closed");
+    TORCH_CHECK(!aborted_, "RcclPlane: communicator aborted/closed");
     for (const auto& op : ops) {
       const auto& t = std::get<2>(op);
       const int64_t peer = std::get<1>(op), kind = std::get<0>(op);
@@ -126,11 +134,17 @@ class RcclPlane {
     }
     GroupRec rec;
     ncclResult_t r;
+    bool gone = false;
     {
       py::gil_scoped_release nogil;
+      std::lock_guard<std::mutex> il(issue_mu_);
       std::shared_lock<std::shared_mutex> cl(comm_mu_);
-      if (comm_ == nullptr) throw std::runtime_error("RcclPlane: communicator aborted");
-      r = ncclGroupStart();
+      if (comm_ == nullptr) {
+        gone = true;
+        r = ncclInvalidUsage;
+      } else {
+        r = ncclGroupStart();
+      }
       for (const auto& op : ops) {
         if (r != ncclSuccess) break;
         const auto& t = std::get<2>(op);
@@ -139,14 +153,24 @@ class RcclPlane {
         r = std::get<0>(op) == 0 ? ncclSend(t.data_ptr(), nbytes, ncclUint8, peer, comm_, stream_)
                                  : ncclRecv(t.data_ptr(), nbytes, ncclUint8, peer, comm_, stream_);
       }
-      ncclResult_t e = ncclGroupEnd();
-      if (r == ncclSuccess) r = e;
-      if (r == ncclInProgress) r = settle(timeout_s);
+      if (!gone) {
+        ncclResult_t e = ncclGroupEnd();
+        if (r == ncclSuccess) r = e;
+        if (r == ncclInProgress) r = settle(timeout_s);
+        // the completion event is recorded right behind the group, before
+        // another issuer can enqueue on the comm stream
+        if (r == ncclSuccess && hipEventCreateWithFlags(&rec.done, hipEventDisableTiming) == hipSuccess &&
+            hipEventRecord(rec.done, stream_) != hipSuccess) {
+          hipEventDestroy(rec.done);
+          rec.done = nullptr;
+        }
+      }
     }
+    if (gone) throw std::runtime_error("RcclPlane: communicator aborted");
     if (r != ncclSuccess) throw std::runtime_error("RcclPlane group: " + nccl_msg(r));
-    hip_ok(hipEventCreateWithFlags(&rec.done, hipEventDisableTiming), "hipEventCreate");
-    hip_ok(hipEventRecord(rec.done, stream_), "hipEventRecord(done)");
+    TORCH_CHECK(rec.done != nullptr, "RcclPlane: could not record the group's completion event");
     for (const auto& op : ops) rec.keep.push_back(std::get<2>(op));
+    std::lock_guard<std::mutex> lk(mu_);
     const int64_t gid = next_gid_++;
     groups_.emplace(gid, std::move(rec));
     return gid;
@@ -277,7 +301,8 @@ class RcclPlane {
   int nranks_, rank_, device_;
   ncclComm_t comm_ = nullptr;
   hipStream_t stream_ = nullptr;
-  std::mutex mu_;                 // group bookkeeping
+  std::mutex mu_;                 // group bookkeeping (never held across a GIL transition)
+  std::mutex issue_mu_;           // one group enqueue at a time (taken with the GIL released)
   std::shared_mutex comm_mu_;     // comm_ lifetime: shared for calls, exclusive for abort/close
   std::atomic<bool> abort_req_{false};
   std::unordered_map<int64_t, GroupRec> groups_;

@@ -18,7 +18,13 @@ file behind when a process dies, and a dead peer is visible at once:
 
 One dispatcher thread per endpoint multiplexes every inbound connection with
 ``selectors`` and hands each record to ``on_record``; handlers must not block
-for long (weights never travel here, only their headers).
+for long.  Weights normally never travel here, only their headers; when the
+data plane cannot carry a model (it failed, or this rank was left out of a
+rebuilt generation) the model goes out as one bus record anyway.  Records
+larger than one socket packet (``MAX_RECORD``) are split into fragments that
+are written back to back under the connection's lock and reassembled by the
+receiver, so a 26 MB CNN or a 350 MB ViT still arrives -- slowly, through
+host memory, but intact.
 """
 
 from __future__ import annotations
@@ -27,13 +33,18 @@ import errno
 import selectors
 import socket
 import threading
-from typing import Callable, Dict, Optional
+from typing import Callable, Dict, List, Optional
 
 from p2pfl_amd.management.logger import logger
 from p2pfl_amd.utils.lockcheck import make_lock
 
 MAX_RECORD = 1 << 20
 _HELLO = b"\x00P2FBUS1"
+_HELLO_BULK = b"\x00P2FBULK"  # large-record connection (its close is not a peer exit)
+# fragment of a large record: marker + 1 flag byte (1 = last fragment) + data
+_FRAG = b"\x00P2FFRG"
+FRAG_DATA = MAX_RECORD - len(_FRAG) - 1
+MAX_MESSAGE = 2 << 30  # reassembly bound per record
 SOCK_BUF = 4 << 20
 
 
@@ -75,9 +86,12 @@ class BusEndpoint:
         self._wr, self._ww = socket.socketpair()
         self._wr.setblocking(False)
         self._sel.register(self._wr, selectors.EVENT_READ, "wake")
-        self._out: Dict[str, socket.socket] = {}
-        self._out_locks: Dict[str, threading.Lock] = {}
+        self._out: Dict[tuple, socket.socket] = {}
+        self._out_locks: Dict[tuple, threading.Lock] = {}
         self._out_lock = make_lock("BusEndpoint._out_lock")
+        # inbound fragments of a large record, per connection (dispatcher thread only)
+        self._partial: Dict[socket.socket, List[bytes]] = {}
+        self._bulk: set = set()
         self._closed = threading.Event()
         self._thread = threading.Thread(target=self._loop, name=f"bus-{addr}", daemon=True)
 
@@ -116,52 +130,68 @@ class BusEndpoint:
     # ------------------------------------------------------------------
     # send
     # ------------------------------------------------------------------
-    def _connection(self, dst: str) -> "tuple[socket.socket, threading.Lock]":
+    def _connection(self, dst: str, bulk: bool = False) -> "tuple[socket.socket, threading.Lock]":
+        key = (dst, bulk)
         with self._out_lock:
-            s = self._out.get(dst)
+            s = self._out.get(key)
             if s is not None:
-                return s, self._out_locks[dst]
-            lk = self._out_locks.get(dst)
+                return s, self._out_locks[key]
+            lk = self._out_locks.get(key)
             if lk is None:
-                lk = self._out_locks[dst] = make_lock("BusEndpoint.conn_lock")
-        # one connection per destination: a second socket that said hello and
-        # then closed would look like the peer's process going away
+                lk = self._out_locks[key] = make_lock("BusEndpoint.conn_lock")
+        # one connection per destination (plus one bulk connection for large
+        # records): a second socket that said hello and then closed would look
+        # like the peer's process going away
         with lk:
             with self._out_lock:
-                s = self._out.get(dst)
+                s = self._out.get(key)
             if s is not None:
                 return s, lk
             s = socket.socket(socket.AF_UNIX, socket.SOCK_SEQPACKET)
             try:
                 s.setsockopt(socket.SOL_SOCKET, socket.SO_SNDBUF, SOCK_BUF)
                 s.connect(bus_name(dst))
-                s.sendall(_HELLO + self.addr.encode())
+                s.sendall((_HELLO_BULK if bulk else _HELLO) + self.addr.encode())
             except OSError as e:
                 s.close()
                 raise ConnectionError(f"cannot reach {dst}: {e}") from e
             with self._out_lock:
-                self._out[dst] = s
+                self._out[key] = s
             return s, lk
 
     def drop(self, dst: str) -> None:
-        """Forget the cached connection to ``dst`` (it will be reopened on demand)."""
+        """Forget the cached connections to ``dst`` (they will be reopened on demand)."""
         with self._out_lock:
-            s = self._out.pop(dst, None)
-        if s is not None:
-            try:
-                s.close()
-            except OSError:
-                pass
+            socks = [self._out.pop((dst, b), None) for b in (False, True)]
+        for s in socks:
+            if s is not None:
+                try:
+                    s.close()
+                except OSError:
+                    pass
 
     def send(self, dst: str, record: bytes) -> None:
         if self._closed.is_set():
             raise ConnectionError("bus endpoint closed")
-        if len(record) > MAX_RECORD:
-            raise ValueError(f"control record of {len(record)} bytes exceeds {MAX_RECORD}")
-        s, lk = self._connection(dst)
+        if len(record) > MAX_MESSAGE:
+            raise ValueError(f"bus record of {len(record)} bytes exceeds {MAX_MESSAGE}")
+        # large records travel on their own connection, so control records
+        # (acks, votes, heartbeats) never queue behind a multi-MB model and the
+        # receiver's dispatcher never waits on a sender that waits on it
+        bulk = len(record) > MAX_RECORD or record.startswith(_FRAG)
+        s, lk = self._connection(dst, bulk)
         try:
             with lk:
-                s.sendall(record)
+                if not bulk:
+                    s.sendall(record)
+                else:
+                    # fragments of one record are contiguous on the connection
+                    # (the lock is held across all of them), so the receiver
+                    # needs no record ids
+                    view = memoryview(record)
+                    for off in range(0, len(record), FRAG_DATA):
+                        last = off + FRAG_DATA >= len(record)
+                        s.sendall(_FRAG + (b"\x01" if last else b"\x00") + view[off : off + FRAG_DATA])
         except OSError as e:
             self.drop(dst)
             raise ConnectionError(f"send to {dst} failed: {e}") from e
@@ -220,6 +250,10 @@ class BusEndpoint:
                 data = b""
             if not data:  # peer closed its end (node stopped or process died)
                 src = peers.pop(sock, None)
+                self._partial.pop(sock, None)
+                if sock in self._bulk:  # only the main connection's end means the peer left
+                    self._bulk.discard(sock)
+                    src = None
                 try:
                     self._sel.unregister(sock)
                 except Exception:
@@ -235,7 +269,19 @@ class BusEndpoint:
             if src is None:
                 if data.startswith(_HELLO):
                     peers[sock] = data[len(_HELLO):].decode()
+                elif data.startswith(_HELLO_BULK):
+                    peers[sock] = data[len(_HELLO_BULK):].decode()
+                    self._bulk.add(sock)
                 continue
+            if data.startswith(_FRAG):
+                parts = self._partial.setdefault(sock, [])
+                parts.append(data[len(_FRAG) + 1 :])
+                if data[len(_FRAG)] != 1:
+                    if sum(len(p) for p in parts) > MAX_MESSAGE:
+                        logger.error(self.addr, f"oversized fragmented record from {src}; dropped")
+                        self._partial.pop(sock, None)
+                    continue
+                data = b"".join(self._partial.pop(sock))
             try:
                 self._on_record(src, data)
             except Exception as e:

@@ -120,11 +120,12 @@ class RcclBackend(Backend):
 
     name = "rccl"
 
-    def __init__(self, uid: bytes, members: List[int], rank: int, device: torch.device, group_timeout: float) -> None:
+    def __init__(self, uid: bytes, members: List[int], rank: int, device: torch.device, group_timeout: float,
+                 init_timeout: float = 120.0) -> None:
         from p2pfl_amd import ops
 
         self.device = torch.device(device)
-        self.plane = ops.ext().RcclPlane(uid, len(members), members.index(rank), int(self.device.index or 0), 120.0)
+        self.plane = ops.ext().RcclPlane(uid, len(members), members.index(rank), int(self.device.index or 0), init_timeout)
         self.stream = torch.cuda.ExternalStream(self.plane.stream, device=self.device)
         self.group_timeout = group_timeout
 
@@ -323,17 +324,35 @@ class SimBackend(Backend):
 # ----------------------------------------------------------------------------
 # membership
 # ----------------------------------------------------------------------------
-def agree_members(store: Any, prefix: str, gen: int, rank: int, world: int, lost: List[int], grace: float) -> List[int]:
+def agree_members(store: Any, prefix: str, gen: int, rank: int, world: int, lost: List[int], grace: float,
+                  wait_all: float = 5.0) -> List[int]:
     """Survivors of generation ``gen - 1`` agree on the members of generation ``gen``.
 
-    Each survivor announces itself, waits ``grace`` seconds, then proposes the
-    set of announced ranks; the first proposal stored wins (compare-and-set),
-    so every survivor builds the communicator over the same list.
+    Each survivor announces itself and waits until every rank it does not
+    know to be lost has announced too (at most ``max(grace, wait_all)``
+    seconds: a rank that died unnoticed is not waited for forever, and the
+    common case needs no fixed sleep), then proposes the set of announced
+    ranks; the first proposal stored wins (compare-and-set), so every survivor
+    builds the communicator over the same list.  A survivor that announces too
+    late to be included asks for generation ``gen + 1`` instead of giving up
+    (:meth:`XgmiDataPlane._rebuild`).
     """
     base = f"{prefix}/g{gen}"
     store.set(f"{base}/alive/{rank}", "1")
-    time.sleep(grace)
-    alive = [r for r in range(world) if r not in lost and store.check([f"{base}/alive/{r}"])]
+    expect = [f"{base}/alive/{r}" for r in range(world) if r not in lost]
+    t0 = time.monotonic()
+    while True:
+        if store.check([f"{base}/members"]):
+            break  # someone already decided; joining late changes nothing
+        if all(store.check([k]) for k in expect):
+            break
+        waited = time.monotonic() - t0
+        if waited >= max(grace, wait_all):
+            break
+        time.sleep(0.005)
+    # every announced rank is alive, including one the others had written off
+    # (left out of an earlier generation): only ranks that never announce stay out
+    alive = [r for r in range(world) if store.check([f"{base}/alive/{r}"])]
     if rank not in alive:
         alive.append(rank)
     got = store.compare_set(f"{base}/members", "", json.dumps(sorted(alive)))
@@ -384,6 +403,13 @@ class XgmiDataPlane:
         self.ready = threading.Event()
         self.failed: Optional[str] = None
         self.stats = collections.Counter()
+        # generation-0 backend actually in use ("rccl", or "gloo" after a fallback)
+        self.backend_name: Optional[str] = None
+        self.fallback_reason: Optional[str] = None
+        # False: a failed primary backend fails the plane instead of degrading
+        self.allow_fallback = True
+        self._late_joins = 0
+        self.max_late_joins = 3
         self._issuer = threading.Thread(target=self._issue_loop, name=f"xgmi-issue-{self.name}", daemon=True)
         self._completer = threading.Thread(target=self._complete_loop, name=f"xgmi-complete-{self.name}", daemon=True)
         self._alloc_stream: Any = None
@@ -434,19 +460,27 @@ class XgmiDataPlane:
         if self.fallback is None or self._store is None or self.world == 1:
             if backend is None:
                 raise err  # type: ignore[misc]
+            self.backend_name = backend.name
             return backend
         keys = [f"{self._prefix}/g0/ok/{r}" for r in members]
         self._store.set(keys[members.index(self.rank)], "1" if backend is not None else "0")
         self._store.wait(keys, datetime.timedelta(seconds=self.group_timeout * 2))
         if all(bytes(self._store.get(k)) == b"1" for k in keys):
+            self.backend_name = backend.name  # type: ignore[union-attr]
             return backend  # type: ignore[return-value]
-        logger.warning(self.name, f"xgmi data plane: primary backend failed on some rank ({err}); using the fallback")
+        failed_on = [r for r, k in zip(members, keys) if bytes(self._store.get(k)) != b"1"]
+        self.fallback_reason = f"primary backend failed on rank(s) {failed_on}" + (f": {err}" if err else "")
         if backend is not None:
             try:
                 backend.abort()
             except Exception:
                 pass
-        return self.fallback(0, members)
+        if not self.allow_fallback:
+            raise RuntimeError(f"{self.fallback_reason}; fallback disallowed")
+        logger.warning(self.name, f"xgmi data plane: {self.fallback_reason}; using the fallback")
+        fb = self.fallback(0, members)
+        self.backend_name = fb.name
+        return fb
 
     def _preconnect(self) -> None:
         """Epoch 0: exchange one element with every member (opens every xGMI
@@ -549,6 +583,8 @@ class XgmiDataPlane:
                 op.epoch = int(epoch)
                 self._pending[op.epoch].append(op)
             self._cv.notify_all()
+        if bad is None:
+            logger.tracer.record(self.name, "xgmi_ack", op.t0, time.monotonic() - op.t0, peer=op.peer, epoch=op.epoch)
         if bad is not None:
             logger.error(self.name, f"xgmi push {seq} dropped: {bad}")
             self._done(op, False, bad, False)
@@ -619,6 +655,7 @@ class XgmiDataPlane:
                 self._done(op, False, "no answer from the receiver", True)
             if not ops:
                 continue
+            t_issue = time.monotonic()
             try:
                 h = backend.issue(ops, index)
             except Exception as e:
@@ -630,7 +667,7 @@ class XgmiDataPlane:
                 continue
             self.stats["groups"] += 1
             with self._cv:
-                self._inflight.append((h, ops, time.monotonic(), gen))
+                self._inflight.append((h, ops, t_issue, gen))
                 self._cv.notify_all()
 
     def _complete_loop(self) -> None:
@@ -666,6 +703,13 @@ class XgmiDataPlane:
                 backend.release(h)
             except Exception:
                 pass
+            t_done = time.monotonic()
+            nbytes = sum(op.tensor.numel() * op.tensor.element_size() for op in ops)
+            logger.tracer.record(self.name, "xgmi_group", t0, t_done - t0, epoch=ops[0].epoch, ops=len(ops), nbytes=nbytes)
+            for op in ops:
+                if op.seq >= 0:  # not the pre-connect exchange
+                    key = "link_tx_bytes" if op.kind == SEND else "link_rx_bytes"
+                    logger.tracer.count(self.name, f"{key}/{op.peer}", op.tensor.numel() * op.tensor.element_size())
             for op in ops:
                 if op.kind == SEND:
                     self.stats["sent"] += 1
@@ -759,27 +803,48 @@ class XgmiDataPlane:
         try:
             members = agree_members(self._store, self._prefix, gen, self.rank, self.world, sorted(self._lost), self.rebuild_grace)
             if self.rank not in members:
+                # announced too late for generation `gen`: ask everyone to
+                # build gen + 1 (which waits for this rank's announcement)
+                # instead of failing for good
+                self._late_joins += 1
+                if self._late_joins <= self.max_late_joins:
+                    logger.info(self.name, f"left out of data-plane generation {gen}; requesting generation {gen + 1}")
+                    # announce for gen + 1 BEFORE asking for it: the others
+                    # have written this rank off as lost and would not wait
+                    self._store.set(f"{self._prefix}/g{gen + 1}/alive/{self.rank}", "1")
+                    self.request_rebuild("rejoin after being left out", gen=gen + 1)
+                    return
                 raise RuntimeError("excluded from the new generation")
             if self._stopped:
                 return
             backend = self._make_backend(gen, members)
         except Exception as e:
             with self._cv:
+                if self.gen != gen:
+                    return  # superseded by a newer generation while agreeing
                 self.failed = f"data plane rebuild failed: {e}"
                 self._rebuilding = False
                 self._cv.notify_all()
             logger.error(self.name, self.failed)
             return
         with self._cv:
-            self.members = members
-            self._index = {r: i for i, r in enumerate(members)}
-            self._lost |= {r for r in range(self.world) if r not in members}
-            self._backend = backend
-            self._alloc_stream = getattr(backend, "stream", None)
-            self._open = 0
-            self._rebuilding = False
-            self.stats["rebuilds"] += 1
-            self._cv.notify_all()
+            superseded = self.gen != gen  # a newer generation was requested meanwhile
+            if not superseded:
+                self.members = members
+                self._index = {r: i for i, r in enumerate(members)}
+                self._lost = (self._lost | {r for r in range(self.world) if r not in members}) - set(members)
+                self._backend = backend
+                self._alloc_stream = getattr(backend, "stream", None)
+                self._open = 0
+                self._rebuilding = False
+                self.stats["rebuilds"] += 1
+                self._cv.notify_all()
+        if superseded:
+            try:
+                backend.abort()
+            except Exception:
+                pass
+            return
         logger.info(self.name, f"xgmi data plane generation {gen} up: members {members}")
 
 
@@ -796,7 +861,7 @@ def make_backend_factory(kind: str, rank: int, store: Any, prefix: str, device: 
             if rank == members[0]:
                 store.set(key, ops.ext().rccl_unique_id())
             uid = store.get(key)  # blocks until the first member published it
-            return RcclBackend(bytes(uid), members, rank, device, timeout)
+            return RcclBackend(bytes(uid), members, rank, device, timeout, init_timeout=max(timeout, 30.0))
         if kind == "gloo":
             return GlooBackend(store, base + "/gloo", members, rank, timeout)
         if kind == "sim":

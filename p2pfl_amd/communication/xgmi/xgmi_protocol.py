@@ -70,6 +70,7 @@ class XgmiJob:
 
     ``backend``: ``"rccl"`` (GPU), ``"gloo"`` (CPU, multi-process),
     ``"sim"`` (in-process tests, needs ``fabric``), or ``"auto"``.
+    :attr:`backend_in_use` is what the data plane actually agreed on.
     """
 
     def __init__(
@@ -85,8 +86,13 @@ class XgmiJob:
         ack_timeout: float = 10.0,
         group_timeout: float = 60.0,
         rebuild_grace: float = 0.5,
+        allow_fallback: bool = True,
     ) -> None:
         self.rank, self.world, self.store = rank, world, store
+        # with the rccl backend: may the plane degrade to gloo through host
+        # memory when RCCL cannot come up on every rank?  (False: the plane
+        # fails and says why -- benchmarks must not report a gloo number as xGMI)
+        self.allow_fallback = allow_fallback
         self.device = torch.device(device) if device is not None else torch.device("cpu")
         if backend == "auto":
             from p2pfl_amd import ops
@@ -150,6 +156,7 @@ class XgmiJob:
                 ack_timeout=self.ack_timeout, group_timeout=self.group_timeout, rebuild_grace=self.rebuild_grace,
                 name=name, preconnect=self.backend == "rccl",
             )
+            self.plane.allow_fallback = self.allow_fallback
             if self.backend == "rccl":
                 # gloo staged through host memory if RCCL cannot come up on every rank
                 self.plane.fallback = make_backend_factory(
@@ -158,6 +165,12 @@ class XgmiJob:
             plane = self.plane
         plane.start()
         return plane
+
+    @property
+    def backend_in_use(self) -> Optional[str]:
+        """The data plane's agreed backend once it is up (``None`` before / if it failed)."""
+        plane = self.plane
+        return plane.backend_name if plane is not None else None
 
     def stop_plane(self) -> None:
         with self._lock:

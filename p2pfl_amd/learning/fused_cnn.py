@@ -326,8 +326,11 @@ class FusedCNNLearner(TorchLearner):
     def fit(self) -> None:
         if self.epochs <= 0 or self.model is None:
             return
-        with self._on_stream():
-            self._fit_fused()
+        try:
+            with self._on_stream():
+                self._fit_fused()
+        finally:
+            self._arena_changed()  # no snapshot taken mid-fit survives it
 
     def _fit_fused(self) -> None:
         self._interrupt.clear()

@@ -54,10 +54,13 @@ class Settings:
     aggregate is pushed to every lagging neighbour; a newer round's diffusion
     supersedes an older one."""
 
-    NODE_STREAMS: bool = True
+    NODE_STREAMS: bool | str = "auto"
     """GPU learners train / evaluate on their own HIP stream (virtual peers in
     one process then overlap each other and the aggregation / transport work
-    left on the default stream)."""
+    left on the default stream).  ``"auto"``: only while more than one learner
+    of this process lives on the same GPU (one peer per GPU gains nothing from
+    a private stream); ``True`` / ``False`` force it.  The hand-off between the
+    learner's stream and the default stream is event-ordered (no host sync)."""
 
     TRAIN_SET_SIZE: int = 4
     """Number of nodes elected to train each experiment."""

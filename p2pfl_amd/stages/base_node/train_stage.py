@@ -93,5 +93,8 @@ class TrainStage(Stage):
             model_fn,
             create_connection=True,
             wakeup=state.changed,
-            peer_status_fn=peer_has,
+            # a re-send is due when the peer's report moved OR this node's own
+            # aggregate grew (a richer partial aggregate goes out at once
+            # instead of waiting a GOSSIP_MODELS_PERIOD per hop)
+            peer_status_fn=lambda n: (peer_has(n), sorted(aggregator.get_aggregated_models())),
         )

@@ -248,3 +248,143 @@ def test_primary_backend_failure_on_one_rank_switches_every_rank_to_fallback():
     finally:
         for p in planes:
             p.stop()
+
+
+def test_bus_carries_records_larger_than_one_packet():
+    """A record above MAX_RECORD (the fallback path of a model the data plane
+    cannot carry) arrives intact, in order with the small records around it,
+    and the bulk connection that carried it does not count as the peer leaving."""
+    from p2pfl_amd.communication.xgmi.bus import MAX_RECORD
+
+    got, closed = [], []
+    a = BusEndpoint("busA-frag", lambda src, data: got.append(data), lambda src: closed.append(src))
+    b = BusEndpoint("busB-frag", lambda src, data: None)
+    a.start()
+    b.start()
+    try:
+        big = bytes(random.Random(0).getrandbits(8) for _ in range(4096)) * (3 * MAX_RECORD // 4096 + 7)
+        b.send("busA-frag", b"before")
+        b.send("busA-frag", big)
+        b.send("busA-frag", b"after")
+        b.send("busA-frag", big[: MAX_RECORD + 1])
+        t0 = time.time()
+        while len(got) < 4 and time.time() - t0 < 10:
+            time.sleep(0.01)
+        small = [g for g in got if len(g) < 16]
+        large = [g for g in got if len(g) >= 16]
+        assert small == [b"before", b"after"]
+        assert large == [big, big[: MAX_RECORD + 1]]
+        b.drop("busA-frag")  # closes both connections: the main one reports the exit
+        t0 = time.time()
+        while not closed and time.time() - t0 < 5:
+            time.sleep(0.01)
+        assert closed == ["busB-frag"]
+    finally:
+        a.close()
+        b.close()
+
+
+def test_unusable_data_plane_still_delivers_models_larger_than_a_bus_packet():
+    """With the data plane down (init/rebuild failed), a 26 MB CNN must still
+    reach the peer over the control bus instead of evicting the neighbour."""
+    from p2pfl_amd.communication.xgmi import XgmiSimNetwork
+    from p2pfl_amd.data import MnistFederatedDM
+    from p2pfl_amd.models import CNN
+    from p2pfl_amd.node import Node
+    from p2pfl_amd.utils import check_equal_models, wait_4_results, wait_convergence
+
+    net = XgmiSimNetwork()
+    nodes = [Node(CNN(seed=i), MnistFederatedDM(sub_id=i, number_sub=400), protocol=net.protocol) for i in range(2)]
+    for nd in nodes:
+        nd.start()
+    try:
+        nodes[1].connect(nodes[0].addr)
+        wait_convergence(nodes, 1, only_direct=True, wait=10)
+        for nd in nodes:
+            plane = nd._communication_protocol.plane
+            assert plane.ready.wait(10)
+            plane.failed = "forced off by the test"
+        nodes[0].set_start_learning(rounds=1, epochs=0)
+        wait_4_results(nodes, timeout=120)
+        check_equal_models(nodes)
+        # still neighbours: nobody was dropped for an oversized record
+        assert nodes[1].addr in nodes[0].get_neighbors(only_direct=True)
+    finally:
+        for nd in nodes:
+            nd.stop()
+
+
+def test_late_rank_rejoins_next_generation_instead_of_failing():
+    """A survivor that announces after the others agreed on generation g
+    requests g + 1, and every survivor ends in the same generation."""
+    import torch.distributed as dist
+
+    from p2pfl_amd.communication.xgmi.data_plane import agree_members
+
+    store = dist.HashStore()
+    # ranks 0 and 1 agree on g1 without rank 2 (it is late: its announcement
+    # has not arrived within their wait)
+    got = agree_members(store, "lj", 1, 0, 3, [], 0.0, wait_all=0.05)
+    assert got == [0]
+    assert agree_members(store, "lj", 1, 1, 3, [], 0.0, wait_all=0.05) == [0]
+    # rank 2 is excluded from g1: it announces for g2 and then asks for it;
+    # g2 includes everyone who announced, even a rank written off as lost
+    store.set("lj/g2/alive/2", "1")
+    res = {}
+    ths = [threading.Thread(target=lambda r=r: res.__setitem__(r, agree_members(store, "lj", 2, r, 3, [2] if r < 2 else [], 0.0, wait_all=2.0)))
+           for r in range(3)]
+    for th in ths:
+        th.start()
+    for th in ths:
+        th.join()
+    assert res[0] == res[1] == res[2] == [0, 1, 2]
+
+
+def test_plane_fallback_disallowed_fails_loudly():
+    import torch.distributed as dist
+
+    from p2pfl_amd.communication.xgmi.data_plane import SimBackend
+
+    fabric, store = SimFabric(), dist.HashStore()
+
+    def primary(rank):
+        def make(gen, members):
+            if rank == 1:
+                raise RuntimeError("no RCCL here")
+            return SimBackend(fabric, members, rank)
+        return make
+
+    planes = []
+    for r in range(2):
+        p = XgmiDataPlane(r, 2, primary(r), store=store, prefix="nf", preconnect=False, group_timeout=10)
+        p.fallback = make_backend_factory("sim", r, store, "nf", torch.device("cpu"), fabric)
+        p.allow_fallback = False
+        planes.append(p)
+    for p in planes:
+        p.start()
+    try:
+        for p in planes:
+            assert p.ready.wait(10)
+            assert p.failed is not None and "fallback disallowed" in p.failed and "[1]" in p.failed
+            assert not p.usable
+    finally:
+        for p in planes:
+            p.stop()
+
+
+@pytest.mark.timeout(600)
+def test_bench_reports_the_backend_actually_used():
+    """--plane-backend rccl on a machine without RCCL: with --allow-fallback the
+    JSON says xgmi/gloo (the fallback is never reported as rccl); without it the
+    run fails instead of producing a mislabelled number."""
+    base = [sys.executable, "bench.py", "--gpus", "2", "--steps", "1", "--warmup", "0", "--impl", "torch",
+            "--number-sub", "400", "--watchdog", "240", "--plane-backend", "rccl"]
+    r = subprocess.run(base + ["--allow-fallback"], cwd=ROOT, env=_env(), capture_output=True, text=True, timeout=560)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
+    rec = [json.loads(ln) for ln in r.stdout.splitlines() if ln.startswith("{")][0]
+    assert rec["transport"] == "xgmi/gloo"
+    # per-rank, per-round breakdown on stderr at N > 1
+    assert any("round 1: wall" in ln and "pushes: ack" in ln for ln in r.stderr.splitlines()), r.stderr[-3000:]
+    r = subprocess.run(base, cwd=ROOT, env=_env(), capture_output=True, text=True, timeout=560)
+    assert r.returncode != 0
+    assert "fallback disallowed" in (r.stdout + r.stderr)
