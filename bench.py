@@ -501,7 +501,8 @@ def main() -> None:
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=3, help="timed federated rounds")
     ap.add_argument("--warmup", type=int, default=1, help="untimed federated rounds")
-    ap.add_argument("--aggregation", choices=["gossip", "allreduce"], default="gossip")
+    ap.add_argument("--aggregation", choices=["gossip", "allreduce"], default="gossip",
+                    help="gossip: the product (Node + stages + xGMI gossip); allreduce: LEGACY round-1 comparison runner")
     ap.add_argument("--impl", choices=["fused", "torch", "reference"], default="fused")
     ap.add_argument("--model", choices=["cnn", "resnet18", "resnet50", "vit_b16"], default="cnn")
     ap.add_argument("--epochs", type=int, default=1)

@@ -28,15 +28,18 @@ P2_DEVICE f32x4 load4(const void* base, int64_t i, bool bf16) {
 }
 
 // bf16_mask bit k: input k is bf16 (else fp32).  The mask is uniform across
-// the grid, so the per-input dtype test never diverges.
+// the grid, so the per-input dtype test never diverges.  acc_in (may alias
+// out, may be null) seeds the fp32 accumulator: a running FedAvg sum folds the
+// models in as they arrive and only the last call applies the 1/sum(w) scale.
 template <int K>
-__global__ __launch_bounds__(256) void wsum_kernel(WSumArgs a, uint32_t bf16_mask, void* __restrict__ out, int out_bf16,
-                                                   int64_t n4, int accumulate) {
+__global__ __launch_bounds__(256) void wsum_kernel(WSumArgs a, uint32_t bf16_mask, const float* acc_in, float scale,
+                                                   void* out, int out_bf16, int64_t n4) {
   const int64_t stride = int64_t(gridDim.x) * blockDim.x;
   for (int64_t i = int64_t(blockIdx.x) * blockDim.x + threadIdx.x; i < n4; i += stride) {
-    f32x4 acc = accumulate ? reinterpret_cast<const f32x4*>(out)[i] : f32x4{0.f, 0.f, 0.f, 0.f};
+    f32x4 acc = acc_in ? reinterpret_cast<const f32x4*>(acc_in)[i] : f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int k = 0; k < K; ++k) acc += a.w[k] * load4(a.src[k], i, (bf16_mask >> k) & 1u);
+    acc *= scale;
     if (out_bf16) {
       reinterpret_cast<uint2*>(out)[i] = uint2{pack_bf16x2(acc[0], acc[1]), pack_bf16x2(acc[2], acc[3])};
     } else {
@@ -45,16 +48,17 @@ __global__ __launch_bounds__(256) void wsum_kernel(WSumArgs a, uint32_t bf16_mas
   }
 }
 
-__global__ void wsum_tail(WSumArgs a, uint32_t bf16_mask, int k, void* out, int out_bf16, int64_t start, int64_t n,
-                          int accumulate) {
+__global__ void wsum_tail(WSumArgs a, uint32_t bf16_mask, int k, const float* acc_in, float scale, void* out,
+                          int out_bf16, int64_t start, int64_t n) {
   int64_t i = start + blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
-  float acc = accumulate ? reinterpret_cast<const float*>(out)[i] : 0.f;
+  float acc = acc_in ? acc_in[i] : 0.f;
   for (int j = 0; j < k; ++j) {
     const float v = ((bf16_mask >> j) & 1u) ? bf16_to_f32(reinterpret_cast<const uint16_t*>(a.src[j])[i])
                                             : reinterpret_cast<const float*>(a.src[j])[i];
     acc = fmaf(a.w[j], v, acc);
   }
+  acc *= scale;
   if (out_bf16)
     reinterpret_cast<uint16_t*>(out)[i] = f32_to_bf16(acc);
   else
@@ -62,14 +66,16 @@ __global__ void wsum_tail(WSumArgs a, uint32_t bf16_mask, int k, void* out, int 
 }
 
 template <int K>
-static void launch_k(const WSumArgs& a, uint32_t mask, void* out, int out_bf16, int64_t n4, int acc, hipStream_t s) {
-  hipLaunchKernelGGL(wsum_kernel<K>, dim3(stream_grid(n4, 256)), dim3(256), 0, s, a, mask, out, out_bf16, n4, acc);
+static void launch_k(const WSumArgs& a, uint32_t mask, const float* acc_in, float scale, void* out, int out_bf16,
+                     int64_t n4, hipStream_t s) {
+  hipLaunchKernelGGL(wsum_kernel<K>, dim3(stream_grid(n4, 256)), dim3(256), 0, s, a, mask, acc_in, scale, out,
+                     out_bf16, n4);
 }
 
-void weighted_sum(const void* const* srcs, const int* src_bf16, const float* weights, int k, void* out, int out_bf16,
-                  int64_t n, hipStream_t stream) {
+void weighted_sum(const void* const* srcs, const int* src_bf16, const float* weights, int k, const float* acc_in,
+                  float scale, void* out, int out_bf16, int64_t n, hipStream_t stream) {
   int done = 0;
-  while (done < k) {
+  do {
     const int kk = (k - done) < kMaxInputs ? (k - done) : kMaxInputs;
     WSumArgs a{};
     uint32_t mask = 0;
@@ -78,31 +84,37 @@ void weighted_sum(const void* const* srcs, const int* src_bf16, const float* wei
       a.w[j] = weights[done + j];
       if (src_bf16[done + j]) mask |= 1u << j;
     }
-    const int acc = done > 0;  // chunks after the first accumulate (fp32 output only; checked by the caller)
+    // chunks after the first accumulate into out (fp32 output only; checked by
+    // the caller); only the last chunk applies the scale
+    const float* acc = done > 0 ? static_cast<const float*>(out) : acc_in;
+    const bool last = done + kk >= k;
+    const float sc = last ? scale : 1.f;
+    const int ob = last ? out_bf16 : 0;
     const int64_t n4 = n / 4;
     switch (kk) {
-      case 1: launch_k<1>(a, mask, out, out_bf16, n4, acc, stream); break;
-      case 2: launch_k<2>(a, mask, out, out_bf16, n4, acc, stream); break;
-      case 3: launch_k<3>(a, mask, out, out_bf16, n4, acc, stream); break;
-      case 4: launch_k<4>(a, mask, out, out_bf16, n4, acc, stream); break;
-      case 5: launch_k<5>(a, mask, out, out_bf16, n4, acc, stream); break;
-      case 6: launch_k<6>(a, mask, out, out_bf16, n4, acc, stream); break;
-      case 7: launch_k<7>(a, mask, out, out_bf16, n4, acc, stream); break;
-      case 8: launch_k<8>(a, mask, out, out_bf16, n4, acc, stream); break;
-      case 9: launch_k<9>(a, mask, out, out_bf16, n4, acc, stream); break;
-      case 10: launch_k<10>(a, mask, out, out_bf16, n4, acc, stream); break;
-      case 11: launch_k<11>(a, mask, out, out_bf16, n4, acc, stream); break;
-      case 12: launch_k<12>(a, mask, out, out_bf16, n4, acc, stream); break;
-      case 13: launch_k<13>(a, mask, out, out_bf16, n4, acc, stream); break;
-      case 14: launch_k<14>(a, mask, out, out_bf16, n4, acc, stream); break;
-      case 15: launch_k<15>(a, mask, out, out_bf16, n4, acc, stream); break;
-      default: launch_k<16>(a, mask, out, out_bf16, n4, acc, stream); break;
+      case 0: launch_k<0>(a, mask, acc, sc, out, ob, n4, stream); break;
+      case 1: launch_k<1>(a, mask, acc, sc, out, ob, n4, stream); break;
+      case 2: launch_k<2>(a, mask, acc, sc, out, ob, n4, stream); break;
+      case 3: launch_k<3>(a, mask, acc, sc, out, ob, n4, stream); break;
+      case 4: launch_k<4>(a, mask, acc, sc, out, ob, n4, stream); break;
+      case 5: launch_k<5>(a, mask, acc, sc, out, ob, n4, stream); break;
+      case 6: launch_k<6>(a, mask, acc, sc, out, ob, n4, stream); break;
+      case 7: launch_k<7>(a, mask, acc, sc, out, ob, n4, stream); break;
+      case 8: launch_k<8>(a, mask, acc, sc, out, ob, n4, stream); break;
+      case 9: launch_k<9>(a, mask, acc, sc, out, ob, n4, stream); break;
+      case 10: launch_k<10>(a, mask, acc, sc, out, ob, n4, stream); break;
+      case 11: launch_k<11>(a, mask, acc, sc, out, ob, n4, stream); break;
+      case 12: launch_k<12>(a, mask, acc, sc, out, ob, n4, stream); break;
+      case 13: launch_k<13>(a, mask, acc, sc, out, ob, n4, stream); break;
+      case 14: launch_k<14>(a, mask, acc, sc, out, ob, n4, stream); break;
+      case 15: launch_k<15>(a, mask, acc, sc, out, ob, n4, stream); break;
+      default: launch_k<16>(a, mask, acc, sc, out, ob, n4, stream); break;
     }
     const int64_t tail = n - n4 * 4;
     if (tail > 0)
-      hipLaunchKernelGGL(wsum_tail, dim3(1), dim3(64), 0, stream, a, mask, kk, out, out_bf16, n4 * 4, n, acc);
+      hipLaunchKernelGGL(wsum_tail, dim3(1), dim3(64), 0, stream, a, mask, kk, acc, sc, out, ob, n4 * 4, n);
     done += kk;
-  }
+  } while (done < k);
 }
 
 }  // namespace p2

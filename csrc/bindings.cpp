@@ -29,14 +29,23 @@ void check_arena(const torch::Tensor& t, const char* name) {
   TORCH_CHECK(reinterpret_cast<uintptr_t>(t.data_ptr()) % 16 == 0, name, " must be 16-byte aligned");
 }
 
-void weighted_sum(std::vector<torch::Tensor> srcs, std::vector<double> weights, torch::Tensor out) {
-  TORCH_CHECK(!srcs.empty() && srcs.size() == weights.size(), "weighted_sum: bad inputs");
+void weighted_sum(std::vector<torch::Tensor> srcs, std::vector<double> weights, torch::Tensor out,
+                  c10::optional<torch::Tensor> acc_in, double scale) {
+  TORCH_CHECK(srcs.size() == weights.size(), "weighted_sum: bad inputs");
   check_arena(out, "out");
   const bool out_bf16 = out.scalar_type() == torch::kBFloat16;
   TORCH_CHECK(!out_bf16 || srcs.size() <= size_t(p2::kMaxInputs), "weighted_sum: bf16 output supports at most ",
               p2::kMaxInputs, " inputs");
   const c10::DeviceGuard guard(out.device());
   const int64_t n = out.numel();
+  const float* acc = nullptr;
+  if (acc_in.has_value() && acc_in->defined()) {
+    check_arena(*acc_in, "acc_in");
+    TORCH_CHECK(acc_in->scalar_type() == torch::kFloat32 && acc_in->numel() == n && acc_in->device() == out.device(),
+                "weighted_sum: acc_in must be an fp32 arena of the output's size and device");
+    acc = acc_in->data_ptr<float>();
+  }
+  TORCH_CHECK(!srcs.empty() || acc != nullptr, "weighted_sum: no inputs");
   std::vector<const void*> ptrs;
   std::vector<int> bf;
   std::vector<float> w;
@@ -48,7 +57,8 @@ void weighted_sum(std::vector<torch::Tensor> srcs, std::vector<double> weights, 
     bf.push_back(srcs[i].scalar_type() == torch::kBFloat16 ? 1 : 0);
     w.push_back(float(weights[i]));
   }
-  p2::weighted_sum(ptrs.data(), bf.data(), w.data(), int(ptrs.size()), out.data_ptr(), out_bf16 ? 1 : 0, n, stream());
+  p2::weighted_sum(ptrs.data(), bf.data(), w.data(), int(ptrs.size()), acc, float(scale), out.data_ptr(),
+                   out_bf16 ? 1 : 0, n, stream());
 }
 
 uint16_t* opt_bf16(const c10::optional<torch::Tensor>& t, int64_t n) {
@@ -212,7 +222,10 @@ void register_conv(pybind11::module& m);
 
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.doc() = "p2pfl_amd native HIP/CDNA4 kernels (gfx950)";
-  m.def("weighted_sum", &weighted_sum, "out = sum_i w_i * src_i (flat arenas, fp32/bf16 in, fp32/bf16 out)");
+  m.def("weighted_sum", &weighted_sum,
+        "out = scale * (acc_in + sum_i w_i * src_i) (flat arenas, fp32/bf16 in, fp32/bf16 out, fp32 running sum)",
+        pybind11::arg("srcs"), pybind11::arg("weights"), pybind11::arg("out"), pybind11::arg("acc_in") = pybind11::none(),
+        pybind11::arg("scale") = 1.0);
   m.def("adam_step", &adam_step, "fused whole-arena Adam/AdamW step");
   m.def("sgd_step", &sgd_step, "fused whole-arena SGD(+momentum/nesterov) step");
   m.def("adam_mt_step", &adam_mt_step, "multi-tensor Adam/AdamW over per-tensor grads into flat fp32 state",

@@ -8,10 +8,14 @@ namespace p2 {
 
 constexpr int kMaxInputs = 16;
 
-// out[i] = sum_j weights[j] * srcs[j][i]; each src fp32 or bf16 (src_bf16[j]),
-// out fp32 or bf16, fp32 accumulation; k may exceed kMaxInputs (fp32 out only).
-void weighted_sum(const void* const* srcs, const int* src_bf16, const float* weights, int k, void* out, int out_bf16,
-                  int64_t n, hipStream_t s);
+// out[i] = scale * (acc_in[i] + sum_j weights[j] * srcs[j][i]), fp32
+// accumulation in input order (acc_in: fp32 running sum or null = 0; it may
+// alias out).  Each src fp32 or bf16 (src_bf16[j]); out fp32 or bf16; k may be
+// 0 (just scale acc_in) and may exceed kMaxInputs (fp32 out only).  Folding a
+// set of inputs in several calls (running sum, scale on the last) gives the
+// bitwise-same result as one call over all of them.
+void weighted_sum(const void* const* srcs, const int* src_bf16, const float* weights, int k, const float* acc_in,
+                  float scale, void* out, int out_bf16, int64_t n, hipStream_t s);
 
 struct AdamParams {
   float lr, beta1, beta2, eps, weight_decay;

@@ -27,7 +27,6 @@
 #include <atomic>
 #include <cstring>
 #include <mutex>
-#include <shared_mutex>
 #include <stdexcept>
 #include <string>
 #include <thread>
@@ -82,13 +81,17 @@ class RcclPlane {
     ncclResult_t r;
     {
       py::gil_scoped_release nogil;
+      std::lock_guard<std::mutex> nl(nccl_mu_);
       r = ncclCommInitRankConfig(&comm_, nranks_, uid, rank_, &cfg);
       if (r == ncclInProgress) r = settle(init_timeout_s);
+      if (r != ncclSuccess) {
+        if (comm_ != nullptr) ncclCommAbort(comm_);
+        comm_ = nullptr;
+      }
     }
     if (r != ncclSuccess) {
-      if (comm_ != nullptr) ncclCommAbort(comm_);
-      comm_ = nullptr;
       hipStreamDestroy(stream_);
+      stream_ = nullptr;
       throw std::runtime_error("ncclCommInitRankConfig: " + nccl_msg(r));
     }
   }
@@ -105,17 +108,29 @@ class RcclPlane {
   // first waits on every stream in `after` (the producers of the send
   // buffers / previous users of the receive buffers).  Returns a group id.
   //
-  // Lock discipline (no host mutex is ever held while the GIL is taken back):
-  // argument checks run under the GIL only; the RCCL group is enqueued with
-  // the GIL released under issue_mu_ (one group at a time on the
-  // communicator) and comm_mu_ (shared; abort takes it exclusively), both of
-  // which are dropped before the GIL is re-acquired; the group's bookkeeping
-  // entry is added afterwards under a short mu_ section.  wait/query/release
-  // take mu_ with the GIL held, so holding mu_ across a GIL re-acquire would
-  // be a lock-order inversion (issuer: mu_ -> GIL, completer: GIL -> mu_).
+  // Threading (the data plane issues from one thread and completes from
+  // another):
+  //  * no RCCL or HIP call is made while holding the GIL -- a call that blocks
+  //    inside the runtime must never stall every Python thread;
+  //  * no host mutex is held across a GIL re-acquire (mu_ guards only the
+  //    group table, in short sections taken with the GIL held);
+  //  * every RCCL call on the communicator is serialised by nccl_mu_.  With a
+  //    non-blocking communicator ncclGroupEnd hands the group to a job thread,
+  //    and ncclCommGetAsyncError may *join* that job: two threads polling it
+  //    concurrently (issuer settling its group, completer checking for
+  //    errors) would both join one thread.  The completer therefore only
+  //    try-locks nccl_mu_ to poll for asynchronous errors and skips the poll
+  //    while a group is being issued.
   int64_t issue(const std::vector<std::tuple<int64_t, int64_t, torch::Tensor>>& ops, const std::vector<int64_t>& after,
                 double timeout_s) {
     TORCH_CHECK(!aborted_, "RcclPlane: communicator aborted/closed");
+    struct RawOp {
+      int kind, peer;
+      void* ptr;
+      size_t nbytes;
+    };
+    std::vector<RawOp> raw;
+    GroupRec rec;
     for (const auto& op : ops) {
       const auto& t = std::get<2>(op);
       const int64_t peer = std::get<1>(op), kind = std::get<0>(op);
@@ -123,53 +138,55 @@ class RcclPlane {
       TORCH_CHECK(peer >= 0 && peer < nranks_, "RcclPlane: peer ", peer, " out of range");
       TORCH_CHECK(t.is_cuda() && t.is_contiguous(), "RcclPlane: buffers must be contiguous GPU tensors");
       TORCH_CHECK(t.get_device() == device_, "RcclPlane: buffer on device ", t.get_device(), ", plane on ", device_);
+      raw.push_back({int(kind), int(peer), t.data_ptr(), size_t(t.numel()) * t.element_size()});
+      rec.keep.push_back(t);  // buffers stay alive until the group is released
     }
-    hip_ok(hipSetDevice(device_), "hipSetDevice");
-    for (int64_t s : after) {
-      hipEvent_t ev;
-      hip_ok(hipEventCreateWithFlags(&ev, hipEventDisableTiming), "hipEventCreate");
-      hip_ok(hipEventRecord(ev, reinterpret_cast<hipStream_t>(s)), "hipEventRecord(producer)");
-      hip_ok(hipStreamWaitEvent(stream_, ev, 0), "hipStreamWaitEvent");
-      hip_ok(hipEventDestroy(ev), "hipEventDestroy");
-    }
-    GroupRec rec;
-    ncclResult_t r;
+    ncclResult_t r = ncclSuccess;
     bool gone = false;
+    std::string herr;
     {
       py::gil_scoped_release nogil;
-      std::lock_guard<std::mutex> il(issue_mu_);
-      std::shared_lock<std::shared_mutex> cl(comm_mu_);
+      std::lock_guard<std::mutex> nl(nccl_mu_);
       if (comm_ == nullptr) {
         gone = true;
-        r = ncclInvalidUsage;
       } else {
-        r = ncclGroupStart();
-      }
-      for (const auto& op : ops) {
-        if (r != ncclSuccess) break;
-        const auto& t = std::get<2>(op);
-        const size_t nbytes = size_t(t.numel()) * t.element_size();
-        const int peer = int(std::get<1>(op));
-        r = std::get<0>(op) == 0 ? ncclSend(t.data_ptr(), nbytes, ncclUint8, peer, comm_, stream_)
-                                 : ncclRecv(t.data_ptr(), nbytes, ncclUint8, peer, comm_, stream_);
-      }
-      if (!gone) {
-        ncclResult_t e = ncclGroupEnd();
-        if (r == ncclSuccess) r = e;
-        if (r == ncclInProgress) r = settle(timeout_s);
-        // the completion event is recorded right behind the group, before
-        // another issuer can enqueue on the comm stream
-        if (r == ncclSuccess && hipEventCreateWithFlags(&rec.done, hipEventDisableTiming) == hipSuccess &&
-            hipEventRecord(rec.done, stream_) != hipSuccess) {
-          hipEventDestroy(rec.done);
-          rec.done = nullptr;
+        auto hcheck = [&](hipError_t e, const char* what) {
+          if (e != hipSuccess && herr.empty()) herr = std::string(what) + ": " + hipGetErrorString(e);
+          return e == hipSuccess;
+        };
+        hcheck(hipSetDevice(device_), "hipSetDevice");
+        for (int64_t s : after) {
+          if (!herr.empty()) break;
+          hipEvent_t ev;
+          if (!hcheck(hipEventCreateWithFlags(&ev, hipEventDisableTiming), "hipEventCreate")) break;
+          if (hcheck(hipEventRecord(ev, reinterpret_cast<hipStream_t>(s)), "hipEventRecord(producer)"))
+            hcheck(hipStreamWaitEvent(stream_, ev, 0), "hipStreamWaitEvent");
+          hipEventDestroy(ev);
+        }
+        if (herr.empty()) {
+          r = ncclGroupStart();
+          for (const auto& op : raw) {
+            if (r != ncclSuccess) break;
+            r = op.kind == 0 ? ncclSend(op.ptr, op.nbytes, ncclUint8, op.peer, comm_, stream_)
+                             : ncclRecv(op.ptr, op.nbytes, ncclUint8, op.peer, comm_, stream_);
+          }
+          ncclResult_t e = ncclGroupEnd();
+          if (r == ncclSuccess) r = e;
+          if (r == ncclInProgress) r = settle(timeout_s);
+          // the completion event is recorded right behind the group, before
+          // another group can be enqueued on the comm stream
+          if (r == ncclSuccess && hcheck(hipEventCreateWithFlags(&rec.done, hipEventDisableTiming), "hipEventCreate") &&
+              !hcheck(hipEventRecord(rec.done, stream_), "hipEventRecord(done)")) {
+            hipEventDestroy(rec.done);
+            rec.done = nullptr;
+          }
         }
       }
     }
     if (gone) throw std::runtime_error("RcclPlane: communicator aborted");
+    if (!herr.empty()) throw std::runtime_error("RcclPlane: " + herr);
     if (r != ncclSuccess) throw std::runtime_error("RcclPlane group: " + nccl_msg(r));
     TORCH_CHECK(rec.done != nullptr, "RcclPlane: could not record the group's completion event");
-    for (const auto& op : ops) rec.keep.push_back(std::get<2>(op));
     std::lock_guard<std::mutex> lk(mu_);
     const int64_t gid = next_gid_++;
     groups_.emplace(gid, std::move(rec));
@@ -179,10 +196,16 @@ class RcclPlane {
   // 1: complete, 0: still running.  Throws on an asynchronous RCCL error.
   int query(int64_t gid) {
     hipEvent_t ev = event_of(gid);
-    hipError_t e = hipEventQuery(ev);
+    hipError_t e;
+    ncclResult_t a = ncclSuccess;
+    {
+      py::gil_scoped_release nogil;
+      e = hipEventQuery(ev);
+      if (e == hipErrorNotReady) a = poll_async_error();
+    }
     if (e == hipSuccess) return 1;
     if (e != hipErrorNotReady) hip_ok(e, "hipEventQuery");
-    check_async();
+    if (a != ncclSuccess && a != ncclInProgress) throw std::runtime_error("RCCL async error: " + nccl_msg(a));
     return 0;
   }
 
@@ -200,8 +223,10 @@ class RcclPlane {
         hipError_t e = hipEventQuery(ev);
         if (e == hipSuccess) { done = 1; break; }
         if (e != hipErrorNotReady) { err = std::string("hipEventQuery: ") + hipGetErrorString(e); break; }
-        ncclResult_t a = async_error_nolock();
-        if (a != ncclSuccess && a != ncclInProgress) { err = "RCCL async error: " + nccl_msg(a); break; }
+        if ((spins & 15) == 0) {
+          ncclResult_t a = poll_async_error();
+          if (a != ncclSuccess && a != ncclInProgress) { err = "RCCL async error: " + nccl_msg(a); break; }
+        }
         if (Clock::now() >= t_end) break;
         // spin briefly (xGMI transfers of a few MB take ~100 us), then back off
         if (++spins > 200) std::this_thread::sleep_for(std::chrono::microseconds(spins > 2000 ? 200 : 20));
@@ -213,45 +238,56 @@ class RcclPlane {
 
   // Make `stream` wait for the group (consumers may enqueue before it is done).
   void stream_wait(int64_t gid, int64_t stream) {
-    hip_ok(hipStreamWaitEvent(reinterpret_cast<hipStream_t>(stream), event_of(gid), 0), "hipStreamWaitEvent");
+    hipEvent_t ev = event_of(gid);
+    hipError_t e;
+    {
+      py::gil_scoped_release nogil;
+      e = hipStreamWaitEvent(reinterpret_cast<hipStream_t>(stream), ev, 0);
+    }
+    hip_ok(e, "hipStreamWaitEvent");
   }
 
   void release(int64_t gid) {
-    std::lock_guard<std::mutex> lk(mu_);
-    auto it = groups_.find(gid);
-    if (it == groups_.end()) return;
-    if (it->second.done) hipEventDestroy(it->second.done);
-    groups_.erase(it);
+    GroupRec rec;
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      auto it = groups_.find(gid);
+      if (it == groups_.end()) return;
+      rec = std::move(it->second);
+      groups_.erase(it);
+    }
+    if (rec.done) hipEventDestroy(rec.done);
+    // rec.keep (the transfer buffers) is dropped here, with the GIL held
   }
 
   int async_error() {
-    ncclResult_t a = async_error_nolock();
-    return int(a);
+    py::gil_scoped_release nogil;
+    return int(poll_async_error());
   }
 
   // Abort every in-flight operation (a peer died); the plane is unusable afterwards.
   void abort() {
     abort_req_ = true;
     py::gil_scoped_release nogil;
-    std::unique_lock<std::shared_mutex> cl(comm_mu_);  // in-progress settles see abort_req_ and let go
+    std::lock_guard<std::mutex> nl(nccl_mu_);  // an in-progress settle sees abort_req_ and lets go
     if (comm_ != nullptr) ncclCommAbort(comm_);
     comm_ = nullptr;
     aborted_ = true;
   }
 
-  // Orderly shutdown after all groups completed (collective over live ranks in RCCL's view).
   // Orderly shutdown: let in-flight groups drain (bounded), then release the
   // communicator.  Abort rather than ncclCommDestroy so that teardown can never
   // wait on a peer (a rank that left early must not hang the survivors' exit).
   void close(double timeout_s) {
     py::gil_scoped_release nogil;
     const auto t_end = Clock::now() + std::chrono::duration<double>(timeout_s);
-    while (hipStreamQuery(stream_) == hipErrorNotReady && Clock::now() < t_end)
+    while (stream_ && hipStreamQuery(stream_) == hipErrorNotReady && Clock::now() < t_end)
       std::this_thread::sleep_for(std::chrono::microseconds(200));
     abort_req_ = true;
-    std::unique_lock<std::shared_mutex> cl(comm_mu_);
+    std::lock_guard<std::mutex> nl(nccl_mu_);
     if (comm_ != nullptr) ncclCommAbort(comm_);
     comm_ = nullptr;
+    aborted_ = true;
   }
 
   int64_t stream() const { return reinterpret_cast<int64_t>(stream_); }
@@ -272,20 +308,19 @@ class RcclPlane {
     return it->second.done;
   }
 
-  ncclResult_t async_error_nolock() {
-    std::shared_lock<std::shared_mutex> cl(comm_mu_);
+  // Asynchronous error of the communicator without ever blocking: while a
+  // group is being issued (nccl_mu_ held) the poll is skipped (InProgress).
+  ncclResult_t poll_async_error() {
+    std::unique_lock<std::mutex> nl(nccl_mu_, std::try_to_lock);
+    if (!nl.owns_lock()) return ncclInProgress;
     if (comm_ == nullptr) return aborted_ ? ncclRemoteError : ncclSuccess;
     ncclResult_t a = ncclSuccess;
     ncclResult_t r = ncclCommGetAsyncError(comm_, &a);
     return r == ncclSuccess ? a : r;
   }
 
-  void check_async() {
-    ncclResult_t a = async_error_nolock();
-    if (a != ncclSuccess && a != ncclInProgress) throw std::runtime_error("RCCL async error: " + nccl_msg(a));
-  }
-
-  // Non-blocking communicator: poll until the last call settles (GIL already released).
+  // Non-blocking communicator: poll until the last call settles (GIL released,
+  // nccl_mu_ held by the caller).
   ncclResult_t settle(double timeout_s) {
     const auto t_end = Clock::now() + std::chrono::duration<double>(timeout_s);
     ncclResult_t a = ncclInProgress;
@@ -301,9 +336,8 @@ class RcclPlane {
   int nranks_, rank_, device_;
   ncclComm_t comm_ = nullptr;
   hipStream_t stream_ = nullptr;
-  std::mutex mu_;                 // group bookkeeping (never held across a GIL transition)
-  std::mutex issue_mu_;           // one group enqueue at a time (taken with the GIL released)
-  std::shared_mutex comm_mu_;     // comm_ lifetime: shared for calls, exclusive for abort/close
+  std::mutex mu_;        // group table (short sections, GIL held, never across a GIL transition)
+  std::mutex nccl_mu_;   // every RCCL call on comm_ (taken with the GIL released)
   std::atomic<bool> abort_req_{false};
   std::unordered_map<int64_t, GroupRec> groups_;
   int64_t next_gid_ = 1;

@@ -13,6 +13,7 @@ from p2pfl_amd.commands.command import Command
 from p2pfl_amd.commands.models_agregated_command import ModelsAggregatedCommand
 from p2pfl_amd.learning.exceptions import DecodingParamsError, ModelNotMatchingError
 from p2pfl_amd.management.logger import logger
+from p2pfl_amd.utils import finite
 
 
 class AddModelCommand(Command):
@@ -97,6 +98,8 @@ class AddModelCommand(Command):
                 logger.debug(self.state.addr, f"Model from {contributors} not needed; skipped decode.")
                 return
             params = learner.decode_parameters(weights)
+            finite.check(self.state.addr, "received model", params, source=source, contributors=list(contributors),
+                         round=round)
             models_added = self.aggregator.add_model(params, list(contributors), weight)
             if not models_added and self._probe_uncovered(list(contributors)):
                 models_added = self.aggregator.add_model(params, list(contributors), weight)

@@ -69,7 +69,12 @@ class DeviceLoader:
             return torch.arange(n, device=self.y.device)
         g = torch.Generator().manual_seed(self._seed * 100003 + self._epoch)
         self._epoch += 1
-        return torch.randperm(n, generator=g).to(self.y.device)
+        perm = torch.randperm(n, generator=g)
+        if self.y.device.type == "cuda":
+            # pinned + non-blocking: the host never waits for the GPU's queue
+            # to drain just to hand it the next epoch's batch order
+            return perm.pin_memory().to(self.y.device, non_blocking=True)
+        return perm.to(self.y.device)
 
     def __iter__(self) -> Iterator[Tuple[torch.Tensor, torch.Tensor]]:
         perm = self.permutation()

@@ -83,7 +83,13 @@ class Aggregator:
             self._waiting_aggregated_model = False
             self._running = False
             self._lost = set()
+            self._models_changed_locked()
             self._done.set()
+
+    def _models_changed_locked(self) -> None:
+        """Hook (lock held): the stored models changed and the aggregation is
+        not complete yet.  Strategies may start folding them in (FedAvg keeps
+        a running sum); the default does nothing."""
 
     # ------------------------------------------------------------------
     # queries
@@ -206,6 +212,8 @@ class Aggregator:
             logger.info(self.node_name, f"Model added ({len(now)}/{len(self._train_set)}) from {nodes}")
             if self._complete_locked():
                 self._done.set()
+            else:
+                self._models_changed_locked()
             return now
 
     # ------------------------------------------------------------------

@@ -20,12 +20,14 @@ import os
 
 import math
 import threading
+import time
 from typing import Any, Dict, List, Optional, Tuple
 
 import torch
 
 from p2pfl_amd import ops
 from p2pfl_amd.learning.arena import FlatParams, ModuleArena
+from p2pfl_amd.learning.host_completion import HostCompletions
 from p2pfl_amd.learning.torch_learner import TorchLearner
 from p2pfl_amd.management.logger import logger
 from p2pfl_amd.utils.lockcheck import make_lock, make_rlock
@@ -42,6 +44,9 @@ _MERGED_ADAM = os.environ.get("P2PFL_CNN_MERGED_ADAM", "1") != "0"
 # W1^T shadow, 12.8 MB less written per step by the FC1 Adam stream); "0"
 # selects the W1^T-shadow kernel.
 _ROUTE_RM = os.environ.get("P2PFL_CNN_ROUTE_RM", "1") != "0"
+# conv1 + conv2 forward in one launch with P1 kept in LDS (P2PFL_CNN_FUSED_CONV=0:
+# the two separate kernels, P1 through memory)
+_FUSED_CONV = os.environ.get("P2PFL_CNN_FUSED_CONV", "1") != "0"
 _NAMES = ("conv1.weight", "conv1.bias", "conv2.weight", "conv2.bias", "l1.weight", "l1.bias", "l2.weight", "l2.bias")
 FEAT, HID = 3136, 2048
 
@@ -60,6 +65,7 @@ class FusedCNNEngine:
         mrows: int = 32,
         arena: Optional[ModuleArena] = None,
         split_fc1: int = 7,
+        fused_conv: Optional[bool] = None,
     ) -> None:
         self.C = ops.ext().cnn
         self.C.init()
@@ -76,6 +82,7 @@ class FusedCNNEngine:
         self.lr, self.betas, self.eps, self.wd = lr, betas, eps, weight_decay
         self.mrows = mrows
         self.S1 = split_fc1
+        self.fused_conv = _FUSED_CONV if fused_conv is None else bool(fused_conv)
         dev, bf = self.device, torch.bfloat16
         z = lambda *s, dt=torch.float32: torch.zeros(*s, dtype=dt, device=dev)  # noqa: E731
         n = self.arena.flat.numel()
@@ -127,8 +134,12 @@ class FusedCNNEngine:
 
     def forward(self, x: torch.Tensor, labels: torch.Tensor, idx: Optional[torch.Tensor], B: int, stats: torch.Tensor, train: bool) -> None:
         C, M = self.C, self.mrows
-        C.conv1_fwd(x, idx, self.params, self.off, self.p1, self.am1, self.p1s if train else None, B)
-        C.conv2_fwd(self.p1, self.w2r, self.params, self.off, self.a1, self.am2, B, M)
+        if self.fused_conv:
+            C.conv12_fwd(x, idx, self.params, self.off, self.w2r, self.am1, self.p1s if train else None, self.a1,
+                         self.am2, B, M)
+        else:
+            C.conv1_fwd(x, idx, self.params, self.off, self.p1, self.am1, self.p1s if train else None, B)
+            C.conv2_fwd(self.p1, self.w2r, self.params, self.off, self.a1, self.am2, B, M)
         C.gemm_skinny(self.a1, self.w1bf, self.slabs1, M, HID, FEAT, self.S1)
         C.head(self.slabs1, self.S1, M, self.params, self.off, labels, idx, B, train, self.H, self.dH, self.dlogits, stats)
 
@@ -214,8 +225,11 @@ class _EvalForward:
 
     def forward(self, x: torch.Tensor, labels: torch.Tensor, idx: Optional[torch.Tensor], B: int, stats: torch.Tensor) -> None:
         e, C, M = self.eng, self.eng.C, self.MROWS
-        C.conv1_fwd(x, idx, e.params, e.off, self.p1, self.am1, None, B)
-        C.conv2_fwd(self.p1, e.w2r, e.params, e.off, self.a1, self.am2, B, M)
+        if e.fused_conv:
+            C.conv12_fwd(x, idx, e.params, e.off, e.w2r, self.am1, None, self.a1, self.am2, B, M)
+        else:
+            C.conv1_fwd(x, idx, e.params, e.off, self.p1, self.am1, None, B)
+            C.conv2_fwd(self.p1, e.w2r, e.params, e.off, self.a1, self.am2, B, M)
         C.gemm_skinny(self.a1, e.w1bf, self.slabs1, M, HID, FEAT, e.S1)
         C.head(self.slabs1, e.S1, M, e.params, e.off, labels, idx, B, False, self.H, self.dH, self.dlogits, stats)
 
@@ -252,12 +266,27 @@ class FusedCNNLearner(TorchLearner):
         self._stream = torch.cuda.Stream(self.device)
         self._dirty_shadows = False
         self._eval_fwd = _EvalForward(self.engine)
+        # asynchronous passes: metrics are read back by a completion thread;
+        # the validation pass runs on its own stream next to whatever follows
+        # the training epoch (the gossip snapshot + RCCL push of the weights)
+        self._completions = HostCompletions(self_addr)
+        self._val_stream = torch.cuda.Stream(self.device)
+        self._val_done: Optional[torch.cuda.Event] = None  # last side-stream reader of the arena
+        self._fit_done: Optional[torch.cuda.Event] = None  # bounds the host's run-ahead to one fit
 
     # -- parameters: keep the bf16 shadows in sync -------------------------
+    def _wait_arena_readers(self) -> None:
+        """Order the caller's stream after the side-stream validation pass (it
+        reads the weights and shares the evaluation buffers)."""
+        ev = self._val_done
+        if ev is not None:
+            torch.cuda.current_stream(self.device).wait_event(ev)
+
     def set_parameters(self, params) -> None:
         if isinstance(params, FlatParams) and params.flat.data_ptr() == self.engine.params.data_ptr():
             self._arena_changed()
             return  # the arena itself: weights and bf16 shadows are already current
+        self._wait_arena_readers()
         super().set_parameters(params)
         with torch.cuda.stream(torch.cuda.current_stream(self.device)):
             self.engine.pack_shadows()
@@ -323,6 +352,13 @@ class FusedCNNLearner(TorchLearner):
         return eg
 
     # -- NodeLearner ------------------------------------------------------
+    @staticmethod
+    def _readback(stats: torch.Tensor) -> torch.Tensor:
+        """Pinned host copy of a device stats tensor, enqueued behind the pass."""
+        host = torch.empty(stats.shape, dtype=stats.dtype, pin_memory=True)
+        host.copy_(stats, non_blocking=True)
+        return host
+
     def fit(self) -> None:
         if self.epochs <= 0 or self.model is None:
             return
@@ -333,56 +369,119 @@ class FusedCNNLearner(TorchLearner):
             self._arena_changed()  # no snapshot taken mid-fit survives it
 
     def _fit_fused(self) -> None:
+        """Enqueue the round's epochs (HIP-graph replays) and their validation passes.
+
+        Returns as soon as the work is queued: per-step losses and validation
+        metrics are logged by the completion thread when they land.  Everything
+        that later reads or replaces the weights -- the gossip snapshot and
+        its RCCL push, FedAvg, ``set_parameters`` -- is ordered behind the
+        epoch by the stream.  The host runs at most one fit ahead of the GPU.
+        """
         self._interrupt.clear()
         self._arena_changed()
+        prev = self._fit_done
+        if prev is not None:
+            prev.synchronize()  # the previous round's training finished on the GPU
         with self._lock:
             self.engine.reset_optimizer()  # Adam re-created per fit (reference quirk Q23)
             loader = self.data.train_dataloader()
-            steps = math.ceil(len(loader.dataset) / loader.batch_size)
+            n, bs = len(loader.dataset), loader.batch_size
+            steps = math.ceil(n / bs)
+            cur = torch.cuda.current_stream(self.device)
             for epoch in range(self.epochs):
                 if self._interrupt.is_set():
                     return
+                self._wait_arena_readers()  # the previous epoch's validation read these weights
                 self.engine.adam_t.fill_(epoch * steps)  # Adam step base for this epoch's graph
-                with logger.span(self._addr, "train_epoch"):
-                    stats = self._run("train", loader, True, loader.permutation())
-                    # one host copy, then plain floats: per-element tensor
-                    # indexing costs microseconds each, x steps, while the GPU idles
-                    loss_sums = [row[0] for row in stats.cpu().tolist()]
-                steps = len(loss_sums)
+                t0, t1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                t0.record(cur)
+                stats = self._run("train", loader, True, loader.permutation())
+                t1.record(cur)
+                host = self._readback(stats)
+                done = torch.cuda.Event()
+                done.record(cur)
+                base = self._step
                 self._step += steps
-                bs = loader.batch_size
-                n = len(loader.dataset)
-                every = max(1, self.log_every_n_steps)
-                for j in range(steps):
-                    if (self._step - steps + j + 1) % every == 0:
-                        self._log("train_loss", loss_sums[j] / min(bs, n - j * bs), step=self._step - steps + j + 1)
-                self.last_train_loss = sum(loss_sums) / n
+                self._completions.submit(done, lambda h=host, b=base, a=t0, z=t1: self._log_epoch(h, b, steps, bs, n, a, z))
                 if not (self.defer_final_validation and epoch == self.epochs - 1):
-                    self._validate()
+                    self._validate_async()
+            fit_done = torch.cuda.Event()
+            fit_done.record(cur)
+            self._fit_done = fit_done
 
-    def _eval_pass(self, name: str, loader) -> Dict[str, float]:
+    def _log_epoch(self, host: torch.Tensor, base: int, steps: int, bs: int, n: int, t0: Any, t1: Any) -> None:
+        loss_sums = [row[0] for row in host.tolist()]
+        every = max(1, self.log_every_n_steps)
+        for j in range(steps):
+            if (base + j + 1) % every == 0:
+                self._log("train_loss", loss_sums[j] / min(bs, n - j * bs), step=base + j + 1)
+        self.last_train_loss = sum(loss_sums) / n
+        # GPU time of the replayed epoch (the host only enqueued it)
+        ms = t0.elapsed_time(t1)
+        logger.tracer.record(self._addr, "train_epoch_gpu", time.perf_counter() - ms * 1e-3, ms * 1e-3)
+
+    def _eval_async(self, name: str, loader, on_done) -> None:
+        """Enqueue an evaluation pass on the current stream; ``on_done(loss, metric)``
+        runs on the completion thread."""
         with self._lock:
-            loss, correct = self._run(name, loader, False, None)[0, :2].tolist()
+            stats = self._run(name, loader, False, None)
+        host = self._readback(stats[0, :2])
+        ev = torch.cuda.Event()
+        ev.record(torch.cuda.current_stream(self.device))
         n = max(1, len(loader.dataset))
-        return {"loss": loss / n, "metric": correct / n}
 
-    def _validate(self) -> None:
+        def fin() -> None:
+            loss, correct = host.tolist()
+            on_done(loss / n, correct / n)
+
+        self._completions.submit(ev, fin)
+        return ev
+
+    def _validate_async(self) -> None:
         loader = self.data.val_dataloader()
         if loader is None or len(loader.dataset) == 0:
             return
-        r = self._eval_pass("val", loader)
-        self._log("val_loss", r["loss"], step=self._step)
-        self._log("val_metric", r["metric"], step=self._step)
+        vs = self._val_stream
+        vs.wait_stream(torch.cuda.current_stream(self.device))  # after the epoch that produced the weights
+        step = self._step
+        with torch.cuda.stream(vs):
+            self._val_done = self._eval_async(
+                "val", loader, lambda loss, acc: (self._log("val_loss", loss, step=step), self._log("val_metric", acc, step=step))
+            )
+
+    def _validate(self) -> None:
+        self._validate_async()
+        self._completions.drain()
+
+    def evaluate_async(self, on_results: Optional[Any] = None) -> bool:
+        """Enqueue the test pass; results are logged (and handed to
+        ``on_results``) when they land.  False when there is nothing to
+        evaluate (``epochs == 0``, reference quirk Q18)."""
+        if self.epochs <= 0 or self.model is None:
+            return False
+
+        def done(loss: float, acc: float) -> None:
+            results = {"test_loss": loss, "test_metric": acc}
+            for k, v in results.items():
+                self._log(k, v)
+            if on_results is not None:
+                on_results(results)
+
+        with logger.span(self._addr, "evaluate"), self._on_stream():
+            self._wait_arena_readers()  # shares the evaluation buffers with validation
+            self._eval_async("test", self.data.test_dataloader(), done)
+        return True
 
     def evaluate(self) -> Dict[str, float]:
-        if self.epochs <= 0 or self.model is None:
+        box: Dict[str, float] = {}
+        if not self.evaluate_async(box.update):
             return {}
-        with logger.span(self._addr, "evaluate"), self._on_stream():
-            r = self._eval_pass("test", self.data.test_dataloader())
-        results = {"test_loss": r["loss"], "test_metric": r["metric"]}
-        for k, v in results.items():
-            self._log(k, v)
-        return results
+        self._completions.drain()
+        return box
+
+    def drain(self, timeout: Optional[float] = None) -> bool:
+        """Wait for every enqueued pass's host work (metrics) to finish."""
+        return self._completions.drain(timeout)
 
 
 def auto_learner(model: Any, data: Any, self_addr: str, epochs: int, **kw):

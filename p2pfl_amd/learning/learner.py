@@ -55,3 +55,15 @@ class NodeLearner:
     def snapshot_parameters(self, params: Optional[Any] = None) -> Any:
         """Detached copy suitable for shipping in-process; defaults to bytes."""
         return self.encode_parameters(params)
+
+    # -- optional (asynchronous learners) -----------------------------------
+    def evaluate_async(self, on_results: Any = None) -> bool:
+        """Enqueue an evaluation whose results reach ``on_results`` later.
+
+        Learners that evaluate synchronously return False and the caller uses
+        :meth:`evaluate`."""
+        return False
+
+    def drain(self, timeout: Optional[float] = None) -> bool:
+        """Wait until the host work of every enqueued pass (metric logging) ran."""
+        return True

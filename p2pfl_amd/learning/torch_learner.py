@@ -42,6 +42,7 @@ from p2pfl_amd.learning.learner import NodeLearner
 from p2pfl_amd.learning.wire import decode_params, encode_params
 from p2pfl_amd.management.logger import logger
 from p2pfl_amd.settings import Settings
+from p2pfl_amd.utils import finite
 
 
 def default_device() -> torch.device:
@@ -199,8 +200,11 @@ class TorchLearner(NodeLearner):
             cur.wait_stream(cs)
 
     def set_parameters(self, params: Mapping[str, torch.Tensor]) -> None:
+        finite.check(self._addr, "set_parameters input", params if isinstance(params, FlatParams) else None)
         with self._on_stream():
             self._set_parameters(params)
+        if finite.ENABLED and self.arena is not None:
+            finite.check(self._addr, "parameters after set_parameters", self.arena.flat)
 
     def _set_parameters(self, params: Mapping[str, torch.Tensor]) -> None:
         assert self.arena is not None
@@ -333,6 +337,8 @@ class TorchLearner(NodeLearner):
     def fit(self) -> None:
         if self.epochs <= 0 or self.model is None:
             return
+        if finite.ENABLED and self.arena is not None:
+            finite.check(self._addr, "parameters before fit", self.arena.flat)
         try:
             with self._on_stream():
                 self._fit()
@@ -340,6 +346,8 @@ class TorchLearner(NodeLearner):
             # a snapshot taken while fit() ran (weights still moving) must not
             # be served as the trained model's payload
             self._arena_changed()
+        if finite.ENABLED and self.arena is not None:
+            finite.check(self._addr, "parameters after fit", self.arena.flat, step=self._step)
 
     def _fit(self) -> None:
         self._interrupt.clear()

@@ -11,7 +11,7 @@ from __future__ import annotations
 
 import importlib
 import os
-from typing import List, Optional, Sequence
+from typing import Tuple, List, Optional, Sequence
 
 import torch
 
@@ -59,12 +59,52 @@ def normalized_weights(weights: Sequence[float]) -> List[float]:
     return [float(w) / total for w in weights]
 
 
+def fedavg_weights(weights: Sequence[float]) -> Tuple[List[float], float]:
+    """(per-input weights, final scale) of a weighted mean: ``sum w_i x_i / sum w_i``
+    is computed as raw-weight fp32 FMAs followed by ONE multiply by ``1 / sum w``,
+    so it can be folded in several pieces (running sum) with bitwise-equal
+    results.  All-zero weights fall back to the plain mean."""
+    total = float(sum(weights))
+    if total <= 0:
+        return [1.0] * len(weights), 1.0 / len(weights)
+    return [float(w) for w in weights], 1.0 / total
+
+
+def weighted_sum_into(
+    out: torch.Tensor,
+    flats: Sequence[torch.Tensor],
+    weights: Sequence[float],
+    acc_in: Optional[torch.Tensor] = None,
+    scale: float = 1.0,
+) -> torch.Tensor:
+    """``out = scale * (acc_in + sum_i weights[i] * flats[i])`` in fp32 (``acc_in``
+    None = 0; it may be ``out`` itself).  One fused kernel on the GPU; the same
+    operation sequence on the CPU, so pieces folded separately equal one call."""
+    if not flats and acc_in is None:
+        raise ValueError("no inputs")
+    dev_t = flats[0] if flats else out
+    if not _gpu(dev_t):
+        acc = acc_in.clone() if acc_in is not None else torch.zeros(out.shape, dtype=torch.float32, device=out.device)
+        for f, w in zip(flats, weights):
+            acc.add_(f.to(acc.device, torch.float32), alpha=float(w))
+        if scale != 1.0:
+            acc.mul_(scale)
+        out.copy_(acc)
+        return out
+    dev = out.device
+    ok = (torch.float32, torch.bfloat16)
+    srcs = [f if (f.device == dev and f.dtype in ok and f.is_contiguous() and f.data_ptr() % 16 == 0)
+            else f.to(dev, torch.float32).contiguous() for f in flats]
+    ext().weighted_sum(srcs, [float(w) for w in weights], out, acc_in, float(scale))
+    return out
+
+
 def weighted_average_reference(flats: Sequence[torch.Tensor], weights: Sequence[float]) -> torch.Tensor:
-    w = normalized_weights(weights)
+    w, scale = fedavg_weights(weights)
     acc = torch.zeros_like(flats[0], dtype=torch.float32)
     for f, wi in zip(flats, w):
         acc.add_(f.float(), alpha=wi)
-    return acc
+    return acc.mul_(scale)
 
 
 def weighted_average(
@@ -87,6 +127,7 @@ def weighted_average(
             raise ValueError("inputs differ in size")
     if out is not None:
         out_dtype = out.dtype
+    w, scale = fedavg_weights(weights)
     if not _gpu(flats[0]):
         res = weighted_average_reference(flats, weights)
         if out is not None:
@@ -94,20 +135,15 @@ def weighted_average(
             return out
         return res.to(out_dtype)
     dev = flats[0].device
-    ok = (torch.float32, torch.bfloat16)
-    srcs = [f if (f.device == dev and f.dtype in ok and f.is_contiguous() and f.data_ptr() % 16 == 0)
-            else f.to(dev, torch.float32).contiguous() for f in flats]
-    w = normalized_weights(weights)
-    if out_dtype == torch.bfloat16 and len(srcs) > 16:
-        res = weighted_average(srcs, w)  # fp32 partial sums, then one cast
+    if out_dtype == torch.bfloat16 and len(flats) > 16:
+        res = weighted_average(flats, weights)  # fp32 partial sums, then one cast
         if out is None:
             return res.to(torch.bfloat16)
         out.copy_(res)
         return out
     if out is None:
         out = torch.empty(n, dtype=out_dtype, device=dev)
-    ext().weighted_sum(srcs, w, out)
-    return out
+    return weighted_sum_into(out, flats, w, None, scale)
 
 
 # ----------------------------------------------------------------------------

@@ -12,6 +12,7 @@ concurrently on different streams never share a counter.
 
 from __future__ import annotations
 
+import threading
 from typing import Dict, List, Tuple
 
 import torch
@@ -23,6 +24,9 @@ import torch
 IN_LAUNCH_MAX_SPLITS = 4
 RING = 1 << 18  # counters per stream (1 MiB)
 _RINGS: Dict[Tuple[int, int], List] = {}
+# virtual peers launch from several node threads: the ring cursor is shared
+# per stream (torch hands out pooled streams), so taking a slice is atomic
+_LOCK = threading.Lock()
 
 
 def counters(tiles: int, device: torch.device) -> torch.Tensor:
@@ -31,14 +35,15 @@ def counters(tiles: int, device: torch.device) -> torch.Tensor:
         raise ValueError(f"split-K launch with {tiles} tiles exceeds the counter ring")
     stream = torch.cuda.current_stream(device)
     key = (stream.device_index, stream.cuda_stream)
-    ring = _RINGS.get(key)
-    if ring is None:
-        ring = _RINGS[key] = [torch.zeros(RING, dtype=torch.int32, device=device), 0]
-    if ring[1] + tiles > RING:
-        ring[1] = 0
-    off = ring[1]
-    ring[1] += (tiles + 15) // 16 * 16
-    return ring[0][off : off + tiles]
+    with _LOCK:
+        ring = _RINGS.get(key)
+        if ring is None:
+            ring = _RINGS[key] = [torch.zeros(RING, dtype=torch.int32, device=device), 0]
+        if ring[1] + tiles > RING:
+            ring[1] = 0
+        off = ring[1]
+        ring[1] += (tiles + 15) // 16 * 16
+        return ring[0][off : off + tiles]
 
 
 def tiles_of(rows: int, cols: int) -> int:

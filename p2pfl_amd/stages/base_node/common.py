@@ -19,14 +19,29 @@ def model_payload(state: Any, protocol: Any, params: Optional[Any] = None) -> An
 
 
 def evaluate_and_share(state: Any, protocol: Any) -> Dict[str, float]:
+    """Evaluate the local model and broadcast the metrics (reference
+    ``train_stage.py:95-112``).  With an asynchronous learner the pass is only
+    enqueued here; the metrics go out from its completion thread when they land
+    (returns ``{}``), so the round does not wait for the test pass."""
     logger.info(state.addr, "Evaluating...")
-    if state.learner is None:
+    learner = state.learner
+    if learner is None:
         raise Exception("Learner not initialized.")
-    results = state.learner.evaluate()
-    logger.info(state.addr, f"Evaluated. Results: {results}")
-    if results:
-        flat = [str(x) for kv in results.items() for x in kv]
-        protocol.broadcast(protocol.build_msg(MetricsCommand.get_name(), flat, round=state.round))
+    rnd = state.round
+
+    def share(results: Dict[str, float]) -> None:
+        logger.info(state.addr, f"Evaluated. Results: {results}")
+        if results:
+            flat = [str(x) for kv in results.items() for x in kv]
+            try:
+                protocol.broadcast(protocol.build_msg(MetricsCommand.get_name(), flat, round=rnd))
+            except Exception as e:  # the node may have stopped meanwhile
+                logger.debug(state.addr, f"metrics broadcast skipped: {e}")
+
+    if learner.evaluate_async(share):
+        return {}
+    results = learner.evaluate()
+    share(results)
     return results
 
 

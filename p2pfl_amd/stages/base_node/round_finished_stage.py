@@ -46,6 +46,9 @@ class RoundFinishedStage(Stage):
             diffusion.join()
         state.diffusions = []
         evaluate_and_share(state, communication_protocol)
+        # the final metrics must be logged before the experiment counts as finished
+        if state.learner is not None:
+            state.learner.drain()
         # experiment over: reset per-experiment peer bookkeeping so a new
         # experiment re-gossips the initial model (the reference kept stale
         # nei_status entries and could stall a second experiment)

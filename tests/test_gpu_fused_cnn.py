@@ -216,3 +216,36 @@ def test_evaluate_matches_torch_reference():
         acc = (logits.argmax(1) == ld.y).float().mean().item()
     assert abs(res["test_loss"] - loss) < 3e-2 * max(1.0, loss), (res, loss)
     assert abs(res["test_metric"] - acc) <= 2.0 / len(ld.dataset) + 1e-6, (res, acc)
+
+
+def test_async_fit_orders_validation_before_replaced_weights():
+    """fit() only enqueues: the validation pass runs on a side stream and its
+    metrics land later.  A set_parameters() issued right after fit() must not
+    overtake that pass -- the logged validation metrics are the trained
+    weights', identical to a learner that synchronises after every pass."""
+    from p2pfl_amd.data import MnistFederatedDM
+    from p2pfl_amd.learning.fused_cnn import FusedCNNLearner
+    from p2pfl_amd.management.logger import logger
+
+    ops.ext()
+    got = []
+    for sync in (False, True):
+        torch.manual_seed(0)
+        addr = f"async-{sync}"
+        ln = FusedCNNLearner(CNN(seed=21), MnistFederatedDM(sub_id=1, number_sub=40), addr, 1, device=torch.device("cuda"))
+        seen = {}
+        ln._log = lambda k, v, step=None, _s=seen: _s.__setitem__(k, v)  # noqa: E731
+        ln.fit()
+        if sync:
+            ln.drain()
+        trained = ln.get_parameters().clone()
+        zero = trained.clone()
+        zero.flat.zero_()
+        ln.set_parameters(zero)  # enqueued right behind the fit
+        assert ln.drain(60)
+        assert float(ln.get_parameters().flat.abs().sum()) == 0.0
+        got.append((trained.flat, seen["val_loss"], seen["val_metric"], seen["train_loss"] if "train_loss" in seen else None))
+    torch.testing.assert_close(got[0][0], got[1][0], rtol=0, atol=0)
+    assert got[0][1] == got[1][1] and got[0][2] == got[1][2]
+    # validation of a zeroed CNN would give the uniform loss log(10)
+    assert abs(got[0][1] - 2.302585) > 1e-3

@@ -247,3 +247,33 @@ def test_multi_tensor_channels_last(opt):
     with pytest.raises(RuntimeError):  # an OIHW-contiguous gradient is rejected for a channels-last tensor
         bad = [g.contiguous() for g in grads]
         ops.sgd_mt_step(p, st[0], bad, mt, lr=0.05, momentum=0.9, p_bf16=shadow)
+
+
+@pytest.mark.gpu
+def test_weighted_sum_running_fold_is_bitwise_equal_to_one_shot():
+    """The FedAvg kernel seeded with a running fp32 sum (acc_in) and scaled at
+    the end: folding inputs in pieces equals one launch bit for bit, including
+    bf16 inputs, a zero-input scale-only launch and > 16 inputs."""
+    from p2pfl_amd import ops
+
+    ops.ext()
+    dev = torch.device("cuda", 0)
+    g = torch.Generator(device=dev).manual_seed(5)
+    n = 6_497_163  # not a multiple of 4: the tail kernel runs too
+    flats = [torch.randn(n, device=dev, generator=g) for _ in range(19)]
+    flats[3] = flats[3].to(torch.bfloat16)
+    w = [float(100 + 13 * i) for i in range(19)]
+    scale = 1.0 / sum(w)
+    one = torch.empty(n, device=dev)
+    ops.weighted_sum_into(one, flats, w, None, scale)
+    acc = torch.empty(n, device=dev)
+    ops.weighted_sum_into(acc, flats[:2], w[:2])
+    ops.weighted_sum_into(acc, flats[2:7], w[2:7], acc_in=acc)
+    ops.weighted_sum_into(acc, flats[7:], w[7:], acc_in=acc)
+    out = torch.empty(n, device=dev)
+    ops.weighted_sum_into(out, [], [], acc_in=acc, scale=scale)
+    assert torch.equal(out, one)
+    ref = sum(f.double() * wi for f, wi in zip(flats, w)) * scale
+    torch.testing.assert_close(one.double(), ref, rtol=1e-5, atol=1e-5)
+    # the wrapper FedAvg uses
+    torch.testing.assert_close(ops.weighted_average(flats, w), one, rtol=0, atol=0)

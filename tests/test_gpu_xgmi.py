@@ -95,55 +95,26 @@ def test_rccl_plane_native_binding_checks_and_abort():
         p.issue([(0, 0, a)], [], 5.0)
 
 
+@pytest.mark.timeout(180)
 def test_rccl_plane_issue_and_wait_from_two_threads_never_deadlock():
     """Regression for the issue()/wait() lock-order inversion: one thread issues
     small groups back to back while another polls wait() with a short timeout
     and releases them (issue used to hold the bookkeeping mutex while taking the
-    GIL back; wait holds the GIL while taking that mutex)."""
-    from p2pfl_amd import ops
+    GIL back; wait holds the GIL while taking that mutex).  Own process: a hang
+    dumps every thread's stack and fails the test (tests/rccl_stress_worker.py)."""
+    import os
+    import subprocess
+    import sys
 
-    C = ops.ext()
-    p = C.RcclPlane(C.rccl_unique_id(), 1, 0, 0, 60.0)
-    dev = torch.device("cuda", 0)
-    import queue
-
-    q: "queue.Queue" = queue.Queue()
-    n_groups = 400
-    errors = []
-
-    def issuer():
-        try:
-            for i in range(n_groups):
-                a = torch.full((4096,), float(i), device=dev)
-                b = torch.empty_like(a)
-                q.put((p.issue([(0, 0, a), (1, 0, b)], [torch.cuda.current_stream(dev).cuda_stream], 30.0), i, b))
-        except Exception as e:  # noqa: BLE001
-            errors.append(e)
-        q.put(None)
-
-    def completer():
-        try:
-            while True:
-                item = q.get()
-                if item is None:
-                    return
-                gid, i, b = item
-                while p.wait(gid, 0.0005) == 0:
-                    p.query(gid)
-                p.release(gid)
-                assert float(b[0]) == float(i) and float(b[-1]) == float(i)
-        except Exception as e:  # noqa: BLE001
-            errors.append(e)
-
-    th = [threading.Thread(target=issuer), threading.Thread(target=completer)]
-    for t in th:
-        t.start()
-    for t in th:
-        t.join(120)
-    assert not any(t.is_alive() for t in th), "issue/wait deadlocked"
-    assert not errors, errors
-    assert p.in_flight() == 0
-    p.abort()
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, PYTHONPATH=root, P2PFL_LOCKCHECK="0")
+    try:
+        r = subprocess.run([sys.executable, os.path.join(root, "tests", "rccl_stress_worker.py"), "400"], cwd=root,
+                           env=env, capture_output=True, text=True, timeout=150)
+    except subprocess.TimeoutExpired as e:
+        pytest.fail(f"stress worker hung: {e.stdout!r} {e.stderr!r}")
+    print(r.stdout)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-6000:]
 
 
 def _free_port() -> int:

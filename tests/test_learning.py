@@ -374,3 +374,61 @@ def test_channels_last_shadow_optimizer_matches_torch(opt_name):
     arena.params.flat.mul_(0.5)
     arena.refresh_shadow()
     assert torch.equal(w0.detach(), master)
+
+
+def test_fedavg_running_sum_is_bitwise_equal_to_one_shot_for_any_arrival_order():
+    """Models folded into the running sum as they arrive (any order, any
+    interleaving with partial aggregations) give exactly the one-shot result."""
+    import itertools
+    import random
+
+    import torch
+
+    from p2pfl_amd.learning.aggregators.fedavg import FedAvg
+    from p2pfl_amd.learning.arena import flatten
+
+    names = ["n3", "n0", "n2", "n1", "n4"]
+    rng = torch.Generator().manual_seed(0)
+    models = {n: flatten({"w": torch.randn(37, 11, generator=rng), "b": torch.randn(5, generator=rng)}) for n in names}
+    weights = {n: 100 + 17 * i for i, n in enumerate(names)}
+    oneshot = FedAvg()
+    oneshot.running_sum = False
+    oneshot.set_nodes_to_aggregate(names)
+    for n in names:
+        oneshot.add_model(models[n], [n], weights[n])
+    want = oneshot.wait_and_get_aggregation(timeout=1).flat.clone()
+    orders = list(itertools.permutations(names))
+    random.Random(1).shuffle(orders)
+    folded_any = False
+    for order in orders[:25]:
+        agg = FedAvg()
+        agg.set_nodes_to_aggregate(names)
+        for n in order:
+            agg.add_model(models[n], [n], weights[n])
+            agg.get_partial_aggregation([])  # gossip asks for partial aggregates in between
+            folded_any |= agg._run is not None and len(agg._run.keys) > 0
+        got = agg.wait_and_get_aggregation(timeout=1).flat
+        assert torch.equal(got, want), order
+    assert folded_any
+    ref = sum(models[n].flat * weights[n] for n in names) / sum(weights.values())
+    torch.testing.assert_close(want, ref, rtol=1e-6, atol=1e-6)
+
+
+def test_check_finite_debug_mode_names_the_first_bad_tensor(monkeypatch):
+    import pytest
+    import torch
+
+    from p2pfl_amd.learning.aggregators.fedavg import FedAvg
+    from p2pfl_amd.learning.arena import flatten
+    from p2pfl_amd.utils import finite
+
+    monkeypatch.setattr(finite, "ENABLED", True)
+    good = flatten({"w": torch.ones(8)})
+    bad = flatten({"w": torch.tensor([1.0, float("nan")] + [0.0] * 6)})
+    agg = FedAvg("nodeX")
+    agg.set_nodes_to_aggregate(["a", "b"])
+    agg.add_model(good, ["a"], 1)
+    agg.add_model(bad, ["b"], 1)
+    with pytest.raises(finite.NonFiniteError, match="FedAvg input.*key=b"):
+        agg.wait_and_get_aggregation(timeout=1)
+    finite.check("n", "fine", good)  # no error on finite data
