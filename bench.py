@@ -372,7 +372,8 @@ def _print_round_breakdown(rank, addr, tracer, round_ends, W, K) -> None:
         groups = [s for s in inr if s.name == "xgmi_group"]
         gbytes = sum(int(s.attrs.get("nbytes", 0)) for s in groups)
         print(
-            f"[bench rank {rank}] round {r}: wall {(t1 - t0) * 1e3:.2f} ms | fit {tot('fit'):.2f} evaluate {tot('evaluate'):.2f} "
+            f"[bench rank {rank}] round {r}: wall {(t1 - t0) * 1e3:.2f} ms | fit {tot('fit'):.2f} (GPU epoch "
+            f"{tot('train_epoch_gpu'):.2f}) evaluate {tot('evaluate'):.2f} "
             f"wait_aggregation {tot('wait_aggregation'):.2f} aggregate {tot('aggregate'):.2f} | pushes: "
             f"ack {('%.3f' % (sum(acks) / len(acks))) if acks else '-'} ms mean over {len(acks)}, "
             f"{len(groups)} groups {sum(s.duration for s in groups) * 1e3:.2f} ms total "

@@ -61,11 +61,6 @@ void conv1_fwd(const uint8_t* x, const int64_t* idx, const float* params, Offset
 void conv2_fwd(const uint16_t* p1, const uint16_t* w2r, const float* params, Offsets off, uint16_t* a1, uint8_t* am2,
                int B, hipStream_t s);
 
-// conv1 + conv2 (with both ReLU / max-pool stages) in one launch, P1 kept in
-// LDS: writes A1/AM2, AM1 and (p1s non-null, training) P1s; P1 is not written.
-void conv12_fwd(const uint8_t* x, const int64_t* idx, const float* params, Offsets off, const uint16_t* w2r,
-                uint8_t* am1, uint16_t* p1s, uint16_t* a1, uint8_t* am2, int B, hipStream_t s);
-
 void gemm_skinny(const uint16_t* A, const uint16_t* Bt, float* slabs, int mrows, int N, int K, int S, hipStream_t s);
 
 void head(const float* slabs, int S, int mrows, const float* params, Offsets off, const int64_t* labels,

@@ -209,198 +209,6 @@ __global__ __launch_bounds__(64) void conv2_fwd_kernel(const uint16_t* __restric
   }
 }
 
-// ---------------------------------------------------------------------------
-// 2+3 fused. conv1 + ReLU + pool1 + conv2 + ReLU + pool2 in ONE launch.
-//    Grid (7, B): block (py, b) produces pooled conv2 row py of image b (64 oc
-//    x 7 px).  Everything conv2 needs -- P1 rows 2py-2 .. 2py+3 (6 rows x 14
-//    px x 32 ic, halo included) -- is computed by the block itself from the
-//    16 input rows it covers and kept in LDS, so P1 never goes through HBM and
-//    the two convolutions need no kernel boundary.  The halo recompute is
-//    cheap because conv1 runs on MFMA too:
-//  * conv1 as implicit GEMM: M = the 4 conv positions of each of 84 pooling
-//    windows (window-major: rows 4w..4w+3 of a 32-row tile are window w's
-//    (dy, dx) = 0..3, so an MFMA lane ends up holding whole windows and the
-//    2x2 max-pool is done in registers), N = 32 oc, K = 25 taps (padded to
-//    32).  The A operand is the raw uint8 pixel value (exact in bf16); the
-//    fp32 weight is split into bf16 hi + lo parts (two MFMAs) so the product
-//    keeps ~16 mantissa bits, and /255 is applied to the fp32 sum: the same
-//    numerics as the fp32 direct conv it replaces, within ~1e-5 relative.
-//  * conv2 as implicit GEMM from the LDS copy of P1: M = the 28 positions of
-//    the two conv rows (window-major again, pool2 in registers), N = 64 oc (2
-//    waves), K = 25 taps x 32 ic split over 2 waves and reduced in a fixed
-//    order; the conv2 weight fragments (bf16 W2r from L2) are loaded at the
-//    start of the kernel, behind the conv1 work.
-//  Outputs: A1 + AM2 (conv2 pool), AM1 for the block's own two P1 rows and,
-//  when training, their five kx-shifted planar copies (P1s) for the conv2
-//  weight gradient.  The P1 HWC tensor itself is no longer written.
-// ---------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void conv12_fwd_kernel(const uint8_t* __restrict__ x,
-                                                         const int64_t* __restrict__ idx,
-                                                         const float* __restrict__ w1, const float* __restrict__ b1,
-                                                         const uint16_t* __restrict__ w2r,
-                                                         const float* __restrict__ b2, uint8_t* __restrict__ am1,
-                                                         uint16_t* __restrict__ p1s, uint16_t* __restrict__ a1,
-                                                         uint8_t* __restrict__ am2) {
-  __shared__ uint16_t img[16][32];                                // raw pixels (bf16), rows 4py-6.., cols -2..
-  __shared__ __attribute__((aligned(16))) uint16_t p1l[6][14][kC1];  // P1 rows 2py-2 .. 2py+3, HWC
-  __shared__ uint16_t sv[kC1][2][16];                             // own P1 rows for P1s, cols 14/15 zero
-  __shared__ float red[2][16][64];                                // conv2 K-half partial sums
-  const int py = blockIdx.x, b = blockIdx.y, tid = threadIdx.x;
-  const int wave = tid >> 6, lane = tid & 63, r = lane & 31, h = lane >> 5;
-  const int64_t row = idx ? idx[b] : b;
-  const uint8_t* src = x + row * (kImg * kImg);
-
-  // -- loads that do not depend on conv1: input window, conv1 weights (as
-  //    bf16 hi/lo B fragments), conv2 weight fragments of this wave's role
-  for (int i = tid; i < 16 * 32; i += 256) {
-    const int rr = i >> 5, cc = i & 31, sy = 4 * py - 6 + rr, sx = cc - 2;
-    const bool ok = sy >= 0 && sy < kImg && sx >= 0 && sx < kImg;
-    img[rr][cc] = ok ? f32_to_bf16(float(src[sy * kImg + sx])) : uint16_t(0);
-  }
-  if (tid < kC1 * 2 * 2) sv[tid >> 2][(tid >> 1) & 1][14 + (tid & 1)] = 0;
-  uint4 bhi[2], blo[2];
-#pragma unroll
-  for (int ks = 0; ks < 2; ++ks) {
-    uint16_t hi[8], lo[8];
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const int t = ks * 16 + 8 * h + j;
-      const float wv = t < kTaps ? w1[r * kTaps + t] : 0.f;
-      hi[j] = f32_to_bf16(wv);
-      lo[j] = f32_to_bf16(wv - bf16_to_f32(hi[j]));
-    }
-    bhi[ks] = make_uint4(uint32_t(hi[0]) | (uint32_t(hi[1]) << 16), uint32_t(hi[2]) | (uint32_t(hi[3]) << 16),
-                         uint32_t(hi[4]) | (uint32_t(hi[5]) << 16), uint32_t(hi[6]) | (uint32_t(hi[7]) << 16));
-    blo[ks] = make_uint4(uint32_t(lo[0]) | (uint32_t(lo[1]) << 16), uint32_t(lo[2]) | (uint32_t(lo[3]) << 16),
-                         uint32_t(lo[4]) | (uint32_t(lo[5]) << 16), uint32_t(lo[6]) | (uint32_t(lo[7]) << 16));
-  }
-  const float bias1 = b1[r];
-  const int oh = wave & 1, kh = wave >> 1;  // conv2 role: oc half, K half (k-steps 25kh .. 25kh+24)
-  const uint16_t* wrow = w2r + size_t(oh * 32 + r) * kTaps * kC1 + 8 * h;
-  uint4 bw2[25];
-#pragma unroll
-  for (int i = 0; i < 25; ++i) {
-    const int s = 25 * kh + i;
-    bw2[i] = *reinterpret_cast<const uint4*>(wrow + (s >> 1) * kC1 + (s & 1) * 16);
-  }
-  const float bias2 = b2[oh * 32 + r];
-  __syncthreads();
-
-  // -- conv1: 84 pooling windows (6 P1 rows x 14 px) in 11 tiles of 8 windows
-  for (int t = wave; t < 11; t += 4) {
-    const int wl = min(8 * t + (r >> 2), 83);  // tile 10's dummy rows duplicate window 83
-    const int d = r & 3, prl = wl / 14, pc = wl % 14;
-    const int iy = 2 * prl + (d >> 1), ix = 2 * pc + (d & 1);  // img coords of tap (0, 0)
-    uint4 a[2];
-#pragma unroll
-    for (int ks = 0; ks < 2; ++ks) {
-      uint16_t v[8];
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const int tp = ks * 16 + 8 * h + j;
-        const int ky = tp / 5, kx = tp % 5;
-        v[j] = tp < kTaps ? img[iy + ky][ix + kx] : uint16_t(0);
-      }
-      a[ks] = make_uint4(uint32_t(v[0]) | (uint32_t(v[1]) << 16), uint32_t(v[2]) | (uint32_t(v[3]) << 16),
-                         uint32_t(v[4]) | (uint32_t(v[5]) << 16), uint32_t(v[6]) | (uint32_t(v[7]) << 16));
-    }
-    f32x16 acc = {};
-    acc = mfma32(a[0], bhi[0], acc);
-    acc = mfma32(a[0], blo[0], acc);
-    acc = mfma32(a[1], bhi[1], acc);
-    acc = mfma32(a[1], blo[1], acc);
-    // lane (oc = r, h) holds windows 8t + 2j + h, positions d = 0..3 in acc[4j + d]
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int w = 8 * t + 2 * j + h;
-      if (w >= 84) continue;
-      float best = acc[4 * j];
-      int arg = 0;
-#pragma unroll
-      for (int dd = 1; dd < 4; ++dd)
-        if (acc[4 * j + dd] > best) {
-          best = acc[4 * j + dd];
-          arg = dd;
-        }
-      const float tot = best * (1.f / 255.f) + bias1;
-      const int pr = w / 14, pcc = w % 14, pra = 2 * py - 2 + pr;
-      const uint16_t v = f32_to_bf16(fmaxf(tot, 0.f));
-      p1l[pr][pcc][r] = (pra >= 0 && pra < 14) ? v : uint16_t(0);
-      if (pr == 2 || pr == 3) {  // this block's own P1 rows
-        am1[(size_t(b) * 196 + pra * 14 + pcc) * kC1 + r] = tot > 0.f ? uint8_t(arg) : uint8_t(4);
-        sv[r][pr - 2][pcc] = v;
-      }
-    }
-  }
-  __syncthreads();
-
-  // -- conv2 from LDS: rows 4 px + d = window px (pool2), d = (dy, dx)
-  {
-    const int pxw = min(r >> 2, 6), d = r & 3;
-    const int yr = d >> 1, xx = 2 * pxw + (d & 1);
-    f32x16 acc = {};
-#pragma unroll
-    for (int i = 0; i < 25; ++i) {
-      const int s = 25 * kh + i, tp = s >> 1, ky = tp / 5, kx = tp % 5;
-      const int pcc = xx + kx - 2;
-      const bool ok = pcc >= 0 && pcc < 14;
-      const uint4 av = *reinterpret_cast<const uint4*>(&p1l[yr + ky][ok ? pcc : 0][(s & 1) * 16 + 8 * h]);
-      acc = mfma32(ok ? av : make_uint4(0, 0, 0, 0), bw2[i], acc);
-    }
-    if (kh == 1) {
-#pragma unroll
-      for (int i = 0; i < 16; ++i) red[oh][i][lane] = acc[i];
-    }
-    __syncthreads();
-    if (kh == 0) {
-#pragma unroll
-      for (int i = 0; i < 16; ++i) acc[i] += red[oh][i][lane];
-      const int oc = oh * 32 + r;
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int px = 2 * j + h;
-        if (px >= 7) continue;
-        float best = acc[4 * j];
-        int arg = 0;
-#pragma unroll
-        for (int dd = 1; dd < 4; ++dd)
-          if (acc[4 * j + dd] > best) {
-            best = acc[4 * j + dd];
-            arg = dd;
-          }
-        best += bias2;
-        const size_t o = size_t(b) * kFeat + oc * 49 + py * 7 + px;
-        a1[o] = f32_to_bf16(fmaxf(best, 0.f));
-        am2[o] = best > 0.f ? uint8_t(arg) : uint8_t(4);
-      }
-    } else if (p1s) {
-      // waves 2-3: the five kx-shifted planar copies of this block's P1 rows
-      // P1s[b][kx][oc][2py + rr + 2][c] = P1[oc][2py + rr][c + kx - 2]  (0 outside)
-      for (int i = tid - 128; i < 5 * kC1 * 2 * 2; i += 128) {
-        const int half = i & 1, rr = (i >> 1) & 1, o = (i >> 2) % kC1, kx = i / (4 * kC1);
-        uint16_t u[8];
-#pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          const int xs = half * 8 + j + kx - 2;
-          u[j] = (xs >= 0 && xs < 14) ? sv[o][rr][xs] : uint16_t(0);
-        }
-        uint4 v;
-        v.x = uint32_t(u[0]) | (uint32_t(u[1]) << 16);
-        v.y = uint32_t(u[2]) | (uint32_t(u[3]) << 16);
-        v.z = uint32_t(u[4]) | (uint32_t(u[5]) << 16);
-        v.w = uint32_t(u[6]) | (uint32_t(u[7]) << 16);
-        *reinterpret_cast<uint4*>(p1s + ((size_t(b) * 5 + kx) * kC1 + o) * kP1sPlane + (2 * py + rr + 2) * 16 + half * 8) = v;
-      }
-    }
-  }
-}
-
-void conv12_fwd(const uint8_t* x, const int64_t* idx, const float* params, Offsets off, const uint16_t* w2r,
-                uint8_t* am1, uint16_t* p1s, uint16_t* a1, uint8_t* am2, int B, hipStream_t s) {
-  hipLaunchKernelGGL(conv12_fwd_kernel, dim3(7, B), dim3(256), 0, s, x, idx, params + off.c1w, params + off.c1b, w2r,
-                     params + off.c2b, am1, p1s, a1, am2);
-}
-
 void init_fwd_attributes() {}
 
 void conv2_fwd(const uint16_t* p1, const uint16_t* w2r, const float* params, Offsets off, uint16_t* a1,

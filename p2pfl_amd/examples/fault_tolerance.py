@@ -26,11 +26,16 @@ def main(argv=None) -> None:
     p.add_argument("--number-sub", type=int, default=64, help="dataset shards (per-peer data = 1/number-sub)")
     p.add_argument("--fast", action="store_true", help="test settings (short heartbeats)")
     p.add_argument("--lr", type=float, default=None, help="override the ResNet SGD learning rate (default 0.05)")
+    p.add_argument("--no-step-graphs", action="store_true", help="eager training steps (no HIP-graph replay)")
     p.add_argument("--overlap", choices=["on", "off", "async", "streams"], default="on",
                    help="on: background diffusion (Settings.ASYNC_DIFFUSION) + per-node HIP streams; "
                         "off: the reference's blocking diffusion, all peers on the default stream; "
                         "async / streams: only one of the two")
     args = p.parse_args(argv)
+    if args.no_step_graphs:
+        import os
+
+        os.environ["P2PFL_STEP_GRAPHS"] = "0"
 
     from p2pfl_amd.communication.memory import InMemoryCommunicationProtocol
     from p2pfl_amd.management.logger import logger
@@ -80,7 +85,24 @@ def main(argv=None) -> None:
         time.sleep(0.2)
         victim.stop()
         survivors = [n for n in nodes if n is not victim]
-        wait_4_results(survivors, timeout=1800)
+        from p2pfl_amd.utils import finite
+
+        t_wait, t_print = time.monotonic(), 0.0
+        while any(n.state.round is not None for n in survivors):
+            if finite.FIRST_FAILURE:  # P2PFL_CHECK_FINITE=1: stop at the first non-finite tensor
+                node, msg = finite.FIRST_FAILURE[0]
+                print(json.dumps({"non_finite": True, "node": node, "error": msg}), flush=True)
+                import os
+
+                os._exit(3)
+            if time.monotonic() - t_print > 10:  # progress (also keeps watchdogs fed)
+                t_print = time.monotonic()
+                print(f"[fault_tolerance] {time.monotonic() - t_wait:.0f}s: rounds "
+                      f"{[n.state.round for n in survivors]}", flush=True)
+            if time.monotonic() - t_wait > 1800:
+                raise TimeoutError("survivors did not finish")
+            time.sleep(0.05)
+        wait_4_results(survivors, timeout=60)
         total = time.perf_counter() - t0
         try:
             check_equal_models(survivors)

@@ -44,9 +44,6 @@ _MERGED_ADAM = os.environ.get("P2PFL_CNN_MERGED_ADAM", "1") != "0"
 # W1^T shadow, 12.8 MB less written per step by the FC1 Adam stream); "0"
 # selects the W1^T-shadow kernel.
 _ROUTE_RM = os.environ.get("P2PFL_CNN_ROUTE_RM", "1") != "0"
-# conv1 + conv2 forward in one launch with P1 kept in LDS (P2PFL_CNN_FUSED_CONV=0:
-# the two separate kernels, P1 through memory)
-_FUSED_CONV = os.environ.get("P2PFL_CNN_FUSED_CONV", "1") != "0"
 _NAMES = ("conv1.weight", "conv1.bias", "conv2.weight", "conv2.bias", "l1.weight", "l1.bias", "l2.weight", "l2.bias")
 FEAT, HID = 3136, 2048
 
@@ -65,7 +62,6 @@ class FusedCNNEngine:
         mrows: int = 32,
         arena: Optional[ModuleArena] = None,
         split_fc1: int = 7,
-        fused_conv: Optional[bool] = None,
     ) -> None:
         self.C = ops.ext().cnn
         self.C.init()
@@ -82,7 +78,6 @@ class FusedCNNEngine:
         self.lr, self.betas, self.eps, self.wd = lr, betas, eps, weight_decay
         self.mrows = mrows
         self.S1 = split_fc1
-        self.fused_conv = _FUSED_CONV if fused_conv is None else bool(fused_conv)
         dev, bf = self.device, torch.bfloat16
         z = lambda *s, dt=torch.float32: torch.zeros(*s, dtype=dt, device=dev)  # noqa: E731
         n = self.arena.flat.numel()
@@ -134,12 +129,8 @@ class FusedCNNEngine:
 
     def forward(self, x: torch.Tensor, labels: torch.Tensor, idx: Optional[torch.Tensor], B: int, stats: torch.Tensor, train: bool) -> None:
         C, M = self.C, self.mrows
-        if self.fused_conv:
-            C.conv12_fwd(x, idx, self.params, self.off, self.w2r, self.am1, self.p1s if train else None, self.a1,
-                         self.am2, B, M)
-        else:
-            C.conv1_fwd(x, idx, self.params, self.off, self.p1, self.am1, self.p1s if train else None, B)
-            C.conv2_fwd(self.p1, self.w2r, self.params, self.off, self.a1, self.am2, B, M)
+        C.conv1_fwd(x, idx, self.params, self.off, self.p1, self.am1, self.p1s if train else None, B)
+        C.conv2_fwd(self.p1, self.w2r, self.params, self.off, self.a1, self.am2, B, M)
         C.gemm_skinny(self.a1, self.w1bf, self.slabs1, M, HID, FEAT, self.S1)
         C.head(self.slabs1, self.S1, M, self.params, self.off, labels, idx, B, train, self.H, self.dH, self.dlogits, stats)
 
@@ -225,11 +216,8 @@ class _EvalForward:
 
     def forward(self, x: torch.Tensor, labels: torch.Tensor, idx: Optional[torch.Tensor], B: int, stats: torch.Tensor) -> None:
         e, C, M = self.eng, self.eng.C, self.MROWS
-        if e.fused_conv:
-            C.conv12_fwd(x, idx, e.params, e.off, e.w2r, self.am1, None, self.a1, self.am2, B, M)
-        else:
-            C.conv1_fwd(x, idx, e.params, e.off, self.p1, self.am1, None, B)
-            C.conv2_fwd(self.p1, e.w2r, e.params, e.off, self.a1, self.am2, B, M)
+        C.conv1_fwd(x, idx, e.params, e.off, self.p1, self.am1, None, B)
+        C.conv2_fwd(self.p1, e.w2r, e.params, e.off, self.a1, self.am2, B, M)
         C.gemm_skinny(self.a1, e.w1bf, self.slabs1, M, HID, FEAT, e.S1)
         C.head(self.slabs1, e.S1, M, e.params, e.off, labels, idx, B, False, self.H, self.dH, self.dlogits, stats)
 

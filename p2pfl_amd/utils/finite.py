@@ -19,6 +19,8 @@ import torch
 from p2pfl_amd.management.logger import logger
 
 ENABLED = os.environ.get("P2PFL_CHECK_FINITE") == "1"
+# first failure of the process (node, message), for drivers that stop early
+FIRST_FAILURE: "list" = []
 
 
 class NonFiniteError(FloatingPointError):
@@ -40,4 +42,6 @@ def check(node: str, what: str, t: Any, **ctx: Any) -> None:
     if bad:
         msg = f"non-finite {what}: {bad} of {flat.numel()} elements" + "".join(f", {k}={v}" for k, v in ctx.items())
         logger.error(node, msg)
+        if not FIRST_FAILURE:
+            FIRST_FAILURE.append((node, msg))
         raise NonFiniteError(f"{node}: {msg}")

@@ -29,7 +29,14 @@ import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
 
 
+def _say(msg: str) -> None:
+    print(f"[rccl_worker {os.environ.get('RANK')}] {time.strftime('%H:%M:%S')} {msg}", flush=True)
+
+
 def main(out: str) -> None:
+    import faulthandler
+
+    faulthandler.dump_traceback_later(float(os.environ.get("P2PFL_WORKER_WATCHDOG", "100")), exit=True)
     from p2pfl_amd.communication.xgmi.data_plane import XgmiDataPlane, make_backend_factory
 
     rank, world = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
@@ -40,8 +47,10 @@ def main(out: str) -> None:
                           store=store, prefix="r2", device=dev, ack_timeout=30.0, group_timeout=60.0, preconnect=True)
     plane.allow_fallback = False
     t0 = time.perf_counter()
+    _say("communicator init")
     plane.start(block=True)
     init_s = time.perf_counter() - t0
+    _say(f"plane up in {init_s:.2f}s: backend {plane.backend_name}, failed={plane.failed}")
     if plane.failed:
         raise SystemExit(f"rank {rank}: {plane.failed}")
     peer = 1 - rank
@@ -50,10 +59,16 @@ def main(out: str) -> None:
     received, sent_ok = [], []
     done = threading.Semaphore(0)
 
-    # header exchange through the store (the transport uses the control bus)
+    # header exchange through the store (the transport uses the control bus).
+    # A TCPStore client holds its connection lock for the whole of a blocking
+    # get(), so every thread that waits on a key gets its own client.
+    def client():
+        return dist.TCPStore("127.0.0.1", int(os.environ["MASTER_PORT"]), world, False)
+
     def serve_headers():
+        st = client()
         for i in range(pushes):
-            hdr = json.loads(store.get(f"hdr/{peer}/{i}").decode())
+            hdr = json.loads(st.get(f"hdr/{peer}/{i}").decode())
 
             def on_recv(buf, reason, i=i):
                 with lock:
@@ -62,11 +77,12 @@ def main(out: str) -> None:
 
             e, why = plane.accept(peer, hdr, on_recv)
             assert e is not None, why
-            store.set(f"ack/{peer}/{i}", json.dumps([hdr["seq"], e, hdr["gen"]]))
+            st.set(f"ack/{peer}/{i}", json.dumps([hdr["seq"], e, hdr["gen"]]))
 
     def collect_acks(seqs):
+        st = client()
         for i in range(pushes):
-            seq, e, gen = json.loads(store.get(f"ack/{rank}/{i}").decode())
+            seq, e, gen = json.loads(st.get(f"ack/{rank}/{i}").decode())
             plane.on_ack(seq, e, gen)
 
     srcs = []
@@ -88,11 +104,14 @@ def main(out: str) -> None:
         store.set(f"hdr/{rank}/{i}", json.dumps(hdr))
     acker = threading.Thread(target=collect_acks, args=(seqs,), daemon=True)
     acker.start()
+    _say(f"{pushes} pushes proposed")
     t1 = time.perf_counter()
-    for _ in range(2 * pushes):
-        if not done.acquire(timeout=120):
+    for k in range(2 * pushes):
+        if not done.acquire(timeout=60):
+            _say(f"stalled after {k} completions; stats {dict(plane.stats)}")
             raise SystemExit(f"rank {rank}: transfers stalled")
     xfer_s = time.perf_counter() - t1
+    _say(f"transfers done in {xfer_s:.3f}s; stats {dict(plane.stats)}")
     ok = all(o for _, o, _ in sent_ok) and len(sent_ok) == pushes
     bad = []
     for i, buf, reason in received:

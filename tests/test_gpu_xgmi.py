@@ -125,7 +125,7 @@ def _free_port() -> int:
         return s.getsockname()[1]
 
 
-@pytest.mark.timeout(300)
+@pytest.mark.timeout(200)
 def test_two_rank_rccl_communicator_on_one_gpu_concurrent_pushes(tmp_path):
     """A REAL 2-rank RCCL communicator (one process per rank) on the box's single
     GPU: each rank looks like its own host (distinct NCCL_HOSTID), so RCCL forms
@@ -143,13 +143,14 @@ def test_two_rank_rccl_communicator_on_one_gpu_concurrent_pushes(tmp_path):
     procs = []
     for r in range(2):
         env = dict(os.environ, RANK=str(r), WORLD_SIZE="2", MASTER_PORT=str(port), PYTHONPATH=root,
-                   NCCL_HOSTID=f"p2pfl-test-r{r}", NCCL_SOCKET_IFNAME="lo", NCCL_IB_DISABLE="1", P2PFL_LOCKCHECK="0")
+                   NCCL_HOSTID=f"p2pfl-test-r{r}", NCCL_SOCKET_IFNAME="lo", NCCL_IB_DISABLE="1", P2PFL_LOCKCHECK="0",
+                   P2PFL_WORKER_WATCHDOG="120")
         procs.append(subprocess.Popen([sys.executable, os.path.join(root, "tests", "rccl_worker.py"), out], cwd=root,
                                       env=env, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True))
     outs = []
     for p in procs:
         try:
-            o, _ = p.communicate(timeout=240)
+            o, _ = p.communicate(timeout=150)
         except subprocess.TimeoutExpired:
             p.kill()
             o, _ = p.communicate()
