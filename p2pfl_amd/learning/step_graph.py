@@ -25,6 +25,7 @@ from typing import Any, Optional, Tuple
 
 import torch
 
+from p2pfl_amd.ops import splitk
 from p2pfl_amd.utils.lockcheck import make_lock
 
 # virtual peers (one node thread each) may capture concurrently: serialise
@@ -137,7 +138,8 @@ class TrainStepGraph:
                 self._body(graph=False)  # lazy inits (workspaces, solver choices) outside the capture
             self.stream.synchronize()
             g = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(g, stream=self.stream, capture_error_mode="thread_local"):
+            self.counters = splitk.GraphCounters(learner.device)  # split-K tile counters owned by this graph
+            with splitk.graph_scope(self.counters), torch.cuda.graph(g, stream=self.stream, capture_error_mode="thread_local"):
                 self.loss = self._body(graph=True)
             torch.cuda.synchronize(learner.device)
             opt.mt.fill_grad_table(self.gtab)  # the graph's gradient buffers, fixed for every replay
@@ -217,7 +219,8 @@ class EvalStepGraph:
                 self.step(self.idx, float(self.B), cache=False)  # warm-up, creates the sums
             self.stream.synchronize()
             g = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(g, stream=self.stream, capture_error_mode="thread_local"):
+            self.counters = splitk.GraphCounters(learner.device)
+            with splitk.graph_scope(self.counters), torch.cuda.graph(g, stream=self.stream, capture_error_mode="thread_local"):
                 self.step(self.idx, float(self.B), cache=False)
             torch.cuda.synchronize(learner.device)
         self.graph = g

@@ -29,10 +29,54 @@ _RINGS: Dict[Tuple[int, int], List] = {}
 _LOCK = threading.Lock()
 
 
+# Counters of launches captured into a HIP graph belong to THAT graph: two
+# graphs may be captured on the same pooled stream, and a per-stream ring that
+# wraps around would hand a later capture (or eager launch) the slice an
+# earlier graph baked in -- replayed concurrently on different streams, the
+# two launches would corrupt each other's tile counts.  A capture therefore
+# takes its slices from a ring of its own (kept alive by the graph object),
+# which never wraps.
+_SCOPE = threading.local()
+
+
+class GraphCounters:
+    """Counter ring owned by one captured graph (see :func:`graph_scope`)."""
+
+    def __init__(self, device: torch.device, size: int = RING) -> None:
+        self.buf = torch.zeros(size, dtype=torch.int32, device=device)
+        self.used = 0
+
+    def take(self, tiles: int) -> torch.Tensor:
+        off = self.used
+        if off + tiles > self.buf.numel():
+            raise RuntimeError(f"graph counter ring exhausted ({off} + {tiles} > {self.buf.numel()})")
+        self.used += (tiles + 15) // 16 * 16
+        return self.buf[off : off + tiles]
+
+
+class graph_scope:
+    """``with graph_scope(ring): <capture>`` -- split-K launches captured by this
+    thread take their counters from ``ring``."""
+
+    def __init__(self, ring: GraphCounters) -> None:
+        self.ring = ring
+
+    def __enter__(self) -> GraphCounters:
+        self.prev = getattr(_SCOPE, "ring", None)
+        _SCOPE.ring = self.ring
+        return self.ring
+
+    def __exit__(self, *exc) -> None:
+        _SCOPE.ring = self.prev
+
+
 def counters(tiles: int, device: torch.device) -> torch.Tensor:
     """A zeroed int32 slice of ``tiles`` counters for one launch on the current stream."""
     if tiles > RING:
         raise ValueError(f"split-K launch with {tiles} tiles exceeds the counter ring")
+    scoped = getattr(_SCOPE, "ring", None)
+    if scoped is not None:
+        return scoped.take(tiles)
     stream = torch.cuda.current_stream(device)
     key = (stream.device_index, stream.cuda_stream)
     with _LOCK:

@@ -46,3 +46,26 @@ def test_conv_split_choices():
     assert mn_splits(32768, 64, 576) == 1
     assert mn_splits(512, 512, 4608) == 16
     assert wgrad_splits(64, 576, 32768) >= 16
+
+
+def test_split_k_counters_of_a_captured_graph_come_from_its_own_ring():
+    """Two graphs captured on one pooled stream must never share counter slices
+    (concurrent replays would corrupt each other's tile counts); eager launches
+    keep using the per-stream ring."""
+    import pytest
+    import torch
+
+    from p2pfl_amd.ops import splitk
+
+    dev = torch.device("cpu")
+    a, b = splitk.GraphCounters(dev, 64), splitk.GraphCounters(dev, 64)
+    with splitk.graph_scope(a):
+        s1 = splitk.counters(10, dev)
+        s2 = splitk.counters(10, dev)
+        with splitk.graph_scope(b):
+            s3 = splitk.counters(10, dev)
+    assert s1.data_ptr() != s2.data_ptr() and s1.untyped_storage().data_ptr() == a.buf.untyped_storage().data_ptr()
+    assert s3.untyped_storage().data_ptr() == b.buf.untyped_storage().data_ptr()
+    assert getattr(splitk._SCOPE, "ring", None) is None
+    with splitk.graph_scope(a), pytest.raises(RuntimeError, match="exhausted"):
+        splitk.counters(60, dev)  # a graph's ring never wraps onto slices it already baked in
