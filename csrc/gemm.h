@@ -34,9 +34,12 @@ struct GemmParams {
   int splits;
   float* ws;      // split-K workspace for the in-launch reduction
   int* counters;  // per-tile arrival counters (see above), or null
-  int variant;  // tuning experiments: bit0 setprio around MFMAs, bit1 A-panel tile order, bit2 no XCD remap, bit3 single LDS buffer (4 workgroups / CU), bit4/bit5 timing probes (no stores / no K loop), bit6 256 x 256 tile (8 waves), bit7 no DMA after the prologue (probe), bit8 legacy panel tile order instead of grouped (bit1 then picks A- vs B-panel order), bits 9-10 where the double-buffer prefetch is issued (0 before the K-tile's fragment reads, 1 after the first ones, 2 one chunk per k-substep)
+  int variant;  // tuning experiments: bit0 setprio around MFMAs, bit1 A-panel tile order, bit2 no XCD remap, bit3 single LDS buffer (4 workgroups / CU), bit4/bit5 timing probes (no stores / no K loop), bit6 256 x 256 tile (8 waves), bit7 no DMA after the prologue (probe), bit8 legacy panel tile order instead of grouped (bit1 then picks A- vs B-panel order), bits 9-10 where the double-buffer prefetch is issued (0 before the K-tile's fragment reads, 1 after the first ones, 2 one chunk per k-substep), bit11 the ping-pong 256 x 256 pipeline of gemm_pp.hip (continuous per-phase DMA, staggered wave halves)
 };
 
 void gemm_bf16(const GemmParams& p, hipStream_t s);
+// the ping-pong pipeline (gemm_pp.hip); gemm_bf16 routes variant bit 11 here
+bool gemm_pp_supported(const GemmParams& p);
+void gemm_bf16_pp(const GemmParams& p, hipStream_t s);
 
 }  // namespace p2

@@ -74,6 +74,10 @@ void gemm_bf16(const GemmParams& p, hipStream_t s) {
   using namespace p2gemm;
   GemmParams q = p;
   if (q.splits < 1) q.splits = 1;
+  if ((q.variant & 2048) && gemm_pp_supported(q)) {
+    gemm_bf16_pp(q, s);
+    return;
+  }
   if (p.a_kmajor && p.b_kmajor)
     launch(q, PlainK{p.a, p.lda, p.M, p.K}, PlainK{p.b, p.ldb, p.N, p.K}, s);
   else if (p.a_kmajor)

@@ -246,6 +246,8 @@ def test_async_fit_orders_validation_before_replaced_weights():
         assert float(ln.get_parameters().flat.abs().sum()) == 0.0
         got.append((trained.flat, seen["val_loss"], seen["val_metric"], seen["train_loss"] if "train_loss" in seen else None))
     torch.testing.assert_close(got[0][0], got[1][0], rtol=0, atol=0)
-    assert got[0][1] == got[1][1] and got[0][2] == got[1][2]
+    # the evaluation head folds per-sample losses with fp32 atomics (order varies
+    # run to run, ~1 ulp of the sum); the correct-count is exact
+    assert got[0][1] == pytest.approx(got[1][1], rel=1e-5) and got[0][2] == got[1][2]
     # validation of a zeroed CNN would give the uniform loss log(10)
     assert abs(got[0][1] - 2.302585) > 1e-3
