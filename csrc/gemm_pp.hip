@@ -149,7 +149,11 @@ __global__ __launch_bounds__(512) void gemm_pp_kernel(GemmParams p, int tiles_m,
   int kper = (p.K + p.splits - 1) / p.splits;
   kper = (kper + BK - 1) / BK * BK;
   const int kb = split * kper, ke = min(p.K, kb + kper);
-  const int nt = ke > kb ? (ke - kb + BK - 1) / BK : 0;
+  // timing probes (variant bits): 12 no DMA after the prologue, 13 no stagger,
+  // 14 no C stores, 15 no K loop
+  const int probe = p.variant >> 12;
+  const int nt = (ke > kb && !(probe & 8)) ? (ke - kb + BK - 1) / BK : 0;
+  const bool dma_on = !(probe & 1), stag = !(probe & 2);
 
   SA sa;
   SB sb;
@@ -259,14 +263,14 @@ __global__ __launch_bounds__(512) void gemm_pp_kernel(GemmParams p, int tiles_m,
       vm0();
     }
     bar();
-    if (wr == 1) bar();  // stagger: waves 4-7 run one barrier behind
+    if (stag && wr == 1) bar();  // stagger: waves 4-7 run one barrier behind
     constexpr int b0 = 0, b1 = 1;
     for (int it = 0; it < nt; it += 2) {
-      const bool n1 = it + 1 < nt, n2 = it + 2 < nt, n3 = it + 3 < nt;
+      const bool n1 = it + 1 < nt, n2 = dma_on && it + 2 < nt, n3 = dma_on && it + 3 < nt;
       // ph1: (a-lo, b-lo) of tile it; Blo of tile it + 1 -> buffer 1
       read_a(b0, 0);
       read_b(b0, 0);
-      if (n1) stage(2, it + 1, 1);
+      if (dma_on && n1) stage(2, it + 1, 1);
       lgkm0();
       bar();
       mma(0, 0);
@@ -330,7 +334,7 @@ __global__ __launch_bounds__(512) void gemm_pp_kernel(GemmParams p, int tiles_m,
       mma(1, 0);
       bar();
     }
-    if (wr == 0) bar();  // balance the stagger
+    if (stag && wr == 0) bar();  // balance the stagger
   }
   // ---- epilogue.  Block (i, j) of the wave: i = 2 h + i' -> tile rows
   // 128 h + 64 wr + 32 i', j -> tile cols 128 j + 32 wc; lane holds rows
@@ -410,23 +414,26 @@ __global__ __launch_bounds__(512) void gemm_pp_kernel(GemmParams p, int tiles_m,
       *reinterpret_cast<uint2*>(smem + r * LROW + c * 2) = uint2{pack_bf16x2(v[0], v[1]), pack_bf16x2(v[2], v[3])};
     }
   };
-#pragma unroll
-  for (int i = 0; i < FM; ++i)
-#pragma unroll
-    for (int j = 0; j < FN; ++j)
-#pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        if (p.splits > 1) {
+  if (p.splits > 1) {  // the reducer: one 4-value group of all slices at a time (acc is in its own slab)
+    for (int i = 0; i < FM; ++i)
+      for (int j = 0; j < FN; ++j)
+        for (int g = 0; g < 4; ++g) {
           const int m = row_of(i), n = col_of(j, g);
           f32x4 sum = {0.f, 0.f, 0.f, 0.f};
           if (m < p.M && n < p.N)
             for (int s2 = 0; s2 < p.splits; ++s2) sum += *reinterpret_cast<const f32x4*>(slabs + s2 * mn + int64_t(m) * p.N + n);
           finish(i, j, g, sum[0], sum[1], sum[2], sum[3]);
-        } else {
-          finish(i, j, g, acc[i][j][4 * g], acc[i][j][4 * g + 1], acc[i][j][4 * g + 2], acc[i][j][4 * g + 3]);
         }
-      }
-  if (!p.c_bf16) return;
+  } else {  // fully unrolled: acc is only ever indexed by constants (else it lands in scratch)
+#pragma unroll
+    for (int i = 0; i < FM; ++i)
+#pragma unroll
+      for (int j = 0; j < FN; ++j)
+#pragma unroll
+        for (int g = 0; g < 4; ++g)
+          finish(i, j, g, acc[i][j][4 * g], acc[i][j][4 * g + 1], acc[i][j][4 * g + 2], acc[i][j][4 * g + 3]);
+  }
+  if (!p.c_bf16 || (probe & 4)) return;
   __syncthreads();
 #pragma unroll
   for (int q = 0; q < 256 * 32 / 512; ++q) {  // 256 rows x 32 16-byte chunks

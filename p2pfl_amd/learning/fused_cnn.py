@@ -324,13 +324,15 @@ class FusedCNNLearner(TorchLearner):
         eg.stats = torch.zeros((len(plan) if train else 1, 4), dtype=torch.float32, device=self.device)
         if not self.use_graphs:
             return eg
+        from p2pfl_amd.learning.step_graph import no_gc
+
         # capture on a side stream; state that the graph mutates (weights,
         # Adam moments, step counter) is saved and restored around the capture
         with _CAPTURE_LOCK:
             torch.cuda.synchronize(self.device)
             saved = [t.clone() for t in (self.engine.params, self.engine.m, self.engine.v, self.engine.adam_t)]
             graph = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(graph, stream=self._stream, capture_error_mode="thread_local"):
+            with no_gc(), torch.cuda.graph(graph, stream=self._stream, capture_error_mode="thread_local"):
                 self._enqueue(loader, plan, train, eg.perm, eg.stats)
             torch.cuda.synchronize(self.device)
             for dst, src in zip((self.engine.params, self.engine.m, self.engine.v, self.engine.adam_t), saved):

@@ -19,6 +19,7 @@ seeds SGD momentum) and a short last batch run eagerly.
 
 from __future__ import annotations
 
+import gc
 import threading
 from contextlib import contextmanager
 from typing import Any, Optional, Tuple
@@ -77,6 +78,22 @@ class DeviceGate:
 
 
 GATE = DeviceGate()
+
+
+@contextmanager
+def no_gc():
+    """Collect now, then keep Python's cyclic GC off for the capture: a collection
+    during capture can run the destructor of an unrelated object holding device
+    resources (another learner's graph, events, streams) -- a HIP call that
+    invalidates this thread's capture and aborts the process."""
+    gc.collect()
+    was = gc.isenabled()
+    gc.disable()
+    try:
+        yield
+    finally:
+        if was:
+            gc.enable()
 
 
 def graphable_loader(loader: Any) -> bool:
@@ -139,7 +156,7 @@ class TrainStepGraph:
             self.stream.synchronize()
             g = torch.cuda.CUDAGraph()
             self.counters = splitk.GraphCounters(learner.device)  # split-K tile counters owned by this graph
-            with splitk.graph_scope(self.counters), torch.cuda.graph(g, stream=self.stream, capture_error_mode="thread_local"):
+            with no_gc(), splitk.graph_scope(self.counters), torch.cuda.graph(g, stream=self.stream, capture_error_mode="thread_local"):
                 self.loss = self._body(graph=True)
             torch.cuda.synchronize(learner.device)
             opt.mt.fill_grad_table(self.gtab)  # the graph's gradient buffers, fixed for every replay
@@ -220,7 +237,7 @@ class EvalStepGraph:
             self.stream.synchronize()
             g = torch.cuda.CUDAGraph()
             self.counters = splitk.GraphCounters(learner.device)
-            with splitk.graph_scope(self.counters), torch.cuda.graph(g, stream=self.stream, capture_error_mode="thread_local"):
+            with no_gc(), splitk.graph_scope(self.counters), torch.cuda.graph(g, stream=self.stream, capture_error_mode="thread_local"):
                 self.step(self.idx, float(self.B), cache=False)
             torch.cuda.synchronize(learner.device)
         self.graph = g

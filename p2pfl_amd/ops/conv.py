@@ -31,7 +31,7 @@ from p2pfl_amd.ops import autotune
 from p2pfl_amd.ops.splitk import IN_LAUNCH_MAX_SPLITS, counters, tiles_of
 
 # counters a test can read to prove the native path ran
-STATS = {"native_fwd": 0, "torch_fwd": 0}
+STATS = {"native_fwd": 0, "torch_fwd": 0, "gemm_1x1_fwd": 0}
 
 # "native" | "library" | "auto" (measured per shape, ops/autotune.py); env P2PFL_NATIVE_CONV
 _POLICY = autotune.policy("P2PFL_NATIVE_CONV")
@@ -201,8 +201,46 @@ def _native_faster(x: torch.Tensor, conv: nn.Conv2d) -> bool:
     return autotune.choose(key, [("native", native), ("library", library)]) == "native"
 
 
+# 1x1 convolutions (ResNet-50 bottlenecks and downsample shortcuts) run as the
+# GEMM they are: NHWC pixels x C times W^T, through ops.gemm.linear (native MFMA
+# GEMM or hipBLASLt, measured per shape; all memory from PyTorch's allocator).
+# MIOpen solves them with GEMM-based solvers whose library-internal workspace
+# is not graph-safe: replayed in a captured step graph they corrupted the
+# weight gradients whenever PyTorch's allocator had to map new segments
+# (profiles/r3_nan_root_cause.md).  P2PFL_CONV1X1_GEMM=0 restores conv2d.
+_ONE_BY_ONE_GEMM = os.environ.get("P2PFL_CONV1X1_GEMM", "1") != "0"
+
+
+def _is_1x1(x: torch.Tensor, conv: nn.Conv2d) -> bool:
+    from p2pfl_amd.ops import _gpu
+
+    return (_ONE_BY_ONE_GEMM and _gpu(x) and x.dim() == 4 and tuple(conv.kernel_size) == (1, 1) and conv.groups == 1
+            and _sym(conv.padding) == 0 and _sym(conv.dilation) == 1 and _sym(conv.stride) in (1, 2)
+            and conv.padding_mode == "zeros" and conv.weight.shape[0] % 8 == 0 and conv.weight.shape[1] % 8 == 0)
+
+
+def conv1x1_gemm(x: torch.Tensor, conv: nn.Conv2d) -> torch.Tensor:
+    """``conv(x)`` for a 1x1 convolution as a GEMM over channels-last pixels (stride 2: every
+    other row / column first).  Returns a channels-last NCHW tensor; autograd flows through
+    the view ops and :func:`p2pfl_amd.ops.gemm.linear`."""
+    from p2pfl_amd.ops.gemm import linear
+
+    s = _sym(conv.stride)
+    x4 = x.permute(0, 2, 3, 1)
+    if s == 2:
+        x4 = x4[:, ::2, ::2, :]
+    N, H, W_, C = x4.shape
+    O = conv.weight.shape[0]
+    y2 = linear(x4.reshape(N * H * W_, C), conv.weight.reshape(O, C), conv.bias)
+    STATS["gemm_1x1_fwd"] += 1
+    return y2.view(N, H, W_, O).permute(0, 3, 1, 2)
+
+
 def conv2d(x: torch.Tensor, conv: nn.Conv2d) -> torch.Tensor:
-    """``conv(x)`` on the implicit-GEMM kernels or MIOpen (``_POLICY``; "auto" = measured per shape)."""
+    """``conv(x)`` on the implicit-GEMM kernels or MIOpen (``_POLICY``; "auto" = measured per shape);
+    1x1 convolutions as GEMMs (:func:`conv1x1_gemm`)."""
+    if _is_1x1(x, conv):
+        return conv1x1_gemm(x, conv)
     if native_ok(x, conv) and _POLICY != "library" and (_POLICY == "native" or _native_faster(x, conv)):
         STATS["native_fwd"] += 1
         return _Conv2dNHWC.apply(x, conv.weight, _sym(conv.stride), _sym(conv.padding), _sym(conv.dilation))

@@ -83,13 +83,25 @@ def _product(a, b, a_kmajor, b_kmajor, dtype, splits=1):
 _VARIANT_ENV = os.environ.get("P2PFL_GEMM_VARIANT")
 
 
-def _variant(a_kmajor: bool, splits: int, M: int = 0, N: int = 0, K: int = 0) -> int:
+PP = 2048  # variant bit 11: the ping-pong 256 x 256 pipeline (csrc/gemm_pp.hip)
+
+
+def pp_eligible(M: int, N: int, K: int, a_kmajor: bool, b_kmajor: bool) -> bool:
+    """Products the ping-pong kernel takes and wins on (profiles/r3_gemm_pingpong.md):
+    at least ~150 tiles of 256 x 256 (below that one partial wave of big tiles
+    loses to the 128 x 128 tile), and no K tail in a k-major operand (k-major
+    tails are not caught by its buffer range check)."""
+    tiles = -(-M // 256) * -(-N // 256)
+    return tiles >= 150 and (K % 64 == 0 or not (a_kmajor or b_kmajor))
+
+
+def _variant(a_kmajor: bool, splits: int, M: int = 0, N: int = 0, K: int = 0, b_kmajor: bool = True) -> int:
     if _VARIANT_ENV is not None:
         return int(_VARIANT_ENV)
-    if splits == 1 and M * N >= 4096 * 4096 and K >= 2048:
-        # large products: the 256 x 256 8-wave tile (half the operand bytes
-        # per FLOP; profiles/r2_gemm_256.md), grouped XCD-local tile order
-        return 64
+    if splits == 1 and pp_eligible(M, N, K, a_kmajor, b_kmajor):
+        # large products: 256 x 256 tile, per-phase DMA streaming, staggered
+        # wave halves (1284 vs 1106 TF/s for the round-2 256 tile at 8192^3)
+        return PP
     return 2 if (splits > 1 or not a_kmajor) else 10
 
 
@@ -134,7 +146,7 @@ def gemm(
     if out is None:
         out = torch.empty((M, N), dtype=out_dtype, device=dev)
     z = torch.empty((M, N), dtype=torch.bfloat16, device=dev) if (gelu and want_z) else None
-    _C().gemm(a, b, a_kmajor, b_kmajor, out, bias, gelu, z, residual, 1, _variant(a_kmajor, 1, M, N, K))
+    _C().gemm(a, b, a_kmajor, b_kmajor, out, bias, gelu, z, residual, 1, _variant(a_kmajor, 1, M, N, K, b_kmajor))
     return out, z
 
 

@@ -105,6 +105,9 @@ def main():
                     t = timeit(lambda: fn(v, out, s, ws, cn), iters=30)
                     if best is None or t < best[0]:
                         best = (t, s)
+                if best is None:
+                    row.append("-")
+                    continue
                 t, s = best
                 row.append(f"{2 * m * n * k / t / 1e12:.0f}" + (f" (s{s})" if s > 1 else ""))
             t = timeit(lib, iters=30)
@@ -112,5 +115,26 @@ def main():
             print(f"| {name} {kind} {m}x{n}x{k} | " + " | ".join(row) + " |", flush=True)
 
 
-if __name__ == "__main__":
+if __name__ == "__main__" and "--probes" not in sys.argv:
     main()
+
+
+def probes():
+    """Where the ping-pong kernel's time goes: timing probes (variant bits 12-15)."""
+    names = [(PP, "full"), (PP | 4096, "no DMA"), (PP | 8192, "no stagger"), (PP | 16384, "no C stores"),
+             (PP | 32768, "no K loop"), (PP | 4096 | 16384, "no DMA, no stores"), (64, "v64"), (10, "v10")]
+    print("| shape | " + " | ".join(n for _, n in names) + " |")
+    print("|---|" + "---:|" * len(names))
+    for (m, n, k) in ((8192, 8192, 8192), (4096, 4096, 4096), (6304, 2304, 768), (6304, 3072, 768)):
+        a = (torch.rand(m, k, device="cuda") * 2 - 1).to(bf)
+        b = (torch.rand(n, k, device="cuda") * 2 - 1).to(bf)
+        o = torch.empty(m, n, device="cuda", dtype=bf)
+        row = []
+        for v, _ in names:
+            t = timeit(lambda: C.gemm(a, b, True, True, o, None, False, None, None, 1, v), iters=20, warm=3)
+            row.append(f"{t * 1e6:.1f} us / {2 * m * n * k / t / 1e12:.0f}")
+        print(f"| {m}x{n}x{k} | " + " | ".join(row) + " |", flush=True)
+
+
+if __name__ == "__main__" and "--probes" in sys.argv:
+    probes()

@@ -20,25 +20,7 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import torch  # noqa: E402
 
 
-def poison_free_blocks(dev: torch.device, fill: bool = True) -> list:
-    """Allocate (and, with ``fill``, NaN-fill) every free block of the caching allocator."""
-    keep = []
-    sizes = [1 << s for s in range(30, 9, -1)]
-    for sz in sizes:
-        while True:
-            free_cached = torch.cuda.memory_reserved(dev) - torch.cuda.memory_allocated(dev)
-            if free_cached < sz:
-                break
-            before = torch.cuda.memory_reserved(dev)
-            t = torch.empty(sz // 4, dtype=torch.float32, device=dev)
-            if torch.cuda.memory_reserved(dev) > before:  # new segment: not a freed block
-                del t
-                break
-            if fill:
-                t.fill_(float("nan"))
-            keep.append(t)
-    torch.cuda.synchronize(dev)
-    return keep
+from p2pfl_amd.utils.alloc_probe import poison_free_blocks  # noqa: E402,F401  (re-exported for graph_uaf_bisect)
 
 
 def main() -> None:
@@ -48,6 +30,10 @@ def main() -> None:
     ap.add_argument("--poison", action="store_true")
     ap.add_argument("--fits", type=int, default=3)
     ap.add_argument("--hold-only", action="store_true", help="hold the free blocks but keep their content (no NaN)")
+    ap.add_argument("--trace-steps", action="store_true")
+    ap.add_argument("--fresh", choices=("nan", "zero", "one"), default=None,
+                    help="before fit 1: hold the free blocks, then fill one big new block with this value and free it, "
+                         "so fit 1's new allocations come from memory of known content")
     a = ap.parse_args()
     if a.no_graphs:
         os.environ["P2PFL_STEP_GRAPHS"] = "0"
@@ -69,13 +55,36 @@ def main() -> None:
         model = (ResNet50 if a.model == "resnet50" else ResNet18)(seed=1234)
         data = Cifar10FederatedDM(sub_id=0, number_sub=64, partitioner="dirichlet", alpha=0.5)
     ln = TorchLearner(model, data, "poison", 1, device=dev)
+    if a.trace_steps:
+        # name the first step of the second fit whose loss or weights turn non-finite
+        from p2pfl_amd.learning.step_graph import TrainStepGraph
+
+        state = {"fit": 0, "step": 0, "reported": False}
+        orig_run = TrainStepGraph.run
+
+        def run(self, idx):
+            loss = orig_run(self, idx)
+            if state["fit"] == 1 and not state["reported"]:
+                torch.cuda.synchronize(dev)
+                lf = bool(torch.isfinite(loss).all())
+                wf = bool(torch.isfinite(ln.arena.flat).all())
+                if state["step"] < 3 or not (lf and wf):
+                    print(f"   replay {state['step']}: loss {float(loss):.4f} finite={lf} weights finite={wf}", flush=True)
+                if not (lf and wf):
+                    state["reported"] = True
+            state["step"] += 1
+            return loss
+
+        TrainStepGraph.run = run
     keep = []
     for i in range(a.fits):
         ln.fit()
         torch.cuda.synchronize(dev)
         flat = ln.get_parameters().flat
         bad = int((~torch.isfinite(flat)).sum())
-        print(f"fit {i}: non-finite parameters {bad} of {flat.numel()}; graph={ln._step_graph is not None}", flush=True)
+        sg = ln._step_graph
+        print(f"fit {i}: non-finite parameters {bad} of {flat.numel()}; graph={sg is not None} "
+              f"graph_id={id(sg.graph) if sg is not None and sg.graph is not None else None}", flush=True)
         if bad:
             names = ln.arena.layout.names
             per = [(n, int((~torch.isfinite(t)).sum()), t.numel()) for n, t in ln.get_parameters().items()]
@@ -85,6 +94,18 @@ def main() -> None:
                 print(f"   {n}: {k}/{m}", flush=True)
             print(f"   last: {first[-1][0]}", flush=True)
             sys.exit(2)
+        if a.fresh and i == 0:
+            keep = poison_free_blocks(dev, fill=False)
+            free_b = torch.cuda.mem_get_info(dev)[0]
+            big = torch.empty(int(free_b * 0.5) // 4, dtype=torch.float32, device=dev)
+            big.fill_({"nan": float("nan"), "zero": 0.0, "one": 1.0}[a.fresh])
+            torch.cuda.synchronize(dev)
+            print(f"held {len(keep)} free blocks; {big.numel() * 4 / 2**30:.1f} GiB of fresh memory filled with "
+                  f"{a.fresh} and returned to the cache", flush=True)
+            del big
+        if a.trace_steps:
+            state["fit"], state["step"] = i + 1, 0
+            print(f"   after fit {i}: weights finite={bool(torch.isfinite(ln.arena.flat).all())}", flush=True)
         if (a.poison or a.hold_only) and i == 0:
             keep = poison_free_blocks(dev, fill=not a.hold_only)
             print(f"poisoned {sum(t.numel() for t in keep) * 4 / 2**20:.1f} MiB of free cached blocks in {len(keep)} tensors",

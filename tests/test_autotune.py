@@ -69,3 +69,16 @@ def test_split_k_counters_of_a_captured_graph_come_from_its_own_ring():
     assert getattr(splitk._SCOPE, "ring", None) is None
     with splitk.graph_scope(a), pytest.raises(RuntimeError, match="exhausted"):
         splitk.counters(60, dev)  # a graph's ring never wraps onto slices it already baked in
+
+
+def test_gemm_variant_rule_takes_the_ping_pong_kernel_for_large_products():
+    import importlib
+
+    gemm = importlib.import_module("p2pfl_amd.ops.gemm")
+
+    assert gemm._variant(True, 1, 6304, 2304, 768) == gemm.PP  # ViT QKV forward: 225 tiles of 256^2
+    assert gemm._variant(True, 1, 6304, 768, 768) == 10  # 75 tiles: the 128 x 128 tile
+    assert gemm._variant(True, 1, 8192, 8192, 8192, False) == gemm.PP
+    assert gemm._variant(True, 1, 8192, 8192, 8008) != gemm.PP  # k-major K tail
+    assert gemm._variant(False, 1, 8192, 8192, 6304, False) == gemm.PP  # m/n-major tails are range-checked
+    assert gemm._variant(False, 4, 768, 768, 6304, False) == 2  # split-K weight gradient

@@ -18,6 +18,7 @@ def _require_ext(monkeypatch):
     ops.ext()
     # these tests exercise the hand-written kernels: no per-shape library choice
     monkeypatch.setattr(conv_ops, "_POLICY", "native")
+    monkeypatch.setattr(conv_ops, "_ONE_BY_ONE_GEMM", False)  # 1x1 shapes here test the implicit-GEMM kernels
 
 
 def _operands(N, C, H, W, O, k, seed, integer=False):

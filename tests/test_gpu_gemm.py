@@ -158,3 +158,51 @@ def test_gemm256_epilogue_bias_gelu_residual(monkeypatch):
     torch.testing.assert_close(z.float(), zref, atol=3e-2, rtol=8e-3)
     outb, _ = ops.gemm(a, b, bias=bias, gelu=True, residual=res, out_dtype=torch.bfloat16)
     torch.testing.assert_close(outb.float(), ref, atol=5e-2, rtol=1e-2)
+
+
+@pytest.mark.parametrize("a_kmajor,b_kmajor", [(True, True), (True, False), (False, True), (False, False)])
+@pytest.mark.parametrize("M,N,K", [(512, 512, 256), (296, 264, 128), (1000, 776, 448), (264, 520, 200)])
+def test_pingpong_gemm_layouts_vs_fp32(a_kmajor, b_kmajor, M, N, K):
+    """The ping-pong 256 x 256 kernel (variant bit 11): every layout, M / N tails (clamped rows),
+    odd K-tile counts, and (m/n-major only) a K tail through the buffer range check."""
+    from p2pfl_amd.ops.gemm import PP
+
+    if (a_kmajor or b_kmajor) and K % 64:
+        pytest.skip("k-major operands need K % 64 == 0 on this kernel")
+    if not a_kmajor and M % 8:
+        pytest.skip("m-major A needs M % 8 == 0")
+    a, b = _operands(M, N, K, a_kmajor, b_kmajor, seed=M + 3 * N + K)
+    out = torch.empty(M, N, device="cuda", dtype=torch.float32)
+    ops.ext().gemm(a, b, a_kmajor, b_kmajor, out, None, False, None, None, 1, PP)
+    ref, _ = ops.gemm_reference(a, b, a_kmajor, b_kmajor)
+    torch.testing.assert_close(out, ref, atol=2e-3, rtol=1e-4)
+
+
+def test_pingpong_gemm_epilogues_and_split_k():
+    """Bias + GELU (+ pre-activation) and residual epilogues, bf16 out; split-K reduced in the launch."""
+    from p2pfl_amd.ops.gemm import PP
+    from p2pfl_amd.ops.splitk import counters, tiles_of
+
+    C = ops.ext()
+    M, N, K = 6304, 3072, 768  # ViT-B/16 fc1: 300 tiles, the shape ops.gemm sends here
+    a, b = _operands(M, N, K, True, True, seed=11)
+    bias = torch.randn(N, device="cuda")
+    out = torch.empty(M, N, device="cuda", dtype=torch.bfloat16)
+    z = torch.empty_like(out)
+    C.gemm(a, b, True, True, out, bias, True, z, None, 1, PP)
+    ref, zr = ops.gemm_reference(a, b, True, True, bias, True)
+    torch.testing.assert_close(z.float(), zr, atol=0.25, rtol=1e-2)
+    torch.testing.assert_close(out.float(), ref, atol=0.25, rtol=1e-2)
+    res = torch.randn(M, 768, device="cuda").to(torch.bfloat16)
+    a2, b2 = _operands(M, 768, 768, True, True, seed=12)
+    out2 = torch.empty(M, 768, device="cuda", dtype=torch.bfloat16)
+    C.gemm(a2, b2, True, True, out2, bias[:768].contiguous(), False, None, res, 1, PP)
+    ref2, _ = ops.gemm_reference(a2, b2, True, True, bias[:768], False, res)
+    torch.testing.assert_close(out2.float(), ref2, atol=0.25, rtol=1e-2)
+    # weight-gradient shape: both operands m/n-major, K = 6304 tokens (tail), 3 slices
+    a3, b3 = _operands(768, 768, 6304, False, False, seed=13)
+    out3 = torch.empty(768, 768, device="cuda", dtype=torch.float32)
+    ws = torch.empty(3 * 768 * 768, device="cuda")
+    C.gemm(a3, b3, False, False, out3, None, False, None, None, 3, PP, ws, counters(tiles_of(768, 768), out3.device))
+    ref3, _ = ops.gemm_reference(a3, b3, False, False)
+    torch.testing.assert_close(out3, ref3, atol=5e-3, rtol=1e-4)
