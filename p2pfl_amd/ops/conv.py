@@ -241,7 +241,13 @@ def conv2d(x: torch.Tensor, conv: nn.Conv2d) -> torch.Tensor:
     1x1 convolutions as GEMMs (:func:`conv1x1_gemm`)."""
     if _is_1x1(x, conv):
         return conv1x1_gemm(x, conv)
-    if native_ok(x, conv) and _POLICY != "library" and (_POLICY == "native" or _native_faster(x, conv)):
+    # Inside a HIP-graph capture the implicit-GEMM kernels run whatever the
+    # eager timing preferred: MIOpen convolutions replayed from captured step
+    # graphs corrupted weights as soon as several learners' graphs and eager
+    # steps shared the device (profiles/r3_nan_root_cause.md); eager steps may
+    # still take MIOpen.
+    capturing = x.is_cuda and torch.cuda.is_current_stream_capturing()
+    if native_ok(x, conv) and _POLICY != "library" and (_POLICY == "native" or capturing or _native_faster(x, conv)):
         STATS["native_fwd"] += 1
         return _Conv2dNHWC.apply(x, conv.weight, _sym(conv.stride), _sym(conv.padding), _sym(conv.dilation))
     STATS["torch_fwd"] += 1
