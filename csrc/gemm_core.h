@@ -192,7 +192,7 @@ P2_DEVICE uint4 frag(const char* lds, int rb, int ks, int lane) {
   }
 }
 
-P2_DEVICE float gelu_f(float z) { return 0.5f * z * (1.f + erff(z * 0.70710678118654752f)); }
+P2_DEVICE float gelu_f(float z) { return 0.5f * z * (1.f + erf_fast(z * 0.70710678118654752f)); }
 
 // XCD-aware bijective remap of a linear workgroup id (blocks sharing an XCD get consecutive ids).
 P2_DEVICE int xcd_remap(int orig, int nwg) {
@@ -204,9 +204,35 @@ P2_DEVICE int xcd_remap(int orig, int nwg) {
 // 8-wave tile at least the whole bf16 output tile (padded rows), so its
 // epilogue stages C in one pass (132 KB; still one workgroup per CU).
 template <class CFG, int NBUF>
-constexpr int smem_bytes() {
+constexpr int smem_bytes() {  // NBUF: LDS stages of the K loop (1, 2, or a 3-5 stage ring)
   constexpr int pipe = NBUF * CFG::STAGE, epi = CFG::BM * (CFG::BN * 2 + 16);
   return (CFG::NT >= 512 && epi > pipe) ? epi : pipe;
+}
+
+// s_waitcnt vmcnt(LPT * n) for a runtime n in [0, MAXN] (the count must be an
+// immediate): waits until at most n K-tiles of LPT DMAs each are in flight.
+template <int LPT, int MAXN>
+P2_DEVICE void vmcnt_tiles(int n) {
+  static_assert(LPT * MAXN <= 63, "vmcnt is 6 bits");
+  if constexpr (MAXN >= 3) {
+    if (n >= 3) {
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(LPT * 3) : "memory");
+      return;
+    }
+  }
+  if constexpr (MAXN >= 2) {
+    if (n == 2) {
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(LPT * 2) : "memory");
+      return;
+    }
+  }
+  if constexpr (MAXN >= 1) {
+    if (n == 1) {
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(LPT) : "memory");
+      return;
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
 
 // The whole kernel body.  `p` carries M/N/K, split-K and the epilogue.
@@ -323,7 +349,27 @@ P2_DEVICE void gemm_body(const GemmParams& p, const LA& la, const LB& lb, int ti
       if (p.variant & 1) __builtin_amdgcn_s_setprio(0);
     }
   };
-  if constexpr (NBUF == 2) {
+  if constexpr (NBUF >= 3) {
+    // NBUF-stage ring for short-K, small-grid products (the CIFAR convolutions:
+    // one workgroup per CU, 9-72 K-tiles): NBUF - 1 K-tiles are in flight while
+    // one is consumed, so the HBM/L2 round trip is paid about once per
+    // NBUF - 1 tiles instead of once per tile.  One raw barrier per K-tile;
+    // the counted vmcnt retires exactly the tile read next (never vmcnt(0)
+    // until the tail); the buffer restaged at iteration it is the one read at
+    // it - 1, which every wave finished before passing this barrier.
+    constexpr int LPT = (HA / G + HB / G) * 4;  // DMAs per thread per K-tile
+    auto buf = [&](int t) { return smem + (t % NBUF) * CFG::STAGE; };
+    for (int j = 0; j < NBUF - 1 && j < nt; ++j) stage_all(kb + j * BK, buf(j));
+    for (int it = 0; it < nt; ++it) {
+      const int ahead = min(nt - it - 1, NBUF - 2);  // K-tiles allowed to stay in flight
+      vmcnt_tiles<LPT, NBUF - 2>(ahead);
+      __builtin_amdgcn_sched_barrier(0);
+      __builtin_amdgcn_s_barrier();
+      __builtin_amdgcn_sched_barrier(0);
+      if (it + NBUF - 1 < nt) stage_all(kb + (it + NBUF - 1) * BK, buf(it + NBUF - 1));
+      compute(buf(it), -1, smem);
+    }
+  } else if constexpr (NBUF == 2) {
     // Two K-tiles per iteration so both LDS buffers sit at constant offsets:
     // the compiler can then tell the DMA into one buffer from the ds_reads of
     // the other and does not drain the in-flight prefetch (vmcnt(0)) before
@@ -403,21 +449,66 @@ P2_DEVICE void gemm_body(const GemmParams& p, const LA& la, const LB& lb, int ti
       for (int j = 0; j < FN; ++j)
 #pragma unroll
         for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.f;
-    for (int s2 = 0; s2 < p.splits; ++s2) {
-      const float* base = slabs + s2 * mn;
+    // A tile wholly inside C (the common case) loads every group of a slice
+    // unconditionally: a per-group bounds test made hipcc branch around each
+    // load and wait for it (one memory round trip per group and slice -- 28 us
+    // of a 36 us 4-slice CIFAR convolution).  Two slices per iteration.
+    const bool full = m0 + CFG::BM <= p.M && n0 + CFG::BN <= p.N;
+    if (full && FM * FN <= 4) {
+      auto ld = [&](int s2, int i, int j, int g) __attribute__((always_inline)) {
+        return *reinterpret_cast<const f32x4*>(slabs + s2 * mn + int64_t(row_of(i)) * p.N + col_of(j, g));
+      };
+      int s2 = 0;
+      // two slices in flight need 128 more registers: only the <= 2-workgroup/CU schedules
+      for (; NBUF >= 2 && s2 + 2 <= p.splits; s2 += 2) {
+        f32x4 v0[FM][FN][4], v1[FM][FN][4];
 #pragma unroll
-      for (int i = 0; i < FM; ++i)
+        for (int i = 0; i < FM; ++i)
 #pragma unroll
-        for (int j = 0; j < FN; ++j)
+          for (int j = 0; j < FN; ++j)
 #pragma unroll
-          for (int g = 0; g < 4; ++g) {
-            const int m = row_of(i), n = col_of(j, g);
-            if (m < p.M && n < p.N) {
-              const f32x4 v = *reinterpret_cast<const f32x4*>(base + int64_t(m) * p.N + n);
+            for (int g = 0; g < 4; ++g) {
+              v0[i][j][g] = ld(s2, i, j, g);
+              v1[i][j][g] = ld(s2 + 1, i, j, g);
+            }
+#pragma unroll
+        for (int i = 0; i < FM; ++i)
+#pragma unroll
+          for (int j = 0; j < FN; ++j)
+#pragma unroll
+            for (int g = 0; g < 4; ++g)
+#pragma unroll
+              for (int e = 0; e < 4; ++e) acc[i][j][4 * g + e] += v0[i][j][g][e] + v1[i][j][g][e];
+      }
+      for (; s2 < p.splits; ++s2) {
+#pragma unroll
+        for (int i = 0; i < FM; ++i)
+#pragma unroll
+          for (int j = 0; j < FN; ++j)
+#pragma unroll
+            for (int g = 0; g < 4; ++g) {
+              const f32x4 v = ld(s2, i, j, g);
 #pragma unroll
               for (int e = 0; e < 4; ++e) acc[i][j][4 * g + e] += v[e];
             }
-          }
+      }
+    } else {
+      for (int s2 = 0; s2 < p.splits; ++s2) {
+        const float* base = slabs + s2 * mn;
+#pragma unroll
+        for (int i = 0; i < FM; ++i)
+#pragma unroll
+          for (int j = 0; j < FN; ++j)
+#pragma unroll
+            for (int g = 0; g < 4; ++g) {
+              const int m = row_of(i), n = col_of(j, g);
+              if (m < p.M && n < p.N) {
+                const f32x4 v = *reinterpret_cast<const f32x4*>(base + int64_t(m) * p.N + n);
+#pragma unroll
+                for (int e = 0; e < 4; ++e) acc[i][j][4 * g + e] += v[e];
+              }
+            }
+      }
     }
   }
   // bias, GELU (+ pre-activation, stored directly), residual: in place on acc

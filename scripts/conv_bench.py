@@ -1,4 +1,4 @@
-"""Time the implicit-GEMM convolutions against MIOpen (F.conv2d) on the ResNet-18 CIFAR shapes.
+"""Time the implicit-GEMM convolutions against MIOpen (F.conv2d) on the ResNet-18 CIFAR shapes (GPU time, host launch cost hidden).
 
     python scripts/conv_bench.py [--batch 32] [--out profiles/r2_conv_bench.md]
 
@@ -18,7 +18,14 @@ import torch  # noqa: E402
 
 from p2pfl_amd import ops  # noqa: E402
 from p2pfl_amd.ops.conv import _run_split, mn_splits, out_hw, wgrad_splits  # noqa: E402
-from scripts.gemm_bench import timeit  # noqa: E402
+from p2pfl_amd.ops.autotune import _time  # noqa: E402
+
+
+def timeit(fn, iters=30):
+    """GPU time per call in seconds: the stream is parked behind a spin kernel while
+    the calls are enqueued, so host launch cost (large for the library path) is
+    not measured -- as in a replayed HIP graph, where these kernels run."""
+    return _time(fn, iters) * 1e-3
 
 
 def main() -> None:
@@ -28,6 +35,7 @@ def main() -> None:
     ap.add_argument("--variants", default="10,10,2", help="csrc/gemm.h variant bits for fwd,dgrad,wgrad")
     args = ap.parse_args()
     C_ = ops.ext()
+    torch.backends.cudnn.benchmark = True  # MIOpen find mode, as the learner runs it
     vf, vd, vw = (int(v) for v in args.variants.split(","))
     N = args.batch
     bf = torch.bfloat16
