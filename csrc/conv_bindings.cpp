@@ -40,9 +40,13 @@ p2::ConvShape make_shape(int64_t N, int64_t H, int64_t W, int64_t C, int64_t O, 
 
 hipStream_t stream_of(const torch::Tensor& t) { return c10::hip::getCurrentHIPStream(t.device().index()).stream(); }
 
+// fp32 elements of one split-K slice: fragment-native 128 x 128 tiles (gemm_core.h SlabGeom)
+int64_t slab_elems(int64_t rows, int64_t cols) { return ((rows + 127) / 128) * ((cols + 127) / 128) * 128 * 128; }
+
 // Split-K configuration: without `counters`, splits > 1 writes fp32 slabs to the output
-// tensor itself; with `counters` (int32, one per 128 x 128 output tile, all zero) the slabs
-// go to `ws` (fp32, splits * rows * cols) and the launch reduces them itself.
+// tensor itself (reduce with tile_slab_reduce); with `counters` (int32, one per 128 x 128
+// output tile, all zero) the slabs go to `ws` (fp32, splits * slab_elems) and the launch
+// reduces them itself.
 p2::SplitK make_splitk(int64_t splits, const c10::optional<torch::Tensor>& ws, const c10::optional<torch::Tensor>& counters,
                        int64_t rows, int64_t cols, const torch::Tensor& like, const char* who) {
   TORCH_CHECK(splits >= 1 && splits <= 128, who, ": 1 <= splits <= 128");
@@ -57,9 +61,9 @@ p2::SplitK make_splitk(int64_t splits, const c10::optional<torch::Tensor>& ws, c
                 who, ": counters must be a contiguous int32 GPU tensor with >= ", tiles, " entries");
     TORCH_CHECK(ws.has_value() && ws->defined(), who, ": counters need a workspace");
     TORCH_CHECK(ws->is_cuda() && ws->scalar_type() == torch::kFloat32 && ws->is_contiguous() &&
-                    ws->numel() >= splits * rows * cols && reinterpret_cast<uintptr_t>(ws->data_ptr()) % 16 == 0 &&
+                    ws->numel() >= splits * slab_elems(rows, cols) && reinterpret_cast<uintptr_t>(ws->data_ptr()) % 16 == 0 &&
                     ws->device() == like.device(),
-                who, ": workspace must be contiguous fp32 with splits * rows * cols elements");
+                who, ": workspace must be contiguous fp32 with splits * slab_elems(rows, cols) elements");
     k.counters = counters->data_ptr<int>();
     k.ws = ws->data_ptr<float>();
   }
@@ -74,8 +78,9 @@ void check_out(const torch::Tensor& out, const p2::SplitK& k, int n, int h, int 
     TORCH_CHECK(out.size(0) == n && out.size(1) == h && out.size(2) == w && out.size(3) == c, who, ": out shape");
   } else {
     TORCH_CHECK(out.is_cuda() && out.scalar_type() == torch::kFloat32 && out.is_contiguous() &&
-                    out.numel() == int64_t(k.splits) * n * h * w * c && reinterpret_cast<uintptr_t>(out.data_ptr()) % 16 == 0,
-                who, ": split-K out must be contiguous fp32 with splits * rows * cols elements");
+                    out.numel() >= int64_t(k.splits) * slab_elems(int64_t(n) * h * w, c) &&
+                    reinterpret_cast<uintptr_t>(out.data_ptr()) % 16 == 0,
+                who, ": split-K out must be contiguous fp32 with splits * slab_elems(rows, cols) elements");
   }
 }
 
@@ -131,7 +136,8 @@ void conv_wgrad(torch::Tensor dy, torch::Tensor x, int64_t kh, int64_t kw, int64
   const auto k = make_splitk(splits, ws, counters, s.O, kh * kw * s.C, x, "conv_wgrad");
   int out_bf16 = 0;
   if (k.splits > 1 && !k.counters) {
-    TORCH_CHECK(out.scalar_type() == torch::kFloat32 && out.numel() == splits * n, "conv_wgrad: split-K out must be fp32 [splits, n]");
+    TORCH_CHECK(out.scalar_type() == torch::kFloat32 && out.is_contiguous() && out.numel() >= splits * slab_elems(s.O, kh * kw * s.C),
+                "conv_wgrad: split-K out must be contiguous fp32 with splits * slab_elems elements");
   } else {
     TORCH_CHECK(out.numel() == n && (out.scalar_type() == torch::kFloat32 || out.scalar_type() == torch::kBFloat16),
                 "conv_wgrad: out must be [O, kh, kw, C] bf16/fp32");

@@ -38,6 +38,10 @@ struct GemmParams {
 };
 
 void gemm_bf16(const GemmParams& p, hipStream_t s);
+// out[M][ldc] = sum of the `splits` fragment-native split-K slabs (gemm_core.h SlabGeom)
+// that a launch without counters wrote to `ws`; `variant` = that launch's (tile shape, order)
+void tile_slab_reduce(const float* ws, int splits, int M, int N, int64_t ldc, void* out, int out_bf16, int variant,
+                      hipStream_t s);
 // the ping-pong pipeline (gemm_pp.hip); gemm_bf16 routes variant bit 11 here
 bool gemm_pp_supported(const GemmParams& p);
 void gemm_bf16_pp(const GemmParams& p, hipStream_t s);

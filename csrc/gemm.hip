@@ -88,4 +88,20 @@ void gemm_bf16(const GemmParams& p, hipStream_t s) {
     launch(q, PlainMN{p.a, p.lda, p.M, p.K}, PlainMN{p.b, p.ldb, p.N, p.K}, s);
 }
 
+void tile_slab_reduce(const float* ws, int splits, int M, int N, int64_t ldc, void* out, int out_bf16, int variant,
+                      hipStream_t s) {
+  using namespace p2gemm;
+  if (variant & 64) {
+    const int tm = (M + 255) / 256, tn = (N + 255) / 256;
+    const int64_t groups = int64_t(tm) * tn * (256 * 256 / 4);
+    hipLaunchKernelGGL(tile_slab_reduce_kernel<Tile256>, dim3(int((groups + 255) / 256)), dim3(256), 0, s, ws, splits, M,
+                       N, ldc, out, out_bf16, variant, tm, tn);
+  } else {
+    const int tm = (M + 127) / 128, tn = (N + 127) / 128;
+    const int64_t groups = int64_t(tm) * tn * (128 * 128 / 4);
+    hipLaunchKernelGGL(tile_slab_reduce_kernel<Tile128>, dim3(int((groups + 255) / 256)), dim3(256), 0, s, ws, splits, M,
+                       N, ldc, out, out_bf16, variant, tm, tn);
+  }
+}
+
 }  // namespace p2

@@ -1,6 +1,8 @@
 // PyTorch bindings of the hand-written MFMA GEMM (p2pfl_amd._C.gemm).
 // Shapes, strides, dtypes and alignment are validated on the host before the
 // launch: a mismatched call is a Python exception, never a GPU fault.
+#include <algorithm>
+
 #include <torch/extension.h>
 #include <c10/core/DeviceGuard.h>
 #include <c10/hip/HIPStream.h>
@@ -8,6 +10,13 @@
 #include "gemm.h"
 
 namespace {
+
+// fp32 elements of one split-K slice: the fragment-native tiles of the kernel the
+// variant selects (gemm_core.h SlabGeom), or the ping-pong kernel's row-major M x N
+int64_t slab_elems(int64_t M, int64_t N, int64_t variant) {
+  const int64_t t = (variant & 64) ? 256 : 128;
+  return std::max(M * N, ((M + t - 1) / t) * ((N + t - 1) / t) * t * t);
+}
 
 void check_bf16_2d(const torch::Tensor& t, const char* name) {
   TORCH_CHECK(t.is_cuda() && t.scalar_type() == torch::kBFloat16, name, " must be a bf16 GPU tensor");
@@ -55,15 +64,15 @@ void gemm(torch::Tensor a, torch::Tensor b, bool a_kmajor, bool b_kmajor, torch:
                     counters->numel() >= tiles && counters->device() == a.device(),
                 "gemm: counters must be a contiguous int32 GPU tensor with one entry per 128x128 tile");
     TORCH_CHECK(ws.has_value() && ws->defined() && ws->is_cuda() && ws->scalar_type() == torch::kFloat32 &&
-                    ws->is_contiguous() && ws->numel() >= splits * M * N && ws->device() == a.device() &&
+                    ws->is_contiguous() && ws->numel() >= splits * slab_elems(M, N, variant) && ws->device() == a.device() &&
                     reinterpret_cast<uintptr_t>(ws->data_ptr()) % 16 == 0,
-                "gemm: split-K workspace must be contiguous fp32 with splits * M * N elements");
+                "gemm: split-K workspace must be contiguous fp32 with splits * slab_elems(M, N) elements");
     p.ws = ws->data_ptr<float>();
     p.counters = counters->data_ptr<int>();
   }
   if (splits > 1 && !in_launch) {
-    TORCH_CHECK(out.scalar_type() == torch::kFloat32 && out.is_contiguous() && out.numel() == splits * M * N,
-                "gemm: split-K output must be a contiguous fp32 [splits, M, N] tensor");
+    TORCH_CHECK(out.scalar_type() == torch::kFloat32 && out.is_contiguous() && out.numel() >= splits * slab_elems(M, N, variant),
+                "gemm: split-K output must be contiguous fp32 with splits * slab_elems(M, N) elements (reduce with tile_slab_reduce)");
     TORCH_CHECK(!bias.has_value() && !gelu && !residual.has_value(), "gemm: no epilogue with split-K");
     p.ldc = N;
   } else {
@@ -99,9 +108,28 @@ void gemm(torch::Tensor a, torch::Tensor b, bool a_kmajor, bool b_kmajor, torch:
   p2::gemm_bf16(p, c10::hip::getCurrentHIPStream().stream());
 }
 
+// C[M, N] (bf16 / fp32, contiguous) = sum of the `splits` fragment-native slabs in `ws`
+// written by a split-K gemm / conv launch without counters with this `variant`.
+void tile_slab_reduce(torch::Tensor ws, int64_t splits, int64_t M, int64_t N, torch::Tensor out, int64_t variant) {
+  TORCH_CHECK(ws.is_cuda() && ws.scalar_type() == torch::kFloat32 && ws.is_contiguous() &&
+                  ws.numel() >= splits * slab_elems(M, N, variant) && reinterpret_cast<uintptr_t>(ws.data_ptr()) % 16 == 0,
+              "tile_slab_reduce: ws must be contiguous fp32 with splits * slab_elems(M, N) elements");
+  TORCH_CHECK(!(variant & 2048), "tile_slab_reduce: the ping-pong kernel writes row-major slabs");
+  TORCH_CHECK(splits >= 1 && M >= 1 && N >= 8 && N % 4 == 0, "tile_slab_reduce: bad shape");
+  TORCH_CHECK(out.is_cuda() && out.is_contiguous() && out.numel() == M * N && out.device() == ws.device() &&
+                  (out.scalar_type() == torch::kFloat32 || out.scalar_type() == torch::kBFloat16) &&
+                  reinterpret_cast<uintptr_t>(out.data_ptr()) % 16 == 0,
+              "tile_slab_reduce: out must be contiguous fp32/bf16 with M * N elements");
+  const c10::DeviceGuard guard(ws.device());
+  p2::tile_slab_reduce(ws.data_ptr<float>(), int(splits), int(M), int(N), N, out.data_ptr(),
+                       out.scalar_type() == torch::kBFloat16, int(variant), c10::hip::getCurrentHIPStream().stream());
+}
+
 }  // namespace
 
 void register_gemm(pybind11::module& m) {
+  m.def("tile_slab_reduce", &tile_slab_reduce, "sum of fragment-native split-K slabs into C", pybind11::arg("ws"),
+        pybind11::arg("splits"), pybind11::arg("M"), pybind11::arg("N"), pybind11::arg("out"), pybind11::arg("variant"));
   m.def("gemm", &gemm, "bf16 MFMA GEMM with fused bias/GELU/residual epilogue and split-K",
         pybind11::arg("a"), pybind11::arg("b"), pybind11::arg("a_kmajor"), pybind11::arg("b_kmajor"),
         pybind11::arg("out"), pybind11::arg("bias") = pybind11::none(), pybind11::arg("gelu") = false,

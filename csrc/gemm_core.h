@@ -235,6 +235,33 @@ P2_DEVICE void vmcnt_tiles(int n) {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
 
+// Output tile (tm, tn) of linear tile index t (see the tile-order note in gemm_body).
+P2_DEVICE void tile_coords(int variant, int t, int tiles_m, int tiles_n, int& tm, int& tn) {
+  if (variant & 256) {
+    tm = (variant & 2) ? t / tiles_n : t % tiles_m;
+    tn = (variant & 2) ? t % tiles_n : t / tiles_m;
+  } else {
+    constexpr int GROUP_M = 8;
+    const int per_group = GROUP_M * tiles_n, g0 = (t / per_group) * GROUP_M;
+    const int gsize = min(tiles_m - g0, GROUP_M), r = t % per_group;
+    tm = g0 + r % gsize;
+    tn = r / gsize;
+  }
+}
+
+// Split-K partial tiles are stored fragment-native: slice s of tile t is one
+// contiguous block of TILEF = NT * FM * FN * 16 floats (= BM * BN), group q of
+// lane l of wave w at ((w * QN + q) * 64 + l) * 4 (QN = 4 FM FN groups per lane),
+// so every store / load instruction moves 1 KB contiguous (a row-major slab
+// scattered each wave's 16-byte groups over 32 rows).  Only the reducers read
+// this layout: the in-launch last arriver and tile_slab_reduce_kernel.
+template <class CFG>
+struct SlabGeom {
+  static constexpr int QN = CFG::FM * CFG::FN * 4;
+  static constexpr int TILEF = CFG::NT * CFG::FM * CFG::FN * 16;
+  static_assert(TILEF == CFG::BM * CFG::BN, "fragment slab covers the tile");
+};
+
 // The whole kernel body.  `p` carries M/N/K, split-K and the epilogue.
 template <class CFG, int NBUF, class LA, class LB>
 P2_DEVICE void gemm_body(const GemmParams& p, const LA& la, const LB& lb, int tiles_m, int tiles_n, char* smem) {
@@ -254,16 +281,7 @@ P2_DEVICE void gemm_body(const GemmParams& p, const LA& la, const LB& lb, int ti
   // L2 hit rate 48 % -> the bound on the K loop).  Variant bit 8: legacy
   // panel order, consecutive tiles sharing the B panel (bit 1: the A panel).
   int tm, tn;
-  if (p.variant & 256) {
-    tm = (p.variant & 2) ? t / tiles_n : t % tiles_m;
-    tn = (p.variant & 2) ? t % tiles_n : t / tiles_m;
-  } else {
-    constexpr int GROUP_M = 8;
-    const int per_group = GROUP_M * tiles_n, g0 = (t / per_group) * GROUP_M;
-    const int gsize = min(tiles_m - g0, GROUP_M), r = t % per_group;
-    tm = g0 + r % gsize;
-    tn = r / gsize;
-  }
+  tile_coords(p.variant, t, tiles_m, tiles_n, tm, tn);
   const int m0 = tm * CFG::BM, n0 = tn * CFG::BN;
   int kper = (p.K + p.splits - 1) / p.splits;
   kper = (kper + BK - 1) / BK * BK;
@@ -405,110 +423,82 @@ P2_DEVICE void gemm_body(const GemmParams& p, const LA& la, const LB& lb, int ti
   auto row_of = [&](int i) { return m0 + wm * 32 * FM + i * 32 + (lane & 31); };
   auto col_of = [&](int j, int g) { return n0 + wn * 32 * FN + j * 32 + 8 * g + 4 * h; };
   if (p.splits > 1) {
-    // every K-slice writes its raw fp32 partial tile (N % 8 == 0: a group is all in or all out)
+    // every K-slice writes its raw fp32 partial tile, fragment-native (SlabGeom)
+    using SG = SlabGeom<CFG>;
     float* slabs = p.counters ? p.ws : reinterpret_cast<float*>(p.c);
-    const int64_t mn = int64_t(p.M) * p.N;
+    const int tiles = tiles_m * tiles_n;
+    const uint32_t lane_off = uint32_t(((wave * SG::QN) * 64 + lane) * 16);
+    auto tile_rsrc = [&](int s) __attribute__((always_inline)) {
+      return __builtin_amdgcn_make_buffer_rsrc(slabs + (int64_t(s) * tiles + t) * SG::TILEF, 0, SG::TILEF * 4, 0x00020000);
+    };
+    {
+      const auto rs = tile_rsrc(split);
 #pragma unroll
-    for (int i = 0; i < FM; ++i)
+      for (int i = 0; i < FM; ++i)
 #pragma unroll
-      for (int j = 0; j < FN; ++j)
+        for (int j = 0; j < FN; ++j)
 #pragma unroll
-        for (int g = 0; g < 4; ++g) {
-          const int m = row_of(i), n = col_of(j, g);
-          if (m < p.M && n < p.N)
-            *reinterpret_cast<f32x4*>(slabs + split * mn + int64_t(m) * p.N + n) =
-                f32x4{acc[i][j][4 * g], acc[i][j][4 * g + 1], acc[i][j][4 * g + 2], acc[i][j][4 * g + 3]};
-        }
+          for (int g = 0; g < 4; ++g) {
+            const int q = (i * FN + j) * 4 + g;
+            const f32x4 v = {acc[i][j][4 * g], acc[i][j][4 * g + 1], acc[i][j][4 * g + 2], acc[i][j][4 * g + 3]};
+            // in-launch: sc1 (write-through) stores, so the hand-off needs no
+            // release fence (an agent release wrote back the whole L2 per slice)
+            if (p.counters)
+              __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), rs, lane_off + q * 1024, 0, 16);
+            else
+              __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), rs, lane_off + q * 1024, 0, 0);
+          }
+    }
     if (!p.counters) return;
     // In-launch reduction: the slice that arrives last at this tile's counter
-    // sums all slices' slabs and runs the epilogue (agent-scope release before
-    // the ticket, acquire after it; the counter is reset for the next launch,
-    // so the zero-initialised counter array is reusable).
+    // sums all slices' slabs and runs the epilogue.  Every wave drains its sc1
+    // stores, then one relaxed agent-scope ticket; the last arriver reads the
+    // slabs with sc1 loads (every one of them), so no acquire fence either.
+    // The counter is reset for the next launch.
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     int* flag = reinterpret_cast<int*>(smem);
     if (tid == 0) {
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       const int old = __hip_atomic_fetch_add(p.counters + t, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       flag[0] = old == p.splits - 1;
+      if (old == p.splits - 1) __hip_atomic_store(p.counters + t, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     __syncthreads();
     if (!flag[0]) return;
-    if (tid == 0) {
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __hip_atomic_store(p.counters + t, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-    __syncthreads();
-    // acc := sum of all slices (own slab included); the 16 groups of a lane are
-    // independent loads, so each slice costs one memory round trip
+    // acc := sum of all slices (own slab included), all groups of a slice in
+    // flight at once (two slices when the register budget allows)
 #pragma unroll
     for (int i = 0; i < FM; ++i)
 #pragma unroll
       for (int j = 0; j < FN; ++j)
 #pragma unroll
         for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.f;
-    // A tile wholly inside C (the common case) loads every group of a slice
-    // unconditionally: a per-group bounds test made hipcc branch around each
-    // load and wait for it (one memory round trip per group and slice -- 28 us
-    // of a 36 us 4-slice CIFAR convolution).  Two slices per iteration.
-    const bool full = m0 + CFG::BM <= p.M && n0 + CFG::BN <= p.N;
-    if (full && FM * FN <= 4) {
-      auto ld = [&](int s2, int i, int j, int g) __attribute__((always_inline)) {
-        return *reinterpret_cast<const f32x4*>(slabs + s2 * mn + int64_t(row_of(i)) * p.N + col_of(j, g));
-      };
-      int s2 = 0;
-      // two slices in flight need 128 more registers: only the <= 2-workgroup/CU schedules
-      for (; NBUF >= 2 && s2 + 2 <= p.splits; s2 += 2) {
-        f32x4 v0[FM][FN][4], v1[FM][FN][4];
+    auto ld = [&](const __amdgpu_buffer_rsrc_t& rs, int q) __attribute__((always_inline)) {
+      return __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, lane_off + q * 1024, 0, 16));
+    };
+    int s2 = 0;
+    for (; NBUF >= 2 && SG::QN <= 16 && s2 + 2 <= p.splits; s2 += 2) {
+      const auto r0 = tile_rsrc(s2), r1 = tile_rsrc(s2 + 1);
+      f32x4 v0[SG::QN], v1[SG::QN];
 #pragma unroll
-        for (int i = 0; i < FM; ++i)
-#pragma unroll
-          for (int j = 0; j < FN; ++j)
-#pragma unroll
-            for (int g = 0; g < 4; ++g) {
-              v0[i][j][g] = ld(s2, i, j, g);
-              v1[i][j][g] = ld(s2 + 1, i, j, g);
-            }
-#pragma unroll
-        for (int i = 0; i < FM; ++i)
-#pragma unroll
-          for (int j = 0; j < FN; ++j)
-#pragma unroll
-            for (int g = 0; g < 4; ++g)
-#pragma unroll
-              for (int e = 0; e < 4; ++e) acc[i][j][4 * g + e] += v0[i][j][g][e] + v1[i][j][g][e];
+      for (int q = 0; q < SG::QN; ++q) {
+        v0[q] = ld(r0, q);
+        v1[q] = ld(r1, q);
       }
-      for (; s2 < p.splits; ++s2) {
 #pragma unroll
-        for (int i = 0; i < FM; ++i)
+      for (int q = 0; q < SG::QN; ++q)
 #pragma unroll
-          for (int j = 0; j < FN; ++j)
+        for (int e = 0; e < 4; ++e) acc[q / (4 * FN)][(q / 4) % FN][4 * (q % 4) + e] += v0[q][e] + v1[q][e];
+    }
+    for (; s2 < p.splits; ++s2) {
+      const auto r0 = tile_rsrc(s2);
+      f32x4 v0[SG::QN];
 #pragma unroll
-            for (int g = 0; g < 4; ++g) {
-              const f32x4 v = ld(s2, i, j, g);
+      for (int q = 0; q < SG::QN; ++q) v0[q] = ld(r0, q);
 #pragma unroll
-              for (int e = 0; e < 4; ++e) acc[i][j][4 * g + e] += v[e];
-            }
-      }
-    } else {
-      for (int s2 = 0; s2 < p.splits; ++s2) {
-        const float* base = slabs + s2 * mn;
+      for (int q = 0; q < SG::QN; ++q)
 #pragma unroll
-        for (int i = 0; i < FM; ++i)
-#pragma unroll
-          for (int j = 0; j < FN; ++j)
-#pragma unroll
-            for (int g = 0; g < 4; ++g) {
-              const int m = row_of(i), n = col_of(j, g);
-              if (m < p.M && n < p.N) {
-                const f32x4 v = *reinterpret_cast<const f32x4*>(base + int64_t(m) * p.N + n);
-#pragma unroll
-                for (int e = 0; e < 4; ++e) acc[i][j][4 * g + e] += v[e];
-              }
-            }
-      }
+        for (int e = 0; e < 4; ++e) acc[q / (4 * FN)][(q / 4) % FN][4 * (q % 4) + e] += v0[q][e];
     }
   }
   // bias, GELU (+ pre-activation, stored directly), residual: in place on acc
@@ -586,6 +576,50 @@ P2_DEVICE void gemm_body(const GemmParams& p, const LA& la, const LB& lb, int ti
         *reinterpret_cast<uint4*>(reinterpret_cast<uint16_t*>(p.c) + int64_t(m) * p.ldc + n) =
             *reinterpret_cast<const uint4*>(smem + r * LROW + c * 16);
     }
+  }
+}
+
+// Reduce the fragment-native split-K slabs of a launch without counters
+// (`splits` slices of every tile) into C (bf16 or fp32, row stride ldc).  One
+// thread per 4-value group, spread over the whole chip (a workgroup per tile
+// left most CUs idle); consecutive threads read consecutive 16-byte groups of
+// each slice, four slices in flight.
+template <class CFG>
+__global__ __launch_bounds__(256) void tile_slab_reduce_kernel(const float* __restrict__ slabs, int splits, int M, int N,
+                                                               int64_t ldc, void* out, int out_bf16, int variant,
+                                                               int tiles_m, int tiles_n) {
+  using SG = SlabGeom<CFG>;
+  constexpr int FN = CFG::FN, FM = CFG::FM, GPT = SG::TILEF / 4;  // 4-value groups per tile
+  const int tiles = tiles_m * tiles_n;
+  const int64_t e = int64_t(blockIdx.x) * 256 + threadIdx.x;
+  if (e >= int64_t(tiles) * GPT) return;
+  const int t = int(e / GPT), r = int(e % GPT);
+  const int wave = r / (SG::QN * 64), q = (r / 64) % SG::QN, lane = r % 64;
+  const f32x4* src = reinterpret_cast<const f32x4*>(slabs) + e;
+  const int64_t stride = int64_t(tiles) * GPT;  // groups per slice
+  f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+  int s = 0;
+  for (; s + 4 <= splits; s += 4) {
+    f32x4 v[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) v[u] = src[(s + u) * stride];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) acc += v[u];
+  }
+  for (; s < splits; ++s) acc += src[s * stride];
+  int tm, tn;
+  tile_coords(variant, t, tiles_m, tiles_n, tm, tn);
+  const int wm = wave / CFG::WAVES_N, wn = wave % CFG::WAVES_N;
+  const int i = q / (4 * FN), j = (q / 4) % FN, g = q % 4;
+  const int m = tm * CFG::BM + wm * 32 * FM + i * 32 + (lane & 31);
+  const int n = tn * CFG::BN + wn * 32 * FN + j * 32 + 8 * g + 4 * (lane >> 5);
+  if (m < M && n < N) {
+    const int64_t off = int64_t(m) * ldc + n;
+    if (out_bf16)
+      *reinterpret_cast<uint2*>(reinterpret_cast<uint16_t*>(out) + off) =
+          uint2{pack_bf16x2(acc[0], acc[1]), pack_bf16x2(acc[2], acc[3])};
+    else
+      *reinterpret_cast<f32x4*>(reinterpret_cast<float*>(out) + off) = acc;
   }
 }
 

@@ -28,7 +28,7 @@ import torch.nn.functional as F
 from torch import nn
 
 from p2pfl_amd.ops import autotune
-from p2pfl_amd.ops.splitk import IN_LAUNCH_MAX_SPLITS, counters, tiles_of
+from p2pfl_amd.ops.splitk import counters, slab_elems, tiles_of
 
 # counters a test can read to prove the native path ran
 STATS = {"native_fwd": 0, "torch_fwd": 0, "gemm_1x1_fwd": 0}
@@ -78,18 +78,27 @@ def mn_splits(M: int, N: int, K: int) -> int:
     return s
 
 
-def _run_split(launch, rows: int, cols: int, s: int, out: torch.Tensor) -> None:
+# Convolutions reduce their split-K slabs with the chip-wide tile_slab_reduce
+# launch even at 2-4 slices: measured faster than the in-launch last-arriver
+# reduction on every CIFAR ResNet-18 shape (e.g. 128x16x16 forward, 4 slices:
+# 19.5 vs 22.7 us; profiles/r3_conv_native.md).  The in-launch path (needed by
+# GEMMs with a fused epilogue) stays available: P2PFL_CONV_IN_LAUNCH_SPLITS=4.
+_CONV_IN_LAUNCH_MAX_SPLITS = int(os.environ.get("P2PFL_CONV_IN_LAUNCH_SPLITS", "1"))
+
+
+def _run_split(launch, rows: int, cols: int, s: int, out: torch.Tensor, variant: int = 0) -> None:
     """``launch(target, splits, ws, counters)`` producing ``out``: directly, split-K reduced
-    in the launch, or split-K into fp32 slabs reduced by one ``slab_sum``."""
+    in the launch, or split-K into fp32 slabs (fragment-native tiles) reduced by one
+    ``tile_slab_reduce`` launch (``variant``: the launch's tile order)."""
     if s == 1:
         launch(out, 1, None, None)
         return
-    ws = torch.empty(s * rows * cols, dtype=torch.float32, device=out.device)
-    if s <= IN_LAUNCH_MAX_SPLITS:
+    ws = torch.empty(s * slab_elems(rows, cols), dtype=torch.float32, device=out.device)
+    if s <= _CONV_IN_LAUNCH_MAX_SPLITS:
         launch(out, s, ws, counters(tiles_of(rows, cols), out.device))
         return
     launch(ws, s, None, None)
-    _C().slab_sum(ws.view(s, rows * cols), out.view(-1))
+    _C().tile_slab_reduce(ws, s, rows, cols, out.view(rows, cols), variant)
 
 
 def native_ok(x: torch.Tensor, conv: nn.Conv2d) -> bool:
@@ -129,7 +138,7 @@ class _Conv2dNHWC(torch.autograd.Function):
         rows = N * OH * OW
         _run_split(
             lambda o, s, ws, cnt: _C().conv_fwd(x4, w4, stride, pad, dil, o, s, _V_FWD, ws, cnt),
-            rows, O, mn_splits(rows, O, kh * kw * C), y4,
+            rows, O, mn_splits(rows, O, kh * kw * C), y4, _V_FWD,
         )
         ctx.save_for_backward(x4, w)
         ctx.cfg = (stride, pad, dil)
@@ -154,7 +163,7 @@ class _Conv2dNHWC(torch.autograd.Function):
             rows = shape[0] * shape[1] * shape[2]
             _run_split(
                 lambda o, s, ws, cnt: C.conv_dgrad(dy4, w4, stride, pad, dil, o, shape, s, _V_DGRAD, ws, cnt),
-                rows, shape[3], mn_splits(rows, shape[3], kh * kw * O), dx4,
+                rows, shape[3], mn_splits(rows, shape[3], kh * kw * O), dx4, _V_DGRAD,
             )
             dx = dx4.permute(0, 3, 1, 2)
         if ctx.needs_input_grad[1]:
@@ -163,7 +172,7 @@ class _Conv2dNHWC(torch.autograd.Function):
             dw4 = torch.empty((O, kh, kw, Cin), dtype=w.dtype, device=w.device)
             _run_split(
                 lambda o, s, ws, cnt: C.conv_wgrad(dy4, x4, kh, kw, stride, pad, dil, o, s, _V_WGRAD, ws, cnt),
-                O, kh * kw * Cin, wgrad_splits(O, kh * kw * Cin, npix), dw4,
+                O, kh * kw * Cin, wgrad_splits(O, kh * kw * Cin, npix), dw4, _V_WGRAD,
             )
             dw = dw4.permute(0, 3, 1, 2)
         return dx, dw, None, None, None

@@ -23,7 +23,7 @@ import torch
 import torch.nn.functional as F
 
 from p2pfl_amd.ops import autotune
-from p2pfl_amd.ops.splitk import IN_LAUNCH_MAX_SPLITS, counters, tiles_of
+from p2pfl_amd.ops.splitk import IN_LAUNCH_MAX_SPLITS, counters, slab_elems, tiles_of
 
 
 def _C():
@@ -133,15 +133,18 @@ def gemm(
         if out is None:
             out = torch.empty((M, N), dtype=out_dtype, device=dev)
         z = torch.empty((M, N), dtype=torch.bfloat16, device=dev) if (gelu and want_z) else None
-        ws = torch.empty(splits * M * N, dtype=torch.float32, device=dev)
         v = _variant(a_kmajor, splits)
+        ws = torch.empty(splits * slab_elems(M, N, v), dtype=torch.float32, device=dev)
         if splits <= IN_LAUNCH_MAX_SPLITS:  # the last slice of each tile reduces it in the launch
             _C().gemm(a, b, a_kmajor, b_kmajor, out, bias, gelu, z, residual, splits, v, ws, counters(tiles_of(M, N), dev))
             return out, z
         if bias is not None or gelu or residual is not None:
             raise ValueError("a split-K GEMM with more than 4 slices has no epilogue")
         _C().gemm(a, b, a_kmajor, b_kmajor, ws, None, False, None, None, splits, v)
-        _C().slab_sum(ws.view(splits, M * N), out.view(-1))
+        if v & PP:  # the ping-pong kernel writes row-major slabs
+            _C().slab_sum(ws[: splits * M * N].view(splits, M * N), out.view(-1))
+        else:
+            _C().tile_slab_reduce(ws, splits, M, N, out, v)
         return out, z
     if out is None:
         out = torch.empty((M, N), dtype=out_dtype, device=dev)

@@ -65,9 +65,9 @@ def main() -> None:
         dw4 = torch.empty(O, k, k, C, device="cuda", dtype=bf)
         sf, sd, sw = mn_splits(N * OH * OW, O, k * k * C), mn_splits(N * H * H, C, k * k * O), wgrad_splits(O, k * k * C, N * OH * OW)
         mine = [
-            timeit(lambda: _run_split(lambda o, sp, ws, cnt: C_.conv_fwd(x4, w4, s, p, 1, o, sp, vf, ws, cnt), N * OH * OW, O, sf, y4)),
-            timeit(lambda: _run_split(lambda o, sp, ws, cnt: C_.conv_dgrad(dy4, w4, s, p, 1, o, [N, H, H, C], sp, vd, ws, cnt), N * H * H, C, sd, dx4)),
-            timeit(lambda: _run_split(lambda o, sp, ws, cnt: C_.conv_wgrad(dy4, x4, k, k, s, p, 1, o, sp, vw, ws, cnt), O, k * k * C, sw, dw4)),
+            timeit(lambda: _run_split(lambda o, sp, ws, cnt: C_.conv_fwd(x4, w4, s, p, 1, o, sp, vf, ws, cnt), N * OH * OW, O, sf, y4, vf)),
+            timeit(lambda: _run_split(lambda o, sp, ws, cnt: C_.conv_dgrad(dy4, w4, s, p, 1, o, [N, H, H, C], sp, vd, ws, cnt), N * H * H, C, sd, dx4, vd)),
+            timeit(lambda: _run_split(lambda o, sp, ws, cnt: C_.conv_wgrad(dy4, x4, k, k, s, p, 1, o, sp, vw, ws, cnt), O, k * k * C, sw, dw4, vw)),
         ]
         xr = x.clone().requires_grad_()
         wr = w.clone().requires_grad_()

@@ -19,7 +19,7 @@ bf = torch.bfloat16
 N = 32
 probes = [(2, "v2"), (2 | 16, "no stores"), (2 | 32, "no K loop"), (2 | 128, "no DMA after prologue"),
           (2 | 32 | 16, "no K loop, no stores"), (4096, "4-stage ring"), (10, "v10 (1 buf)")]
-print("| conv fwd | " + " | ".join(n for _, n in probes) + " | v2, split via slab_sum | v2 splits 1 | v2 splits 2 | MIOpen (find) |")
+print("| conv fwd | " + " | ".join(n for _, n in probes) + " | v2, in-launch reduction (<= 4 slices) | v2 splits 1 | v2 splits 2 | MIOpen (find) |")
 print("|---|" + "---:|" * (len(probes) + 4))
 for name, C, H, O, k, s, p in [("l1 64x32x32 3x3", 64, 32, 64, 3, 1, 1), ("l2 128x16x16 3x3", 128, 16, 128, 3, 1, 1),
                                ("l3 256x8x8 3x3", 256, 8, 256, 3, 1, 1), ("l4 512x4x4 3x3", 512, 4, 512, 3, 1, 1),
@@ -32,17 +32,17 @@ for name, C, H, O, k, s, p in [("l1 64x32x32 3x3", 64, 32, 64, 3, 1, 1), ("l2 12
     sf = mn_splits(N * OH * OW, O, k * k * C)
     row = []
     for v, _ in probes:
-        t = _time(lambda: _run_split(lambda o, sp, ws, cnt: C_.conv_fwd(x4, w4, s, p, 1, o, sp, v, ws, cnt), N * OH * OW, O, sf, y4), 30)
+        t = _time(lambda: _run_split(lambda o, sp, ws, cnt: C_.conv_fwd(x4, w4, s, p, 1, o, sp, v, ws, cnt), N * OH * OW, O, sf, y4, v), 30)
         row.append(f"{t * 1e3:.1f}")
     import p2pfl_amd.ops.conv as conv_mod
 
-    keep = conv_mod.IN_LAUNCH_MAX_SPLITS
-    conv_mod.IN_LAUNCH_MAX_SPLITS = 1  # split-K through raw slabs + the slab_sum kernel
-    t = _time(lambda: conv_mod._run_split(lambda o, sp, ws, cnt: C_.conv_fwd(x4, w4, s, p, 1, o, sp, 2, ws, cnt), N * OH * OW, O, sf, y4), 30)
-    conv_mod.IN_LAUNCH_MAX_SPLITS = keep
+    keep = conv_mod._CONV_IN_LAUNCH_MAX_SPLITS
+    conv_mod._CONV_IN_LAUNCH_MAX_SPLITS = 4  # split-K reduced by the last-arriving slice (<= 4 slices)
+    t = _time(lambda: conv_mod._run_split(lambda o, sp, ws, cnt: C_.conv_fwd(x4, w4, s, p, 1, o, sp, 2, ws, cnt), N * OH * OW, O, sf, y4, 2), 30)
+    conv_mod._CONV_IN_LAUNCH_MAX_SPLITS = keep
     row.append(f"{t * 1e3:.1f}")
     for s1 in (1, 2):
-        t = _time(lambda: conv_mod._run_split(lambda o, sp, ws, cnt: C_.conv_fwd(x4, w4, s, p, 1, o, sp, 2, ws, cnt), N * OH * OW, O, s1, y4), 30)
+        t = _time(lambda: conv_mod._run_split(lambda o, sp, ws, cnt: C_.conv_fwd(x4, w4, s, p, 1, o, sp, 2, ws, cnt), N * OH * OW, O, s1, y4, 2), 30)
         row.append(f"{t * 1e3:.1f}")
     t = _time(lambda: torch.nn.functional.conv2d(x, w, None, s, p), 30)
     row.append(f"{t * 1e3:.1f}")

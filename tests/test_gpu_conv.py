@@ -88,30 +88,39 @@ def test_conv_autograd_vs_fp32(N, C, H, W, O, k, s, p, d):
 def test_conv_fwd_dgrad_split_k(splits):
     N, C, H, W, O, k = 2, 128, 4, 4, 256, 3
     x, w = _operands(N, C, H, W, O, k, seed=splits, integer=True)
+    from p2pfl_amd.ops.splitk import slab_elems
+
+    C_ = ops.ext()
     x4, w4 = x.permute(0, 2, 3, 1), w.permute(0, 2, 3, 1)
-    slabs = torch.empty(splits, N * H * W * O, device="cuda")
-    ops.ext().conv_fwd(x4, w4, 1, 1, 1, slabs, splits)
+    rows = N * H * W
+    # raw fragment-native slabs (no counters), summed by tile_slab_reduce with the launch's variant
+    slabs = torch.empty(splits * slab_elems(rows, O), device="cuda")
+    C_.conv_fwd(x4, w4, 1, 1, 1, slabs, splits)
+    y = torch.empty(rows, O, device="cuda")
+    C_.tile_slab_reduce(slabs, splits, rows, O, y, 10)
     ref = _ref(x, w, 1, 1, 1)
-    torch.testing.assert_close(slabs.sum(0).view(N, H, W, O).permute(0, 3, 1, 2), ref, atol=0, rtol=0)
+    torch.testing.assert_close(y.view(N, H, W, O).permute(0, 3, 1, 2), ref, atol=0, rtol=0)
     dy = torch.randint(-2, 3, (N, O, H, W), device="cuda").to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
-    slabs = torch.empty(splits, N * H * W * C, device="cuda")
-    ops.ext().conv_dgrad(dy.permute(0, 2, 3, 1), w4, 1, 1, 1, slabs, [N, H, W, C], splits)
+    slabs = torch.empty(splits * slab_elems(rows, C), device="cuda")
+    C_.conv_dgrad(dy.permute(0, 2, 3, 1), w4, 1, 1, 1, slabs, [N, H, W, C], splits)
+    dx = torch.empty(rows, C, device="cuda")
+    C_.tile_slab_reduce(slabs, splits, rows, C, dx, 10)
     xr = x.float().requires_grad_()
     _ref(xr, w, 1, 1, 1).backward(dy.float())
-    torch.testing.assert_close(slabs.sum(0).view(N, H, W, C).permute(0, 3, 1, 2), xr.grad, atol=0, rtol=0)
+    torch.testing.assert_close(dx.view(N, H, W, C).permute(0, 3, 1, 2), xr.grad, atol=0, rtol=0)
 
 
 @pytest.mark.parametrize("splits", [2, 8, 32])
 def test_conv_split_k_in_launch_reduction(splits):
     """Split-K reduced by the last-arriving slice: equals the slab sum, and the counters end at zero."""
-    from p2pfl_amd.ops.splitk import tiles_of
+    from p2pfl_amd.ops.splitk import slab_elems, tiles_of
 
     N, C, H, W, O, k = 4, 128, 8, 8, 256, 3
     x, w = _operands(N, C, H, W, O, k, seed=3 * splits, integer=True)
     x4, w4 = x.permute(0, 2, 3, 1), w.permute(0, 2, 3, 1)
     rows = N * H * W
     cnt = torch.zeros(tiles_of(rows, O), dtype=torch.int32, device="cuda")
-    ws = torch.empty(splits * rows * O, device="cuda")
+    ws = torch.empty(splits * slab_elems(rows, max(O, C)), device="cuda")
     y4 = torch.empty(N, H, W, O, device="cuda", dtype=torch.bfloat16)
     for _ in range(3):  # counters are reusable launch after launch
         ops.ext().conv_fwd(x4, w4, 1, 1, 1, y4, splits, 10, ws, cnt)
@@ -128,7 +137,7 @@ def test_conv_split_k_in_launch_reduction(splits):
     torch.testing.assert_close(dx4.permute(0, 3, 1, 2).float(), xr.grad.to(torch.bfloat16).float(), atol=0, rtol=0)
     dw4 = torch.empty(O, k, k, C, device="cuda", dtype=torch.float32)
     cnt = torch.zeros(tiles_of(O, k * k * C), dtype=torch.int32, device="cuda")
-    ws = torch.empty(splits * O * k * k * C, device="cuda")
+    ws = torch.empty(splits * slab_elems(O, k * k * C), device="cuda")
     ops.ext().conv_wgrad(dy.permute(0, 2, 3, 1), x4, k, k, 1, 1, 1, dw4, splits, 2, ws, cnt)
     torch.testing.assert_close(dw4, wr.grad.permute(0, 2, 3, 1), atol=0, rtol=0)
     assert int(cnt.abs().sum()) == 0
@@ -139,10 +148,16 @@ def test_conv_wgrad_split_k(splits):
     N, C, H, W, O, k = 8, 64, 16, 16, 64, 3
     x, w = _operands(N, C, H, W, O, k, seed=splits)
     dy = torch.randn(N, O, H, W, device="cuda").to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    from p2pfl_amd.ops.splitk import slab_elems
+
     n = O * k * k * C
-    out = torch.empty((splits, n) if splits > 1 else (O, k, k, C), dtype=torch.float32, device="cuda")
+    out = torch.empty((splits * slab_elems(O, k * k * C),) if splits > 1 else (O, k, k, C), dtype=torch.float32, device="cuda")
     ops.ext().conv_wgrad(dy.permute(0, 2, 3, 1), x.permute(0, 2, 3, 1), k, k, 1, 1, 1, out, splits)
-    dw = out.sum(0) if splits > 1 else out.view(-1)
+    if splits > 1:
+        dw = torch.empty(O, k * k * C, device="cuda")
+        ops.ext().tile_slab_reduce(out, splits, O, k * k * C, dw, 2)
+    else:
+        dw = out.view(-1)
     xr = x.float().requires_grad_()
     wr = w.float().requires_grad_()
     _ref(xr, wr, 1, 1, 1).backward(dy.float())
