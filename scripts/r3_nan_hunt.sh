@@ -9,7 +9,7 @@ mkdir -p "$ROOT/gpurun_out/nan"
 export TMPDIR=/tmp P2PFL_CHECK_FINITE=1 P2PFL_LOCKCHECK=0 PYTHONPATH="$ROOT"
 TAG=$1; shift
 cd /tmp
-timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$ROOT/gpurun_out/nan/prof_$TAG" -o run -- \
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$ROOT/gpurun_out/nan/prof_$TAG" -o run -- \
   python3 -u -m p2pfl_amd.examples.fault_tolerance "$@" 2>&1 | grep --line-buffered -v "duplicate kernel symbol" \
   | tee "$ROOT/gpurun_out/nan/run_$TAG.log" | grep --line-buffered -E "non_finite|non-finite|fault_tolerance|round_ms|Error" 
 st=("${PIPESTATUS[@]}")
