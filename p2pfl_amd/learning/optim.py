@@ -224,6 +224,11 @@ class _MTOptimizer:
         for t in self.state_tensors():
             t.zero_()
 
+    def graph_first_step_ok(self) -> bool:
+        """Whether ``step_graph`` on freshly reset state equals the eager first step
+        (so a fit can replay its captured graph from step 0)."""
+        return True
+
     def zero_grad(self, set_to_none: bool = True) -> None:
         # always None: autograd then hands over each new gradient without a
         # zero-fill + accumulate kernel per parameter
@@ -288,8 +293,13 @@ class MTSGD(_MTOptimizer):
             nesterov=self.nesterov, first_step=self.t == 1, p_bf16=self.arena.shadow,
         )
 
+    def graph_first_step_ok(self) -> bool:
+        # eager step 1 seeds buf = g; the graph step computes buf = m * buf + (1 - dampening) g,
+        # which on the zeroed buffer of a reset optimizer is exactly g when dampening == 0
+        return self.buf is None or self.dampening == 0
+
     def step_graph(self, gtab: torch.Tensor) -> None:
-        """Graph-capturable step for t >= 2 (the first step, which seeds the momentum buffer, runs eagerly)."""
+        """Graph-capturable step (momentum buffer already seeded, or zero with dampening 0)."""
         ops.sgd_mt_step(
             self.arena.flat, self.buf, [], self.mt,
             lr=self.lr, momentum=self.momentum, dampening=self.dampening, weight_decay=self.weight_decay,

@@ -415,14 +415,18 @@ class TorchLearner(NodeLearner):
             if self._interrupt.is_set():
                 return False
             idx = perm[s : s + B]
-            if idx.numel() == B and opt.t >= 1:
+            # every full batch replays the graph, the fit's first one too when the optimizer's
+            # graph step on its reset state equals the eager first step (Adam; SGD without
+            # dampening): no eager step -- ~200 host-side launches -- per fit
+            first_ok = opt.t >= 1 or (hasattr(opt, "graph_first_step_ok") and opt.graph_first_step_ok())
+            if idx.numel() == B and first_ok:
                 sg = self._step_graph
                 if sg is None or sg.key != key:
                     sg = self._step_graph = TrainStepGraph(self, opt, loader)
                     sg.capture(idx)  # takes the gate exclusively
                 with self._gate():
                     logged = {"train_loss": sg.run(idx)}
-            else:  # first step (seeds optimizer state) and a short last batch
+            else:  # first step when it must seed optimizer state eagerly, and a short last batch
                 with self._gate():
                     x = loader.x.index_select(0, idx)
                     if loader.normalize:

@@ -56,7 +56,7 @@ def test_step_graph_matches_eager(name):
     make = {"sgd_net": _SGDNet, "vit_tiny": lambda: ViT_Tiny(seed=0)}[name]
     eager, graph = _pair(make)
     assert graph.mixed and eager.mixed
-    assert len(graph.data.train_dataloader().dataset) > 2 * 32  # first step eager, then replays
+    assert len(graph.data.train_dataloader().dataset) > 2 * 32  # several full batches replayed (the first too: dampening 0)
     for _round in range(2):  # the second fit reuses the captured graph after an optimizer reset
         eager.fit()
         graph.fit()
