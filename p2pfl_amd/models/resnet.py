@@ -7,17 +7,23 @@ without max-pool for 32x32 inputs, ``stem="imagenet"`` the 7x7/stride-2 stem
 plus max-pool.  Inputs are uint8 images (the data modules keep datasets as
 uint8 on the device); normalisation to [0, 1] happens in ``forward``.
 
-Activations run channels-last on the GPU.  Every convolution but the
-3-channel stem goes through :func:`~p2pfl_amd.ops.conv.conv2d`, which has two
-implementations per shape: the hand-written implicit-GEMM MFMA kernels
-(``csrc/conv.hip``: forward, input and weight gradient, reading the learner's
-channels-last bf16 weight shadow) and MIOpen.  By default
-(:mod:`~p2pfl_amd.ops.autotune`) both are timed once per shape on the GPU and
-the faster one runs; on the CIFAR ResNet-18 shapes at batch 32 MIOpen is
-still faster on most of them (``BASELINE.md``), so most convolutions run in
-MIOpen.  ``P2PFL_NATIVE_CONV=1`` forces the native kernels everywhere; the
-stem (and any shape the native kernels do not take) always uses ``F.conv2d``.  Every
-``BatchNorm2d -> (+ shortcut) -> ReLU`` chain runs as the fused HIP kernel of
+Activations run channels-last on the GPU.  What runs per convolution
+(:func:`~p2pfl_amd.ops.conv.conv2d`):
+
+* 1x1 convolutions (bottlenecks, downsample shortcuts) are GEMMs over the
+  channels-last pixels (:func:`~p2pfl_amd.ops.conv.conv1x1_gemm` ->
+  :func:`~p2pfl_amd.ops.gemm.linear`: the hand-written MFMA GEMM or hipBLASLt,
+  whichever measured faster for the shape);
+* every other convolution but the 3-channel stem, inside the captured HIP step
+  graphs (all full-batch training and evaluation steps), runs on the
+  hand-written implicit-GEMM MFMA kernels (``csrc/conv.hip``: forward, input and
+  weight gradient, reading the learner's channels-last bf16 weight shadow) --
+  MIOpen convolutions replayed from graphs were not memory-safe
+  (``profiles/r3_nan_root_cause.md``); eager steps (short last batches) take
+  whichever of the native kernels and MIOpen measured faster;
+* the stem uses ``F.conv2d`` (MIOpen).
+
+Every ``BatchNorm2d -> (+ shortcut) -> ReLU`` chain runs as the fused HIP kernel of
 ``csrc/batchnorm.hip`` (:func:`~p2pfl_amd.ops.batchnorm.batch_norm_act`).  Optimiser: SGD with momentum 0.9 and weight decay 5e-4 (fused
 into one arena kernel by the learner), a standard federated CIFAR setup.
 """
