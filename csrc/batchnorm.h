@@ -14,15 +14,20 @@ struct BnPlan {
   int tpr, rp, gx, S;
 };
 BnPlan bn_plan(int M, int C);
+// Plan of the statistics + finalize kernels (one launch instead of two; bf16,
+// C <= 2048, S * C <= 16384): S == 0 when the shape is not eligible.
+BnPlan bn_fused_plan(int M, int C);
 
 // Training forward: batch statistics (biased variance, shifted sums), running
 // stats update (unbiased variance, PyTorch momentum convention), then
 //   y = act((x - mean) * scale + b [+ res])      scale = w * rstd
 // part: [2, S, C] fp32; coef: [3, C] fp32 scratch; mean / rstd: [C] (saved for backward).
-// run_mean / run_var / nbt may be null (no running statistics).
+// run_mean / run_var / nbt may be null (no running statistics).  ctr: a zeroed
+// int (left zero) enabling the statistics + finalize kernel when bn_fused_plan
+// allows it (part then needs [2, fused S, C]); null keeps the separate launches.
 void bn_fwd_train(bool bf16, const void* x, const void* res, const float* w, const float* b, float* run_mean,
                   float* run_var, int64_t* nbt, float momentum, float eps, void* y, float* mean, float* rstd,
-                  float* coef, float* part, int M, int C, bool relu, hipStream_t s);
+                  float* coef, float* part, int* ctr, int M, int C, bool relu, hipStream_t s);
 
 // Inference forward with running statistics (one launch; coef unused, kept for
 // the call signature).  w, b, run_mean, run_var must be 16-byte aligned.
@@ -33,9 +38,9 @@ void bn_fwd_eval(bool bf16, const void* x, const void* res, const float* w, cons
 //   dz = relu ? dy * (y > 0) : dy
 //   db = sum dz, dw = rstd * sum dz (x - mean)
 //   dx = w rstd (dz - db / M - xhat dw / M);   dres = dz (if dres != null)
-// part: [2, S, C]; coef: [3, C] scratch.
+// part: [2, S, C]; coef: [3, C] scratch; ctr as bn_fwd_train.
 void bn_bwd(bool bf16, const void* dy, const void* y, const void* x, const float* w, const float* mean,
-            const float* rstd, void* dx, void* dres, float* dw, float* db, float* coef, float* part, int M, int C,
-            bool relu, hipStream_t s);
+            const float* rstd, void* dx, void* dres, float* dw, float* db, float* coef, float* part, int* ctr, int M,
+            int C, bool relu, hipStream_t s);
 
 }  // namespace p2bn

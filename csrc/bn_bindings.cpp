@@ -30,6 +30,21 @@ float* opt_f32(const c10::optional<torch::Tensor>& t, int64_t C, const torch::Te
   return f32(*t, C, x, name);
 }
 
+// zeroed int32 arrival counter of the statistics + finalize kernels (ops/splitk.py ring), or null
+int* opt_ctr(const c10::optional<torch::Tensor>& t, const torch::Tensor& x) {
+  if (!t.has_value() || !t->defined()) return nullptr;
+  TORCH_CHECK(t->device() == x.device() && t->scalar_type() == torch::kInt32 && t->numel() >= 1,
+              "counters must be a zeroed int32 tensor on x's device");
+  return t->data_ptr<int>();
+}
+
+// partial rows for whichever kernel runs
+int64_t part_rows(int64_t M, int64_t C, bool fused) {
+  const auto p = p2bn::bn_plan(int(M), int(C));
+  const auto f = p2bn::bn_fused_plan(int(M), int(C));
+  return fused && f.S > p.S ? f.S : p.S;
+}
+
 void check_shape(const torch::Tensor& x) {
   TORCH_CHECK(x.dim() == 2, "x must be [M, C]");
   const int64_t M = x.size(0), C = x.size(1);
@@ -43,7 +58,7 @@ std::vector<torch::Tensor> bn_fwd_train(torch::Tensor x, torch::Tensor w, torch:
                                         c10::optional<torch::Tensor> running_mean,
                                         c10::optional<torch::Tensor> running_var,
                                         c10::optional<torch::Tensor> num_batches_tracked, double momentum, double eps,
-                                        bool relu) {
+                                        bool relu, c10::optional<torch::Tensor> counters) {
   const c10::DeviceGuard g(x.device());
   check_shape(x);
   const int64_t M = x.size(0), C = x.size(1);
@@ -66,11 +81,11 @@ std::vector<torch::Tensor> bn_fwd_train(torch::Tensor x, torch::Tensor w, torch:
   auto y = torch::empty_like(x);
   auto opt = x.options().dtype(torch::kFloat32);
   auto mean = torch::empty({C}, opt), rstd = torch::empty({C}, opt), coef = torch::empty({3, C}, opt);
-  const auto plan = p2bn::bn_plan(int(M), int(C));
-  auto part = torch::empty({2, plan.S, C}, opt);
+  int* ctr = opt_ctr(counters, x);
+  auto part = torch::empty({2, part_rows(M, C, ctr != nullptr), C}, opt);
   p2bn::bn_fwd_train(bf, x.data_ptr(), rp, f32(w, C, x, "weight"), f32(b, C, x, "bias"), rm, rv, nbt, float(momentum),
                      float(eps), y.data_ptr(), mean.data_ptr<float>(), rstd.data_ptr<float>(), coef.data_ptr<float>(),
-                     part.data_ptr<float>(), int(M), int(C), relu, stream());
+                     part.data_ptr<float>(), ctr, int(M), int(C), relu, stream());
   return {y, mean, rstd};
 }
 
@@ -97,7 +112,8 @@ torch::Tensor bn_fwd_eval(torch::Tensor x, torch::Tensor w, torch::Tensor b, c10
 
 // returns {dx, dw, db} or {dx, dw, db, dres}
 std::vector<torch::Tensor> bn_bwd(torch::Tensor dy, torch::Tensor y, torch::Tensor x, torch::Tensor w,
-                                  torch::Tensor mean, torch::Tensor rstd, bool relu, bool need_dres) {
+                                  torch::Tensor mean, torch::Tensor rstd, bool relu, bool need_dres,
+                                  c10::optional<torch::Tensor> counters) {
   const c10::DeviceGuard g(x.device());
   check_shape(x);
   const int64_t M = x.size(0), C = x.size(1);
@@ -108,11 +124,11 @@ std::vector<torch::Tensor> bn_bwd(torch::Tensor dy, torch::Tensor y, torch::Tens
   auto dres = need_dres ? torch::empty_like(x) : torch::Tensor();
   auto opt = x.options().dtype(torch::kFloat32);
   auto dw = torch::empty({C}, opt), db = torch::empty({C}, opt), coef = torch::empty({3, C}, opt);
-  const auto plan = p2bn::bn_plan(int(M), int(C));
-  auto part = torch::empty({2, plan.S, C}, opt);
+  int* ctr = opt_ctr(counters, x);
+  auto part = torch::empty({2, part_rows(M, C, ctr != nullptr), C}, opt);
   p2bn::bn_bwd(bf, dy.data_ptr(), relu ? y.data_ptr() : nullptr, x.data_ptr(), f32(w, C, x, "weight"),
                f32(mean, C, x, "mean"), f32(rstd, C, x, "rstd"), dx.data_ptr(), need_dres ? dres.data_ptr() : nullptr,
-               dw.data_ptr<float>(), db.data_ptr<float>(), coef.data_ptr<float>(), part.data_ptr<float>(), int(M),
+               dw.data_ptr<float>(), db.data_ptr<float>(), coef.data_ptr<float>(), part.data_ptr<float>(), ctr, int(M),
                int(C), relu, stream());
   if (need_dres) return {dx, dw, db, dres};
   return {dx, dw, db};
@@ -126,9 +142,11 @@ void register_bn(pybind11::module& m) {
   f.def("fwd_train", &bn_fwd_train, py::arg("x"), py::arg("w"), py::arg("b"), py::arg("residual") = py::none(),
         py::arg("running_mean") = py::none(), py::arg("running_var") = py::none(),
         py::arg("num_batches_tracked") = py::none(), py::arg("momentum") = 0.1, py::arg("eps") = 1e-5,
-        py::arg("relu") = true);
+        py::arg("relu") = true, py::arg("counters") = py::none());
   f.def("fwd_eval", &bn_fwd_eval, py::arg("x"), py::arg("w"), py::arg("b"), py::arg("residual") = py::none(),
         py::arg("running_mean"), py::arg("running_var"), py::arg("eps") = 1e-5, py::arg("relu") = true);
   f.def("bwd", &bn_bwd, py::arg("dy"), py::arg("y"), py::arg("x"), py::arg("w"), py::arg("mean"), py::arg("rstd"),
-        py::arg("relu"), py::arg("need_dres"));
+        py::arg("relu"), py::arg("need_dres"), py::arg("counters") = py::none());
+  f.def("fused_rows", [](int64_t M, int64_t C) { return p2bn::bn_fused_plan(int(M), int(C)).S; },
+        "partial rows of the statistics + finalize kernels for an [M, C] activation (0: not eligible)");
 }

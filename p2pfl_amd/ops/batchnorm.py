@@ -15,6 +15,7 @@ counts not divisible by 8 and ``momentum=None`` use the plain PyTorch chain.
 
 from __future__ import annotations
 
+import os
 from typing import Optional
 
 import torch
@@ -24,12 +25,26 @@ from torch import nn
 
 # host-side counters of the extra passes the backward had to insert
 STATS = {"dy_cast": 0, "dy_relayout": 0}
+# statistics + finalize as one launch for eligible bf16 shapes (P2PFL_BN_FUSED_STATS=1).  Off by
+# default: per call it is 8.4 us against 4.9 + 4.9 us for the two launches, but the ResNet-18 /
+# ResNet-50 rounds measured 3.5 % / 2.5 % slower with it (profiles/r3_bn_stats_finalize.md).
+_FUSED_STATS = os.environ.get("P2PFL_BN_FUSED_STATS", "0") == "1"
 
 
 def _bx():
     from p2pfl_amd.ops import ext
 
     return ext().bn
+
+
+def _counter(x2: torch.Tensor):
+    """Arrival counter of the statistics + finalize kernel (one launch instead of
+    two, csrc/batchnorm.hip) when the [M, C] activation is eligible, else None."""
+    if x2.dtype != torch.bfloat16 or not _FUSED_STATS or _bx().fused_rows(x2.shape[0], x2.shape[1]) <= 0:
+        return None
+    from p2pfl_amd.ops import splitk
+
+    return splitk.counters(1, x2.device)
 
 
 def _nhwc_2d(t: torch.Tensor) -> torch.Tensor:
@@ -56,7 +71,8 @@ class _BatchNormAct(torch.autograd.Function):
         shape = x.shape
         x2 = _nhwc_2d(x)
         r2 = _nhwc_2d(residual.to(x.dtype)) if residual is not None else None
-        y2, mean, rstd = _bx().fwd_train(x2, weight, bias, r2, running_mean, running_var, nbt, float(momentum), float(eps), bool(relu))
+        y2, mean, rstd = _bx().fwd_train(x2, weight, bias, r2, running_mean, running_var, nbt, float(momentum), float(eps), bool(relu),
+                                         _counter(x2))
         ctx.save_for_backward(x2, y2, weight, mean, rstd)
         ctx.shape, ctx.relu, ctx.has_res = shape, bool(relu), residual is not None
         ctx.res_dtype = residual.dtype if residual is not None else None
@@ -71,7 +87,7 @@ class _BatchNormAct(torch.autograd.Function):
         if not dy.is_contiguous(memory_format=torch.channels_last):
             STATS["dy_relayout"] += 1
             dy = dy.contiguous(memory_format=torch.channels_last)
-        out = _bx().bwd(_nhwc_2d(dy), y2, x2, weight, mean, rstd, ctx.relu, ctx.has_res and ctx.needs_input_grad[3])
+        out = _bx().bwd(_nhwc_2d(dy), y2, x2, weight, mean, rstd, ctx.relu, ctx.has_res and ctx.needs_input_grad[3], _counter(x2))
         dx = _from_2d(out[0], ctx.shape)
         dres = _from_2d(out[3], ctx.shape).to(ctx.res_dtype) if len(out) > 3 else None
         return dx, out[1].to(weight.dtype), out[2].to(weight.dtype), dres, None, None, None, None, None, None

@@ -157,3 +157,40 @@ def test_resnet18_uses_fused_bn_and_trains():
         finally:
             del os.environ["P2PFL_FORCE_TORCH_OPS"]
     torch.testing.assert_close(a, b, atol=0.15, rtol=0.05)
+
+
+@pytest.mark.parametrize("shape", [(32, 64, 32, 32), (5, 64, 9, 11), (8, 512, 4, 4), (2, 2048, 2, 2), (3, 24, 5, 7)])
+@pytest.mark.parametrize("residual,relu", [(False, True), (True, False)])
+def test_fused_stats_finalize_matches_separate_launches(shape, residual, relu):
+    """Statistics + finalize in one launch (last block to arrive finalizes) vs the
+    separate statistics / finalize launches: same values up to the reduction order,
+    and the arrival counter is zero again after each launch."""
+    bx = ops.ext().bn
+    C = shape[1]
+    M = shape[0] * shape[2] * shape[3]
+    assert bx.fused_rows(M, C) > 0
+    g = torch.Generator(device="cuda").manual_seed(M + C)
+    x = torch.randn(M, C, device="cuda", generator=g).mul(2).add(0.5).to(torch.bfloat16)
+    r = torch.randn(M, C, device="cuda", generator=g).to(torch.bfloat16) if residual else None
+    dy = torch.randn(M, C, device="cuda", generator=g).to(torch.bfloat16)
+    outs = []
+    for fused in (True, False):
+        bn = _bn(C, 4)
+        ctr = torch.zeros(16, dtype=torch.int32, device="cuda") if fused else None
+        y, mean, rstd = bx.fwd_train(x, bn.weight, bn.bias, r, bn.running_mean, bn.running_var, bn.num_batches_tracked,
+                                     0.1, 1e-5, relu, ctr)
+        back = bx.bwd(dy, y, x, bn.weight, mean, rstd, relu, residual, ctr)
+        torch.cuda.synchronize()
+        if fused:
+            assert int(ctr.abs().sum()) == 0
+        outs.append((y.float(), mean, rstd, bn.running_mean.clone(), bn.running_var.clone(), int(bn.num_batches_tracked),
+                     *[t.float() for t in back]))
+    (yf, *rest_f), (ys, *rest_s) = outs
+    torch.testing.assert_close(yf, ys, atol=2e-2, rtol=1e-2)
+    for a, b in zip(rest_f, rest_s):
+        if isinstance(a, int):
+            assert a == b == 1
+        elif a.dtype == torch.float32 and a.dim() == 1:
+            torch.testing.assert_close(a, b, atol=1e-4, rtol=1e-4)
+        else:
+            torch.testing.assert_close(a, b, atol=2e-2, rtol=1e-2)
