@@ -46,11 +46,15 @@ def gemm_reference(a, b, a_kmajor=True, b_kmajor=True, bias=None, gelu=False, re
     return c, z
 
 
+# Upper bound of the weight-gradient split-K factor (P2PFL_GEMM_MAX_SPLITS).
+_MAX_SPLITS = int(os.environ.get("P2PFL_GEMM_MAX_SPLITS", "16"))
+
+
 def splits_for(M: int, N: int, K: int) -> int:
     """Split-K factor so that a small M x N grid still covers the 256 CUs."""
     tiles = -(-M // 128) * -(-N // 128)
     s = 1
-    while tiles * s < 256 and K // (s * 2) >= 512 and s < 16:
+    while tiles * s < 256 and K // (s * 2) >= 512 and s < _MAX_SPLITS:
         s *= 2
     return s
 
