@@ -46,8 +46,10 @@ def gemm_reference(a, b, a_kmajor=True, b_kmajor=True, bias=None, gelu=False, re
     return c, z
 
 
-# Upper bound of the weight-gradient split-K factor (P2PFL_GEMM_MAX_SPLITS).
-_MAX_SPLITS = int(os.environ.get("P2PFL_GEMM_MAX_SPLITS", "16"))
+# Upper bound of the weight-gradient split-K factor (P2PFL_GEMM_MAX_SPLITS).  64: the
+# ResNet-50 1x1 weight gradients (K = 32768 pixels, 2-8 tiles) ran at 16 slices on 32
+# workgroups; 64 measured 124.0 / 126.3 vs 128.3 / 128.1 ms per round (scripts/r3_gpu34.sh).
+_MAX_SPLITS = int(os.environ.get("P2PFL_GEMM_MAX_SPLITS", "64"))
 
 
 def splits_for(M: int, N: int, K: int) -> int:

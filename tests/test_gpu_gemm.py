@@ -63,6 +63,17 @@ def test_gemm_split_k(splits):
     torch.testing.assert_close(out, ref, atol=5e-3, rtol=1e-4)
 
 
+def test_wgrad_split_factor_64_on_long_k():
+    """1x1-conv weight gradient class (ResNet-50: K = 32768 pixels, 2 tiles): 64 K-slices
+    reduced by tile_slab_reduce, vs fp32."""
+    M, N, K = 256, 64, 32768
+    assert gemm_mod.splits_for(M, N, K) == 64
+    a, b = _operands(M, N, K, False, False, seed=64)
+    out = gemm_mod._product(a, b, False, False, torch.float32, gemm_mod.splits_for(M, N, K))
+    ref, _ = ops.gemm_reference(a, b, False, False)
+    torch.testing.assert_close(out, ref, atol=2e-2, rtol=1e-4)
+
+
 @pytest.mark.parametrize("bias_dtype", [torch.float32, torch.bfloat16])
 def test_gemm_epilogue_bias_gelu_residual(bias_dtype):
     M, N, K = 300, 256, 128
