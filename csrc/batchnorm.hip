@@ -64,6 +64,7 @@ P2_DEVICE void ld8f(const float* p, float (&v)[8]) { V8<float>::load(p, v); }
 
 constexpr int kThreads = 256;
 constexpr int kRedCols = kThreads * 8;  // LDS columns of one phase-reduction slab
+constexpr int kInFlight = 4;             // rows per thread in flight in the statistics passes
 
 // ---------------------------------------------------------------------------
 // Block-level fixed-order reduction of two per-thread [8] accumulators over
@@ -109,29 +110,25 @@ __global__ __launch_bounds__(kThreads) void bn_stats_kernel(const T* __restrict_
     float sh[8];
     V8<T>::load(x + c, sh);
     const int step = rp * gridDim.y;
-    int r = blockIdx.y * rp + ph;
-    // two rows in flight per iteration
-    for (; r + step < M; r += 2 * step) {
-      float v0[8], v1[8];
-      V8<T>::load(x + size_t(r) * C + c, v0);
-      V8<T>::load(x + size_t(r + step) * C + c, v1);
+    // kInFlight rows per iteration, loaded unconditionally (rows past M re-read
+    // row 0 and count zero): a load under a branch gets its own vmcnt(0), which
+    // serialised the rows one memory round trip at a time
+    for (int r = blockIdx.y * rp + ph; r < M; r += kInFlight * step) {
+      float v[kInFlight][8];
 #pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const float d0 = v0[j] - sh[j], d1 = v1[j] - sh[j];
-        s1[j] += d0;
-        s2[j] = fmaf(d0, d0, s2[j]);
-        s1[j] += d1;
-        s2[j] = fmaf(d1, d1, s2[j]);
+      for (int u = 0; u < kInFlight; ++u) {
+        const int ru = r + u * step;
+        V8<T>::load(x + size_t(ru < M ? ru : 0) * C + c, v[u]);
       }
-    }
-    if (r < M) {
-      float v0[8];
-      V8<T>::load(x + size_t(r) * C + c, v0);
 #pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const float d0 = v0[j] - sh[j];
-        s1[j] += d0;
-        s2[j] = fmaf(d0, d0, s2[j]);
+      for (int u = 0; u < kInFlight; ++u) {
+        const bool in = r + u * step < M;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const float d = in ? v[u][j] - sh[j] : 0.f;
+          s1[j] += d;
+          s2[j] = fmaf(d, d, s2[j]);
+        }
       }
     }
   }
@@ -155,21 +152,26 @@ __global__ __launch_bounds__(kThreads) void bn_bwd_stats_kernel(const T* __restr
     float mu[8];
     ld8f(mean + c, mu);
     const int step = rp * gridDim.y;
-    for (int r = blockIdx.y * rp + ph; r < M; r += step) {
-      const size_t e = size_t(r) * C + c;
-      float g[8], xv[8];
-      V8<T>::load(dy + e, g);
-      V8<T>::load(x + e, xv);
-      if (RELU) {
-        float yv[8];
-        V8<T>::load(y + e, yv);
+    // kInFlight rows per iteration, loads unconditional (see bn_stats_kernel)
+    for (int r = blockIdx.y * rp + ph; r < M; r += kInFlight * step) {
+      float g[kInFlight][8], xv[kInFlight][8], yv[kInFlight][8];
 #pragma unroll
-        for (int j = 0; j < 8; ++j) g[j] = yv[j] > 0.f ? g[j] : 0.f;
+      for (int u = 0; u < kInFlight; ++u) {
+        const int ru = r + u * step;
+        const size_t e = size_t(ru < M ? ru : 0) * C + c;
+        V8<T>::load(dy + e, g[u]);
+        V8<T>::load(x + e, xv[u]);
+        if (RELU) V8<T>::load(y + e, yv[u]);
       }
 #pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        s1[j] += g[j];
-        s2[j] = fmaf(g[j], xv[j] - mu[j], s2[j]);
+      for (int u = 0; u < kInFlight; ++u) {
+        const bool in = r + u * step < M;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const float gg = in && (!RELU || yv[u][j] > 0.f) ? g[u][j] : 0.f;
+          s1[j] += gg;
+          s2[j] = fmaf(gg, xv[u][j] - mu[j], s2[j]);
+        }
       }
     }
   }
