@@ -455,6 +455,19 @@ P2_DEVICE void gemm_body(const GemmParams& p, const LA& la, const LB& lb, int ti
     // stores, then one relaxed agent-scope ticket; the last arriver reads the
     // slabs with sc1 loads (every one of them), so no acquire fence either.
     // The counter is reset for the next launch.
+    //
+    // HARDWARE ASSUMPTION (gfx950, not the HIP memory model): the slab stores
+    // and loads carry the device-scope cache-policy bit (aux = 16, "sc1"), so a
+    // store is written through the issuing XCD's L2 before its vmcnt retires,
+    // and a load is served from the device coherence point, never from a stale
+    // line in the reading XCD's L2.  The s_waitcnt vmcnt(0) + barrier before the
+    // ticket therefore orders every slab store before the atomic at device
+    // scope, which is what an agent release fence would give (at the cost of a
+    // whole-L2 write-back per slice).  Slices of one tile land on different XCDs
+    // (round-robin workgroup dispatch), and the workspace is re-used by the
+    // next launch, so tests/test_gpu_gemm.py::test_in_launch_splitk_reused_workspace
+    // runs many back-to-back split-K launches over one workspace against the
+    // separate-launch reducer to pin this assumption.
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     int* flag = reinterpret_cast<int*>(smem);

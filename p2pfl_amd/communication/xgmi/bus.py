@@ -159,10 +159,14 @@ class BusEndpoint:
                 self._out[key] = s
             return s, lk
 
-    def drop(self, dst: str) -> None:
-        """Forget the cached connections to ``dst`` (they will be reopened on demand)."""
+    def drop(self, dst: str, only_bulk: bool = False) -> None:
+        """Forget the cached connections to ``dst`` (they will be reopened on demand).
+
+        ``only_bulk``: drop just the bulk connection -- a failed large send must
+        not close the control connection, whose close the peer reads as this
+        node leaving."""
         with self._out_lock:
-            socks = [self._out.pop((dst, b), None) for b in (False, True)]
+            socks = [self._out.pop((dst, b), None) for b in ((True,) if only_bulk else (False, True))]
         for s in socks:
             if s is not None:
                 try:
@@ -193,7 +197,7 @@ class BusEndpoint:
                         last = off + FRAG_DATA >= len(record)
                         s.sendall(_FRAG + (b"\x01" if last else b"\x00") + view[off : off + FRAG_DATA])
         except OSError as e:
-            self.drop(dst)
+            self.drop(dst, only_bulk=bulk)
             raise ConnectionError(f"send to {dst} failed: {e}") from e
 
     def reachable(self, dst: str) -> bool:

@@ -25,7 +25,7 @@ Differences from the reference:
 from __future__ import annotations
 
 import threading
-from typing import Any, Dict, List, Optional, Tuple
+from typing import Any, Callable, Dict, List, Optional, Tuple
 
 from p2pfl_amd.management.logger import logger
 from p2pfl_amd.settings import Settings
@@ -83,13 +83,17 @@ class Aggregator:
             self._waiting_aggregated_model = False
             self._running = False
             self._lost = set()
-            self._models_changed_locked()
+            self._models_changed_locked()  # no models: drops any running state, no work to run
             self._done.set()
 
-    def _models_changed_locked(self) -> None:
+    def _models_changed_locked(self) -> Optional[Callable[[], None]]:
         """Hook (lock held): the stored models changed and the aggregation is
         not complete yet.  Strategies may start folding them in (FedAvg keeps
-        a running sum); the default does nothing."""
+        a running sum): the hook only plans under the lock and returns the work
+        as a callable, which :meth:`add_model` runs after releasing the lock (so
+        flattening / kernel launches never hold up the receive and gossip
+        threads).  The default does nothing."""
+        return None
 
     # ------------------------------------------------------------------
     # queries
@@ -181,6 +185,13 @@ class Aggregator:
         if not nodes:
             logger.debug(self.node_name, "Received a model without a list of contributors.")
             return []
+        job: List[Optional[Callable[[], None]]] = [None]
+        now = self._add_model(model, nodes, weight, job)
+        if job[0] is not None:
+            job[0]()
+        return now
+
+    def _add_model(self, model: Any, nodes: List[str], weight: int, job: List[Optional[Callable[[], None]]]) -> List[str]:
         with self._lock:
             if self._waiting_aggregated_model and not self._models:
                 if self._full_aggregate_locked(nodes):
@@ -213,7 +224,7 @@ class Aggregator:
             if self._complete_locked():
                 self._done.set()
             else:
-                self._models_changed_locked()
+                job[0] = self._models_changed_locked()
             return now
 
     # ------------------------------------------------------------------

@@ -34,6 +34,14 @@ class _RunningSum:
     weights: List[float] = field(default_factory=list)
 
 
+def _used_here(t: torch.Tensor) -> None:
+    """``t`` (allocated on another thread's stream) is read by a kernel about to
+    be enqueued on this thread's stream: its block must not be recycled on the
+    allocating stream before that kernel ran."""
+    if t.is_cuda:
+        t.record_stream(torch.cuda.current_stream(t.device))
+
+
 class FedAvg(Aggregator):
     """Sample-weighted mean of the models.
 
@@ -53,10 +61,16 @@ class FedAvg(Aggregator):
         self._run: Optional[_RunningSum] = None
 
     # -- running sum ----------------------------------------------------------
-    def _models_changed_locked(self) -> None:
+    # Folds are copy-on-write: a fold writes a NEW accumulator (acc_in = the
+    # old one) and installs a new _RunningSum; an accumulator a reader took
+    # (aggregate(), a partial aggregation on a gossip thread) is never written
+    # again.  Only the planning runs under Aggregator._lock; flattening and the
+    # launch run after add_model released it, and the result is published only
+    # if the running sum it extends is still the current one.
+    def _models_changed_locked(self):
         if not self.running_sum or not self._models:
             self._run = None
-            return
+            return None
         keys = sorted(self._models)
         run = self._run
         if run is not None and (keys[: len(run.keys)] != run.keys
@@ -65,7 +79,7 @@ class FedAvg(Aggregator):
         have = {n for k in self._models for n in k.split()}
         missing = [n for n in self._train_set if n not in have and n not in self._lost]
         if not missing:
-            return  # complete: aggregate() adds the rest in one launch
+            return None  # complete: aggregate() adds the rest in one launch
         # a future entry is keyed by still-missing names, so it sorts at or
         # after min(missing): everything before that is final in the order
         bound = min(missing)
@@ -76,24 +90,37 @@ class FedAvg(Aggregator):
                 break
             fold.append(k)
         if not fold:
-            return
+            return None
         entries = [self._models[k] for k in fold]
+        return lambda: self._fold(run, fold, entries)
+
+    def _fold(self, base: Optional[_RunningSum], fold: List[str], entries: List[Any]) -> None:
+        """Extend ``base`` by ``entries`` into a fresh accumulator (lock NOT held)."""
         ref = entries[0][0]
         device = next(iter(ref.values())).device if len(ref) else torch.device("cpu")
         flats = [flatten(m, device=device) for m, _ in entries]
-        if run is None:
-            run = _RunningSum(torch.empty(flats[0].flat.numel(), dtype=torch.float32, device=device), flats[0].layout)
-        for f in flats:
-            if not f.layout.compatible(run.layout):
-                self._run = None
-                return
+        layout = base.layout if base is not None else flats[0].layout
+        if not all(f.layout.compatible(layout) for f in flats):
+            with self._lock:
+                if self._run is base:
+                    self._run = None
+            return
         w = [float(x) for _, x in entries]
+        acc = torch.empty(flats[0].flat.numel(), dtype=torch.float32, device=device)
         with logger.span(self.node_name, "fold_models", k=len(fold)):
-            ops.weighted_sum_into(run.acc, [f.flat for f in flats], w, acc_in=run.acc if run.keys else None)
-        run.keys += fold
-        run.entries += entries
-        run.weights += w
-        self._run = run
+            if base is not None:
+                _used_here(base.acc)
+            ops.weighted_sum_into(acc, [f.flat for f in flats], w, acc_in=base.acc if base is not None else None)
+        new = _RunningSum(acc, layout,
+                          (base.keys if base else []) + fold,
+                          (base.entries if base else []) + entries,
+                          (base.weights if base else []) + w)
+        with self._lock:
+            # publish only on top of the sum this fold extended, and only if the
+            # folded entries are still the stored ones (a full aggregate or
+            # clear() may have replaced them meanwhile)
+            if self._run is base and all(self._models.get(k) is e for k, e in zip(new.keys, new.entries)):
+                self._run = new
 
     # -- strategy -------------------------------------------------------------
     def aggregate(self, models: Dict[str, Tuple[Any, int]]) -> FlatParams:
@@ -114,6 +141,8 @@ class FedAvg(Aggregator):
             start = len(run.keys) if use else 0
             acc = run.acc if use else None
             layout = run.layout if use else None
+        if acc is not None:
+            _used_here(acc)  # never written again (copy-on-write folds); keep it alive for this stream
         flats: List[FlatParams] = [flatten(m, device=device) for m, _ in entries[start:]]
         layout = layout if layout is not None else flats[0].layout
         for f in flats:

@@ -139,35 +139,50 @@ class TrainStepGraph:
         return loss.detach()
 
     def capture(self, idx: torch.Tensor) -> None:
-        """Warm up and capture; parameters, optimizer and BN state are restored afterwards."""
+        """Warm up, then capture; parameters, optimizer and BN state are restored after the warm-up.
+
+        The warm-up step does every lazy first use -- workspaces, the per-shape
+        autotune timing (``ops/autotune.py``), library solver choices -- which
+        can take seconds on a fresh device.  It is ordinary eager work, so it
+        runs under the SHARED gate next to the other peers' steps; only the
+        capture itself (host-side recording, no kernel executes) takes the gate
+        exclusively, so a capturing peer never stalls the others for longer
+        than the recording (reference requirement: training must not stall the
+        node, ``train_stage.py:88-93``).
+        """
         learner, opt = self.learner, self.opt
         arena = learner.arena
-        cur = torch.cuda.current_stream(learner.device)
-        with GATE.exclusive(), _CAPTURE_LOCK:
-            torch.cuda.synchronize(learner.device)
-            keep = [arena.flat, arena.shadow] + opt.state_tensors()
-            saved = [t.clone() for t in keep if t is not None]
-            ints = {k: v.clone() for k, v in getattr(arena, "_int_buffers", {}).items()}
-            t_host = opt.t
-            self.idx.copy_(idx)
+        dev = learner.device
+        cur = torch.cuda.current_stream(dev)
+        with GATE.shared():
             self.stream.wait_stream(cur)
             with torch.cuda.stream(self.stream):
+                keep = [t for t in [arena.flat, arena.shadow] + opt.state_tensors() if t is not None]
+                saved = [t.clone() for t in keep]
+                ints = {k: v.clone() for k, v in getattr(arena, "_int_buffers", {}).items()}
+                t_host = opt.t
+                self.idx.copy_(idx)
                 self._body(graph=False)  # lazy inits (workspaces, solver choices) outside the capture
+                for dst, src in zip(keep, saved):
+                    dst.copy_(src)
+                for k, v in ints.items():
+                    arena._int_buffers[k].copy_(v)
             self.stream.synchronize()
+            del saved, ints
+            opt.t = t_host
+            for p in opt.mt.params:  # eager gradients are not the graph's
+                p.grad = None
+        with GATE.exclusive(), _CAPTURE_LOCK:
+            torch.cuda.synchronize(dev)
             g = torch.cuda.CUDAGraph()
-            self.counters = splitk.GraphCounters(learner.device)  # split-K tile counters owned by this graph
+            self.counters = splitk.GraphCounters(dev)  # split-K tile counters owned by this graph
             with no_gc(), splitk.graph_scope(self.counters), torch.cuda.graph(g, stream=self.stream, capture_error_mode="thread_local"):
                 self.loss = self._body(graph=True)
-            torch.cuda.synchronize(learner.device)
             opt.mt.fill_grad_table(self.gtab)  # the graph's gradient buffers, fixed for every replay
-            for dst, src in zip([t for t in keep if t is not None], saved):
-                dst.copy_(src)
-            for k, v in ints.items():
-                arena._int_buffers[k].copy_(v)
-            opt.t = t_host
+            opt.t = t_host  # recording executed nothing; host-side counters back to the pre-capture state
             for p in opt.mt.params:  # eager steps allocate their own gradients
                 p.grad = None
-            torch.cuda.synchronize(learner.device)
+            torch.cuda.synchronize(dev)
         self.graph = g
 
     def run(self, idx: torch.Tensor) -> torch.Tensor:
@@ -229,12 +244,14 @@ class EvalStepGraph:
     def capture(self, idx: torch.Tensor) -> None:
         learner = self.learner
         cur = torch.cuda.current_stream(learner.device)
-        with GATE.exclusive(), _CAPTURE_LOCK:
-            self.idx.copy_(idx)
+        with GATE.shared():  # warm-up (first-use work, creates the sums) next to the other peers
             self.stream.wait_stream(cur)
             with torch.cuda.stream(self.stream):
-                self.step(self.idx, float(self.B), cache=False)  # warm-up, creates the sums
+                self.idx.copy_(idx)
+                self.step(self.idx, float(self.B), cache=False)
             self.stream.synchronize()
+        with GATE.exclusive(), _CAPTURE_LOCK:  # recording only
+            torch.cuda.synchronize(learner.device)
             g = torch.cuda.CUDAGraph()
             self.counters = splitk.GraphCounters(learner.device)
             with no_gc(), splitk.graph_scope(self.counters), torch.cuda.graph(g, stream=self.stream, capture_error_mode="thread_local"):

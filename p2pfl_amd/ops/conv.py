@@ -254,9 +254,9 @@ def conv2d(x: torch.Tensor, conv: nn.Conv2d) -> torch.Tensor:
     # eager timing preferred: MIOpen convolutions replayed from captured step
     # graphs corrupted weights as soon as several learners' graphs and eager
     # steps shared the device (profiles/r3_nan_root_cause.md); eager steps may
-    # still take MIOpen.
+    # still take MIOpen.  This holds under every policy, "library" included.
     capturing = x.is_cuda and torch.cuda.is_current_stream_capturing()
-    if native_ok(x, conv) and _POLICY != "library" and (_POLICY == "native" or capturing or _native_faster(x, conv)):
+    if native_ok(x, conv) and (capturing or _POLICY == "native" or (_POLICY != "library" and _native_faster(x, conv))):
         STATS["native_fwd"] += 1
         return _Conv2dNHWC.apply(x, conv.weight, _sym(conv.stride), _sym(conv.padding), _sym(conv.dilation))
     STATS["torch_fwd"] += 1

@@ -72,6 +72,7 @@ class _Checker:
         self.violations: List[Violation] = []
         self._seen_cycles: Set[Tuple[str, ...]] = set()
         self.acquisitions = 0
+        self.max_hold: Dict[str, Tuple[float, str]] = {}  # class -> (longest hold s, thread)
 
     # -- held-lock stack -------------------------------------------------
     def held(self) -> List["_Tracked"]:
@@ -168,6 +169,9 @@ class _Checker:
                 break
         lk._held_in = None
         dt = time.monotonic() - getattr(lk, "_t_acq", time.monotonic())
+        prev = self.max_hold.get(lk.cls)
+        if prev is None or dt > prev[0]:
+            self.max_hold[lk.cls] = (dt, threading.current_thread().name)
         if dt > self.hold_warn_s and lk.cls not in _HOLD_EXEMPT:
             with self._mu:
                 self.violations.append(
@@ -182,6 +186,7 @@ class _Checker:
             self.violations.clear()
             self._seen_cycles.clear()
             self.acquisitions = 0
+            self.max_hold.clear()
 
 
 class LockOrderError(RuntimeError):
@@ -329,6 +334,12 @@ def violations() -> List[Violation]:
         return list(_checker.violations)
 
 
+def max_holds() -> Dict[str, Tuple[float, str]]:
+    """Longest observed hold per lock class: ``{class: (seconds, thread name)}``."""
+    with _checker._mu:
+        return dict(_checker.max_hold)
+
+
 def report() -> Dict[str, Any]:
     """Observed order graph and violations (for logs / CI artefacts)."""
     with _checker._mu:
@@ -336,6 +347,7 @@ def report() -> Dict[str, Any]:
             "enabled": _checker.enabled,
             "acquisitions_while_holding": _checker.acquisitions,
             "class_edges": sorted(f"{a} -> {b}" for a, b in _checker.class_edges),
+            "max_hold_s": {k: round(v[0], 4) for k, v in sorted(_checker.max_hold.items())},
             "violations": [str(v) for v in _checker.violations],
         }
 

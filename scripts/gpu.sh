@@ -1,0 +1,75 @@
+#!/usr/bin/env bash
+# One parameterised GPU runner (replaces the round-3 one-off scripts/r3_*.sh).
+#
+# Every step runs under its own time limit, output goes to gpurun_out/<tag>.log,
+# and the lock checker stays ON (the driver's configuration, tests/conftest.py).
+# A timeout, abort, segfault or kill ends the script at once so nothing more
+# touches a possibly-wedged GPU; an ordinary failure ends it too (exit 1).
+#
+#   scripts/gpu.sh suite                    pytest -m gpu (whole GPU suite) + smoke()
+#   scripts/gpu.sh tests <pytest args...>   selected tests, e.g. tests/test_gpu_conv.py -k bn
+#   scripts/gpu.sh smoke                    __graft_entry__.smoke()
+#   scripts/gpu.sh bench [bench args...]    bench.py (N=1 headline unless args say otherwise)
+#   scripts/gpu.sh models [steps]           configs 3-5: resnet18, resnet50, vit_b16 rounds
+#   scripts/gpu.sh rehearsal [N...]         split-hosts multi-rank rehearsal on the one GPU (default 2 4 8)
+#   scripts/gpu.sh prof <tag> <cmd...>      rocprofv3 --kernel-trace --stats of <cmd> -> gpurun_out/prof_<tag>
+#   scripts/gpu.sh py <secs> <tag> <cmd...> any python command, own limit
+#
+# Several modes can be chained with "+", e.g.
+#   scripts/gpu.sh suite + bench + models
+set -u
+set -o pipefail
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+mkdir -p gpurun_out
+export TMPDIR=/tmp PYTHONPATH="$PWD${PYTHONPATH:+:$PYTHONPATH}"
+
+step() {  # step <secs> <tag> <cmd...>
+  local secs=$1 tag=$2; shift 2
+  echo "=== [$tag] $* (limit ${secs}s, env: P2PFL_LOCKCHECK=${P2PFL_LOCKCHECK:-default(1 under pytest)})"
+  timeout -k 10 "$secs" "$@" > "gpurun_out/$tag.log" 2>&1
+  local rc=$?
+  echo "=== [$tag] exit $rc"
+  tail -n 25 "gpurun_out/$tag.log" | cut -c1-400
+  if [ $rc -ne 0 ]; then echo "=== stopping after [$tag] (exit $rc)"; exit $rc; fi
+}
+
+run_mode() {
+  local mode=$1; shift
+  case $mode in
+    suite)
+      step 900 pytest_gpu python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread -rs
+      step 300 smoke python -c "import __graft_entry__ as g; g.smoke()" ;;
+    tests)
+      step 600 pytest_sel python -u -m pytest -x -v --timeout 200 --timeout-method thread "$@" ;;
+    smoke)
+      step 300 smoke python -c "import __graft_entry__ as g; g.smoke()" ;;
+    bench)
+      step 300 bench python -u bench.py "$@" ;;
+    models)
+      local k=${1:-3}
+      for m in resnet18 resnet50 vit_b16; do
+        step 300 "bench_$m" python -u bench.py --model $m --steps "$k" --warmup 1
+      done ;;
+    rehearsal)
+      for n in ${@:-2 4 8}; do
+        step 300 "rehearsal_n$n" env P2PFL_RCCL_SPLIT_HOSTS=1 P2PFL_BENCH_SPANS=1 python -u bench.py --gpus "$n" --steps 6 --warmup 2 --watchdog 240
+      done ;;
+    prof)
+      local tag=$1; shift
+      rm -rf "gpurun_out/prof_$tag"
+      step 400 "prof_$tag" rocprofv3 --kernel-trace --stats -d "gpurun_out/prof_$tag" -o run -- "$@" ;;
+    py)
+      local secs=$1 tag=$2; shift 2
+      step "$secs" "$tag" "$@" ;;
+    *) echo "unknown mode $mode"; exit 2 ;;
+  esac
+}
+
+args=("$@")
+i=0
+while [ $i -lt ${#args[@]} ]; do
+  mode=${args[$i]}; i=$((i + 1)); sub=()
+  while [ $i -lt ${#args[@]} ] && [ "${args[$i]}" != "+" ]; do sub+=("${args[$i]}"); i=$((i + 1)); done
+  i=$((i + 1))
+  run_mode "$mode" "${sub[@]+"${sub[@]}"}"
+done

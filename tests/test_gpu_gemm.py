@@ -217,3 +217,36 @@ def test_pingpong_gemm_epilogues_and_split_k():
     C.gemm(a3, b3, False, False, out3, None, False, None, None, 3, PP, ws, counters(tiles_of(768, 768), out3.device))
     ref3, _ = ops.gemm_reference(a3, b3, False, False)
     torch.testing.assert_close(out3, ref3, atol=5e-3, rtol=1e-4)
+
+
+@pytest.mark.parametrize("splits", [2, 3, 4])
+def test_in_launch_splitk_reused_workspace(splits):
+    """Back-to-back in-launch split-K launches over ONE reused workspace and counter
+    array, on a grid of many tiles (slices of a tile land on different XCDs): each
+    launch must see only its own slabs (pins the sc1 hand-off assumption documented
+    in csrc/gemm_core.h).  Integer operands make every summation order exact, so the
+    in-launch reduction must equal the fp32 product bit for bit, launch after launch."""
+    from p2pfl_amd.ops.splitk import counters, slab_elems, tiles_of
+
+    C = ops.ext()
+    M, N, K = 1024, 768, 2048  # 48 tiles x splits workgroups
+    ws = torch.empty(splits * slab_elems(M, N), device="cuda")
+    cnt = counters(tiles_of(M, N), torch.device("cuda"))
+    outs, refs = [], []
+    for it in range(24):
+        g = torch.Generator(device="cuda").manual_seed(100 + it)
+        A = torch.randint(-2, 3, (M, K), device="cuda", generator=g).to(torch.bfloat16)
+        B = torch.randint(-2, 3, (N, K), device="cuda", generator=g).to(torch.bfloat16)
+        out = torch.empty(M, N, device="cuda", dtype=torch.float32)
+        C.gemm(A.t().contiguous(), B.t().contiguous(), False, False, out, None, False, None, None, splits, 0, ws, cnt)
+        outs.append(out)
+        refs.append(A.float() @ B.float().t())
+    torch.cuda.synchronize()
+    for it, (o, r) in enumerate(zip(outs, refs)):
+        assert torch.equal(o, r), f"launch {it}: max err {(o - r).abs().max().item()}"
+    # the separate-launch reducer on the same last operands agrees too
+    ws2 = torch.empty(splits * slab_elems(M, N), device="cuda")
+    out2 = torch.empty(M, N, device="cuda", dtype=torch.float32)
+    C.gemm(A.t().contiguous(), B.t().contiguous(), False, False, ws2, None, False, None, None, splits, 0, None, None)
+    C.tile_slab_reduce(ws2, splits, M, N, out2, 0)
+    assert torch.equal(out2, refs[-1])

@@ -414,6 +414,79 @@ def test_fedavg_running_sum_is_bitwise_equal_to_one_shot_for_any_arrival_order()
     torch.testing.assert_close(want, ref, rtol=1e-6, atol=1e-6)
 
 
+def test_fedavg_partial_aggregates_are_exact_while_models_arrive_concurrently(monkeypatch):
+    """Receive threads fold models into the running sum while gossip threads
+    take partial aggregates: every partial must be the average of exactly the
+    contributors it reports (a fold must never write an accumulator a reader
+    already took -- ADVICE r3 high), and the final aggregate stays bitwise equal
+    to the one-shot average."""
+    import threading
+    import time
+
+    import torch
+
+    from p2pfl_amd.learning.aggregators import fedavg as fedavg_mod
+    from p2pfl_amd.learning.aggregators.fedavg import FedAvg
+    from p2pfl_amd.learning.arena import flatten
+
+    real_flatten = fedavg_mod.flatten
+
+    def slow_flatten(*a, **k):  # widen the window between taking the sum and launching on it
+        time.sleep(0.0005)
+        return real_flatten(*a, **k)
+
+    monkeypatch.setattr(fedavg_mod, "flatten", slow_flatten)
+    names = [f"n{i}" for i in range(8)]
+    rng = torch.Generator().manual_seed(3)
+    models = {n: flatten({"w": torch.randn(64, 33, generator=rng), "b": torch.randn(9, generator=rng)}) for n in names}
+    weights = {n: 50 + 13 * i for i, n in enumerate(names)}
+
+    def expected(contribs):
+        tot = sum(weights[c] for c in contribs)
+        return sum(models[c].flat.double() * weights[c] for c in contribs) / tot
+
+    oneshot = FedAvg()
+    oneshot.running_sum = False
+    oneshot.set_nodes_to_aggregate(names)
+    for n in names:
+        oneshot.add_model(models[n], [n], weights[n])
+    want = oneshot.wait_and_get_aggregation(timeout=1).flat.clone()
+
+    for trial in range(6):
+        agg = FedAvg()
+        agg.set_nodes_to_aggregate(names)
+        errors = []
+        stop = threading.Event()
+        order = names[trial % 8:] + names[: trial % 8]
+
+        def receiver(part):
+            for n in part:
+                agg.add_model(models[n], [n], weights[n])
+                time.sleep(0.001)
+
+        def gossiper(excl):
+            while not stop.is_set():
+                model, contribs, w = agg.get_partial_aggregation(excl)
+                if model is None:
+                    continue
+                assert w == sum(weights[c] for c in contribs)
+                got = (model.flat if hasattr(model, "flat") else model).double()
+                if not torch.allclose(got, expected(contribs), rtol=1e-5, atol=1e-5):
+                    errors.append(sorted(contribs))
+
+        rx = [threading.Thread(target=receiver, args=(order[i::2],)) for i in range(2)]
+        gx = [threading.Thread(target=gossiper, args=(ex,)) for ex in ([], [names[1]], [names[6]])]
+        for t in gx + rx:
+            t.start()
+        for t in rx:
+            t.join()
+        stop.set()
+        for t in gx:
+            t.join()
+        assert not errors, f"wrong partial aggregates for {errors[:3]}"
+        assert torch.equal(agg.wait_and_get_aggregation(timeout=1).flat, want)
+
+
 def test_check_finite_debug_mode_names_the_first_bad_tensor(monkeypatch):
     import pytest
     import torch
