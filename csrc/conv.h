@@ -35,6 +35,22 @@ void conv_dgrad(const ConvShape& s, const uint16_t* dy, const uint16_t* w, void*
 void conv_wgrad(const ConvShape& s, const uint16_t* dy, const uint16_t* x, void* out, int out_bf16, const SplitK& k,
                 int variant, hipStream_t st);
 
+// Small-C direct convolution (the 3-channel stem, csrc/stem.hip).  x is fp32
+// (xtype 0), bf16 (1) or uint8 (2) with arbitrary element strides, scaled by
+// xscale and rounded to bf16; w is (O, kh, kw, C) bf16, y (N, OH, OW, O) bf16.
+// O % 16 == 0 (forward) and O in {32, 64} (wgrad); kh * kw * C <= 160.
+struct StemShape {
+  int N, H, W, C, O, OH, OW, kh, kw, stride, pad;
+  int64_t sn, sc, sh, sw;
+  float xscale;
+};
+void stem_fwd(const StemShape& s, const void* x, int xtype, const uint16_t* w, uint16_t* y, hipStream_t st);
+// part: fp32 workspace of stem_wgrad_parts(N, OH, OW) * O * kh * kw * C elements;
+// dw (O, kh, kw, C) bf16 (out_bf16) or fp32.
+int stem_wgrad_parts(int N, int OH, int OW);
+void stem_wgrad(const StemShape& s, const void* x, int xtype, const uint16_t* dy, float* part, void* dw, int out_bf16,
+                hipStream_t st);
+
 // out[i] = sum_s slabs[s][i] (fp32 in; bf16 or fp32 out), n % 4 == 0.
 void slab_sum(const float* slabs, int splits, int64_t n, void* out, int out_bf16, hipStream_t st);
 

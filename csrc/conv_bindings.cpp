@@ -165,9 +165,85 @@ void slab_sum(torch::Tensor slabs, torch::Tensor out) {
                stream_of(out));
 }
 
+// ---- small-C direct convolution (stem) ----------------------------------------------
+p2::StemShape stem_shape(const torch::Tensor& x, const torch::Tensor& w, int64_t stride, int64_t pad, double xscale,
+                         int& xtype, const char* who) {
+  TORCH_CHECK(x.is_cuda() && x.dim() == 4, who, ": x must be a 4-D GPU tensor (N, C, H, W) in any memory layout");
+  TORCH_CHECK(x.scalar_type() == torch::kFloat32 || x.scalar_type() == torch::kBFloat16 || x.scalar_type() == torch::kUInt8,
+              who, ": x must be fp32, bf16 or uint8");
+  xtype = x.scalar_type() == torch::kFloat32 ? 0 : (x.scalar_type() == torch::kBFloat16 ? 1 : 2);
+  check_nhwc(w, "w");
+  TORCH_CHECK(w.size(3) == x.size(1), who, ": channel mismatch");
+  TORCH_CHECK(stride >= 1 && stride <= 4 && pad >= 0 && pad <= 8, who, ": stride 1-4, pad 0-8");
+  p2::StemShape s{};
+  s.N = int(x.size(0));
+  s.C = int(x.size(1));
+  s.H = int(x.size(2));
+  s.W = int(x.size(3));
+  s.O = int(w.size(0));
+  s.kh = int(w.size(1));
+  s.kw = int(w.size(2));
+  s.stride = int(stride);
+  s.pad = int(pad);
+  s.OH = out_size(s.H, s.kh, s.stride, s.pad, 1);
+  s.OW = out_size(s.W, s.kw, s.stride, s.pad, 1);
+  TORCH_CHECK(s.OH >= 1 && s.OW >= 1, who, ": empty output");
+  TORCH_CHECK(s.kh * s.kw * s.C <= 160 && s.O % 16 == 0 && s.O <= 256, who, ": needs kh*kw*C <= 160, O % 16 == 0, O <= 256");
+  TORCH_CHECK(s.kh * s.kw * s.C * s.O * 4 <= 40 * 1024, who, ": weight image exceeds the LDS budget");
+  TORCH_CHECK(int64_t(s.N) * s.OH * s.OW < (int64_t(1) << 30) && x.numel() < (int64_t(1) << 31), who, ": size overflow");
+  s.sn = x.stride(0);
+  s.sc = x.stride(1);
+  s.sh = x.stride(2);
+  s.sw = x.stride(3);
+  s.xscale = float(xscale);
+  TORCH_CHECK(x.device() == w.device(), who, ": device mismatch");
+  return s;
+}
+
+// x (N, C, H, W) any layout, w [O, kh, kw, C] bf16  ->  y [N, OH, OW, O] bf16
+void stem_fwd(torch::Tensor x, torch::Tensor w, int64_t stride, int64_t pad, double xscale, torch::Tensor y) {
+  int xtype = 0;
+  const auto s = stem_shape(x, w, stride, pad, xscale, xtype, "stem_fwd");
+  check_nhwc(y, "y");
+  TORCH_CHECK(y.size(0) == s.N && y.size(1) == s.OH && y.size(2) == s.OW && y.size(3) == s.O && y.device() == x.device(),
+              "stem_fwd: y must be [N, OH, OW, O]");
+  const c10::DeviceGuard g(x.device());
+  p2::stem_fwd(s, x.data_ptr(), xtype, reinterpret_cast<const uint16_t*>(w.data_ptr()),
+               reinterpret_cast<uint16_t*>(y.data_ptr()), stream_of(x));
+}
+
+int64_t stem_wgrad_parts(int64_t N, int64_t OH, int64_t OW) { return p2::stem_wgrad_parts(int(N), int(OH), int(OW)); }
+
+// dy [N, OH, OW, O] bf16, x (N, C, H, W) any layout; w only for its shape -> dw [O, kh, kw, C] bf16 / fp32
+void stem_wgrad(torch::Tensor dy, torch::Tensor x, torch::Tensor w, int64_t stride, int64_t pad, double xscale,
+                torch::Tensor part, torch::Tensor dw) {
+  int xtype = 0;
+  const auto s = stem_shape(x, w, stride, pad, xscale, xtype, "stem_wgrad");
+  TORCH_CHECK(s.O == 32 || s.O == 64, "stem_wgrad: O must be 32 or 64");
+  check_nhwc(dy, "dy");
+  TORCH_CHECK(dy.size(0) == s.N && dy.size(1) == s.OH && dy.size(2) == s.OW && dy.size(3) == s.O, "stem_wgrad: dy shape");
+  const int64_t n = int64_t(s.O) * s.kh * s.kw * s.C;
+  TORCH_CHECK(part.is_cuda() && part.scalar_type() == torch::kFloat32 && part.is_contiguous() &&
+                  part.numel() >= p2::stem_wgrad_parts(s.N, s.OH, s.OW) * n,
+              "stem_wgrad: part must be contiguous fp32 with stem_wgrad_parts * O * kh * kw * C elements");
+  TORCH_CHECK(dw.is_cuda() && dw.is_contiguous() && dw.numel() == n &&
+                  (dw.scalar_type() == torch::kFloat32 || dw.scalar_type() == torch::kBFloat16),
+              "stem_wgrad: dw must be contiguous [O, kh, kw, C] bf16/fp32");
+  TORCH_CHECK(dy.device() == x.device() && part.device() == x.device() && dw.device() == x.device(), "stem_wgrad: device");
+  const c10::DeviceGuard g(x.device());
+  p2::stem_wgrad(s, x.data_ptr(), xtype, reinterpret_cast<const uint16_t*>(dy.data_ptr()), part.data_ptr<float>(),
+                 dw.data_ptr(), dw.scalar_type() == torch::kBFloat16, stream_of(x));
+}
+
 }  // namespace
 
 void register_conv(pybind11::module& m) {
+  m.def("stem_fwd", &stem_fwd, "small-C direct convolution forward (stem)", pybind11::arg("x"), pybind11::arg("w"),
+        pybind11::arg("stride"), pybind11::arg("pad"), pybind11::arg("xscale"), pybind11::arg("y"));
+  m.def("stem_wgrad_parts", &stem_wgrad_parts, "partial rows of the stem weight gradient");
+  m.def("stem_wgrad", &stem_wgrad, "small-C direct convolution weight gradient (stem)", pybind11::arg("dy"),
+        pybind11::arg("x"), pybind11::arg("w"), pybind11::arg("stride"), pybind11::arg("pad"), pybind11::arg("xscale"),
+        pybind11::arg("part"), pybind11::arg("dw"));
   using pybind11::arg;
   m.def("conv_fwd", &conv_fwd, "implicit-GEMM conv forward (NHWC bf16)", arg("x"), arg("w"), arg("stride"), arg("pad"),
         arg("dil"), arg("y"), arg("splits") = 1, arg("variant") = 10, arg("ws") = pybind11::none(),

@@ -31,6 +31,7 @@ from p2pfl_amd.learning.host_completion import HostCompletions
 from p2pfl_amd.learning.torch_learner import TorchLearner
 from p2pfl_amd.management.logger import logger
 from p2pfl_amd.utils.lockcheck import make_lock, make_rlock
+from p2pfl_amd.utils.streams import private_stream
 
 # Several learners (virtual peers on one GPU, each on its own node thread)
 # may capture epoch graphs concurrently: captures are serialised process-wide
@@ -251,14 +252,14 @@ class FusedCNNLearner(TorchLearner):
         self.use_graphs = use_graphs
         self._graphs: Dict[str, _EpochGraph] = {}
         self._lock = make_rlock("FusedCNNLearner._lock")  # fit() -> _validate() re-enters
-        self._stream = torch.cuda.Stream(self.device)
+        self._stream = private_stream(self.device)
         self._dirty_shadows = False
         self._eval_fwd = _EvalForward(self.engine)
         # asynchronous passes: metrics are read back by a completion thread;
         # the validation pass runs on its own stream next to whatever follows
         # the training epoch (the gossip snapshot + RCCL push of the weights)
         self._completions = HostCompletions(self_addr)
-        self._val_stream = torch.cuda.Stream(self.device)
+        self._val_stream = private_stream(self.device)
         self._val_done: Optional[torch.cuda.Event] = None  # last side-stream reader of the arena
         self._fit_done: Optional[torch.cuda.Event] = None  # bounds the host's run-ahead to one fit
 

@@ -28,6 +28,7 @@ import torch
 
 from p2pfl_amd.ops import splitk
 from p2pfl_amd.utils.lockcheck import make_lock
+from p2pfl_amd.utils.streams import private_stream
 
 # virtual peers (one node thread each) may capture concurrently: serialise
 # captures process-wide, capture in thread-local mode (other threads' work stays legal)
@@ -110,7 +111,7 @@ class TrainStepGraph:
         self.key = self.make_key(learner, opt, loader)
         self.idx = torch.zeros(self.B, dtype=torch.int64, device=dev)
         self.gtab = torch.zeros(len(opt.mt.params), dtype=torch.int64, device=dev)
-        self.stream = torch.cuda.Stream(dev)
+        self.stream = private_stream(dev)
         self.graph: Optional[torch.cuda.CUDAGraph] = None
         self.loss: Optional[torch.Tensor] = None
 
@@ -212,7 +213,7 @@ class EvalStepGraph:
         self.idx = torch.zeros(self.B, dtype=torch.int64, device=dev)
         self.keys: list = []
         self.sums: Optional[torch.Tensor] = None
-        self.stream = torch.cuda.Stream(dev)
+        self.stream = private_stream(dev)
         self.graph: Optional[torch.cuda.CUDAGraph] = None
 
     @staticmethod

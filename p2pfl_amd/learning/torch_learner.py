@@ -41,6 +41,7 @@ from p2pfl_amd.learning.exceptions import DecodingParamsError, ModelNotMatchingE
 from p2pfl_amd.learning.learner import NodeLearner
 from p2pfl_amd.learning.wire import decode_params, encode_params
 from p2pfl_amd.management.logger import logger
+from p2pfl_amd.utils.streams import private_stream
 from p2pfl_amd.settings import Settings
 from p2pfl_amd.utils import finite
 
@@ -172,7 +173,7 @@ class TorchLearner(NodeLearner):
         if not want:
             return None
         if self._compute_stream is None:
-            self._compute_stream = torch.cuda.Stream(self.device)
+            self._compute_stream = private_stream(self.device)
         return self._compute_stream
 
     @contextlib.contextmanager

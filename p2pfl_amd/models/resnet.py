@@ -21,7 +21,8 @@ Activations run channels-last on the GPU.  What runs per convolution
   MIOpen convolutions replayed from graphs were not memory-safe
   (``profiles/r3_nan_root_cause.md``); eager steps (short last batches) take
   whichever of the native kernels and MIOpen measured faster;
-* the stem uses ``F.conv2d`` (MIOpen).
+* the 3-channel stem runs the direct small-C kernels of ``csrc/stem.hip``
+  (forward + weight gradient, reading the uint8 / fp32 batch as it comes).
 
 Every ``BatchNorm2d -> (+ shortcut) -> ReLU`` chain runs as the fused HIP kernel of
 ``csrc/batchnorm.hip`` (:func:`~p2pfl_amd.ops.batchnorm.batch_norm_act`).  Optimiser: SGD with momentum 0.9 and weight decay 5e-4 (fused
@@ -38,10 +39,12 @@ from torch import nn
 
 from p2pfl_amd.models.base import FLModule, seed_everything
 from p2pfl_amd.ops.batchnorm import batch_norm_act
-from p2pfl_amd.ops.conv import conv2d
+from p2pfl_amd.ops.conv import conv2d, stem_conv2d, stem_ok
 
 # NHWC activations on the GPU (P2PFL_CHANNELS_LAST=0 keeps NCHW)
 _CHANNELS_LAST = os.environ.get("P2PFL_CHANNELS_LAST", "1") != "0"
+# 3-channel stem on the direct HIP kernels (csrc/stem.hip); P2PFL_NATIVE_STEM=0 restores F.conv2d
+_NATIVE_STEM = os.environ.get("P2PFL_NATIVE_STEM", "1") != "0"
 
 
 def _shortcut(sc: nn.Module, x: torch.Tensor) -> torch.Tensor:
@@ -138,11 +141,18 @@ class ResNet(FLModule):
                 nn.init.zeros_(m.bias)
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
-        if x.dtype == torch.uint8:
-            x = x.float().mul_(1.0 / 255.0)
-        if x.is_cuda and _CHANNELS_LAST:
-            x = x.contiguous(memory_format=torch.channels_last)
-        x = batch_norm_act(conv2d(x, self.stem[0]), self.stem[1])
+        stem = self.stem[0]
+        if _NATIVE_STEM and stem_ok(x, stem):
+            # direct small-C kernel: reads the batch as it is (uint8 with the 1/255 folded
+            # in, or fp32, NCHW) -- no normalisation pass, no channels-last copy, no MIOpen
+            x = stem_conv2d(x, stem, 1.0 / 255.0 if x.dtype == torch.uint8 else 1.0)
+        else:
+            if x.dtype == torch.uint8:
+                x = x.float().mul_(1.0 / 255.0)
+            if x.is_cuda and _CHANNELS_LAST:
+                x = x.contiguous(memory_format=torch.channels_last)
+            x = conv2d(x, stem)
+        x = batch_norm_act(x, self.stem[1])
         if len(self.stem) > 3:
             x = self.stem[3](x)
         x = self.layer4(self.layer3(self.layer2(self.layer1(x))))

@@ -31,7 +31,7 @@ from p2pfl_amd.ops import autotune
 from p2pfl_amd.ops.splitk import counters, slab_elems, tiles_of
 
 # counters a test can read to prove the native path ran
-STATS = {"native_fwd": 0, "torch_fwd": 0, "gemm_1x1_fwd": 0}
+STATS = {"native_fwd": 0, "torch_fwd": 0, "gemm_1x1_fwd": 0, "stem_fwd": 0}
 
 # "native" | "library" | "auto" (measured per shape, ops/autotune.py); env P2PFL_NATIVE_CONV
 _POLICY = autotune.policy("P2PFL_NATIVE_CONV")
@@ -250,6 +250,8 @@ def conv2d(x: torch.Tensor, conv: nn.Conv2d) -> torch.Tensor:
     1x1 convolutions as GEMMs (:func:`conv1x1_gemm`)."""
     if _is_1x1(x, conv):
         return conv1x1_gemm(x, conv)
+    if x.shape[1] < 8 and stem_ok(x, conv) and _POLICY != "library":
+        return stem_conv2d(x, conv)
     # Inside a HIP-graph capture the implicit-GEMM kernels run whatever the
     # eager timing preferred: MIOpen convolutions replayed from captured step
     # graphs corrupted weights as soon as several learners' graphs and eager
@@ -261,6 +263,72 @@ def conv2d(x: torch.Tensor, conv: nn.Conv2d) -> torch.Tensor:
         return _Conv2dNHWC.apply(x, conv.weight, _sym(conv.stride), _sym(conv.padding), _sym(conv.dilation))
     STATS["torch_fwd"] += 1
     return conv(x)
+
+
+# ---- small-C direct convolution: the 3-channel stem (csrc/stem.hip) -------------------
+def stem_ok(x: torch.Tensor, conv: nn.Conv2d) -> bool:
+    """The stem kernels take this convolution: few input channels (kh*kw*C <= 160),
+    O in {32, 64}, bf16 channels-last weight, symmetric stride/padding, no bias, and an
+    input that needs no gradient (it is data)."""
+    from p2pfl_amd.ops import _gpu
+
+    if not _gpu(x) or x.dim() != 4 or x.dtype not in (torch.float32, torch.bfloat16, torch.uint8):
+        return False
+    if torch.is_grad_enabled() and x.requires_grad:
+        return False
+    w = conv.weight
+    if w.dtype != torch.bfloat16 or conv.bias is not None or conv.groups != 1 or conv.padding_mode != "zeros":
+        return False
+    if isinstance(conv.padding, str) or _sym(conv.dilation) != 1:
+        return False
+    stride, pad = _sym(conv.stride), _sym(conv.padding)
+    O, C, kh, kw = w.shape
+    if stride < 1 or stride > 4 or pad < 0 or pad > 8 or C != x.shape[1] or O not in (32, 64):
+        return False
+    if kh * kw * C > 160 or kh * kw * C * O * 4 > 40 * 1024:
+        return False
+    return w.permute(0, 2, 3, 1).is_contiguous() and w.data_ptr() % 16 == 0
+
+
+class _StemConv(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, w, stride, pad, xscale):
+        w4 = w.permute(0, 2, 3, 1)
+        N, _, H, W_ = x.shape
+        O, kh, kw = w4.shape[0], w4.shape[1], w4.shape[2]
+        OH, OW = out_hw(H, W_, (kh, kw), stride, pad, 1)
+        y4 = torch.empty((N, OH, OW, O), dtype=torch.bfloat16, device=x.device)
+        _C().stem_fwd(x, w4, stride, pad, xscale, y4)
+        ctx.save_for_backward(x, w)
+        ctx.cfg = (stride, pad, xscale)
+        return y4.permute(0, 3, 1, 2)
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, w = ctx.saved_tensors
+        stride, pad, xscale = ctx.cfg
+        dw = None
+        if ctx.needs_input_grad[1]:
+            if dy.dtype != torch.bfloat16:
+                dy = dy.to(torch.bfloat16)
+            dy4 = dy.permute(0, 2, 3, 1)
+            if not dy4.is_contiguous() or dy4.data_ptr() % 16:
+                dy4 = dy4.contiguous()
+            w4 = w.permute(0, 2, 3, 1)
+            C = _C()
+            parts = C.stem_wgrad_parts(dy4.shape[0], dy4.shape[1], dy4.shape[2])
+            part = torch.empty(parts * w4.numel(), dtype=torch.float32, device=w.device)
+            dw4 = torch.empty(w4.shape, dtype=w.dtype, device=w.device)
+            C.stem_wgrad(dy4, x, w4, stride, pad, xscale, part, dw4)
+            dw = dw4.permute(0, 3, 1, 2)
+        return None, dw, None, None, None
+
+
+def stem_conv2d(x: torch.Tensor, conv: nn.Conv2d, xscale: float = 1.0) -> torch.Tensor:
+    """``conv(x * xscale)`` on the small-C direct kernels (:func:`stem_ok` must hold); x in
+    any layout / fp32, bf16 or uint8; returns a channels-last bf16 NCHW tensor."""
+    STATS["stem_fwd"] += 1
+    return _StemConv.apply(x, conv.weight, _sym(conv.stride), _sym(conv.padding), float(xscale))
 
 
 def conv2d_reference(x: torch.Tensor, w: torch.Tensor, stride: int, pad: int, dil: int) -> torch.Tensor:

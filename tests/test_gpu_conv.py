@@ -222,3 +222,79 @@ def test_autotune_picks_and_caches_a_path(monkeypatch):
     torch.testing.assert_close(y.float(), ref, atol=3e-2, rtol=2e-2)
     ops.conv2d(x.clone().requires_grad_(), conv)
     assert len(autotune.choices()) == 1  # cached
+
+
+# ---- small-C direct convolution (3-channel stem, csrc/stem.hip) -------------------------
+STEM_CASES = [
+    # N, C, H, W, O, k, stride, pad, x layout
+    (4, 3, 32, 32, 64, 3, 1, 1, "nchw"),
+    (3, 3, 17, 13, 64, 3, 1, 1, "cl"),
+    (2, 3, 40, 40, 64, 7, 2, 3, "nchw"),
+    (5, 1, 28, 28, 32, 5, 1, 2, "nchw"),
+    (2, 4, 9, 11, 32, 3, 2, 0, "cl"),
+]
+
+
+@pytest.mark.parametrize("N,C,H,W,O,k,s,p,layout", STEM_CASES)
+@pytest.mark.parametrize("xdtype", [torch.float32, torch.uint8])
+def test_stem_conv_fwd_wgrad_vs_fp32(N, C, H, W, O, k, s, p, layout, xdtype):
+    """Forward and weight gradient of the direct small-C kernels against fp32 PyTorch on
+    the same bf16-rounded operands (input read in its own layout / dtype, 1/255 folded)."""
+    g = torch.Generator(device="cuda").manual_seed(N * 100 + k)
+    if xdtype == torch.uint8:
+        x = torch.randint(0, 256, (N, C, H, W), device="cuda", generator=g, dtype=torch.uint8)
+        scale = 1.0 / 255.0
+        xref = (x.float() * scale).to(torch.bfloat16).float()
+    else:
+        x = torch.randn(N, C, H, W, device="cuda", generator=g)
+        scale = 1.0
+        xref = x.to(torch.bfloat16).float()
+    if layout == "cl":
+        x = x.contiguous(memory_format=torch.channels_last)
+    conv = nn.Conv2d(C, O, k, s, p, bias=False).cuda()
+    with torch.no_grad():
+        conv.weight.copy_(torch.randn(O, C, k, k, device="cuda", generator=g) / (C * k * k) ** 0.5)
+    conv.weight.data = conv.weight.data.to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    assert conv_ops.stem_ok(x, conv)
+    y = conv_ops.stem_conv2d(x, conv, scale)
+    wr = conv.weight.detach().float().requires_grad_()
+    yr = F.conv2d(xref, wr, None, s, p)
+    assert y.shape == yr.shape and y.is_contiguous(memory_format=torch.channels_last)
+    torch.testing.assert_close(y.float(), yr, atol=2e-2, rtol=1e-2)
+    dy = torch.randn(yr.shape, device="cuda", generator=g).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    y.backward(dy)
+    yr.backward(dy.float())
+    scale_g = wr.grad.abs().max().item()
+    torch.testing.assert_close(conv.weight.grad.float(), wr.grad, atol=1e-2 * scale_g, rtol=1e-2)
+    assert conv.weight.grad.is_contiguous(memory_format=torch.channels_last)
+
+
+def test_stem_wgrad_is_deterministic():
+    x = torch.rand(8, 3, 32, 32, device="cuda")
+    conv = nn.Conv2d(3, 64, 3, 1, 1, bias=False).cuda()
+    conv.weight.data = conv.weight.data.to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    dy = torch.randn(8, 64, 32, 32, device="cuda").to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    grads = []
+    for _ in range(3):
+        conv.weight.grad = None
+        conv_ops.stem_conv2d(x, conv).backward(dy)
+        grads.append(conv.weight.grad.clone())
+    assert all(torch.equal(grads[0], g) for g in grads[1:])
+
+
+def test_resnet_stem_runs_native(monkeypatch):
+    """ResNet's forward sends the 3-channel stem to the direct kernels (no F.conv2d)."""
+    from p2pfl_amd.models.resnet import ResNet18
+
+    m = ResNet18().cuda()
+    for mod in m.modules():
+        if isinstance(mod, nn.Conv2d):
+            mod.weight.data = mod.weight.data.to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    calls = []
+    monkeypatch.setattr(F, "conv2d", lambda *a, **k: calls.append(a) or torch.zeros(()))
+    before = conv_ops.STATS["stem_fwd"]
+    x = torch.randint(0, 256, (2, 3, 32, 32), dtype=torch.uint8, device="cuda")
+    m.eval()
+    with torch.no_grad(), torch.autocast("cuda", dtype=torch.bfloat16):
+        y = m(x)
+    assert conv_ops.STATS["stem_fwd"] == before + 1 and not calls and y.shape == (2, 10)

@@ -53,7 +53,7 @@ class _FakeOpt:
 
 @pytest.fixture
 def fake_cuda(monkeypatch):
-    monkeypatch.setattr(torch.cuda, "Stream", lambda *a, **k: _FakeStream())
+    monkeypatch.setattr(step_graph, "private_stream", lambda *a, **k: _FakeStream())
     monkeypatch.setattr(torch.cuda, "current_stream", lambda *a, **k: _FakeStream())
     monkeypatch.setattr(torch.cuda, "stream", lambda s: contextlib.nullcontext())
     monkeypatch.setattr(torch.cuda, "synchronize", lambda *a, **k: None)
