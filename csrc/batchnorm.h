@@ -29,6 +29,11 @@ void bn_fwd_train(bool bf16, const void* x, const void* res, const float* w, con
                   float* run_var, int64_t* nbt, float momentum, float eps, void* y, float* mean, float* rstd,
                   float* coef, float* part, int* ctr, int M, int C, bool relu, hipStream_t s);
 
+// Apply pass only, with coefficients [mean | w * rstd | b] computed elsewhere
+// (the statistics epilogue of a convolution, gemm_core.h BnEpi).
+void bn_apply_train(bool bf16, const void* x, const void* res, const float* coef, void* y, int M, int C, bool relu,
+                    hipStream_t s);
+
 // Inference forward with running statistics (one launch; coef unused, kept for
 // the call signature).  w, b, run_mean, run_var must be 16-byte aligned.
 void bn_fwd_eval(bool bf16, const void* x, const void* res, const float* w, const float* b, const float* run_mean,

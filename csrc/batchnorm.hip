@@ -688,6 +688,16 @@ static void fwd_eval_t(const void* xv, const void* rv, const float* w, const flo
     hipLaunchKernelGGL((bn_apply_fwd_kernel<T, false, false>), grid, blk, 0, s, x, r, rm, w, b, rvar, eps, y, n8, C);
 }
 
+void bn_apply_train(bool bf16, const void* x, const void* res, const float* coef, void* y, int M, int C, bool relu,
+                    hipStream_t s) {
+  if (bf16)
+    apply_fwd<uint16_t>(static_cast<const uint16_t*>(x), static_cast<const uint16_t*>(res), coef, static_cast<uint16_t*>(y),
+                        M, C, relu, s);
+  else
+    apply_fwd<float>(static_cast<const float*>(x), static_cast<const float*>(res), coef, static_cast<float*>(y), M, C,
+                     relu, s);
+}
+
 void bn_fwd_eval(bool bf16, const void* x, const void* res, const float* w, const float* b, const float* run_mean,
                  const float* run_var, float eps, void* y, float* coef, int M, int C, bool relu, hipStream_t s) {
   if (bf16)

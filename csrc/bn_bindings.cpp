@@ -89,6 +89,25 @@ std::vector<torch::Tensor> bn_fwd_train(torch::Tensor x, torch::Tensor w, torch:
   return {y, mean, rstd};
 }
 
+// y = act((x - coef[0]) * coef[1] + coef[2] [+ residual]) with precomputed coefficients
+torch::Tensor bn_apply_train(torch::Tensor x, c10::optional<torch::Tensor> residual, torch::Tensor coef, bool relu) {
+  const c10::DeviceGuard g(x.device());
+  check_shape(x);
+  const int64_t M = x.size(0), C = x.size(1);
+  const bool bf = act(x, x, "x");
+  const void* rp = nullptr;
+  if (residual.has_value() && residual->defined()) {
+    act(*residual, x, "residual");
+    rp = residual->data_ptr();
+  }
+  TORCH_CHECK(coef.device() == x.device() && coef.is_contiguous() && coef.scalar_type() == torch::kFloat32 &&
+                  coef.numel() == 3 * C,
+              "coef must be a contiguous fp32 [3, C] tensor on x's device");
+  auto y = torch::empty_like(x);
+  p2bn::bn_apply_train(bf, x.data_ptr(), rp, coef.data_ptr<float>(), y.data_ptr(), int(M), int(C), relu, stream());
+  return y;
+}
+
 torch::Tensor bn_fwd_eval(torch::Tensor x, torch::Tensor w, torch::Tensor b, c10::optional<torch::Tensor> residual,
                           torch::Tensor running_mean, torch::Tensor running_var, double eps, bool relu) {
   const c10::DeviceGuard g(x.device());
@@ -143,6 +162,7 @@ void register_bn(pybind11::module& m) {
         py::arg("running_mean") = py::none(), py::arg("running_var") = py::none(),
         py::arg("num_batches_tracked") = py::none(), py::arg("momentum") = 0.1, py::arg("eps") = 1e-5,
         py::arg("relu") = true, py::arg("counters") = py::none());
+  f.def("apply_train", &bn_apply_train, py::arg("x"), py::arg("residual"), py::arg("coef"), py::arg("relu"));
   f.def("fwd_eval", &bn_fwd_eval, py::arg("x"), py::arg("w"), py::arg("b"), py::arg("residual") = py::none(),
         py::arg("running_mean"), py::arg("running_var"), py::arg("eps") = 1e-5, py::arg("relu") = true);
   f.def("bwd", &bn_bwd, py::arg("dy"), py::arg("y"), py::arg("x"), py::arg("w"), py::arg("mean"), py::arg("rstd"),

@@ -25,8 +25,10 @@ struct SplitK {
   float* ws = nullptr;
   int* counters = nullptr;
 };
+// bn (optional): BatchNorm training statistics of the bf16 output computed in the
+// launch (gemm.h BnEpi); needs splits == 1 or in-launch split-K (counters).
 void conv_fwd(const ConvShape& s, const uint16_t* x, const uint16_t* w, void* y, const SplitK& k, int variant,
-              hipStream_t st);
+              hipStream_t st, const BnEpi* bn = nullptr);
 void conv_dgrad(const ConvShape& s, const uint16_t* dy, const uint16_t* w, void* dx, const SplitK& k, int variant,
                 hipStream_t st);
 // dw[O][kh*kw*C] = sum over output pixels of dy (x) im2col(x)    (O % 8 == 0, C % 8 == 0)

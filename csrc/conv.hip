@@ -226,10 +226,11 @@ __global__ __launch_bounds__(64) void slab_sum_kernel(const float* __restrict__ 
 namespace p2 {
 
 void conv_fwd(const ConvShape& s, const uint16_t* x, const uint16_t* w, void* y, const SplitK& k, int variant,
-              hipStream_t st) {
+              hipStream_t st, const BnEpi* bn) {
   using namespace p2gemm;
   const int M = s.N * s.OH * s.OW, K = s.kh * s.kw * s.C;
-  const GemmParams p = base_params(M, s.O, K, y, s.O, k.splits <= 1 || k.counters, k, variant);
+  GemmParams p = base_params(M, s.O, K, y, s.O, k.splits <= 1 || k.counters, k, variant);
+  if (bn) p.bn = *bn;
   const ConvFwdA la{x, make_fastdiv(s.OH * s.OW), make_fastdiv(s.OW), M, s.H, s.W, s.C, s.stride, s.pad, s.dil, s.kw};
   launch(p, la, PlainK{w, K, s.O, K}, st);
 }

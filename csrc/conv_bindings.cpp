@@ -102,6 +102,64 @@ void conv_fwd(torch::Tensor x, torch::Tensor w, int64_t stride, int64_t pad, int
                y.data_ptr(), k, int(variant), stream_of(x));
 }
 
+int bn_groups(int64_t tiles_m) { return int((tiles_m + 15) / 16); }
+
+// conv_fwd + BatchNorm training statistics in the launch (gemm.h BnEpi): part is fp32
+// (tiles_m + groups) * 2 * O, cnt int32 tiles_n * (groups + 1) zeroed; mean / rstd [O]
+// and coef [3, O] out; running_mean / running_var / nbt updated when given.
+void conv_fwd_bn(torch::Tensor x, torch::Tensor w, int64_t stride, int64_t pad, int64_t dil, torch::Tensor y,
+                 int64_t splits, int64_t variant, OptT ws, OptT counters, torch::Tensor part, torch::Tensor cnt,
+                 torch::Tensor bn_w, torch::Tensor bn_b, OptT run_mean, OptT run_var, OptT nbt, torch::Tensor mean,
+                 torch::Tensor rstd, torch::Tensor coef, double eps, double momentum) {
+  check_nhwc(x, "x");
+  check_nhwc(w, "w");
+  TORCH_CHECK(w.size(3) == x.size(3), "conv_fwd_bn: channel mismatch");
+  const auto s = make_shape(x.size(0), x.size(1), x.size(2), x.size(3), w.size(0), w.size(1), w.size(2), stride, pad, dil);
+  TORCH_CHECK(s.C % 64 == 0 && s.O % 8 == 0, "conv_fwd_bn: needs C % 64 == 0 and O % 8 == 0");
+  const int64_t M = int64_t(s.N) * s.OH * s.OW;
+  const auto k = make_splitk(splits, ws, counters, M, s.O, x, "conv_fwd_bn");
+  TORCH_CHECK(k.splits == 1 || k.counters, "conv_fwd_bn: split-K needs the in-launch reduction (counters)");
+  check_out(y, k, s.N, s.OH, s.OW, s.O, "conv_fwd_bn");
+  const int64_t tiles_m = (M + 127) / 128, tiles_n = (s.O + 127) / 128, groups = bn_groups(tiles_m);
+  auto f32v = [&](const torch::Tensor& t, int64_t n, const char* name) {
+    TORCH_CHECK(t.is_cuda() && t.device() == x.device() && t.scalar_type() == torch::kFloat32 && t.is_contiguous() &&
+                    t.numel() == n,
+                "conv_fwd_bn: ", name, " must be a contiguous fp32 tensor of ", n, " elements on x's device");
+    return t.data_ptr<float>();
+  };
+  p2::BnEpi e{};
+  TORCH_CHECK(part.is_cuda() && part.device() == x.device() && part.scalar_type() == torch::kFloat32 &&
+                  part.is_contiguous() && part.numel() >= (tiles_m + groups) * 2 * s.O,
+              "conv_fwd_bn: part must hold (tiles_m + groups) * 2 * O fp32");
+  TORCH_CHECK(cnt.is_cuda() && cnt.device() == x.device() && cnt.scalar_type() == torch::kInt32 && cnt.is_contiguous() &&
+                  cnt.numel() >= tiles_n * (groups + 1),
+              "conv_fwd_bn: cnt must hold tiles_n * (groups + 1) zeroed int32");
+  e.part = part.data_ptr<float>();
+  e.cnt = cnt.data_ptr<int>();
+  e.w = f32v(bn_w, s.O, "bn weight");
+  e.b = f32v(bn_b, s.O, "bn bias");
+  const bool track = run_mean.has_value() && run_mean->defined();
+  TORCH_CHECK(track == (run_var.has_value() && run_var->defined()), "conv_fwd_bn: running_mean and running_var go together");
+  if (track) {
+    e.run_mean = f32v(*run_mean, s.O, "running_mean");
+    e.run_var = f32v(*run_var, s.O, "running_var");
+  }
+  if (nbt.has_value() && nbt->defined()) {
+    TORCH_CHECK(nbt->device() == x.device() && nbt->scalar_type() == torch::kInt64 && nbt->numel() == 1,
+                "conv_fwd_bn: num_batches_tracked must be an int64 scalar on x's device");
+    e.nbt = nbt->data_ptr<int64_t>();
+  }
+  e.mean = f32v(mean, s.O, "mean");
+  e.rstd = f32v(rstd, s.O, "rstd");
+  e.coef = f32v(coef, 3 * s.O, "coef");
+  e.eps = float(eps);
+  e.momentum = float(momentum);
+  TORCH_CHECK(x.device() == w.device() && y.device() == x.device(), "conv_fwd_bn: device mismatch");
+  const c10::DeviceGuard g(x.device());
+  p2::conv_fwd(s, reinterpret_cast<const uint16_t*>(x.data_ptr()), reinterpret_cast<const uint16_t*>(w.data_ptr()),
+               y.data_ptr(), k, int(variant), stream_of(x), &e);
+}
+
 // dy [N, OH, OW, O], w [O, kh, kw, C]  ->  dx [N, H, W, C]  (dx_shape = (N, H, W, C), dx may hold slabs)
 void conv_dgrad(torch::Tensor dy, torch::Tensor w, int64_t stride, int64_t pad, int64_t dil, torch::Tensor dx,
                 std::vector<int64_t> dx_shape, int64_t splits, int64_t variant, OptT ws, OptT counters) {
@@ -238,13 +296,17 @@ void stem_wgrad(torch::Tensor dy, torch::Tensor x, torch::Tensor w, int64_t stri
 }  // namespace
 
 void register_conv(pybind11::module& m) {
+  using pybind11::arg;
   m.def("stem_fwd", &stem_fwd, "small-C direct convolution forward (stem)", pybind11::arg("x"), pybind11::arg("w"),
         pybind11::arg("stride"), pybind11::arg("pad"), pybind11::arg("xscale"), pybind11::arg("y"));
+  m.def("conv_fwd_bn", &conv_fwd_bn, "implicit-GEMM conv forward + BatchNorm statistics in the launch", arg("x"),
+        arg("w"), arg("stride"), arg("pad"), arg("dil"), arg("y"), arg("splits"), arg("variant"), arg("ws"),
+        arg("counters"), arg("part"), arg("cnt"), arg("bn_w"), arg("bn_b"), arg("run_mean"), arg("run_var"), arg("nbt"),
+        arg("mean"), arg("rstd"), arg("coef"), arg("eps"), arg("momentum"));
   m.def("stem_wgrad_parts", &stem_wgrad_parts, "partial rows of the stem weight gradient");
   m.def("stem_wgrad", &stem_wgrad, "small-C direct convolution weight gradient (stem)", pybind11::arg("dy"),
         pybind11::arg("x"), pybind11::arg("w"), pybind11::arg("stride"), pybind11::arg("pad"), pybind11::arg("xscale"),
         pybind11::arg("part"), pybind11::arg("dw"));
-  using pybind11::arg;
   m.def("conv_fwd", &conv_fwd, "implicit-GEMM conv forward (NHWC bf16)", arg("x"), arg("w"), arg("stride"), arg("pad"),
         arg("dil"), arg("y"), arg("splits") = 1, arg("variant") = 10, arg("ws") = pybind11::none(),
         arg("counters") = pybind11::none());

@@ -18,6 +18,28 @@ namespace p2 {
 // last slice to finish a tile reduces the tile in the same launch and runs
 // the epilogue into c.  `counters` holds one int per output tile, zero
 // before the launch; the kernel leaves it zero again.
+// BatchNorm training statistics emitted by a GEMM / convolution epilogue (bf16 C
+// only): every output tile writes per-column (mean, M2) of its bf16-rounded
+// values as a partial; the last tile of a group of 16 tile-rows combines its
+// group (Chan's parallel formula, fixed order), the last group finalizes the
+// column: batch mean / rstd, the apply coefficients [mean | w * rstd | b] of
+// csrc/batchnorm.hip, running statistics (momentum, unbiased variance) and
+// num_batches_tracked.  `part` holds (tiles_m + groups) * 2 * N floats; `cnt`
+// tiles_n * (groups + 1) ints, zero before the launch and left zero.
+struct BnEpi {
+  float* part;
+  int* cnt;
+  const float* w;
+  const float* b;
+  float* run_mean;  // optional (no running statistics when null)
+  float* run_var;
+  int64_t* nbt;     // optional
+  float* mean;      // [N] out
+  float* rstd;      // [N] out
+  float* coef;      // [3N] out
+  float eps, momentum;
+};
+
 struct GemmParams {
   const uint16_t* a;
   const uint16_t* b;
@@ -34,6 +56,7 @@ struct GemmParams {
   int splits;
   float* ws;      // split-K workspace for the in-launch reduction
   int* counters;  // per-tile arrival counters (see above), or null
+  BnEpi bn;       // BatchNorm statistics epilogue when bn.part != null
   int variant;  // tuning experiments: bit0 setprio around MFMAs, bit1 A-panel tile order, bit2 no XCD remap, bit3 single LDS buffer (4 workgroups / CU), bit4/bit5 timing probes (no stores / no K loop), bit6 256 x 256 tile (8 waves), bit7 no DMA after the prologue (probe), bit8 legacy panel tile order instead of grouped (bit1 then picks A- vs B-panel order), bits 9-10 where the double-buffer prefetch is issued (0 before the K-tile's fragment reads, 1 after the first ones, 2 one chunk per k-substep), bit11 the ping-pong 256 x 256 pipeline of gemm_pp.hip (continuous per-phase DMA, staggered wave halves)
 };
 

@@ -262,6 +262,122 @@ struct SlabGeom {
   static_assert(TILEF == CFG::BM * CFG::BN, "fragment slab covers the tile");
 };
 
+// ---- BatchNorm statistics epilogue (GemmParams::bn) -------------------------------
+// Running (count, mean, M2) of one column; Chan et al.'s pairwise update.
+struct Moments {
+  float n, mean, m2;
+};
+P2_DEVICE Moments moments_merge(Moments a, const Moments& b) {
+  if (b.n <= 0.f) return a;
+  if (a.n <= 0.f) return b;
+  const float n = a.n + b.n, d = b.mean - a.mean, f = b.n / n;
+  a.mean = fmaf(d, f, a.mean);
+  a.m2 = a.m2 + b.m2 + d * d * a.n * f;
+  a.n = n;
+  return a;
+}
+P2_DEVICE void st_sc1(float* base, int n, int idx, float v) {
+  const auto rs = __builtin_amdgcn_make_buffer_rsrc(base, 0, n * 4, 0x00020000);
+  __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), rs, idx * 4, 0, 16);
+}
+P2_DEVICE float ld_sc1(const float* base, int n, int idx) {
+  const auto rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(base), 0, n * 4, 0x00020000);
+  return __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rs, idx * 4, 0, 16));
+}
+// Arrival ticket of a workgroup whose sc1 stores must be visible to the last
+// arriver (same hand-off as the split-K reduction; see the hardware note
+// there).  True in the last of `total` arrivals, which resets the counter.
+P2_DEVICE bool last_arrival(int* ctr, int total, int* flag_lds) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const int old = __hip_atomic_fetch_add(ctr, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    flag_lds[0] = old == total - 1;
+    if (old == total - 1) __hip_atomic_store(ctr, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  __syncthreads();
+  return flag_lds[0] != 0;
+}
+
+constexpr int kBnGroup = 16;  // tile rows per first-level group
+
+// The tile's column moments (`mo`, held by threads tid < BN for column n0 + tid)
+// go out as this tile's partial; the two-level reduction finalizes the columns.
+template <class CFG>
+P2_DEVICE void bn_epilogue_reduce(const GemmParams& p, Moments mo, int tm, int tn, int tiles_m, char* smem) {
+  const BnEpi& e = p.bn;
+  const int tid = threadIdx.x, N = p.N, n0 = tn * CFG::BN;
+  const int groups = (tiles_m + kBnGroup - 1) / kBnGroup, g = tm / kBnGroup;
+  const int gsize = min(kBnGroup, tiles_m - g * kBnGroup);
+  const int nparts = (tiles_m + groups) * 2 * N;
+  const int n = n0 + tid;
+  const bool col = tid < CFG::BN && n < N;
+  if (col) {
+    st_sc1(e.part, nparts, (tm * 2) * N + n, mo.mean);
+    st_sc1(e.part, nparts, (tm * 2 + 1) * N + n, mo.m2);
+  }
+  int* flag = reinterpret_cast<int*>(smem);
+  auto tile_rows = [&](int t) { return float(min(CFG::BM, p.M - t * CFG::BM)); };
+  if (!last_arrival(e.cnt + tn * (groups + 1) + g, gsize, flag)) return;
+  // level 1: combine the group's tile partials in tile order
+  Moments acc{0.f, 0.f, 0.f};
+  if (col) {
+    float mv[kBnGroup], m2v[kBnGroup];
+#pragma unroll
+    for (int i = 0; i < kBnGroup; ++i) {
+      const int t = g * kBnGroup + i;
+      mv[i] = i < gsize ? ld_sc1(e.part, nparts, (t * 2) * N + n) : 0.f;
+      m2v[i] = i < gsize ? ld_sc1(e.part, nparts, (t * 2 + 1) * N + n) : 0.f;
+    }
+#pragma unroll
+    for (int i = 0; i < kBnGroup; ++i)
+      if (i < gsize) acc = moments_merge(acc, Moments{tile_rows(g * kBnGroup + i), mv[i], m2v[i]});
+  }
+  if (groups > 1) {
+    if (col) {
+      st_sc1(e.part, nparts, ((tiles_m + g) * 2) * N + n, acc.mean);
+      st_sc1(e.part, nparts, ((tiles_m + g) * 2 + 1) * N + n, acc.m2);
+    }
+    if (!last_arrival(e.cnt + tn * (groups + 1) + groups, groups, flag)) return;
+    acc = Moments{0.f, 0.f, 0.f};
+    if (col) {
+      for (int g0 = 0; g0 < groups; g0 += kBnGroup) {
+        float mv[kBnGroup], m2v[kBnGroup];
+#pragma unroll
+        for (int i = 0; i < kBnGroup; ++i) {
+          const int gg = g0 + i;
+          mv[i] = gg < groups ? ld_sc1(e.part, nparts, ((tiles_m + gg) * 2) * N + n) : 0.f;
+          m2v[i] = gg < groups ? ld_sc1(e.part, nparts, ((tiles_m + gg) * 2 + 1) * N + n) : 0.f;
+        }
+#pragma unroll
+        for (int i = 0; i < kBnGroup; ++i) {
+          const int gg = g0 + i;
+          if (gg >= groups) continue;
+          float rows = 0.f;
+          for (int t = gg * kBnGroup; t < min(tiles_m, (gg + 1) * kBnGroup); ++t) rows += tile_rows(t);
+          acc = moments_merge(acc, Moments{rows, mv[i], m2v[i]});
+        }
+      }
+    }
+  }
+  if (!col) return;
+  // finalize column n (same outputs as bn_finalize_fwd_kernel)
+  const float M = float(p.M);
+  const float var = fmaxf(acc.m2 / M, 0.f);
+  const float rs = rsqrtf(var + e.eps);
+  e.mean[n] = acc.mean;
+  e.rstd[n] = rs;
+  e.coef[n] = acc.mean;
+  e.coef[N + n] = e.w[n] * rs;
+  e.coef[2 * N + n] = e.b[n];
+  if (e.run_mean) {
+    const float unb = p.M > 1 ? acc.m2 / (M - 1.f) : var;
+    e.run_mean[n] = (1.f - e.momentum) * e.run_mean[n] + e.momentum * acc.mean;
+    e.run_var[n] = (1.f - e.momentum) * e.run_var[n] + e.momentum * unb;
+  }
+  if (e.nbt && n == 0) e.nbt[0] += 1;
+}
+
 // The whole kernel body.  `p` carries M/N/K, split-K and the epilogue.
 template <class CFG, int NBUF, class LA, class LB>
 P2_DEVICE void gemm_body(const GemmParams& p, const LA& la, const LB& lb, int tiles_m, int tiles_n, char* smem) {
@@ -563,6 +679,13 @@ P2_DEVICE void gemm_body(const GemmParams& p, const LA& la, const LB& lb, int ti
   constexpr int PASSES = ONE ? 1 : CFG::WAVES_M, ROWS = CFG::BM / PASSES;
   static_assert(ROWS * LROW <= smem_bytes<CFG, NBUF>(), "epilogue image must fit the kernel's LDS");
   static_assert((ROWS * CPR) % CFG::NT == 0, "whole chunks per thread");
+  // BatchNorm statistics (p.bn): thread = column tid % BN x row phase tid / BN of
+  // each pass's LDS image (the bf16 values as stored), shifted single-pass sums
+  // per pass, merged across passes and phases in fixed order
+  constexpr int BNPH = CFG::NT / CFG::BN, PROWS = ROWS / BNPH;
+  const bool bn_on = p.bn.part != nullptr;
+  const int bn_c = tid % CFG::BN, bn_ph = tid / CFG::BN;
+  Moments bn_mo{0.f, 0.f, 0.f};
 #pragma unroll
   for (int pass = 0; pass < PASSES; ++pass) {
     __syncthreads();  // LDS free: main loop (or previous pass) done
@@ -581,6 +704,20 @@ P2_DEVICE void gemm_body(const GemmParams& p, const LA& la, const LB& lb, int ti
           }
     }
     __syncthreads();
+    if (bn_on && n0 + bn_c < p.N) {
+      const int r0 = bn_ph * PROWS, rend = min(PROWS, p.M - (m0 + pass * ROWS + r0));
+      if (rend > 0) {
+        const float x0 = bf16_to_f32(*reinterpret_cast<const uint16_t*>(smem + r0 * LROW + bn_c * 2));
+        float s1 = 0.f, s2 = 0.f;
+        for (int r = 0; r < rend; ++r) {
+          const float d = bf16_to_f32(*reinterpret_cast<const uint16_t*>(smem + (r0 + r) * LROW + bn_c * 2)) - x0;
+          s1 += d;
+          s2 = fmaf(d, d, s2);
+        }
+        const float cnt = float(rend), mu = s1 / cnt;
+        bn_mo = moments_merge(bn_mo, Moments{cnt, x0 + mu, fmaxf(s2 - s1 * mu, 0.f)});
+      }
+    }
 #pragma unroll
     for (int q = 0; q < ROWS * CPR / CFG::NT; ++q) {
       const int chunk = q * CFG::NT + tid, r = chunk / CPR, c = chunk % CPR;
@@ -589,6 +726,23 @@ P2_DEVICE void gemm_body(const GemmParams& p, const LA& la, const LB& lb, int ti
         *reinterpret_cast<uint4*>(reinterpret_cast<uint16_t*>(p.c) + int64_t(m) * p.ldc + n) =
             *reinterpret_cast<const uint4*>(smem + r * LROW + c * 16);
     }
+  }
+  if (bn_on) {
+    // merge the row phases in order (column c's phases sit BN threads apart)
+    __syncthreads();
+    float* red = reinterpret_cast<float*>(smem);
+    red[tid] = bn_mo.n;
+    red[CFG::NT + tid] = bn_mo.mean;
+    red[2 * CFG::NT + tid] = bn_mo.m2;
+    __syncthreads();
+    Moments mo{0.f, 0.f, 0.f};
+    if (tid < CFG::BN)
+      for (int ph = 0; ph < BNPH; ++ph) {
+        const int q = ph * CFG::BN + tid;
+        mo = moments_merge(mo, Moments{red[q], red[CFG::NT + q], red[2 * CFG::NT + q]});
+      }
+    __syncthreads();
+    bn_epilogue_reduce<CFG>(p, mo, tm, tn, tiles_m, smem);
   }
 }
 

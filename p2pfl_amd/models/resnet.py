@@ -39,7 +39,7 @@ from torch import nn
 
 from p2pfl_amd.models.base import FLModule, seed_everything
 from p2pfl_amd.ops.batchnorm import batch_norm_act
-from p2pfl_amd.ops.conv import conv2d, stem_conv2d, stem_ok
+from p2pfl_amd.ops.conv import conv2d, conv_bn_act, stem_conv2d, stem_ok
 
 # NHWC activations on the GPU (P2PFL_CHANNELS_LAST=0 keeps NCHW)
 _CHANNELS_LAST = os.environ.get("P2PFL_CHANNELS_LAST", "1") != "0"
@@ -48,10 +48,10 @@ _NATIVE_STEM = os.environ.get("P2PFL_NATIVE_STEM", "1") != "0"
 
 
 def _shortcut(sc: nn.Module, x: torch.Tensor) -> torch.Tensor:
-    """Identity, or the projection conv + BN (no activation) through the fused BN kernel."""
+    """Identity, or the projection conv + BN (no activation)."""
     if isinstance(sc, nn.Identity):
         return x
-    return batch_norm_act(conv2d(x, sc[0]), sc[1], relu=False)
+    return conv_bn_act(x, sc[0], sc[1], relu=False)
 
 
 class BasicBlock(nn.Module):
@@ -68,8 +68,8 @@ class BasicBlock(nn.Module):
             self.shortcut = nn.Sequential(nn.Conv2d(cin, cout, 1, stride, bias=False), nn.BatchNorm2d(cout))
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
-        out = batch_norm_act(conv2d(x, self.conv1), self.bn1)
-        return batch_norm_act(conv2d(out, self.conv2), self.bn2, residual=_shortcut(self.shortcut, x))
+        out = conv_bn_act(x, self.conv1, self.bn1)
+        return conv_bn_act(out, self.conv2, self.bn2, residual=_shortcut(self.shortcut, x))
 
 
 class Bottleneck(nn.Module):
@@ -89,9 +89,9 @@ class Bottleneck(nn.Module):
             self.shortcut = nn.Sequential(nn.Conv2d(cin, cout, 1, stride, bias=False), nn.BatchNorm2d(cout))
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
-        out = batch_norm_act(conv2d(x, self.conv1), self.bn1)
-        out = batch_norm_act(conv2d(out, self.conv2), self.bn2)
-        return batch_norm_act(conv2d(out, self.conv3), self.bn3, residual=_shortcut(self.shortcut, x))
+        out = conv_bn_act(x, self.conv1, self.bn1)
+        out = conv_bn_act(out, self.conv2, self.bn2)
+        return conv_bn_act(out, self.conv3, self.bn3, residual=_shortcut(self.shortcut, x))
 
 
 class ResNet(FLModule):

@@ -80,17 +80,56 @@ class _BatchNormAct(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, dy):
-        x2, y2, weight, mean, rstd = ctx.saved_tensors
-        if dy.dtype != x2.dtype:
-            STATS["dy_cast"] += 1
-            dy = dy.to(x2.dtype)
-        if not dy.is_contiguous(memory_format=torch.channels_last):
-            STATS["dy_relayout"] += 1
-            dy = dy.contiguous(memory_format=torch.channels_last)
-        out = _bx().bwd(_nhwc_2d(dy), y2, x2, weight, mean, rstd, ctx.relu, ctx.has_res and ctx.needs_input_grad[3], _counter(x2))
-        dx = _from_2d(out[0], ctx.shape)
-        dres = _from_2d(out[3], ctx.shape).to(ctx.res_dtype) if len(out) > 3 else None
-        return dx, out[1].to(weight.dtype), out[2].to(weight.dtype), dres, None, None, None, None, None, None
+        return _bn_backward(ctx, dy) + (None, None, None, None, None, None)
+
+
+def _bn_backward(ctx, dy):
+    """(dx, dweight, dbias, dresidual) of act(bn(x) [+ residual]) from the saved x2, y2, weight, mean, rstd."""
+    x2, y2, weight, mean, rstd = ctx.saved_tensors
+    if dy.dtype != x2.dtype:
+        STATS["dy_cast"] += 1
+        dy = dy.to(x2.dtype)
+    if not dy.is_contiguous(memory_format=torch.channels_last):
+        STATS["dy_relayout"] += 1
+        dy = dy.contiguous(memory_format=torch.channels_last)
+    out = _bx().bwd(_nhwc_2d(dy), y2, x2, weight, mean, rstd, ctx.relu, ctx.has_res and ctx.needs_input_grad[3], _counter(x2))
+    dx = _from_2d(out[0], ctx.shape)
+    dres = _from_2d(out[3], ctx.shape).to(ctx.res_dtype) if len(out) > 3 else None
+    return dx, out[1].to(weight.dtype), out[2].to(weight.dtype), dres
+
+
+class _BatchNormApply(torch.autograd.Function):
+    """Training BatchNorm whose batch statistics were computed elsewhere -- the
+    statistics epilogue of the producing convolution (``gemm_core.h`` BnEpi),
+    which also updated the running statistics: only the apply pass runs here.
+    Backward is the fused BN backward of :class:`_BatchNormAct`."""
+
+    @staticmethod
+    def forward(ctx, x, weight, bias, residual, mean, rstd, coef, relu):
+        shape = x.shape
+        x2 = _nhwc_2d(x)
+        r2 = _nhwc_2d(residual.to(x.dtype)) if residual is not None else None
+        y2 = _bx().apply_train(x2, r2, coef, bool(relu))
+        ctx.save_for_backward(x2, y2, weight, mean, rstd)
+        ctx.shape, ctx.relu, ctx.has_res = shape, bool(relu), residual is not None
+        ctx.res_dtype = residual.dtype if residual is not None else None
+        return _from_2d(y2, shape)
+
+    @staticmethod
+    def backward(ctx, dy):
+        return _bn_backward(ctx, dy) + (None, None, None, None)
+
+
+def batch_norm_apply(x: torch.Tensor, bn: nn.BatchNorm2d, mean: torch.Tensor, rstd: torch.Tensor, coef: torch.Tensor,
+                     residual: Optional[torch.Tensor] = None, relu: bool = True) -> torch.Tensor:
+    """``act(bn(x) [+ residual])`` in training mode with precomputed statistics (see :class:`_BatchNormApply`)."""
+    return _BatchNormApply.apply(x, bn.weight, bn.bias, residual, mean, rstd, coef, relu)
+
+
+def fused_stats_ok(bn: nn.BatchNorm2d) -> bool:
+    """A training BatchNorm whose statistics a producing kernel can compute (see ops.conv.conv_bn_act)."""
+    return (bn.training and bn.momentum is not None and bn.affine and bn.weight.dtype == torch.float32
+            and bn.bias.dtype == torch.float32 and bn.weight.is_contiguous() and bn.bias.is_contiguous())
 
 
 def _native_ok(x: torch.Tensor, bn: nn.BatchNorm2d, residual: Optional[torch.Tensor]) -> bool:

@@ -31,7 +31,10 @@ from p2pfl_amd.ops import autotune
 from p2pfl_amd.ops.splitk import counters, slab_elems, tiles_of
 
 # counters a test can read to prove the native path ran
-STATS = {"native_fwd": 0, "torch_fwd": 0, "gemm_1x1_fwd": 0, "stem_fwd": 0}
+STATS = {"native_fwd": 0, "torch_fwd": 0, "gemm_1x1_fwd": 0, "stem_fwd": 0, "native_fwd_bn": 0}
+# training BatchNorm statistics computed by the producing convolution's launch
+# (conv_bn_act); P2PFL_CONV_BN_STATS=0 keeps the separate BN statistics passes
+_FUSED_BN = os.environ.get("P2PFL_CONV_BN_STATS", "1") != "0"
 
 # "native" | "library" | "auto" (measured per shape, ops/autotune.py); env P2PFL_NATIVE_CONV
 _POLICY = autotune.policy("P2PFL_NATIVE_CONV")
@@ -176,6 +179,76 @@ class _Conv2dNHWC(torch.autograd.Function):
             )
             dw = dw4.permute(0, 3, 1, 2)
         return dx, dw, None, None, None
+
+
+class _Conv2dNHWCBN(torch.autograd.Function):
+    """:class:`_Conv2dNHWC` whose launch also computes the training BatchNorm
+    statistics of its bf16 output (``gemm_core.h`` BnEpi: per-tile column moments,
+    reduced by the last-arriving tiles, finalized in the same launch) -- the BN
+    statistics and finalize passes of ``csrc/batchnorm.hip`` disappear.  Returns
+    (y, mean, rstd, coef); the three statistics are not differentiable."""
+
+    @staticmethod
+    def forward(ctx, x, w, stride, pad, dil, bn_w, bn_b, rm, rv, nbt, eps, momentum):
+        from p2pfl_amd.ops import splitk
+
+        if x.dtype != torch.bfloat16:
+            x = x.to(torch.bfloat16)
+        x4 = x.permute(0, 2, 3, 1)
+        if not x4.is_contiguous() or x4.data_ptr() % 16:
+            x4 = x4.contiguous()
+        w4 = w.permute(0, 2, 3, 1)
+        N, H, W_, C = x4.shape
+        O, kh, kw = w4.shape[0], w4.shape[1], w4.shape[2]
+        OH, OW = out_hw(H, W_, (kh, kw), stride, pad, dil)
+        y4 = torch.empty((N, OH, OW, O), dtype=torch.bfloat16, device=x.device)
+        rows = N * OH * OW
+        s = mn_splits(rows, O, kh * kw * C)
+        ws = cnt = None
+        if s > 1:  # in-launch reduction: the statistics epilogue sees whole tiles
+            ws = torch.empty(s * slab_elems(rows, O), dtype=torch.float32, device=x.device)
+            cnt = counters(tiles_of(rows, O), x.device)
+        tiles_m, tiles_n = -(-rows // 128), -(-O // 128)
+        groups = -(-tiles_m // 16)
+        part = torch.empty((tiles_m + groups) * 2 * O, dtype=torch.float32, device=x.device)
+        bcnt = splitk.counters(tiles_n * (groups + 1), x.device)
+        f32 = dict(dtype=torch.float32, device=x.device)
+        mean, rstd, coef = torch.empty(O, **f32), torch.empty(O, **f32), torch.empty(3 * O, **f32)
+        _C().conv_fwd_bn(x4, w4, stride, pad, dil, y4, s, _V_FWD, ws, cnt, part, bcnt, bn_w, bn_b, rm, rv, nbt,
+                         mean, rstd, coef, float(eps), float(momentum))
+        ctx.save_for_backward(x4, w)
+        ctx.cfg = (stride, pad, dil)
+        ctx.mark_non_differentiable(mean, rstd, coef)
+        return y4.permute(0, 3, 1, 2), mean, rstd, coef
+
+    @staticmethod
+    def backward(ctx, dy, _dmean, _drstd, _dcoef):
+        dx, dw, _, _, _ = _Conv2dNHWC.backward(ctx, dy)
+        return dx, dw, None, None, None, None, None, None, None, None, None, None
+
+
+def conv_bn_act(x: torch.Tensor, conv: nn.Conv2d, bn: nn.BatchNorm2d, residual=None, relu: bool = True) -> torch.Tensor:
+    """``act(bn(conv(x)) [+ residual])``.  In training, on the native implicit-GEMM
+    kernels, the convolution's launch computes the batch statistics (and updates the
+    running ones): only the BN apply pass remains a separate launch.  Anything else
+    composes :func:`conv2d` and :func:`~p2pfl_amd.ops.batchnorm.batch_norm_act`."""
+    from p2pfl_amd.ops import batchnorm as bnops
+
+    capturing = x.is_cuda and torch.cuda.is_current_stream_capturing()
+    if (_FUSED_BN and bnops.fused_stats_ok(bn) and native_ok(x, conv) and (capturing or _POLICY != "library")
+            and (residual is None or residual.is_contiguous(memory_format=torch.channels_last))):
+        track = bn.track_running_stats
+        rm = bn.running_mean if track else None
+        rv = bn.running_var if track else None
+        nbt = bn.num_batches_tracked if track and bn.num_batches_tracked is not None else None
+        STATS["native_fwd_bn"] += 1
+        y, mean, rstd, coef = _Conv2dNHWCBN.apply(x, conv.weight, _sym(conv.stride), _sym(conv.padding),
+                                                  _sym(conv.dilation), bn.weight, bn.bias, rm, rv, nbt, bn.eps,
+                                                  bn.momentum)
+        if residual is not None and residual.shape != y.shape:
+            raise ValueError("conv_bn_act: residual shape mismatch")
+        return bnops.batch_norm_apply(y, bn, mean, rstd, coef, residual, relu)
+    return bnops.batch_norm_act(conv2d(x, conv), bn, residual=residual, relu=relu)
 
 
 def _native_faster(x: torch.Tensor, conv: nn.Conv2d) -> bool:

@@ -194,3 +194,76 @@ def test_fused_stats_finalize_matches_separate_launches(shape, residual, relu):
             torch.testing.assert_close(a, b, atol=1e-4, rtol=1e-4)
         else:
             torch.testing.assert_close(a, b, atol=2e-2, rtol=1e-2)
+
+
+# ---- convolution launch computing the BatchNorm statistics (gemm_core.h BnEpi) -------------
+CONV_BN_CASES = [
+    # N, C, H, W, O, stride: tiles_m 256 (16 groups), 2 tile columns, ragged rows, split-K shapes
+    (32, 64, 32, 32, 64, 1),
+    (8, 64, 16, 16, 256, 2),
+    (3, 128, 7, 5, 128, 1),
+    (32, 256, 4, 4, 512, 1),
+    (2, 64, 33, 9, 64, 1),
+]
+
+
+@pytest.mark.parametrize("N,C,H,W,O,s", CONV_BN_CASES)
+@pytest.mark.parametrize("residual,relu", [(False, True), (True, True), (False, False)])
+def test_conv_bn_act_statistics_epilogue_vs_fp32(monkeypatch, N, C, H, W, O, s, residual, relu):
+    """conv_bn_act: the convolution launch computes batch mean / variance of its bf16 output,
+    the apply coefficients and the running statistics; output, running stats and all
+    gradients match conv + BatchNorm (+ residual) (+ ReLU) in fp32 on the same bf16 operands."""
+    from p2pfl_amd.ops import conv as conv_ops
+    import torch.nn.functional as F
+
+    ops.ext()
+    monkeypatch.setattr(conv_ops, "_POLICY", "native")
+    g = torch.Generator(device="cuda").manual_seed(N * 7 + O)
+    x = _cl(torch.randn(N, C, H, W, device="cuda", generator=g)).to(torch.bfloat16).requires_grad_(True)
+    conv = nn.Conv2d(C, O, 3, s, 1, bias=False).cuda()
+    with torch.no_grad():
+        conv.weight.copy_(torch.randn(O, C, 3, 3, device="cuda", generator=g) / (9 * C) ** 0.5 + 0.02)
+    conv.weight.data = conv.weight.data.to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    bn, ref = _bn(O, 11), _bn(O, 11)
+    OH, OW = (H + 2 - 3) // s + 1, (W + 2 - 3) // s + 1
+    r = _cl(torch.randn(N, O, OH, OW, device="cuda", generator=g)).to(torch.bfloat16).requires_grad_(True) if residual else None
+    before = conv_ops.STATS["native_fwd_bn"]
+    y = conv_ops.conv_bn_act(x, conv, bn, r, relu)
+    assert conv_ops.STATS["native_fwd_bn"] == before + 1
+    xr = x.detach().float().requires_grad_(True)
+    wr = conv.weight.detach().float().requires_grad_(True)
+    rr = r.detach().float().requires_grad_(True) if residual else None
+    yc = F.conv2d(xr, wr, None, s, 1)
+    # the kernel normalises its bf16-rounded output: the reference does the same
+    yc_b = yc + (yc.detach().to(torch.bfloat16).float() - yc.detach())
+    yr = batch_norm_act_reference(yc_b, ref.weight, ref.bias, ref.running_mean, ref.running_var, True, 0.1, ref.eps, rr, relu)
+    torch.testing.assert_close(y.float(), yr, atol=4e-2, rtol=2e-2)
+    torch.testing.assert_close(bn.running_mean, ref.running_mean, atol=1e-4, rtol=1e-3)
+    torch.testing.assert_close(bn.running_var, ref.running_var, atol=1e-4, rtol=1e-3)
+    assert int(bn.num_batches_tracked) == 1
+    dy = _cl(torch.randn(y.shape, device="cuda", generator=g)).to(torch.bfloat16)
+    y.backward(dy)
+    yr.backward(dy.float())
+    for a, e, name in [(x.grad, xr.grad, "dx"), (conv.weight.grad, wr.grad, "dW"), (bn.weight.grad, ref.weight.grad, "dgamma"),
+                       (bn.bias.grad, ref.bias.grad, "dbeta")] + ([(r.grad, rr.grad, "dres")] if residual else []):
+        scale = e.abs().max().item() + 1e-6
+        torch.testing.assert_close(a.float(), e, atol=3e-2 * scale, rtol=3e-2, msg=lambda m, n=name: f"{n}: {m}")
+
+
+def test_conv_bn_statistics_are_deterministic_and_counters_reset(monkeypatch):
+    """Repeated launches (counters reused from the ring) give bitwise-equal statistics."""
+    from p2pfl_amd.ops import conv as conv_ops
+
+    ops.ext()
+    monkeypatch.setattr(conv_ops, "_POLICY", "native")
+    x = _cl(torch.randn(32, 64, 32, 32, device="cuda")).to(torch.bfloat16)
+    conv = nn.Conv2d(64, 64, 3, 1, 1, bias=False).cuda()
+    conv.weight.data = conv.weight.data.to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    outs = []
+    for _ in range(4):
+        bn = _bn(64, 3)
+        with torch.no_grad():
+            outs.append((conv_ops.conv_bn_act(x, conv, bn), bn.running_mean.clone(), bn.running_var.clone()))
+    for o in outs[1:]:
+        for a, b in zip(outs[0], o):
+            assert torch.equal(a, b)
