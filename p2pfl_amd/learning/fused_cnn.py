@@ -294,6 +294,9 @@ class FusedCNNLearner(TorchLearner):
 
         g = self._graphs.get(name)
         if g is None or g.key != key:
+            import gc
+
+            gc.collect()  # outside the exclusive section (see step_graph.no_gc)
             with GATE.exclusive():  # no other learner's GPU work during the capture
                 g = self._capture(name, loader, plan, train, key)
             self._graphs[name] = g
@@ -333,7 +336,7 @@ class FusedCNNLearner(TorchLearner):
             torch.cuda.synchronize(self.device)
             saved = [t.clone() for t in (self.engine.params, self.engine.m, self.engine.v, self.engine.adam_t)]
             graph = torch.cuda.CUDAGraph()
-            with no_gc(), torch.cuda.graph(graph, stream=self._stream, capture_error_mode="thread_local"):
+            with no_gc(collect=False), torch.cuda.graph(graph, stream=self._stream, capture_error_mode="thread_local"):
                 self._enqueue(loader, plan, train, eg.perm, eg.stats)
             torch.cuda.synchronize(self.device)
             for dst, src in zip((self.engine.params, self.engine.m, self.engine.v, self.engine.adam_t), saved):

@@ -82,12 +82,14 @@ GATE = DeviceGate()
 
 
 @contextmanager
-def no_gc():
-    """Collect now, then keep Python's cyclic GC off for the capture: a collection
-    during capture can run the destructor of an unrelated object holding device
-    resources (another learner's graph, events, streams) -- a HIP call that
-    invalidates this thread's capture and aborts the process."""
-    gc.collect()
+def no_gc(collect: bool = True):
+    """Collect now (unless the caller just did, outside its locks), then keep
+    Python's cyclic GC off for the capture: a collection during capture can run
+    the destructor of an unrelated object holding device resources (another
+    learner's graph, events, streams) -- a HIP call that invalidates this
+    thread's capture and aborts the process."""
+    if collect:
+        gc.collect()
     was = gc.isenabled()
     gc.disable()
     try:
@@ -173,11 +175,12 @@ class TrainStepGraph:
             opt.t = t_host
             for p in opt.mt.params:  # eager gradients are not the graph's
                 p.grad = None
+        gc.collect()  # before the exclusive section: a full collection can take a while
         with GATE.exclusive(), _CAPTURE_LOCK:
             torch.cuda.synchronize(dev)
             g = torch.cuda.CUDAGraph()
             self.counters = splitk.GraphCounters(dev)  # split-K tile counters owned by this graph
-            with no_gc(), splitk.graph_scope(self.counters), torch.cuda.graph(g, stream=self.stream, capture_error_mode="thread_local"):
+            with no_gc(collect=False), splitk.graph_scope(self.counters), torch.cuda.graph(g, stream=self.stream, capture_error_mode="thread_local"):
                 self.loss = self._body(graph=True)
             opt.mt.fill_grad_table(self.gtab)  # the graph's gradient buffers, fixed for every replay
             opt.t = t_host  # recording executed nothing; host-side counters back to the pre-capture state
@@ -251,11 +254,12 @@ class EvalStepGraph:
                 self.idx.copy_(idx)
                 self.step(self.idx, float(self.B), cache=False)
             self.stream.synchronize()
+        gc.collect()
         with GATE.exclusive(), _CAPTURE_LOCK:  # recording only
             torch.cuda.synchronize(learner.device)
             g = torch.cuda.CUDAGraph()
             self.counters = splitk.GraphCounters(learner.device)
-            with no_gc(), splitk.graph_scope(self.counters), torch.cuda.graph(g, stream=self.stream, capture_error_mode="thread_local"):
+            with no_gc(collect=False), splitk.graph_scope(self.counters), torch.cuda.graph(g, stream=self.stream, capture_error_mode="thread_local"):
                 self.step(self.idx, float(self.B), cache=False)
             torch.cuda.synchronize(learner.device)
         self.graph = g
