@@ -834,6 +834,7 @@ class XgmiDataPlane:
                 self._index = {r: i for i, r in enumerate(members)}
                 self._lost = (self._lost | {r for r in range(self.world) if r not in members}) - set(members)
                 self._backend = backend
+                self.backend_name = getattr(backend, "name", self.backend_name)  # what generation `gen` runs on
                 self._alloc_stream = getattr(backend, "stream", None)
                 self._open = 0
                 self._rebuilding = False

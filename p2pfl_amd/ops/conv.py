@@ -321,17 +321,21 @@ def conv1x1_gemm(x: torch.Tensor, conv: nn.Conv2d) -> torch.Tensor:
 def conv2d(x: torch.Tensor, conv: nn.Conv2d) -> torch.Tensor:
     """``conv(x)`` on the implicit-GEMM kernels or MIOpen (``_POLICY``; "auto" = measured per shape);
     1x1 convolutions as GEMMs (:func:`conv1x1_gemm`)."""
-    if _is_1x1(x, conv):
-        return conv1x1_gemm(x, conv)
-    if x.shape[1] < 8 and stem_ok(x, conv) and _POLICY != "library":
-        return stem_conv2d(x, conv)
     # Inside a HIP-graph capture the implicit-GEMM kernels run whatever the
     # eager timing preferred: MIOpen convolutions replayed from captured step
     # graphs corrupted weights as soon as several learners' graphs and eager
     # steps shared the device (profiles/r3_nan_root_cause.md); eager steps may
-    # still take MIOpen.  This holds under every policy, "library" included.
+    # still take MIOpen.  This holds under every policy, "library" included,
+    # and for 1x1 convolutions too (no hipBLASLt GEMM inside a graph).
     capturing = x.is_cuda and torch.cuda.is_current_stream_capturing()
-    if native_ok(x, conv) and (capturing or _POLICY == "native" or (_POLICY != "library" and _native_faster(x, conv))):
+    if capturing and native_ok(x, conv):
+        STATS["native_fwd"] += 1
+        return _Conv2dNHWC.apply(x, conv.weight, _sym(conv.stride), _sym(conv.padding), _sym(conv.dilation))
+    if _is_1x1(x, conv):
+        return conv1x1_gemm(x, conv)
+    if x.shape[1] < 8 and stem_ok(x, conv) and _POLICY != "library":
+        return stem_conv2d(x, conv)
+    if native_ok(x, conv) and (_POLICY == "native" or (_POLICY != "library" and _native_faster(x, conv))):
         STATS["native_fwd"] += 1
         return _Conv2dNHWC.apply(x, conv.weight, _sym(conv.stride), _sym(conv.padding), _sym(conv.dilation))
     STATS["torch_fwd"] += 1

@@ -245,3 +245,47 @@ def test_bench_two_ranks_on_one_gpu_fail_loudly_without_fallback():
     assert r.returncode == 0, (r.stdout + r.stderr)[-4000:]
     rec = [json.loads(ln) for ln in r.stdout.splitlines() if ln.startswith("{")][0]
     assert rec["transport"] == "xgmi/gloo"
+
+
+@pytest.mark.timeout(420)
+def test_rccl_rank_killed_mid_transfer_survivors_rebuild_over_rccl(tmp_path):
+    """a REAL 3-rank RCCL communicator (three processes on the box's
+    one GPU, one NCCL_HOSTID each).  Rank 2 dies while its round-1 push is in flight
+    (the receivers' RCCL groups wait for a send that never comes); the survivors must
+    ncclCommAbort, agree on {0, 1}, build generation 1 OVER RCCL (no gloo fallback
+    allowed) and finish the remaining rounds with bitwise-equal models
+    (tests/xgmi_worker.py; reference failure semantics: grpc_client.py:159-179,
+    node_test.py:126-152)."""
+    import json
+    import os
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    port = _free_port()
+    out = str(tmp_path / "fault.json")
+    procs = []
+    for r in range(3):
+        env = dict(os.environ, RANK=str(r), WORLD_SIZE="3", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port),
+                   PYTHONPATH=root, NCCL_HOSTID=f"p2pfl-fault-r{r}", NCCL_SOCKET_IFNAME="lo", NCCL_IB_DISABLE="1",
+                   P2PFL_WORKER_DEVICE="cuda")
+        procs.append(subprocess.Popen([sys.executable, os.path.join(root, "tests", "xgmi_worker.py"), out, "fault"],
+                                      cwd=root, env=env, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True))
+    outs = []
+    for p in procs:
+        try:
+            o, _ = p.communicate(timeout=360)
+        except subprocess.TimeoutExpired:
+            p.kill()
+            o, _ = p.communicate()
+        outs.append(o)
+    assert procs[2].returncode == 17, outs[2][-3000:]  # the victim died on purpose
+    assert procs[0].returncode == 0, outs[0][-5000:]
+    assert procs[1].returncode == 0, outs[1][-5000:]
+    with open(out) as f:
+        rec = json.load(f)
+    print(json.dumps(rec))
+    assert rec["rounds_done"] == rec["rounds"]
+    assert rec["stats"].get("rebuilds", 0) == 1, rec["stats"]
+    assert rec["backend"] == "rccl", rec
+    assert rec["digests"][0] == rec["digests"][1] and rec["digests"][0], rec["digests"]

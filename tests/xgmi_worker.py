@@ -7,6 +7,11 @@ its round-1 model push arrives -- the receiver has accepted the transfer and
 launched a receive that can never complete, so the survivors must abort the
 communicator and rebuild it over ranks {0, 1}.  Ranks 0 and 1 must still
 finish every round with the same model; rank 0 writes the outcome to OUT_JSON.
+
+``P2PFL_WORKER_DEVICE=cuda``: the same scenario on the GPU with the RCCL data
+plane (no fallback): every rank is its own RCCL "host" (``NCCL_HOSTID`` set by
+the test), so three processes on one MI355X form a real 3-rank communicator;
+the survivors ``ncclCommAbort`` it and build generation 1 over RCCL.
 """
 
 from __future__ import annotations
@@ -37,9 +42,18 @@ def main(out: str, mode: str) -> None:
     Settings.TRAIN_SET_SIZE = world
     Settings.GOSSIP_MODELS_PER_ROUND = world - 1
     rounds = 3
-    job = XgmiJob(rank, world, store, device=torch.device("cpu"), backend="gloo", prefix="fault", job_id=f"f{os.environ['MASTER_PORT']}",
-                  ack_timeout=3.0, group_timeout=20.0, rebuild_grace=0.5)
-    node = Node(MLP(seed=0), MnistFederatedDM(sub_id=rank, number_sub=4 * world), protocol=job.protocol)
+    on_gpu = os.environ.get("P2PFL_WORKER_DEVICE", "cpu") == "cuda"
+    dev = torch.device("cuda", 0) if on_gpu else torch.device("cpu")
+    extra = {}
+    if on_gpu:
+        from p2pfl_amd import ops
+
+        ops.ext()
+        extra = dict(allow_fallback=False)
+    job = XgmiJob(rank, world, store, device=dev, backend="rccl" if on_gpu else "gloo", prefix="fault",
+                  job_id=f"f{os.environ['MASTER_PORT']}", ack_timeout=3.0, group_timeout=20.0, rebuild_grace=0.5, **extra)
+    node = Node(MLP(seed=0), MnistFederatedDM(sub_id=rank, number_sub=4 * world), protocol=job.protocol,
+                **({"device": dev} if on_gpu else {}))
     proto = node._communication_protocol
     if mode == "fault" and rank == world - 1:
         orig_start = proto.start
@@ -78,12 +92,20 @@ def main(out: str, mode: str) -> None:
     assert node.wait_learning(timeout=240), "learning did not finish"
     flat = node.state.learner.get_parameters().flat if node.state.learner is not None else None
     s = float(flat.double().sum()) if flat is not None else float("nan")
+    digest = ""
+    if flat is not None:
+        import hashlib
+
+        digest = hashlib.sha1(flat.detach().float().cpu().numpy().tobytes()).hexdigest()
     store.set(f"sum/{rank}", str(s))
+    store.set(f"digest/{rank}", digest)
     if rank == 0:
         other = float(store.get("sum/1").decode())
         with open(out, "w") as f:
             json.dump({"rounds": rounds, "rounds_done": rounds if node.state.round is None else node.state.round,
-                       "sums": [s, other], "stats": dict(proto.plane.stats) if proto.plane else {}}, f)
+                       "sums": [s, other], "digests": [digest, store.get("digest/1").decode()],
+                       "backend": getattr(job, "backend_in_use", None),
+                       "stats": dict(proto.plane.stats) if proto.plane else {}}, f)
     store.set(f"done/{rank}", "1")
     store.wait([f"done/{r}" for r in range(world - 1)])
     del rounds_done
