@@ -34,6 +34,12 @@ void bn_fwd_train(bool bf16, const void* x, const void* res, const float* w, con
 void bn_apply_train(bool bf16, const void* x, const void* res, const float* coef, void* y, int M, int C, bool relu,
                     hipStream_t s);
 
+// Backward apply pass only (bf16), coef = [A | B | D] computed elsewhere (the
+// backward statistics epilogue of a convolution's input gradient):
+//   dx = A dz' + B (x - mean) + D,  dz' = relu ? dy * (y > 0) : dy
+void bn_apply_bwd_only(const void* dy, const void* y, const void* x, const float* mean, const float* coef, void* dx,
+                       int M, int C, bool relu, hipStream_t s);
+
 // Inference forward with running statistics (one launch; coef unused, kept for
 // the call signature).  w, b, run_mean, run_var must be 16-byte aligned.
 void bn_fwd_eval(bool bf16, const void* x, const void* res, const float* w, const float* b, const float* run_mean,

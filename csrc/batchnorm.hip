@@ -698,6 +698,12 @@ void bn_apply_train(bool bf16, const void* x, const void* res, const float* coef
                      relu, s);
 }
 
+void bn_apply_bwd_only(const void* dy, const void* y, const void* x, const float* mean, const float* coef, void* dx,
+                       int M, int C, bool relu, hipStream_t s) {
+  apply_bwd<uint16_t>(static_cast<const uint16_t*>(dy), static_cast<const uint16_t*>(y), static_cast<const uint16_t*>(x),
+                      mean, coef, static_cast<uint16_t*>(dx), nullptr, M, C, relu, s);
+}
+
 void bn_fwd_eval(bool bf16, const void* x, const void* res, const float* w, const float* b, const float* run_mean,
                  const float* run_var, float eps, void* y, float* coef, int M, int C, bool relu, hipStream_t s) {
   if (bf16)

@@ -108,6 +108,25 @@ torch::Tensor bn_apply_train(torch::Tensor x, c10::optional<torch::Tensor> resid
   return y;
 }
 
+// dx = A dz' + B (x - mean) + D (bf16 [M, C]); y: BN output (ReLU mask) or undefined
+torch::Tensor bn_apply_bwd(torch::Tensor dy, c10::optional<torch::Tensor> y, torch::Tensor x, torch::Tensor mean,
+                           torch::Tensor coef) {
+  const c10::DeviceGuard g(x.device());
+  check_shape(x);
+  const int64_t M = x.size(0), C = x.size(1);
+  TORCH_CHECK(act(x, x, "x"), "apply_bwd: bf16 only");
+  act(dy, x, "dy");
+  const bool relu = y.has_value() && y->defined();
+  if (relu) act(*y, x, "y");
+  TORCH_CHECK(coef.device() == x.device() && coef.is_contiguous() && coef.scalar_type() == torch::kFloat32 &&
+                  coef.numel() == 3 * C,
+              "coef must be a contiguous fp32 [3, C] tensor on x's device");
+  auto dx = torch::empty_like(x);
+  p2bn::bn_apply_bwd_only(dy.data_ptr(), relu ? y->data_ptr() : nullptr, x.data_ptr(), f32(mean, C, x, "mean"),
+                          coef.data_ptr<float>(), dx.data_ptr(), int(M), int(C), relu, stream());
+  return dx;
+}
+
 torch::Tensor bn_fwd_eval(torch::Tensor x, torch::Tensor w, torch::Tensor b, c10::optional<torch::Tensor> residual,
                           torch::Tensor running_mean, torch::Tensor running_var, double eps, bool relu) {
   const c10::DeviceGuard g(x.device());
@@ -163,6 +182,7 @@ void register_bn(pybind11::module& m) {
         py::arg("num_batches_tracked") = py::none(), py::arg("momentum") = 0.1, py::arg("eps") = 1e-5,
         py::arg("relu") = true, py::arg("counters") = py::none());
   f.def("apply_train", &bn_apply_train, py::arg("x"), py::arg("residual"), py::arg("coef"), py::arg("relu"));
+  f.def("apply_bwd", &bn_apply_bwd, py::arg("dy"), py::arg("y"), py::arg("x"), py::arg("mean"), py::arg("coef"));
   f.def("fwd_eval", &bn_fwd_eval, py::arg("x"), py::arg("w"), py::arg("b"), py::arg("residual") = py::none(),
         py::arg("running_mean"), py::arg("running_var"), py::arg("eps") = 1e-5, py::arg("relu") = true);
   f.def("bwd", &bn_bwd, py::arg("dy"), py::arg("y"), py::arg("x"), py::arg("w"), py::arg("mean"), py::arg("rstd"),

@@ -29,8 +29,10 @@ struct SplitK {
 // launch (gemm.h BnEpi); needs splits == 1 or in-launch split-K (counters).
 void conv_fwd(const ConvShape& s, const uint16_t* x, const uint16_t* w, void* y, const SplitK& k, int variant,
               hipStream_t st, const BnEpi* bn = nullptr);
+// bn (optional, backward mode: BnEpi::bx set): BatchNorm backward statistics of the
+// BN whose output this dgrad differentiates, computed in the launch.
 void conv_dgrad(const ConvShape& s, const uint16_t* dy, const uint16_t* w, void* dx, const SplitK& k, int variant,
-                hipStream_t st);
+                hipStream_t st, const BnEpi* bn = nullptr);
 // dw[O][kh*kw*C] = sum over output pixels of dy (x) im2col(x)    (O % 8 == 0, C % 8 == 0)
 // splits == 1: written as bf16 (out_bf16) or fp32; splits > 1: fp32 slabs
 // [splits][O][kh*kw*C] at `out` (reduce with slab_sum).

@@ -236,10 +236,11 @@ void conv_fwd(const ConvShape& s, const uint16_t* x, const uint16_t* w, void* y,
 }
 
 void conv_dgrad(const ConvShape& s, const uint16_t* dy, const uint16_t* w, void* dx, const SplitK& k, int variant,
-                hipStream_t st) {
+                hipStream_t st, const BnEpi* bn) {
   using namespace p2gemm;
   const int M = s.N * s.H * s.W, K = s.kh * s.kw * s.O;
-  const GemmParams p = base_params(M, s.C, K, dx, s.C, k.splits <= 1 || k.counters, k, variant);
+  GemmParams p = base_params(M, s.C, K, dx, s.C, k.splits <= 1 || k.counters, k, variant);
+  if (bn) p.bn = *bn;
   const ConvDgradA la{dy, make_fastdiv(s.H * s.W), make_fastdiv(s.W), M, s.OH, s.OW, s.O, s.stride, s.pad, s.dil, s.kw};
   launch(p, la, ConvDgradB{w, s.C, s.O, s.kh * s.kw}, st);
 }

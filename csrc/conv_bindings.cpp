@@ -160,6 +160,63 @@ void conv_fwd_bn(torch::Tensor x, torch::Tensor w, int64_t stride, int64_t pad, 
                y.data_ptr(), k, int(variant), stream_of(x), &e);
 }
 
+// conv_dgrad + the backward statistics of the BatchNorm(+ReLU) that produced this
+// convolution's input (gemm.h BnEpi backward mode): bx / by = that BN's input /
+// output [N, H, W, C] bf16 (by undefined: no ReLU), bmean / brstd its saved
+// statistics, bn_w its weight; dgamma / dbeta [C] and coef [3, C] out.
+void conv_dgrad_bn(torch::Tensor dy, torch::Tensor w, int64_t stride, int64_t pad, int64_t dil, torch::Tensor dx,
+                   std::vector<int64_t> dx_shape, int64_t splits, int64_t variant, OptT ws, OptT counters,
+                   torch::Tensor part, torch::Tensor cnt, torch::Tensor bn_w, torch::Tensor bx, OptT by,
+                   torch::Tensor bmean, torch::Tensor brstd, torch::Tensor dgamma, torch::Tensor dbeta,
+                   torch::Tensor coef) {
+  check_nhwc(dy, "dy");
+  check_nhwc(w, "w");
+  TORCH_CHECK(dx_shape.size() == 4, "conv_dgrad_bn: dx_shape is (N, H, W, C)");
+  const auto s =
+      make_shape(dx_shape[0], dx_shape[1], dx_shape[2], dx_shape[3], w.size(0), w.size(1), w.size(2), stride, pad, dil);
+  TORCH_CHECK(w.size(3) == s.C, "conv_dgrad_bn: channel mismatch");
+  TORCH_CHECK(s.O % 64 == 0 && s.C % 8 == 0, "conv_dgrad_bn: needs O % 64 == 0 and C % 8 == 0");
+  TORCH_CHECK(dy.size(0) == s.N && dy.size(1) == s.OH && dy.size(2) == s.OW && dy.size(3) == s.O, "conv_dgrad_bn: dy shape");
+  const int64_t M = int64_t(s.N) * s.H * s.W;
+  const auto k = make_splitk(splits, ws, counters, M, s.C, dy, "conv_dgrad_bn");
+  TORCH_CHECK(k.splits == 1 || k.counters, "conv_dgrad_bn: split-K needs the in-launch reduction (counters)");
+  check_out(dx, k, s.N, s.H, s.W, s.C, "conv_dgrad_bn");
+  const int64_t tiles_m = (M + 127) / 128, tiles_n = (s.C + 127) / 128, groups = bn_groups(tiles_m);
+  auto f32v = [&](const torch::Tensor& t, int64_t n, const char* name) {
+    TORCH_CHECK(t.is_cuda() && t.device() == dy.device() && t.scalar_type() == torch::kFloat32 && t.is_contiguous() &&
+                    t.numel() == n,
+                "conv_dgrad_bn: ", name, " must be a contiguous fp32 tensor of ", n, " elements on dy's device");
+    return t.data_ptr<float>();
+  };
+  auto act = [&](const torch::Tensor& t, const char* name) {
+    check_nhwc(t, name);
+    TORCH_CHECK(t.device() == dy.device() && t.size(0) == s.N && t.size(1) == s.H && t.size(2) == s.W && t.size(3) == s.C,
+                "conv_dgrad_bn: ", name, " must be [N, H, W, C] like dx");
+    return reinterpret_cast<const uint16_t*>(t.data_ptr());
+  };
+  TORCH_CHECK(part.is_cuda() && part.device() == dy.device() && part.scalar_type() == torch::kFloat32 &&
+                  part.is_contiguous() && part.numel() >= (tiles_m + groups) * 2 * s.C,
+              "conv_dgrad_bn: part must hold (tiles_m + groups) * 2 * C fp32");
+  TORCH_CHECK(cnt.is_cuda() && cnt.device() == dy.device() && cnt.scalar_type() == torch::kInt32 && cnt.is_contiguous() &&
+                  cnt.numel() >= tiles_n * (groups + 1),
+              "conv_dgrad_bn: cnt must hold tiles_n * (groups + 1) zeroed int32");
+  p2::BnEpi e{};
+  e.part = part.data_ptr<float>();
+  e.cnt = cnt.data_ptr<int>();
+  e.w = f32v(bn_w, s.C, "bn weight");
+  e.bx = act(bx, "bx");
+  if (by.has_value() && by->defined()) e.by = act(*by, "by");
+  e.bmean = f32v(bmean, s.C, "bmean");
+  e.brstd = f32v(brstd, s.C, "brstd");
+  e.dw = f32v(dgamma, s.C, "dgamma");
+  e.db = f32v(dbeta, s.C, "dbeta");
+  e.coef = f32v(coef, 3 * s.C, "coef");
+  TORCH_CHECK(dy.device() == w.device() && dx.device() == dy.device(), "conv_dgrad_bn: device mismatch");
+  const c10::DeviceGuard g(dy.device());
+  p2::conv_dgrad(s, reinterpret_cast<const uint16_t*>(dy.data_ptr()), reinterpret_cast<const uint16_t*>(w.data_ptr()),
+                 dx.data_ptr(), k, int(variant), stream_of(dy), &e);
+}
+
 // dy [N, OH, OW, O], w [O, kh, kw, C]  ->  dx [N, H, W, C]  (dx_shape = (N, H, W, C), dx may hold slabs)
 void conv_dgrad(torch::Tensor dy, torch::Tensor w, int64_t stride, int64_t pad, int64_t dil, torch::Tensor dx,
                 std::vector<int64_t> dx_shape, int64_t splits, int64_t variant, OptT ws, OptT counters) {
@@ -303,6 +360,10 @@ void register_conv(pybind11::module& m) {
         arg("w"), arg("stride"), arg("pad"), arg("dil"), arg("y"), arg("splits"), arg("variant"), arg("ws"),
         arg("counters"), arg("part"), arg("cnt"), arg("bn_w"), arg("bn_b"), arg("run_mean"), arg("run_var"), arg("nbt"),
         arg("mean"), arg("rstd"), arg("coef"), arg("eps"), arg("momentum"));
+  m.def("conv_dgrad_bn", &conv_dgrad_bn, "implicit-GEMM conv input gradient + BatchNorm backward statistics",
+        arg("dy"), arg("w"), arg("stride"), arg("pad"), arg("dil"), arg("dx"), arg("dx_shape"), arg("splits"),
+        arg("variant"), arg("ws"), arg("counters"), arg("part"), arg("cnt"), arg("bn_w"), arg("bx"), arg("by"),
+        arg("bmean"), arg("brstd"), arg("dgamma"), arg("dbeta"), arg("coef"));
   m.def("stem_wgrad_parts", &stem_wgrad_parts, "partial rows of the stem weight gradient");
   m.def("stem_wgrad", &stem_wgrad, "small-C direct convolution weight gradient (stem)", pybind11::arg("dy"),
         pybind11::arg("x"), pybind11::arg("w"), pybind11::arg("stride"), pybind11::arg("pad"), pybind11::arg("xscale"),

@@ -38,6 +38,18 @@ struct BnEpi {
   float* rstd;      // [N] out
   float* coef;      // [3N] out
   float eps, momentum;
+  // Backward mode (bx != null): C is dz, the gradient w.r.t. the output of an
+  // act(bn(x)) whose input x = bx and output (for the ReLU mask) = by (null: no
+  // ReLU) are bf16 [M][N]; the launch reduces s1 = sum dz', s2 = sum dz' (x -
+  // bmean) with dz' = dz * (by > 0), and the finalize writes dw = rstd * s2,
+  // db = s1 and coef = [A | B | D] of csrc/batchnorm.hip's apply_bwd
+  // (dx = A dz' + B (x - mean) + D) instead of the forward outputs.
+  const uint16_t* bx;
+  const uint16_t* by;
+  const float* bmean;
+  const float* brstd;
+  float* dw;
+  float* db;
 };
 
 struct GemmParams {

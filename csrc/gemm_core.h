@@ -276,6 +276,12 @@ P2_DEVICE Moments moments_merge(Moments a, const Moments& b) {
   a.n = n;
   return a;
 }
+// forward statistics merge by Chan's formula; backward sums (s1, s2 in the mean /
+// m2 slots) simply add
+P2_DEVICE Moments bn_merge(bool bwd, Moments a, const Moments& b) {
+  if (bwd) return Moments{a.n + b.n, a.mean + b.mean, a.m2 + b.m2};
+  return moments_merge(a, b);
+}
 P2_DEVICE void st_sc1(float* base, int n, int idx, float v) {
   const auto rs = __builtin_amdgcn_make_buffer_rsrc(base, 0, n * 4, 0x00020000);
   __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), rs, idx * 4, 0, 16);
@@ -306,6 +312,7 @@ constexpr int kBnGroup = 16;  // tile rows per first-level group
 template <class CFG>
 P2_DEVICE void bn_epilogue_reduce(const GemmParams& p, Moments mo, int tm, int tn, int tiles_m, char* smem) {
   const BnEpi& e = p.bn;
+  const bool bwd = e.bx != nullptr;
   const int tid = threadIdx.x, N = p.N, n0 = tn * CFG::BN;
   const int groups = (tiles_m + kBnGroup - 1) / kBnGroup, g = tm / kBnGroup;
   const int gsize = min(kBnGroup, tiles_m - g * kBnGroup);
@@ -331,7 +338,7 @@ P2_DEVICE void bn_epilogue_reduce(const GemmParams& p, Moments mo, int tm, int t
     }
 #pragma unroll
     for (int i = 0; i < kBnGroup; ++i)
-      if (i < gsize) acc = moments_merge(acc, Moments{tile_rows(g * kBnGroup + i), mv[i], m2v[i]});
+      if (i < gsize) acc = bn_merge(bwd, acc, Moments{tile_rows(g * kBnGroup + i), mv[i], m2v[i]});
   }
   if (groups > 1) {
     if (col) {
@@ -355,14 +362,23 @@ P2_DEVICE void bn_epilogue_reduce(const GemmParams& p, Moments mo, int tm, int t
           if (gg >= groups) continue;
           float rows = 0.f;
           for (int t = gg * kBnGroup; t < min(tiles_m, (gg + 1) * kBnGroup); ++t) rows += tile_rows(t);
-          acc = moments_merge(acc, Moments{rows, mv[i], m2v[i]});
+          acc = bn_merge(bwd, acc, Moments{rows, mv[i], m2v[i]});
         }
       }
     }
   }
   if (!col) return;
-  // finalize column n (same outputs as bn_finalize_fwd_kernel)
   const float M = float(p.M);
+  if (bwd) {  // same outputs as bn_finalize_bwd_kernel
+    const float rs = e.brstd[n], A = e.w[n] * rs, s1 = acc.mean, s2 = acc.m2;
+    e.db[n] = s1;
+    e.dw[n] = s2 * rs;
+    e.coef[n] = A;
+    e.coef[N + n] = -A * rs * rs * s2 / M;
+    e.coef[2 * N + n] = -A * s1 / M;
+    return;
+  }
+  // finalize column n (same outputs as bn_finalize_fwd_kernel)
   const float var = fmaxf(acc.m2 / M, 0.f);
   const float rs = rsqrtf(var + e.eps);
   e.mean[n] = acc.mean;
@@ -704,7 +720,21 @@ P2_DEVICE void gemm_body(const GemmParams& p, const LA& la, const LB& lb, int ti
           }
     }
     __syncthreads();
-    if (bn_on && n0 + bn_c < p.N) {
+    if (bn_on && p.bn.bx && n0 + bn_c < p.N) {
+      // backward sums: dz' = dz * (bn output > 0), against the BN input x - mean
+      const int r0 = bn_ph * PROWS, rend = min(PROWS, p.M - (m0 + pass * ROWS + r0));
+      const int n = n0 + bn_c;
+      const float mu = p.bn.bmean[n];
+      float s1 = 0.f, s2 = 0.f;
+      for (int r = 0; r < rend; ++r) {
+        const int64_t off = int64_t(m0 + pass * ROWS + r0 + r) * p.N + n;
+        float g = bf16_to_f32(*reinterpret_cast<const uint16_t*>(smem + (r0 + r) * LROW + bn_c * 2));
+        if (p.bn.by && !(bf16_to_f32(p.bn.by[off]) > 0.f)) g = 0.f;
+        s1 += g;
+        s2 = fmaf(g, bf16_to_f32(p.bn.bx[off]) - mu, s2);
+      }
+      bn_mo = Moments{bn_mo.n + float(max(rend, 0)), bn_mo.mean + s1, bn_mo.m2 + s2};
+    } else if (bn_on && n0 + bn_c < p.N) {
       const int r0 = bn_ph * PROWS, rend = min(PROWS, p.M - (m0 + pass * ROWS + r0));
       if (rend > 0) {
         const float x0 = bf16_to_f32(*reinterpret_cast<const uint16_t*>(smem + r0 * LROW + bn_c * 2));
@@ -739,7 +769,7 @@ P2_DEVICE void gemm_body(const GemmParams& p, const LA& la, const LB& lb, int ti
     if (tid < CFG::BN)
       for (int ph = 0; ph < BNPH; ++ph) {
         const int q = ph * CFG::BN + tid;
-        mo = moments_merge(mo, Moments{red[q], red[CFG::NT + q], red[2 * CFG::NT + q]});
+        mo = bn_merge(p.bn.bx != nullptr, mo, Moments{red[q], red[CFG::NT + q], red[2 * CFG::NT + q]});
       }
     __syncthreads();
     bn_epilogue_reduce<CFG>(p, mo, tm, tn, tiles_m, smem);

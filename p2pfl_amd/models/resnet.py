@@ -24,8 +24,13 @@ Activations run channels-last on the GPU.  What runs per convolution
 * the 3-channel stem runs the direct small-C kernels of ``csrc/stem.hip``
   (forward + weight gradient, reading the uint8 / fp32 batch as it comes).
 
-Every ``BatchNorm2d -> (+ shortcut) -> ReLU`` chain runs as the fused HIP kernel of
-``csrc/batchnorm.hip`` (:func:`~p2pfl_amd.ops.batchnorm.batch_norm_act`).  Optimiser: SGD with momentum 0.9 and weight decay 5e-4 (fused
+In training, every convolution's launch also computes the batch statistics of the
+BatchNorm that follows it (``gemm_core.h`` BnEpi), and the input-gradient launch of
+a block's inner convolution computes the backward statistics of the BatchNorm before
+it (:func:`~p2pfl_amd.ops.conv.bn_act_conv_bn_stats`): per BasicBlock the forward is
+conv1 -> [bn1 apply, conv2] -> bn2 apply (+ shortcut) (+ ReLU), three launches where
+the separate BN kernels needed nine.  Evaluation (running statistics) runs the one-pass
+BN kernel of ``csrc/batchnorm.hip`` (:func:`~p2pfl_amd.ops.batchnorm.batch_norm_act`).  Optimiser: SGD with momentum 0.9 and weight decay 5e-4 (fused
 into one arena kernel by the learner), a standard federated CIFAR setup.
 """
 
@@ -38,8 +43,8 @@ import torch
 from torch import nn
 
 from p2pfl_amd.models.base import FLModule, seed_everything
-from p2pfl_amd.ops.batchnorm import batch_norm_act
-from p2pfl_amd.ops.conv import conv2d, conv_bn_act, stem_conv2d, stem_ok
+from p2pfl_amd.ops.batchnorm import batch_norm_act, batch_norm_apply
+from p2pfl_amd.ops.conv import bn_act_conv_bn_stats, conv2d, conv_bn_act, conv_bn_stats, stem_conv2d, stem_ok
 
 # NHWC activations on the GPU (P2PFL_CHANNELS_LAST=0 keeps NCHW)
 _CHANNELS_LAST = os.environ.get("P2PFL_CHANNELS_LAST", "1") != "0"
@@ -68,6 +73,10 @@ class BasicBlock(nn.Module):
             self.shortcut = nn.Sequential(nn.Conv2d(cin, cout, 1, stride, bias=False), nn.BatchNorm2d(cout))
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
+        st = conv_bn_stats(x, self.conv1, self.bn1)
+        st = bn_act_conv_bn_stats(st, self.bn1, True, self.conv2, self.bn2) if st is not None else None
+        if st is not None:  # conv1 -> [bn1 apply, conv2] -> bn2 apply: 3 launches forward
+            return batch_norm_apply(st[0], self.bn2, st[1], st[2], st[3], _shortcut(self.shortcut, x), True)
         out = conv_bn_act(x, self.conv1, self.bn1)
         return conv_bn_act(out, self.conv2, self.bn2, residual=_shortcut(self.shortcut, x))
 
@@ -89,6 +98,11 @@ class Bottleneck(nn.Module):
             self.shortcut = nn.Sequential(nn.Conv2d(cin, cout, 1, stride, bias=False), nn.BatchNorm2d(cout))
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
+        st = conv_bn_stats(x, self.conv1, self.bn1)
+        st = bn_act_conv_bn_stats(st, self.bn1, True, self.conv2, self.bn2) if st is not None else None
+        st = bn_act_conv_bn_stats(st, self.bn2, True, self.conv3, self.bn3) if st is not None else None
+        if st is not None:
+            return batch_norm_apply(st[0], self.bn3, st[1], st[2], st[3], _shortcut(self.shortcut, x), True)
         out = conv_bn_act(x, self.conv1, self.bn1)
         out = conv_bn_act(out, self.conv2, self.bn2)
         return conv_bn_act(out, self.conv3, self.bn3, residual=_shortcut(self.shortcut, x))

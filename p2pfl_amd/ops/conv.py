@@ -31,7 +31,7 @@ from p2pfl_amd.ops import autotune
 from p2pfl_amd.ops.splitk import counters, slab_elems, tiles_of
 
 # counters a test can read to prove the native path ran
-STATS = {"native_fwd": 0, "torch_fwd": 0, "gemm_1x1_fwd": 0, "stem_fwd": 0, "native_fwd_bn": 0}
+STATS = {"native_fwd": 0, "torch_fwd": 0, "gemm_1x1_fwd": 0, "stem_fwd": 0, "native_fwd_bn": 0, "bn_act_conv": 0}
 # training BatchNorm statistics computed by the producing convolution's launch
 # (conv_bn_act); P2PFL_CONV_BN_STATS=0 keeps the separate BN statistics passes
 _FUSED_BN = os.environ.get("P2PFL_CONV_BN_STATS", "1") != "0"
@@ -181,6 +181,54 @@ class _Conv2dNHWC(torch.autograd.Function):
         return dx, dw, None, None, None
 
 
+def _nhwc_bf16(t: torch.Tensor) -> torch.Tensor:
+    """[N, C, H, W] channels-last (bf16) -> its contiguous, 16-byte aligned NHWC storage view."""
+    if t.dtype != torch.bfloat16:
+        t = t.to(torch.bfloat16)
+    t4 = t.permute(0, 2, 3, 1)
+    if not t4.is_contiguous() or t4.data_ptr() % 16:
+        t4 = t4.contiguous()
+    return t4
+
+
+def _fwd_bn_launch(x4, w, stride, pad, dil, bn_w, bn_b, rm, rv, nbt, eps, momentum):
+    """One conv_fwd_bn launch: (y4 NHWC bf16, mean, rstd, coef) -- the forward product
+    plus the training BatchNorm statistics of its output (split-K reduced in the launch)."""
+    from p2pfl_amd.ops import splitk
+
+    w4 = w.permute(0, 2, 3, 1)
+    N, H, W_, C = x4.shape
+    O, kh, kw = w4.shape[0], w4.shape[1], w4.shape[2]
+    OH, OW = out_hw(H, W_, (kh, kw), stride, pad, dil)
+    y4 = torch.empty((N, OH, OW, O), dtype=torch.bfloat16, device=x4.device)
+    rows = N * OH * OW
+    s = mn_splits(rows, O, kh * kw * C)
+    ws = cnt = None
+    if s > 1:  # in-launch reduction: the statistics epilogue sees whole tiles
+        ws = torch.empty(s * slab_elems(rows, O), dtype=torch.float32, device=x4.device)
+        cnt = counters(tiles_of(rows, O), x4.device)
+    tiles_m, tiles_n = -(-rows // 128), -(-O // 128)
+    groups = -(-tiles_m // 16)
+    part = torch.empty((tiles_m + groups) * 2 * O, dtype=torch.float32, device=x4.device)
+    bcnt = splitk.counters(tiles_n * (groups + 1), x4.device)
+    f32 = dict(dtype=torch.float32, device=x4.device)
+    mean, rstd, coef = torch.empty(O, **f32), torch.empty(O, **f32), torch.empty(3 * O, **f32)
+    _C().conv_fwd_bn(x4, w4, stride, pad, dil, y4, s, _V_FWD, ws, cnt, part, bcnt, bn_w, bn_b, rm, rv, nbt,
+                     mean, rstd, coef, float(eps), float(momentum))
+    return y4, mean, rstd, coef
+
+
+def _wgrad_launch(dy4, x4, w, stride, pad, dil):
+    O, kh, kw, Cin = w.shape[0], w.shape[2], w.shape[3], w.shape[1]
+    npix = dy4.shape[0] * dy4.shape[1] * dy4.shape[2]
+    dw4 = torch.empty((O, kh, kw, Cin), dtype=w.dtype, device=w.device)
+    _run_split(
+        lambda o, s, ws, cnt: _C().conv_wgrad(dy4, x4, kh, kw, stride, pad, dil, o, s, _V_WGRAD, ws, cnt),
+        O, kh * kw * Cin, wgrad_splits(O, kh * kw * Cin, npix), dw4, _V_WGRAD,
+    )
+    return dw4.permute(0, 3, 1, 2)
+
+
 class _Conv2dNHWCBN(torch.autograd.Function):
     """:class:`_Conv2dNHWC` whose launch also computes the training BatchNorm
     statistics of its bf16 output (``gemm_core.h`` BnEpi: per-tile column moments,
@@ -190,32 +238,8 @@ class _Conv2dNHWCBN(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, x, w, stride, pad, dil, bn_w, bn_b, rm, rv, nbt, eps, momentum):
-        from p2pfl_amd.ops import splitk
-
-        if x.dtype != torch.bfloat16:
-            x = x.to(torch.bfloat16)
-        x4 = x.permute(0, 2, 3, 1)
-        if not x4.is_contiguous() or x4.data_ptr() % 16:
-            x4 = x4.contiguous()
-        w4 = w.permute(0, 2, 3, 1)
-        N, H, W_, C = x4.shape
-        O, kh, kw = w4.shape[0], w4.shape[1], w4.shape[2]
-        OH, OW = out_hw(H, W_, (kh, kw), stride, pad, dil)
-        y4 = torch.empty((N, OH, OW, O), dtype=torch.bfloat16, device=x.device)
-        rows = N * OH * OW
-        s = mn_splits(rows, O, kh * kw * C)
-        ws = cnt = None
-        if s > 1:  # in-launch reduction: the statistics epilogue sees whole tiles
-            ws = torch.empty(s * slab_elems(rows, O), dtype=torch.float32, device=x.device)
-            cnt = counters(tiles_of(rows, O), x.device)
-        tiles_m, tiles_n = -(-rows // 128), -(-O // 128)
-        groups = -(-tiles_m // 16)
-        part = torch.empty((tiles_m + groups) * 2 * O, dtype=torch.float32, device=x.device)
-        bcnt = splitk.counters(tiles_n * (groups + 1), x.device)
-        f32 = dict(dtype=torch.float32, device=x.device)
-        mean, rstd, coef = torch.empty(O, **f32), torch.empty(O, **f32), torch.empty(3 * O, **f32)
-        _C().conv_fwd_bn(x4, w4, stride, pad, dil, y4, s, _V_FWD, ws, cnt, part, bcnt, bn_w, bn_b, rm, rv, nbt,
-                         mean, rstd, coef, float(eps), float(momentum))
+        x4 = _nhwc_bf16(x)
+        y4, mean, rstd, coef = _fwd_bn_launch(x4, w, stride, pad, dil, bn_w, bn_b, rm, rv, nbt, eps, momentum)
         ctx.save_for_backward(x4, w)
         ctx.cfg = (stride, pad, dil)
         ctx.mark_non_differentiable(mean, rstd, coef)
@@ -227,6 +251,101 @@ class _Conv2dNHWCBN(torch.autograd.Function):
         return dx, dw, None, None, None, None, None, None, None, None, None, None
 
 
+class _BNActConvBN(torch.autograd.Function):
+    """``y2 = conv(act(bn1(y1)))`` + bn2's training statistics, where bn1's batch
+    statistics (mean1, rstd1, coef1) came from the launch that produced y1.
+
+    Forward: bn1's apply pass, then one ``conv_fwd_bn`` launch.  Backward: ONE
+    input-gradient launch also reduces bn1's backward statistics (``conv_dgrad_bn``:
+    sum dz', sum dz' (y1 - mean1), finalized into dgamma1, dbeta1 and the apply
+    coefficients), then bn1's backward apply pass gives dy1 -- bn1's separate
+    backward statistics and finalize passes disappear -- and the weight gradient.
+    """
+
+    @staticmethod
+    def forward(ctx, y1, g1, b1, mean1, rstd1, coef1, relu1, w, stride, pad, dil, bn_w, bn_b, rm, rv, nbt, eps, momentum):
+        from p2pfl_amd.ops.batchnorm import _bx
+
+        y14 = _nhwc_bf16(y1)
+        C = y14.shape[3]
+        z4 = _bx().apply_train(y14.reshape(-1, C), None, coef1, bool(relu1)).view(y14.shape)
+        y24, mean, rstd, coef = _fwd_bn_launch(z4, w, stride, pad, dil, bn_w, bn_b, rm, rv, nbt, eps, momentum)
+        ctx.save_for_backward(y14, z4, w, g1, mean1, rstd1)
+        ctx.cfg = (stride, pad, dil, bool(relu1))
+        ctx.mark_non_differentiable(mean, rstd, coef)
+        return y24.permute(0, 3, 1, 2), mean, rstd, coef
+
+    @staticmethod
+    def backward(ctx, dy, _dmean, _drstd, _dcoef):
+        from p2pfl_amd.ops import splitk
+        from p2pfl_amd.ops.batchnorm import _bx
+
+        y14, z4, w, g1, mean1, rstd1 = ctx.saved_tensors
+        stride, pad, dil, relu1 = ctx.cfg
+        dy4 = _nhwc_bf16(dy)
+        w4 = w.permute(0, 2, 3, 1)
+        shape = list(y14.shape)
+        O, kh, kw = w4.shape[0], w4.shape[1], w4.shape[2]
+        C = shape[3]
+        rows = shape[0] * shape[1] * shape[2]
+        dx4 = torch.empty(y14.shape, dtype=torch.bfloat16, device=dy4.device)
+        s = mn_splits(rows, C, kh * kw * O)
+        ws = cnt = None
+        if s > 1:
+            ws = torch.empty(s * slab_elems(rows, C), dtype=torch.float32, device=dy4.device)
+            cnt = counters(tiles_of(rows, C), dy4.device)
+        tiles_m, tiles_n = -(-rows // 128), -(-C // 128)
+        groups = -(-tiles_m // 16)
+        part = torch.empty((tiles_m + groups) * 2 * C, dtype=torch.float32, device=dy4.device)
+        bcnt = splitk.counters(tiles_n * (groups + 1), dy4.device)
+        f32 = dict(dtype=torch.float32, device=dy4.device)
+        dg, db, coefb = torch.empty(C, **f32), torch.empty(C, **f32), torch.empty(3 * C, **f32)
+        _C().conv_dgrad_bn(dy4, w4, stride, pad, dil, dx4, shape, s, _V_DGRAD, ws, cnt, part, bcnt, g1, y14,
+                           z4 if relu1 else None, mean1, rstd1, dg, db, coefb)
+        dy1 = _bx().apply_bwd(dx4.view(rows, C), z4.view(rows, C) if relu1 else None, y14.view(rows, C), mean1, coefb)
+        dy1 = dy1.view(y14.shape).permute(0, 3, 1, 2)
+        dw = _wgrad_launch(dy4, z4, w, stride, pad, dil) if ctx.needs_input_grad[7] else None
+        return (dy1, dg.to(g1.dtype), db.to(g1.dtype), None, None, None, None, dw) + (None,) * 10
+
+
+def conv_bn_stats(x: torch.Tensor, conv: nn.Conv2d, bn: nn.BatchNorm2d):
+    """``(y, mean, rstd, coef)``: ``conv(x)`` on the native kernels with bn's training
+    statistics computed by the same launch, or None when that path does not apply."""
+    from p2pfl_amd.ops import batchnorm as bnops
+
+    capturing = x.is_cuda and torch.cuda.is_current_stream_capturing()
+    if not (_FUSED_BN and bnops.fused_stats_ok(bn) and native_ok(x, conv) and (capturing or _POLICY != "library")):
+        return None
+    track = bn.track_running_stats
+    rm = bn.running_mean if track else None
+    rv = bn.running_var if track else None
+    nbt = bn.num_batches_tracked if track and bn.num_batches_tracked is not None else None
+    STATS["native_fwd_bn"] += 1
+    return _Conv2dNHWCBN.apply(x, conv.weight, _sym(conv.stride), _sym(conv.padding), _sym(conv.dilation), bn.weight,
+                               bn.bias, rm, rv, nbt, bn.eps, bn.momentum)
+
+
+def bn_act_conv_bn_stats(st, bn1: nn.BatchNorm2d, relu1: bool, conv: nn.Conv2d, bn: nn.BatchNorm2d):
+    """Given ``st = (y1, mean1, rstd1, coef1)`` from :func:`conv_bn_stats` (or this
+    function), ``conv(act(bn1(y1)))`` with bn's statistics from the same launch
+    (:class:`_BNActConvBN`), or None when that path does not apply."""
+    from p2pfl_amd.ops import batchnorm as bnops
+
+    y1, mean1, rstd1, coef1 = st
+    capturing = y1.is_cuda and torch.cuda.is_current_stream_capturing()
+    if not (_FUSED_BN and bnops.fused_stats_ok(bn) and native_ok(y1, conv) and (capturing or _POLICY != "library")
+            and conv.weight.shape[0] % 64 == 0):
+        return None
+    track = bn.track_running_stats
+    rm = bn.running_mean if track else None
+    rv = bn.running_var if track else None
+    nbt = bn.num_batches_tracked if track and bn.num_batches_tracked is not None else None
+    STATS["native_fwd_bn"] += 1
+    STATS["bn_act_conv"] += 1
+    return _BNActConvBN.apply(y1, bn1.weight, bn1.bias, mean1, rstd1, coef1, bool(relu1), conv.weight, _sym(conv.stride),
+                              _sym(conv.padding), _sym(conv.dilation), bn.weight, bn.bias, rm, rv, nbt, bn.eps, bn.momentum)
+
+
 def conv_bn_act(x: torch.Tensor, conv: nn.Conv2d, bn: nn.BatchNorm2d, residual=None, relu: bool = True) -> torch.Tensor:
     """``act(bn(conv(x)) [+ residual])``.  In training, on the native implicit-GEMM
     kernels, the convolution's launch computes the batch statistics (and updates the
@@ -234,20 +353,12 @@ def conv_bn_act(x: torch.Tensor, conv: nn.Conv2d, bn: nn.BatchNorm2d, residual=N
     composes :func:`conv2d` and :func:`~p2pfl_amd.ops.batchnorm.batch_norm_act`."""
     from p2pfl_amd.ops import batchnorm as bnops
 
-    capturing = x.is_cuda and torch.cuda.is_current_stream_capturing()
-    if (_FUSED_BN and bnops.fused_stats_ok(bn) and native_ok(x, conv) and (capturing or _POLICY != "library")
-            and (residual is None or residual.is_contiguous(memory_format=torch.channels_last))):
-        track = bn.track_running_stats
-        rm = bn.running_mean if track else None
-        rv = bn.running_var if track else None
-        nbt = bn.num_batches_tracked if track and bn.num_batches_tracked is not None else None
-        STATS["native_fwd_bn"] += 1
-        y, mean, rstd, coef = _Conv2dNHWCBN.apply(x, conv.weight, _sym(conv.stride), _sym(conv.padding),
-                                                  _sym(conv.dilation), bn.weight, bn.bias, rm, rv, nbt, bn.eps,
-                                                  bn.momentum)
-        if residual is not None and residual.shape != y.shape:
-            raise ValueError("conv_bn_act: residual shape mismatch")
-        return bnops.batch_norm_apply(y, bn, mean, rstd, coef, residual, relu)
+    if residual is None or residual.is_contiguous(memory_format=torch.channels_last):
+        st = conv_bn_stats(x, conv, bn)
+        if st is not None:
+            if residual is not None and residual.shape != st[0].shape:
+                raise ValueError("conv_bn_act: residual shape mismatch")
+            return bnops.batch_norm_apply(st[0], bn, st[1], st[2], st[3], residual, relu)
     return bnops.batch_norm_act(conv2d(x, conv), bn, residual=residual, relu=relu)
 
 

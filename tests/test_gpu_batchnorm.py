@@ -267,3 +267,48 @@ def test_conv_bn_statistics_are_deterministic_and_counters_reset(monkeypatch):
     for o in outs[1:]:
         for a, b in zip(outs[0], o):
             assert torch.equal(a, b)
+
+
+@pytest.mark.parametrize("block,cin,cout,stride,hw", [("basic", 64, 64, 1, 16), ("basic", 64, 128, 2, 16),
+                                                       ("bottleneck", 256, 64, 1, 8), ("bottleneck", 64, 128, 2, 8)])
+def test_fused_block_chain_matches_fp32_block(monkeypatch, block, cin, cout, stride, hw):
+    """A whole ResNet block on the fused chain (conv launches computing BN statistics,
+    the inner convolutions' input-gradient launches computing the previous BN's backward
+    statistics) against the same block in fp32 PyTorch: output, running statistics,
+    input gradient and every parameter gradient."""
+    import copy
+
+    from p2pfl_amd.models.resnet import BasicBlock, Bottleneck
+    from p2pfl_amd.ops import conv as conv_ops
+
+    ops.ext()
+    monkeypatch.setattr(conv_ops, "_POLICY", "native")
+    torch.manual_seed(cin + cout + stride)
+    blk = (BasicBlock(cin, cout, stride) if block == "basic" else Bottleneck(cin, cout, stride)).cuda().train()
+    ref = copy.deepcopy(blk).float()
+    for m in blk.modules():
+        if isinstance(m, nn.Conv2d):
+            m.weight.data = m.weight.data.to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    for m in ref.modules():
+        if isinstance(m, nn.Conv2d):
+            m.weight.data = m.weight.data.to(torch.bfloat16).float()
+    x = _cl(torch.randn(16, cin, hw, hw, device="cuda")).to(torch.bfloat16).requires_grad_(True)
+    before = conv_ops.STATS["bn_act_conv"]
+    y = blk(x)
+    assert conv_ops.STATS["bn_act_conv"] > before, "the fused chain did not run"
+    xr = x.detach().float().requires_grad_(True)
+    yr = ref(xr)
+    torch.testing.assert_close(y.float(), yr, atol=8e-2, rtol=5e-2)
+    for (n, a), b in zip(blk.named_buffers(), ref.buffers()):
+        if a.dtype.is_floating_point:
+            torch.testing.assert_close(a, b, atol=2e-3, rtol=2e-2, msg=lambda m, n=n: f"{n}: {m}")
+        else:
+            assert torch.equal(a, b), n
+    dy = _cl(torch.randn(y.shape, device="cuda")).to(torch.bfloat16)
+    y.backward(dy)
+    yr.backward(dy.float())
+    pairs = [("x", x.grad, xr.grad)] + [(n, a.grad, b.grad) for (n, a), b in zip(blk.named_parameters(), ref.parameters())]
+    for n, a, e in pairs:
+        assert a is not None, n
+        scale = e.abs().max().item() + 1e-6
+        torch.testing.assert_close(a.float(), e, atol=5e-2 * scale, rtol=5e-2, msg=lambda m, n=n: f"{n}: {m}")
