@@ -232,6 +232,7 @@ void register_bn(pybind11::module& m);
 void register_rccl(pybind11::module& m);
 void register_gemm(pybind11::module& m);
 void register_conv(pybind11::module& m);
+void register_head(pybind11::module& m);
 
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.doc() = "p2pfl_amd native HIP/CDNA4 kernels (gfx950)";
@@ -260,4 +261,5 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   register_rccl(m);
   register_gemm(m);
   register_conv(m);
+  register_head(m);
 }

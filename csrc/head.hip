@@ -1,0 +1,205 @@
+// Classification head of the CNN families in two launches (gfx950): global
+// average pool -> Linear (N <= 64 classes) -> softmax cross-entropy, forward and
+// backward.  On PyTorch-ROCm this tail is a dozen launches per training step
+// (adaptive_avg_pool2d, the Linear GEMM + bias on hipBLASLt, log_softmax,
+// nll_loss, their backward kernels, the bias-gradient reduction, the pooling
+// broadcast) for a few KFLOP of work.
+//
+//   forward  (grid B): workgroup b pools sample b's [HW][C] channels-last feature
+//            map in fp32, computes its N logits (per-thread channel partials,
+//            fixed-order LDS reduction), its log-sum-exp loss and argmax hit; the
+//            last workgroup to arrive (relaxed ticket, sc1 partials) writes the
+//            batch-mean loss and accuracy in fixed sample order.
+//   backward (grid B + 1): workgroup b < B writes dF[b] = (dL/dlogits_b . W) / HW
+//            broadcast over its HW pixels (bf16, channels-last); workgroup B
+//            computes dW = dlogits^T pooled and db = column sums of dlogits.
+//
+// The reference's heads: nn.Linear + CrossEntropyLoss in
+// /root/reference/p2pfl/learning/pytorch/mnist_examples/models/cnn.py:71-98.
+#include "common.h"
+
+namespace p2head {
+using namespace p2;
+
+constexpr int kT = 256;
+constexpr int kMaxN = 64;
+
+template <typename TW>
+P2_DEVICE float ldw(const TW* w, int64_t i);
+template <>
+P2_DEVICE float ldw<float>(const float* w, int64_t i) { return w[i]; }
+template <>
+P2_DEVICE float ldw<uint16_t>(const uint16_t* w, int64_t i) { return bf16_to_f32(w[i]); }
+
+P2_DEVICE void st_sc1f(float* p, float v) {
+  const auto rs = __builtin_amdgcn_make_buffer_rsrc(p, 0, 4, 0x00020000);
+  __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), rs, 0, 0, 16);
+}
+P2_DEVICE float ld_sc1f(const float* p) {
+  const auto rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(p), 0, 4, 0x00020000);
+  return __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rs, 0, 0, 16));
+}
+
+// f: [B][HW][C] bf16; w: [N][C]; bias [N] fp32 (or null); y [B] int64 (or null: logits only)
+template <typename TW>
+__global__ __launch_bounds__(kT) void head_fwd_kernel(const uint16_t* __restrict__ f, const TW* __restrict__ w,
+                                                      const float* __restrict__ bias, const int64_t* __restrict__ y,
+                                                      float* __restrict__ pooled, float* __restrict__ logits,
+                                                      float* __restrict__ loss_rows, float* __restrict__ loss_out, float* __restrict__ acc_out,
+                                                      int* __restrict__ ctr, int B, int HW, int C, int N) {
+  __shared__ float red[kMaxN][kT / 64];
+  __shared__ float lg[kMaxN];
+  __shared__ int last;
+  const int b = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const float inv = 1.f / float(HW);
+  float part[kMaxN];
+#pragma unroll
+  for (int n = 0; n < kMaxN; ++n) part[n] = 0.f;
+  const uint16_t* fb = f + int64_t(b) * HW * C;
+  for (int c = tid; c < C; c += kT) {
+    float s = 0.f;
+    for (int p = 0; p < HW; ++p) s += bf16_to_f32(fb[int64_t(p) * C + c]);
+    s *= inv;
+    pooled[int64_t(b) * C + c] = s;
+#pragma unroll
+    for (int n = 0; n < kMaxN; ++n)
+      if (n < N) part[n] = fmaf(s, ldw<TW>(w, int64_t(n) * C + c), part[n]);
+  }
+  // fixed-order reduction: wave sums, then the 4 waves in order
+#pragma unroll
+  for (int n = 0; n < kMaxN; ++n) {
+    if (n >= N) break;
+    const float v = wave_sum(part[n]);
+    if (lane == 0) red[n][wave] = v;
+  }
+  __syncthreads();
+  if (tid < N) {
+    float z = red[tid][0] + red[tid][1] + red[tid][2] + red[tid][3];
+    if (bias) z += bias[tid];
+    lg[tid] = z;
+    logits[int64_t(b) * N + tid] = z;
+  }
+  __syncthreads();
+  if (!y) return;
+  if (tid == 0) {
+    float mx = lg[0];
+    int arg = 0;
+    for (int n = 1; n < N; ++n)
+      if (lg[n] > mx) {
+        mx = lg[n];
+        arg = n;
+      }
+    float se = 0.f;
+    for (int n = 0; n < N; ++n) se += __expf(lg[n] - mx);
+    const int yy = min(max(int(y[b]), 0), N - 1);
+    const float lv = (logf(se) + mx) - lg[yy];
+    st_sc1f(loss_rows + b, lv);
+    st_sc1f(loss_rows + B + b, arg == yy ? 1.f : 0.f);
+  }
+  // last arrival writes [mean loss, accuracy] in sample order
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (tid == 0) {
+    const int old = __hip_atomic_fetch_add(ctr, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    last = old == B - 1;
+    if (last) __hip_atomic_store(ctr, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  __syncthreads();
+  if (!last || tid != 0) return;
+  float sl = 0.f, sa = 0.f;
+  for (int i = 0; i < B; ++i) {
+    sl += ld_sc1f(loss_rows + i);
+    sa += ld_sc1f(loss_rows + B + i);
+  }
+  loss_out[0] = sl / float(B);
+  acc_out[0] = sa / float(B);
+}
+
+// dl[n] of sample b: (softmax(logits_b)[n] - [n == y_b]) * gscale
+P2_DEVICE void dlogits(const float* lg, int yy, int N, float gscale, float* dl) {
+  float mx = lg[0];
+  for (int n = 1; n < N; ++n) mx = fmaxf(mx, lg[n]);
+  float se = 0.f;
+  for (int n = 0; n < N; ++n) se += __expf(lg[n] - mx);
+  const float r = 1.f / se;
+  for (int n = 0; n < N; ++n) dl[n] = (__expf(lg[n] - mx) * r - (n == yy ? 1.f : 0.f)) * gscale;
+}
+
+template <typename TW>
+__global__ __launch_bounds__(kT) void head_bwd_kernel(const float* __restrict__ gloss, const float* __restrict__ logits,
+                                                      const int64_t* __restrict__ y, const float* __restrict__ pooled,
+                                                      const TW* __restrict__ w, uint16_t* __restrict__ df,
+                                                      TW* __restrict__ dw, float* __restrict__ db, int B, int HW,
+                                                      int C, int N) {
+  __shared__ float dl[kMaxN];
+  const int b = blockIdx.x, tid = threadIdx.x;
+  const float gscale = gloss[0] / float(B);
+  if (b < B) {
+    if (tid == 0) dlogits(logits + int64_t(b) * N, min(max(int(y[b]), 0), N - 1), N, gscale, dl);
+    __syncthreads();
+    const float inv = 1.f / float(HW);
+    uint16_t* out = df + int64_t(b) * HW * C;
+    for (int c = tid; c < C; c += kT) {
+      float s = 0.f;
+      for (int n = 0; n < N; ++n) s = fmaf(dl[n], ldw<TW>(w, int64_t(n) * C + c), s);
+      const uint16_t v = f32_to_bf16(s * inv);
+      for (int p = 0; p < HW; ++p) out[int64_t(p) * C + c] = v;
+    }
+    return;
+  }
+  // workgroup B: dW[n][c] = sum_b dl_b[n] pooled[b][c], db[n] = sum_b dl_b[n]
+  __shared__ float dla[64][kMaxN];  // dl of up to 64 samples per chunk
+  for (int b0 = 0; b0 < B; b0 += 64) {
+    const int nb = min(64, B - b0);
+    __syncthreads();
+    if (tid < nb) dlogits(logits + int64_t(b0 + tid) * N, min(max(int(y[b0 + tid]), 0), N - 1), N, gscale, dla[tid]);
+    __syncthreads();
+    if (b0 == 0 && tid < N) {
+      float s = 0.f;
+      for (int i = 0; i < nb; ++i) s += dla[i][tid];
+      db[tid] = s;
+    } else if (tid < N) {
+      float s = db[tid];
+      for (int i = 0; i < nb; ++i) s += dla[i][tid];
+      db[tid] = s;
+    }
+    for (int e = tid; e < N * C; e += kT) {
+      const int n = e / C, c = e - n * C;
+      float s = b0 == 0 ? 0.f : ldw<TW>(dw, e);
+      for (int i = 0; i < nb; ++i) s = fmaf(dla[i][n], pooled[int64_t(b0 + i) * C + c], s);
+      if constexpr (sizeof(TW) == 4)
+        dw[e] = s;
+      else
+        dw[e] = f32_to_bf16(s);
+    }
+  }
+}
+
+}  // namespace p2head
+
+namespace p2 {
+
+void head_fwd(const uint16_t* f, const void* w, int w_bf16, const float* bias, const int64_t* y, float* pooled,
+              float* logits, float* loss_rows, float* loss, float* acc, int* ctr, int B, int HW, int C, int N,
+              hipStream_t s) {
+  using namespace p2head;
+  if (w_bf16)
+    hipLaunchKernelGGL(head_fwd_kernel<uint16_t>, dim3(B), dim3(kT), 0, s, f, static_cast<const uint16_t*>(w), bias, y,
+                       pooled, logits, loss_rows, loss, acc, ctr, B, HW, C, N);
+  else
+    hipLaunchKernelGGL(head_fwd_kernel<float>, dim3(B), dim3(kT), 0, s, f, static_cast<const float*>(w), bias, y,
+                       pooled, logits, loss_rows, loss, acc, ctr, B, HW, C, N);
+}
+
+void head_bwd(const float* gloss, const float* logits, const int64_t* y, const float* pooled, const void* w, int w_bf16,
+              uint16_t* df, void* dw, float* db, int B, int HW, int C, int N, hipStream_t s) {
+  using namespace p2head;
+  if (w_bf16)
+    hipLaunchKernelGGL(head_bwd_kernel<uint16_t>, dim3(B + 1), dim3(kT), 0, s, gloss, logits, y, pooled,
+                       static_cast<const uint16_t*>(w), df, static_cast<uint16_t*>(dw), db, B, HW, C, N);
+  else
+    hipLaunchKernelGGL(head_bwd_kernel<float>, dim3(B + 1), dim3(kT), 0, s, gloss, logits, y, pooled,
+                       static_cast<const float*>(w), df, static_cast<float*>(dw), db, B, HW, C, N);
+}
+
+}  // namespace p2

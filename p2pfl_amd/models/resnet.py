@@ -44,12 +44,15 @@ from torch import nn
 
 from p2pfl_amd.models.base import FLModule, seed_everything
 from p2pfl_amd.ops.batchnorm import batch_norm_act, batch_norm_apply
+from p2pfl_amd.ops.head import head_ok, head_xent
 from p2pfl_amd.ops.conv import bn_act_conv_bn_stats, conv2d, conv_bn_act, conv_bn_stats, stem_conv2d, stem_ok
 
 # NHWC activations on the GPU (P2PFL_CHANNELS_LAST=0 keeps NCHW)
 _CHANNELS_LAST = os.environ.get("P2PFL_CHANNELS_LAST", "1") != "0"
 # 3-channel stem on the direct HIP kernels (csrc/stem.hip); P2PFL_NATIVE_STEM=0 restores F.conv2d
 _NATIVE_STEM = os.environ.get("P2PFL_NATIVE_STEM", "1") != "0"
+# pool + fc + cross-entropy on csrc/head.hip (P2PFL_NATIVE_HEAD=0: PyTorch / hipBLASLt)
+_NATIVE_HEAD = os.environ.get("P2PFL_NATIVE_HEAD", "1") != "0"
 
 
 def _shortcut(sc: nn.Module, x: torch.Tensor) -> torch.Tensor:
@@ -154,7 +157,8 @@ class ResNet(FLModule):
                 nn.init.ones_(m.weight)
                 nn.init.zeros_(m.bias)
 
-    def forward(self, x: torch.Tensor) -> torch.Tensor:
+    def features(self, x: torch.Tensor) -> torch.Tensor:
+        """The last stage's feature map (channels-last on the GPU)."""
         stem = self.stem[0]
         if _NATIVE_STEM and stem_ok(x, stem):
             # direct small-C kernel: reads the batch as it is (uint8 with the 1/255 folded
@@ -169,9 +173,32 @@ class ResNet(FLModule):
         x = batch_norm_act(x, self.stem[1])
         if len(self.stem) > 3:
             x = self.stem[3](x)
-        x = self.layer4(self.layer3(self.layer2(self.layer1(x))))
-        x = torch.flatten(nn.functional.adaptive_avg_pool2d(x, 1), 1)
+        return self.layer4(self.layer3(self.layer2(self.layer1(x))))
+
+    def forward(self, x: torch.Tensor) -> torch.Tensor:
+        x = torch.flatten(nn.functional.adaptive_avg_pool2d(self.features(x), 1), 1)
         return self.fc(x)
+
+    # pool + fc + cross-entropy as two HIP launches (ops/head.py) when the shapes allow
+    def training_step(self, batch, batch_idx: int) -> torch.Tensor:
+        x, y = batch
+        f = self.features(x)
+        if _NATIVE_HEAD and head_ok(f, self.fc, y):
+            loss, _, _ = head_xent(f, self.fc, y)
+        else:
+            loss = self.loss_fn(self.fc(torch.flatten(nn.functional.adaptive_avg_pool2d(f, 1), 1)), y)
+        self.log("train_loss", loss, prog_bar=True)
+        return loss
+
+    def _eval_step(self, batch, prefix: str) -> torch.Tensor:
+        x, y = batch
+        f = self.features(x)
+        if _NATIVE_HEAD and head_ok(f, self.fc, y):
+            loss, _, acc = head_xent(f, self.fc, y)
+            self.log(f"{prefix}_loss", loss, prog_bar=True)
+            self.log(f"{prefix}_metric", acc, prog_bar=True)
+            return loss
+        return super()._eval_step(batch, prefix)
 
     def channels_last_parameter_names(self) -> List[str]:
         """Spatial conv weights a mixed-precision arena keeps in channels-last order (NHWC activations)."""

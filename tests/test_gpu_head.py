@@ -1,0 +1,62 @@
+"""Pool + Linear + cross-entropy head (csrc/head.hip) vs fp32 PyTorch."""
+
+from __future__ import annotations
+
+import pytest
+import torch
+from torch import nn
+
+from p2pfl_amd import ops
+from p2pfl_amd.ops.head import head_ok, head_reference, head_xent
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.mark.parametrize("B,C,H,W,N", [(32, 512, 4, 4, 10), (7, 2048, 4, 4, 10), (3, 64, 1, 1, 64), (70, 256, 2, 3, 5)])
+@pytest.mark.parametrize("wdtype", [torch.float32, torch.bfloat16])
+def test_head_xent_vs_fp32(B, C, H, W, N, wdtype):
+    ops.ext()
+    g = torch.Generator(device="cuda").manual_seed(B + C + N)
+    f = torch.randn(B, C, H, W, device="cuda", generator=g).to(torch.bfloat16)
+    f = f.contiguous(memory_format=torch.channels_last).requires_grad_(True)
+    fc = nn.Linear(C, N).cuda()
+    fc.weight.data = fc.weight.data.to(wdtype)
+    y = torch.randint(0, N, (B,), device="cuda", generator=g)
+    assert head_ok(f, fc, y)
+    loss, logits, acc = head_xent(f, fc, y)
+    fr = f.detach().float().requires_grad_(True)
+    wr = fc.weight.detach().float().requires_grad_(True)
+    br = fc.bias.detach().float().requires_grad_(True)
+    lr, logr = head_reference(fr, wr, br, y)
+    torch.testing.assert_close(logits, logr, atol=1e-3, rtol=1e-3)
+    torch.testing.assert_close(loss, lr, atol=1e-4, rtol=1e-4)
+    assert abs(acc.item() - (logr.argmax(1) == y).float().mean().item()) < 1e-6
+    loss.backward()
+    lr.backward()
+    torch.testing.assert_close(f.grad.float(), fr.grad, atol=1e-4, rtol=2e-2)
+    tol = dict(atol=1e-3, rtol=1e-2) if wdtype == torch.bfloat16 else dict(atol=1e-5, rtol=1e-4)
+    torch.testing.assert_close(fc.weight.grad.float(), wr.grad, **tol)
+    torch.testing.assert_close(fc.bias.grad, br.grad, atol=1e-6, rtol=1e-4)
+    assert fc.weight.grad.dtype == wdtype and f.grad.is_contiguous(memory_format=torch.channels_last)
+
+
+def test_resnet_training_step_uses_native_head(monkeypatch):
+    """ResNet's training step goes through the head kernels and matches the
+    PyTorch head on the same features."""
+    from p2pfl_amd.models.resnet import ResNet18
+
+    ops.ext()
+    m = ResNet18(seed=0).cuda().eval()
+    x = torch.randint(0, 256, (4, 3, 32, 32), dtype=torch.uint8, device="cuda")
+    y = torch.randint(0, 10, (4,), device="cuda")
+    calls = []
+    import p2pfl_amd.models.resnet as rn
+
+    real = rn.head_xent
+    monkeypatch.setattr(rn, "head_xent", lambda *a: calls.append(1) or real(*a))
+    with torch.autocast("cuda", dtype=torch.bfloat16):
+        f = m.features(x.float() / 255).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+        loss = m.validation_step((x.float() / 255, y), 0)
+    assert calls, "the head kernels did not run"
+    lr, _ = head_reference(f, m.fc.weight, m.fc.bias, y)
+    torch.testing.assert_close(loss, lr, atol=5e-3, rtol=5e-3)
