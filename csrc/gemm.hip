@@ -78,6 +78,10 @@ void gemm_bf16(const GemmParams& p, hipStream_t s) {
     gemm_bf16_pp(q, s);
     return;
   }
+  if (q.variant & 4096) {
+    gemm_bf16_w4(q, s);
+    return;
+  }
   if (p.a_kmajor && p.b_kmajor)
     launch(q, PlainK{p.a, p.lda, p.M, p.K}, PlainK{p.b, p.ldb, p.N, p.K}, s);
   else if (p.a_kmajor)
@@ -91,7 +95,12 @@ void gemm_bf16(const GemmParams& p, hipStream_t s) {
 void tile_slab_reduce(const float* ws, int splits, int M, int N, int64_t ldc, void* out, int out_bf16, int variant,
                       hipStream_t s) {
   using namespace p2gemm;
-  if (variant & 64) {
+  if (variant & 4096) {  // 4-wave tile: slabs of whole 256 x 256 tiles, same fragment-native order per wave
+    const int tm = (M + 255) / 256, tn = (N + 255) / 256;
+    const int64_t groups = int64_t(tm) * tn * (256 * 256 / 4);
+    hipLaunchKernelGGL(tile_slab_reduce_kernel<TileCfg<256, 256, 2, 2>>, dim3(int((groups + 255) / 256)), dim3(256), 0, s,
+                       ws, splits, M, N, ldc, out, out_bf16, variant, tm, tn);
+  } else if (variant & 64) {
     const int tm = (M + 255) / 256, tn = (N + 255) / 256;
     const int64_t groups = int64_t(tm) * tn * (256 * 256 / 4);
     hipLaunchKernelGGL(tile_slab_reduce_kernel<Tile256>, dim3(int((groups + 255) / 256)), dim3(256), 0, s, ws, splits, M,
