@@ -98,8 +98,9 @@ void tile_slab_reduce(const float* ws, int splits, int M, int N, int64_t ldc, vo
   if (variant & 4096) {  // 4-wave tile: slabs of whole 256 x 256 tiles, same fragment-native order per wave
     const int tm = (M + 255) / 256, tn = (N + 255) / 256;
     const int64_t groups = int64_t(tm) * tn * (256 * 256 / 4);
-    hipLaunchKernelGGL(tile_slab_reduce_kernel<TileCfg<256, 256, 2, 2>>, dim3(int((groups + 255) / 256)), dim3(256), 0, s,
-                       ws, splits, M, N, ldc, out, out_bf16, variant, tm, tn);
+    using Tile4w = TileCfg<256, 256, 2, 2>;
+    hipLaunchKernelGGL(tile_slab_reduce_kernel<Tile4w>, dim3(int((groups + 255) / 256)), dim3(256), 0, s, ws, splits, M,
+                       N, ldc, out, out_bf16, variant, tm, tn);
   } else if (variant & 64) {
     const int tm = (M + 255) / 256, tn = (N + 255) / 256;
     const int64_t groups = int64_t(tm) * tn * (256 * 256 / 4);
