@@ -271,11 +271,12 @@ def test_conv_bn_statistics_are_deterministic_and_counters_reset(monkeypatch):
 
 @pytest.mark.parametrize("block,cin,cout,stride,hw", [("basic", 64, 64, 1, 16), ("basic", 64, 128, 2, 16),
                                                        ("bottleneck", 256, 64, 1, 8), ("bottleneck", 64, 128, 2, 8)])
-def test_fused_block_chain_matches_fp32_block(monkeypatch, block, cin, cout, stride, hw):
+def test_fused_block_chain_matches_separate_bn_kernels_and_fp32(monkeypatch, block, cin, cout, stride, hw):
     """A whole ResNet block on the fused chain (conv launches computing BN statistics,
     the inner convolutions' input-gradient launches computing the previous BN's backward
-    statistics) against the same block in fp32 PyTorch: output, running statistics,
-    input gradient and every parameter gradient."""
+    statistics) against (a) the same bf16 block with the separate BN kernels and (b) the
+    block in fp32 PyTorch: output, running statistics, input gradient and every
+    parameter gradient."""
     import copy
 
     from p2pfl_amd.models.resnet import BasicBlock, Bottleneck
@@ -289,32 +290,50 @@ def test_fused_block_chain_matches_fp32_block(monkeypatch, block, cin, cout, str
     for m in blk.modules():
         if isinstance(m, nn.Conv2d):
             m.weight.data = m.weight.data.to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    sep = copy.deepcopy(blk)
     for m in ref.modules():
         if isinstance(m, nn.Conv2d):
             m.weight.data = m.weight.data.to(torch.bfloat16).float()
-    x = _cl(torch.randn(16, cin, hw, hw, device="cuda")).to(torch.bfloat16).requires_grad_(True)
-    before = conv_ops.STATS["bn_act_conv"]
-    y = blk(x)
-    assert conv_ops.STATS["bn_act_conv"] > before, "the fused chain did not run"
-    xr = x.detach().float().requires_grad_(True)
+    x0 = _cl(torch.randn(16, cin, hw, hw, device="cuda")).to(torch.bfloat16)
+    dy = _cl(torch.randn(blk(x0.clone()).shape, device="cuda")).to(torch.bfloat16)
+    for m in (blk, sep):  # the probe call above advanced blk's running statistics: start both fresh
+        for b in m.modules():
+            if isinstance(b, nn.BatchNorm2d):
+                b.reset_running_stats()
+    for b in ref.modules():
+        if isinstance(b, nn.BatchNorm2d):
+            b.reset_running_stats()
+
+    def run(model, fused):
+        monkeypatch.setattr(conv_ops, "_FUSED_BN", fused)
+        x = x0.clone().requires_grad_(True)
+        before = conv_ops.STATS["bn_act_conv"]
+        y = model(x)
+        assert (conv_ops.STATS["bn_act_conv"] > before) == fused
+        y.backward(dy)
+        return x, y
+
+    xf, yf = run(blk, True)
+    xs, ys = run(sep, False)
+    xr = x0.float().requires_grad_(True)
     yr = ref(xr)
-    torch.testing.assert_close(y.float(), yr, atol=8e-2, rtol=5e-2)
-    for (n, a), b in zip(blk.named_buffers(), ref.buffers()):
+    yr.backward(dy.float())
+
+    def rel(a, e):
+        return ((a.float() - e.float()).norm() / (e.float().norm() + 1e-12)).item()
+
+    # (a) fused vs separate BN kernels: same bf16 arithmetic up to summation order
+    assert rel(yf, ys) < 1e-2
+    for (n, a), b in zip(blk.named_buffers(), sep.buffers()):
         if a.dtype.is_floating_point:
-            torch.testing.assert_close(a, b, atol=2e-3, rtol=2e-2, msg=lambda m, n=n: f"{n}: {m}")
+            torch.testing.assert_close(a, b, atol=1e-3, rtol=1e-2, msg=lambda m, n=n: f"{n}: {m}")
         else:
             assert torch.equal(a, b), n
-    dy = _cl(torch.randn(y.shape, device="cuda")).to(torch.bfloat16)
-    y.backward(dy)
-    yr.backward(dy.float())
-    pairs = [("x", x.grad, xr.grad)] + [(n, a.grad, b.grad) for (n, a), b in zip(blk.named_parameters(), ref.parameters())]
-    for n, a, e in pairs:
-        assert a is not None, n
-        # bf16 activations vs an fp32 block: a few elements sit on the ReLU threshold and
-        # flip their mask, so judge each gradient by its relative L2 error and by the
-        # fraction of elements within tolerance, not by the worst element
-        a = a.float()
-        rel = ((a - e).norm() / (e.norm() + 1e-12)).item()
-        scale = e.abs().max().item() + 1e-6
-        close = ((a - e).abs() <= 5e-2 * scale + 5e-2 * e.abs()).float().mean().item()
-        assert rel < 5e-2 and close > 0.98, f"{n}: relative L2 error {rel:.3g}, within tolerance {close:.4f}"
+    pairs = [("x", xf.grad, xs.grad, xr.grad)] + [
+        (n, a.grad, b.grad, c.grad) for (n, a), b, c in zip(blk.named_parameters(), sep.parameters(), ref.parameters())]
+    for n, a, b, c in pairs:
+        assert a is not None and b is not None, n
+        assert rel(a, b) < 3e-2, f"{n}: fused vs separate BN kernels, relative L2 error {rel(a, b):.3g}"
+        # (b) vs fp32: bf16 activations flip a few ReLU masks; a loose sanity bound
+        assert rel(a, c) < 0.12, f"{n}: fused vs fp32, relative L2 error {rel(a, c):.3g}"
+    torch.testing.assert_close(yf.float(), yr, atol=8e-2, rtol=5e-2)
