@@ -34,8 +34,22 @@
 // the ViT-B/16 shapes of BASELINE.json config 4.
 #include "gemm_core.h"
 
+#include <utility>
+
 namespace p2w4 {
 using namespace p2gemm;
+
+// f(std::integral_constant<int, I>) for I = 0 .. N-1, expanded at compile time: the
+// accumulator indices stay constant expressions, so the accumulator array is never
+// demoted to scratch memory (a plain unrolled loop over 64 groups was, 1088 B/lane)
+template <class F, int... I>
+P2_DEVICE void static_for_impl(F&& f, std::integer_sequence<int, I...>) {
+  (f(std::integral_constant<int, I>{}), ...);
+}
+template <int N, class F>
+P2_DEVICE void static_for(F&& f) {
+  static_for_impl(f, std::make_integer_sequence<int, N>{});
+}
 
 constexpr int TM = 256, TN = 256, NTH = 256;
 constexpr int STAGE4 = 4 * TILE;  // A halves 0,1 | B halves 2,3 (16 KB each)
@@ -110,10 +124,13 @@ __global__ __launch_bounds__(NTH, 1) void gemm_w4_kernel(GemmParams p, LA la, LB
   const int h = lane >> 5;
   // explicit AGPR reads, one 4-value group at a time: left to itself the compiler
   // copies all 256 accumulators to VGPRs before the epilogue and spills
-  auto rd = [&](int i, int j, int g) __attribute__((always_inline)) {
+  auto rd = [&](auto qc) __attribute__((always_inline)) {
+    constexpr int q = decltype(qc)::value, i = q >> 4, j = (q >> 2) & 3, g = q & 3;
     f32x4 r;
-#pragma unroll
-    for (int e = 0; e < 4; ++e) asm volatile("v_accvgpr_read_b32 %0, %1" : "=v"(r[e]) : "a"(acc[i][j][4 * g + e]));
+    asm volatile("v_accvgpr_read_b32 %0, %1" : "=v"(r[0]) : "a"(acc[i][j][4 * g + 0]));
+    asm volatile("v_accvgpr_read_b32 %0, %1" : "=v"(r[1]) : "a"(acc[i][j][4 * g + 1]));
+    asm volatile("v_accvgpr_read_b32 %0, %1" : "=v"(r[2]) : "a"(acc[i][j][4 * g + 2]));
+    asm volatile("v_accvgpr_read_b32 %0, %1" : "=v"(r[3]) : "a"(acc[i][j][4 * g + 3]));
     return r;
   };
   const uint32_t lane_off = uint32_t(((wave * QN) * 64 + lane) * 16);
@@ -124,16 +141,15 @@ __global__ __launch_bounds__(NTH, 1) void gemm_w4_kernel(GemmParams p, LA la, LB
   if (SPLIT) {
     // this slice's fragment-native fp32 slab (sc1 stores when reduced in the launch)
     const auto rs = rsrc(split);
-#pragma unroll
-    for (int q = 0; q < QN; ++q) {
-      const int i = q >> 4, j = (q >> 2) & 3, g = q & 3;
-      const f32x4 v = rd(i, j, g);
+    static_for<QN>([&](auto qc) __attribute__((always_inline)) {
+      constexpr int q = decltype(qc)::value;
+      const f32x4 v = rd(qc);
       if (p.counters)
         __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), rs, lane_off + q * 1024, 0, 16);
       else
         __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), rs, lane_off + q * 1024, 0, 0);
       __builtin_amdgcn_sched_barrier(0);  // keep the AGPR reads next to their store
-    }
+    });
     if (!p.counters) return;
     // the last slice to reach the tile reduces it (hand-off of gemm_core.h)
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -210,13 +226,10 @@ __global__ __launch_bounds__(NTH, 1) void gemm_w4_kernel(GemmParams p, LA la, LB
           }
         }
       } else {
-#pragma unroll
-        for (int i = 0; i < 4; ++i)
-#pragma unroll
-          for (int j = 0; j < 4; ++j)
-#pragma unroll
-            for (int g = 0; g < 4; ++g)
-              finish(i, j, g, rd(i, j, g));
+        static_for<QN>([&](auto qc) __attribute__((always_inline)) {
+          constexpr int q = decltype(qc)::value;
+          finish(q >> 4, (q >> 2) & 3, q & 3, rd(qc));
+        });
       }
     }
     if (!p.c_bf16) continue;

@@ -296,7 +296,8 @@ class FusedCNNLearner(TorchLearner):
         if g is None or g.key != key:
             import gc
 
-            gc.collect()  # outside the exclusive section (see step_graph.no_gc)
+            with GATE.shared():  # outside the exclusive section, never during another thread's capture
+                gc.collect()
             with GATE.exclusive():  # no other learner's GPU work during the capture
                 g = self._capture(name, loader, plan, train, key)
             self._graphs[name] = g

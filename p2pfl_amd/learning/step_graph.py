@@ -175,7 +175,8 @@ class TrainStepGraph:
             opt.t = t_host
             for p in opt.mt.params:  # eager gradients are not the graph's
                 p.grad = None
-        gc.collect()  # before the exclusive section: a full collection can take a while
+        with GATE.shared():  # before the exclusive section (a full collection can take a while), but
+            gc.collect()  # never while another thread records: a destructor's HIP call would break its capture
         with GATE.exclusive(), _CAPTURE_LOCK:
             torch.cuda.synchronize(dev)
             g = torch.cuda.CUDAGraph()
@@ -254,7 +255,7 @@ class EvalStepGraph:
                 self.idx.copy_(idx)
                 self.step(self.idx, float(self.B), cache=False)
             self.stream.synchronize()
-        gc.collect()
+            gc.collect()  # under the shared gate: never while another thread records
         with GATE.exclusive(), _CAPTURE_LOCK:  # recording only
             torch.cuda.synchronize(learner.device)
             g = torch.cuda.CUDAGraph()
