@@ -337,7 +337,7 @@ class FusedCNNLearner(TorchLearner):
             torch.cuda.synchronize(self.device)
             saved = [t.clone() for t in (self.engine.params, self.engine.m, self.engine.v, self.engine.adam_t)]
             graph = torch.cuda.CUDAGraph()
-            with no_gc(collect=False), torch.cuda.graph(graph, stream=self._stream, capture_error_mode="thread_local"):
+            with no_gc(collect=False), torch.cuda.graph(graph, stream=self._stream, capture_error_mode="relaxed"):
                 self._enqueue(loader, plan, train, eg.perm, eg.stats)
             torch.cuda.synchronize(self.device)
             for dst, src in zip((self.engine.params, self.engine.m, self.engine.v, self.engine.adam_t), saved):

@@ -31,7 +31,12 @@ from p2pfl_amd.utils.lockcheck import make_lock
 from p2pfl_amd.utils.streams import private_stream
 
 # virtual peers (one node thread each) may capture concurrently: serialise
-# captures process-wide, capture in thread-local mode (other threads' work stays legal)
+# captures process-wide.  Captures run in "relaxed" error mode: the exclusive
+# device gate already keeps every other learner's GPU work out of the recording
+# window, and what other threads may still do then -- drop the last reference to
+# a graph / event (a destroy call), wait on an event in a completion thread --
+# must not invalidate this thread's capture (in "thread_local" mode on ROCm it
+# did: the process aborted in tests/test_gpu_node.py::test_virtual_peers_on_gpu).
 _CAPTURE_LOCK = make_lock("StepGraph._CAPTURE_LOCK")
 
 
@@ -181,7 +186,7 @@ class TrainStepGraph:
             torch.cuda.synchronize(dev)
             g = torch.cuda.CUDAGraph()
             self.counters = splitk.GraphCounters(dev)  # split-K tile counters owned by this graph
-            with no_gc(collect=False), splitk.graph_scope(self.counters), torch.cuda.graph(g, stream=self.stream, capture_error_mode="thread_local"):
+            with no_gc(collect=False), splitk.graph_scope(self.counters), torch.cuda.graph(g, stream=self.stream, capture_error_mode="relaxed"):
                 self.loss = self._body(graph=True)
             opt.mt.fill_grad_table(self.gtab)  # the graph's gradient buffers, fixed for every replay
             opt.t = t_host  # recording executed nothing; host-side counters back to the pre-capture state
@@ -260,7 +265,7 @@ class EvalStepGraph:
             torch.cuda.synchronize(learner.device)
             g = torch.cuda.CUDAGraph()
             self.counters = splitk.GraphCounters(learner.device)
-            with no_gc(collect=False), splitk.graph_scope(self.counters), torch.cuda.graph(g, stream=self.stream, capture_error_mode="thread_local"):
+            with no_gc(collect=False), splitk.graph_scope(self.counters), torch.cuda.graph(g, stream=self.stream, capture_error_mode="relaxed"):
                 self.step(self.idx, float(self.B), cache=False)
             torch.cuda.synchronize(learner.device)
         self.graph = g
