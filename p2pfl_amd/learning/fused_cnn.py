@@ -284,14 +284,19 @@ class FusedCNNLearner(TorchLearner):
     def _plan(self, n: int, B: int) -> List[Tuple[int, int]]:
         return [(s, min(B, n - s)) for s in range(0, n, B)]
 
-    def _run(self, name: str, loader, train: bool, perm: Optional[torch.Tensor]) -> torch.Tensor:
-        """Enqueue a pass over ``loader``; returns a [steps, 2] stats tensor (loss sum, correct)."""
+    def _graph_key(self, name: str, loader, train: bool):
         n = len(loader.dataset)
         B = loader.batch_size if train else _EvalForward.MROWS
-        plan = self._plan(n, B)
-        key = (name, n, B, loader.x.data_ptr(), loader.y.data_ptr())
+        return self._plan(n, B), (name, n, B, loader.x.data_ptr(), loader.y.data_ptr())
+
+    def _ensure_graph(self, name: str, loader, train: bool) -> "_EpochGraph":
+        """The captured pass for ``loader`` (capturing it on first use).  Called
+        WITHOUT ``self._lock``: waiting for the exclusive device gate can take as
+        long as another peer's warm-up, and the capture saves / restores the state
+        it touches inside the exclusive section, so no other enqueue can see it."""
         from p2pfl_amd.learning.step_graph import GATE
 
+        plan, key = self._graph_key(name, loader, train)
         g = self._graphs.get(name)
         if g is None or g.key != key:
             import gc
@@ -301,6 +306,14 @@ class FusedCNNLearner(TorchLearner):
             with GATE.exclusive():  # no other learner's GPU work during the capture
                 g = self._capture(name, loader, plan, train, key)
             self._graphs[name] = g
+        return g
+
+    def _run(self, name: str, loader, train: bool, perm: Optional[torch.Tensor]) -> torch.Tensor:
+        """Enqueue a pass over ``loader``; returns a [steps, 2] stats tensor (loss sum, correct)."""
+        from p2pfl_amd.learning.step_graph import GATE
+
+        plan, _ = self._graph_key(name, loader, train)
+        g = self._ensure_graph(name, loader, train)
         with GATE.shared():
             if perm is not None:
                 g.perm.copy_(perm, non_blocking=True)
@@ -377,6 +390,7 @@ class FusedCNNLearner(TorchLearner):
         prev = self._fit_done
         if prev is not None:
             prev.synchronize()  # the previous round's training finished on the GPU
+        self._ensure_graph("train", self.data.train_dataloader(), True)  # first-use capture outside the lock
         with self._lock:
             self.engine.reset_optimizer()  # Adam re-created per fit (reference quirk Q23)
             loader = self.data.train_dataloader()
@@ -418,6 +432,7 @@ class FusedCNNLearner(TorchLearner):
     def _eval_async(self, name: str, loader, on_done) -> None:
         """Enqueue an evaluation pass on the current stream; ``on_done(loss, metric)``
         runs on the completion thread."""
+        self._ensure_graph(name, loader, False)  # first-use capture outside the lock
         with self._lock:
             stats = self._run(name, loader, False, None)
         host = self._readback(stats[0, :2])
