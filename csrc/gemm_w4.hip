@@ -110,10 +110,15 @@ __global__ __launch_bounds__(NTH, 1) void gemm_w4_kernel(GemmParams p, LA la, LB
 #pragma unroll
         for (int j = 0; j < 4; ++j) fb[cb ^ 1][j] = frag<LB::KMAJ>(b_half + cur, 32 * j, ks + 1, lane);
       }
+      // the 8 fragment reads of substep ks + 1 are issued before the 16 MFMAs of ks
+      // (left alone, the scheduler sank each read next to its first use and exposed
+      // the LDS latency 4x per substep at one wave per SIMD)
+      __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
       for (int i = 0; i < 4; ++i)
 #pragma unroll
         for (int j = 0; j < 4; ++j) acc[i][j] = mfma(fb[cb][j], fa[cb][i], acc[i][j]);
+      __builtin_amdgcn_sched_barrier(0);
     }
   }
 
