@@ -13,6 +13,8 @@
 #   scripts/gpu.sh models [steps]           configs 3-5: resnet18, resnet50, vit_b16 rounds
 #   scripts/gpu.sh rehearsal [N...]         split-hosts multi-rank rehearsal on the one GPU (default 2 4 8)
 #   scripts/gpu.sh prof <tag> <cmd...>      rocprofv3 --kernel-trace --stats of <cmd> -> gpurun_out/prof_<tag>
+#   scripts/gpu.sh overlap [on|off] [rounds] 8 virtual ResNet-50 peers (fault-tolerance scenario) under a
+#                                           kernel trace + cross-stream overlap summary of training / FedAvg
 #   scripts/gpu.sh py <secs> <tag> <cmd...> any python command, own limit
 #
 # Several modes can be chained with "+", e.g.
@@ -58,6 +60,18 @@ run_mode() {
       local tag=$1; shift
       rm -rf "gpurun_out/prof_$tag"
       step 400 "prof_$tag" rocprofv3 --kernel-trace --stats -d "gpurun_out/prof_$tag" -o run -- "$@" ;;
+    overlap)
+      local mode=${1:-on} rounds=${2:-5} d=gpurun_out/prof_overlap_${1:-on}
+      rm -rf "$d"
+      step 600 "overlap_$mode" rocprofv3 --kernel-trace --output-format csv -d "$d" -o run -- \
+        python -u -m p2pfl_amd.examples.fault_tolerance --peers 8 --rounds "$rounds" --overlap "$mode"
+      local csv
+      csv=$(ls "$d"/*kernel_trace.csv "$d"/*/*kernel_trace.csv 2>/dev/null | head -1)
+      step 120 "overlap_${mode}_train" python tools/overlap_summary.py "$csv" --a 'conv_kernel|p2bn|sgd_mt|p2head' \
+        --b 'conv_kernel|p2bn|sgd_mt|p2head' --out "$d/overlap_train.md"
+      step 120 "overlap_${mode}_fedavg" python tools/overlap_summary.py "$csv" --a 'wsum|weighted' \
+        --b 'conv_kernel|p2bn|sgd_mt|p2head' --out "$d/overlap_fedavg.md"
+      rm -f "$csv" ;;
     py)
       local secs=$1 tag=$2; shift 2
       step "$secs" "$tag" "$@" ;;
