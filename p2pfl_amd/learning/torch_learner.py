@@ -193,12 +193,20 @@ class TorchLearner(NodeLearner):
         if cs is None or cur == cs:
             yield
             return
-        cs.wait_stream(cur)
+        from p2pfl_amd.learning.step_graph import GATE
+
+        # the hand-off events are recorded on the caller's stream -- usually the
+        # legacy default stream, which ROCm treats as part of a graph capture in
+        # progress on another peer's thread (hipErrorCapturedEvent): never while
+        # another thread records
+        with GATE.shared():
+            cs.wait_stream(cur)
         try:
             with torch.cuda.stream(cs):
                 yield
         finally:
-            cur.wait_stream(cs)
+            with GATE.shared():
+                cur.wait_stream(cs)
 
     def set_parameters(self, params: Mapping[str, torch.Tensor]) -> None:
         finite.check(self._addr, "set_parameters input", params if isinstance(params, FlatParams) else None)
