@@ -22,6 +22,10 @@ import torch.distributed as dist  # noqa: E402
 
 
 def main(out: str, model_name: str = "mlp", rounds: int = 2) -> None:
+    import faulthandler
+
+    # a hung worker dumps every thread's stack and exits instead of stalling its test
+    faulthandler.dump_traceback_later(float(os.environ.get("P2PFL_WORKER_WATCHDOG", "240")), exit=True)
     from p2pfl_amd.communication.xgmi import XgmiJob
     from p2pfl_amd.data import MnistFederatedDM
     from p2pfl_amd.learning.fused_cnn import auto_learner
