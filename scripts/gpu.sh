@@ -28,8 +28,13 @@ export TMPDIR=/tmp PYTHONPATH="$PWD${PYTHONPATH:+:$PYTHONPATH}"
 step() {  # step <secs> <tag> <cmd...>
   local secs=$1 tag=$2; shift 2
   echo "=== [$tag] $* (limit ${secs}s, env: P2PFL_LOCKCHECK=${P2PFL_LOCKCHECK:-default(1 under pytest)})"
+  # heartbeat on stdout while the step runs (a fresh box's first torch import and the
+  # long tests print nothing for minutes; gpurun takes 3 silent minutes for a hang)
+  ( while sleep 50; do echo "[gpu.sh] $tag still running $(date +%T): $(tail -c 120 "gpurun_out/$tag.log" | tr '\n' ' ')"; done ) &
+  local hb=$!
   timeout -k 10 "$secs" "$@" > "gpurun_out/$tag.log" 2>&1
   local rc=$?
+  kill "$hb" 2>/dev/null; wait "$hb" 2>/dev/null
   echo "=== [$tag] exit $rc"
   tail -n 25 "gpurun_out/$tag.log" | cut -c1-400
   if [ $rc -ne 0 ]; then echo "=== stopping after [$tag] (exit $rc)"; exit $rc; fi
@@ -39,7 +44,7 @@ run_mode() {
   local mode=$1; shift
   case $mode in
     suite)
-      step 900 pytest_gpu python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread -rs
+      step 900 pytest_gpu python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread -rs
       step 300 smoke python -c "import __graft_entry__ as g; g.smoke()" ;;
     tests)
       step 600 pytest_sel python -u -m pytest -x -v --timeout 200 --timeout-method thread "$@" ;;
