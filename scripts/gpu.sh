@@ -64,7 +64,8 @@ run_mode() {
     prof)
       local tag=$1; shift
       rm -rf "gpurun_out/prof_$tag"
-      step 400 "prof_$tag" rocprofv3 --kernel-trace --stats -d "gpurun_out/prof_$tag" -o run -- "$@" ;;
+      step 400 "prof_$tag" rocprofv3 --kernel-trace --stats --output-format csv -d "gpurun_out/prof_$tag" -o run -- "$@"
+      step 120 "prof_${tag}_summary" python tools/prof_summary.py "gpurun_out/prof_$tag" --window-ms "${PROF_WINDOW_MS:-150}" --top 40 ;;
     overlap)
       local mode=${1:-on} rounds=${2:-5} d=gpurun_out/prof_overlap_${1:-on}
       rm -rf "$d"
