@@ -163,22 +163,31 @@ struct ConvWgradB {
   }
 };
 
-template <int NBUF, class LA, class LB>
+template <int NBUF, class LA, class LB, bool BN>
 __global__ __launch_bounds__(NT, NBUF == 1 ? 3 : (NBUF == 2 ? 2 : 1)) void conv_kernel(GemmParams p, LA la, LB lb, int tiles_m, int tiles_n) {
   __shared__ __attribute__((aligned(16))) char smem[smem_bytes<Tile128, NBUF>()];
-  gemm_body<Tile128, NBUF>(p, la, lb, tiles_m, tiles_n, smem);
+  gemm_body<Tile128, NBUF, LA, LB, BN>(p, la, lb, tiles_m, tiles_n, smem);
 }
 
-template <class LA, class LB>
-static void launch(const GemmParams& p, const LA& la, const LB& lb, hipStream_t s) {
+template <class LA, class LB, bool BN>
+static void launch_t(const GemmParams& p, const LA& la, const LB& lb, hipStream_t s) {
   int tm, tn;
   const int grid = gemm_grid<Tile128>(p, tm, tn);
   if (p.variant & 4096)  // 4-stage ring, one workgroup per CU: short-K / small-grid shapes
-    hipLaunchKernelGGL((conv_kernel<4, LA, LB>), dim3(grid), dim3(NT), 0, s, p, la, lb, tm, tn);
+    hipLaunchKernelGGL((conv_kernel<4, LA, LB, BN>), dim3(grid), dim3(NT), 0, s, p, la, lb, tm, tn);
   else if (p.variant & 8)
-    hipLaunchKernelGGL((conv_kernel<1, LA, LB>), dim3(grid), dim3(NT), 0, s, p, la, lb, tm, tn);
+    hipLaunchKernelGGL((conv_kernel<1, LA, LB, BN>), dim3(grid), dim3(NT), 0, s, p, la, lb, tm, tn);
   else
-    hipLaunchKernelGGL((conv_kernel<2, LA, LB>), dim3(grid), dim3(NT), 0, s, p, la, lb, tm, tn);
+    hipLaunchKernelGGL((conv_kernel<2, LA, LB, BN>), dim3(grid), dim3(NT), 0, s, p, la, lb, tm, tn);
+}
+
+// the BatchNorm-statistics instantiation only where a launch asks for it
+template <class LA, class LB>
+static void launch(const GemmParams& p, const LA& la, const LB& lb, hipStream_t s) {
+  if (p.bn.part)
+    launch_t<LA, LB, true>(p, la, lb, s);
+  else
+    launch_t<LA, LB, false>(p, la, lb, s);
 }
 
 static GemmParams base_params(int M, int N, int K, void* c, int64_t ldc, int c_bf16, const p2::SplitK& k,

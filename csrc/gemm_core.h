@@ -395,7 +395,9 @@ P2_DEVICE void bn_epilogue_reduce(const GemmParams& p, Moments mo, int tm, int t
 }
 
 // The whole kernel body.  `p` carries M/N/K, split-K and the epilogue.
-template <class CFG, int NBUF, class LA, class LB>
+// BN: compile the BatchNorm statistics epilogue in (GemmParams::bn; the conv
+// kernels that produce a BN input instantiate it, the Linear GEMMs do not)
+template <class CFG, int NBUF, class LA, class LB, bool BN = false>
 P2_DEVICE void gemm_body(const GemmParams& p, const LA& la, const LB& lb, int tiles_m, int tiles_n, char* smem) {
   constexpr int FM = CFG::FM, FN = CFG::FN, HA = CFG::HA, HB = CFG::HB, G = CFG::GROUPS;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -646,6 +648,104 @@ P2_DEVICE void gemm_body(const GemmParams& p, const LA& la, const LB& lb, int ti
         for (int e = 0; e < 4; ++e) acc[q / (4 * FN)][(q / 4) % FN][4 * (q % 4) + e] += v0[q][e];
     }
   }
+  // BatchNorm statistics (p.bn) of this tile, from the accumulators: each lane
+  // holds 4 consecutive columns x FM rows per (j, g); the bf16-rounded values (what
+  // is stored) are summed over the lane's rows, then over the 32 lanes of its half
+  // wave (xor shuffles), then over the WAVES_M waves sharing the columns (LDS, fixed
+  // order).  Forward: sums shifted by the tile's first row (one value per column,
+  // broadcast) -> (count, mean, M2); backward: dz' = dz (bn output > 0) and
+  // dz' (x - mean) from the BN's input / output tensors, read in the accumulator
+  // layout (8-byte vectors).
+  if (BN && p.bn.part != nullptr) {
+    const BnEpi& e = p.bn;
+    const bool bwd = e.bx != nullptr;
+    const int h = lane >> 5;
+    const int mrow0 = m0 + wm * 32 * FM;  // first row of this wave
+    __syncthreads();  // LDS free (main loop done)
+    float* red = reinterpret_cast<float*>(smem);  // [WAVES_M][BN] x (shift, s1, s2)
+    // one (j, g) group of 4 columns at a time: few live registers (the single-buffer
+    // conv kernels run at 168 VGPRs)
+#pragma unroll
+    for (int j = 0; j < FN; ++j)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const int n = n0 + wn * 32 * FN + j * 32 + 8 * g + 4 * h;
+        const bool ncol = n < p.N;
+        float mu[4] = {0.f, 0.f, 0.f, 0.f}, sh[4], s1[4] = {0.f, 0.f, 0.f, 0.f}, s2[4] = {0.f, 0.f, 0.f, 0.f};
+        if (bwd && ncol) {
+          const f32x4 mv = *reinterpret_cast<const f32x4*>(e.bmean + n);
+          mu[0] = mv[0], mu[1] = mv[1], mu[2] = mv[2], mu[3] = mv[3];
+        }
+#pragma unroll
+        for (int q = 0; q < 4; ++q)  // forward shift: the column's value in the wave's first row
+          sh[q] = bwd ? 0.f : __shfl(bf16_to_f32(f32_to_bf16(acc[0][j][4 * g + q])), lane & 32, 64);
+#pragma unroll
+        for (int i = 0; i < FM; ++i) {
+          const int m = mrow0 + i * 32 + (lane & 31);
+          if (m >= p.M || !ncol) continue;
+          float xv[4] = {0.f, 0.f, 0.f, 0.f}, yv[4] = {1.f, 1.f, 1.f, 1.f};
+          if (bwd) {
+            const int64_t off = int64_t(m) * p.N + n;
+            const uint2 xr = *reinterpret_cast<const uint2*>(e.bx + off);
+            xv[0] = __uint_as_float(xr.x << 16), xv[1] = __uint_as_float(xr.x & 0xffff0000u);
+            xv[2] = __uint_as_float(xr.y << 16), xv[3] = __uint_as_float(xr.y & 0xffff0000u);
+            if (e.by) {
+              const uint2 yr = *reinterpret_cast<const uint2*>(e.by + off);
+              yv[0] = __uint_as_float(yr.x << 16), yv[1] = __uint_as_float(yr.x & 0xffff0000u);
+              yv[2] = __uint_as_float(yr.y << 16), yv[3] = __uint_as_float(yr.y & 0xffff0000u);
+            }
+          }
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            const float v = bf16_to_f32(f32_to_bf16(acc[i][j][4 * g + q]));
+            if (bwd) {
+              const float gz = yv[q] > 0.f ? v : 0.f;
+              s1[q] += gz;
+              s2[q] = fmaf(gz, xv[q] - mu[q], s2[q]);
+            } else {
+              const float d = v - sh[q];
+              s1[q] += d;
+              s2[q] = fmaf(d, d, s2[q]);
+            }
+          }
+        }
+        // sum over the 32 rows of the half wave (lanes sharing h)
+#pragma unroll
+        for (int off = 1; off < 32; off <<= 1)
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            s1[q] += __shfl_xor(s1[q], off, 64);
+            s2[q] += __shfl_xor(s2[q], off, 64);
+          }
+        if ((lane & 31) == 0) {
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            float* dst = red + (wm * CFG::BN + (n - n0) + q) * 3;
+            dst[0] = sh[q];
+            dst[1] = s1[q];
+            dst[2] = s2[q];
+          }
+        }
+      }
+    __syncthreads();
+    Moments mo{0.f, 0.f, 0.f};
+    if (tid < CFG::BN) {
+#pragma unroll
+      for (int w = 0; w < CFG::WAVES_M; ++w) {
+        const float* src = red + (w * CFG::BN + tid) * 3;
+        const float cnt = float(max(0, min(32 * FM, p.M - (m0 + w * 32 * FM))));
+        if (bwd) {
+          mo = bn_merge(true, mo, Moments{cnt, src[1], src[2]});
+        } else if (cnt > 0.f) {
+          const float mu = src[1] / cnt;
+          mo = moments_merge(mo, Moments{cnt, src[0] + mu, fmaxf(src[2] - src[1] * mu, 0.f)});
+        }
+      }
+    }
+    __syncthreads();
+    bn_epilogue_reduce<CFG>(p, mo, tm, tn, tiles_m, smem);
+    __syncthreads();  // the bf16 staging below reuses the LDS
+  }
   // bias, GELU (+ pre-activation, stored directly), residual: in place on acc
 #pragma unroll
   for (int i = 0; i < FM; ++i)
@@ -695,13 +795,6 @@ P2_DEVICE void gemm_body(const GemmParams& p, const LA& la, const LB& lb, int ti
   constexpr int PASSES = ONE ? 1 : CFG::WAVES_M, ROWS = CFG::BM / PASSES;
   static_assert(ROWS * LROW <= smem_bytes<CFG, NBUF>(), "epilogue image must fit the kernel's LDS");
   static_assert((ROWS * CPR) % CFG::NT == 0, "whole chunks per thread");
-  // BatchNorm statistics (p.bn): thread = column tid % BN x row phase tid / BN of
-  // each pass's LDS image (the bf16 values as stored), shifted single-pass sums
-  // per pass, merged across passes and phases in fixed order
-  constexpr int BNPH = CFG::NT / CFG::BN, PROWS = ROWS / BNPH;
-  const bool bn_on = p.bn.part != nullptr;
-  const int bn_c = tid % CFG::BN, bn_ph = tid / CFG::BN;
-  Moments bn_mo{0.f, 0.f, 0.f};
 #pragma unroll
   for (int pass = 0; pass < PASSES; ++pass) {
     __syncthreads();  // LDS free: main loop (or previous pass) done
@@ -720,34 +813,6 @@ P2_DEVICE void gemm_body(const GemmParams& p, const LA& la, const LB& lb, int ti
           }
     }
     __syncthreads();
-    if (bn_on && p.bn.bx && n0 + bn_c < p.N) {
-      // backward sums: dz' = dz * (bn output > 0), against the BN input x - mean
-      const int r0 = bn_ph * PROWS, rend = min(PROWS, p.M - (m0 + pass * ROWS + r0));
-      const int n = n0 + bn_c;
-      const float mu = p.bn.bmean[n];
-      float s1 = 0.f, s2 = 0.f;
-      for (int r = 0; r < rend; ++r) {
-        const int64_t off = int64_t(m0 + pass * ROWS + r0 + r) * p.N + n;
-        float g = bf16_to_f32(*reinterpret_cast<const uint16_t*>(smem + (r0 + r) * LROW + bn_c * 2));
-        if (p.bn.by && !(bf16_to_f32(p.bn.by[off]) > 0.f)) g = 0.f;
-        s1 += g;
-        s2 = fmaf(g, bf16_to_f32(p.bn.bx[off]) - mu, s2);
-      }
-      bn_mo = Moments{bn_mo.n + float(max(rend, 0)), bn_mo.mean + s1, bn_mo.m2 + s2};
-    } else if (bn_on && n0 + bn_c < p.N) {
-      const int r0 = bn_ph * PROWS, rend = min(PROWS, p.M - (m0 + pass * ROWS + r0));
-      if (rend > 0) {
-        const float x0 = bf16_to_f32(*reinterpret_cast<const uint16_t*>(smem + r0 * LROW + bn_c * 2));
-        float s1 = 0.f, s2 = 0.f;
-        for (int r = 0; r < rend; ++r) {
-          const float d = bf16_to_f32(*reinterpret_cast<const uint16_t*>(smem + (r0 + r) * LROW + bn_c * 2)) - x0;
-          s1 += d;
-          s2 = fmaf(d, d, s2);
-        }
-        const float cnt = float(rend), mu = s1 / cnt;
-        bn_mo = moments_merge(bn_mo, Moments{cnt, x0 + mu, fmaxf(s2 - s1 * mu, 0.f)});
-      }
-    }
 #pragma unroll
     for (int q = 0; q < ROWS * CPR / CFG::NT; ++q) {
       const int chunk = q * CFG::NT + tid, r = chunk / CPR, c = chunk % CPR;
@@ -756,23 +821,6 @@ P2_DEVICE void gemm_body(const GemmParams& p, const LA& la, const LB& lb, int ti
         *reinterpret_cast<uint4*>(reinterpret_cast<uint16_t*>(p.c) + int64_t(m) * p.ldc + n) =
             *reinterpret_cast<const uint4*>(smem + r * LROW + c * 16);
     }
-  }
-  if (bn_on) {
-    // merge the row phases in order (column c's phases sit BN threads apart)
-    __syncthreads();
-    float* red = reinterpret_cast<float*>(smem);
-    red[tid] = bn_mo.n;
-    red[CFG::NT + tid] = bn_mo.mean;
-    red[2 * CFG::NT + tid] = bn_mo.m2;
-    __syncthreads();
-    Moments mo{0.f, 0.f, 0.f};
-    if (tid < CFG::BN)
-      for (int ph = 0; ph < BNPH; ++ph) {
-        const int q = ph * CFG::BN + tid;
-        mo = bn_merge(p.bn.bx != nullptr, mo, Moments{red[q], red[CFG::NT + q], red[2 * CFG::NT + q]});
-      }
-    __syncthreads();
-    bn_epilogue_reduce<CFG>(p, mo, tm, tn, tiles_m, smem);
   }
 }
 

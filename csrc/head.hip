@@ -68,9 +68,10 @@ __global__ __launch_bounds__(kT) void head_fwd_kernel(const uint16_t* __restrict
   // fixed-order reduction: wave sums, then the 4 waves in order
 #pragma unroll
   for (int n = 0; n < kMaxN; ++n) {
-    if (n >= N) break;
-    const float v = wave_sum(part[n]);
-    if (lane == 0) red[n][wave] = v;
+    if (n < N) {  // (no early exit: keeps the loop unrolled and part[] in registers)
+      const float v = wave_sum(part[n]);
+      if (lane == 0) red[n][wave] = v;
+    }
   }
   __syncthreads();
   if (tid < N) {

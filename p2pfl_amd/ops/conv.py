@@ -243,6 +243,7 @@ class _Conv2dNHWCBN(torch.autograd.Function):
         ctx.save_for_backward(x4, w)
         ctx.cfg = (stride, pad, dil)
         ctx.mark_non_differentiable(mean, rstd, coef)
+        ctx.set_materialize_grads(False)  # no zero-filled gradients for the three statistics
         return y4.permute(0, 3, 1, 2), mean, rstd, coef
 
     @staticmethod
@@ -273,6 +274,7 @@ class _BNActConvBN(torch.autograd.Function):
         ctx.save_for_backward(y14, z4, w, g1, mean1, rstd1)
         ctx.cfg = (stride, pad, dil, bool(relu1))
         ctx.mark_non_differentiable(mean, rstd, coef)
+        ctx.set_materialize_grads(False)
         return y24.permute(0, 3, 1, 2), mean, rstd, coef
 
     @staticmethod

@@ -50,6 +50,7 @@ class _HeadXent(torch.autograd.Function):
         ctx.fshape = list(f4.shape)
         ctx.has_b = b is not None
         ctx.mark_non_differentiable(logits, acc)
+        ctx.set_materialize_grads(False)  # no zero-filled gradients for logits / accuracy
         return loss, logits, acc
 
     @staticmethod
