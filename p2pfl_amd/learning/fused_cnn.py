@@ -390,7 +390,10 @@ class FusedCNNLearner(TorchLearner):
         prev = self._fit_done
         if prev is not None:
             prev.synchronize()  # the previous round's training finished on the GPU
-        self._ensure_graph("train", self.data.train_dataloader(), True)  # first-use capture outside the lock
+        self._ensure_graph("train", self.data.train_dataloader(), True)  # first-use captures outside the lock
+        val = self.data.val_dataloader()
+        if val is not None and len(val.dataset) > 0:
+            self._ensure_graph("val", val, False)
         with self._lock:
             self.engine.reset_optimizer()  # Adam re-created per fit (reference quirk Q23)
             loader = self.data.train_dataloader()
