@@ -15,6 +15,9 @@
 #   scripts/gpu.sh prof <tag> <cmd...>      rocprofv3 --kernel-trace --stats of <cmd> -> gpurun_out/prof_<tag>
 #   scripts/gpu.sh overlap [on|off] [rounds] 8 virtual ResNet-50 peers (fault-tolerance scenario) under a
 #                                           kernel trace + cross-stream overlap summary of training / FedAvg
+#   scripts/gpu.sh pmc <tag> <cmd...>       rocprofv3 --kernel-trace --pmc passes of <cmd> (one counter group
+#                                           per pass, each under its own kill timer; groups from $PMC_PASSES,
+#                                           ";"-separated) + scripts/pmc_summary.py table -> gpurun_out/pmc_<tag>.md
 #   scripts/gpu.sh py <secs> <tag> <cmd...> any python command, own limit
 #
 # Several modes can be chained with "+", e.g.
@@ -78,6 +81,20 @@ run_mode() {
       step 120 "overlap_${mode}_fedavg" python tools/overlap_summary.py "$csv" --a 'wsum|weighted' \
         --b 'conv_kernel|p2bn|sgd_mt|p2head' --out "$d/overlap_fedavg.md"
       rm -f "$csv" ;;
+    pmc)
+      # per-pass limits of the hardware (MI355X_MICROARCH.md): <= 8 SQ, 4 TCC (FETCH_SIZE 3, WRITE_SIZE 2), 2 GRBM
+      local tag=$1; shift
+      local passes=${PMC_PASSES:-"FETCH_SIZE;WRITE_SIZE;SQ_VALU_MFMA_BUSY_CYCLES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE GRBM_GUI_ACTIVE"}
+      local dirs=() n=0 group
+      IFS=';' read -ra groups <<< "$passes"
+      for group in "${groups[@]}"; do
+        n=$((n + 1)); rm -rf "gpurun_out/pmc_${tag}_$n"
+        # shellcheck disable=SC2086
+        step 120 "pmc_${tag}_$n" timeout -s KILL 100 rocprofv3 --kernel-trace --pmc $group --output-format csv \
+          -d "gpurun_out/pmc_${tag}_$n" -o run -- "$@"
+        dirs+=("gpurun_out/pmc_${tag}_$n")
+      done
+      step 120 "pmc_${tag}_summary" sh -c "python scripts/pmc_summary.py ${dirs[*]} --md > gpurun_out/pmc_$tag.md" ;;
     py)
       local secs=$1 tag=$2; shift 2
       step "$secs" "$tag" "$@" ;;

@@ -9,6 +9,8 @@ summed over dimensions; durations come from the kernel trace of the same pass
   FETCH_SIZE tallies a wide coalesced read at half its bytes
   (MI355X_MICROARCH.md, rocprofv3 section), so it is doubled; Infinity-Cache
   hits are counted too, so this is memory-side traffic, not strictly HBM.
+* ``parked`` / ``issue-stall`` = SQ_WAIT_ANY / SQ_WAIT_INST_ANY over
+  SQ_WAVE_CYCLES (waves at s_waitcnt / barrier, and waves unable to issue).
 * ``MFMA busy``  = SQ_VALU_MFMA_BUSY_CYCLES / (GRBM_GUI_ACTIVE / 8 * CUs) --
   matrix-core busy cycles over the kernel's cycles on every CU
   (GRBM_GUI_ACTIVE is summed over the 8 XCDs).
@@ -70,7 +72,7 @@ def main() -> None:
         for k, v in pd.items():
             durs[k] += v
     cols = sorted({c for cs in counters.values() for c in cs})
-    head = ["kernel", "dur us"] + cols + ["HBM GB/s", "MFMA busy"]
+    head = ["kernel", "dur us"] + cols + ["HBM GB/s", "parked", "issue-stall", "MFMA busy"]
     rows = []
     for k, cs in counters.items():
         du = statistics.median(durs[k]) / 1e3 if durs.get(k) else float("nan")
@@ -79,7 +81,11 @@ def main() -> None:
         mb = cs.get("SQ_VALU_MFMA_BUSY_CYCLES")
         gui = cs.get("GRBM_GUI_ACTIVE")
         mf = mb / (gui / 8.0 * CUS) if mb is not None and gui else float("nan")
-        rows.append([k, f"{du:.2f}"] + [f"{cs.get(c, float('nan')):.4g}" for c in cols] + [f"{gbs:.0f}", f"{mf:.1%}"])
+        wc = cs.get("SQ_WAVE_CYCLES")
+        park = cs["SQ_WAIT_ANY"] / wc if wc and "SQ_WAIT_ANY" in cs else float("nan")
+        stall = cs["SQ_WAIT_INST_ANY"] / wc if wc and "SQ_WAIT_INST_ANY" in cs else float("nan")
+        rows.append([k, f"{du:.2f}"] + [f"{cs.get(c, float('nan')):.4g}" for c in cols]
+                    + [f"{gbs:.0f}", f"{park:.1%}", f"{stall:.1%}", f"{mf:.1%}"])
     rows.sort(key=lambda r: -float(r[1]) if r[1] != "nan" else 0)
     if md:
         print("| " + " | ".join(head) + " |")
