@@ -85,7 +85,7 @@ void route_fc2(const uint16_t* dH, const uint16_t* w1t, const uint8_t* am2, int 
 void route_fc2_rm(const uint16_t* dH, const uint16_t* w1, const uint8_t* am2, int mrows, int B, uint16_t* dc2m,
                   float* gb, const float* dlogits, const uint16_t* H, float* params, float* m, float* v,
                   float* gdump, Offsets off, const int* adam_t, int t_off, AdamCfg cfg, bool with_fc2,
-                  hipStream_t s);
+                  float* ws, int* ctr, hipStream_t s);  // ws/ctr non-null: split-K over 2 slices
 
 // One launch: conv2 input gradient + pool1/ReLU backward + conv1 weight
 // gradient (-> wslab1 [B][7][832]) and conv2 weight gradient

@@ -135,25 +135,37 @@ void k_route_fc2(torch::Tensor dH, torch::Tensor w1, torch::Tensor am2, int64_t 
                  torch::Tensor dc2m, torch::Tensor gb, torch::Tensor dlogits, torch::Tensor H, torch::Tensor params,
                  torch::Tensor m, torch::Tensor v, c10::optional<torch::Tensor> gdump, std::vector<int64_t> off,
                  torch::Tensor adam_t, int64_t t_off, double lr, double b1, double b2, double eps, double wd,
-                 bool with_fc2, bool row_major) {
+                 bool with_fc2, bool row_major, c10::optional<torch::Tensor> ws, c10::optional<torch::Tensor> ctr) {
   const c10::DeviceGuard g(dH.device());
   check_batch(int(B), int(mrows));
   TORCH_CHECK(mrows <= 64, "route_fc2: mrows must be 32 or 64");
+  TORCH_CHECK(ws.has_value() == ctr.has_value(), "route_fc2: split-K needs both ws and ctr");
+  TORCH_CHECK(!ws.has_value() || row_major, "route_fc2: split-K only on the row-major W1 kernel");
   Offsets o = offsets(off);
   const int64_t n = params_end(o);
-  // row_major: w1 is the forward shadow W1 [2048][3136]; else the W1^T shadow [3136][2048]
-  (row_major ? p2cnn::route_fc2_rm : p2cnn::route_fc2)(
-                   reinterpret_cast<uint16_t*>(ptr<at::BFloat16>(dH, torch::kBFloat16, mrows * 2048, "dH")),
-                   reinterpret_cast<uint16_t*>(ptr<at::BFloat16>(w1, torch::kBFloat16, 2048 * 3136, "w1")),
-                   ptr<uint8_t>(am2, torch::kUInt8, B * 3136, "am2"), int(mrows), int(B),
-                   reinterpret_cast<uint16_t*>(ptr<at::BFloat16>(dc2m, torch::kBFloat16, B * 64 * 224, "dc2m")),
-                   ptr<float>(gb, torch::kFloat32, B * 3136, "gb"),
-                   ptr<float>(dlogits, torch::kFloat32, B * 10, "dlogits"),
-                   reinterpret_cast<uint16_t*>(ptr<at::BFloat16>(H, torch::kBFloat16, B * 2048, "H")),
-                   ptr<float>(params, torch::kFloat32, n, "params"), ptr<float>(m, torch::kFloat32, n, "m"),
-                   ptr<float>(v, torch::kFloat32, n, "v"), optr<float>(gdump, torch::kFloat32, n, "gdump"), o,
-                   ptr<int>(adam_t, torch::kInt32, 1, "adam_t", 4), int(t_off), cfg(lr, b1, b2, eps, wd), with_fc2,
-                   stream());
+  const auto dHp = reinterpret_cast<uint16_t*>(ptr<at::BFloat16>(dH, torch::kBFloat16, mrows * 2048, "dH"));
+  const auto w1p = reinterpret_cast<uint16_t*>(ptr<at::BFloat16>(w1, torch::kBFloat16, 2048 * 3136, "w1"));
+  const auto am2p = ptr<uint8_t>(am2, torch::kUInt8, B * 3136, "am2");
+  const auto dc2p = reinterpret_cast<uint16_t*>(ptr<at::BFloat16>(dc2m, torch::kBFloat16, B * 64 * 224, "dc2m"));
+  const auto gbp = ptr<float>(gb, torch::kFloat32, B * 3136, "gb");
+  const auto dlp = ptr<float>(dlogits, torch::kFloat32, B * 10, "dlogits");
+  const auto Hp = reinterpret_cast<uint16_t*>(ptr<at::BFloat16>(H, torch::kBFloat16, B * 2048, "H"));
+  float* pp = ptr<float>(params, torch::kFloat32, n, "params");
+  float* mp = ptr<float>(m, torch::kFloat32, n, "m");
+  float* vp = ptr<float>(v, torch::kFloat32, n, "v");
+  float* gd = optr<float>(gdump, torch::kFloat32, n, "gdump");
+  const int* tp = ptr<int>(adam_t, torch::kInt32, 1, "adam_t", 4);
+  if (row_major) {
+    // split-K partials: [98 tiles][2 slices][mrows * 32] fp32; one ticket per tile
+    float* wsp = optr<float>(ws, torch::kFloat32, 98 * 2 * mrows * 32, "ws");
+    int* cp = optr<int>(ctr, torch::kInt32, 98, "ctr", 4);
+    p2cnn::route_fc2_rm(dHp, w1p, am2p, int(mrows), int(B), dc2p, gbp, dlp, Hp, pp, mp, vp, gd, o, tp, int(t_off),
+                        cfg(lr, b1, b2, eps, wd), with_fc2, wsp, cp, stream());
+  } else {
+    // w1 is the W1^T shadow [3136][2048]
+    p2cnn::route_fc2(dHp, w1p, am2p, int(mrows), int(B), dc2p, gbp, dlp, Hp, pp, mp, vp, gd, o, tp, int(t_off),
+                     cfg(lr, b1, b2, eps, wd), with_fc2, stream());
+  }
 }
 
 void k_conv2_bwd(torch::Tensor dc2m, torch::Tensor p1s, torch::Tensor am1, torch::Tensor w2q, torch::Tensor x,
@@ -248,7 +260,8 @@ void register_cnn(pybind11::module& m) {
   c.def("route_fc2", &k_route_fc2, pybind11::arg("dH"), pybind11::arg("w1"), pybind11::arg("am2"), pybind11::arg("mrows"), pybind11::arg("B"),
         pybind11::arg("dc2m"), pybind11::arg("gb"), pybind11::arg("dlogits"), pybind11::arg("H"), pybind11::arg("params"), pybind11::arg("m"), pybind11::arg("v"),
         pybind11::arg("gdump"), pybind11::arg("off"), pybind11::arg("adam_t"), pybind11::arg("t_off"), pybind11::arg("lr"), pybind11::arg("b1"),
-        pybind11::arg("b2"), pybind11::arg("eps"), pybind11::arg("wd"), pybind11::arg("with_fc2") = true, pybind11::arg("row_major") = false);
+        pybind11::arg("b2"), pybind11::arg("eps"), pybind11::arg("wd"), pybind11::arg("with_fc2") = true, pybind11::arg("row_major") = false,
+        pybind11::arg("ws") = pybind11::none(), pybind11::arg("ctr") = pybind11::none());
   c.def("fc1_wgrad_adam", &k_fc1_wgrad_adam);
   c.def("conv2_bwd", &k_conv2_bwd);
   c.def("conv_adam", &k_conv_adam);

@@ -217,7 +217,28 @@ P2_DEVICE int xcd_local(int orig, int nwg) {
   return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + orig / 8;
 }
 
-template <int MT>
+// Write-through (sc1) store / load of a split-K partial: the tile's last
+// arriving K-slice reads the others' partials from another CU (possibly another
+// XCD), so they bypass the non-coherent L1 / per-XCD L2 (the hand-off of
+// gemm_core.h: drain vmcnt, barrier, relaxed agent-scope ticket).
+P2_DEVICE void st_sc1f(float* p, float v) {
+  const auto rs = __builtin_amdgcn_make_buffer_rsrc(p, 0, 4, 0x00020000);
+  __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), rs, 0, 0, 16);
+}
+P2_DEVICE float ld_sc1f(const float* p) {
+  const auto rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(p), 0, 4, 0x00020000);
+  return __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rs, 0, 0, 16));
+}
+
+// KS > 1: split-K over KS workgroups per 32-feature tile (98 x KS blocks).  The
+// kernel is bound by what one CU can pull (each tile block streams 128 KB of W1
+// and re-reads the 128 KB dH: ~11 B/cycle/CU, MI355X_MICROARCH.md), so with 98
+// blocks 158 CUs idle; KS = 2 halves the bytes per block.  Each slice reduces its
+// 8 waves in LDS, stores its fp32 partial (sc1), and the last slice to take the
+// tile's ticket sums the KS partials in slice order (deterministic, whichever
+// slice arrives last) and runs the routing epilogue.  ws: [98][KS][MT*1024] fp32,
+// ctr: [98] int, zero between launches (the last arriver resets its entry).
+template <int MT, int KS>
 __global__ __launch_bounds__(512) void route_rm_kernel(const uint16_t* __restrict__ dH,
                                                        const uint16_t* __restrict__ w1,
                                                        const uint8_t* __restrict__ am2, int B,
@@ -226,18 +247,22 @@ __global__ __launch_bounds__(512) void route_rm_kernel(const uint16_t* __restric
                                                        const uint16_t* __restrict__ H, float* __restrict__ p,
                                                        float* __restrict__ m, float* __restrict__ v,
                                                        float* __restrict__ gdump, Offsets off,
-                                                       const int* __restrict__ adam_t, int t_off, AdamCfg cfg) {
-  if (int(blockIdx.x) >= kRouteBlocks) {
-    fc2_role<512>(blockIdx.x - kRouteBlocks, dlogits, H, B, p, m, v, gdump, off, adam_t, t_off, cfg);
+                                                       const int* __restrict__ adam_t, int t_off, AdamCfg cfg,
+                                                       float* __restrict__ ws, int* __restrict__ ctr) {
+  constexpr int NB = kRouteBlocks * KS;
+  if (int(blockIdx.x) >= NB) {
+    fc2_role<512>(blockIdx.x - NB, dlogits, H, B, p, m, v, gdump, off, adam_t, t_off, cfg);
     return;
   }
-  const int bid = xcd_local(blockIdx.x, kRouteBlocks);
+  const int bid = xcd_local(blockIdx.x, NB);
+  const int tile = bid / KS, split = bid % KS;
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  static_assert(8 * MT * 1024 * 4 <= kRouteRmLds, "reduction buffer must fit the tile");
+  static_assert(8 * MT * 1024 * 4 <= kRouteRmLds / KS, "reduction buffer must fit the tile");
   float* red = reinterpret_cast<float*>(smem);
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, r = lane & 31, h = lane >> 5;
-  const int n0 = bid * 32;
-  constexpr int K = kHid, NG = K / 64, NGW = NG / 8;
+  const int n0 = tile * 32;
+  constexpr int K = kHid, NG = K / 64, NGW = NG / 8 / KS;
+  const int gbase = split * (NG / KS);  // first 64-wide k-group of this slice
   uint8_t acode[2 * MT];
 #pragma unroll
   for (int q = 0; q < 2 * MT; ++q) {
@@ -245,23 +270,23 @@ __global__ __launch_bounds__(512) void route_rm_kernel(const uint16_t* __restric
     const int b = (e >> 10) * 32 + acc_row_b((e >> 6) & 15, (e & 63) >> 5);
     acode[q] = b < B ? am2[size_t(b) * kFeat + n0 + (e & 31)] : uint8_t(4);
   }
-  // W1 rows of this wave's k-groups -> LDS [k][32 features] (64-B rows): one
-  // wave instruction = 16 rows x 4 lanes x 16 B
+  // W1 rows of this wave's k-groups -> LDS [k - kbase][32 features] (64-B rows):
+  // one wave instruction = 16 rows x 4 lanes x 16 B
 #pragma unroll
   for (int gi = 0; gi < NGW; ++gi) {
-    const int k0 = (wave + 8 * gi) * 64;
+    const int kl = (wave + 8 * gi) * 64, k0 = gbase * 64 + kl;
 #pragma unroll
     for (int c = 0; c < 4; ++c) {
       const int row = k0 + 16 * c + (lane >> 2);
       __builtin_amdgcn_global_load_lds(
           (const __attribute__((address_space(1))) void*)(w1 + size_t(row) * kFeat + n0 + (lane & 3) * 8),
-          (__attribute__((address_space(3))) void*)(smem + (k0 + 16 * c) * 64), 16, 0, 0);
+          (__attribute__((address_space(3))) void*)(smem + (kl + 16 * c) * 64), 16, 0, 0);
     }
   }
   uint4 aq[NGW][MT][4];
 #pragma unroll
   for (int gi = 0; gi < NGW; ++gi) {
-    const int k0 = (wave + 8 * gi) * 64;
+    const int k0 = (gbase + wave + 8 * gi) * 64;
 #pragma unroll
     for (int mt = 0; mt < MT; ++mt)
 #pragma unroll
@@ -276,13 +301,13 @@ __global__ __launch_bounds__(512) void route_rm_kernel(const uint16_t* __restric
   const int g = lane >> 4, qq = (lane >> 2) & 3, col = 16 * (g & 1) + 4 * (lane & 3);
 #pragma unroll
   for (int gi = 0; gi < NGW; ++gi) {
-    const int k0 = (wave + 8 * gi) * 64;
+    const int kl = (wave + 8 * gi) * 64;
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
       uint4 bq;
 #pragma unroll
       for (int t = 0; t < 2; ++t) {
-        const int row = k0 + 32 * (g >> 1) + 8 * q + 4 * t + qq;
+        const int row = kl + 32 * (g >> 1) + 8 * q + 4 * t + qq;
         const s16x4 w = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
             (__attribute__((address_space(3))) s16x4*)(smem + row * 64 + col * 2));
         const uint2 u = __builtin_bit_cast(uint2, w);
@@ -304,12 +329,41 @@ __global__ __launch_bounds__(512) void route_rm_kernel(const uint16_t* __restric
 #pragma unroll
     for (int i = 0; i < 16; ++i) red[((wave * MT + mt) * 16 + i) * 64 + lane] = acc[mt][i];
   __syncthreads();
+  float part[2 * MT];
 #pragma unroll
   for (int q = 0; q < 2 * MT; ++q) {
     const int e = tid + 512 * q;
     float gsum = 0.f;
 #pragma unroll
     for (int w = 0; w < 8; ++w) gsum += red[w * MT * 1024 + e];
+    part[q] = gsum;
+  }
+  if (KS > 1) {
+    float* slab = ws + size_t(tile) * KS * (MT * 1024);
+#pragma unroll
+    for (int q = 0; q < 2 * MT; ++q) st_sc1f(slab + split * (MT * 1024) + tid + 512 * q, part[q]);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();  // every wave's partial written; the reduction buffer is dead
+    int* flag = reinterpret_cast<int*>(smem);
+    if (tid == 0) {
+      const int old = __hip_atomic_fetch_add(ctr + tile, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      flag[0] = old == KS - 1;
+      if (old == KS - 1) __hip_atomic_store(ctr + tile, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    __syncthreads();
+    if (!flag[0]) return;
+#pragma unroll
+    for (int q = 0; q < 2 * MT; ++q) {
+      float t = 0.f;
+#pragma unroll
+      for (int s2 = 0; s2 < KS; ++s2) t += s2 == split ? part[q] : ld_sc1f(slab + s2 * (MT * 1024) + tid + 512 * q);
+      part[q] = t;
+    }
+  }
+#pragma unroll
+  for (int q = 0; q < 2 * MT; ++q) {
+    const int e = tid + 512 * q;
+    const float gsum = part[q];
     const int mt = e >> 10, i = (e >> 6) & 15, ln = e & 63;
     const int b = mt * 32 + acc_row_b(i, ln >> 5), feat = n0 + (ln & 31);
     if (b >= B) continue;
@@ -328,14 +382,19 @@ __global__ __launch_bounds__(512) void route_rm_kernel(const uint16_t* __restric
 void route_fc2_rm(const uint16_t* dH, const uint16_t* w1, const uint8_t* am2, int mrows, int B, uint16_t* dc2m,
                   float* gb, const float* dlogits, const uint16_t* H, float* params, float* m, float* v,
                   float* gdump, Offsets off, const int* adam_t, int t_off, AdamCfg cfg, bool with_fc2,
-                  hipStream_t s) {
-  const dim3 grid(kRouteBlocks + (with_fc2 ? kFc2Blocks : 0));
-  if (mrows == 32)
-    hipLaunchKernelGGL(route_rm_kernel<1>, grid, dim3(512), kRouteRmLds, s, dH, w1, am2, B, dc2m, gb, dlogits, H,
-                       params, m, v, gdump, off, adam_t, t_off, cfg);
-  else
-    hipLaunchKernelGGL(route_rm_kernel<2>, grid, dim3(512), kRouteRmLds, s, dH, w1, am2, B, dc2m, gb, dlogits, H,
-                       params, m, v, gdump, off, adam_t, t_off, cfg);
+                  float* ws, int* ctr, hipStream_t s) {
+  const int ks = (ws && ctr) ? 2 : 1;
+  const dim3 grid(kRouteBlocks * ks + (with_fc2 ? kFc2Blocks : 0));
+  const int lds = kRouteRmLds / ks;
+#define P2_ROUTE(MT, KS)                                                                                            \
+  hipLaunchKernelGGL((route_rm_kernel<MT, KS>), grid, dim3(512), lds, s, dH, w1, am2, B, dc2m, gb, dlogits, H, params, \
+                     m, v, gdump, off, adam_t, t_off, cfg, ws, ctr)
+  if (mrows == 32) {
+    if (ks == 2) P2_ROUTE(1, 2); else P2_ROUTE(1, 1);
+  } else {
+    if (ks == 2) P2_ROUTE(2, 2); else P2_ROUTE(2, 1);
+  }
+#undef P2_ROUTE
 }
 
 void route_fc2(const uint16_t* dH, const uint16_t* w1t, const uint8_t* am2, int mrows, int B, uint16_t* dc2m,
@@ -950,10 +1009,14 @@ void init_attributes() {
   init_fwd_attributes();
   P2_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(conv2_bwd_kernel),
                                hipFuncAttributeMaxDynamicSharedMemorySize, kDgLds));
-  P2_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(route_rm_kernel<1>),
+  P2_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(route_rm_kernel<1, 1>),
                                hipFuncAttributeMaxDynamicSharedMemorySize, kRouteRmLds));
-  P2_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(route_rm_kernel<2>),
+  P2_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(route_rm_kernel<2, 1>),
                                hipFuncAttributeMaxDynamicSharedMemorySize, kRouteRmLds));
+  P2_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(route_rm_kernel<1, 2>),
+                               hipFuncAttributeMaxDynamicSharedMemorySize, kRouteRmLds / 2));
+  P2_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(route_rm_kernel<2, 2>),
+                               hipFuncAttributeMaxDynamicSharedMemorySize, kRouteRmLds / 2));
 }
 
 }  // namespace p2cnn

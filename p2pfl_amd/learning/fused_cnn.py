@@ -45,6 +45,10 @@ _MERGED_ADAM = os.environ.get("P2PFL_CNN_MERGED_ADAM", "1") != "0"
 # W1^T shadow, 12.8 MB less written per step by the FC1 Adam stream); "0"
 # selects the W1^T-shadow kernel.
 _ROUTE_RM = os.environ.get("P2PFL_CNN_ROUTE_RM", "1") != "0"
+# dA1 routing split over 2 K-slices per feature tile (196 workgroups instead of
+# 98, the last slice to arrive reduces; csrc/cnn_bwd.hip route_rm_kernel);
+# "0" keeps one workgroup per tile.
+_ROUTE_SPLIT = os.environ.get("P2PFL_CNN_ROUTE_SPLIT", "1") != "0"
 _NAMES = ("conv1.weight", "conv1.bias", "conv2.weight", "conv2.bias", "l1.weight", "l1.bias", "l2.weight", "l2.bias")
 FEAT, HID = 3136, 2048
 
@@ -102,6 +106,10 @@ class FusedCNNEngine:
         self.dc2m, self.gb = z(M * 64 * 224, dt=bf), z(M * FEAT)
         self.wslab1, self.wslab2 = z(M * 7 * 832), z(self.C.wgrad_groups(M) * 51200)
         self.stats = z(2)
+        # split-K partials + tickets of the routing kernel (tickets return to zero after every launch)
+        split = self.route_rm and _ROUTE_SPLIT
+        self.route_ws = z(98 * 2 * M * 32) if split else None
+        self.route_ctr = z(98, dt=torch.int32) if split else None
         self.gdump: Optional[torch.Tensor] = None
         self.pack_shadows()
 
@@ -167,14 +175,16 @@ class FusedCNNEngine:
             # FC2 and conv-parameter Adam (latency-bound) and the FC1 wgrad +
             # Adam stream (HBM-bound)
             C.route_fc2(self.dH, self.w1_route, self.am2, M, B, self.dc2m, self.gb, self.dlogits, self.H,
-                        self.params, self.m, self.v, self.gdump, self.off, self.adam_t, t_off, *a, False, self.route_rm)
+                        self.params, self.m, self.v, self.gdump, self.off, self.adam_t, t_off, *a, False, self.route_rm,
+                        self.route_ws, self.route_ctr)
             C.conv2_bwd(self.dc2m, self.p1s, self.am1, self.w2q, x, idx, self.wslab1, self.wslab2, B)
             C.fc1_conv_adam(self.dH, self.a1, M, self.wslab1, self.wslab2, self.gb, B, self.params, self.m, self.v,
                             self.gdump, self.w1bf, self.w1tbf, self.w2r, self.w2q, self.off, self.adam_t, t_off, *a,
                             self.dlogits, self.H)
             return
         C.route_fc2(self.dH, self.w1_route, self.am2, M, B, self.dc2m, self.gb, self.dlogits, self.H,
-                    self.params, self.m, self.v, self.gdump, self.off, self.adam_t, t_off, *a, True, self.route_rm)
+                    self.params, self.m, self.v, self.gdump, self.off, self.adam_t, t_off, *a, True, self.route_rm,
+                    self.route_ws, self.route_ctr)
         C.fc1_wgrad_adam(self.dH, self.a1, M, self.params, self.m, self.v, self.gdump, self.w1bf, self.w1tbf, self.off, self.adam_t, t_off, *a)
         C.conv2_bwd(self.dc2m, self.p1s, self.am1, self.w2q, x, idx, self.wslab1, self.wslab2, B)
         C.conv_adam(self.wslab1, self.wslab2, self.gb, B, self.params, self.m, self.v, self.gdump, self.w2r, self.w2q, self.off, self.adam_t, t_off, *a)

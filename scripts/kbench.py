@@ -46,13 +46,16 @@ def main() -> None:
     # launches do not drift the weights into NaN territory
     P, Mm, V = eng.params.clone(), eng.m.clone(), eng.v.clone()
     w1t = eng.w1bf.view(2048, 3136).t().contiguous()  # for the W1^T-shadow variants
+    rws = torch.zeros(98 * 2 * M * 32, device=dev)  # split-K routing partials / tickets
+    rctr = torch.zeros(98, dtype=torch.int32, device=dev)
     ks = {
         "conv1_fwd": lambda: C.conv1_fwd(x, None, eng.params, eng.off, eng.p1, eng.am1, eng.p1s, B),
         "conv2_fwd": lambda: C.conv2_fwd(eng.p1, eng.w2r, eng.params, eng.off, eng.a1, eng.am2, B, M),
         "gemm_fc1": lambda: C.gemm_skinny(eng.a1, eng.w1bf, eng.slabs1, M, 2048, 3136, eng.S1),
         "head": lambda: C.head(eng.slabs1, eng.S1, M, eng.params, eng.off, y, None, B, True, eng.H, eng.dH, eng.dlogits, stats),
         "route_fc2": lambda: C.route_fc2(eng.dH, eng.w1_route, eng.am2, M, B, eng.dc2m, eng.gb, eng.dlogits, eng.H, P, Mm, V, None, eng.off, eng.adam_t, 1, *a, True, eng.route_rm),
-        "route_dA1_only": lambda: C.route_fc2(eng.dH, eng.w1_route, eng.am2, M, B, eng.dc2m, eng.gb, eng.dlogits, eng.H, P, Mm, V, None, eng.off, eng.adam_t, 1, *a, False, eng.route_rm),
+        "route_dA1_only": lambda: C.route_fc2(eng.dH, eng.w1bf, eng.am2, M, B, eng.dc2m, eng.gb, eng.dlogits, eng.H, P, Mm, V, None, eng.off, eng.adam_t, 1, *a, False, True),
+        "route_dA1_split2": lambda: C.route_fc2(eng.dH, eng.w1bf, eng.am2, M, B, eng.dc2m, eng.gb, eng.dlogits, eng.H, P, Mm, V, None, eng.off, eng.adam_t, 1, *a, False, True, rws, rctr),
         "route_dA1_w1t": lambda: C.route_fc2(eng.dH, w1t, eng.am2, M, B, eng.dc2m, eng.gb, eng.dlogits, eng.H, P, Mm, V, None, eng.off, eng.adam_t, 1, *a, False, False),
         "fc1_conv_adam_w1t": lambda: C.fc1_conv_adam(eng.dH, eng.a1, M, eng.wslab1, eng.wslab2, eng.gb, B, P, Mm, V, None, eng.w1bf, w1t, eng.w2r, eng.w2q, eng.off, eng.adam_t, 1, *a, eng.dlogits, eng.H),
         "fc1_conv_adam": lambda: C.fc1_conv_adam(eng.dH, eng.a1, M, eng.wslab1, eng.wslab2, eng.gb, B, P, Mm, V, None, eng.w1bf, eng.w1tbf, eng.w2r, eng.w2q, eng.off, eng.adam_t, 1, *a),
@@ -96,7 +99,7 @@ def main() -> None:
         torch.cuda.synchronize()
         res["step_graph"] = round(e0.elapsed_time(e1) * 1000.0 / 100, 2)
     if not only:
-        res["sum_isolated"] = round(sum(v for k, v in res.items() if k in ("conv1_fwd", "conv2_fwd", "gemm_fc1", "head", "route_dA1_only", "conv2_bwd", "fc2_fc1_conv_adam")), 2)
+        res["sum_isolated"] = round(sum(v for k, v in res.items() if k in ("conv1_fwd", "conv2_fwd", "gemm_fc1", "head", "route_dA1_split2" if eng.route_ws is not None else "route_dA1_only", "conv2_bwd", "fc2_fc1_conv_adam")), 2)
     print(json.dumps({"us_per_kernel": res, "batch": B}))
 
 

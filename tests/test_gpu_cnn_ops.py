@@ -192,29 +192,36 @@ def test_fc1_wgrad_adam(eng):
     eng.pack_shadows()
 
 
-def _route(eng, seed, row_major=None):
+def _route(eng, seed, row_major=None, split=None):
     """Random dH through route_fc2 (dA1 = dH W1, pool2/ReLU backward) into the dC2 map.
 
     The launch's FC2-Adam blocks update scratch copies, not the engine's weights.
     ``row_major`` picks the kernel reading W1 (LDS transpose reads) or a W1^T
     shadow (built here when the engine keeps none); default: the engine's.
+    ``split`` (row-major only) runs the 2-slice split-K variant with its
+    in-launch reduction; default: the engine's choice.
     """
     g = torch.Generator(device="cuda").manual_seed(seed)
     dh = (torch.randn(32, 2048, device="cuda", generator=g) * 1e-2).to(torch.bfloat16)
     P, Mm, V = eng.params.clone(), eng.m.clone(), eng.v.clone()
     rm = eng.route_rm if row_major is None else row_major
     w1 = eng.w1bf if rm else eng.w1bf.view(2048, 3136).t().contiguous()
+    sp = (eng.route_ws is not None) if split is None else split
+    ws = ctr = None
+    if rm and sp:
+        ws = eng.route_ws if eng.route_ws is not None else torch.zeros(98 * 2 * 32 * 32, device="cuda")
+        ctr = eng.route_ctr if eng.route_ctr is not None else torch.zeros(98, dtype=torch.int32, device="cuda")
     eng.C.route_fc2(dh, w1, eng.am2, 32, B, eng.dc2m, eng.gb, eng.dlogits, eng.H,
-                    P, Mm, V, None, eng.off, eng.adam_t, 1, *eng._adam(), row_major=rm)
+                    P, Mm, V, None, eng.off, eng.adam_t, 1, *eng._adam(), row_major=rm, ws=ws, ctr=ctr)
     torch.cuda.synchronize()
     return dh
 
 
-@pytest.mark.parametrize("row_major", [True, False])
-def test_gemm_da1_route(eng, row_major):
+@pytest.mark.parametrize("row_major,split", [(True, True), (True, False), (False, False)])
+def test_gemm_da1_route(eng, row_major, split):
     x = _x(6)
     _forward(eng, x)
-    dh = _route(eng, 21, row_major)
+    dh = _route(eng, 21, row_major, split)
     w1 = _bf(_p(eng, "l1.weight"))
     da1 = dh.float() @ w1  # [32, 3136]
     am2 = eng.am2.view(-1, 3136)[:B]
@@ -224,6 +231,21 @@ def test_gemm_da1_route(eng, row_major):
     m = eng.dc2m.view(-1, 64, 14, 16)[:B]
     assert _close(m[..., :14], _bf(want), rtol=8e-3, atol=1e-6) < 1e-4
     assert not bool(m[..., 14:].any())  # row padding stays zero
+
+
+def test_route_split_k_repeatable(eng):
+    """Split-K routing: the tile tickets return to zero after every launch, and the
+    slice-order reduction makes repeated launches bitwise identical."""
+    x = _x(6)
+    _forward(eng, x)
+    outs = []
+    for _ in range(3):
+        _route(eng, 21, True, True)
+        outs.append((eng.gb.clone(), eng.dc2m.clone()))
+    for gb, dc in outs[1:]:
+        assert torch.equal(gb, outs[0][0]) and torch.equal(dc, outs[0][1])
+    if eng.route_ctr is not None:
+        assert not bool(eng.route_ctr.any())
 
 
 def test_conv2_bwd(eng):
@@ -262,7 +284,8 @@ def test_conv2_bwd_partial_batch(eng, Bp):
     dh = (torch.randn(32, 2048, device="cuda", generator=g) * 1e-2).to(torch.bfloat16)
     dh[Bp:] = 0
     P, Mm, V = eng.params.clone(), eng.m.clone(), eng.v.clone()
-    eng.C.route_fc2(dh, eng.w1_route, eng.am2, 32, Bp, eng.dc2m, eng.gb, eng.dlogits, eng.H, P, Mm, V, None, eng.off, eng.adam_t, 1, *eng._adam(), row_major=eng.route_rm)
+    eng.C.route_fc2(dh, eng.w1_route, eng.am2, 32, Bp, eng.dc2m, eng.gb, eng.dlogits, eng.H, P, Mm, V, None, eng.off,
+                    eng.adam_t, 1, *eng._adam(), row_major=eng.route_rm, ws=eng.route_ws, ctr=eng.route_ctr)
     eng.C.conv2_bwd(eng.dc2m, eng.p1s, eng.am1, eng.w2q, x.reshape(-1, 784), None, eng.wslab1, eng.wslab2, Bp)
     torch.cuda.synchronize()
     dc2 = eng.dc2m.view(-1, 64, 14, 16)[:Bp, :, :, :14].float()

@@ -34,8 +34,8 @@ def test_pmc_summary_joins_counters_and_durations(tmp_path):
         text=True,
     )
     line = [ln for ln in out.splitlines() if ln.startswith("head_kernel")][0].split()
-    # columns: name, dur, FETCH_SIZE, GRBM_GUI_ACTIVE, SQ_VALU_MFMA_BUSY_CYCLES, WRITE_SIZE, GB/s, MFMA busy
+    # columns: name, dur, FETCH_SIZE, GRBM_GUI_ACTIVE, SQ_VALU_MFMA_BUSY_CYCLES, WRITE_SIZE, GB/s, parked, issue-stall, MFMA busy
     assert line[1] == "10.00"
     # (2 * 100 KB + 300 KB) / 10 us = 50 GB/s
-    assert line[-2] == "50"
+    assert line[-4] == "50"  # then parked, issue-stall (nan: no SQ_WAVE_CYCLES), MFMA busy
     assert line[-1] == "25.0%"
