@@ -638,6 +638,63 @@ P2_DEVICE void conv2_wgrad_role(int t, int g, const uint16_t* __restrict__ dc2m,
   }
 }
 
+// wgrad block (image pair g, column tap kx): the per-wave role above re-reads the
+// pair's dC2 rows from L2 once per tap (25 x) -- 336 KB per 4-wave block, so the
+// role is bound by what one CU can fetch (~11 B/cycle/CU, MI355X_MICROARCH.md),
+// not by its 56 MFMAs per wave.  Here the block stages the pair's dC2 map
+// (2 x 28 KB) and its kx-shifted P1 planes (2 x 18 KB) into LDS once, by
+// global_load_lds, and wave w computes the row taps ky = w (and wave 0 also
+// ky = 4) from LDS: 94 KB fetched per block, 5 x groups blocks.  Same slab
+// layout and summation order per tap as the per-wave role.
+constexpr int kWgA = kWgG * kC2 * 224 * 2;      // dC2 of the pair: [img][oc][224] bf16
+constexpr int kWgB = kWgG * kC1 * kP1sPlane * 2;  // P1 planes at kx: [img][ic][18 x 16] bf16
+static_assert(kWgA + kWgB <= 143424, "wgrad staging must fit the launch's LDS");
+
+P2_DEVICE void glds_copy(const uint16_t* src, char* dst, int bytes, int wave, int lane) {
+  // 1 KB per wave instruction (64 lanes x 16 B), lane-linear LDS image
+  for (int c = wave; c * 1024 < bytes; c += 4)
+    __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(src + c * 512 + lane * 8),
+                                     (__attribute__((address_space(3))) void*)(dst + c * 1024), 16, 0, 0);
+}
+
+P2_DEVICE void conv2_wgrad_block(int g, int kx, const uint16_t* __restrict__ dc2m, const uint16_t* __restrict__ p1s,
+                                 float* __restrict__ wslab, int B, char* smem) {
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, r = lane & 31, h = lane >> 5;
+  const int b0 = g * kWgG, nb = min(kWgG, B - b0);
+  const uint16_t* sa = reinterpret_cast<const uint16_t*>(smem);
+  const uint16_t* sb = reinterpret_cast<const uint16_t*>(smem + kWgA);
+  // the pair's images are consecutive in the dC2 map; the P1 planes of one kx
+  // are one contiguous [ic][plane] block per image
+  glds_copy(dc2m + size_t(b0) * kC2 * 224, smem, nb * kC2 * 224 * 2, wave, lane);
+  for (int i = 0; i < nb; ++i)
+    glds_copy(p1s + (size_t(b0 + i) * 5 + kx) * kC1 * kP1sPlane, smem + kWgA + i * (kC1 * kP1sPlane * 2),
+              kC1 * kP1sPlane * 2, wave, lane);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  for (int ky = wave; ky < 5; ky += 4) {
+    f32x16 acc0 = {}, acc1 = {};
+    for (int i = 0; i < nb; ++i) {
+      const uint16_t* a = sa + (i * kC2 + r) * 224 + 8 * h;
+      const uint16_t* bb = sb + (i * kC1 + r) * kP1sPlane + ky * 16 + 8 * h;
+#pragma unroll
+      for (int ks = 0; ks < 14; ++ks) {
+        const uint4 a0 = *reinterpret_cast<const uint4*>(a + ks * 16);
+        const uint4 a1 = *reinterpret_cast<const uint4*>(a + 32 * 224 + ks * 16);
+        const uint4 bq = *reinterpret_cast<const uint4*>(bb + ks * 16);
+        acc0 = mfma32b(a0, bq, acc0);
+        acc1 = mfma32b(a1, bq, acc1);
+      }
+    }
+    float* out = wslab + (size_t(g) * kTaps + ky * 5 + kx) * kC2 * kC1 + r;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      const int oc = acc_row_b(i, h);
+      out[oc * kC1] = acc0[i];
+      out[(oc + 32) * kC1] = acc1[i];
+    }
+  }
+}
+
 // dgrad block: 4 waves = 4 consecutive 32-position tiles of one image
 // (group 0: tiles 0-3 = conv rows 0..9, group 1: tiles 4-6 = rows 9..13; the
 // 4th wave of group 1 only helps staging).  The block stages, in one memory
@@ -765,11 +822,15 @@ __global__ __launch_bounds__(256) void conv2_bwd_kernel(const uint16_t* __restri
                                                         const uint16_t* __restrict__ w2q,
                                                         const uint8_t* __restrict__ xds,
                                                         const int64_t* __restrict__ idx, float* __restrict__ wslab1,
-                                                        float* __restrict__ wslab2, int B, int first_block) {
+                                                        float* __restrict__ wslab2, int B, int first_block,
+                                                        int wg_blocks) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int j = blockIdx.x + first_block, nd = 2 * B;
   if (j < nd) {
     conv2_dgrad_block(j & 1, j >> 1, dc2m, am1, w2q, xds, idx, wslab1, smem);
+  } else if (wg_blocks) {
+    const int k = j - nd;  // (image pair, kx)
+    conv2_wgrad_block(k / 5, k % 5, dc2m, p1s, wslab2, B, smem);
   } else {
     const int k = (j - nd) * 4 + (threadIdx.x >> 6);
     if (k < kTaps * wgrad_groups(B)) conv2_wgrad_role(k % kTaps, k / kTaps, dc2m, p1s, wslab2, B);
@@ -789,11 +850,17 @@ void conv2_bwd(const uint16_t* dc2m, const uint16_t* p1s, const uint8_t* am1, co
     const char* e = getenv("P2CNN_CONV2BWD_ROLES");
     return e ? atoi(e) : 3;
   }();
-  const int nd = 2 * B, nw = (kTaps * wgrad_groups(B) + 3) / 4;
+  // wgrad as LDS-staged (image pair, kx) blocks (default) or as the per-wave
+  // (tap, image pair) role streaming from L2 (P2CNN_CONV2_WG_BLOCKS=0)
+  static const int wg_blocks = [] {
+    const char* e = getenv("P2CNN_CONV2_WG_BLOCKS");
+    return e ? atoi(e) : 1;
+  }();
+  const int nd = 2 * B, nw = wg_blocks ? 5 * wgrad_groups(B) : (kTaps * wgrad_groups(B) + 3) / 4;
   const int first = roles == 2 ? nd : 0;
   const int blocks = roles == 1 ? nd : roles == 2 ? nw : nd + nw;
   hipLaunchKernelGGL(conv2_bwd_kernel, dim3(blocks), dim3(256), kDgLds, s, dc2m, p1s, am1, w2q, x, idx, wslab1, wslab2,
-                     B, first);
+                     B, first, wg_blocks);
 }
 
 // ---------------------------------------------------------------------------
