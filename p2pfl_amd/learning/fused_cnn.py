@@ -66,7 +66,7 @@ class FusedCNNEngine:
         weight_decay: float = 0.0,
         mrows: int = 32,
         arena: Optional[ModuleArena] = None,
-        split_fc1: int = 7,
+        split_fc1: Optional[int] = None,
     ) -> None:
         self.C = ops.ext().cnn
         self.C.init()
@@ -82,7 +82,12 @@ class FusedCNNEngine:
         self.off: List[int] = [int(o) for o in lay.offsets]
         self.lr, self.betas, self.eps, self.wd = lr, betas, eps, weight_decay
         self.mrows = mrows
-        self.S1 = split_fc1
+        # K-slices of the FC1 GEMM (gemm_skinny: 64 column tiles x S1 workgroups); the
+        # head reads the S1 fp32 partial rows of its sample, so fewer slices mean fewer
+        # bytes for the head's 32 workgroups (P2PFL_CNN_FC1_SPLITS overrides)
+        self.S1 = int(split_fc1 if split_fc1 is not None else os.environ.get("P2PFL_CNN_FC1_SPLITS", "7"))
+        if not 1 <= self.S1 <= 49:
+            raise ValueError(f"FC1 split count {self.S1} outside [1, 49]")
         dev, bf = self.device, torch.bfloat16
         z = lambda *s, dt=torch.float32: torch.zeros(*s, dtype=dt, device=dev)  # noqa: E731
         n = self.arena.flat.numel()
