@@ -63,9 +63,11 @@ void conv2_fwd(const uint16_t* p1, const uint16_t* w2r, const float* params, Off
 
 void gemm_skinny(const uint16_t* A, const uint16_t* Bt, float* slabs, int mrows, int N, int K, int S, hipStream_t s);
 
+// w2bf non-null: the FC2 weight is read from its bf16 copy [10][2048] (half the
+// bytes of the fp32 master) -- kept current by fc1_conv_adam / pack_shadows
 void head(const float* slabs, int S, int mrows, const float* params, Offsets off, const int64_t* labels,
           const int64_t* idx, int B, int train, uint16_t* H, uint16_t* dH, float* dlogits, float* stats,
-          hipStream_t s);
+          const uint16_t* w2bf, hipStream_t s);
 
 void fc1_wgrad_adam(const uint16_t* dH, const uint16_t* a1, int mrows, float* params, float* m, float* v,
                     float* gdump, uint16_t* w1bf, uint16_t* w1tbf, Offsets off, const int* adam_t, int t_off,
@@ -104,11 +106,11 @@ void conv_adam(const float* wslab1, const float* wslab2, const float* gb, int B,
 void fc1_conv_adam(const uint16_t* dH, const uint16_t* a1, int mrows, const float* wslab1, const float* wslab2,
                    const float* gb, int B, float* params, float* m, float* v, float* gdump, uint16_t* w1bf,
                    uint16_t* w1tbf, uint16_t* w2r, uint16_t* w2q, Offsets off, const int* adam_t, int t_off,
-                   AdamCfg cfg, const float* dlogits, const uint16_t* H, hipStream_t s);
+                   AdamCfg cfg, const float* dlogits, const uint16_t* H, uint16_t* w2bf, hipStream_t s);
 
 // Standalone packing of the bf16 shadows from fp32 params (after set_parameters).
 void pack_shadows(const float* params, Offsets off, uint16_t* w2r, uint16_t* w2q, uint16_t* w1bf, uint16_t* w1tbf,
-                  hipStream_t s);
+                  uint16_t* w2bf, hipStream_t s);
 
 constexpr int kP1sPlane = 18 * 16;                 // one shifted padded P1 channel plane
 constexpr int kP1s = 5 * kC1 * kP1sPlane;          // P1s elements per image (46080)

@@ -95,7 +95,7 @@ void k_gemm_skinny(torch::Tensor A, torch::Tensor Bt, torch::Tensor slabs, int64
 
 void k_head(torch::Tensor slabs, int64_t S, int64_t mrows, torch::Tensor params, std::vector<int64_t> off,
             torch::Tensor labels, c10::optional<torch::Tensor> idx, int64_t B, bool train, torch::Tensor H,
-            torch::Tensor dH, torch::Tensor dlogits, torch::Tensor stats) {
+            torch::Tensor dH, torch::Tensor dlogits, torch::Tensor stats, c10::optional<torch::Tensor> w2bf) {
   const c10::DeviceGuard g(params.device());
   check_batch(int(B), int(mrows));
   Offsets o = offsets(off);
@@ -106,6 +106,7 @@ void k_head(torch::Tensor slabs, int64_t S, int64_t mrows, torch::Tensor params,
               reinterpret_cast<uint16_t*>(ptr<at::BFloat16>(H, torch::kBFloat16, mrows * 2048, "H")),
               reinterpret_cast<uint16_t*>(ptr<at::BFloat16>(dH, torch::kBFloat16, mrows * 2048, "dH")),
               ptr<float>(dlogits, torch::kFloat32, mrows * 10, "dlogits"), ptr<float>(stats, torch::kFloat32, 2, "stats", 4),
+              reinterpret_cast<const uint16_t*>(optr<at::BFloat16>(w2bf, torch::kBFloat16, 10 * 2048, "w2bf")),
               stream());
 }
 
@@ -208,7 +209,7 @@ void k_fc1_conv_adam(torch::Tensor dH, torch::Tensor a1, int64_t mrows, torch::T
                      c10::optional<torch::Tensor> gdump, torch::Tensor w1bf, c10::optional<torch::Tensor> w1tbf, torch::Tensor w2r,
                      torch::Tensor w2q, std::vector<int64_t> off, torch::Tensor adam_t, int64_t t_off, double lr,
                      double b1, double b2, double eps, double wd, c10::optional<torch::Tensor> dlogits,
-                     c10::optional<torch::Tensor> H) {
+                     c10::optional<torch::Tensor> H, c10::optional<torch::Tensor> w2bf) {
   const c10::DeviceGuard g(params.device());
   check_batch(int(B), int(mrows));
   TORCH_CHECK(mrows <= 64, "fc1_conv_adam: mrows must be 32 or 64");
@@ -229,11 +230,12 @@ void k_fc1_conv_adam(torch::Tensor dH, torch::Tensor a1, int64_t mrows, torch::T
       reinterpret_cast<uint16_t*>(ptr<at::BFloat16>(w2q, torch::kBFloat16, 51200, "w2q")), o,
       ptr<int>(adam_t, torch::kInt32, 1, "adam_t", 4), int(t_off), cfg(lr, b1, b2, eps, wd),
       optr<float>(dlogits, torch::kFloat32, B * 10, "dlogits"),
-      reinterpret_cast<const uint16_t*>(optr<at::BFloat16>(H, torch::kBFloat16, B * 2048, "H")), stream());
+      reinterpret_cast<const uint16_t*>(optr<at::BFloat16>(H, torch::kBFloat16, B * 2048, "H")),
+      reinterpret_cast<uint16_t*>(optr<at::BFloat16>(w2bf, torch::kBFloat16, 10 * 2048, "w2bf")), stream());
 }
 
 void k_pack_shadows(torch::Tensor params, std::vector<int64_t> off, torch::Tensor w2r, torch::Tensor w2q,
-                    torch::Tensor w1bf, c10::optional<torch::Tensor> w1tbf) {
+                    torch::Tensor w1bf, c10::optional<torch::Tensor> w1tbf, c10::optional<torch::Tensor> w2bf) {
   const c10::DeviceGuard g(params.device());
   Offsets o = offsets(off);
   p2cnn::pack_shadows(ptr<float>(params, torch::kFloat32, params_end(o), "params"), o,
@@ -241,6 +243,7 @@ void k_pack_shadows(torch::Tensor params, std::vector<int64_t> off, torch::Tenso
                       reinterpret_cast<uint16_t*>(ptr<at::BFloat16>(w2q, torch::kBFloat16, 51200, "w2q")),
                       reinterpret_cast<uint16_t*>(ptr<at::BFloat16>(w1bf, torch::kBFloat16, 2048 * 3136, "w1bf")),
                       reinterpret_cast<uint16_t*>(optr<at::BFloat16>(w1tbf, torch::kBFloat16, 2048 * 3136, "w1tbf")),
+                      reinterpret_cast<uint16_t*>(optr<at::BFloat16>(w2bf, torch::kBFloat16, 10 * 2048, "w2bf")),
                       stream());
 }
 
@@ -256,7 +259,10 @@ void register_cnn(pybind11::module& m) {
   c.def("conv1_fwd", &k_conv1_fwd);
   c.def("conv2_fwd", &k_conv2_fwd);
   c.def("gemm_skinny", &k_gemm_skinny);
-  c.def("head", &k_head);
+  c.def("head", &k_head, pybind11::arg("slabs"), pybind11::arg("S"), pybind11::arg("mrows"), pybind11::arg("params"),
+        pybind11::arg("off"), pybind11::arg("labels"), pybind11::arg("idx"), pybind11::arg("B"), pybind11::arg("train"),
+        pybind11::arg("H"), pybind11::arg("dH"), pybind11::arg("dlogits"), pybind11::arg("stats"),
+        pybind11::arg("w2bf") = pybind11::none());
   c.def("route_fc2", &k_route_fc2, pybind11::arg("dH"), pybind11::arg("w1"), pybind11::arg("am2"), pybind11::arg("mrows"), pybind11::arg("B"),
         pybind11::arg("dc2m"), pybind11::arg("gb"), pybind11::arg("dlogits"), pybind11::arg("H"), pybind11::arg("params"), pybind11::arg("m"), pybind11::arg("v"),
         pybind11::arg("gdump"), pybind11::arg("off"), pybind11::arg("adam_t"), pybind11::arg("t_off"), pybind11::arg("lr"), pybind11::arg("b1"),
@@ -269,8 +275,10 @@ void register_cnn(pybind11::module& m) {
         pybind11::arg("wslab2"), pybind11::arg("gb"), pybind11::arg("B"), pybind11::arg("params"), pybind11::arg("m"), pybind11::arg("v"), pybind11::arg("gdump"),
         pybind11::arg("w1bf"), pybind11::arg("w1tbf"), pybind11::arg("w2r"), pybind11::arg("w2q"), pybind11::arg("off"), pybind11::arg("adam_t"),
         pybind11::arg("t_off"), pybind11::arg("lr"), pybind11::arg("b1"), pybind11::arg("b2"), pybind11::arg("eps"), pybind11::arg("wd"),
-        pybind11::arg("dlogits") = pybind11::none(), pybind11::arg("H") = pybind11::none());
-  c.def("pack_shadows", &k_pack_shadows);
+        pybind11::arg("dlogits") = pybind11::none(), pybind11::arg("H") = pybind11::none(),
+        pybind11::arg("w2bf") = pybind11::none());
+  c.def("pack_shadows", &k_pack_shadows, pybind11::arg("params"), pybind11::arg("off"), pybind11::arg("w2r"),
+        pybind11::arg("w2q"), pybind11::arg("w1bf"), pybind11::arg("w1tbf"), pybind11::arg("w2bf") = pybind11::none());
   c.def("wgrad_groups", [](int64_t B) { return int64_t(p2cnn::wgrad_groups(int(B))); },
         "conv2 weight-gradient partial slabs (of 51200 floats) written for a batch of B");
 }

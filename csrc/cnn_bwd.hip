@@ -88,7 +88,7 @@ template <int TPB>
 P2_DEVICE void fc2_role(int blk, const float* __restrict__ dlogits, const uint16_t* __restrict__ H, int B,
                         float* __restrict__ p, float* __restrict__ m, float* __restrict__ v,
                         float* __restrict__ gdump, const Offsets& off, const int* __restrict__ adam_t, int t_off,
-                        const AdamCfg& cfg) {
+                        const AdamCfg& cfg, uint16_t* __restrict__ w2bf = nullptr) {
   const int e = blk * TPB + threadIdx.x;
   const int nW = kCls * kHid;
   if (e >= nW + kCls) return;
@@ -115,6 +115,7 @@ P2_DEVICE void fc2_role(int blk, const float* __restrict__ dlogits, const uint16
   p[pi] = pv;
   m[pi] = mv;
   v[pi] = vv;
+  if (w2bf && e < nW) w2bf[e] = f32_to_bf16(pv);  // the head's bf16 copy of W2
 }
 
 template <int MT>
@@ -1029,13 +1030,14 @@ __global__ __launch_bounds__(256) void fc1_conv_adam_kernel(
     const float* __restrict__ ws2, const float* __restrict__ gb, int B, float* __restrict__ p, float* __restrict__ m,
     float* __restrict__ v, float* __restrict__ gdump, uint16_t* __restrict__ w1bf, uint16_t* __restrict__ w1tbf,
     uint16_t* __restrict__ w2r, uint16_t* __restrict__ w2q, Offsets off, const int* __restrict__ adam_t, int t_off,
-    AdamCfg cfg, const float* __restrict__ dlogits, const uint16_t* __restrict__ H, int nf2) {
+    AdamCfg cfg, const float* __restrict__ dlogits, const uint16_t* __restrict__ H, int nf2,
+    uint16_t* __restrict__ w2bf) {
   constexpr int kLds = Fc1Lds<MR>::kBytes > kConvAdamLds ? Fc1Lds<MR>::kBytes : kConvAdamLds;
   __shared__ __attribute__((aligned(16))) char smem[kLds];
   constexpr int kCA = kC2 + kC1Blocks, kBx = (kFeat + 127) / 128;
   int j = blockIdx.x;
   if (j < nf2) {
-    fc2_role<256>(j, dlogits, H, B, p, m, v, gdump, off, adam_t, t_off, cfg);
+    fc2_role<256>(j, dlogits, H, B, p, m, v, gdump, off, adam_t, t_off, cfg, w2bf);
     return;
   }
   j -= nf2;
@@ -1050,15 +1052,15 @@ __global__ __launch_bounds__(256) void fc1_conv_adam_kernel(
 void fc1_conv_adam(const uint16_t* dH, const uint16_t* a1, int mrows, const float* wslab1, const float* wslab2,
                    const float* gb, int B, float* params, float* m, float* v, float* gdump, uint16_t* w1bf,
                    uint16_t* w1tbf, uint16_t* w2r, uint16_t* w2q, Offsets off, const int* adam_t, int t_off,
-                   AdamCfg cfg, const float* dlogits, const uint16_t* H, hipStream_t s) {
+                   AdamCfg cfg, const float* dlogits, const uint16_t* H, uint16_t* w2bf, hipStream_t s) {
   const int nf2 = dlogits ? kFc2Blocks256 : 0;
   const dim3 grid(nf2 + kC2 + kC1Blocks + ((kFeat + 127) / 128) * (kHid / 32));
   if (mrows == 32)
     hipLaunchKernelGGL(fc1_conv_adam_kernel<32>, grid, dim3(256), 0, s, dH, a1, wslab1, wslab2, gb, B, params, m, v,
-                       gdump, w1bf, w1tbf, w2r, w2q, off, adam_t, t_off, cfg, dlogits, H, nf2);
+                       gdump, w1bf, w1tbf, w2r, w2q, off, adam_t, t_off, cfg, dlogits, H, nf2, w2bf);
   else
     hipLaunchKernelGGL(fc1_conv_adam_kernel<64>, grid, dim3(256), 0, s, dH, a1, wslab1, wslab2, gb, B, params, m, v,
-                       gdump, w1bf, w1tbf, w2r, w2q, off, adam_t, t_off, cfg, dlogits, H, nf2);
+                       gdump, w1bf, w1tbf, w2r, w2q, off, adam_t, t_off, cfg, dlogits, H, nf2, w2bf);
 }
 
 void conv_adam(const float* wslab1, const float* wslab2, const float* gb, int B, float* params, float* m, float* v,

@@ -315,7 +315,7 @@ __global__ __launch_bounds__(256) void head_kernel(const float* __restrict__ sla
                                                    const int64_t* __restrict__ idx, int B, int train,
                                                    uint16_t* __restrict__ H, uint16_t* __restrict__ dH,
                                                    float* __restrict__ dlogits,
-                                                   float* __restrict__ stats) {
+                                                   float* __restrict__ stats, const uint16_t* __restrict__ w2bf) {
   __shared__ float red[4][kCls];
   __shared__ float dl[kCls];
   const int b = blockIdx.x, tid = threadIdx.x, k0 = tid * 8;
@@ -334,12 +334,25 @@ __global__ __launch_bounds__(256) void head_kernel(const float* __restrict__ sla
   // issue every global load up front: this thread's 8-column slice of W2
   // (reused by the backward), the bias, and the split-K partial sums
   float wv[kCls][8];
+  if (w2bf) {  // bf16 copy: 16 B per class row slice instead of 32
 #pragma unroll
-  for (int c = 0; c < kCls; ++c) {
-    const float4* wp = reinterpret_cast<const float4*>(wl2 + size_t(c) * kHid + k0);
-    const float4 u = wp[0], w = wp[1];
-    wv[c][0] = u.x; wv[c][1] = u.y; wv[c][2] = u.z; wv[c][3] = u.w;
-    wv[c][4] = w.x; wv[c][5] = w.y; wv[c][6] = w.z; wv[c][7] = w.w;
+    for (int c = 0; c < kCls; ++c) {
+      const uint4 q = *reinterpret_cast<const uint4*>(w2bf + size_t(c) * kHid + k0);
+      const uint32_t u[4] = {q.x, q.y, q.z, q.w};
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        wv[c][2 * j] = __uint_as_float(u[j] << 16);
+        wv[c][2 * j + 1] = __uint_as_float(u[j] & 0xffff0000u);
+      }
+    }
+  } else {
+#pragma unroll
+    for (int c = 0; c < kCls; ++c) {
+      const float4* wp = reinterpret_cast<const float4*>(wl2 + size_t(c) * kHid + k0);
+      const float4 u = wp[0], w = wp[1];
+      wv[c][0] = u.x; wv[c][1] = u.y; wv[c][2] = u.z; wv[c][3] = u.w;
+      wv[c][4] = w.x; wv[c][5] = w.y; wv[c][6] = w.z; wv[c][7] = w.w;
+    }
   }
   float hv[8];
   {
@@ -424,9 +437,9 @@ __global__ __launch_bounds__(256) void head_kernel(const float* __restrict__ sla
 
 void head(const float* slabs, int S, int mrows, const float* params, Offsets off, const int64_t* labels,
           const int64_t* idx, int B, int train, uint16_t* H, uint16_t* dH, float* dlogits,
-          float* stats, hipStream_t s) {
+          float* stats, const uint16_t* w2bf, hipStream_t s) {
   hipLaunchKernelGGL(head_kernel, dim3(train ? mrows : B), dim3(256), 0, s, slabs, S, mrows, params + off.l1b,
-                     params + off.l2w, params + off.l2b, labels, idx, B, train, H, dH, dlogits, stats);
+                     params + off.l2w, params + off.l2b, labels, idx, B, train, H, dH, dlogits, stats, w2bf);
 }
 
 // ---------------------------------------------------------------------------
@@ -435,8 +448,12 @@ void head(const float* slabs, int S, int mrows, const float* params, Offsets off
 __global__ __launch_bounds__(256) void pack_shadows_kernel(const float* __restrict__ params, Offsets off,
                                                            uint16_t* __restrict__ w2r, uint16_t* __restrict__ w2q,
                                                            uint16_t* __restrict__ w1bf,
-                                                           uint16_t* __restrict__ w1tbf) {
+                                                           uint16_t* __restrict__ w1tbf, uint16_t* __restrict__ w2bf) {
   const int64_t n2 = int64_t(kC2) * kC1 * kTaps, n1 = int64_t(kHid) * kFeat;
+  if (w2bf)
+    for (int64_t e = int64_t(blockIdx.x) * blockDim.x + threadIdx.x; e < int64_t(kCls) * kHid;
+         e += int64_t(gridDim.x) * blockDim.x)
+      w2bf[e] = f32_to_bf16(params[off.l2w + e]);
   const int64_t stride = int64_t(gridDim.x) * blockDim.x;
   for (int64_t e = int64_t(blockIdx.x) * blockDim.x + threadIdx.x; e < n2 + n1; e += stride) {
     if (e < n2) {
@@ -455,8 +472,8 @@ __global__ __launch_bounds__(256) void pack_shadows_kernel(const float* __restri
 }
 
 void pack_shadows(const float* params, Offsets off, uint16_t* w2r, uint16_t* w2q, uint16_t* w1bf, uint16_t* w1tbf,
-                  hipStream_t s) {
-  hipLaunchKernelGGL(pack_shadows_kernel, dim3(2048), dim3(256), 0, s, params, off, w2r, w2q, w1bf, w1tbf);
+                  uint16_t* w2bf, hipStream_t s) {
+  hipLaunchKernelGGL(pack_shadows_kernel, dim3(2048), dim3(256), 0, s, params, off, w2r, w2q, w1bf, w1tbf, w2bf);
 }
 
 }  // namespace p2cnn

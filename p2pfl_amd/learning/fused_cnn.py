@@ -98,6 +98,10 @@ class FusedCNNEngine:
         self.route_rm = _ROUTE_RM
         self.w1bf = z(HID * FEAT, dt=bf)
         self.w1tbf = None if self.route_rm else z(HID * FEAT, dt=bf)
+        # bf16 FC2 weight read by the head (half the bytes of the fp32 master per
+        # head workgroup); refreshed by the merged Adam launch's FC2 blocks, so only
+        # kept on that path
+        self.w2bf = z(10 * HID, dt=bf) if _MERGED_ADAM else None
         # activations / workspaces (sized for mrows samples)
         M = mrows
         self.p1, self.am1 = z(M * 196 * 32, dt=bf), z(M * 196 * 32, dt=torch.uint8)
@@ -130,7 +134,7 @@ class FusedCNNEngine:
 
     def pack_shadows(self) -> None:
         """Refresh the bf16 weight copies after the fp32 parameters changed externally."""
-        self.C.pack_shadows(self.params, self.off, self.w2r, self.w2q, self.w1bf, self.w1tbf)
+        self.C.pack_shadows(self.params, self.off, self.w2r, self.w2q, self.w1bf, self.w1tbf, self.w2bf)
 
     def reset_optimizer(self) -> None:
         self.m.zero_()
@@ -146,7 +150,8 @@ class FusedCNNEngine:
         C.conv1_fwd(x, idx, self.params, self.off, self.p1, self.am1, self.p1s if train else None, B)
         C.conv2_fwd(self.p1, self.w2r, self.params, self.off, self.a1, self.am2, B, M)
         C.gemm_skinny(self.a1, self.w1bf, self.slabs1, M, HID, FEAT, self.S1)
-        C.head(self.slabs1, self.S1, M, self.params, self.off, labels, idx, B, train, self.H, self.dH, self.dlogits, stats)
+        C.head(self.slabs1, self.S1, M, self.params, self.off, labels, idx, B, train, self.H, self.dH, self.dlogits, stats,
+               self.w2bf)
 
     def train_step_async(
         self, x: torch.Tensor, labels: torch.Tensor, idx: Optional[torch.Tensor], B: int, stats: torch.Tensor, t_off: int
@@ -185,7 +190,7 @@ class FusedCNNEngine:
             C.conv2_bwd(self.dc2m, self.p1s, self.am1, self.w2q, x, idx, self.wslab1, self.wslab2, B)
             C.fc1_conv_adam(self.dH, self.a1, M, self.wslab1, self.wslab2, self.gb, B, self.params, self.m, self.v,
                             self.gdump, self.w1bf, self.w1tbf, self.w2r, self.w2q, self.off, self.adam_t, t_off, *a,
-                            self.dlogits, self.H)
+                            self.dlogits, self.H, self.w2bf)
             return
         C.route_fc2(self.dH, self.w1_route, self.am2, M, B, self.dc2m, self.gb, self.dlogits, self.H,
                     self.params, self.m, self.v, self.gdump, self.off, self.adam_t, t_off, *a, True, self.route_rm,
@@ -235,7 +240,7 @@ class _EvalForward:
         C.conv1_fwd(x, idx, e.params, e.off, self.p1, self.am1, None, B)
         C.conv2_fwd(self.p1, e.w2r, e.params, e.off, self.a1, self.am2, B, M)
         C.gemm_skinny(self.a1, e.w1bf, self.slabs1, M, HID, FEAT, e.S1)
-        C.head(self.slabs1, e.S1, M, e.params, e.off, labels, idx, B, False, self.H, self.dH, self.dlogits, stats)
+        C.head(self.slabs1, e.S1, M, e.params, e.off, labels, idx, B, False, self.H, self.dH, self.dlogits, stats, e.w2bf)
 
 
 class _EpochGraph:

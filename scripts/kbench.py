@@ -46,20 +46,22 @@ def main() -> None:
     # launches do not drift the weights into NaN territory
     P, Mm, V = eng.params.clone(), eng.m.clone(), eng.v.clone()
     w1t = eng.w1bf.view(2048, 3136).t().contiguous()  # for the W1^T-shadow variants
+    w2s = torch.zeros(10 * 2048, dtype=torch.bfloat16, device=dev)  # scratch bf16 W2 copy for the Adam arm
     rws = torch.zeros(98 * 2 * M * 32, device=dev)  # split-K routing partials / tickets
     rctr = torch.zeros(98, dtype=torch.int32, device=dev)
     ks = {
         "conv1_fwd": lambda: C.conv1_fwd(x, None, eng.params, eng.off, eng.p1, eng.am1, eng.p1s, B),
         "conv2_fwd": lambda: C.conv2_fwd(eng.p1, eng.w2r, eng.params, eng.off, eng.a1, eng.am2, B, M),
         "gemm_fc1": lambda: C.gemm_skinny(eng.a1, eng.w1bf, eng.slabs1, M, 2048, 3136, eng.S1),
-        "head": lambda: C.head(eng.slabs1, eng.S1, M, eng.params, eng.off, y, None, B, True, eng.H, eng.dH, eng.dlogits, stats),
+        "head": lambda: C.head(eng.slabs1, eng.S1, M, eng.params, eng.off, y, None, B, True, eng.H, eng.dH, eng.dlogits, stats, eng.w2bf),
+        "head_w2fp32": lambda: C.head(eng.slabs1, eng.S1, M, eng.params, eng.off, y, None, B, True, eng.H, eng.dH, eng.dlogits, stats),
         "route_fc2": lambda: C.route_fc2(eng.dH, eng.w1_route, eng.am2, M, B, eng.dc2m, eng.gb, eng.dlogits, eng.H, P, Mm, V, None, eng.off, eng.adam_t, 1, *a, True, eng.route_rm),
         "route_dA1_only": lambda: C.route_fc2(eng.dH, eng.w1bf, eng.am2, M, B, eng.dc2m, eng.gb, eng.dlogits, eng.H, P, Mm, V, None, eng.off, eng.adam_t, 1, *a, False, True),
         "route_dA1_split2": lambda: C.route_fc2(eng.dH, eng.w1bf, eng.am2, M, B, eng.dc2m, eng.gb, eng.dlogits, eng.H, P, Mm, V, None, eng.off, eng.adam_t, 1, *a, False, True, rws, rctr),
         "route_dA1_w1t": lambda: C.route_fc2(eng.dH, w1t, eng.am2, M, B, eng.dc2m, eng.gb, eng.dlogits, eng.H, P, Mm, V, None, eng.off, eng.adam_t, 1, *a, False, False),
         "fc1_conv_adam_w1t": lambda: C.fc1_conv_adam(eng.dH, eng.a1, M, eng.wslab1, eng.wslab2, eng.gb, B, P, Mm, V, None, eng.w1bf, w1t, eng.w2r, eng.w2q, eng.off, eng.adam_t, 1, *a, eng.dlogits, eng.H),
         "fc1_conv_adam": lambda: C.fc1_conv_adam(eng.dH, eng.a1, M, eng.wslab1, eng.wslab2, eng.gb, B, P, Mm, V, None, eng.w1bf, eng.w1tbf, eng.w2r, eng.w2q, eng.off, eng.adam_t, 1, *a),
-        "fc2_fc1_conv_adam": lambda: C.fc1_conv_adam(eng.dH, eng.a1, M, eng.wslab1, eng.wslab2, eng.gb, B, P, Mm, V, None, eng.w1bf, eng.w1tbf, eng.w2r, eng.w2q, eng.off, eng.adam_t, 1, *a, eng.dlogits, eng.H),
+        "fc2_fc1_conv_adam": lambda: C.fc1_conv_adam(eng.dH, eng.a1, M, eng.wslab1, eng.wslab2, eng.gb, B, P, Mm, V, None, eng.w1bf, eng.w1tbf, eng.w2r, eng.w2q, eng.off, eng.adam_t, 1, *a, eng.dlogits, eng.H, w2s),
         "fc1_wgrad_adam": lambda: C.fc1_wgrad_adam(eng.dH, eng.a1, M, P, Mm, V, None, eng.w1bf, eng.w1tbf, eng.off, eng.adam_t, 1, *a),
         "conv2_bwd": lambda: C.conv2_bwd(eng.dc2m, eng.p1s, eng.am1, eng.w2q, x, None, eng.wslab1, eng.wslab2, B),
         "conv_adam": lambda: C.conv_adam(eng.wslab1, eng.wslab2, eng.gb, B, P, Mm, V, None, eng.w2r, eng.w2q, eng.off, eng.adam_t, 1, *a),

@@ -123,14 +123,20 @@ def test_gemm_skinny(eng, N, K, S):
     torch.testing.assert_close(got, want, atol=2e-3 * K**0.5, rtol=1e-4)
 
 
-def test_head_and_fc2_wgrad(eng):
+@pytest.mark.parametrize("w2_bf16", [False, True])
+def test_head_and_fc2_wgrad(eng, w2_bf16):
+    """Head (FC1 epilogue, FC2, cross-entropy, dH) reading W2 in fp32 or from its bf16
+    copy (the reference is then taken on the bf16-rounded W2); then the FC2 gradient."""
     g = torch.Generator(device="cuda").manual_seed(7)
     slabs = torch.randn(eng.S1 * 32 * 2048, device="cuda", generator=g) * 0.05
     labels = torch.randint(0, 10, (B,), device="cuda", generator=g)
     stats = torch.zeros(4, device="cuda")
-    eng.C.head(slabs, eng.S1, 32, eng.params, eng.off, labels, None, B, True, eng.H, eng.dH, eng.dlogits, stats)
+    w2bf = _p(eng, "l2.weight").to(torch.bfloat16).contiguous() if w2_bf16 else None
+    eng.C.head(slabs, eng.S1, 32, eng.params, eng.off, labels, None, B, True, eng.H, eng.dH, eng.dlogits, stats, w2bf)
     torch.cuda.synchronize()
     b1, w2, b2 = _p(eng, "l1.bias"), _p(eng, "l2.weight"), _p(eng, "l2.bias")
+    if w2_bf16:
+        w2 = _bf(w2)
     h = F.relu(slabs.view(eng.S1, 32, 2048).sum(0)[:B] + b1)
     logits = h @ w2.t() + b2
     loss = F.cross_entropy(logits, labels, reduction="sum")
@@ -346,3 +352,23 @@ def test_bf16_reference_has_similar_gradient_error():
     }
     print("torch bf16-autocast vs fp32 gradient rel err:", rel)
 
+
+
+def test_w2_bf16_copy_tracks_the_fp32_weight():
+    """The head's bf16 FC2 weight is refreshed by every training step's Adam launch and
+    by pack_shadows: after steps it equals the fp32 master rounded to bf16."""
+    from p2pfl_amd.learning import fused_cnn
+    from p2pfl_amd.learning.fused_cnn import FusedCNNEngine
+
+    if not fused_cnn._MERGED_ADAM:
+        pytest.skip("the bf16 W2 copy is kept on the merged-Adam path only")
+    e = FusedCNNEngine(CNN(seed=5).cuda(), device=torch.device("cuda"))
+    o = e.off[6]
+    assert torch.equal(e.w2bf, e.params[o : o + 20480].to(torch.bfloat16))
+    x = _x(4).reshape(-1, 784)
+    y = torch.randint(0, 10, (B,), device="cuda")
+    for _ in range(3):
+        e.train_step(x, y)
+    torch.cuda.synchronize()
+    w2 = e.params[o : o + 20480]
+    assert torch.equal(e.w2bf, w2.to(torch.bfloat16))
