@@ -15,6 +15,8 @@
 // MFMA: v_mfma_f32_32x32x16_bf16.  Lane l (r = l & 31, h = l >> 5) supplies
 // A[row r][k = 8h + j] and B[k = 8h + j][col r], j = 0..7; the accumulator
 // register i of lane l holds C[row (i&3) + 8(i>>2) + 4h][col r].
+#include <cstdlib>
+
 #include "cnn.h"
 #include "common.h"
 
@@ -209,11 +211,92 @@ __global__ __launch_bounds__(64) void conv2_fwd_kernel(const uint16_t* __restric
   }
 }
 
+// Same conv2, LDS-staged: one 7-wave block per (oc half, image).  The kernel
+// above streams every operand fragment from L2 per wave -- 50 KB of P1 pixels
+// and 50 KB of weights for each of its 448 waves, ~175 KB per CU -- and is bound
+// by what one CU can fetch (~11 B/cycle/CU, MI355X_MICROARCH.md).  Here the
+// block copies the image's P1 (12.25 KB) and its 32 oc rows of the weight
+// (50 KB) into LDS once (global_load_lds), and its 7 waves (pooled rows) read
+// every fragment from LDS: ~62 KB fetched per block.  Same k order, MFMA
+// sequence and pool epilogue as the streaming kernel (bitwise-equal results).
+constexpr int kC2P1 = 196 * kC1 * 2;            // 12544 B
+constexpr int kC2W = 32 * kTaps * kC1 * 2;      // 51200 B
+constexpr int kC2Out = 7 * 32 * 33 * 4;         // per-wave pool exchange, 29568 B
+constexpr int kC2Lds = kC2P1 + kC2W + kC2Out;   // 93312 B
+
+P2_DEVICE void glds_copy_n(const uint16_t* src, char* dst, int bytes, int wave, int nwaves, int lane) {
+  // 1 KB per wave instruction (64 lanes x 16 B); a partial last chunk masks lanes
+  for (int c = wave; c * 1024 < bytes; c += nwaves)
+    if (c * 1024 + lane * 16 < bytes)
+      __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(src + c * 512 + lane * 8),
+                                       (__attribute__((address_space(3))) void*)(dst + c * 1024), 16, 0, 0);
+}
+
+__global__ __launch_bounds__(448) void conv2_fwd_lds_kernel(const uint16_t* __restrict__ p1,
+                                                            const uint16_t* __restrict__ w2r,
+                                                            const float* __restrict__ b2, uint16_t* __restrict__ a1,
+                                                            uint8_t* __restrict__ am2) {
+  __shared__ __attribute__((aligned(16))) char smem[kC2Lds];
+  const int nh = blockIdx.x, b = blockIdx.y;
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, r = lane & 31, h = lane >> 5;
+  const int py = wave;
+  glds_copy_n(p1 + size_t(b) * 196 * kC1, smem, kC2P1, wave, 7, lane);
+  glds_copy_n(w2r + size_t(nh * 32) * kTaps * kC1, smem + kC2P1, kC2W, wave, 7, lane);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  const uint16_t* img = reinterpret_cast<const uint16_t*>(smem) + 8 * h;
+  const uint16_t* wrow = reinterpret_cast<const uint16_t*>(smem + kC2P1) + r * kTaps * kC1 + 8 * h;
+  float(*sout)[33] = reinterpret_cast<float(*)[33]>(smem + kC2P1 + kC2W + wave * (32 * 33 * 4));
+  const int rr = r < 28 ? r : 27;
+  const int y = 2 * py + (rr >= 14 ? 1 : 0), x = rr >= 14 ? rr - 14 : rr;
+  const uint4 z4 = make_uint4(0, 0, 0, 0);
+  f32x16 acc = {};
+#pragma unroll 10
+  for (int s = 0; s < 50; ++s) {
+    const int t = s >> 1, ky = t / 5, kx = t % 5, ic = (s & 1) * 16;
+    const int iy = y + ky - 2, ix = x + kx - 2;
+    const bool ok = iy >= 0 && iy < 14 && ix >= 0 && ix < 14;
+    const uint4 v = *reinterpret_cast<const uint4*>(img + (ok ? iy * 14 + ix : 0) * kC1 + ic);
+    const uint4 bq = *reinterpret_cast<const uint4*>(wrow + t * kC1 + ic);
+    acc = mfma32(ok ? v : z4, bq, acc);
+  }
+#pragma unroll
+  for (int i = 0; i < 16; ++i) {
+    const int row = acc_row(i, h);
+    if (row < 28) sout[row][r] = acc[i];
+  }
+  __syncthreads();
+  for (int e = lane; e < 7 * 32; e += 64) {
+    const int oc = e / 7, px = e % 7;
+    const float v[4] = {sout[2 * px][oc], sout[2 * px + 1][oc], sout[14 + 2 * px][oc], sout[15 + 2 * px][oc]};
+    float best = v[0];
+    int arg = 0;
+#pragma unroll
+    for (int d = 1; d < 4; ++d)
+      if (v[d] > best) {
+        best = v[d];
+        arg = d;
+      }
+    best += b2[nh * 32 + oc];
+    const size_t o = size_t(b) * kFeat + (nh * 32 + oc) * 49 + py * 7 + px;
+    a1[o] = f32_to_bf16(fmaxf(best, 0.f));
+    am2[o] = best > 0.f ? uint8_t(arg) : uint8_t(4);
+  }
+}
+
 void init_fwd_attributes() {}
 
 void conv2_fwd(const uint16_t* p1, const uint16_t* w2r, const float* params, Offsets off, uint16_t* a1,
                uint8_t* am2, int B, hipStream_t s) {
-  hipLaunchKernelGGL(conv2_fwd_kernel, dim3(7, 2, B), dim3(64), 0, s, p1, w2r, params + off.c2b, a1, am2);
+  // P2CNN_CONV2_FWD_LDS=0: the per-wave streaming kernel (A/B measurement knob, read once)
+  static const bool lds = [] {
+    const char* e = getenv("P2CNN_CONV2_FWD_LDS");
+    return !e || atoi(e) != 0;
+  }();
+  if (lds)
+    hipLaunchKernelGGL(conv2_fwd_lds_kernel, dim3(2, B), dim3(448), 0, s, p1, w2r, params + off.c2b, a1, am2);
+  else
+    hipLaunchKernelGGL(conv2_fwd_kernel, dim3(7, 2, B), dim3(64), 0, s, p1, w2r, params + off.c2b, a1, am2);
 }
 
 // ---------------------------------------------------------------------------
