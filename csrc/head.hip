@@ -10,9 +10,10 @@
 //            fixed-order LDS reduction), its log-sum-exp loss and argmax hit; the
 //            last workgroup to arrive (relaxed ticket, sc1 partials) writes the
 //            batch-mean loss and accuracy in fixed sample order.
-//   backward (grid B + 1): workgroup b < B writes dF[b] = (dL/dlogits_b . W) / HW
-//            broadcast over its HW pixels (bf16, channels-last); workgroup B
-//            computes dW = dlogits^T pooled and db = column sums of dlogits.
+//   backward (grid B + ceil(N C / 256)): workgroup b < B writes dF[b] =
+//            (dL/dlogits_b . W) / HW broadcast over its HW pixels (bf16,
+//            channels-last); the others compute dW = dlogits^T pooled, one element
+//            per thread, and db = column sums of dlogits.
 //
 // The reference's heads: nn.Linear + CrossEntropyLoss in
 // /root/reference/p2pfl/learning/pytorch/mnist_examples/models/cnn.py:71-98.
@@ -57,8 +58,16 @@ __global__ __launch_bounds__(kT) void head_fwd_kernel(const uint16_t* __restrict
   for (int n = 0; n < kMaxN; ++n) part[n] = 0.f;
   const uint16_t* fb = f + int64_t(b) * HW * C;
   for (int c = tid; c < C; c += kT) {
-    float s = 0.f;
-    for (int p = 0; p < HW; ++p) s += bf16_to_f32(fb[int64_t(p) * C + c]);
+    // 8 independent partial sums: the pixel loads of one channel are all in flight
+    // at once instead of one dependent L2 round trip per pixel (HW = 16..49)
+    float q[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    int p = 0;
+    for (; p + 8 <= HW; p += 8) {
+#pragma unroll
+      for (int u = 0; u < 8; ++u) q[u] += bf16_to_f32(fb[int64_t(p + u) * C + c]);
+    }
+    for (int u = 0; p < HW; ++p, ++u) q[u] += bf16_to_f32(fb[int64_t(p) * C + c]);
+    float s = ((q[0] + q[1]) + (q[2] + q[3])) + ((q[4] + q[5]) + (q[6] + q[7]));
     s *= inv;
     pooled[int64_t(b) * C + c] = s;
 #pragma unroll
@@ -142,38 +151,49 @@ __global__ __launch_bounds__(kT) void head_bwd_kernel(const float* __restrict__ 
     uint16_t* out = df + int64_t(b) * HW * C;
     for (int c = tid; c < C; c += kT) {
       float s = 0.f;
-      for (int n = 0; n < N; ++n) s = fmaf(dl[n], ldw<TW>(w, int64_t(n) * C + c), s);
+#pragma unroll
+      for (int n = 0; n < kMaxN; ++n)  // unrolled + predicated: the N weight loads issue together
+        if (n < N) s = fmaf(dl[n], ldw<TW>(w, int64_t(n) * C + c), s);
       const uint16_t v = f32_to_bf16(s * inv);
       for (int p = 0; p < HW; ++p) out[int64_t(p) * C + c] = v;
     }
     return;
   }
-  // workgroup B: dW[n][c] = sum_b dl_b[n] pooled[b][c], db[n] = sum_b dl_b[n]
+  // workgroups B.. : one thread per dW element, dW[n][c] = sum_b dl_b[n] pooled[b][c]
+  // (samples in order, loads unrolled so they are in flight together); the first
+  // of them also writes db[n] = sum_b dl_b[n].  (One workgroup looping over all
+  // N x C elements spent ~70 us on dependent pooled loads for ResNet-18.)
   __shared__ float dla[64][kMaxN];  // dl of up to 64 samples per chunk
+  const int e = (b - B) * kT + tid;
+  const int n = e / C, c = e - n * C;
+  const bool live = e < N * C;
+  float s = 0.f, sb = 0.f;
   for (int b0 = 0; b0 < B; b0 += 64) {
     const int nb = min(64, B - b0);
     __syncthreads();
     if (tid < nb) dlogits(logits + int64_t(b0 + tid) * N, min(max(int(y[b0 + tid]), 0), N - 1), N, gscale, dla[tid]);
     __syncthreads();
-    if (b0 == 0 && tid < N) {
-      float s = 0.f;
-      for (int i = 0; i < nb; ++i) s += dla[i][tid];
-      db[tid] = s;
-    } else if (tid < N) {
-      float s = db[tid];
-      for (int i = 0; i < nb; ++i) s += dla[i][tid];
-      db[tid] = s;
+    if (live) {
+      int i = 0;
+      for (; i + 8 <= nb; i += 8) {
+        float pv[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) pv[u] = pooled[int64_t(b0 + i + u) * C + c];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) s = fmaf(dla[i + u][n], pv[u], s);
+      }
+      for (; i < nb; ++i) s = fmaf(dla[i][n], pooled[int64_t(b0 + i) * C + c], s);
     }
-    for (int e = tid; e < N * C; e += kT) {
-      const int n = e / C, c = e - n * C;
-      float s = b0 == 0 ? 0.f : ldw<TW>(dw, e);
-      for (int i = 0; i < nb; ++i) s = fmaf(dla[i][n], pooled[int64_t(b0 + i) * C + c], s);
-      if constexpr (sizeof(TW) == 4)
-        dw[e] = s;
-      else
-        dw[e] = f32_to_bf16(s);
-    }
+    if (b == B && tid < N)
+      for (int i = 0; i < nb; ++i) sb += dla[i][tid];
   }
+  if (live) {
+    if constexpr (sizeof(TW) == 4)
+      dw[e] = s;
+    else
+      dw[e] = f32_to_bf16(s);
+  }
+  if (b == B && tid < N) db[tid] = sb;
 }
 
 }  // namespace p2head
@@ -196,10 +216,10 @@ void head_bwd(const float* gloss, const float* logits, const int64_t* y, const f
               uint16_t* df, void* dw, float* db, int B, int HW, int C, int N, hipStream_t s) {
   using namespace p2head;
   if (w_bf16)
-    hipLaunchKernelGGL(head_bwd_kernel<uint16_t>, dim3(B + 1), dim3(kT), 0, s, gloss, logits, y, pooled,
+    hipLaunchKernelGGL(head_bwd_kernel<uint16_t>, dim3(B + (N * C + kT - 1) / kT), dim3(kT), 0, s, gloss, logits, y, pooled,
                        static_cast<const uint16_t*>(w), df, static_cast<uint16_t*>(dw), db, B, HW, C, N);
   else
-    hipLaunchKernelGGL(head_bwd_kernel<float>, dim3(B + 1), dim3(kT), 0, s, gloss, logits, y, pooled,
+    hipLaunchKernelGGL(head_bwd_kernel<float>, dim3(B + (N * C + kT - 1) / kT), dim3(kT), 0, s, gloss, logits, y, pooled,
                        static_cast<const float*>(w), df, static_cast<float*>(dw), db, B, HW, C, N);
 }
 
