@@ -167,10 +167,33 @@ __global__ __launch_bounds__(256) void adam_mt_kernel(float* __restrict__ p, flo
     // slab of an output channel is L2-resident while its block runs)
     const uint32_t C = cl_c(T.flags), HW = cl_hw(T.flags);
     uint16_t* SB = shadow ? pbf + T.off : nullptr;
-    for (int64_t i = threadIdx.x; i < len; i += 256) {
-      const uint32_t j = cl_index(uint32_t(start + i), C, HW);
-      adam_elem(P[i], load_grad1(g, gbf, j), M[i], V[i], h);
-      if (SB) SB[j] = f32_to_bf16(P[i]);
+    // 4 elements per thread in flight (state loads + gradient gathers issued
+    // together): one dependent round trip per element made this loop latency-bound
+    for (int64_t i0 = threadIdx.x; i0 < len; i0 += 4 * 256) {
+      float pv[4], gv[4], mv[4], vv[4];
+      uint32_t j[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int64_t i = i0 + u * 256;
+        if (i < len) {
+          j[u] = cl_index(uint32_t(start + i), C, HW);
+          pv[u] = P[i];
+          mv[u] = M[i];
+          vv[u] = V[i];
+          gv[u] = load_grad1(g, gbf, j[u]);
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int64_t i = i0 + u * 256;
+        if (i < len) {
+          adam_elem(pv[u], gv[u], mv[u], vv[u], h);
+          P[i] = pv[u];
+          M[i] = mv[u];
+          V[i] = vv[u];
+          if (SB) SB[j[u]] = f32_to_bf16(pv[u]);
+        }
+      }
     }
     return;
   }
@@ -199,6 +222,17 @@ __global__ __launch_bounds__(256) void adam_mt_kernel(float* __restrict__ p, flo
   }
 }
 
+// register form (a pointer to a local would put the momentum on the stack)
+P2_DEVICE float sgd_regs(float& p, float g, float& b, bool has_b, const SgdParams& h) {
+  if (h.weight_decay != 0.f) g = fmaf(h.weight_decay, p, g);
+  if (has_b) {
+    b = h.first_step ? g : fmaf(h.momentum, b, (1.f - h.dampening) * g);
+    g = h.nesterov ? fmaf(h.momentum, b, g) : b;
+  }
+  p = fmaf(-h.lr, g, p);
+  return p;
+}
+
 P2_DEVICE float sgd_elem(float& p, float g, float* b, const SgdParams& h) {
   if (h.weight_decay != 0.f) g = fmaf(h.weight_decay, p, g);
   if (b) {
@@ -223,17 +257,56 @@ __global__ __launch_bounds__(256) void sgd_mt_kernel(float* __restrict__ p, floa
   float* P = p + T.off + start;
   float* B = buf ? buf + T.off + start : nullptr;
   uint16_t* PB = shadow ? pbf + T.off + start : nullptr;
-  if (T.flags & kMTPermCL) {  // see adam_mt_kernel
+  if (T.flags & kMTPermCL) {  // see adam_mt_kernel (4 elements per thread in flight)
     const uint32_t C = cl_c(T.flags), HW = cl_hw(T.flags);
     uint16_t* SB = shadow ? pbf + T.off : nullptr;
-    for (int64_t i = threadIdx.x; i < len; i += 256) {
-      const uint32_t j = cl_index(uint32_t(start + i), C, HW);
-      const float np = sgd_elem(P[i], load_grad1(g, gbf, j), B ? B + i : nullptr, h);
-      if (SB) SB[j] = f32_to_bf16(np);
+    for (int64_t i0 = threadIdx.x; i0 < len; i0 += 4 * 256) {
+      float pv[4], gv[4], bv[4];
+      uint32_t j[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int64_t i = i0 + u * 256;
+        if (i < len) {
+          j[u] = cl_index(uint32_t(start + i), C, HW);
+          pv[u] = P[i];
+          bv[u] = B ? B[i] : 0.f;
+          gv[u] = load_grad1(g, gbf, j[u]);
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int64_t i = i0 + u * 256;
+        if (i < len) {
+          const float np = sgd_regs(pv[u], gv[u], bv[u], B != nullptr, h);
+          P[i] = np;
+          if (B) B[i] = bv[u];
+          if (SB) SB[j[u]] = f32_to_bf16(np);
+        }
+      }
     }
     return;
   }
-  for (int64_t i = threadIdx.x; i < len; i += 256) {
+  // contiguous tensors: 16-B vectors, as adam_mt_kernel
+  const int64_t len4 = (reinterpret_cast<uintptr_t>(P) & 15) == 0 ? (len & ~int64_t(3)) : 0;
+  for (int64_t i = int64_t(threadIdx.x) * 4; i < len4; i += 256 * 4) {
+    float gg[4];
+    load_grad4(g, gbf, start + i, gg);
+    float4 pp = *reinterpret_cast<float4*>(P + i);
+    float4 bb = B ? *reinterpret_cast<float4*>(B + i) : float4{0.f, 0.f, 0.f, 0.f};
+    sgd_regs(pp.x, gg[0], bb.x, B != nullptr, h);
+    sgd_regs(pp.y, gg[1], bb.y, B != nullptr, h);
+    sgd_regs(pp.z, gg[2], bb.z, B != nullptr, h);
+    sgd_regs(pp.w, gg[3], bb.w, B != nullptr, h);
+    *reinterpret_cast<float4*>(P + i) = pp;
+    if (B) *reinterpret_cast<float4*>(B + i) = bb;
+    if (PB) {
+      uint2 o;
+      o.x = pack_bf16x2(pp.x, pp.y);
+      o.y = pack_bf16x2(pp.z, pp.w);
+      *reinterpret_cast<uint2*>(PB + i) = o;
+    }
+  }
+  for (int64_t i = len4 + threadIdx.x; i < len; i += 256) {
     const float np = sgd_elem(P[i], load_grad1(g, gbf, start + i), B ? B + i : nullptr, h);
     if (PB) PB[i] = f32_to_bf16(np);
   }
