@@ -288,10 +288,12 @@ void init_fwd_attributes() {}
 
 void conv2_fwd(const uint16_t* p1, const uint16_t* w2r, const float* params, Offsets off, uint16_t* a1,
                uint8_t* am2, int B, hipStream_t s) {
-  // P2CNN_CONV2_FWD_LDS=0: the per-wave streaming kernel (A/B measurement knob, read once)
+  // P2CNN_CONV2_FWD_LDS=1: the LDS-staged kernel -- measured slower, 8.2 vs 6.0 us
+  // (scripts/kbench.py, round 4): staging everything before the first MFMA
+  // serialises what the 448 streaming waves overlap.  Kept as a measured arm.
   static const bool lds = [] {
     const char* e = getenv("P2CNN_CONV2_FWD_LDS");
-    return !e || atoi(e) != 0;
+    return e && atoi(e) != 0;
   }();
   if (lds)
     hipLaunchKernelGGL(conv2_fwd_lds_kernel, dim3(2, B), dim3(448), 0, s, p1, w2r, params + off.c2b, a1, am2);

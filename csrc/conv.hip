@@ -24,6 +24,8 @@
 // (/root/reference/p2pfl/learning/pytorch/mnist_examples/models/cnn.py:55-62);
 // the ResNet targets are BASELINE.json configs 3 and 5.
 #include "conv.h"
+#include <cstdlib>
+
 #include "gemm_core.h"
 
 namespace p2gemm {
@@ -183,7 +185,13 @@ static void launch_t(const GemmParams& p, const LA& la, const LB& lb, hipStream_
 
 // the BatchNorm-statistics instantiation only where a launch asks for it
 template <class LA, class LB>
-static void launch(const GemmParams& p, const LA& la, const LB& lb, hipStream_t s) {
+static void launch(const GemmParams& p0, const LA& la, const LB& lb, hipStream_t s) {
+  static const int bn_mode = [] {
+    const char* e = getenv("P2_BN_EPI_MODE");
+    return e ? atoi(e) : 0;
+  }();
+  GemmParams p = p0;
+  p.bn.mode = bn_mode;
   if (p.bn.part)
     launch_t<LA, LB, true>(p, la, lb, s);
   else

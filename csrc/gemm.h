@@ -50,6 +50,10 @@ struct BnEpi {
   const float* brstd;
   float* dw;
   float* db;
+  // measurement knob (P2_BN_EPI_MODE, read once by the conv launcher): 0 = full
+  // epilogue; 1 = per-tile statistics only (no cross-tile reduction: outputs are
+  // not finalized); 2 = statistics + partial stores + first-level ticket only
+  int mode;
 };
 
 struct GemmParams {

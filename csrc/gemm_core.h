@@ -326,6 +326,7 @@ P2_DEVICE void bn_epilogue_reduce(const GemmParams& p, Moments mo, int tm, int t
   int* flag = reinterpret_cast<int*>(smem);
   auto tile_rows = [&](int t) { return float(min(CFG::BM, p.M - t * CFG::BM)); };
   if (!last_arrival(e.cnt + tn * (groups + 1) + g, gsize, flag)) return;
+  if (e.mode == 2) return;
   // level 1: combine the group's tile partials in tile order
   Moments acc{0.f, 0.f, 0.f};
   if (col) {
@@ -743,7 +744,7 @@ P2_DEVICE void gemm_body(const GemmParams& p, const LA& la, const LB& lb, int ti
       }
     }
     __syncthreads();
-    bn_epilogue_reduce<CFG>(p, mo, tm, tn, tiles_m, smem);
+    if (e.mode != 1) bn_epilogue_reduce<CFG>(p, mo, tm, tn, tiles_m, smem);
     __syncthreads();  // the bf16 staging below reuses the LDS
   }
   // bias, GELU (+ pre-activation, stored directly), residual: in place on acc

@@ -46,9 +46,10 @@ _MERGED_ADAM = os.environ.get("P2PFL_CNN_MERGED_ADAM", "1") != "0"
 # selects the W1^T-shadow kernel.
 _ROUTE_RM = os.environ.get("P2PFL_CNN_ROUTE_RM", "1") != "0"
 # dA1 routing split over 2 K-slices per feature tile (196 workgroups instead of
-# 98, the last slice to arrive reduces; csrc/cnn_bwd.hip route_rm_kernel);
-# "0" keeps one workgroup per tile.
-_ROUTE_SPLIT = os.environ.get("P2PFL_CNN_ROUTE_SPLIT", "1") != "0"
+# 98, the last slice to arrive reduces; csrc/cnn_bwd.hip route_rm_kernel).  Off:
+# measured 17.2 us vs 7.5 us unsplit (scripts/kbench.py, MI355X, round 4) -- the
+# cross-CU hand-off costs more than the halved per-workgroup stream saves.
+_ROUTE_SPLIT = os.environ.get("P2PFL_CNN_ROUTE_SPLIT", "0") == "1"
 _NAMES = ("conv1.weight", "conv1.bias", "conv2.weight", "conv2.bias", "l1.weight", "l1.bias", "l2.weight", "l2.bias")
 FEAT, HID = 3136, 2048
 
