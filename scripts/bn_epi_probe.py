@@ -38,7 +38,7 @@ def main():
     res = {"mode": int(os.environ.get("P2_BN_EPI_MODE", "0"))}
     for C, HW in ((64, 32), (128, 16), (256, 8), (512, 4)):
         x4 = torch.randn(32, HW, HW, C, device=dev).to(torch.bfloat16)
-        w = (torch.randn(C, C, 3, 3, device=dev) * 0.05).to(torch.bfloat16)
+        w = (torch.randn(C, C, 3, 3, device=dev) * 0.05).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
         w4 = w.permute(0, 2, 3, 1)
         bw, bb = torch.ones(C, device=dev), torch.zeros(C, device=dev)
         rm, rv = torch.zeros(C, device=dev), torch.ones(C, device=dev)
