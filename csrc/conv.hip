@@ -165,13 +165,13 @@ struct ConvWgradB {
   }
 };
 
-template <int NBUF, class LA, class LB, bool BN>
+template <int NBUF, class LA, class LB, int BN>
 __global__ __launch_bounds__(NT, NBUF == 1 ? 3 : (NBUF == 2 ? 2 : 1)) void conv_kernel(GemmParams p, LA la, LB lb, int tiles_m, int tiles_n) {
   __shared__ __attribute__((aligned(16))) char smem[smem_bytes<Tile128, NBUF>()];
   gemm_body<Tile128, NBUF, LA, LB, BN>(p, la, lb, tiles_m, tiles_n, smem);
 }
 
-template <class LA, class LB, bool BN>
+template <class LA, class LB, int BN>
 static void launch_t(const GemmParams& p, const LA& la, const LB& lb, hipStream_t s) {
   int tm, tn;
   const int grid = gemm_grid<Tile128>(p, tm, tn);
@@ -183,8 +183,9 @@ static void launch_t(const GemmParams& p, const LA& la, const LB& lb, hipStream_
     hipLaunchKernelGGL((conv_kernel<2, LA, LB, BN>), dim3(grid), dim3(NT), 0, s, p, la, lb, tm, tn);
 }
 
-// the BatchNorm-statistics instantiation only where a launch asks for it
-template <class LA, class LB>
+// the BatchNorm-statistics instantiation only where a launch asks for it; BNK: the
+// statistics direction this product can carry (1 forward, 2 input gradient, 0 none)
+template <int BNK, class LA, class LB>
 static void launch(const GemmParams& p0, const LA& la, const LB& lb, hipStream_t s) {
   static const int bn_mode = [] {
     const char* e = getenv("P2_BN_EPI_MODE");
@@ -192,10 +193,13 @@ static void launch(const GemmParams& p0, const LA& la, const LB& lb, hipStream_t
   }();
   GemmParams p = p0;
   p.bn.mode = bn_mode;
-  if (p.bn.part)
-    launch_t<LA, LB, true>(p, la, lb, s);
-  else
-    launch_t<LA, LB, false>(p, la, lb, s);
+  if constexpr (BNK != 0) {
+    if (p.bn.part) {
+      launch_t<LA, LB, BNK>(p, la, lb, s);
+      return;
+    }
+  }
+  launch_t<LA, LB, 0>(p, la, lb, s);
 }
 
 static GemmParams base_params(int M, int N, int K, void* c, int64_t ldc, int c_bf16, const p2::SplitK& k,
@@ -249,7 +253,7 @@ void conv_fwd(const ConvShape& s, const uint16_t* x, const uint16_t* w, void* y,
   GemmParams p = base_params(M, s.O, K, y, s.O, k.splits <= 1 || k.counters, k, variant);
   if (bn) p.bn = *bn;
   const ConvFwdA la{x, make_fastdiv(s.OH * s.OW), make_fastdiv(s.OW), M, s.H, s.W, s.C, s.stride, s.pad, s.dil, s.kw};
-  launch(p, la, PlainK{w, K, s.O, K}, st);
+  launch<1>(p, la, PlainK{w, K, s.O, K}, st);
 }
 
 void conv_dgrad(const ConvShape& s, const uint16_t* dy, const uint16_t* w, void* dx, const SplitK& k, int variant,
@@ -259,7 +263,7 @@ void conv_dgrad(const ConvShape& s, const uint16_t* dy, const uint16_t* w, void*
   GemmParams p = base_params(M, s.C, K, dx, s.C, k.splits <= 1 || k.counters, k, variant);
   if (bn) p.bn = *bn;
   const ConvDgradA la{dy, make_fastdiv(s.H * s.W), make_fastdiv(s.W), M, s.OH, s.OW, s.O, s.stride, s.pad, s.dil, s.kw};
-  launch(p, la, ConvDgradB{w, s.C, s.O, s.kh * s.kw}, st);
+  launch<2>(p, la, ConvDgradB{w, s.C, s.O, s.kh * s.kw}, st);
 }
 
 void conv_wgrad(const ConvShape& s, const uint16_t* dy, const uint16_t* x, void* out, int out_bf16, const SplitK& k,
@@ -270,7 +274,7 @@ void conv_wgrad(const ConvShape& s, const uint16_t* dy, const uint16_t* x, void*
       base_params(s.O, ncols, npix, out, ncols, (k.splits > 1 && !k.counters) ? 0 : out_bf16, k, variant);
   const ConvWgradB lb{x,   make_fastdiv(s.OH * s.OW), make_fastdiv(s.OW), make_fastdiv(s.C), npix, s.H, s.W, s.C,
                       s.stride, s.pad, s.dil, s.kw, ncols};
-  launch(p, PlainMN{dy, s.O, s.O, npix}, lb, st);
+  launch<0>(p, PlainMN{dy, s.O, s.O, npix}, lb, st);
 }
 
 void slab_sum(const float* slabs, int splits, int64_t n, void* out, int out_bf16, hipStream_t st) {

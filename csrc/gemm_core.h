@@ -309,10 +309,9 @@ constexpr int kBnGroup = 16;  // tile rows per first-level group
 
 // The tile's column moments (`mo`, held by threads tid < BN for column n0 + tid)
 // go out as this tile's partial; the two-level reduction finalizes the columns.
-template <class CFG>
+template <class CFG, bool bwd>
 P2_DEVICE void bn_epilogue_reduce(const GemmParams& p, Moments mo, int tm, int tn, int tiles_m, char* smem) {
   const BnEpi& e = p.bn;
-  const bool bwd = e.bx != nullptr;
   const int tid = threadIdx.x, N = p.N, n0 = tn * CFG::BN;
   const int groups = (tiles_m + kBnGroup - 1) / kBnGroup, g = tm / kBnGroup;
   const int gsize = min(kBnGroup, tiles_m - g * kBnGroup);
@@ -398,7 +397,7 @@ P2_DEVICE void bn_epilogue_reduce(const GemmParams& p, Moments mo, int tm, int t
 // The whole kernel body.  `p` carries M/N/K, split-K and the epilogue.
 // BN: compile the BatchNorm statistics epilogue in (GemmParams::bn; the conv
 // kernels that produce a BN input instantiate it, the Linear GEMMs do not)
-template <class CFG, int NBUF, class LA, class LB, bool BN = false>
+template <class CFG, int NBUF, class LA, class LB, int BN = 0>
 P2_DEVICE void gemm_body(const GemmParams& p, const LA& la, const LB& lb, int tiles_m, int tiles_n, char* smem) {
   constexpr int FM = CFG::FM, FN = CFG::FN, HA = CFG::HA, HB = CFG::HB, G = CFG::GROUPS;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -651,35 +650,48 @@ P2_DEVICE void gemm_body(const GemmParams& p, const LA& la, const LB& lb, int ti
   }
   // BatchNorm statistics (p.bn) of this tile, from the accumulators: each lane
   // holds 4 consecutive columns x FM rows per (j, g); the bf16-rounded values (what
-  // is stored) are summed over the lane's rows, then over the 32 lanes of its half
-  // wave (xor shuffles), then over the WAVES_M waves sharing the columns (LDS, fixed
-  // order).  Forward: sums shifted by the tile's first row (one value per column,
-  // broadcast) -> (count, mean, M2); backward: dz' = dz (bn output > 0) and
-  // dz' (x - mean) from the BN's input / output tensors, read in the accumulator
-  // layout (8-byte vectors).
-  if (BN && p.bn.part != nullptr) {
+  // is stored) are summed over the lane's rows, then lanes r and r ^ 16 are added
+  // (one independent shuffle per value), the 16 row-pair partials of every column
+  // go through LDS and one thread per (wave row, column) adds them in fixed order;
+  // the WAVES_M wave rows sharing a column are merged last.  (A 5-step xor-shuffle
+  // tree per value was 352 dependent LDS-crossbar round trips per wave: +12 us per
+  // launch, scripts/bn_epi_probe.py.)  Forward: sums shifted by the column's value
+  // in the wave's first row (v_readlane, no LDS) -> (count, mean, M2); backward:
+  // dz' = dz (bn output > 0) and dz' (x - mean) from the BN's input / output
+  // tensors, read in the accumulator layout (8-byte vectors).
+  if (BN && p.bn.part != nullptr && p.bn.mode != 3) {
     const BnEpi& e = p.bn;
-    const bool bwd = e.bx != nullptr;
+    constexpr bool bwd = BN == 2;  // compiled per direction: no runtime branches on it
     const int h = lane >> 5;
     const int mrow0 = m0 + wm * 32 * FM;  // first row of this wave
-    __syncthreads();  // LDS free (main loop done)
-    float* red = reinterpret_cast<float*>(smem);  // [WAVES_M][BN] x (shift, s1, s2)
-    // one (j, g) group of 4 columns at a time: few live registers (the single-buffer
-    // conv kernels run at 168 VGPRs)
+    constexpr int CW = CFG::WAVES_N * 32;  // columns of one pass (one j per wave)
+    float* s1p = reinterpret_cast<float*>(smem);          // [WAVES_M][16][CW]
+    float* s2p = s1p + CFG::WAVES_M * 16 * CW;            // [WAVES_M][16][CW]
+    float* shp = s2p + CFG::WAVES_M * 16 * CW;            // [WAVES_M][CW]
+    static_assert((2 * 16 + 1) * CFG::WAVES_M * CW * 4 <= smem_bytes<CFG, NBUF>(), "BN pass buffers fit the LDS");
+    static_assert(CFG::WAVES_M * CFG::BN * 3 * 4 <= smem_bytes<CFG, NBUF>(), "BN merge buffer fits the LDS");
+    float keep[FN][3];
 #pragma unroll
-    for (int j = 0; j < FN; ++j)
+    for (int j = 0; j < FN; ++j) {
+      float s1[4][4], s2[4][4], sh[4][4];
 #pragma unroll
       for (int g = 0; g < 4; ++g) {
         const int n = n0 + wn * 32 * FN + j * 32 + 8 * g + 4 * h;
         const bool ncol = n < p.N;
-        float mu[4] = {0.f, 0.f, 0.f, 0.f}, sh[4], s1[4] = {0.f, 0.f, 0.f, 0.f}, s2[4] = {0.f, 0.f, 0.f, 0.f};
+        float mu[4] = {0.f, 0.f, 0.f, 0.f};
         if (bwd && ncol) {
           const f32x4 mv = *reinterpret_cast<const f32x4*>(e.bmean + n);
           mu[0] = mv[0], mu[1] = mv[1], mu[2] = mv[2], mu[3] = mv[3];
         }
 #pragma unroll
-        for (int q = 0; q < 4; ++q)  // forward shift: the column's value in the wave's first row
-          sh[q] = bwd ? 0.f : __shfl(bf16_to_f32(f32_to_bf16(acc[0][j][4 * g + q])), lane & 32, 64);
+        for (int q = 0; q < 4; ++q) {
+          s1[g][q] = 0.f;
+          s2[g][q] = 0.f;
+          const int v0 = __float_as_int(bf16_to_f32(f32_to_bf16(acc[0][j][4 * g + q])));
+          const float a = __int_as_float(__builtin_amdgcn_readlane(v0, 0));
+          const float b = __int_as_float(__builtin_amdgcn_readlane(v0, 32));
+          sh[g][q] = bwd ? 0.f : (h ? b : a);
+        }
 #pragma unroll
         for (int i = 0; i < FM; ++i) {
           const int m = mrow0 + i * 32 + (lane & 31);
@@ -701,33 +713,62 @@ P2_DEVICE void gemm_body(const GemmParams& p, const LA& la, const LB& lb, int ti
             const float v = bf16_to_f32(f32_to_bf16(acc[i][j][4 * g + q]));
             if (bwd) {
               const float gz = yv[q] > 0.f ? v : 0.f;
-              s1[q] += gz;
-              s2[q] = fmaf(gz, xv[q] - mu[q], s2[q]);
+              s1[g][q] += gz;
+              s2[g][q] = fmaf(gz, xv[q] - mu[q], s2[g][q]);
             } else {
-              const float d = v - sh[q];
-              s1[q] += d;
-              s2[q] = fmaf(d, d, s2[q]);
+              const float d = v - sh[g][q];
+              s1[g][q] += d;
+              s2[g][q] = fmaf(d, d, s2[g][q]);
             }
           }
         }
-        // sum over the 32 rows of the half wave (lanes sharing h)
+      }
+      // rows r and r ^ 16 of each column: 32 independent shuffles, one wait
 #pragma unroll
-        for (int off = 1; off < 32; off <<= 1)
+      for (int g = 0; g < 4; ++g)
 #pragma unroll
-          for (int q = 0; q < 4; ++q) {
-            s1[q] += __shfl_xor(s1[q], off, 64);
-            s2[q] += __shfl_xor(s2[q], off, 64);
-          }
-        if ((lane & 31) == 0) {
+        for (int q = 0; q < 4; ++q) {
+          s1[g][q] += __shfl_xor(s1[g][q], 16, 64);
+          s2[g][q] += __shfl_xor(s2[g][q], 16, 64);
+        }
+      __syncthreads();  // LDS free (main loop, or the previous pass's reads)
+      if ((lane & 16) == 0) {
+        const int r16 = lane & 15;
 #pragma unroll
-          for (int q = 0; q < 4; ++q) {
-            float* dst = red + (wm * CFG::BN + (n - n0) + q) * 3;
-            dst[0] = sh[q];
-            dst[1] = s1[q];
-            dst[2] = s2[q];
-          }
+        for (int g = 0; g < 4; ++g) {
+          const int c = wn * 32 + 8 * g + 4 * h;
+          *reinterpret_cast<f32x4*>(s1p + (wm * 16 + r16) * CW + c) = f32x4{s1[g][0], s1[g][1], s1[g][2], s1[g][3]};
+          *reinterpret_cast<f32x4*>(s2p + (wm * 16 + r16) * CW + c) = f32x4{s2[g][0], s2[g][1], s2[g][2], s2[g][3]};
+          if (r16 == 0)
+            *reinterpret_cast<f32x4*>(shp + wm * CW + c) = f32x4{sh[g][0], sh[g][1], sh[g][2], sh[g][3]};
         }
       }
+      __syncthreads();
+      if (tid < CFG::WAVES_M * CW) {
+        const int w = tid / CW, c = tid % CW;
+        float a1 = 0.f, a2 = 0.f;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          a1 += s1p[(w * 16 + r) * CW + c];
+          a2 += s2p[(w * 16 + r) * CW + c];
+        }
+        keep[j][0] = shp[w * CW + c];
+        keep[j][1] = a1;
+        keep[j][2] = a2;
+      }
+    }
+    __syncthreads();  // pass buffers dead -> merge buffer
+    float* red = reinterpret_cast<float*>(smem);  // [WAVES_M][BN] x (shift, s1, s2)
+    if (tid < CFG::WAVES_M * CW) {
+      const int w = tid / CW, c = tid % CW, wcol = c / 32, cc = c % 32;
+#pragma unroll
+      for (int j = 0; j < FN; ++j) {
+        float* dst = red + (w * CFG::BN + wcol * 32 * FN + j * 32 + cc) * 3;
+        dst[0] = keep[j][0];
+        dst[1] = keep[j][1];
+        dst[2] = keep[j][2];
+      }
+    }
     __syncthreads();
     Moments mo{0.f, 0.f, 0.f};
     if (tid < CFG::BN) {
@@ -744,7 +785,7 @@ P2_DEVICE void gemm_body(const GemmParams& p, const LA& la, const LB& lb, int ti
       }
     }
     __syncthreads();
-    if (e.mode != 1) bn_epilogue_reduce<CFG>(p, mo, tm, tn, tiles_m, smem);
+    if (e.mode != 1) bn_epilogue_reduce<CFG, bwd>(p, mo, tm, tn, tiles_m, smem);
     __syncthreads();  // the bf16 staging below reuses the LDS
   }
   // bias, GELU (+ pre-activation, stored directly), residual: in place on acc
