@@ -32,9 +32,15 @@ from p2pfl_amd.ops.splitk import counters, slab_elems, tiles_of
 
 # counters a test can read to prove the native path ran
 STATS = {"native_fwd": 0, "torch_fwd": 0, "gemm_1x1_fwd": 0, "stem_fwd": 0, "native_fwd_bn": 0, "bn_act_conv": 0}
-# training BatchNorm statistics computed by the producing convolution's launch
-# (conv_bn_act); P2PFL_CONV_BN_STATS=0 keeps the separate BN statistics passes
-_FUSED_BN = os.environ.get("P2PFL_CONV_BN_STATS", "1") != "0"
+# Training BatchNorm statistics computed by the producing convolution's launch
+# (conv_bn_act, csrc/gemm_core.h BnEpi) -- opt-in (P2PFL_CONV_BN_STATS=1).  Off by
+# default because it measures slower than the separate statistics + finalize
+# launches: per launch the per-tile statistics add ~6.5 us and the cross-workgroup
+# reduction (two last-arriver levels, each a ~2-3 us dependent hand-off between
+# CUs) ~14.5 us, and its split-K must reduce in the launch (+6-12 us on the
+# 16x16 / 8x8 / 4x4 stages), against ~9.6 us for the two separate launches
+# (scripts/bn_epi_probe.py; ResNet-18 round 59.9 vs 49.8 ms; profiles/r4_bn_epilogue.md).
+_FUSED_BN = os.environ.get("P2PFL_CONV_BN_STATS", "0") == "1"
 
 # "native" | "library" | "auto" (measured per shape, ops/autotune.py); env P2PFL_NATIVE_CONV
 _POLICY = autotune.policy("P2PFL_NATIVE_CONV")

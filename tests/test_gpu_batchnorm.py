@@ -218,6 +218,7 @@ def test_conv_bn_act_statistics_epilogue_vs_fp32(monkeypatch, N, C, H, W, O, s, 
 
     ops.ext()
     monkeypatch.setattr(conv_ops, "_POLICY", "native")
+    monkeypatch.setattr(conv_ops, "_FUSED_BN", True)  # the epilogue under test (off by default: slower)
     g = torch.Generator(device="cuda").manual_seed(N * 7 + O)
     x = _cl(torch.randn(N, C, H, W, device="cuda", generator=g)).to(torch.bfloat16).requires_grad_(True)
     conv = nn.Conv2d(C, O, 3, s, 1, bias=False).cuda()
@@ -255,6 +256,7 @@ def test_conv_bn_statistics_are_deterministic_and_counters_reset(monkeypatch):
     from p2pfl_amd.ops import conv as conv_ops
 
     ops.ext()
+    monkeypatch.setattr(conv_ops, "_FUSED_BN", True)
     monkeypatch.setattr(conv_ops, "_POLICY", "native")
     x = _cl(torch.randn(32, 64, 32, 32, device="cuda")).to(torch.bfloat16)
     conv = nn.Conv2d(64, 64, 3, 1, 1, bias=False).cuda()
