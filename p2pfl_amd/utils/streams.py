@@ -7,44 +7,25 @@ two learners can silently share one HIP stream.  An event one peer records on
 the shared stream while the other captures a HIP graph on it becomes a node of
 that capture and every later use of it fails (``hipErrorCapturedEvent``;
 ``tests/test_gpu_node.py::test_virtual_peers_on_gpu``).  :func:`private_stream`
-creates a stream of its own through the extension and destroys it when the
-returned wrapper is collected.
+creates a stream of its own through the extension; it lives until the process
+exits.
 """
 
 from __future__ import annotations
 
 import threading
-import weakref
 
 import torch
 
 
-# Streams are never created or destroyed while another thread records a HIP graph:
-# a finalizer (which runs inside whatever thread's garbage collection happens to
-# fire) only queues the handle, and creation drains the queue under the shared
-# device gate, which a capture holds exclusively (learning/step_graph.py).
-_PENDING: list = []
-_PENDING_LOCK = threading.Lock()
-
-
-def _destroy(handle: int) -> None:
-    with _PENDING_LOCK:
-        _PENDING.append(handle)
-
-
-def _drain() -> None:
-    with _PENDING_LOCK:
-        handles = _PENDING[:]
-        del _PENDING[:]
-    if not handles:
-        return
-    from p2pfl_amd.ops import ext
-
-    for h in handles:
-        try:
-            ext().destroy_stream(h)
-        except Exception:
-            pass
+# Private streams live until the process exits: nothing destroys them.  Destroying a
+# stream while PyTorch still knows its handle is unsafe -- the caching allocator keeps
+# recorded stream uses of freed blocks, and a graph keeps the stream it was captured on
+# -- and the suite's exit crashed in the finalizer pass (weakref._exitfunc, SIGSEGV)
+# while a destroy-on-collect scheme was in place.  A process creates a bounded number
+# (a few per learner); the HIP runtime releases them at exit.
+_STREAMS: list = []
+_LOCK = threading.Lock()
 
 
 def private_stream(device: torch.device) -> torch.cuda.Stream:
@@ -54,9 +35,10 @@ def private_stream(device: torch.device) -> torch.cuda.Stream:
 
     device = torch.device(device)
     idx = device.index if device.index is not None else torch.cuda.current_device()
+    # created under the shared device gate: never while another thread records a graph
     with GATE.shared():
-        _drain()
         handle = int(ext().new_stream(idx))
     s = torch.cuda.ExternalStream(handle, device=torch.device("cuda", idx))
-    weakref.finalize(s, _destroy, handle)
+    with _LOCK:
+        _STREAMS.append(s)
     return s
