@@ -1,12 +1,14 @@
 """``models_ready`` (reference ``commands/models_ready_command.py:26-63``).
 
-Accepts the current or the previous round and records the *local* round for
-the sender (reference quirk Q12, preserved).  With
-``Settings.ASYNC_DIFFUSION`` a node may already train round r+1 when a
-neighbour's "ready for round r" arrives; recording the local round there
-would mark the neighbour as up to date and stop the diffusion it still
-needs, so that mode records the round the neighbour actually reported (the
-highest seen, any round up to the local one).
+Records, for the sender, the round it reported ready (the highest seen, any
+round up to the local one).  The reference records the *local* round instead
+(quirk Q12): a neighbour's "ready for round r - 1" arriving at a node already in
+round r then marks that neighbour up to date, the node's diffusion of its round-r
+aggregate skips it, and the neighbour -- still waiting in round r for this node's
+contribution -- hangs until AGGREGATION_TIMEOUT and aggregates without it (observed
+in ``tests/test_gpu_fused_cnn.py::test_three_fused_peers_in_one_process``: one peer
+finished round 1 three seconds before the others, which then ended round 2 with
+different models).  Recording the reported round lets the diffusion reach it.
 """
 
 from __future__ import annotations
@@ -31,15 +33,10 @@ class ModelsReadyCommand(Command):
         if r is None:
             logger.warning(self.state.addr, "Models ready received when learning is not running")
             return
-        if Settings.ASYNC_DIFFUSION:
-            if round <= r:
-                self.state.nei_status[source] = max(self.state.nei_status.get(source, -1), round)
-                self.state.changed.bump()
-            else:
-                logger.debug(self.state.addr, f"Models ready from {source} for round {round} ahead of ours ({r}).")
-            return
-        if round in (r - 1, r):
-            self.state.nei_status[source] = r
+        if round <= r and (Settings.ASYNC_DIFFUSION or round >= r - 1):
+            self.state.nei_status[source] = max(self.state.nei_status.get(source, -1), round)
             self.state.changed.bump()
+        elif round > r:
+            logger.debug(self.state.addr, f"Models ready from {source} for round {round} ahead of ours ({r}).")
         else:
             logger.error(self.state.addr, f"Models ready from {source} in a late round. Ignored. {round} != {r} / {r - 1}")
