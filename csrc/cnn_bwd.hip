@@ -426,9 +426,9 @@ void route_fc2(const uint16_t* dH, const uint16_t* w1t, const uint8_t* am2, int 
 // ---------------------------------------------------------------------------
 template <int MR>
 struct Fc1Lds {
-  static constexpr int P = MR + 8;
+  static constexpr int AP = 144;  // bf16 pitch of the staged A1 rows (288 B: conflict-free transpose reads)
   static constexpr int GP = 132;  // fp32 pitch of the gradient tile
-  static constexpr int kStage = (32 + 128) * P * 2;
+  static constexpr int kStage = MR * (32 + AP) * 2;  // dH rows [MR][32] | A1 rows [MR][AP]
   static constexpr int kGrad = 32 * GP * 4;
   static constexpr int kMain = kStage > kGrad ? kStage : kGrad;
   static constexpr int kBytes = kMain + 128 * 40 * 2;  // + the transposed bf16 tile
@@ -440,11 +440,15 @@ P2_DEVICE void fc1_wgrad_adam_body(int bx, int by, const uint16_t* __restrict__ 
                                    float* __restrict__ gdump, uint16_t* __restrict__ w1bf,
                                    uint16_t* __restrict__ w1tbf, const Offsets& off,
                                    const int* __restrict__ adam_t, int t_off, const AdamCfg& cfg, char* smem) {
-  constexpr int P = Fc1Lds<MR>::P;
+  constexpr int AP = Fc1Lds<MR>::AP;
   constexpr int GP = Fc1Lds<MR>::GP;
   uint16_t(*tr)[40] = reinterpret_cast<uint16_t(*)[40]>(smem + Fc1Lds<MR>::kMain);
-  uint16_t(*sdh)[P] = reinterpret_cast<uint16_t(*)[P]>(smem);
-  uint16_t(*sa1)[P] = reinterpret_cast<uint16_t(*)[P]>(smem + 32 * P * 2);
+  // dH and A1 are staged as they lie in memory (sample rows, 16-B LDS writes) and the
+  // MFMA fragments are read with the gfx950 transpose read (ds_read_b64_tr_b16): the
+  // transposed staging it replaces was 24 two-byte LDS writes per thread, 84 % of the
+  // kernel's LDS-active cycles in bank conflicts (profiles/r4_cnn_pmc.md)
+  uint16_t* sdh = reinterpret_cast<uint16_t*>(smem);  // [MR][32]  dH[b][n0 + n]
+  uint16_t* sa1 = sdh + MR * 32;                      // [MR][AP]  A1[b][kb + k]
   float(*gt)[GP] = reinterpret_cast<float(*)[GP]>(smem);
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, r = lane & 31, h = lane >> 5;
   const int n0 = by * 32;
@@ -467,35 +471,46 @@ P2_DEVICE void fc1_wgrad_adam_body(int bx, int by, const uint16_t* __restrict__ 
   }
   for (int i = tid; i < MR * 4; i += 256) {
     const int b = i >> 2, q = i & 3;
-    const uint4 u = reinterpret_cast<const uint4*>(dH + size_t(b) * kHid + n0)[q];
-    const uint16_t* e = reinterpret_cast<const uint16_t*>(&u);
-#pragma unroll
-    for (int j = 0; j < 8; ++j) sdh[q * 8 + j][b] = e[j];
+    *reinterpret_cast<uint4*>(sdh + b * 32 + q * 8) = reinterpret_cast<const uint4*>(dH + size_t(b) * kHid + n0)[q];
   }
   for (int i = tid; i < MR * 16; i += 256) {
     const int b = i >> 4, q = i & 15;
     const int k = kb + q * 8;
     uint4 u = make_uint4(0, 0, 0, 0);
     if (k < kFeat) u = reinterpret_cast<const uint4*>(a1 + size_t(b) * kFeat + k)[0];
-    const uint16_t* e = reinterpret_cast<const uint16_t*>(&u);
-#pragma unroll
-    for (int j = 0; j < 8; ++j) sa1[q * 8 + j][b] = e[j];
+    *reinterpret_cast<uint4*>(sa1 + b * AP + q * 8) = u;
   }
   __syncthreads();
   const AdamScal s = adam_scal(cfg, adam_t, t_off);
-  if (bx == 0 && wave == 0 && lane < 32) {  // FC1 bias (reads sdh before the tile reuses it)
+  if (bx == 0 && wave == 0 && lane < 32) {  // FC1 bias (reads the staged dH before the tile reuses it)
     const int n = n0 + lane;
     float g = 0.f;
-    for (int b = 0; b < MR; ++b) g += bf16_to_f32(sdh[lane][b]);
+    for (int b = 0; b < MR; ++b) g += bf16_to_f32(sdh[b * 32 + lane]);
     if (gdump) gdump[off.l1b + n] = g;
     adam_apply(p, m, v, off.l1b + n, g, cfg, s);
   }
+  // C[n][k] = sum_b dH[b][n] A1[b][k]: both fragments by transpose reads of the sample
+  // rows; one k permutation for both operands (lane half hh, substep st, j ->
+  // b = MR/2 hh + 8 st + j), so the product is the plain sum over the batch
+  const int g4 = lane >> 4, qq = (lane >> 2) & 3, c16 = 16 * (g4 & 1) + 4 * (lane & 3), hh = g4 >> 1;
   f32x16 acc = {};
 #pragma unroll
-  for (int ks = 0; ks < MR / 16; ++ks) {
-    const uint4 a = *reinterpret_cast<const uint4*>(&sdh[r][ks * 16 + 8 * h]);
-    const uint4 b = *reinterpret_cast<const uint4*>(&sa1[wave * 32 + r][ks * 16 + 8 * h]);
-    acc = mfma32b(a, b, acc);
+  for (int st = 0; st < MR / 16; ++st) {
+    uint4 a, bq;
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+      const int row = (MR / 2) * hh + 8 * st + 4 * t + qq;
+      const uint2 ua = __builtin_bit_cast(uint2, __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+          (__attribute__((address_space(3))) s16x4*)(sdh + row * 32 + c16)));
+      const uint2 ub = __builtin_bit_cast(uint2, __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+          (__attribute__((address_space(3))) s16x4*)(sa1 + row * AP + wave * 32 + c16)));
+      if (t == 0) {
+        a.x = ua.x, a.y = ua.y, bq.x = ub.x, bq.y = ub.y;
+      } else {
+        a.z = ua.x, a.w = ua.y, bq.z = ub.x, bq.w = ub.y;
+      }
+    }
+    acc = mfma32b(a, bq, acc);
   }
   __syncthreads();  // staging dead -> gradient tile
 #pragma unroll
