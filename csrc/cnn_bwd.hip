@@ -44,13 +44,21 @@ P2_DEVICE AdamScal adam_scal(const AdamCfg& c, const int* t, int t_off) {
   s.inv_sqrt_bc2 = 1.f / sqrtf(1.f - powf(c.beta2, tt));
   return s;
 }
+// m / (sqrt(v) c + eps) with the hardware square root and reciprocal (v_sqrt_f32,
+// v_rcp_f32: 1 ulp each) instead of the correctly rounded sequences (~20 VALU
+// instructions per element more: the Adam streams are issue-bound beside their
+// memory traffic, profiles/r4_cnn_pmc.md).  The update differs from the IEEE one
+// in the last bit of an lr-sized step.
+P2_DEVICE float adam_dir(float mv, float vv, float c, float eps) {
+  return mv * __builtin_amdgcn_rcpf(fmaf(__builtin_amdgcn_sqrtf(vv), c, eps));
+}
 // torch.optim.Adam semantics (L2 weight decay added to the gradient), on
 // values already in registers (lets a caller batch its loads).
 P2_DEVICE void adam_regs(float& pv, float& mv, float& vv, float g, const AdamCfg& c, const AdamScal& s) {
   if (c.weight_decay != 0.f) g = fmaf(c.weight_decay, pv, g);
   mv = fmaf(c.beta1, mv, (1.f - c.beta1) * g);
   vv = fmaf(c.beta2, vv, (1.f - c.beta2) * g * g);
-  pv -= s.step_size * (mv / (sqrtf(vv) * s.inv_sqrt_bc2 + c.eps));
+  pv -= s.step_size * adam_dir(mv, vv, s.inv_sqrt_bc2, c.eps);
 }
 // Same, loading and storing in place.
 P2_DEVICE float adam_apply(float* __restrict__ p, float* __restrict__ m, float* __restrict__ v, int64_t e, float g,
@@ -59,7 +67,7 @@ P2_DEVICE float adam_apply(float* __restrict__ p, float* __restrict__ m, float* 
   if (c.weight_decay != 0.f) g = fmaf(c.weight_decay, pv, g);
   const float mv = fmaf(c.beta1, m[e], (1.f - c.beta1) * g);
   const float vv = fmaf(c.beta2, v[e], (1.f - c.beta2) * g * g);
-  pv -= s.step_size * (mv / (sqrtf(vv) * s.inv_sqrt_bc2 + c.eps));
+  pv -= s.step_size * adam_dir(mv, vv, s.inv_sqrt_bc2, c.eps);
   p[e] = pv;
   m[e] = mv;
   v[e] = vv;
