@@ -732,6 +732,10 @@ constexpr int kDgWin = kDgWinRows * 18 * kOCP * 2;       // 36288 B
 constexpr int kDgXs = 32 * 33 * 4;                       // 4224 B
 constexpr int kDgLds = kDgW + kDgWin + kDgXs;            // 143424 B (one dgrad block per CU)
 
+// STREAM_W: the weight fragments come straight from L2 (16-B loads one 10-step chunk
+// ahead of the MFMAs) instead of the 102 KB LDS copy every block stages before its
+// first MFMA -- that copy serialised ~4 us of fetch ahead of the compute.
+template <bool STREAM_W>
 P2_DEVICE void conv2_dgrad_block(int grp, int b, const uint16_t* __restrict__ dc2m, const uint8_t* __restrict__ am1,
                                  const uint16_t* __restrict__ w2q, const uint8_t* __restrict__ xds,
                                  const int64_t* __restrict__ idx, float* __restrict__ wslab1, char* smem) {
@@ -747,13 +751,15 @@ P2_DEVICE void conv2_dgrad_block(int grp, int b, const uint16_t* __restrict__ dc
   // ---- issue every load.  W2q goes global -> LDS directly (no VGPRs): each
   // ic row (1600 elements = 3200 B) is 4 wave instructions of 50 lanes x 16 B,
   // so no instruction crosses the 16-B row padding; 32 instructions per wave.
+  if (!STREAM_W) {
 #pragma unroll 4
-  for (int k = 0; k < 32; ++k) {
-    const int id = wave * 32 + k, ic = id >> 2, q = id & 3;
-    if (lane < 50)
-      __builtin_amdgcn_global_load_lds(
-          (const __attribute__((address_space(1))) void*)(w2q + ic * (kTaps * kC2) + q * 400 + lane * 8),
-          (__attribute__((address_space(3))) void*)(sw + ic * kW2qRow + q * 400), 16, 0, 0);
+    for (int k = 0; k < 32; ++k) {
+      const int id = wave * 32 + k, ic = id >> 2, q = id & 3;
+      if (lane < 50)
+        __builtin_amdgcn_global_load_lds(
+            (const __attribute__((address_space(1))) void*)(w2q + ic * (kTaps * kC2) + q * 400 + lane * 8),
+            (__attribute__((address_space(3))) void*)(sw + ic * kW2qRow + q * 400), 16, 0, 0);
+    }
   }
   // the window (4 items of two channels x 8 columns), this lane's pool1
   // argmax codes and the image go through registers
@@ -799,14 +805,46 @@ P2_DEVICE void conv2_dgrad_block(int grp, int b, const uint16_t* __restrict__ dc
   if (!active) return;
   // ---- phase 1: C[pos][ic], 100 k-steps, both operands from LDS
   const uint16_t* abase = win + ((y - ylo) * 18 + x) * kOCP + 8 * h;
-  const uint16_t* bbase = sw + r * kW2qRow + 8 * h;
   f32x16 acc = {};
+  if (STREAM_W) {
+    // B fragment of k-step s: 16 B of ic row r at element 16 s + 8 h (row-major
+    // [ic][tap][oc] = element t * 64 + oc0); 10 steps per chunk, one chunk ahead
+    const uint16_t* brow = w2q + r * (kTaps * kC2) + 8 * h;
+    uint4 bx[10], by[10];
+#pragma unroll
+    for (int j = 0; j < 10; ++j) bx[j] = *reinterpret_cast<const uint4*>(brow + 16 * j);
+#pragma unroll
+    for (int c = 0; c < 10; c += 2) {
+      if (c + 1 < 10) {
+#pragma unroll
+        for (int j = 0; j < 10; ++j) by[j] = *reinterpret_cast<const uint4*>(brow + 16 * ((c + 1) * 10 + j));
+      }
+#pragma unroll
+      for (int j = 0; j < 10; ++j) {
+        const int s2 = c * 10 + j, t = s2 >> 2, ky = t / 5, kx = t % 5, oc0 = (s2 & 3) * 16;
+        const uint4 a = *reinterpret_cast<const uint4*>(abase + ((4 - ky) * 18 + (4 - kx)) * kOCP + oc0);
+        acc = mfma32b(a, bx[j], acc);
+      }
+      if (c + 2 < 10) {
+#pragma unroll
+        for (int j = 0; j < 10; ++j) bx[j] = *reinterpret_cast<const uint4*>(brow + 16 * ((c + 2) * 10 + j));
+      }
+#pragma unroll
+      for (int j = 0; j < 10; ++j) {
+        const int s2 = (c + 1) * 10 + j, t = s2 >> 2, ky = t / 5, kx = t % 5, oc0 = (s2 & 3) * 16;
+        const uint4 a = *reinterpret_cast<const uint4*>(abase + ((4 - ky) * 18 + (4 - kx)) * kOCP + oc0);
+        acc = mfma32b(a, by[j], acc);
+      }
+    }
+  } else {
+    const uint16_t* bbase = sw + r * kW2qRow + 8 * h;
 #pragma unroll 4
-  for (int s = 0; s < 100; ++s) {
-    const int t = s >> 2, ky = t / 5, kx = t % 5, oc0 = (s & 3) * 16;
-    const uint4 a = *reinterpret_cast<const uint4*>(abase + ((4 - ky) * 18 + (4 - kx)) * kOCP + oc0);
-    const uint4 bq = *reinterpret_cast<const uint4*>(bbase + t * kC2 + oc0);
-    acc = mfma32b(a, bq, acc);
+    for (int s = 0; s < 100; ++s) {
+      const int t = s >> 2, ky = t / 5, kx = t % 5, oc0 = (s & 3) * 16;
+      const uint4 a = *reinterpret_cast<const uint4*>(abase + ((4 - ky) * 18 + (4 - kx)) * kOCP + oc0);
+      const uint4 bq = *reinterpret_cast<const uint4*>(bbase + t * kC2 + oc0);
+      acc = mfma32b(a, bq, acc);
+    }
   }
   // ---- phase 2: sparse conv1 weight gradient at each pool1 argmax pixel
   float wg[kTaps];
@@ -847,11 +885,14 @@ __global__ __launch_bounds__(256) void conv2_bwd_kernel(const uint16_t* __restri
                                                         const uint8_t* __restrict__ xds,
                                                         const int64_t* __restrict__ idx, float* __restrict__ wslab1,
                                                         float* __restrict__ wslab2, int B, int first_block,
-                                                        int wg_blocks) {
+                                                        int wg_blocks, int stream_w) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int j = blockIdx.x + first_block, nd = 2 * B;
   if (j < nd) {
-    conv2_dgrad_block(j & 1, j >> 1, dc2m, am1, w2q, xds, idx, wslab1, smem);
+    if (stream_w)
+      conv2_dgrad_block<true>(j & 1, j >> 1, dc2m, am1, w2q, xds, idx, wslab1, smem);
+    else
+      conv2_dgrad_block<false>(j & 1, j >> 1, dc2m, am1, w2q, xds, idx, wslab1, smem);
   } else if (wg_blocks) {
     const int k = j - nd;  // (image pair, kx)
     conv2_wgrad_block(k / 5, k % 5, dc2m, p1s, wslab2, B, smem);
@@ -880,11 +921,16 @@ void conv2_bwd(const uint16_t* dc2m, const uint16_t* p1s, const uint8_t* am1, co
     const char* e = getenv("P2CNN_CONV2_WG_BLOCKS");
     return e ? atoi(e) : 1;
   }();
+  // dgrad weight fragments streamed from L2 (default) or staged in LDS (P2CNN_DGRAD_STREAM_W=0)
+  static const int stream_w = [] {
+    const char* e = getenv("P2CNN_DGRAD_STREAM_W");
+    return e ? atoi(e) : 1;
+  }();
   const int nd = 2 * B, nw = wg_blocks ? 5 * wgrad_groups(B) : (kTaps * wgrad_groups(B) + 3) / 4;
   const int first = roles == 2 ? nd : 0;
   const int blocks = roles == 1 ? nd : roles == 2 ? nw : nd + nw;
   hipLaunchKernelGGL(conv2_bwd_kernel, dim3(blocks), dim3(256), kDgLds, s, dc2m, p1s, am1, w2q, x, idx, wslab1, wslab2,
-                     B, first, wg_blocks);
+                     B, first, wg_blocks, stream_w);
 }
 
 // ---------------------------------------------------------------------------
