@@ -734,7 +734,7 @@ constexpr int kDgLds = kDgW + kDgWin + kDgXs;            // 143424 B (one dgrad 
 
 // STREAM_W: the weight fragments come straight from L2 (16-B loads one 10-step chunk
 // ahead of the MFMAs) instead of the 102 KB LDS copy every block stages before its
-// first MFMA -- that copy serialised ~4 us of fetch ahead of the compute.
+// first MFMA.  Measured slower (18.8 vs 12.6 us): off by default.
 template <bool STREAM_W>
 P2_DEVICE void conv2_dgrad_block(int grp, int b, const uint16_t* __restrict__ dc2m, const uint8_t* __restrict__ am1,
                                  const uint16_t* __restrict__ w2q, const uint8_t* __restrict__ xds,
@@ -921,10 +921,12 @@ void conv2_bwd(const uint16_t* dc2m, const uint16_t* p1s, const uint8_t* am1, co
     const char* e = getenv("P2CNN_CONV2_WG_BLOCKS");
     return e ? atoi(e) : 1;
   }();
-  // dgrad weight fragments streamed from L2 (default) or staged in LDS (P2CNN_DGRAD_STREAM_W=0)
+  // dgrad weight fragments staged in LDS (default) or streamed from L2
+  // (P2CNN_DGRAD_STREAM_W=1: measured slower, 18.8 vs 12.6 us for the dgrad role,
+  // scripts/kbench.py round 4 -- the four waves re-fetch every fragment)
   static const int stream_w = [] {
     const char* e = getenv("P2CNN_DGRAD_STREAM_W");
-    return e ? atoi(e) : 1;
+    return e ? atoi(e) : 0;
   }();
   const int nd = 2 * B, nw = wg_blocks ? 5 * wgrad_groups(B) : (kTaps * wgrad_groups(B) + 3) / 4;
   const int first = roles == 2 ? nd : 0;
