@@ -61,15 +61,29 @@ P2_DEVICE float erf_fast(float x) {
   return copysignf(r, x);
 }
 
+// Whole-wave reductions, every lane gets the result (call with all 64 lanes active).
+// Within each row of 16 lanes by DPP (quad_perm [1,0,3,2], [2,3,0,1], row_half_mirror,
+// row_mirror: register-to-register, a few cycles each), then the four row results by
+// v_readlane into scalar registers -- instead of six dependent ds_bpermute round trips
+// through the LDS crossbar.  Fixed combination order: deterministic.
+template <int CTRL>
+P2_DEVICE float dpp_mov(float v) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xF, 0xF, false));
+}
+P2_DEVICE float row_lane(float v, int l) { return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), l)); }
 P2_DEVICE float wave_sum(float v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-  return v;
+  v += dpp_mov<0xB1>(v);   // quad_perm [1,0,3,2]
+  v += dpp_mov<0x4E>(v);   // quad_perm [2,3,0,1]
+  v += dpp_mov<0x141>(v);  // row_half_mirror
+  v += dpp_mov<0x140>(v);  // row_mirror: every lane holds its row's sum
+  return (row_lane(v, 0) + row_lane(v, 16)) + (row_lane(v, 32) + row_lane(v, 48));
 }
 P2_DEVICE float wave_max(float v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
-  return v;
+  v = fmaxf(v, dpp_mov<0xB1>(v));
+  v = fmaxf(v, dpp_mov<0x4E>(v));
+  v = fmaxf(v, dpp_mov<0x141>(v));
+  v = fmaxf(v, dpp_mov<0x140>(v));
+  return fmaxf(fmaxf(row_lane(v, 0), row_lane(v, 16)), fmaxf(row_lane(v, 32), row_lane(v, 48)));
 }
 
 }  // namespace p2
