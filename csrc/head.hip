@@ -74,17 +74,14 @@ __global__ __launch_bounds__(kT) void head_fwd_kernel(const uint16_t* __restrict
     for (int n = 0; n < kMaxN; ++n)
       if (n < N) part[n] = fmaf(s, ldw<TW>(w, int64_t(n) * C + c), part[n]);
   }
-  // fixed-order reduction: wave sums (the N xor-shuffle chains advance together, one
-  // step at a time, so their LDS-crossbar round trips overlap), then the 4 waves in order
+  // fixed-order reduction: wave sums, then the 4 waves in order
 #pragma unroll
-  for (int o = 32; o > 0; o >>= 1)
-#pragma unroll
-    for (int n = 0; n < kMaxN; ++n)
-      if (n < N) part[n] += __shfl_xor(part[n], o, 64);
-  if (lane == 0)
-#pragma unroll
-    for (int n = 0; n < kMaxN; ++n)
-      if (n < N) red[n][wave] = part[n];
+  for (int n = 0; n < kMaxN; ++n) {
+    if (n < N) {  // (no early exit: keeps the loop unrolled and part[] in registers)
+      const float v = wave_sum(part[n]);
+      if (lane == 0) red[n][wave] = v;
+    }
+  }
   __syncthreads();
   if (tid < N) {
     float z = red[tid][0] + red[tid][1] + red[tid][2] + red[tid][3];
@@ -118,32 +115,14 @@ __global__ __launch_bounds__(kT) void head_fwd_kernel(const uint16_t* __restrict
     if (last) __hip_atomic_store(ctr, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
   __syncthreads();
-  if (!last) return;
-  // the whole last workgroup reduces the B rows: strided partial sums (every load of
-  // a thread in flight together), then a fixed-shape LDS tree -- a fixed order for
-  // any arrival order.  (One thread looping over the rows paid one dependent
-  // memory round trip per sample: ~15 us of a 20 us launch at B = 32.)
-  __shared__ float fin[2][kT];
+  if (!last || tid != 0) return;
   float sl = 0.f, sa = 0.f;
-  for (int i = tid; i < B; i += kT) {
+  for (int i = 0; i < B; ++i) {
     sl += ld_sc1f(loss_rows + i);
     sa += ld_sc1f(loss_rows + B + i);
   }
-  fin[0][tid] = sl;
-  fin[1][tid] = sa;
-  __syncthreads();
-#pragma unroll
-  for (int st = kT / 2; st > 0; st >>= 1) {
-    if (tid < st) {
-      fin[0][tid] += fin[0][tid + st];
-      fin[1][tid] += fin[1][tid + st];
-    }
-    __syncthreads();
-  }
-  if (tid == 0) {
-    loss_out[0] = fin[0][0] / float(B);
-    acc_out[0] = fin[1][0] / float(B);
-  }
+  loss_out[0] = sl / float(B);
+  acc_out[0] = sa / float(B);
 }
 
 // dl[n] of sample b: (softmax(logits_b)[n] - [n == y_b]) * gscale

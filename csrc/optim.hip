@@ -125,12 +125,6 @@ P2_DEVICE uint32_t cl_index(uint32_t i, uint32_t C, uint32_t HW) {
   const uint32_t per_o = C * HW, o = i / per_o, r = i - o * per_o, c = r / HW, s = r - c * HW;
   return o * per_o + s * C + c;
 }
-// Logical OIHW index of the element at channels-last (O, kh, kw, I) position ``j``
-// (inverse of cl_index).
-P2_DEVICE uint32_t cl_logical(uint32_t j, uint32_t C, uint32_t HW) {
-  const uint32_t per_o = C * HW, o = j / per_o, r = j - o * per_o, s = r / C, c = r - s * C;
-  return o * per_o + c * HW + s;
-}
 P2_DEVICE uint32_t cl_c(int64_t flags) { return uint32_t((flags >> 8) & 0xFFFFFF); }
 P2_DEVICE uint32_t cl_hw(int64_t flags) { return uint32_t((flags >> 32) & 0xFFFFFF); }
 
@@ -168,38 +162,36 @@ __global__ __launch_bounds__(256) void adam_mt_kernel(float* __restrict__ p, flo
   float* V = v + T.off + start;
   uint16_t* PB = shadow ? pbf + T.off + start : nullptr;
   if (T.flags & kMTPermCL) {
-    // walked in channels-last order: the bf16 gradient, the bf16 shadow and the
-    // optimizer state (m, v: kept in channels-last order for these tensors -- they
-    // are private to this kernel) are contiguous; only the fp32 master weight, in
-    // the arena's OIHW order, is gathered (stride kh*kw elements).  The logical-order
-    // walk it replaces scattered every 2-byte gradient / shadow access C elements apart.
+    // fp32 state in logical (coalesced) order; the bf16 gradient and shadow
+    // are gathered / scattered at their channels-last positions (the whole
+    // slab of an output channel is L2-resident while its block runs)
     const uint32_t C = cl_c(T.flags), HW = cl_hw(T.flags);
-    float* P0 = p + T.off;
-    const uint16_t* G16 = static_cast<const uint16_t*>(g);
-    const float* G32 = static_cast<const float*>(g);
-    for (int64_t j0 = threadIdx.x; j0 < len; j0 += 4 * 256) {
+    uint16_t* SB = shadow ? pbf + T.off : nullptr;
+    // 4 elements per thread in flight (state loads + gradient gathers issued
+    // together): one dependent round trip per element made this loop latency-bound
+    for (int64_t i0 = threadIdx.x; i0 < len; i0 += 4 * 256) {
       float pv[4], gv[4], mv[4], vv[4];
-      uint32_t li[4];
+      uint32_t j[4];
 #pragma unroll
       for (int u = 0; u < 4; ++u) {
-        const int64_t j = j0 + u * 256;
-        if (j < len) {
-          li[u] = cl_logical(uint32_t(start + j), C, HW);
-          pv[u] = P0[li[u]];
-          mv[u] = M[j];
-          vv[u] = V[j];
-          gv[u] = gbf ? bf16_to_f32(G16[start + j]) : G32[start + j];
+        const int64_t i = i0 + u * 256;
+        if (i < len) {
+          j[u] = cl_index(uint32_t(start + i), C, HW);
+          pv[u] = P[i];
+          mv[u] = M[i];
+          vv[u] = V[i];
+          gv[u] = load_grad1(g, gbf, j[u]);
         }
       }
 #pragma unroll
       for (int u = 0; u < 4; ++u) {
-        const int64_t j = j0 + u * 256;
-        if (j < len) {
+        const int64_t i = i0 + u * 256;
+        if (i < len) {
           adam_elem(pv[u], gv[u], mv[u], vv[u], h);
-          P0[li[u]] = pv[u];
-          M[j] = mv[u];
-          V[j] = vv[u];
-          if (PB) PB[j] = f32_to_bf16(pv[u]);
+          P[i] = pv[u];
+          M[i] = mv[u];
+          V[i] = vv[u];
+          if (SB) SB[j[u]] = f32_to_bf16(pv[u]);
         }
       }
     }
@@ -265,32 +257,30 @@ __global__ __launch_bounds__(256) void sgd_mt_kernel(float* __restrict__ p, floa
   float* P = p + T.off + start;
   float* B = buf ? buf + T.off + start : nullptr;
   uint16_t* PB = shadow ? pbf + T.off + start : nullptr;
-  if (T.flags & kMTPermCL) {  // channels-last walk, momentum in channels-last order (see adam_mt_kernel)
+  if (T.flags & kMTPermCL) {  // see adam_mt_kernel (4 elements per thread in flight)
     const uint32_t C = cl_c(T.flags), HW = cl_hw(T.flags);
-    float* P0 = p + T.off;
-    const uint16_t* G16 = static_cast<const uint16_t*>(g);
-    const float* G32 = static_cast<const float*>(g);
-    for (int64_t j0 = threadIdx.x; j0 < len; j0 += 4 * 256) {
+    uint16_t* SB = shadow ? pbf + T.off : nullptr;
+    for (int64_t i0 = threadIdx.x; i0 < len; i0 += 4 * 256) {
       float pv[4], gv[4], bv[4];
-      uint32_t li[4];
+      uint32_t j[4];
 #pragma unroll
       for (int u = 0; u < 4; ++u) {
-        const int64_t j = j0 + u * 256;
-        if (j < len) {
-          li[u] = cl_logical(uint32_t(start + j), C, HW);
-          pv[u] = P0[li[u]];
-          bv[u] = B ? B[j] : 0.f;
-          gv[u] = gbf ? bf16_to_f32(G16[start + j]) : G32[start + j];
+        const int64_t i = i0 + u * 256;
+        if (i < len) {
+          j[u] = cl_index(uint32_t(start + i), C, HW);
+          pv[u] = P[i];
+          bv[u] = B ? B[i] : 0.f;
+          gv[u] = load_grad1(g, gbf, j[u]);
         }
       }
 #pragma unroll
       for (int u = 0; u < 4; ++u) {
-        const int64_t j = j0 + u * 256;
-        if (j < len) {
+        const int64_t i = i0 + u * 256;
+        if (i < len) {
           const float np = sgd_regs(pv[u], gv[u], bv[u], B != nullptr, h);
-          P0[li[u]] = np;
-          if (B) B[j] = bv[u];
-          if (PB) PB[j] = f32_to_bf16(np);
+          P[i] = np;
+          if (B) B[i] = bv[u];
+          if (SB) SB[j[u]] = f32_to_bf16(np);
         }
       }
     }
