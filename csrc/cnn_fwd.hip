@@ -331,13 +331,10 @@ __global__ __launch_bounds__(256) void gemm_skinny_kernel(const uint16_t* __rest
   for (int mt = 0; mt < MT; ++mt) arow[mt] = A + size_t(mt * 32 + r) * K + 32 * h;
   // software pipeline: the next group's 16-B loads are in flight while the
   // current group's MFMAs run
-  // Two register sets in ping-pong (no copies between them: a copy of a register
-  // still being loaded forces a vmcnt wait); the group index of a prefetch is
-  // clamped to the split's last group so every load is unconditional -- a load
-  // under a branch made the compiler drain vmcnt(0) before the MFMAs, waiting for
-  // the prefetch it had just issued.
+  uint4 bq[4], aq[MT][4];
+  int g = g0 + wave;
   auto load = [&](int gg, uint4 (&bb)[4], uint4 (&aa)[MT][4]) {
-    const int k0 = min(gg, g1 - 1) * 64;
+    const int k0 = gg * 64;
 #pragma unroll
     for (int q = 0; q < 4; ++q) bb[q] = ld_nt16(brow + k0 + q * 8);
 #pragma unroll
@@ -345,30 +342,23 @@ __global__ __launch_bounds__(256) void gemm_skinny_kernel(const uint16_t* __rest
 #pragma unroll
       for (int q = 0; q < 4; ++q) aa[mt][q] = reinterpret_cast<const uint4*>(arow[mt] + k0)[q];
   };
-  auto mma = [&](const uint4 (&bb)[4], const uint4 (&aa)[MT][4]) {
+  if (g < g1) load(g, bq, aq);
+  for (; g < g1; g += 4) {
+    uint4 nb[4], na[MT][4];
+    const bool more = g + 4 < g1;
+    if (more) load(g + 4, nb, na);
 #pragma unroll
     for (int q = 0; q < 4; ++q)
 #pragma unroll
-      for (int mt = 0; mt < MT; ++mt) acc[mt] = mfma32(aa[mt][q], bb[q], acc[mt]);
-  };
-  // A wave owns groups g0 + wave, + 4, + 8, ...: with the default 7 splits that is
-  // one or two groups, so each iteration issues the loads of TWO groups before any
-  // MFMA (the second clamped to the split and zeroed when past its end, so its MFMAs
-  // always run and no branch separates a load from its use -- the compiler sank
-  // branch-guarded prefetches next to their MFMAs and drained vmcnt(0) in front of them)
-  uint4 xb[4], xa[MT][4], yb[4], ya[MT][4];
-  for (int g = g0 + wave; g < g1; g += 8) {
-    load(g, xb, xa);
-    load(g + 4, yb, ya);
-    __builtin_amdgcn_sched_barrier(0);
-    mma(xb, xa);
-    if (g + 4 >= g1) {
+      for (int mt = 0; mt < MT; ++mt) acc[mt] = mfma32(aq[mt][q], bq[q], acc[mt]);
+    if (more) {
 #pragma unroll
-      for (int mt = 0; mt < MT; ++mt)
+      for (int q = 0; q < 4; ++q) {
+        bq[q] = nb[q];
 #pragma unroll
-        for (int q = 0; q < 4; ++q) ya[mt][q] = make_uint4(0, 0, 0, 0);
+        for (int mt = 0; mt < MT; ++mt) aq[mt][q] = na[mt][q];
+      }
     }
-    mma(yb, ya);
   }
   const int mrows = MT * 32;
 #pragma unroll
