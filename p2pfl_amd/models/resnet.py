@@ -24,12 +24,13 @@ Activations run channels-last on the GPU.  What runs per convolution
 * the 3-channel stem runs the direct small-C kernels of ``csrc/stem.hip``
   (forward + weight gradient, reading the uint8 / fp32 batch as it comes).
 
-In training, every convolution's launch also computes the batch statistics of the
-BatchNorm that follows it (``gemm_core.h`` BnEpi), and the input-gradient launch of
-a block's inner convolution computes the backward statistics of the BatchNorm before
-it (:func:`~p2pfl_amd.ops.conv.bn_act_conv_bn_stats`): per BasicBlock the forward is
-conv1 -> [bn1 apply, conv2] -> bn2 apply (+ shortcut) (+ ReLU), three launches where
-the separate BN kernels needed nine.  Evaluation (running statistics) runs the one-pass
+In training, BatchNorm runs the separate statistics / finalize / apply kernels of
+``csrc/batchnorm.hip`` by default.  With ``P2PFL_CONV_BN_STATS=1`` every convolution's
+launch also computes the batch statistics of the BatchNorm that follows it
+(``gemm_core.h`` BnEpi) and the input-gradient launch of a block's inner convolution
+the backward statistics of the one before it (:func:`~p2pfl_amd.ops.conv.bn_act_conv_bn_stats`):
+conv1 -> [bn1 apply, conv2] -> bn2 apply per BasicBlock -- fewer launches, but measured
+slower on these shapes (``profiles/r4_bn_epilogue.md``).  Evaluation (running statistics) runs the one-pass
 BN kernel of ``csrc/batchnorm.hip`` (:func:`~p2pfl_amd.ops.batchnorm.batch_norm_act`).  Optimiser: SGD with momentum 0.9 and weight decay 5e-4 (fused
 into one arena kernel by the learner), a standard federated CIFAR setup.
 """
