@@ -5,6 +5,7 @@
 // optimizer state laid out as flat arenas the full update is one streaming
 // pass: float4 loads of p, g, m, v; fp32 math; float4 stores; optional bf16
 // shadow copy of p for bf16 MFMA consumers (saves a separate cast kernel).
+#include <cstdlib>
 #include "common.h"
 #include "kernels.h"
 
@@ -125,6 +126,22 @@ P2_DEVICE uint32_t cl_index(uint32_t i, uint32_t C, uint32_t HW) {
   const uint32_t per_o = C * HW, o = i / per_o, r = i - o * per_o, c = r / HW, s = r - c * HW;
   return o * per_o + s * C + c;
 }
+// n / d by multiply-high (n < 2^31): the magic numbers are computed once per block
+// (uniform), so the per-element channels-last index costs two v_mul_hi instead of
+// two ~25-instruction integer divisions
+struct FastDivU {
+  uint32_t d, mul, shift;
+};
+P2_DEVICE FastDivU make_fastdiv_u(uint32_t d) {
+  const uint32_t l = d <= 1 ? 0u : 32u - __clz(d - 1);
+  const uint64_t mul = ((uint64_t(1) << 32) * ((uint64_t(1) << l) - d)) / d + 1;
+  return FastDivU{d, uint32_t(mul), l};
+}
+P2_DEVICE uint32_t fdivu(uint32_t n, const FastDivU& f) { return (__umulhi(n, f.mul) + n) >> f.shift; }
+P2_DEVICE uint32_t cl_index_fast(uint32_t i, uint32_t C, const FastDivU& per_o, const FastDivU& hw) {
+  const uint32_t o = fdivu(i, per_o), r = i - o * per_o.d, c = fdivu(r, hw), s = r - c * hw.d;
+  return o * per_o.d + s * C + c;
+}
 P2_DEVICE uint32_t cl_c(int64_t flags) { return uint32_t((flags >> 8) & 0xFFFFFF); }
 P2_DEVICE uint32_t cl_hw(int64_t flags) { return uint32_t((flags >> 32) & 0xFFFFFF); }
 
@@ -140,6 +157,7 @@ P2_DEVICE void adam_elem(float& p, float g, float& m, float& v, const AdamParams
   p = p - h.step_size * (m / (sqrtf(v) * h.inv_sqrt_bc2 + h.eps));
 }
 
+template <bool FD>
 __global__ __launch_bounds__(256) void adam_mt_kernel(float* __restrict__ p, float* __restrict__ m,
                                                       float* __restrict__ v, uint16_t* __restrict__ pbf,
                                                       const MTTensor* __restrict__ tens, const int2* __restrict__ chunks,
@@ -166,6 +184,8 @@ __global__ __launch_bounds__(256) void adam_mt_kernel(float* __restrict__ p, flo
     // are gathered / scattered at their channels-last positions (the whole
     // slab of an output channel is L2-resident while its block runs)
     const uint32_t C = cl_c(T.flags), HW = cl_hw(T.flags);
+    FastDivU fpo{}, fhw{};
+    if (FD) fpo = make_fastdiv_u(C * HW), fhw = make_fastdiv_u(HW);
     uint16_t* SB = shadow ? pbf + T.off : nullptr;
     // 4 elements per thread in flight (state loads + gradient gathers issued
     // together): one dependent round trip per element made this loop latency-bound
@@ -176,7 +196,7 @@ __global__ __launch_bounds__(256) void adam_mt_kernel(float* __restrict__ p, flo
       for (int u = 0; u < 4; ++u) {
         const int64_t i = i0 + u * 256;
         if (i < len) {
-          j[u] = cl_index(uint32_t(start + i), C, HW);
+          j[u] = FD ? cl_index_fast(uint32_t(start + i), C, fpo, fhw) : cl_index(uint32_t(start + i), C, HW);
           pv[u] = P[i];
           mv[u] = M[i];
           vv[u] = V[i];
@@ -243,6 +263,7 @@ P2_DEVICE float sgd_elem(float& p, float g, float* b, const SgdParams& h) {
   return p;
 }
 
+template <bool FD>
 __global__ __launch_bounds__(256) void sgd_mt_kernel(float* __restrict__ p, float* __restrict__ buf,
                                                      uint16_t* __restrict__ pbf, const MTTensor* __restrict__ tens,
                                                      const int2* __restrict__ chunks, const uint64_t* __restrict__ gptr,
@@ -259,6 +280,8 @@ __global__ __launch_bounds__(256) void sgd_mt_kernel(float* __restrict__ p, floa
   uint16_t* PB = shadow ? pbf + T.off + start : nullptr;
   if (T.flags & kMTPermCL) {  // see adam_mt_kernel (4 elements per thread in flight)
     const uint32_t C = cl_c(T.flags), HW = cl_hw(T.flags);
+    FastDivU fpo{}, fhw{};
+    if (FD) fpo = make_fastdiv_u(C * HW), fhw = make_fastdiv_u(HW);
     uint16_t* SB = shadow ? pbf + T.off : nullptr;
     for (int64_t i0 = threadIdx.x; i0 < len; i0 += 4 * 256) {
       float pv[4], gv[4], bv[4];
@@ -267,7 +290,7 @@ __global__ __launch_bounds__(256) void sgd_mt_kernel(float* __restrict__ p, floa
       for (int u = 0; u < 4; ++u) {
         const int64_t i = i0 + u * 256;
         if (i < len) {
-          j[u] = cl_index(uint32_t(start + i), C, HW);
+          j[u] = FD ? cl_index_fast(uint32_t(start + i), C, fpo, fhw) : cl_index(uint32_t(start + i), C, HW);
           pv[u] = P[i];
           bv[u] = B ? B[i] : 0.f;
           gv[u] = load_grad1(g, gbf, j[u]);
@@ -312,16 +335,31 @@ __global__ __launch_bounds__(256) void sgd_mt_kernel(float* __restrict__ p, floa
   }
 }
 
+// channels-last index by multiply-high (default) or by integer division (P2_MT_FASTDIV=0; A/B knob, read once)
+static bool mt_fastdiv() {
+  static const bool on = [] {
+    const char* e = getenv("P2_MT_FASTDIV");
+    return !e || atoi(e) != 0;
+  }();
+  return on;
+}
+
 void adam_mt_step(float* p, float* m, float* v, uint16_t* pbf, const MTTensor* tens, const int2* chunks,
                   int n_chunks, const uint64_t* gptr, const AdamParams& h, hipStream_t s) {
-  if (n_chunks > 0)
-    hipLaunchKernelGGL(adam_mt_kernel, dim3(n_chunks), dim3(256), 0, s, p, m, v, pbf, tens, chunks, gptr, h);
+  if (n_chunks <= 0) return;
+  if (mt_fastdiv())
+    hipLaunchKernelGGL(adam_mt_kernel<true>, dim3(n_chunks), dim3(256), 0, s, p, m, v, pbf, tens, chunks, gptr, h);
+  else
+    hipLaunchKernelGGL(adam_mt_kernel<false>, dim3(n_chunks), dim3(256), 0, s, p, m, v, pbf, tens, chunks, gptr, h);
 }
 
 void sgd_mt_step(float* p, float* buf, uint16_t* pbf, const MTTensor* tens, const int2* chunks, int n_chunks,
                  const uint64_t* gptr, const SgdParams& h, hipStream_t s) {
-  if (n_chunks > 0)
-    hipLaunchKernelGGL(sgd_mt_kernel, dim3(n_chunks), dim3(256), 0, s, p, buf, pbf, tens, chunks, gptr, h);
+  if (n_chunks <= 0) return;
+  if (mt_fastdiv())
+    hipLaunchKernelGGL(sgd_mt_kernel<true>, dim3(n_chunks), dim3(256), 0, s, p, buf, pbf, tens, chunks, gptr, h);
+  else
+    hipLaunchKernelGGL(sgd_mt_kernel<false>, dim3(n_chunks), dim3(256), 0, s, p, buf, pbf, tens, chunks, gptr, h);
 }
 
 }  // namespace p2
