@@ -331,8 +331,9 @@ def run_gossip(args, env: _Env) -> dict:
         print(
             f"[bench rank {env.rank}] per-round (mean of {K}): " + ", ".join(f"{k} {v:.2f} ms" for k, v in ph.items())
             + f"; data plane: {stats.get('sent', 0)} sends / {stats.get('received', 0)} recvs / "
-            f"{stats.get('groups', 0)} groups, {stats.get('nacked', 0)} declined; xgmi bytes sent "
-            f"{pushes.get('xgmi_bytes_sent', 0) / 1e6:.1f} MB",
+            f"{stats.get('groups', 0)} groups, {stats.get('nacked', 0)} declined"
+            + "".join(f" [{k.split('/', 1)[1]}: {v}]" for k, v in sorted(stats.items()) if k.startswith("nacked/"))
+            + f"; xgmi bytes sent {pushes.get('xgmi_bytes_sent', 0) / 1e6:.1f} MB",
             file=sys.stderr, flush=True,
         )
         from p2pfl_amd.ops import autotune

@@ -73,7 +73,7 @@ struct GemmParams {
   float* ws;      // split-K workspace for the in-launch reduction
   int* counters;  // per-tile arrival counters (see above), or null
   BnEpi bn;       // BatchNorm statistics epilogue when bn.part != null
-  int variant;  // tuning experiments: bit0 setprio around MFMAs, bit1 A-panel tile order, bit2 no XCD remap, bit3 single LDS buffer (4 workgroups / CU), bit4/bit5 timing probes (no stores / no K loop), bit6 256 x 256 tile (8 waves), bit7 no DMA after the prologue (probe), bit8 legacy panel tile order instead of grouped (bit1 then picks A- vs B-panel order), bits 9-10 where the double-buffer prefetch is issued (0 before the K-tile's fragment reads, 1 after the first ones, 2 one chunk per k-substep), bit11 the ping-pong 256 x 256 pipeline of gemm_pp.hip (continuous per-phase DMA, staggered wave halves), bit12 the 4-wave 256 x 256 kernel of gemm_w4.hip (128 x 128 per wave, AGPR accumulators, one barrier per K-tile)
+  int variant;  // tuning experiments: bit0 setprio around MFMAs, bit1 A-panel tile order, bit2 no XCD remap, bit3 single LDS buffer (4 workgroups / CU), bit4/bit5 timing probes (no stores / no K loop), bit6 256 x 256 tile (8 waves), bit7 no DMA after the prologue (probe), bit8 legacy panel tile order instead of grouped (bit1 then picks A- vs B-panel order), bits 9-10 where the double-buffer prefetch is issued (0 before the K-tile's fragment reads, 1 after the first ones, 2 one chunk per k-substep), bit11 the ping-pong 256 x 256 pipeline of gemm_pp.hip (continuous per-phase DMA, staggered wave halves); with bit 11, bits 12-15 are the ping-pong kernel's timing probes (gemm_pp.hip).  Bit 12 is also the conv kernels' 4-stage ring (conv.hip), whose split-K slabs are 128 x 128 tiles
 };
 
 void gemm_bf16(const GemmParams& p, hipStream_t s);
@@ -84,9 +84,5 @@ void tile_slab_reduce(const float* ws, int splits, int M, int N, int64_t ldc, vo
 // the ping-pong pipeline (gemm_pp.hip); gemm_bf16 routes variant bit 11 here
 bool gemm_pp_supported(const GemmParams& p);
 void gemm_bf16_pp(const GemmParams& p, hipStream_t s);
-// the 4-wave 256 x 256 kernel (gemm_w4.hip); gemm_bf16 routes variant bit 12 here.
-// Its split-K slabs are whole 256 x 256 tiles (gemm_w4_slab_elems per slice).
-void gemm_bf16_w4(const GemmParams& p, hipStream_t s);
-int64_t gemm_w4_slab_elems(int M, int N);
 
 }  // namespace p2

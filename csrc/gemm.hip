@@ -10,6 +10,9 @@
 //   wave 64 x 64 = 2 x 2 tiles of v_mfma_f32_32x32x16_bf16, BK = 64; or
 //   (variant bit 6) 256 x 256 per 512-thread workgroup, 8 waves as 2 x 4,
 //   each 128 x 64 -- half the operand bytes per FLOP, for large products;
+//   (variant bit 12) the 128 x 128 tile on a 4-stage LDS ring (3 K-tiles in
+//   flight, one workgroup per CU): short-K products, where a double buffer
+//   pays the L2/HBM round trip once per K-tile;
 // * the pipeline itself lives in gemm_core.h (shared with the implicit-GEMM
 //   convolutions of conv.hip); this file instantiates it with plain loaders;
 // * operands go HBM -> LDS with global_load_lds (16 B per lane, no VGPR
@@ -38,7 +41,7 @@
 namespace p2gemm {
 
 template <int NBUF, class LA, class LB>
-__global__ __launch_bounds__(NT, NBUF == 1 ? 4 : 2) void gemm_kernel(GemmParams p, LA la, LB lb, int tiles_m, int tiles_n) {
+__global__ __launch_bounds__(NT, NBUF == 1 ? 4 : (NBUF == 2 ? 2 : 1)) void gemm_kernel(GemmParams p, LA la, LB lb, int tiles_m, int tiles_n) {
   __shared__ __attribute__((aligned(16))) char smem[smem_bytes<Tile128, NBUF>()];  // [buf][A | B]
   gemm_body<Tile128, NBUF>(p, la, lb, tiles_m, tiles_n, smem);
 }
@@ -60,7 +63,9 @@ static void launch(const GemmParams& p, const LA& la, const LB& lb, hipStream_t 
     return;
   }
   const int grid = gemm_grid<Tile128>(p, tm, tn);
-  if (p.variant & 8)
+  if (p.variant & 4096)  // 4-stage ring (3 K-tiles in flight), one workgroup per CU: short-K products
+    hipLaunchKernelGGL((gemm_kernel<4, LA, LB>), dim3(grid), dim3(NT), 0, s, p, la, lb, tm, tn);
+  else if (p.variant & 8)
     hipLaunchKernelGGL((gemm_kernel<1, LA, LB>), dim3(grid), dim3(NT), 0, s, p, la, lb, tm, tn);
   else
     hipLaunchKernelGGL((gemm_kernel<2, LA, LB>), dim3(grid), dim3(NT), 0, s, p, la, lb, tm, tn);
@@ -78,10 +83,6 @@ void gemm_bf16(const GemmParams& p, hipStream_t s) {
     gemm_bf16_pp(q, s);
     return;
   }
-  if (q.variant & 4096) {
-    gemm_bf16_w4(q, s);
-    return;
-  }
   if (p.a_kmajor && p.b_kmajor)
     launch(q, PlainK{p.a, p.lda, p.M, p.K}, PlainK{p.b, p.ldb, p.N, p.K}, s);
   else if (p.a_kmajor)
@@ -95,13 +96,7 @@ void gemm_bf16(const GemmParams& p, hipStream_t s) {
 void tile_slab_reduce(const float* ws, int splits, int M, int N, int64_t ldc, void* out, int out_bf16, int variant,
                       hipStream_t s) {
   using namespace p2gemm;
-  if (variant & 4096) {  // 4-wave tile: slabs of whole 256 x 256 tiles, same fragment-native order per wave
-    const int tm = (M + 255) / 256, tn = (N + 255) / 256;
-    const int64_t groups = int64_t(tm) * tn * (256 * 256 / 4);
-    using Tile4w = TileCfg<256, 256, 2, 2>;
-    hipLaunchKernelGGL(tile_slab_reduce_kernel<Tile4w>, dim3(int((groups + 255) / 256)), dim3(256), 0, s, ws, splits, M,
-                       N, ldc, out, out_bf16, variant, tm, tn);
-  } else if (variant & 64) {
+  if (variant & 64) {
     const int tm = (M + 255) / 256, tn = (N + 255) / 256;
     const int64_t groups = int64_t(tm) * tn * (256 * 256 / 4);
     hipLaunchKernelGGL(tile_slab_reduce_kernel<Tile256>, dim3(int((groups + 255) / 256)), dim3(256), 0, s, ws, splits, M,

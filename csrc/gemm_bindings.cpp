@@ -14,7 +14,7 @@ namespace {
 // fp32 elements of one split-K slice: the fragment-native tiles of the kernel the
 // variant selects (gemm_core.h SlabGeom), or the ping-pong kernel's row-major M x N
 int64_t slab_elems(int64_t M, int64_t N, int64_t variant) {
-  const int64_t t = (variant & (64 | 4096)) ? 256 : 128;
+  const int64_t t = (variant & 64) ? 256 : 128;
   return std::max(M * N, ((M + t - 1) / t) * ((N + t - 1) / t) * t * t);
 }
 
@@ -115,7 +115,6 @@ void tile_slab_reduce(torch::Tensor ws, int64_t splits, int64_t M, int64_t N, to
                   ws.numel() >= splits * slab_elems(M, N, variant) && reinterpret_cast<uintptr_t>(ws.data_ptr()) % 16 == 0,
               "tile_slab_reduce: ws must be contiguous fp32 with splits * slab_elems(M, N) elements");
   TORCH_CHECK(!(variant & 2048), "tile_slab_reduce: the ping-pong kernel writes row-major slabs");
-  TORCH_CHECK(!((variant & 64) && (variant & 4096)), "tile_slab_reduce: one tile kind per variant");
   TORCH_CHECK(splits >= 1 && M >= 1 && N >= 8 && N % 4 == 0, "tile_slab_reduce: bad shape");
   TORCH_CHECK(out.is_cuda() && out.is_contiguous() && out.numel() == M * N && out.device() == ws.device() &&
                   (out.scalar_type() == torch::kFloat32 || out.scalar_type() == torch::kBFloat16) &&

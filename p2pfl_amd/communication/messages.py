@@ -15,7 +15,7 @@ from __future__ import annotations
 
 import secrets
 from dataclasses import dataclass, field
-from typing import Any, List
+from typing import Any, Callable, List, Optional
 
 
 def new_message_hash() -> int:
@@ -41,6 +41,12 @@ class WeightsMessage:
     contributors: List[str] = field(default_factory=list)
     weight: int = 1
     cmd: str = ""
+    # Delivery feedback (not on the wire): a transport that learns the fate of a
+    # push asynchronously (the xGMI data plane: propose -> ack / decline ->
+    # transfer) calls on_result("pending"), then "delivered" or "declined: <why>".
+    # Synchronous transports never call it.  See stages/base_node/common.py
+    # DeliveryLedger.
+    on_result: Optional[Callable[[str], None]] = field(default=None, repr=False, compare=False)
 
     def nbytes(self) -> int:
         w = self.weights

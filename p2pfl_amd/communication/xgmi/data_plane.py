@@ -595,6 +595,8 @@ class XgmiDataPlane:
             self._cv.notify_all()
         if op is not None:
             self.stats["nacked"] += 1
+            # per-reason tally ("late round (3 != 2)" -> "late round")
+            self.stats["nacked/" + reason.split(" (")[0]] += 1
             self._done(op, False, reason, evict)
 
     # ------------------------------------------------------------------

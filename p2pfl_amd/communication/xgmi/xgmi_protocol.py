@@ -296,6 +296,9 @@ class XgmiCommunicationProtocol(BaseCommunicationProtocol):
         self._layout_json: Dict[int, str] = {}
         self._departed: set = set()
         self._inbound: set = set()
+        # keys of models already received (an identical proposal arriving
+        # between the transfer and the handler's bookkeeping is declined)
+        self._received: set = set()
 
     def _resolve_address(self, addr: str) -> str:
         if addr in (None, "", "127.0.0.1"):
@@ -378,7 +381,14 @@ class XgmiCommunicationProtocol(BaseCommunicationProtocol):
         nbytes = flat.numel() * flat.element_size()
         t_prop = time.perf_counter()
 
+        feedback = msg.on_result
+
         def on_done(ok: bool, reason: str, evict: bool) -> None:
+            if feedback is not None:
+                try:
+                    feedback("delivered" if ok else f"declined: {reason}")
+                except Exception:
+                    pass
             if ok:
                 logger.tracer.count(self.addr, "xgmi_bytes_sent", nbytes)
                 logger.tracer.count(self.addr, "xgmi_pushes")
@@ -389,6 +399,8 @@ class XgmiCommunicationProtocol(BaseCommunicationProtocol):
                 logger.info(self.addr, f"push of {msg.cmd} to {dst} failed ({reason}); dropping the neighbour")
                 self._neighbors.remove(dst)
 
+        if feedback is not None:
+            feedback("pending")
         hdr = plane.propose(rank, flat, on_done)
         hdr["rk"] = self.job.rank
         rec = ["wput", hdr, msg.source, msg.round, list(msg.contributors), msg.weight, msg.cmd,
@@ -397,6 +409,8 @@ class XgmiCommunicationProtocol(BaseCommunicationProtocol):
             self.bus.send(dst, _pack(rec))
         except Exception:
             plane.cancel(hdr["seq"], "header not delivered")
+            if feedback is not None:
+                feedback("declined: header not delivered")
             raise
         return True
 
@@ -423,12 +437,17 @@ class XgmiCommunicationProtocol(BaseCommunicationProtocol):
         plane = self.plane
         if plane is None or not plane.usable:
             return nack("data plane not running", False)
-        # the same model already on its way here (a re-send that crossed the
-        # receiver's models_aggregated report): one transfer is enough
-        key = (source, rnd, cmd_name, tuple(sorted(contributors)))
+        # the same model already on its way here -- a re-send that crossed the
+        # receiver's models_aggregated report, or the same contributor set from
+        # another peer (an init model or a full aggregate offered by several
+        # neighbours at once; equal contributors = the same average): one
+        # transfer is enough
+        key = (rnd, cmd_name, tuple(sorted(contributors)))
         with self._req_lock:
             if key in self._inbound:
                 return nack("already in flight", False)
+            if key in self._received:
+                return nack("already received", False)
             self._inbound.add(key)
         layout = self._layouts.get(layout_s)
         if layout is None:
@@ -440,6 +459,10 @@ class XgmiCommunicationProtocol(BaseCommunicationProtocol):
         def on_recv(buf: Optional[torch.Tensor], reason: str) -> None:
             with self._req_lock:
                 self._inbound.discard(key)
+                if buf is not None:
+                    if len(self._received) > 4096:  # keep the recent rounds only
+                        self._received = {k for k in self._received if k[0] >= rnd - 2}
+                    self._received.add(key)
             if buf is None:
                 return
             if buf.is_cuda:

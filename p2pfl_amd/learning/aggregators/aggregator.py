@@ -106,6 +106,11 @@ class Aggregator:
     def train_set(self) -> List[str]:
         return list(self._train_set)
 
+    def live_train_set(self) -> List[str]:
+        """Train-set members not marked lost: what a full aggregate must cover."""
+        with self._lock:
+            return [n for n in self._train_set if n not in self._lost]
+
     def _missing(self) -> List[str]:
         have = set(self.get_aggregated_models())
         return [n for n in self._train_set if n not in have]

@@ -123,6 +123,7 @@ def gemm(
     residual: Optional[torch.Tensor] = None,
     splits: int = 1,
     out: Optional[torch.Tensor] = None,
+    variant: Optional[int] = None,
 ) -> Tuple[torch.Tensor, Optional[torch.Tensor]]:
     """``(C, z)`` with ``C[m, n] = sum_k A(m, k) B(n, k)`` (+ epilogue).
 
@@ -139,7 +140,7 @@ def gemm(
         if out is None:
             out = torch.empty((M, N), dtype=out_dtype, device=dev)
         z = torch.empty((M, N), dtype=torch.bfloat16, device=dev) if (gelu and want_z) else None
-        v = _variant(a_kmajor, splits)
+        v = _variant(a_kmajor, splits) if variant is None else variant
         ws = torch.empty(splits * slab_elems(M, N, v), dtype=torch.float32, device=dev)
         if splits <= IN_LAUNCH_MAX_SPLITS:  # the last slice of each tile reduces it in the launch
             _C().gemm(a, b, a_kmajor, b_kmajor, out, bias, gelu, z, residual, splits, v, ws, counters(tiles_of(M, N), dev))
@@ -155,7 +156,8 @@ def gemm(
     if out is None:
         out = torch.empty((M, N), dtype=out_dtype, device=dev)
     z = torch.empty((M, N), dtype=torch.bfloat16, device=dev) if (gelu and want_z) else None
-    _C().gemm(a, b, a_kmajor, b_kmajor, out, bias, gelu, z, residual, 1, _variant(a_kmajor, 1, M, N, K, b_kmajor))
+    v = _variant(a_kmajor, 1, M, N, K, b_kmajor) if variant is None else variant
+    _C().gemm(a, b, a_kmajor, b_kmajor, out, bias, gelu, z, residual, 1, v)
     return out, z
 
 
@@ -179,14 +181,38 @@ def _rows(x: torch.Tensor) -> torch.Tensor:
     return x2
 
 
-class _LinearMFMA(torch.autograd.Function):
+_NAT, _LIB = "native", "library"
+
+
+class _LinearP(torch.autograd.Function):
+    """``y = x W^T + b`` (or ``gelu(x W^T + b)``) whose three products -- forward,
+    input gradient, weight gradient -- each run on the path measured fastest for
+    its own shape (``plan``): the MFMA kernel of ``csrc/gemm*.hip`` or hipBLASLt.
+    The forward's bias / GELU ride in the native epilogue (which also keeps the
+    pre-activation for the backward), or in the fused bias+GELU kernel after a
+    bias-free hipBLASLt GEMM; the bias gradient is the column-sum kernel, or comes
+    out of the fused GELU backward."""
+
     @staticmethod
     @torch.amp.custom_fwd(device_type="cuda", cast_inputs=torch.bfloat16)
-    def forward(ctx, x, w, b):
+    def forward(ctx, x, w, b, gelu, plan):
+        from p2pfl_amd.ops.fused import _fx
+
+        fwd = plan[0]
         x2 = _rows(x.to(torch.bfloat16))
         wc = w.to(torch.bfloat16).contiguous()
-        y, _ = gemm(x2, wc, bias=b)
-        ctx.save_for_backward(x2, wc)
+        pre = gb = None
+        if not gelu:
+            y = gemm(x2, wc, bias=b)[0] if fwd == _NAT else F.linear(x2, wc, b.to(torch.bfloat16) if b is not None else None)
+        elif fwd == _NAT:
+            y, pre = gemm(x2, wc, bias=b, gelu=True, want_z=True)  # pre-activation includes the bias
+            gb = torch.zeros(w.shape[0], dtype=torch.float32, device=x.device)
+        else:
+            pre = torch.mm(x2, wc.t())  # bias-free; the GELU kernel adds it
+            gb = b.float().contiguous()
+            y = _fx().bias_gelu_fwd(pre, gb)
+        ctx.save_for_backward(x2, wc, pre, gb)
+        ctx.gelu, ctx.plan = gelu, plan
         ctx.w_dtype = w.dtype
         ctx.b_dtype = b.dtype if b is not None else None
         ctx.xshape = x.shape
@@ -195,98 +221,74 @@ class _LinearMFMA(torch.autograd.Function):
     @staticmethod
     @torch.amp.custom_bwd(device_type="cuda")
     def backward(ctx, dy):
-        x2, w = ctx.saved_tensors
-        dy2 = _rows(dy.to(torch.bfloat16))
-        dx = dw = db = None
-        if ctx.needs_input_grad[0]:
-            dx = _product(dy2, w, True, False, torch.bfloat16).view(ctx.xshape)
-        if ctx.needs_input_grad[1]:
-            dw = _wgrad(dy2, x2, ctx.w_dtype)
-        if ctx.b_dtype is not None and ctx.needs_input_grad[2]:
-            db = _bias_grad(dy2, ctx.b_dtype)
-        return dx, dw, db
+        from p2pfl_amd.ops.fused import _fx, _wgrad as wgrad_blas
 
-
-class _LinearGeluMFMA(torch.autograd.Function):
-    """h = gelu(x W^T + b): bias and GELU in the GEMM epilogue, which also keeps
-    the pre-activation for the backward pass (no separate bias-GELU pass)."""
-
-    @staticmethod
-    @torch.amp.custom_fwd(device_type="cuda", cast_inputs=torch.bfloat16)
-    def forward(ctx, x, w, b):
-        x2 = _rows(x.to(torch.bfloat16))
-        wc = w.to(torch.bfloat16).contiguous()
-        h, z = gemm(x2, wc, bias=b, gelu=True, want_z=True)
-        ctx.save_for_backward(x2, wc, z)
-        ctx.w_dtype = w.dtype
-        ctx.b_dtype = b.dtype
-        ctx.xshape = x.shape
-        return h.view(*x.shape[:-1], w.shape[0])
-
-    @staticmethod
-    @torch.amp.custom_bwd(device_type="cuda")
-    def backward(ctx, dh):
-        from p2pfl_amd.ops.fused import _fx
-
-        x2, w, z = ctx.saved_tensors
-        dh2 = _rows(dh.to(torch.bfloat16))
-        zero = torch.zeros(z.shape[1], dtype=torch.float32, device=z.device)
-        dz, db = _fx().bias_gelu_bwd(dh2, z, zero)  # dz = dh * gelu'(z), db = column sums of dz
+        x2, w, pre, gb = ctx.saved_tensors
+        _, dg, wg = ctx.plan
+        dz = _rows(dy.to(torch.bfloat16))
+        db = None
+        if ctx.gelu:
+            dz, db = _fx().bias_gelu_bwd(dz, pre, gb)  # dz = dy * gelu'(pre), db = column sums of dz
+        elif ctx.b_dtype is not None and ctx.needs_input_grad[2]:
+            db = _bias_grad(dz, ctx.b_dtype)
         dx = dw = None
         if ctx.needs_input_grad[0]:
-            dx = _product(dz, w, True, False, torch.bfloat16).view(ctx.xshape)
+            dx = (_product(dz, w, True, False, torch.bfloat16) if dg == _NAT else torch.mm(dz, w)).view(ctx.xshape)
         if ctx.needs_input_grad[1]:
-            dw = _wgrad(dz, x2, ctx.w_dtype)
-        return dx, dw, db.to(ctx.b_dtype) if ctx.needs_input_grad[2] else None
+            dw = _wgrad(dz, x2, ctx.w_dtype) if wg == _NAT else wgrad_blas(dz, x2).to(ctx.w_dtype)
+        if db is not None and ctx.b_dtype is not None:
+            db = db.to(ctx.b_dtype)
+        return dx, dw, db if (ctx.b_dtype is not None and ctx.needs_input_grad[2]) else None, None, None
 
 
-# "native" | "library" | "auto" (measured per shape, ops/autotune.py); env P2PFL_NATIVE_GEMM.
-# The library side is hipBLASLt (ops.linear_blas) plus the fused bias+GELU kernel.
+# "native" | "library" | "auto" (measured per product and shape, ops/autotune.py); env P2PFL_NATIVE_GEMM.
+# The library side is hipBLASLt (torch.mm / F.linear) plus the fused bias+GELU kernel.
 _POLICY = autotune.policy("P2PFL_NATIVE_GEMM")
 
 
-def _native_faster(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor], gelu: bool) -> bool:
-    """Time this Linear shape once on both paths (forward, plus the input and
-    weight gradients when autograd needs them) and remember the winner."""
+def _plan(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor], gelu: bool) -> Tuple[str, str, str]:
+    """(forward, input gradient, weight gradient): each product timed once per
+    shape on both paths (HIP events, ops/autotune.py) and the winner remembered.
+    Deciding per product, not per layer, keeps e.g. a native weight gradient that
+    beats hipBLASLt even where the library forward is faster
+    (profiles/r4_gemm_w4.md: native wins all four ViT weight gradients)."""
+    if _POLICY == _NAT:
+        return _NAT, _NAT, _NAT
     grad = torch.is_grad_enabled() and (x.requires_grad or w.requires_grad)
     M = x.numel() // x.shape[-1]
     N, K = w.shape
-    key = ("linear", M, N, K, bool(gelu), bias is not None, grad)
-    if key in autotune._CHOICE:
-        return autotune._CHOICE[key] == "native"
-    from p2pfl_amd.ops.fused import bias_gelu, linear as linear_blas
+    keys = (("linear_fwd", M, N, K, bool(gelu), bias is not None), ("linear_dgrad", M, N, K), ("linear_wgrad", M, N, K))
+    got = [autotune._CHOICE.get(k) for k in keys]
+    if got[0] is not None and (not grad or (got[1] is not None and got[2] is not None)):
+        return (got[0], got[1], got[2]) if grad else (got[0], _LIB, _LIB)  # steady state: no allocation
+    if torch.cuda.is_current_stream_capturing():  # nothing can be timed inside a capture
+        return tuple(g or _NAT for g in got)  # type: ignore[return-value]
+    from p2pfl_amd.ops.fused import _fx, _wgrad as wgrad_blas
 
     x2 = x.detach().reshape(M, K).to(torch.bfloat16)
-    wd = w.detach().to(torch.bfloat16)
+    wd = w.detach().to(torch.bfloat16).contiguous()
     bd = bias.detach() if bias is not None else None
-    bd16 = bd.to(torch.bfloat16) if bd is not None else None  # the library path outside autocast needs one dtype
+    bd16 = bd.to(torch.bfloat16) if bd is not None else None
+    g32 = bd.float().contiguous() if bd is not None else None
+
+    def fwd_native():
+        gemm(x2, wd, bias=bd, gelu=gelu, want_z=gelu and grad)
+
+    def fwd_library():
+        if gelu:
+            _fx().bias_gelu_fwd(torch.mm(x2, wd.t()), g32)
+        else:
+            F.linear(x2, wd, bd16)
+
+    fwd = autotune.choose(keys[0], [(_NAT, fwd_native), (_LIB, fwd_library)])
+    if not grad:
+        return fwd, _LIB, _LIB
     dy = torch.randn(M, N, device=x.device).to(torch.bfloat16)
-
-    def native():
-        if gelu:
-            gemm(x2, wd, bias=bd, gelu=True, want_z=grad)
-        else:
-            gemm(x2, wd, bias=bd)
-        if grad:
-            _product(dy, wd, True, False, torch.bfloat16)
-            _wgrad(dy, x2, torch.bfloat16)
-
-    def library():
-        if gelu:
-            bias_gelu(linear_blas(x2, wd, None), bd)
-        else:
-            linear_blas(x2, wd, bd16)
-        if grad:
-            dy @ wd
-            dy.t() @ x2
-
-    return autotune.choose(key, [("native", native), ("library", library)]) == "native"
-
-
-def _use_native(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor], gelu: bool) -> bool:
-    if _POLICY == "library" or not _ok(x, w):
-        return False
-    return _POLICY == "native" or _native_faster(x, w, bias, gelu)
+    dg = autotune.choose(keys[1],
+                         [(_NAT, lambda: _product(dy, wd, True, False, torch.bfloat16)), (_LIB, lambda: torch.mm(dy, wd))])
+    wg = autotune.choose(keys[2],
+                         [(_NAT, lambda: _wgrad(dy, x2, torch.bfloat16)), (_LIB, lambda: wgrad_blas(dy, x2))])
+    return fwd, dg, wg
 
 
 def _ok(x: torch.Tensor, w: torch.Tensor) -> bool:
@@ -296,9 +298,9 @@ def _ok(x: torch.Tensor, w: torch.Tensor) -> bool:
 
 
 def linear(x: torch.Tensor, weight: torch.Tensor, bias: Optional[torch.Tensor] = None) -> torch.Tensor:
-    """``F.linear`` with forward, input gradient and weight gradient on the MFMA GEMM."""
-    if _use_native(x, weight, bias, False):
-        return _LinearMFMA.apply(x, weight, bias)
+    """``F.linear`` with each of its three products on the MFMA GEMM or hipBLASLt, per measured shape."""
+    if _POLICY != _LIB and _ok(x, weight):
+        return _LinearP.apply(x, weight, bias, False, _plan(x, weight, bias, False))
     if x.is_cuda:
         from p2pfl_amd.ops.fused import linear as linear_blas
 
@@ -308,8 +310,8 @@ def linear(x: torch.Tensor, weight: torch.Tensor, bias: Optional[torch.Tensor] =
 
 def linear_gelu(x: torch.Tensor, weight: torch.Tensor, bias: torch.Tensor) -> torch.Tensor:
     """``gelu(F.linear(x, weight, bias))`` (exact erf GELU), fused epilogue."""
-    if _use_native(x, weight, bias, True):
-        return _LinearGeluMFMA.apply(x, weight, bias)
+    if _POLICY != _LIB and _ok(x, weight):
+        return _LinearP.apply(x, weight, bias, True, _plan(x, weight, bias, True))
     if x.is_cuda:
         from p2pfl_amd.ops.fused import bias_gelu, linear as linear_blas
 

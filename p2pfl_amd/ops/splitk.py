@@ -96,7 +96,7 @@ def tiles_of(rows: int, cols: int) -> int:
 
 def slab_elems(rows: int, cols: int, variant: int = 0) -> int:
     """fp32 elements of one split-K slice: fragment-native tiles of the kernel the
-    variant selects (128 x 128, or 256 x 256 with bit 6 or bit 12; ``csrc/gemm_core.h`` SlabGeom),
+    variant selects (128 x 128, or 256 x 256 with bit 6; ``csrc/gemm_core.h`` SlabGeom),
     or the ping-pong kernel's row-major rows x cols."""
-    t = 256 if variant & (64 | 4096) else 128
+    t = 256 if variant & 64 else 128
     return max(rows * cols, -(-rows // t) * -(-cols // t) * t * t)

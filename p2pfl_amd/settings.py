@@ -45,6 +45,15 @@ class Settings:
     """Fan-out of one model-gossip iteration."""
     GOSSIP_EXIT_ON_X_EQUAL_ROUNDS: int = 10
     """Model gossip stops after this many identical status snapshots."""
+    GOSSIP_RELAY_GRACE: float | None = None
+    """New (exactly-once delivery): how long (s) a node lets the ORIGIN of a
+    contribution deliver it before relaying it to a peer whose
+    ``models_aggregated`` report has not moved (partial-aggregate gossip), and
+    how long it lets a train-set neighbour finish its own aggregation before
+    diffusing the full model to it.  On a full mesh every model then crosses
+    each link once; on sparse topologies a relay follows after the grace.
+    ``None``: ``GOSSIP_MODELS_PERIOD``.  0 restores the reference's eager
+    re-sends (``gossip_model_stage.py:100-104``, ``train_stage.py:134-139``)."""
 
     # ---- training --------------------------------------------------------
     ASYNC_DIFFUSION: bool = False

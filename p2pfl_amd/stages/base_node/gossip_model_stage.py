@@ -11,13 +11,14 @@ r+1 overlaps the communication of round r).
 from __future__ import annotations
 
 import threading
+import time
 from typing import Any, List, Optional, Type
 
 from p2pfl_amd.commands.add_model_command import AddModelCommand
 from p2pfl_amd.commands.models_ready_command import ModelsReadyCommand
 from p2pfl_amd.management.logger import logger
 from p2pfl_amd.settings import Settings
-from p2pfl_amd.stages.base_node.common import model_payload
+from p2pfl_amd.stages.base_node.common import DeliveryLedger, ReportClock, model_payload, relay_grace
 from p2pfl_amd.stages.stage import Stage
 from p2pfl_amd.stages.stage_factory import StageFactory
 
@@ -67,33 +68,86 @@ class GossipModelStage(Stage):
             Diffusion.start(state, protocol, aggregator, fixed_round)
             return
         logger.info(state.addr, "Gossiping aggregated model.")
+        plan = DiffusionPlan(state, protocol, aggregator, fixed_round)
 
-        def candidates() -> List[str]:
-            return [
-                n
-                for n in protocol.get_neighbors(only_direct=True)
-                if n in state.nei_status and state.nei_status[n] < fixed_round
-            ]
-
-        def model_fn(_: str) -> Any:
-            if state.learner is None or state.round is None:
+        def model_fn(n: str) -> Any:
+            if state.learner is None or state.round is None or not plan.due(n):
                 return None
-            return protocol.build_weights(
+            msg = protocol.build_weights(
                 AddModelCommand.get_name(),
                 state.round,
                 model_payload(state, protocol),
                 aggregator.get_aggregated_models(),
                 1,
             )
+            return plan.attach(n, msg)
 
         protocol.gossip_weights(
             lambda: state.round is None,
-            candidates,
-            candidates,
+            plan.candidates,
+            plan.candidates,
             model_fn,
             wakeup=state.changed,
             peer_status_fn=lambda n: state.nei_status.get(n),
         )
+
+
+class DiffusionPlan:
+    """Who gets the round's full aggregate, and when (exactly-once delivery, new).
+
+    Candidates are direct neighbours still behind ``rnd`` (reference
+    ``gossip_model_stage.py:100-104``), minus train-set members whose
+    ``models_aggregated`` report already covers the live train set: they
+    compute the identical aggregate themselves.  A train-set member that is
+    still training is left to collect the models itself; one that is
+    collecting gets the full model only after its report has not moved for
+    ``GOSSIP_RELAY_GRACE`` (it is normally a few milliseconds from
+    finishing on its own); non-members get it at once.  Nothing is offered
+    twice while on its way or delivered (:class:`DeliveryLedger`).
+    """
+
+    def __init__(self, state: Any, protocol: Any, aggregator: Any, rnd: int) -> None:
+        self.state, self.protocol, self.round = state, protocol, rnd
+        self.grace = relay_grace()
+        self.train_set = set(getattr(state, "train_set", ()) or ())
+        live = getattr(aggregator, "live_train_set", None)
+        self.live = set(live() if live is not None else ()) or set(self.train_set)
+        self.ledger = DeliveryLedger(expiry=max(4 * self.grace, Settings.GRPC_TIMEOUT))
+        self.clock = ReportClock(self._report)
+
+    def _report(self, n: str) -> Any:
+        st = self.state
+        if st.round != self.round:  # a later round reset models_aggregated
+            return (st.nei_status.get(n), None)
+        return (st.nei_status.get(n), sorted(getattr(st, "models_aggregated", {}).get(n, [])))
+
+    def _finishes_alone(self, n: str) -> bool:
+        st = self.state
+        if self.grace <= 0 or n not in self.train_set or st.round != self.round:
+            return False
+        return self.live <= set(getattr(st, "models_aggregated", {}).get(n, []))
+
+    def candidates(self) -> List[str]:
+        st = self.state
+        return [
+            n
+            for n in self.protocol.get_neighbors(only_direct=True)
+            if n in st.nei_status and st.nei_status[n] < self.round and not self._finishes_alone(n)
+        ]
+
+    def due(self, n: str) -> bool:
+        token, since = self.clock.get(n)
+        if self.ledger.covered(n, token):
+            return False
+        if self.grace <= 0 or n not in self.train_set:
+            return True
+        st = self.state
+        if st.round == self.round and n not in getattr(st, "models_aggregated", {}).get(n, []):
+            return False  # still training: it collects the round's models itself
+        return time.monotonic() - since >= self.grace
+
+    def attach(self, n: str, msg: Any) -> Any:
+        return self.ledger.attach(n, msg, self.clock.get(n)[0])
 
 
 class Diffusion:
@@ -123,6 +177,7 @@ class Diffusion:
             return protocol.build_weights(AddModelCommand.get_name(), rnd, payload, contributors, 1)
 
         d = Diffusion(state, protocol, rnd, message)
+        d.plan = DiffusionPlan(state, protocol, aggregator, rnd)
         # an older round's diffusion keeps running: a neighbour still at that
         # round needs THAT aggregate (it ignores newer-round models)
         live = [x for x in getattr(state, "diffusions", []) if x.thread.is_alive()]
@@ -131,13 +186,10 @@ class Diffusion:
         d.thread.start()
         return d
 
-    def _candidates(self) -> List[str]:
-        st = self.state
-        return [
-            n
-            for n in self.protocol.get_neighbors(only_direct=True)
-            if n in st.nei_status and st.nei_status[n] < self.round
-        ]
+    def _model(self, n: str) -> Any:
+        if not self.plan.due(n):
+            return None
+        return self.plan.attach(n, self.message())
 
     def _stop(self) -> bool:
         st = self.state
@@ -148,9 +200,9 @@ class Diffusion:
             with logger.span(self.state.addr, "async_diffusion", round=self.round):
                 self.protocol.gossip_weights(
                     self._stop,
-                    self._candidates,
-                    self._candidates,
-                    lambda _n: self.message(),
+                    self.plan.candidates,
+                    self.plan.candidates,
+                    self._model,
                     wakeup=self.state.changed,
                     peer_status_fn=lambda n: self.state.nei_status.get(n),
                 )

@@ -9,12 +9,21 @@ the full aggregate.
 
 from __future__ import annotations
 
+import time
 from typing import Any, List, Optional, Type
 
 from p2pfl_amd.commands.add_model_command import AddModelCommand
 from p2pfl_amd.commands.models_agregated_command import ModelsAggregatedCommand
 from p2pfl_amd.management.logger import logger
-from p2pfl_amd.stages.base_node.common import evaluate_and_share, model_payload, mark_dead_train_set_members
+from p2pfl_amd.settings import Settings
+from p2pfl_amd.stages.base_node.common import (
+    DeliveryLedger,
+    ReportClock,
+    evaluate_and_share,
+    mark_dead_train_set_members,
+    model_payload,
+    relay_grace,
+)
 from p2pfl_amd.stages.stage import Stage
 from p2pfl_amd.stages.stage_factory import StageFactory
 
@@ -57,8 +66,26 @@ class TrainStage(Stage):
 
     @staticmethod
     def _gossip_model_aggregation(state: Any, protocol: Any, aggregator: Any) -> None:
+        """Push partial aggregates to train-set peers until each holds every model.
+
+        Exactly-once on a full mesh (new): a node first offers a peer ONLY its
+        own model -- the one contribution nobody else can deliver -- and relays
+        models of other origins to a peer only once that peer's
+        ``models_aggregated`` report lists its own model (it is collecting, not
+        training) and has not moved for ``GOSSIP_RELAY_GRACE``
+        (on a full mesh their origins deliver them within milliseconds; on a
+        sparse topology the relay follows after the grace).  A contribution on
+        its way or delivered is never offered twice (:class:`DeliveryLedger`).
+        With ``GOSSIP_RELAY_GRACE = 0`` every push carries everything the peer
+        lacks, as in the reference (``train_stage.py:134-168``).
+        """
+        grace = relay_grace()
+        ledger = DeliveryLedger(expiry=max(4 * grace, Settings.GRPC_TIMEOUT))
+
         def peer_has(n: str) -> List[str]:
             return state.models_aggregated.get(n, [])
+
+        clock = ReportClock(lambda n: sorted(peer_has(n)))
 
         def candidates() -> List[str]:
             # A train-set peer is a candidate while it lacks some of the models
@@ -79,12 +106,29 @@ class TrainStage(Stage):
             return [(n, peer_has(n)) for n in protocol.get_neighbors(only_direct=False) if n in state.train_set]
 
         def model_fn(node: str) -> Any:
-            model, contributors, weight = aggregator.get_partial_aggregation(peer_has(node))
-            if model is None or state.round is None or state.learner is None:
+            token, since = clock.get(node)
+            known = set(peer_has(node)) | ledger.covered(node, token)
+            have = aggregator.get_aggregated_models()
+            lack = set(have) - known
+            if not lack or state.round is None or state.learner is None:
                 return None
-            return protocol.build_weights(
+            model = None
+            if grace > 0 and state.addr in lack:
+                # own model only: every other origin delivers its own
+                model, contributors, weight = aggregator.get_partial_aggregation([n for n in have if n != state.addr])
+            if model is None:
+                # relay only to a peer that is collecting (its report lists its
+                # own model) and whose report has not moved for the grace: a peer
+                # still training is not starved, its origins deliver when it is ready
+                if grace > 0 and (node not in peer_has(node) or time.monotonic() - since < grace):
+                    return None
+                model, contributors, weight = aggregator.get_partial_aggregation(sorted(known))
+            if model is None:
+                return None
+            msg = protocol.build_weights(
                 AddModelCommand.get_name(), state.round, model_payload(state, protocol, model), contributors, weight
             )
+            return ledger.attach(node, msg, token)
 
         protocol.gossip_weights(
             lambda: state.round is None,
@@ -93,8 +137,6 @@ class TrainStage(Stage):
             model_fn,
             create_connection=True,
             wakeup=state.changed,
-            # a re-send is due when the peer's report moved OR this node's own
-            # aggregate grew (a richer partial aggregate goes out at once
-            # instead of waiting a GOSSIP_MODELS_PERIOD per hop)
-            peer_status_fn=lambda n: (peer_has(n), sorted(aggregator.get_aggregated_models())),
+            # a peer is reconsidered as soon as its report moves (or a period passed)
+            peer_status_fn=lambda n: peer_has(n),
         )

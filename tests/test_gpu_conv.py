@@ -84,8 +84,12 @@ def test_conv_autograd_vs_fp32(N, C, H, W, O, k, s, p, d):
     assert conv.weight.grad.permute(0, 2, 3, 1).is_contiguous()
 
 
+@pytest.mark.parametrize("variant", [10, 4096 | 10])
 @pytest.mark.parametrize("splits", [2, 16])
-def test_conv_fwd_dgrad_split_k(splits):
+def test_conv_fwd_dgrad_split_k(splits, variant):
+    """Raw split-K slabs reduced by tile_slab_reduce with the launch's own variant --
+    also the 4-stage-ring conv (bit 12), whose slabs are 128 x 128 tiles like every
+    conv kernel's (bit 12 once meant 256 x 256 slabs to the reducer: wrong sums)."""
     N, C, H, W, O, k = 2, 128, 4, 4, 256, 3
     x, w = _operands(N, C, H, W, O, k, seed=splits, integer=True)
     from p2pfl_amd.ops.splitk import slab_elems
@@ -95,16 +99,16 @@ def test_conv_fwd_dgrad_split_k(splits):
     rows = N * H * W
     # raw fragment-native slabs (no counters), summed by tile_slab_reduce with the launch's variant
     slabs = torch.empty(splits * slab_elems(rows, O), device="cuda")
-    C_.conv_fwd(x4, w4, 1, 1, 1, slabs, splits)
+    C_.conv_fwd(x4, w4, 1, 1, 1, slabs, splits, variant)
     y = torch.empty(rows, O, device="cuda")
-    C_.tile_slab_reduce(slabs, splits, rows, O, y, 10)
+    C_.tile_slab_reduce(slabs, splits, rows, O, y, variant)
     ref = _ref(x, w, 1, 1, 1)
     torch.testing.assert_close(y.view(N, H, W, O).permute(0, 3, 1, 2), ref, atol=0, rtol=0)
     dy = torch.randint(-2, 3, (N, O, H, W), device="cuda").to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
     slabs = torch.empty(splits * slab_elems(rows, C), device="cuda")
-    C_.conv_dgrad(dy.permute(0, 2, 3, 1), w4, 1, 1, 1, slabs, [N, H, W, C], splits)
+    C_.conv_dgrad(dy.permute(0, 2, 3, 1), w4, 1, 1, 1, slabs, [N, H, W, C], splits, variant)
     dx = torch.empty(rows, C, device="cuda")
-    C_.tile_slab_reduce(slabs, splits, rows, C, dx, 10)
+    C_.tile_slab_reduce(slabs, splits, rows, C, dx, variant)
     xr = x.float().requires_grad_()
     _ref(xr, w, 1, 1, 1).backward(dy.float())
     torch.testing.assert_close(dx.view(N, H, W, C).permute(0, 3, 1, 2), xr.grad, atol=0, rtol=0)

@@ -86,13 +86,25 @@ def test_gemm_epilogue_bias_gelu_residual(bias_dtype):
     torch.testing.assert_close(z.float(), zref, atol=3e-2, rtol=8e-3)  # z is stored in bf16
 
 
+_PLANS = [None] + [(f, d, w) for f in ("native", "library") for d in ("native", "library") for w in ("native", "library")]
+
+
+@pytest.mark.parametrize("plan", _PLANS)
 @pytest.mark.parametrize("gelu", [False, True])
-def test_linear_autograd_vs_fp32(gelu):
+def test_linear_autograd_vs_fp32(gelu, plan):
+    """Every mix of paths for the three products (forward / input gradient / weight
+    gradient, chosen per product by ops.gemm._plan) against fp32; None = the measured plan."""
+    import importlib
+
+    G = importlib.import_module("p2pfl_amd.ops.gemm")  # the module (ops.gemm is the function)
     torch.manual_seed(0)
     x = torch.randn(4, 197, 768, device="cuda").to(torch.bfloat16).requires_grad_()
     w = (torch.randn(512, 768, device="cuda") * 0.03).to(torch.bfloat16).requires_grad_()
     bias = torch.randn(512, device="cuda").requires_grad_()
-    y = ops.linear_gelu(x, w, bias) if gelu else ops.linear(x, w, bias)
+    if plan is None:
+        y = ops.linear_gelu(x, w, bias) if gelu else ops.linear(x, w, bias)
+    else:
+        y = G._LinearP.apply(x, w, bias, gelu, plan)
     g = torch.randn_like(y)
     y.backward(g)
     xr, wr, br = (t.detach().float().requires_grad_() for t in (x, w, bias))
@@ -250,53 +262,3 @@ def test_in_launch_splitk_reused_workspace(splits):
     C.gemm(A.t().contiguous(), B.t().contiguous(), False, False, ws2, None, False, None, None, splits, 0, None, None)
     C.tile_slab_reduce(ws2, splits, M, N, out2, 0)
     assert torch.equal(out2, refs[-1])
-
-
-@pytest.mark.parametrize("a_kmajor,b_kmajor", [(True, True), (True, False), (False, True), (False, False)])
-@pytest.mark.parametrize("M,N,K", [(512, 512, 256), (296, 264, 128), (1000, 776, 448), (8, 8, 64)])
-def test_w4_gemm_layouts_vs_fp32(a_kmajor, b_kmajor, M, N, K):
-    """The 4-wave 256 x 256 kernel (variant bit 12, csrc/gemm_w4.hip; measured and not
-    dispatched, profiles/r4_gemm_w4.md): every layout, M / N tails, odd K-tile counts."""
-    if not a_kmajor and M % 8:
-        pytest.skip("m-major A needs M % 8 == 0")
-    a, b = _operands(M, N, K, a_kmajor, b_kmajor, seed=M + 5 * N + K)
-    out = torch.empty(M, N, device="cuda", dtype=torch.float32)
-    ops.ext().gemm(a, b, a_kmajor, b_kmajor, out, None, False, None, None, 1, 4096)
-    ref, _ = ops.gemm_reference(a, b, a_kmajor, b_kmajor)
-    torch.testing.assert_close(out, ref, atol=2e-3, rtol=1e-4)
-
-
-def test_w4_gemm_epilogues_and_split_k():
-    """4-wave kernel: bias + GELU (+ pre-activation) and residual epilogues in bf16; split-K
-    reduced in the launch (tickets) and by slabs (tile_slab_reduce), both exact on integers."""
-    from p2pfl_amd.ops.splitk import counters, slab_elems, tiles_of
-
-    C = ops.ext()
-    M, N, K = 1000, 768, 768
-    a, b = _operands(M, N, K, True, True, seed=21)
-    bias = torch.randn(N, device="cuda")
-    res = torch.randn(M, N, device="cuda").to(torch.bfloat16)
-    out = torch.empty(M, N, device="cuda", dtype=torch.bfloat16)
-    z = torch.empty_like(out)
-    C.gemm(a, b, True, True, out, bias, True, z, None, 1, 4096)
-    ref, zr = ops.gemm_reference(a, b, True, True, bias, True)
-    torch.testing.assert_close(z.float(), zr, atol=0.25, rtol=1e-2)
-    torch.testing.assert_close(out.float(), ref, atol=0.25, rtol=1e-2)
-    C.gemm(a, b, True, True, out, bias, False, None, res, 1, 4096)
-    ref, _ = ops.gemm_reference(a, b, True, True, bias, False, res)
-    torch.testing.assert_close(out.float(), ref, atol=0.25, rtol=1e-2)
-    g = torch.Generator(device="cuda").manual_seed(22)
-    Mw, Nw, Kw = 768, 512, 6304
-    A = torch.randint(-2, 3, (Mw, Kw), device="cuda", generator=g).to(torch.bfloat16)
-    B = torch.randint(-2, 3, (Nw, Kw), device="cuda", generator=g).to(torch.bfloat16)
-    want = A.float() @ B.float().t()
-    for splits in (3, 6):
-        ws = torch.empty(splits * slab_elems(Mw, Nw, 4096), device="cuda")
-        o = torch.empty(Mw, Nw, device="cuda", dtype=torch.float32)
-        C.gemm(A.t().contiguous(), B.t().contiguous(), False, False, o, None, False, None, None, splits, 4096, ws,
-               counters(tiles_of(Mw, Nw), o.device))
-        assert torch.equal(o, want)
-        o2 = torch.empty_like(o)
-        C.gemm(A.t().contiguous(), B.t().contiguous(), False, False, ws, None, False, None, None, splits, 4096, None, None)
-        C.tile_slab_reduce(ws, splits, Mw, Nw, o2, 4096)
-        assert torch.equal(o2, want)

@@ -184,6 +184,41 @@ def test_three_processes_push_to_each_other_full_stack():
     assert len(recvs) == 3
 
 
+def _plane_lines(stderr: str):
+    """rank -> (sends, receives, MB sent) from bench.py's per-rank summary lines."""
+    import re
+
+    out = {}
+    for ln in stderr.splitlines():
+        m = re.search(r"\[bench rank (\d+)\] per-round .*data plane: (\d+) sends / (\d+) recvs .*xgmi bytes sent ([\d.]+) MB", ln)
+        if m:
+            out[int(m.group(1))] = (int(m.group(2)), int(m.group(3)), float(m.group(4)))
+    return out
+
+
+@pytest.mark.timeout(600)
+@pytest.mark.parametrize("n", [4, 6])
+def test_full_mesh_round_moves_each_model_exactly_once(n):
+    """Full mesh, every peer in the train set: each round every model crosses
+    each link once -- N - 1 pushes per rank per round, plus the N - 1 pushes of
+    the initial model -- and nothing else (no relayed partials, no diffusion of
+    the full aggregate to peers that finish on their own).  Reference schedule
+    being replaced: gossip_model_stage.py:100-104, gossiper.py:228-239."""
+    W, K = 1, 2
+    cmd = [sys.executable, "bench.py", "--gpus", str(n), "--steps", str(K), "--warmup", str(W), "--impl", "torch",
+           "--number-sub", "800", "--watchdog", "300"]
+    r = subprocess.run(cmd, cwd=ROOT, env=_env(), capture_output=True, text=True, timeout=560)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
+    lines = _plane_lines(r.stderr)
+    assert sorted(lines) == list(range(n)), r.stderr[-3000:]
+    rounds = W + K
+    total_sends = sum(v[0] for v in lines.values())
+    assert total_sends == rounds * n * (n - 1) + (n - 1), lines
+    assert sum(v[1] for v in lines.values()) == total_sends
+    for rank, (sends, _, _) in lines.items():
+        assert rounds * (n - 1) <= sends <= (rounds + 1) * (n - 1), (rank, lines)
+
+
 @pytest.mark.timeout(600)
 def test_rank_killed_mid_transfer_survivors_finish():
     port = _free_port()
