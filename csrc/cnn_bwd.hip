@@ -681,6 +681,28 @@ P2_DEVICE void glds_copy(const uint16_t* src, char* dst, int bytes, int wave, in
                                      (__attribute__((address_space(3))) void*)(dst + c * 1024), 16, 0, 0);
 }
 
+// Row-swizzled variant for images of CPR 16-byte chunks per row: LDS chunk j of
+// row rho holds source chunk j ^ wg_swz(rho).  The wgrad blocks read 16 B per lane
+// from 32 consecutive rows at one column; with rows of 448 B (dC2, 28 chunks) or
+// 576 B (P1 planes, 36 chunks) rows r and r + 4 hit the same 16-byte bank slot, a
+// 4-way conflict on every ds_read_b128 (profiles/r4_cnn_pmc.md: 58 % of the
+// kernel's LDS cycles).  XOR-ing the low two chunk bits with (row >> 2) & 3 spreads
+// every 16-lane read group over all 16 slots.  The destination stays lane-linear
+// (LDS-DMA), the permutation is applied to the source address (CPR % 4 == 0 keeps
+// it inside the row).
+P2_DEVICE int wg_swz(int row) { return (row >> 2) & 3; }
+
+template <int CPR>
+P2_DEVICE void glds_copy_swz(const uint16_t* src, char* dst, int bytes, int wave, int lane) {
+  static_assert(CPR % 4 == 0, "the swizzle permutes chunk groups of 4 inside a row");
+  for (int c = wave; c * 1024 < bytes; c += 4) {
+    const int q = c * 64 + lane, rho = q / CPR, j = q - rho * CPR;
+    const int sq = rho * CPR + (j ^ wg_swz(rho));
+    __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(src + sq * 8),
+                                     (__attribute__((address_space(3))) void*)(dst + c * 1024), 16, 0, 0);
+  }
+}
+
 P2_DEVICE void conv2_wgrad_block(int g, int kx, const uint16_t* __restrict__ dc2m, const uint16_t* __restrict__ p1s,
                                  float* __restrict__ wslab, int B, char* smem) {
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, r = lane & 31, h = lane >> 5;
@@ -689,22 +711,27 @@ P2_DEVICE void conv2_wgrad_block(int g, int kx, const uint16_t* __restrict__ dc2
   const uint16_t* sb = reinterpret_cast<const uint16_t*>(smem + kWgA);
   // the pair's images are consecutive in the dC2 map; the P1 planes of one kx
   // are one contiguous [ic][plane] block per image
-  glds_copy(dc2m + size_t(b0) * kC2 * 224, smem, nb * kC2 * 224 * 2, wave, lane);
+  static_assert(224 % 32 == 0 && kP1sPlane % 32 == 0, "whole 16-B chunk groups per row");
+  glds_copy_swz<224 / 8>(dc2m + size_t(b0) * kC2 * 224, smem, nb * kC2 * 224 * 2, wave, lane);
   for (int i = 0; i < nb; ++i)
-    glds_copy(p1s + (size_t(b0 + i) * 5 + kx) * kC1 * kP1sPlane, smem + kWgA + i * (kC1 * kP1sPlane * 2),
-              kC1 * kP1sPlane * 2, wave, lane);
+    glds_copy_swz<kP1sPlane / 8>(p1s + (size_t(b0 + i) * 5 + kx) * kC1 * kP1sPlane,
+                                 smem + kWgA + i * (kC1 * kP1sPlane * 2), kC1 * kP1sPlane * 2, wave, lane);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
+  // rows i * kC2 + r (+ 32) and i * kC1 + r all have wg_swz == wg_swz(r)
+  const int t = h ^ wg_swz(r);
   for (int ky = wave; ky < 5; ky += 4) {
     f32x16 acc0 = {}, acc1 = {};
     for (int i = 0; i < nb; ++i) {
-      const uint16_t* a = sa + (i * kC2 + r) * 224 + 8 * h;
-      const uint16_t* bb = sb + (i * kC1 + r) * kP1sPlane + ky * 16 + 8 * h;
+      const uint16_t* a = sa + (i * kC2 + r) * 224;
+      const uint16_t* bb = sb + (i * kC1 + r) * kP1sPlane;
 #pragma unroll
       for (int ks = 0; ks < 14; ++ks) {
-        const uint4 a0 = *reinterpret_cast<const uint4*>(a + ks * 16);
-        const uint4 a1 = *reinterpret_cast<const uint4*>(a + 32 * 224 + ks * 16);
-        const uint4 bq = *reinterpret_cast<const uint4*>(bb + ks * 16);
+        // chunk 2 ks + h of the row, and chunk 2 (ky + ks) + h of the P1 plane, swizzled
+        const int ca = (2 * ks) ^ t, cb = (2 * (ky + ks)) ^ t;
+        const uint4 a0 = *reinterpret_cast<const uint4*>(a + 8 * ca);
+        const uint4 a1 = *reinterpret_cast<const uint4*>(a + 32 * 224 + 8 * ca);
+        const uint4 bq = *reinterpret_cast<const uint4*>(bb + 8 * cb);
         acc0 = mfma32b(a0, bq, acc0);
         acc1 = mfma32b(a1, bq, acc1);
       }

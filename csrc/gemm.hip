@@ -40,35 +40,44 @@
 
 namespace p2gemm {
 
-template <int NBUF, class LA, class LB>
+template <int NBUF, class LA, class LB, int EPI>
 __global__ __launch_bounds__(NT, NBUF == 1 ? 4 : (NBUF == 2 ? 2 : 1)) void gemm_kernel(GemmParams p, LA la, LB lb, int tiles_m, int tiles_n) {
   __shared__ __attribute__((aligned(16))) char smem[smem_bytes<Tile128, NBUF>()];  // [buf][A | B]
-  gemm_body<Tile128, NBUF>(p, la, lb, tiles_m, tiles_n, smem);
+  gemm_body<Tile128, NBUF, LA, LB, 0, EPI>(p, la, lb, tiles_m, tiles_n, smem);
 }
 
 // 256 x 256 tile, 8 waves, one workgroup per CU (132 KB of LDS, up to 256
 // registers per lane at two waves per SIMD).
-template <class LA, class LB>
+template <class LA, class LB, int EPI>
 __global__ __launch_bounds__(Tile256::NT) void gemm256_kernel(GemmParams p, LA la, LB lb, int tiles_m, int tiles_n) {
   __shared__ __attribute__((aligned(16))) char smem[smem_bytes<Tile256, 2>()];
-  gemm_body<Tile256, 2>(p, la, lb, tiles_m, tiles_n, smem);
+  gemm_body<Tile256, 2, LA, LB, 0, EPI>(p, la, lb, tiles_m, tiles_n, smem);
 }
 
-template <class LA, class LB>
-static void launch(const GemmParams& p, const LA& la, const LB& lb, hipStream_t s) {
+template <int EPI, class LA, class LB>
+static void launch_e(const GemmParams& p, const LA& la, const LB& lb, hipStream_t s) {
   int tm, tn;
   if (p.variant & 64) {
     const int grid = gemm_grid<Tile256>(p, tm, tn);
-    hipLaunchKernelGGL((gemm256_kernel<LA, LB>), dim3(grid), dim3(Tile256::NT), 0, s, p, la, lb, tm, tn);
+    hipLaunchKernelGGL((gemm256_kernel<LA, LB, EPI>), dim3(grid), dim3(Tile256::NT), 0, s, p, la, lb, tm, tn);
     return;
   }
   const int grid = gemm_grid<Tile128>(p, tm, tn);
   if (p.variant & 4096)  // 4-stage ring (3 K-tiles in flight), one workgroup per CU: short-K products
-    hipLaunchKernelGGL((gemm_kernel<4, LA, LB>), dim3(grid), dim3(NT), 0, s, p, la, lb, tm, tn);
+    hipLaunchKernelGGL((gemm_kernel<4, LA, LB, EPI>), dim3(grid), dim3(NT), 0, s, p, la, lb, tm, tn);
   else if (p.variant & 8)
-    hipLaunchKernelGGL((gemm_kernel<1, LA, LB>), dim3(grid), dim3(NT), 0, s, p, la, lb, tm, tn);
+    hipLaunchKernelGGL((gemm_kernel<1, LA, LB, EPI>), dim3(grid), dim3(NT), 0, s, p, la, lb, tm, tn);
   else
-    hipLaunchKernelGGL((gemm_kernel<2, LA, LB>), dim3(grid), dim3(NT), 0, s, p, la, lb, tm, tn);
+    hipLaunchKernelGGL((gemm_kernel<2, LA, LB, EPI>), dim3(grid), dim3(NT), 0, s, p, la, lb, tm, tn);
+}
+
+template <class LA, class LB>
+static void launch(const GemmParams& p, const LA& la, const LB& lb, hipStream_t s) {
+  switch (epilogue_kind(p)) {
+    case 0: launch_e<0>(p, la, lb, s); break;
+    case 2: launch_e<2>(p, la, lb, s); break;
+    default: launch_e<1>(p, la, lb, s);
+  }
 }
 
 }  // namespace p2gemm

@@ -235,6 +235,17 @@ P2_DEVICE void vmcnt_tiles(int n) {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
 
+// A launch whose epilogue is a plain store of C (no split-K, bias, GELU,
+// residual or BatchNorm statistics): kernels instantiate a compact epilogue for it.
+inline bool plain_epilogue(const GemmParams& p) {
+  return p.splits <= 1 && !p.bias && !p.gelu && !p.residual && !p.bn.part;
+}
+// 0: plain store, 2: + bias only (the Linear forward), 1: everything behind runtime flags
+inline int epilogue_kind(const GemmParams& p) {
+  if (plain_epilogue(p)) return 0;
+  return (p.splits <= 1 && !p.gelu && !p.residual && !p.bn.part) ? 2 : 1;
+}
+
 // Output tile (tm, tn) of linear tile index t (see the tile-order note in gemm_body).
 P2_DEVICE void tile_coords(int variant, int t, int tiles_m, int tiles_n, int& tm, int& tn) {
   if (variant & 256) {
@@ -397,7 +408,10 @@ P2_DEVICE void bn_epilogue_reduce(const GemmParams& p, Moments mo, int tm, int t
 // The whole kernel body.  `p` carries M/N/K, split-K and the epilogue.
 // BN: compile the BatchNorm statistics epilogue in (GemmParams::bn; the conv
 // kernels that produce a BN input instantiate it, the Linear GEMMs do not)
-template <class CFG, int NBUF, class LA, class LB, int BN = 0>
+// EPI (epilogue_kind): 0 compact epilogue for plain stores, 2 bias only (see
+// gemm_pp.hip's note on instruction fetch); 1 every epilogue feature behind
+// runtime flags.
+template <class CFG, int NBUF, class LA, class LB, int BN = 0, int EPI = 1>
 P2_DEVICE void gemm_body(const GemmParams& p, const LA& la, const LB& lb, int tiles_m, int tiles_n, char* smem) {
   constexpr int FM = CFG::FM, FN = CFG::FN, HA = CFG::HA, HB = CFG::HB, G = CFG::GROUPS;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -556,7 +570,7 @@ P2_DEVICE void gemm_body(const GemmParams& p, const LA& la, const LB& lb, int ti
   const int h = lane >> 5;
   auto row_of = [&](int i) { return m0 + wm * 32 * FM + i * 32 + (lane & 31); };
   auto col_of = [&](int j, int g) { return n0 + wn * 32 * FN + j * 32 + 8 * g + 4 * h; };
-  if (p.splits > 1) {
+  if (EPI == 1 && p.splits > 1) {
     // every K-slice writes its raw fp32 partial tile, fragment-native (SlabGeom)
     using SG = SlabGeom<CFG>;
     float* slabs = p.counters ? p.ws : reinterpret_cast<float*>(p.c);
@@ -789,6 +803,7 @@ P2_DEVICE void gemm_body(const GemmParams& p, const LA& la, const LB& lb, int ti
     __syncthreads();  // the bf16 staging below reuses the LDS
   }
   // bias, GELU (+ pre-activation, stored directly), residual: in place on acc
+  if constexpr (EPI != 0)
 #pragma unroll
   for (int i = 0; i < FM; ++i)
 #pragma unroll
@@ -805,23 +820,41 @@ P2_DEVICE void gemm_body(const GemmParams& p, const LA& la, const LB& lb, int ti
                                 : reinterpret_cast<const float*>(p.bias)[n + e];
         }
         const int64_t off = int64_t(m) * p.ldc + n;
-        if (p.gelu) {
-          if (p.z) *reinterpret_cast<uint2*>(p.z + off) = uint2{pack_bf16x2(v[0], v[1]), pack_bf16x2(v[2], v[3])};
+        if constexpr (EPI == 1) {
+          if (p.gelu) {
+            if (p.z) *reinterpret_cast<uint2*>(p.z + off) = uint2{pack_bf16x2(v[0], v[1]), pack_bf16x2(v[2], v[3])};
 #pragma unroll
-          for (int e = 0; e < 4; ++e) v[e] = gelu_f(v[e]);
-        }
-        if (p.residual) {
-          const uint2 rr = *reinterpret_cast<const uint2*>(p.residual + off);
-          v[0] += __uint_as_float(rr.x << 16);
-          v[1] += __uint_as_float(rr.x & 0xffff0000u);
-          v[2] += __uint_as_float(rr.y << 16);
-          v[3] += __uint_as_float(rr.y & 0xffff0000u);
+            for (int e = 0; e < 4; ++e) v[e] = gelu_f(v[e]);
+          }
+          if (p.residual) {
+            const uint2 rr = *reinterpret_cast<const uint2*>(p.residual + off);
+            v[0] += __uint_as_float(rr.x << 16);
+            v[1] += __uint_as_float(rr.x & 0xffff0000u);
+            v[2] += __uint_as_float(rr.y << 16);
+            v[3] += __uint_as_float(rr.y & 0xffff0000u);
+          }
         }
         if (!p.c_bf16)
           *reinterpret_cast<f32x4*>(reinterpret_cast<float*>(p.c) + off) = f32x4{v[0], v[1], v[2], v[3]};
 #pragma unroll
         for (int e = 0; e < 4; ++e) acc[i][j][4 * g + e] = v[e];
       }
+  if constexpr (EPI == 0) {
+    if (!p.c_bf16) {
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int j = 0; j < FN; ++j)
+#pragma unroll
+          for (int g = 0; g < 4; ++g) {
+            const int m = row_of(i), n = col_of(j, g);
+            if (m < p.M && n < p.N)
+              *reinterpret_cast<f32x4*>(reinterpret_cast<float*>(p.c) + int64_t(m) * p.ldc + n) =
+                  f32x4{acc[i][j][4 * g], acc[i][j][4 * g + 1], acc[i][j][4 * g + 2], acc[i][j][4 * g + 3]};
+          }
+      return;
+    }
+  }
   if (!p.c_bf16) return;
   // bf16 C goes out through LDS: a lane's 4-column groups sit on 32 different
   // rows, so direct 8-byte stores scatter over 32 rows per instruction; staged

@@ -127,7 +127,13 @@ P2_DEVICE uint32_t mn_base(int rb, int t, int lane) {
   return row * 256 + (((col >> 3) ^ swz_mn(row)) << 4) + (col & 7) * 2;
 }
 
-template <class SA, class SB, bool KA, bool KB>
+// EPI (epilogue_kind): 0 = plain product (no split-K, bias, GELU, residual),
+// 2 = bias only, 1 = every epilogue feature behind runtime flags.  The plain instance's epilogue is a few hundred
+// instructions instead of ~60 KB of unrolled bias / GELU / split-K code: run once
+// per tile, straight-line, that code is fetched cold from L2 by every workgroup,
+// and on the short-K ViT products the fetch stalls cost more than the stores
+// (scripts/gemm_anatomy.py: 12.5 us for a launch with the K loop switched off).
+template <class SA, class SB, bool KA, bool KB, int EPI>
 __global__ __launch_bounds__(512) void gemm_pp_kernel(GemmParams p, int tiles_m, int tiles_n) {
   __shared__ __attribute__((aligned(16))) char smem[smem_bytes<PPCfg, 2>()];
   constexpr int FM = PPCfg::FM, FN = PPCfg::FN, STG = PPCfg::STAGE;
@@ -351,7 +357,7 @@ __global__ __launch_bounds__(512) void gemm_pp_kernel(GemmParams p, int tiles_m,
   constexpr int LROW = 256 * 2 + 16;  // bf16 staging image [256][256] + 16 B row pad
   const int64_t mn = int64_t(p.M) * p.N;
   float* slabs = p.counters ? p.ws : reinterpret_cast<float*>(p.c);
-  if (p.splits > 1) {
+  if (EPI == 1 && p.splits > 1) {
 #pragma unroll
     for (int i = 0; i < FM; ++i)
 #pragma unroll
@@ -388,13 +394,15 @@ __global__ __launch_bounds__(512) void gemm_pp_kernel(GemmParams p, int tiles_m,
     const int m = row_of(i), n = col_of(j, g);
     if (m >= p.M || n >= p.N) return;
     float v[4] = {v0, v1, v2, v3};
+    const int64_t off = int64_t(m) * p.ldc + n;
+    if constexpr (EPI != 0) {
     if (p.bias) {
 #pragma unroll
       for (int e = 0; e < 4; ++e)
         v[e] += p.bias_bf16 ? bf16_to_f32(reinterpret_cast<const uint16_t*>(p.bias)[n + e])
                             : reinterpret_cast<const float*>(p.bias)[n + e];
     }
-    const int64_t off = int64_t(m) * p.ldc + n;
+    if constexpr (EPI == 1) {
     if (p.gelu) {
       if (p.z) *reinterpret_cast<uint2*>(p.z + off) = uint2{pack_bf16x2(v[0], v[1]), pack_bf16x2(v[2], v[3])};
 #pragma unroll
@@ -407,6 +415,8 @@ __global__ __launch_bounds__(512) void gemm_pp_kernel(GemmParams p, int tiles_m,
       v[2] += __uint_as_float(rr.y << 16);
       v[3] += __uint_as_float(rr.y & 0xffff0000u);
     }
+    }
+    }
     if (!p.c_bf16) {
       *reinterpret_cast<f32x4*>(reinterpret_cast<float*>(p.c) + off) = f32x4{v[0], v[1], v[2], v[3]};
     } else {
@@ -414,7 +424,7 @@ __global__ __launch_bounds__(512) void gemm_pp_kernel(GemmParams p, int tiles_m,
       *reinterpret_cast<uint2*>(smem + r * LROW + c * 2) = uint2{pack_bf16x2(v[0], v[1]), pack_bf16x2(v[2], v[3])};
     }
   };
-  if (p.splits > 1) {  // the reducer: one 4-value group of all slices at a time (acc is in its own slab)
+  if (EPI == 1 && p.splits > 1) {  // the reducer: one 4-value group of all slices at a time (acc is in its own slab)
     for (int i = 0; i < FM; ++i)
       for (int j = 0; j < FN; ++j)
         for (int g = 0; g < 4; ++g) {
@@ -449,7 +459,16 @@ template <bool KA, bool KB>
 static void launch_pp(const GemmParams& p, hipStream_t s) {
   const int tm = (p.M + 255) / 256, tn = (p.N + 255) / 256;
   const int grid = tm * tn * (p.splits > 1 ? p.splits : 1);
-  hipLaunchKernelGGL((gemm_pp_kernel<PPSrc<KA>, PPSrc<KB>, KA, KB>), dim3(grid), dim3(512), 0, s, p, tm, tn);
+  switch (epilogue_kind(p)) {
+    case 0:
+      hipLaunchKernelGGL((gemm_pp_kernel<PPSrc<KA>, PPSrc<KB>, KA, KB, 0>), dim3(grid), dim3(512), 0, s, p, tm, tn);
+      break;
+    case 2:
+      hipLaunchKernelGGL((gemm_pp_kernel<PPSrc<KA>, PPSrc<KB>, KA, KB, 2>), dim3(grid), dim3(512), 0, s, p, tm, tn);
+      break;
+    default:
+      hipLaunchKernelGGL((gemm_pp_kernel<PPSrc<KA>, PPSrc<KB>, KA, KB, 1>), dim3(grid), dim3(512), 0, s, p, tm, tn);
+  }
 }
 
 }  // namespace p2gemm

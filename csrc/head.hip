@@ -101,8 +101,12 @@ __global__ __launch_bounds__(kT) void head_fwd_kernel(const uint16_t* __restrict
       }
     float se = 0.f;
     for (int n = 0; n < N; ++n) se += __expf(lg[n] - mx);
-    const int yy = min(max(int(y[b]), 0), N - 1);
-    const float lv = (logf(se) + mx) - lg[yy];
+    // a label outside [0, N) (F.cross_entropy raises; ignore_index is not
+    // supported here) makes the loss NaN instead of a finite wrong value
+    const int64_t yl = y[b];
+    const bool ok = yl >= 0 && yl < N;
+    const int yy = ok ? int(yl) : 0;
+    const float lv = ok ? (logf(se) + mx) - lg[yy] : __builtin_nanf("");
     st_sc1f(loss_rows + b, lv);
     st_sc1f(loss_rows + B + b, arg == yy ? 1.f : 0.f);
   }
@@ -126,7 +130,12 @@ __global__ __launch_bounds__(kT) void head_fwd_kernel(const uint16_t* __restrict
 }
 
 // dl[n] of sample b: (softmax(logits_b)[n] - [n == y_b]) * gscale
-P2_DEVICE void dlogits(const float* lg, int yy, int N, float gscale, float* dl) {
+P2_DEVICE void dlogits(const float* lg, int64_t yl, int N, float gscale, float* dl) {
+  if (yl < 0 || yl >= N) {  // out-of-range label: NaN gradient, never a silently wrong one
+    for (int n = 0; n < N; ++n) dl[n] = __builtin_nanf("");
+    return;
+  }
+  const int yy = int(yl);
   float mx = lg[0];
   for (int n = 1; n < N; ++n) mx = fmaxf(mx, lg[n]);
   float se = 0.f;
@@ -145,7 +154,7 @@ __global__ __launch_bounds__(kT) void head_bwd_kernel(const float* __restrict__ 
   const int b = blockIdx.x, tid = threadIdx.x;
   const float gscale = gloss[0] / float(B);
   if (b < B) {
-    if (tid == 0) dlogits(logits + int64_t(b) * N, min(max(int(y[b]), 0), N - 1), N, gscale, dl);
+    if (tid == 0) dlogits(logits + int64_t(b) * N, y[b], N, gscale, dl);
     __syncthreads();
     const float inv = 1.f / float(HW);
     uint16_t* out = df + int64_t(b) * HW * C;
@@ -171,7 +180,7 @@ __global__ __launch_bounds__(kT) void head_bwd_kernel(const float* __restrict__ 
   for (int b0 = 0; b0 < B; b0 += 64) {
     const int nb = min(64, B - b0);
     __syncthreads();
-    if (tid < nb) dlogits(logits + int64_t(b0 + tid) * N, min(max(int(y[b0 + tid]), 0), N - 1), N, gscale, dla[tid]);
+    if (tid < nb) dlogits(logits + int64_t(b0 + tid) * N, y[b0 + tid], N, gscale, dla[tid]);
     __syncthreads();
     if (live) {
       int i = 0;

@@ -273,6 +273,9 @@ class FusedCNNLearner(TorchLearner):
         self.use_graphs = use_graphs
         self._graphs: Dict[str, _EpochGraph] = {}
         self._lock = make_rlock("FusedCNNLearner._lock")  # fit() -> _validate() re-enters
+        # one capture per pass key: fit() and the evaluation thread may both
+        # reach _ensure_graph for a pass that has no graph yet
+        self._graph_build_lock = make_lock("FusedCNNLearner._graph_build_lock")
         self._stream = private_stream(self.device)
         self._dirty_shadows = False
         self._eval_fwd = _EvalForward(self.engine)
@@ -319,14 +322,18 @@ class FusedCNNLearner(TorchLearner):
 
         plan, key = self._graph_key(name, loader, train)
         g = self._graphs.get(name)
-        if g is None or g.key != key:
-            import gc
+        if g is not None and g.key == key:
+            return g
+        with self._graph_build_lock:
+            g = self._graphs.get(name)
+            if g is None or g.key != key:
+                import gc
 
-            with GATE.shared():  # outside the exclusive section, never during another thread's capture
-                gc.collect()
-            with GATE.exclusive():  # no other learner's GPU work during the capture
-                g = self._capture(name, loader, plan, train, key)
-            self._graphs[name] = g
+                with GATE.shared():  # outside the exclusive section, never during another thread's capture
+                    gc.collect()
+                with GATE.exclusive():  # no other learner's GPU work during the capture
+                    g = self._capture(name, loader, plan, train, key)
+                self._graphs[name] = g
         return g
 
     def _run(self, name: str, loader, train: bool, perm: Optional[torch.Tensor]) -> torch.Tensor:
@@ -365,18 +372,16 @@ class FusedCNNLearner(TorchLearner):
             return eg
         from p2pfl_amd.learning.step_graph import no_gc
 
-        # capture on a side stream; state that the graph mutates (weights,
-        # Adam moments, step counter) is saved and restored around the capture
+        # capture on a side stream.  Recording executes nothing, so the state the
+        # graph mutates (weights, Adam moments, step counter) is untouched -- no
+        # save / restore, which could also overwrite a set_parameters copy that
+        # landed meanwhile
         with _CAPTURE_LOCK:
             torch.cuda.synchronize(self.device)
-            saved = [t.clone() for t in (self.engine.params, self.engine.m, self.engine.v, self.engine.adam_t)]
             graph = torch.cuda.CUDAGraph()
             with no_gc(collect=False), torch.cuda.graph(graph, stream=self._stream, capture_error_mode="relaxed"):
                 self._enqueue(loader, plan, train, eg.perm, eg.stats)
             torch.cuda.synchronize(self.device)
-            for dst, src in zip((self.engine.params, self.engine.m, self.engine.v, self.engine.adam_t), saved):
-                dst.copy_(src)
-            self.engine.pack_shadows()
         eg.graph = graph
         return eg
 

@@ -55,9 +55,13 @@ class DeviceGate:
         self._cv = threading.Condition()
         self._shared = 0
         self._excl = False
+        self._owner: Optional[int] = None  # thread holding the gate exclusively
 
     @contextmanager
     def shared(self):
+        if self._owner == threading.get_ident():  # the exclusive holder already has the device
+            yield
+            return
         with self._cv:
             while self._excl:
                 self._cv.wait()
@@ -75,15 +79,41 @@ class DeviceGate:
             while self._excl or self._shared:
                 self._cv.wait()
             self._excl = True
+            self._owner = threading.get_ident()
         try:
             yield
         finally:
             with self._cv:
                 self._excl = False
+                self._owner = None
                 self._cv.notify_all()
 
 
 GATE = DeviceGate()
+
+# First warm-ups per model structure: the first peer of a process to warm up a
+# given step runs it with the device to itself -- its per-shape autotune timings
+# (ops/autotune.py, cached process-wide) then see no other peer's kernels, and
+# the other peers' warm-ups, which follow under the shared gate, find every
+# choice made (the round-4 overlap run: eight peers timing and capturing at
+# once made the first round 2.4x longer).
+_WARMED: set = set()
+_WARM_LOCK = threading.Lock()
+
+
+@contextmanager
+def warmup_gate(key: Tuple):
+    """Exclusive gate for the first warm-up of ``key`` in this process, shared after."""
+    with _WARM_LOCK:
+        first = key not in _WARMED
+    if not first:
+        with GATE.shared():
+            yield
+        return
+    with GATE.exclusive():
+        yield
+    with _WARM_LOCK:
+        _WARMED.add(key)
 
 
 @contextmanager
@@ -151,18 +181,21 @@ class TrainStepGraph:
 
         The warm-up step does every lazy first use -- workspaces, the per-shape
         autotune timing (``ops/autotune.py``), library solver choices -- which
-        can take seconds on a fresh device.  It is ordinary eager work, so it
-        runs under the SHARED gate next to the other peers' steps; only the
-        capture itself (host-side recording, no kernel executes) takes the gate
-        exclusively, so a capturing peer never stalls the others for longer
-        than the recording (reference requirement: training must not stall the
-        node, ``train_stage.py:88-93``).
+        can take seconds on a fresh device.  The first warm-up of a model
+        structure in the process takes the gate exclusively (clean autotune
+        timings, see :func:`warmup_gate`); later ones are ordinary eager work
+        under the SHARED gate next to the other peers' steps.  The capture
+        itself (host-side recording, no kernel executes) takes the gate
+        exclusively, so a capturing peer stalls the others only for the
+        recording (reference requirement: training must not stall the node,
+        ``train_stage.py:88-93``).
         """
         learner, opt = self.learner, self.opt
         arena = learner.arena
         dev = learner.device
         cur = torch.cuda.current_stream(dev)
-        with GATE.shared():
+        wkey = ("train", type(learner.model).__name__, self.B, tuple(self.loader.x.shape[1:]), opt.config())
+        with warmup_gate(wkey):
             self.stream.wait_stream(cur)
             with torch.cuda.stream(self.stream):
                 keep = [t for t in [arena.flat, arena.shadow] + opt.state_tensors() if t is not None]
@@ -254,7 +287,8 @@ class EvalStepGraph:
     def capture(self, idx: torch.Tensor) -> None:
         learner = self.learner
         cur = torch.cuda.current_stream(learner.device)
-        with GATE.shared():  # warm-up (first-use work, creates the sums) next to the other peers
+        wkey = ("eval", type(learner.model).__name__, self.key[0], self.B, tuple(self.loader.x.shape[1:]))
+        with warmup_gate(wkey):  # warm-up (first-use work, creates the sums): alone the first time, then shared
             self.stream.wait_stream(cur)
             with torch.cuda.stream(self.stream):
                 self.idx.copy_(idx)

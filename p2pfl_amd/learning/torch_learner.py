@@ -29,7 +29,6 @@ from __future__ import annotations
 import os
 import contextlib
 import threading
-import weakref
 from collections import OrderedDict
 from typing import Any, Dict, Mapping, Optional, Tuple
 
@@ -48,14 +47,6 @@ from p2pfl_amd.utils import finite
 
 def default_device() -> torch.device:
     return torch.device("cuda", torch.cuda.current_device()) if torch.cuda.is_available() else torch.device("cpu")
-
-
-# live GPU learners of this process, for Settings.NODE_STREAMS == "auto"
-_LEARNERS: "weakref.WeakSet[TorchLearner]" = weakref.WeakSet()
-
-
-def _shares_device(learner: "TorchLearner") -> bool:
-    return any(o is not learner and o.device == learner.device and o.model is not None for o in list(_LEARNERS))
 
 
 class TorchLearner(NodeLearner):
@@ -110,8 +101,6 @@ class TorchLearner(NodeLearner):
         # one process train concurrently, and their training overlaps the
         # aggregation / transport work left on the default stream
         self._compute_stream: Optional[torch.cuda.Stream] = None
-        if self.device.type == "cuda":
-            _LEARNERS.add(self)
         self._step_graph: Any = None
         self._eval_graphs: Dict[str, Any] = {}
         self.model: Any = None
@@ -169,7 +158,7 @@ class TorchLearner(NodeLearner):
         if self.device.type != "cuda":
             return None
         mode = Settings.NODE_STREAMS
-        want = _shares_device(self) if mode == "auto" else bool(mode)
+        want = True if mode == "auto" else bool(mode)
         if not want:
             return None
         if self._compute_stream is None:
@@ -185,8 +174,8 @@ class TorchLearner(NodeLearner):
         aggregate a ``set_parameters`` copies), and the caller's stream -- the
         default stream every other thread of the node enqueues on (gossip
         snapshots, FedAvg, transport producer events) -- waits for the block's
-        kernels afterwards.  With one learner per GPU (``NODE_STREAMS="auto"``)
-        everything simply runs on the caller's stream.
+        kernels afterwards.  With ``NODE_STREAMS=False`` everything simply runs
+        on the caller's stream.
         """
         cs = self._stream_for_block()
         cur = torch.cuda.current_stream(self.device) if cs is not None else None

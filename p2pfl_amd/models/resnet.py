@@ -181,10 +181,15 @@ class ResNet(FLModule):
         return self.fc(x)
 
     # pool + fc + cross-entropy as two HIP launches (ops/head.py) when the shapes allow
+    def _native_head(self, f: torch.Tensor, y: torch.Tensor) -> bool:
+        """The fused head computes the default cross-entropy: not for a subclass
+        that overrides ``loss_fn``."""
+        return _NATIVE_HEAD and type(self).loss_fn is FLModule.loss_fn and head_ok(f, self.fc, y)
+
     def training_step(self, batch, batch_idx: int) -> torch.Tensor:
         x, y = batch
         f = self.features(x)
-        if _NATIVE_HEAD and head_ok(f, self.fc, y):
+        if self._native_head(f, y):
             loss, _, _ = head_xent(f, self.fc, y)
         else:
             loss = self.loss_fn(self.fc(torch.flatten(nn.functional.adaptive_avg_pool2d(f, 1), 1)), y)
@@ -194,7 +199,7 @@ class ResNet(FLModule):
     def _eval_step(self, batch, prefix: str) -> torch.Tensor:
         x, y = batch
         f = self.features(x)
-        if _NATIVE_HEAD and head_ok(f, self.fc, y):
+        if self._native_head(f, y):
             loss, _, acc = head_xent(f, self.fc, y)
             self.log(f"{prefix}_loss", loss, prog_bar=True)
             self.log(f"{prefix}_metric", acc, prog_bar=True)

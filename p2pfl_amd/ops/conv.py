@@ -42,7 +42,8 @@ STATS = {"native_fwd": 0, "torch_fwd": 0, "gemm_1x1_fwd": 0, "stem_fwd": 0, "nat
 # (scripts/bn_epi_probe.py; ResNet-18 round 59.9 vs 49.8 ms; profiles/r4_bn_epilogue.md).
 _FUSED_BN = os.environ.get("P2PFL_CONV_BN_STATS", "0") == "1"
 
-# "native" | "library" | "auto" (measured per shape, ops/autotune.py); env P2PFL_NATIVE_CONV
+# env P2PFL_NATIVE_CONV: "library" runs MIOpen for every eager convolution; "native" or "auto"
+# (default) run the implicit-GEMM kernels wherever native_ok holds
 _POLICY = autotune.policy("P2PFL_NATIVE_CONV")
 # csrc/gemm.h variant bits per product (single LDS buffer for the gathers, double buffer for split-K wgrad)
 _V_FWD = int(os.environ.get("P2PFL_CONV_VARIANT_FWD", "10"))
@@ -370,38 +371,6 @@ def conv_bn_act(x: torch.Tensor, conv: nn.Conv2d, bn: nn.BatchNorm2d, residual=N
     return bnops.batch_norm_act(conv2d(x, conv), bn, residual=residual, relu=relu)
 
 
-def _native_faster(x: torch.Tensor, conv: nn.Conv2d) -> bool:
-    """Time native vs MIOpen for this layer shape once (forward, plus both
-    gradients when autograd will need them) and remember the winner."""
-    w = conv.weight
-    stride, pad, dil = _sym(conv.stride), _sym(conv.padding), _sym(conv.dilation)
-    grad = torch.is_grad_enabled() and (x.requires_grad or w.requires_grad)
-    key = ("conv2d", tuple(x.shape), tuple(w.shape), stride, pad, dil, grad)
-    if key in autotune._CHOICE:
-        return autotune._CHOICE[key] == "native"
-    xb = x.detach().to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
-    wd = w.detach()
-    OH, OW = out_hw(x.shape[2], x.shape[3], (w.shape[2], w.shape[3]), stride, pad, dil)
-    dy = torch.randn(x.shape[0], w.shape[0], OH, OW, device=x.device).to(torch.bfloat16)
-    dy = dy.contiguous(memory_format=torch.channels_last)
-
-    def native():
-        with torch.enable_grad():
-            xr = xb.requires_grad_(grad)
-            wr = wd.detach().requires_grad_(grad)
-            y = _Conv2dNHWC.apply(xr, wr, stride, pad, dil)
-            if grad:
-                torch.autograd.backward(y, dy)
-
-    def library():
-        F.conv2d(xb, wd, None, stride, pad, dil)
-        if grad:
-            torch.ops.aten.convolution_backward(dy, xb, wd, None, [stride] * 2, [pad] * 2, [dil] * 2, False, [0, 0],
-                                                1, [True, True, False])
-
-    return autotune.choose(key, [("native", native), ("library", library)]) == "native"
-
-
 # 1x1 convolutions (ResNet-50 bottlenecks and downsample shortcuts) run as the
 # GEMM they are: NHWC pixels x C times W^T, through ops.gemm.linear (native MFMA
 # GEMM or hipBLASLt, measured per shape; all memory from PyTorch's allocator).
@@ -438,13 +407,15 @@ def conv1x1_gemm(x: torch.Tensor, conv: nn.Conv2d) -> torch.Tensor:
 
 
 def conv2d(x: torch.Tensor, conv: nn.Conv2d) -> torch.Tensor:
-    """``conv(x)`` on the implicit-GEMM kernels or MIOpen (``_POLICY``; "auto" = measured per shape);
-    1x1 convolutions as GEMMs (:func:`conv1x1_gemm`)."""
+    """``conv(x)`` on the implicit-GEMM kernels whenever they take the shape (:func:`native_ok`),
+    eager or captured alike -- MIOpen only under ``P2PFL_NATIVE_CONV=library`` or for shapes the
+    kernels refuse; 1x1 convolutions as GEMMs (:func:`conv1x1_gemm`)."""
     # Inside a HIP-graph capture the implicit-GEMM kernels run whatever the
     # eager timing preferred: MIOpen convolutions replayed from captured step
     # graphs corrupted weights as soon as several learners' graphs and eager
     # steps shared the device (profiles/r3_nan_root_cause.md); eager steps may
-    # still take MIOpen.  This holds under every policy, "library" included,
+    # no longer take MIOpen either (the short last batch of an epoch used to
+    # autotune against it).  This holds under every policy, "library" included,
     # and for 1x1 convolutions too (no hipBLASLt GEMM inside a graph).
     capturing = x.is_cuda and torch.cuda.is_current_stream_capturing()
     if capturing and native_ok(x, conv):
@@ -454,7 +425,7 @@ def conv2d(x: torch.Tensor, conv: nn.Conv2d) -> torch.Tensor:
         return conv1x1_gemm(x, conv)
     if x.shape[1] < 8 and stem_ok(x, conv) and _POLICY != "library":
         return stem_conv2d(x, conv)
-    if native_ok(x, conv) and (_POLICY == "native" or (_POLICY != "library" and _native_faster(x, conv))):
+    if native_ok(x, conv) and _POLICY != "library":
         STATS["native_fwd"] += 1
         return _Conv2dNHWC.apply(x, conv.weight, _sym(conv.stride), _sym(conv.padding), _sym(conv.dilation))
     STATS["torch_fwd"] += 1

@@ -101,6 +101,11 @@ def pp_eligible(M: int, N: int, K: int, a_kmajor: bool, b_kmajor: bool) -> bool:
     return tiles >= 150 and (K % 64 == 0 or not (a_kmajor or b_kmajor))
 
 
+def pp_eligible_any(M: int, N: int, K: int, a_kmajor: bool, b_kmajor: bool) -> bool:
+    """Products the ping-pong kernel takes at all (csrc/gemm_pp.hip gemm_pp_supported)."""
+    return M >= 8 and N >= 8 and (K % 64 == 0 or not (a_kmajor or b_kmajor))
+
+
 def _variant(a_kmajor: bool, splits: int, M: int = 0, N: int = 0, K: int = 0, b_kmajor: bool = True) -> int:
     if _VARIANT_ENV is not None:
         return int(_VARIANT_ENV)
@@ -161,11 +166,14 @@ def gemm(
     return out, z
 
 
-def _wgrad(dy2: torch.Tensor, x2: torch.Tensor, dtype: torch.dtype) -> torch.Tensor:
+def _wgrad(dy2: torch.Tensor, x2: torch.Tensor, dtype: torch.dtype, cfg: Optional[Tuple[int, int]] = None) -> torch.Tensor:
     """dW[n, k] = sum_m dy[m, n] x[m, k]: both operands m-major, split over m."""
     M, N = dy2.shape
     K = x2.shape[1]
-    return _product(dy2, x2, False, False, dtype, splits_for(N, K, M))
+    if cfg is None:
+        return _product(dy2, x2, False, False, dtype, splits_for(N, K, M))
+    v, sp = cfg
+    return gemm(dy2, x2, False, False, out_dtype=dtype, splits=sp, variant=v)[0]
 
 
 def _bias_grad(dy2: torch.Tensor, dtype: torch.dtype) -> torch.Tensor:
@@ -183,6 +191,35 @@ def _rows(x: torch.Tensor) -> torch.Tensor:
 
 _NAT, _LIB = "native", "library"
 
+# Native configurations tried per product at first use: (variant, split-K).
+# From scripts/vit_gemm_sweep.py on the ViT-B/16 products (profiles/r5_vit_gemm_sweep.md):
+# the forward / input-gradient products are won by the 128 x 128 tile (single or
+# double LDS buffer) or the 256 x 256 ping-pong kernel without split; the weight
+# gradients (K = 6304 tokens, few output tiles) by the ping-pong kernel or the
+# 4-stage ring at 6-8 slices.
+_FWD_CFGS = ((PP, 1), (2, 1), (10, 1))
+_DGRAD_CFGS = ((2, 1), (10, 1), (PP, 1), (2, 3), (10, 2))
+_WGRAD_CFGS = ((PP, 6), (PP, 8), (10, 6), (4096 | 2, 6), (2, 3))
+
+
+def _cfg_name(v: int, sp: int) -> str:
+    return f"{_NAT}:{v}:{sp}"
+
+
+def _cfg(choice: str) -> Tuple[int, int]:
+    """(variant, splits) of a "native:v:s" choice."""
+    _, v, sp = choice.split(":")
+    return int(v), int(sp)
+
+
+def _cfg_ok(v: int, sp: int, M: int, N: int, K: int, a_kmajor: bool, b_kmajor: bool, epilogue: bool) -> bool:
+    """Configurations the kernels take for this product (no launch may fail)."""
+    if not supported(M, N, K, a_kmajor, b_kmajor) or (sp > 1 and K // sp < 256):
+        return False
+    if v & PP:
+        return (sp == 1 or sp > IN_LAUNCH_MAX_SPLITS) and pp_eligible_any(M, N, K, a_kmajor, b_kmajor) and not (epilogue and sp > 1)
+    return not (epilogue and sp > IN_LAUNCH_MAX_SPLITS)
+
 
 class _LinearP(torch.autograd.Function):
     """``y = x W^T + b`` (or ``gelu(x W^T + b)``) whose three products -- forward,
@@ -194,7 +231,7 @@ class _LinearP(torch.autograd.Function):
     out of the fused GELU backward."""
 
     @staticmethod
-    @torch.amp.custom_fwd(device_type="cuda", cast_inputs=torch.bfloat16)
+    @torch.amp.custom_fwd(device_type="cuda")  # operands cast here, the bias keeps its dtype (no cast kernels)
     def forward(ctx, x, w, b, gelu, plan):
         from p2pfl_amd.ops.fused import _fx
 
@@ -202,14 +239,17 @@ class _LinearP(torch.autograd.Function):
         x2 = _rows(x.to(torch.bfloat16))
         wc = w.to(torch.bfloat16).contiguous()
         pre = gb = None
+        nat = fwd.startswith(_NAT)
+        v, sp = _cfg(fwd) if ":" in fwd else (None, 1)
         if not gelu:
-            y = gemm(x2, wc, bias=b)[0] if fwd == _NAT else F.linear(x2, wc, b.to(torch.bfloat16) if b is not None else None)
-        elif fwd == _NAT:
-            y, pre = gemm(x2, wc, bias=b, gelu=True, want_z=True)  # pre-activation includes the bias
+            # the native epilogue reads an fp32 or a bf16 bias; hipBLASLt needs x's dtype
+            y = gemm(x2, wc, bias=b, variant=v, splits=sp)[0] if nat else F.linear(x2, wc, b.to(torch.bfloat16) if b is not None else None)
+        elif nat:
+            y, pre = gemm(x2, wc, bias=b, gelu=True, want_z=True, variant=v, splits=sp)  # pre-activation includes the bias
             gb = torch.zeros(w.shape[0], dtype=torch.float32, device=x.device)
         else:
-            pre = torch.mm(x2, wc.t())  # bias-free; the GELU kernel adds it
-            gb = b.float().contiguous()
+            pre = torch.mm(x2, wc.t())  # bias-free; the GELU kernel adds it (fp32: fc1.bias is an fp32 parameter)
+            gb = b if (b.dtype == torch.float32 and b.is_contiguous()) else b.float().contiguous()
             y = _fx().bias_gelu_fwd(pre, gb)
         ctx.save_for_backward(x2, wc, pre, gb)
         ctx.gelu, ctx.plan = gelu, plan
@@ -233,9 +273,17 @@ class _LinearP(torch.autograd.Function):
             db = _bias_grad(dz, ctx.b_dtype)
         dx = dw = None
         if ctx.needs_input_grad[0]:
-            dx = (_product(dz, w, True, False, torch.bfloat16) if dg == _NAT else torch.mm(dz, w)).view(ctx.xshape)
+            if dg.startswith(_NAT):
+                v, sp = _cfg(dg) if ":" in dg else (None, 1)
+                dx = gemm(dz, w, True, False, splits=sp, variant=v)[0] if v is not None else _product(dz, w, True, False, torch.bfloat16)
+            else:
+                dx = torch.mm(dz, w)
+            dx = dx.view(ctx.xshape)
         if ctx.needs_input_grad[1]:
-            dw = _wgrad(dz, x2, ctx.w_dtype) if wg == _NAT else wgrad_blas(dz, x2).to(ctx.w_dtype)
+            if wg.startswith(_NAT):
+                dw = _wgrad(dz, x2, ctx.w_dtype, _cfg(wg) if ":" in wg else None)
+            else:
+                dw = wgrad_blas(dz, x2).to(ctx.w_dtype)
         if db is not None and ctx.b_dtype is not None:
             db = db.to(ctx.b_dtype)
         return dx, dw, db if (ctx.b_dtype is not None and ctx.needs_input_grad[2]) else None, None, None
@@ -271,23 +319,25 @@ def _plan(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor], gelu: 
     bd16 = bd.to(torch.bfloat16) if bd is not None else None
     g32 = bd.float().contiguous() if bd is not None else None
 
-    def fwd_native():
-        gemm(x2, wd, bias=bd, gelu=gelu, want_z=gelu and grad)
-
     def fwd_library():
         if gelu:
             _fx().bias_gelu_fwd(torch.mm(x2, wd.t()), g32)
         else:
             F.linear(x2, wd, bd16)
 
-    fwd = autotune.choose(keys[0], [(_NAT, fwd_native), (_LIB, fwd_library)])
+    epi = gelu or bias is not None
+    fwd_c = [(_cfg_name(v, sp), (lambda v=v, sp=sp: gemm(x2, wd, bias=bd, gelu=gelu, want_z=gelu and grad, variant=v, splits=sp)))
+             for v, sp in _FWD_CFGS if _cfg_ok(v, sp, M, N, K, True, True, epi)]
+    fwd = autotune.choose(keys[0], fwd_c + [(_LIB, fwd_library)])
     if not grad:
         return fwd, _LIB, _LIB
     dy = torch.randn(M, N, device=x.device).to(torch.bfloat16)
-    dg = autotune.choose(keys[1],
-                         [(_NAT, lambda: _product(dy, wd, True, False, torch.bfloat16)), (_LIB, lambda: torch.mm(dy, wd))])
-    wg = autotune.choose(keys[2],
-                         [(_NAT, lambda: _wgrad(dy, x2, torch.bfloat16)), (_LIB, lambda: wgrad_blas(dy, x2))])
+    dg_c = [(_cfg_name(v, sp), (lambda v=v, sp=sp: gemm(dy, wd, True, False, splits=sp, variant=v)))
+            for v, sp in _DGRAD_CFGS if _cfg_ok(v, sp, M, K, N, True, False, False)]
+    dg = autotune.choose(keys[1], dg_c + [(_LIB, lambda: torch.mm(dy, wd))])
+    wg_c = [(_cfg_name(v, sp), (lambda v=v, sp=sp: _wgrad(dy, x2, torch.bfloat16, (v, sp))))
+            for v, sp in _WGRAD_CFGS if _cfg_ok(v, sp, N, K, M, False, False, False)]
+    wg = autotune.choose(keys[2], wg_c + [(_LIB, lambda: wgrad_blas(dy, x2))])
     return fwd, dg, wg
 
 

@@ -46,29 +46,32 @@ class Settings:
     GOSSIP_EXIT_ON_X_EQUAL_ROUNDS: int = 10
     """Model gossip stops after this many identical status snapshots."""
     GOSSIP_RELAY_GRACE: float | None = None
-    """New (exactly-once delivery): how long (s) a node lets the ORIGIN of a
+    """New (exactly-once delivery on a full mesh): when every train-set member
+    is a direct neighbour, how long (s) a node lets the ORIGIN of a
     contribution deliver it before relaying it to a peer whose
     ``models_aggregated`` report has not moved (partial-aggregate gossip), and
     how long it lets a train-set neighbour finish its own aggregation before
-    diffusing the full model to it.  On a full mesh every model then crosses
-    each link once; on sparse topologies a relay follows after the grace.
-    ``None``: ``GOSSIP_MODELS_PERIOD``.  0 restores the reference's eager
+    diffusing the full model to it -- every model then crosses each link
+    once.  Sparser neighbourhoods relay at once, as before.  ``None``: a
+    quarter of ``GOSSIP_MODELS_PERIOD``.  0 restores the reference's eager
     re-sends (``gossip_model_stage.py:100-104``, ``train_stage.py:134-139``)."""
 
     # ---- training --------------------------------------------------------
-    ASYNC_DIFFUSION: bool = False
+    ASYNC_DIFFUSION: bool = True
     """Diffuse a round's aggregated model in the background while the next
-    round trains (new; the reference blocks in ``GossipModelStage`` until every
-    direct neighbour has the model).  One immutable device snapshot of the
-    aggregate is pushed to every lagging neighbour; a newer round's diffusion
-    supersedes an older one."""
+    round trains (new, on by default; the reference blocks in
+    ``GossipModelStage`` until every direct neighbour has the model:
+    ``gossip_model_stage.py:84-132``, restored by ``False``).  One immutable
+    device snapshot of the aggregate is pushed to every lagging neighbour; a
+    newer round's diffusion supersedes an older one."""
 
     NODE_STREAMS: bool | str = "auto"
-    """GPU learners train / evaluate on their own HIP stream (virtual peers in
-    one process then overlap each other and the aggregation / transport work
-    left on the default stream).  ``"auto"``: only while more than one learner
-    of this process lives on the same GPU (one peer per GPU gains nothing from
-    a private stream); ``True`` / ``False`` force it.  The hand-off between the
+    """GPU learners train / evaluate on their own HIP stream, so the
+    aggregation and transport work left on the default stream (FedAvg folds of
+    arriving models, payload snapshots, the RCCL comm stream's hand-offs) and
+    other virtual peers' training overlap a running ``fit()``.  ``"auto"``
+    (default): every GPU learner; ``True`` / ``False`` force it (``False``: the
+    learner enqueues on the caller's stream).  The hand-off between the
     learner's stream and the default stream is event-ordered (no host sync)."""
 
     TRAIN_SET_SIZE: int = 4

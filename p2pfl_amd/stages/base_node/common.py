@@ -63,10 +63,17 @@ def mark_dead_train_set_members(state: Any, protocol: Any, aggregator: Any) -> N
         aggregator.mark_lost(lost)
 
 
-def relay_grace() -> float:
-    """``Settings.GOSSIP_RELAY_GRACE`` (None: one ``GOSSIP_MODELS_PERIOD``)."""
+def relay_grace(state: Any = None, protocol: Any = None) -> float:
+    """``Settings.GOSSIP_RELAY_GRACE`` (None: a quarter of ``GOSSIP_MODELS_PERIOD``),
+    or 0 (relay at once) unless every train-set member is a direct neighbour --
+    only then can the origins be expected to deliver their own models."""
     g = Settings.GOSSIP_RELAY_GRACE
-    return float(Settings.GOSSIP_MODELS_PERIOD if g is None else g)
+    g = float(0.25 * Settings.GOSSIP_MODELS_PERIOD if g is None else g)
+    if g > 0 and state is not None and protocol is not None:
+        direct = set(protocol.get_neighbors(only_direct=True)) | {state.addr}
+        if not set(getattr(state, "train_set", ()) or ()) <= direct:
+            return 0.0
+    return g
 
 
 class ReportClock:
@@ -96,12 +103,16 @@ class DeliveryLedger:
     ``delivered`` after the transfer) or already delivered is not offered
     again; a ``declined`` one (e.g. the peer was still in the previous round)
     is.  Transports without delivery feedback keep the reference behaviour: an
-    offer counts until the peer's status report changes.  A proposal with no
-    answer within ``expiry`` seconds no longer counts (the plane lost it).
+    offer counts until the peer's status report changes or one
+    ``GOSSIP_MODELS_PERIOD`` passed (a push the receiver ignored -- e.g. it was
+    still in the previous round -- is sent again, as the reference re-sends
+    every period).  A proposal with no answer within ``expiry`` seconds no
+    longer counts (the plane lost it).
     """
 
     def __init__(self, expiry: float) -> None:
         self.expiry = expiry
+        self.resend = float(Settings.GOSSIP_MODELS_PERIOD)
         self._lock = threading.Lock()
         self._rec: Dict[str, Dict[frozenset, List[Any]]] = {}
 
@@ -127,6 +138,7 @@ class DeliveryLedger:
         out: Set[str] = set()
         with self._lock:
             for key, (st, tok, t) in self._rec.get(peer, {}).items():
-                if st == "delivered" or (st == "pending" and now - t < self.expiry) or (st == "sent" and tok == token):
+                if (st == "delivered" or (st == "pending" and now - t < self.expiry)
+                        or (st == "sent" and tok == token and now - t < self.resend)):
                     out |= key
         return out

@@ -108,7 +108,7 @@ class DiffusionPlan:
 
     def __init__(self, state: Any, protocol: Any, aggregator: Any, rnd: int) -> None:
         self.state, self.protocol, self.round = state, protocol, rnd
-        self.grace = relay_grace()
+        self.grace = relay_grace(state, protocol)
         self.train_set = set(getattr(state, "train_set", ()) or ())
         live = getattr(aggregator, "live_train_set", None)
         self.live = set(live() if live is not None else ()) or set(self.train_set)
@@ -169,7 +169,12 @@ class Diffusion:
         self.thread = threading.Thread(target=self._run, name=f"diffusion-{state.addr}-r{rnd}", daemon=True)
 
     @staticmethod
-    def start(state: Any, protocol: Any, aggregator: Any, rnd: int) -> "Diffusion":
+    def start(state: Any, protocol: Any, aggregator: Any, rnd: int) -> Optional["Diffusion"]:
+        plan = DiffusionPlan(state, protocol, aggregator, rnd)
+        if not plan.candidates():
+            # nobody is behind (e.g. a full mesh where every member aggregated by
+            # itself): no snapshot, no thread
+            return None
         payload = model_payload(state, protocol)  # device snapshot (or encoded bytes), taken now
         contributors = list(aggregator.get_aggregated_models())
 
@@ -177,7 +182,7 @@ class Diffusion:
             return protocol.build_weights(AddModelCommand.get_name(), rnd, payload, contributors, 1)
 
         d = Diffusion(state, protocol, rnd, message)
-        d.plan = DiffusionPlan(state, protocol, aggregator, rnd)
+        d.plan = plan
         # an older round's diffusion keeps running: a neighbour still at that
         # round needs THAT aggregate (it ignores newer-round models)
         live = [x for x in getattr(state, "diffusions", []) if x.thread.is_alive()]

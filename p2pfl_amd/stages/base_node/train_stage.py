@@ -79,7 +79,7 @@ class TrainStage(Stage):
         With ``GOSSIP_RELAY_GRACE = 0`` every push carries everything the peer
         lacks, as in the reference (``train_stage.py:134-168``).
         """
-        grace = relay_grace()
+        grace = relay_grace(state, protocol)
         ledger = DeliveryLedger(expiry=max(4 * grace, Settings.GRPC_TIMEOUT))
 
         def peer_has(n: str) -> List[str]:

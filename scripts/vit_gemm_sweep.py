@@ -8,7 +8,8 @@ Products (M = 32 x 197 = 6304 tokens): forward x.W^T, input gradient dY.W and
 weight gradient dY^T.x of qkv (768->2304), proj (768->768), fc1 (768->3072,
 with the bias+GELU epilogue), fc2 (3072->768) and the patch embedding
 (768->768 over 6272 patches).  Times are HIP-event means over back-to-back
-launches on random operands; TF/s dense (2 MNK / t).
+launches (device time, host launch overhead excluded) on random operands;
+TF/s dense (2 MNK / t).
 """
 
 from __future__ import annotations
@@ -21,6 +22,7 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 import torch  # noqa: E402
 
+from p2pfl_amd.ops import autotune  # noqa: E402
 from p2pfl_amd.ops.fused import _fx  # noqa: E402
 from p2pfl_amd.ops.gemm import gemm  # noqa: E402
 
@@ -35,16 +37,9 @@ SPLITS = (1, 2, 3, 4, 6, 8)
 
 
 def timeit(fn, iters: int) -> float:
-    for _ in range(3):
-        fn()
-    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    torch.cuda.synchronize()
-    s.record()
-    for _ in range(iters):
-        fn()
-    e.record()
-    torch.cuda.synchronize()
-    return s.elapsed_time(e) / iters * 1e3  # us
+    """Device time per call in us, host launch overhead excluded (ops/autotune.py's
+    method: the stream parked on a spin kernel while every timed call is enqueued)."""
+    return autotune._time(fn, iters) * 1e3
 
 
 def main() -> None:

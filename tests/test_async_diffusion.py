@@ -88,7 +88,7 @@ def test_diffusion_payload_is_a_snapshot(async_settings):
     class _State:
         addr = "n0"
         round = 1
-        nei_status = {}
+        nei_status = {"x": 0}  # one neighbour behind round 1
 
         class changed:  # noqa: N801
             version = 0
@@ -111,7 +111,7 @@ def test_diffusion_payload_is_a_snapshot(async_settings):
             return (rnd, payload, tuple(contributors))
 
         def get_neighbors(self, only_direct=False):
-            return []
+            return ["x"]
 
         def gossip_weights(self, stop, cands, status, model_fn, wakeup=None, peer_status_fn=None):
             self.sent.append(model_fn("x"))

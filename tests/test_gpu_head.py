@@ -60,3 +60,39 @@ def test_resnet_training_step_uses_native_head(monkeypatch):
     assert calls, "the head kernels did not run"
     lr, _ = head_reference(f, m.fc.weight, m.fc.bias, y)
     torch.testing.assert_close(loss, lr, atol=5e-3, rtol=5e-3)
+
+
+def test_head_out_of_range_label_is_nan_not_clamped():
+    """A label outside [0, N) gives a NaN loss and NaN gradients (F.cross_entropy
+    raises): never the finite loss of a clamped label."""
+    torch.manual_seed(0)
+    f = torch.randn(4, 64, 4, 4, device="cuda").to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    f.requires_grad_()
+    fc = nn.Linear(64, 10).cuda()
+    y = torch.tensor([1, 2, 10, 3], device="cuda")  # 10 is out of range
+    assert head_ok(f, fc, y)
+    loss, _, _ = head_xent(f, fc, y)
+    assert torch.isnan(loss).item()
+    loss.backward()
+    assert torch.isnan(fc.weight.grad).any().item()
+    y_neg = torch.tensor([1, 2, -100, 3], device="cuda")  # ignore_index is not supported either
+    loss2, _, _ = head_xent(f.detach(), fc, y_neg)
+    assert torch.isnan(loss2).item()
+
+
+def test_resnet_with_custom_loss_fn_skips_the_native_head(monkeypatch):
+    import p2pfl_amd.models.resnet as rn
+
+    class Smoothed(rn.ResNet):
+        def loss_fn(self, out, y):
+            return nn.functional.cross_entropy(out, y, label_smoothing=0.1)
+
+    ops.ext()
+    m = Smoothed(rn.BasicBlock, [2, 2, 2, 2], 10, stem="cifar", seed=0).cuda()
+    calls = []
+    monkeypatch.setattr(rn, "head_xent", lambda *a: calls.append(1))
+    x = torch.rand(2, 3, 32, 32, device="cuda")
+    y = torch.randint(0, 10, (2,), device="cuda")
+    with torch.autocast("cuda", dtype=torch.bfloat16):
+        loss = m.training_step((x, y), 0)
+    assert not calls and torch.isfinite(loss)

@@ -71,10 +71,40 @@ def _make_graph():
     return step_graph.TrainStepGraph(learner, _FakeOpt([p]), loader), arena
 
 
+def _wkey(sg):
+    return ("train", type(sg.learner.model).__name__, sg.B, tuple(sg.loader.x.shape[1:]), sg.opt.config())
+
+
+def test_first_warmup_of_a_model_runs_alone_later_ones_shared(fake_cuda, monkeypatch):
+    """The first warm-up of a model structure takes the gate exclusively (its
+    autotune timings see no other peer's kernels); the next peer's
+    warm-up of the same structure runs under the shared gate."""
+    sg, arena = _make_graph()
+    monkeypatch.setattr(step_graph, "_WARMED", set())
+    gate = step_graph.GATE
+    seen = []
+
+    def body(graph):
+        if not graph:
+            seen.append((gate._excl, gate._shared))
+        return torch.zeros(())
+
+    monkeypatch.setattr(sg, "_body", body)
+    sg.capture(torch.arange(4))
+    assert seen[0] == (True, 0), seen
+    assert _wkey(sg) in step_graph._WARMED
+    sg2, _ = _make_graph()
+    monkeypatch.setattr(sg2, "_body", body)
+    sg2.capture(torch.arange(4))
+    assert seen[1][0] is False and seen[1][1] >= 1, seen
+
+
 def test_slow_warmup_runs_under_shared_gate_and_does_not_hold_capture_lock(fake_cuda, monkeypatch):
     if not lockcheck.is_enabled():
         pytest.skip("P2PFL_LOCKCHECK=0")
     sg, arena = _make_graph()
+    # a later peer's warm-up (the model structure was warmed up once already)
+    monkeypatch.setattr(step_graph, "_WARMED", {_wkey(sg)})
     seen = {}
     gate = step_graph.GATE
 
