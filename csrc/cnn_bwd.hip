@@ -912,9 +912,12 @@ __global__ __launch_bounds__(256) void conv2_bwd_kernel(const uint16_t* __restri
                                                         const uint8_t* __restrict__ xds,
                                                         const int64_t* __restrict__ idx, float* __restrict__ wslab1,
                                                         float* __restrict__ wslab2, int B, int first_block,
-                                                        int wg_blocks, int stream_w) {
+                                                        int wg_blocks, int stream_w, int wg_first) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  const int j = blockIdx.x + first_block, nd = 2 * B;
+  const int nd = 2 * B;
+  // wg_first: the wgrad blocks take the low block ids (dispatched first)
+  int j = blockIdx.x + first_block;
+  if (wg_first) j = j < int(gridDim.x) - nd ? j + nd : j - (int(gridDim.x) - nd);
   if (j < nd) {
     if (stream_w)
       conv2_dgrad_block<true>(j & 1, j >> 1, dc2m, am1, w2q, xds, idx, wslab1, smem);
@@ -955,11 +958,16 @@ void conv2_bwd(const uint16_t* dc2m, const uint16_t* p1s, const uint8_t* am1, co
     const char* e = getenv("P2CNN_DGRAD_STREAM_W");
     return e ? atoi(e) : 0;
   }();
+  // P2CNN_CONV2BWD_WG_FIRST=1 (measurement knob): wgrad blocks before the dgrad blocks
+  static const int wg_first = [] {
+    const char* e = getenv("P2CNN_CONV2BWD_WG_FIRST");
+    return e ? atoi(e) : 0;
+  }();
   const int nd = 2 * B, nw = wg_blocks ? 5 * wgrad_groups(B) : (kTaps * wgrad_groups(B) + 3) / 4;
   const int first = roles == 2 ? nd : 0;
   const int blocks = roles == 1 ? nd : roles == 2 ? nw : nd + nw;
   hipLaunchKernelGGL(conv2_bwd_kernel, dim3(blocks), dim3(256), kDgLds, s, dc2m, p1s, am1, w2q, x, idx, wslab1, wslab2,
-                     B, first, wg_blocks, stream_w);
+                     B, first, wg_blocks, stream_w, roles == 3 ? wg_first : 0);
 }
 
 // ---------------------------------------------------------------------------

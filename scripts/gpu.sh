@@ -13,6 +13,7 @@
 #   scripts/gpu.sh models [steps]           configs 3-5: resnet18, resnet50, vit_b16 rounds
 #   scripts/gpu.sh rehearsal [N...]         split-hosts multi-rank rehearsal on the one GPU (default 2 4 8)
 #   scripts/gpu.sh prof <tag> <cmd...>      rocprofv3 --kernel-trace --stats of <cmd> -> gpurun_out/prof_<tag>
+#                                           (PROF_GAPS=1: also the GPU idle-gap table, tools/gap_summary.py)
 #   scripts/gpu.sh overlap [on|off] [rounds] 8 virtual ResNet-50 peers (fault-tolerance scenario) under a
 #                                           kernel trace + cross-stream overlap summary of training / FedAvg
 #   scripts/gpu.sh pmc <tag> <cmd...>       rocprofv3 --kernel-trace --pmc passes of <cmd> (one counter group
@@ -68,7 +69,13 @@ run_mode() {
       local tag=$1; shift
       rm -rf "gpurun_out/prof_$tag"
       step 400 "prof_$tag" rocprofv3 --kernel-trace --stats --output-format csv -d "gpurun_out/prof_$tag" -o run -- "$@"
-      step 120 "prof_${tag}_summary" python tools/prof_summary.py "gpurun_out/prof_$tag" --window-ms "${PROF_WINDOW_MS:-150}" --top 40 ;;
+      step 120 "prof_${tag}_summary" python tools/prof_summary.py "gpurun_out/prof_$tag" --window-ms "${PROF_WINDOW_MS:-150}" --top 40 \
+        ${PROF_GAPS:+--keep-trace}
+      if [ -n "${PROF_GAPS:-}" ]; then  # idle-gap table of the trace, then drop it (too big to copy back)
+        step 120 "prof_${tag}_gaps" python tools/gap_summary.py "gpurun_out/prof_$tag/run_kernel_trace.csv" \
+          --window-ms "${PROF_WINDOW_MS:-150}" --out "gpurun_out/prof_${tag}_gaps.md"
+        rm -f "gpurun_out/prof_$tag/run_kernel_trace.csv"
+      fi ;;
     overlap)
       local mode=${1:-on} rounds=${2:-5} d=gpurun_out/prof_overlap_${1:-on}
       rm -rf "$d"

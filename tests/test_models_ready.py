@@ -48,3 +48,65 @@ def test_not_running_is_ignored():
     s.round = None
     ModelsReadyCommand(s).execute("mem://a", 1)
     assert s.nei_status == {}
+
+
+def test_sync_diffusion_ends_by_stall_exit_when_a_neighbour_stays_behind(monkeypatch):
+    """Blocking (reference) diffusion with the reported-round bookkeeping: a
+    direct neighbour that keeps reporting round r - 1 stays a candidate, and the
+    diffusion ends through the GOSSIP_EXIT_ON_X_EQUAL_ROUNDS stall exit after
+    that many unchanged snapshots (one push per GOSSIP_MODELS_PERIOD meanwhile),
+    not by hanging (ADVICE r4, Q12 parity break)."""
+    import time
+
+    from p2pfl_amd.communication.gossiper import Gossiper
+    from p2pfl_amd.communication.messages import WeightsMessage
+    from p2pfl_amd.stages.base_node.gossip_model_stage import GossipModelStage
+
+    monkeypatch.setattr(Settings, "ASYNC_DIFFUSION", False)
+    monkeypatch.setattr(Settings, "GOSSIP_EXIT_ON_X_EQUAL_ROUNDS", 3)
+    monkeypatch.setattr(Settings, "GOSSIP_MODELS_PERIOD", 0.05)
+    monkeypatch.setattr(Settings, "GOSSIP_MODELS_PER_ROUND", 2)
+    st = NodeState("mem://me")
+    st.round = 3
+    st.train_set = ["mem://me", "mem://t"]
+    ModelsReadyCommand(st).execute("mem://lag", 2)  # the lagging neighbour reports round 2, forever
+
+    class _Learner:
+        def snapshot_parameters(self, params=None):
+            return b"w"
+
+    st.learner = _Learner()
+    sent = []
+
+    class _Client:
+        def send(self, nei, msg, create_connection=False):
+            sent.append((nei, time.monotonic()))
+
+    class _Proto:
+        supports_device_payloads = True
+        _gossiper = Gossiper("mem://me", _Client())
+
+        def get_neighbors(self, only_direct=False):
+            return ["mem://lag"]
+
+        def build_weights(self, cmd, rnd, payload, contributors, weight):
+            return WeightsMessage("mem://me", rnd, payload, list(contributors), weight, cmd)
+
+        def gossip_weights(self, *a, **k):
+            from p2pfl_amd.communication.protocol import BaseCommunicationProtocol
+
+            return BaseCommunicationProtocol.gossip_weights(self, *a, **k)
+
+    class _Agg:
+        def get_aggregated_models(self):
+            return ["mem://me", "mem://t"]
+
+        def live_train_set(self):
+            return ["mem://me", "mem://t"]
+
+    t0 = time.monotonic()
+    GossipModelStage._gossip_model_diffusion(st, _Proto(), _Agg())
+    took = time.monotonic() - t0
+    assert st.nei_status["mem://lag"] == 2
+    assert 1 <= len(sent) <= 5 and all(n == "mem://lag" for n, _ in sent), sent
+    assert took < 2.0, took  # 3 equal snapshots one period apart, then out
