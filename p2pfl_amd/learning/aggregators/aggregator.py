@@ -32,6 +32,15 @@ from p2pfl_amd.settings import Settings
 from p2pfl_amd.utils.lockcheck import make_rlock
 
 
+def _device_work():
+    """Shared hold of the process's GPU gate (learning/step_graph.py DeviceGate)
+    around aggregation kernels launched from command-handler / gossip threads:
+    never beside another virtual peer's HIP-graph capture."""
+    from p2pfl_amd.learning.step_graph import GATE
+
+    return GATE.shared()
+
+
 class NoModelsToAggregateError(Exception):
     """``aggregate`` called with no models."""
 
@@ -193,7 +202,8 @@ class Aggregator:
         job: List[Optional[Callable[[], None]]] = [None]
         now = self._add_model(model, nodes, weight, job)
         if job[0] is not None:
-            job[0]()
+            with _device_work():
+                job[0]()
         return now
 
     def _add_model(self, model: Any, nodes: List[str], weight: int, job: List[Optional[Callable[[], None]]]) -> List[str]:
@@ -258,7 +268,7 @@ class Aggregator:
             logger.info(self.node_name, "Aggregating models.")
         if not models:
             return None
-        with logger.span(self.node_name, "aggregate", k=len(models)):
+        with logger.span(self.node_name, "aggregate", k=len(models)), _device_work():
             return self.aggregate(models)
 
     def get_partial_aggregation(self, except_nodes: List[str]) -> Tuple[Any, Optional[List[str]], Optional[int]]:
@@ -276,7 +286,7 @@ class Aggregator:
         if len(chosen) == 1:
             result = (next(iter(chosen.values()))[0], contributors, weight)
         else:
-            with logger.span(self.node_name, "partial_aggregate", k=len(chosen)):
+            with logger.span(self.node_name, "partial_aggregate", k=len(chosen)), _device_work():
                 result = (self.aggregate(chosen), contributors, weight)
         with self._lock:
             if all(k in self._models for k in chosen):

@@ -16,9 +16,9 @@ a GPU by :func:`auto_learner`.
 
 from __future__ import annotations
 
-import os
-
+import collections
 import math
+import os
 import threading
 import time
 from typing import Any, Dict, List, Optional, Tuple
@@ -38,6 +38,8 @@ from p2pfl_amd.utils.streams import private_stream
 # and run in thread-local capture mode, so the other peers' kernels and
 # allocations on their own threads stay legal while one peer captures.
 _CAPTURE_LOCK = make_lock("FusedCNN._CAPTURE_LOCK")
+# fits the host may run ahead of the device (P2PFL_FIT_RUN_AHEAD; 1 = the round-4 bound)
+RUN_AHEAD = max(1, int(os.environ.get("P2PFL_FIT_RUN_AHEAD", "2")))
 
 # conv_adam folded into the FC1 Adam launch (P2PFL_CNN_MERGED_ADAM=0: separate launches)
 _MERGED_ADAM = os.environ.get("P2PFL_CNN_MERGED_ADAM", "1") != "0"
@@ -285,7 +287,12 @@ class FusedCNNLearner(TorchLearner):
         self._completions = HostCompletions(self_addr)
         self._val_stream = private_stream(self.device)
         self._val_done: Optional[torch.cuda.Event] = None  # last side-stream reader of the arena
-        self._fit_done: Optional[torch.cuda.Event] = None  # bounds the host's run-ahead to one fit
+        # completion events of the last RUN_AHEAD fits: the host may enqueue
+        # round r + 1 while round r still trains, so the device never idles
+        # while the stage machine moves between rounds (with a one-fit bound the
+        # device waited ~0.3 ms per round for the host to enqueue the next
+        # epoch: profiles/r5_cnn_gaps.md), and stays at most RUN_AHEAD fits ahead
+        self._fit_hist: "collections.deque[torch.cuda.Event]" = collections.deque(maxlen=RUN_AHEAD)
 
     # -- parameters: keep the bf16 shadows in sync -------------------------
     def _wait_arena_readers(self) -> None:
@@ -409,13 +416,13 @@ class FusedCNNLearner(TorchLearner):
         metrics are logged by the completion thread when they land.  Everything
         that later reads or replaces the weights -- the gossip snapshot and
         its RCCL push, FedAvg, ``set_parameters`` -- is ordered behind the
-        epoch by the stream.  The host runs at most one fit ahead of the GPU.
+        epoch by the stream.  The host runs at most ``RUN_AHEAD`` fits ahead of
+        the GPU.
         """
         self._interrupt.clear()
         self._arena_changed()
-        prev = self._fit_done
-        if prev is not None:
-            prev.synchronize()  # the previous round's training finished on the GPU
+        if len(self._fit_hist) == RUN_AHEAD:
+            self._fit_hist[0].synchronize()  # the fit RUN_AHEAD rounds back finished on the GPU
         self._ensure_graph("train", self.data.train_dataloader(), True)  # first-use captures outside the lock
         val = self.data.val_dataloader()
         if val is not None and len(val.dataset) > 0:
@@ -445,7 +452,7 @@ class FusedCNNLearner(TorchLearner):
                     self._validate_async()
             fit_done = torch.cuda.Event()
             fit_done.record(cur)
-            self._fit_done = fit_done
+            self._fit_hist.append(fit_done)
 
     def _log_epoch(self, host: torch.Tensor, base: int, steps: int, bs: int, n: int, t0: Any, t1: Any) -> None:
         loss_sums = [row[0] for row in host.tolist()]

@@ -150,7 +150,9 @@ class TorchLearner(NodeLearner):
     # ------------------------------------------------------------------
     def get_parameters(self) -> FlatParams:
         assert self.arena is not None
-        self.arena.sync_in()
+        if self.arena._int_buffers:
+            with self._gate():  # integer-buffer mirror copies (BatchNorm counters)
+                self.arena.sync_in()
         return self.arena.params
 
     def _stream_for_block(self) -> Optional[torch.cuda.Stream]:
@@ -166,7 +168,7 @@ class TorchLearner(NodeLearner):
         return self._compute_stream
 
     @contextlib.contextmanager
-    def _on_stream(self):
+    def _on_stream(self, hold_gate: bool = False):
         """Run a block on this learner's compute stream.
 
         Event-ordered hand-off, no host synchronisation: the compute stream
@@ -179,19 +181,25 @@ class TorchLearner(NodeLearner):
         """
         cs = self._stream_for_block()
         cur = torch.cuda.current_stream(self.device) if cs is not None else None
+        gate = self._gate() if hold_gate else contextlib.nullcontext()
         if cs is None or cur == cs:
-            yield
+            with gate:
+                yield
             return
         from p2pfl_amd.learning.step_graph import GATE
 
         # the hand-off events are recorded on the caller's stream -- usually the
         # legacy default stream, which ROCm treats as part of a graph capture in
         # progress on another peer's thread (hipErrorCapturedEvent): never while
-        # another thread records
+        # another thread records.  hold_gate: the whole block is short GPU work
+        # issued from a non-learning thread (set_parameters from a command
+        # handler): it runs under the shared gate too, never beside another
+        # peer's capture (a copy launched from a handler thread during a capture
+        # crashed the HIP runtime once under rocprofv3 in the 8-peer scenario)
         with GATE.shared():
             cs.wait_stream(cur)
         try:
-            with torch.cuda.stream(cs):
+            with gate, torch.cuda.stream(cs):
                 yield
         finally:
             with GATE.shared():
@@ -199,7 +207,7 @@ class TorchLearner(NodeLearner):
 
     def set_parameters(self, params: Mapping[str, torch.Tensor]) -> None:
         finite.check(self._addr, "set_parameters input", params if isinstance(params, FlatParams) else None)
-        with self._on_stream():
+        with self._on_stream(hold_gate=True):
             self._set_parameters(params)
         if finite.ENABLED and self.arena is not None:
             finite.check(self._addr, "parameters after set_parameters", self.arena.flat)
@@ -247,7 +255,8 @@ class TorchLearner(NodeLearner):
                 return params
             snap = self._snapshot
             if snap is None or snap[0] != self._arena_version:
-                snap = self._snapshot = (self._arena_version, params.clone())
+                with self._gate():  # a copy launched from a gossip thread: never beside a capture
+                    snap = self._snapshot = (self._arena_version, params.clone())
             return snap[1]
         from p2pfl_amd.learning.arena import flatten
 
