@@ -26,16 +26,18 @@ P2_DEVICE uint4 ld_nt16(const void* p) {
   return __builtin_bit_cast(uint4, v);
 }
 
-// bf16 <-> f32 (round-to-nearest-even), bit-level so it vectorises cleanly.
+// bf16 <-> f32.  f32 -> bf16 is the gfx950 conversion instruction
+// (v_cvt_pk_bf16_f32: round-to-nearest-even, NaN stays NaN; MI355X_MICROARCH.md
+// correctness table): one instruction per pair.  The bit-level sequence used
+// before (add 0x7fff + lsb, plus a branch for NaN) cost ~8 instructions and an
+// exec-masked branch per value -- in an unrolled 256 x 256 GEMM epilogue that
+// was ~6 KB of code fetched cold by every workgroup.
+typedef __bf16 p2_bf16x2_t __attribute__((ext_vector_type(2)));
 P2_DEVICE float bf16_to_f32(uint16_t h) { return __uint_as_float(uint32_t(h) << 16); }
-P2_DEVICE uint16_t f32_to_bf16(float f) {
-  uint32_t u = __float_as_uint(f);
-  if ((u & 0x7f800000u) == 0x7f800000u && (u & 0x7fffffu)) return uint16_t((u >> 16) | 0x40);  // quiet NaN
-  u += 0x7fffu + ((u >> 16) & 1u);
-  return uint16_t(u >> 16);
-}
+P2_DEVICE uint16_t f32_to_bf16(float f) { return __builtin_bit_cast(uint16_t, static_cast<__bf16>(f)); }
 P2_DEVICE uint32_t pack_bf16x2(float lo, float hi) {
-  return uint32_t(f32_to_bf16(lo)) | (uint32_t(f32_to_bf16(hi)) << 16);
+  const p2_bf16x2_t v = {static_cast<__bf16>(lo), static_cast<__bf16>(hi)};
+  return __builtin_bit_cast(uint32_t, v);
 }
 
 // Grid size for a grid-stride memory-bound kernel: enough blocks to cover the

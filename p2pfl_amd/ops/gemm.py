@@ -342,9 +342,13 @@ def _plan(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor], gelu: 
 
 
 def _ok(x: torch.Tensor, w: torch.Tensor) -> bool:
+    """bf16 products on the GPU: a bf16 input, or an fp32 one under bf16 autocast
+    (an fp32 product outside autocast keeps fp32 math on hipBLASLt)."""
     from p2pfl_amd.ops import _gpu
 
-    return _gpu(x) and x.dtype in (torch.bfloat16, torch.float32) and w.shape[0] % 8 == 0 and w.shape[1] % 8 == 0 and x.shape[-1] == w.shape[1]
+    bf16 = x.dtype == torch.bfloat16 or (
+        x.dtype == torch.float32 and torch.is_autocast_enabled("cuda") and torch.get_autocast_dtype("cuda") == torch.bfloat16)
+    return _gpu(x) and bf16 and w.shape[0] % 8 == 0 and w.shape[1] % 8 == 0 and x.shape[-1] == w.shape[1]
 
 
 def linear(x: torch.Tensor, weight: torch.Tensor, bias: Optional[torch.Tensor] = None) -> torch.Tensor:
