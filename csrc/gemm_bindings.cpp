@@ -12,9 +12,11 @@
 namespace {
 
 // fp32 elements of one split-K slice: the fragment-native tiles of the kernel the
-// variant selects (gemm_core.h SlabGeom), or the ping-pong kernel's row-major M x N
+// variant selects (gemm_core.h SlabGeom; 256 x 256 for the 256 tile and the
+// ping-pong kernel's in-launch reduction), or the ping-pong kernel's row-major
+// M x N slabs of a separately reduced launch
 int64_t slab_elems(int64_t M, int64_t N, int64_t variant) {
-  const int64_t t = (variant & 64) ? 256 : 128;
+  const int64_t t = (variant & (64 | 2048)) ? 256 : 128;
   return std::max(M * N, ((M + t - 1) / t) * ((N + t - 1) / t) * t * t);
 }
 

@@ -90,6 +90,7 @@ _VARIANT_ENV = os.environ.get("P2PFL_GEMM_VARIANT")
 
 
 PP = 2048  # variant bit 11: the ping-pong 256 x 256 pipeline (csrc/gemm_pp.hip)
+PP_M16 = 1 << 16  # with PP: the same pipeline on v_mfma_f32_16x16x32_bf16
 
 
 def pp_eligible(M: int, N: int, K: int, a_kmajor: bool, b_kmajor: bool) -> bool:
@@ -153,7 +154,7 @@ def gemm(
         if bias is not None or gelu or residual is not None:
             raise ValueError("a split-K GEMM with more than 4 slices has no epilogue")
         _C().gemm(a, b, a_kmajor, b_kmajor, ws, None, False, None, None, splits, v)
-        if v & PP:  # the ping-pong kernel writes row-major slabs
+        if v & PP:  # the ping-pong kernels write row-major slabs
             _C().slab_sum(ws[: splits * M * N].view(splits, M * N), out.view(-1))
         else:
             _C().tile_slab_reduce(ws, splits, M, N, out, v)
@@ -193,12 +194,13 @@ _NAT, _LIB = "native", "library"
 
 # Native configurations tried per product at first use: (variant, split-K).
 # From scripts/vit_gemm_sweep.py on the ViT-B/16 products (profiles/r5_vit_gemm_sweep.md):
-# the forward / input-gradient products are won by the 128 x 128 tile (single or
-# double LDS buffer) or the 256 x 256 ping-pong kernel without split; the weight
-# gradients (K = 6304 tokens, few output tiles) by the ping-pong kernel or the
-# 4-stage ring at 6-8 slices.
-_FWD_CFGS = ((PP, 1), (2, 1), (10, 1))
-_DGRAD_CFGS = ((2, 1), (10, 1), (PP, 1), (2, 3), (10, 2))
+# the forward products by the ping-pong kernel (its 16x16x32 form on qkv / proj /
+# patch) or the 128 x 128 single-buffer tile (fc1), the input gradients by the
+# ping-pong kernel (2 in-launch slices when N = 768) or the 128 x 128 double
+# buffer, the weight gradients (K = 6304 tokens, few output tiles) by the
+# ping-pong kernel or the 4-stage ring at 6-8 slices.
+_FWD_CFGS = ((PP | PP_M16, 1), (PP, 1), (PP, 2), (2, 1), (10, 1))
+_DGRAD_CFGS = ((PP, 1), (PP, 2), (2, 1), (10, 1), (2, 3), (10, 2))
 _WGRAD_CFGS = ((PP, 6), (PP, 8), (10, 6), (4096 | 2, 6), (2, 3))
 
 
@@ -217,7 +219,7 @@ def _cfg_ok(v: int, sp: int, M: int, N: int, K: int, a_kmajor: bool, b_kmajor: b
     if not supported(M, N, K, a_kmajor, b_kmajor) or (sp > 1 and K // sp < 256):
         return False
     if v & PP:
-        return (sp == 1 or sp > IN_LAUNCH_MAX_SPLITS) and pp_eligible_any(M, N, K, a_kmajor, b_kmajor) and not (epilogue and sp > 1)
+        return pp_eligible_any(M, N, K, a_kmajor, b_kmajor) and not (epilogue and sp > IN_LAUNCH_MAX_SPLITS)
     return not (epilogue and sp > IN_LAUNCH_MAX_SPLITS)
 
 

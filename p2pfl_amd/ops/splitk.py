@@ -96,7 +96,8 @@ def tiles_of(rows: int, cols: int) -> int:
 
 def slab_elems(rows: int, cols: int, variant: int = 0) -> int:
     """fp32 elements of one split-K slice: fragment-native tiles of the kernel the
-    variant selects (128 x 128, or 256 x 256 with bit 6; ``csrc/gemm_core.h`` SlabGeom),
-    or the ping-pong kernel's row-major rows x cols."""
-    t = 256 if variant & 64 else 128
+    variant selects (128 x 128, or 256 x 256 with bit 6 or the ping-pong kernel's
+    in-launch reduction; ``csrc/gemm_core.h`` SlabGeom), or the ping-pong kernel's
+    row-major rows x cols of a separately reduced launch."""
+    t = 256 if variant & (64 | 2048) else 128
     return max(rows * cols, -(-rows // t) * -(-cols // t) * t * t)

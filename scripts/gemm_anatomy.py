@@ -40,6 +40,8 @@ def main() -> None:
     kernels = [
         ("pingpong", 2048, {"full": 0, "no stores": 1 << 14, "no K loop": 1 << 15, "no DMA in loop": 1 << 12,
                             "no stagger": 1 << 13}),
+        ("pingpong16", 2048 | 65536, {"full": 0, "no stores": 1 << 14, "no K loop": 1 << 15, "no DMA in loop": 1 << 12,
+                                      "no stagger": 1 << 13}),
         ("128 dbuf", 2, {"full": 0, "no stores": 16, "no K loop": 32, "no DMA in loop": 128}),
         ("128 1buf", 10, {"full": 0, "no stores": 16, "no K loop": 32}),
         ("128 ring4", 4096 | 2, {"full": 0, "no stores": 16, "no K loop": 32}),

@@ -32,6 +32,7 @@ VARIANTS = {
     4096 | 2: "128 ring4",
     64: "256 dbuf",
     2048: "256 pingpong",
+    2048 | 65536: "256 pingpong16",
 }
 SPLITS = (1, 2, 3, 4, 6, 8)
 
@@ -73,8 +74,6 @@ def main() -> None:
                 for s in SPLITS:
                     if k // s < 256 or (s > 1 and gelu and kind == "fwd" and s > 4):
                         continue
-                    if v == 2048 and s > 1 and s <= 4:
-                        continue  # the ping-pong kernel's split-K goes through row-major slabs only
                     try:
                         t = timeit(lambda: nat(v, s), args.iters)
                     except Exception as e:  # a configuration the bindings refuse

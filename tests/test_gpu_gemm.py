@@ -183,12 +183,14 @@ def test_gemm256_epilogue_bias_gelu_residual(monkeypatch):
     torch.testing.assert_close(outb.float(), ref, atol=5e-2, rtol=1e-2)
 
 
+@pytest.mark.parametrize("m16", [False, True], ids=["mfma32", "mfma16"])
 @pytest.mark.parametrize("a_kmajor,b_kmajor", [(True, True), (True, False), (False, True), (False, False)])
 @pytest.mark.parametrize("M,N,K", [(512, 512, 256), (296, 264, 128), (1000, 776, 448), (264, 520, 200)])
-def test_pingpong_gemm_layouts_vs_fp32(a_kmajor, b_kmajor, M, N, K):
-    """The ping-pong 256 x 256 kernel (variant bit 11): every layout, M / N tails (clamped rows),
-    odd K-tile counts, and (m/n-major only) a K tail through the buffer range check."""
-    from p2pfl_amd.ops.gemm import PP
+def test_pingpong_gemm_layouts_vs_fp32(a_kmajor, b_kmajor, M, N, K, m16):
+    """The ping-pong 256 x 256 kernel (variant bit 11) in both MFMA forms (32x32x16, and
+    16x16x32 with bit 16): every layout, M / N tails (clamped rows), odd K-tile counts,
+    and (m/n-major only) a K tail through the buffer range check."""
+    from p2pfl_amd.ops.gemm import PP, PP_M16
 
     if (a_kmajor or b_kmajor) and K % 64:
         pytest.skip("k-major operands need K % 64 == 0 on this kernel")
@@ -196,15 +198,18 @@ def test_pingpong_gemm_layouts_vs_fp32(a_kmajor, b_kmajor, M, N, K):
         pytest.skip("m-major A needs M % 8 == 0")
     a, b = _operands(M, N, K, a_kmajor, b_kmajor, seed=M + 3 * N + K)
     out = torch.empty(M, N, device="cuda", dtype=torch.float32)
-    ops.ext().gemm(a, b, a_kmajor, b_kmajor, out, None, False, None, None, 1, PP)
+    ops.ext().gemm(a, b, a_kmajor, b_kmajor, out, None, False, None, None, 1, PP | (PP_M16 if m16 else 0))
     ref, _ = ops.gemm_reference(a, b, a_kmajor, b_kmajor)
     torch.testing.assert_close(out, ref, atol=2e-3, rtol=1e-4)
 
 
-def test_pingpong_gemm_epilogues_and_split_k():
+@pytest.mark.parametrize("m16", [False, True], ids=["mfma32", "mfma16"])
+def test_pingpong_gemm_epilogues_and_split_k(m16):
     """Bias + GELU (+ pre-activation) and residual epilogues, bf16 out; split-K reduced in the launch."""
-    from p2pfl_amd.ops.gemm import PP
+    from p2pfl_amd.ops.gemm import PP as PP0, PP_M16
     from p2pfl_amd.ops.splitk import counters, tiles_of
+
+    PP = PP0 | (PP_M16 if m16 else 0)
 
     C = ops.ext()
     M, N, K = 6304, 3072, 768  # ViT-B/16 fc1: 300 tiles, the shape ops.gemm sends here
@@ -231,8 +236,9 @@ def test_pingpong_gemm_epilogues_and_split_k():
     torch.testing.assert_close(out3, ref3, atol=5e-3, rtol=1e-4)
 
 
+@pytest.mark.parametrize("kernel", ["128", "pingpong", "pingpong16"])
 @pytest.mark.parametrize("splits", [2, 3, 4])
-def test_in_launch_splitk_reused_workspace(splits):
+def test_in_launch_splitk_reused_workspace(splits, kernel):
     """Back-to-back in-launch split-K launches over ONE reused workspace and counter
     array, on a grid of many tiles (slices of a tile land on different XCDs): each
     launch must see only its own slabs (pins the sc1 hand-off assumption documented
@@ -240,9 +246,12 @@ def test_in_launch_splitk_reused_workspace(splits):
     in-launch reduction must equal the fp32 product bit for bit, launch after launch."""
     from p2pfl_amd.ops.splitk import counters, slab_elems, tiles_of
 
+    from p2pfl_amd.ops.gemm import PP, PP_M16
+
+    v = {"128": 0, "pingpong": PP, "pingpong16": PP | PP_M16}[kernel]
     C = ops.ext()
-    M, N, K = 1024, 768, 2048  # 48 tiles x splits workgroups
-    ws = torch.empty(splits * slab_elems(M, N), device="cuda")
+    M, N, K = 1024, 768, 2048  # 48 tiles (12 of 256 x 256) x splits workgroups
+    ws = torch.empty(splits * slab_elems(M, N, v), device="cuda")
     cnt = counters(tiles_of(M, N), torch.device("cuda"))
     outs, refs = [], []
     for it in range(24):
@@ -250,12 +259,14 @@ def test_in_launch_splitk_reused_workspace(splits):
         A = torch.randint(-2, 3, (M, K), device="cuda", generator=g).to(torch.bfloat16)
         B = torch.randint(-2, 3, (N, K), device="cuda", generator=g).to(torch.bfloat16)
         out = torch.empty(M, N, device="cuda", dtype=torch.float32)
-        C.gemm(A.t().contiguous(), B.t().contiguous(), False, False, out, None, False, None, None, splits, 0, ws, cnt)
+        C.gemm(A.t().contiguous(), B.t().contiguous(), False, False, out, None, False, None, None, splits, v, ws, cnt)
         outs.append(out)
         refs.append(A.float() @ B.float().t())
     torch.cuda.synchronize()
     for it, (o, r) in enumerate(zip(outs, refs)):
         assert torch.equal(o, r), f"launch {it}: max err {(o - r).abs().max().item()}"
+    if v:
+        return
     # the separate-launch reducer on the same last operands agrees too
     ws2 = torch.empty(splits * slab_elems(M, N), device="cuda")
     out2 = torch.empty(M, N, device="cuda", dtype=torch.float32)
