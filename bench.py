@@ -374,7 +374,7 @@ def _print_round_breakdown(rank, addr, tracer, round_ends, W, K) -> None:
         gbytes = sum(int(s.attrs.get("nbytes", 0)) for s in groups)
         print(
             f"[bench rank {rank}] round {r}: wall {(t1 - t0) * 1e3:.2f} ms | fit {tot('fit'):.2f} (GPU epoch "
-            f"{tot('train_epoch_gpu'):.2f}) evaluate {tot('evaluate'):.2f} "
+            f"{tot('train_epoch_gpu'):.2f}, between epochs {tot('inter_epoch_gpu'):.2f}) evaluate {tot('evaluate'):.2f} "
             f"wait_aggregation {tot('wait_aggregation'):.2f} aggregate {tot('aggregate'):.2f} | pushes: "
             f"ack {('%.3f' % (sum(acks) / len(acks))) if acks else '-'} ms mean over {len(acks)}, "
             f"{len(groups)} groups {sum(s.duration for s in groups) * 1e3:.2f} ms total "

@@ -246,12 +246,34 @@ class _EvalForward:
         C.head(self.slabs1, e.S1, M, e.params, e.off, labels, idx, B, False, self.H, self.dH, self.dlogits, stats, e.w2bf)
 
 
+# Instantiations of the training-epoch graph replayed in turn.  hipGraphLaunch
+# of an executable graph whose previous launch is still running blocks the host
+# until that launch finishes (rocprofv3 --hip-trace: 6.4 ms per round in
+# hipGraphLaunch, the whole epoch), so with ONE instance the host could never
+# enqueue round r + 1's epoch before round r's ended, and the device idled for
+# the graph's submission at every round boundary (profiles/r5_cnn_gaps.md).
+# Two instances (each with its own permutation / stats buffers) let the next
+# epoch's launch overlap the running one.
+EPOCH_GRAPHS = max(1, int(os.environ.get("P2PFL_EPOCH_GRAPHS", "2")))
+
+
 class _EpochGraph:
-    """One captured HIP graph per (dataset, batch plan)."""
+    """One captured HIP graph per (dataset, batch plan); ``alt``: further
+    instances of the same pass, replayed round-robin."""
 
     def __init__(self, graph: Optional[torch.cuda.CUDAGraph], key: Tuple) -> None:
         self.graph = graph
         self.key = key
+        self.alt: List["_EpochGraph"] = []
+        self.turn = 0
+
+    def next(self) -> "_EpochGraph":
+        """The instance to replay now."""
+        if not self.alt:
+            return self
+        inst = ([self] + self.alt)[self.turn % (1 + len(self.alt))]
+        self.turn += 1
+        return inst
 
 
 class FusedCNNLearner(TorchLearner):
@@ -293,6 +315,7 @@ class FusedCNNLearner(TorchLearner):
         # device waited ~0.3 ms per round for the host to enqueue the next
         # epoch: profiles/r5_cnn_gaps.md), and stays at most RUN_AHEAD fits ahead
         self._fit_hist: "collections.deque[torch.cuda.Event]" = collections.deque(maxlen=RUN_AHEAD)
+        self._last_epoch_end: Optional[torch.cuda.Event] = None
 
     # -- parameters: keep the bf16 shadows in sync -------------------------
     def _wait_arena_readers(self) -> None:
@@ -340,6 +363,8 @@ class FusedCNNLearner(TorchLearner):
                     gc.collect()
                 with GATE.exclusive():  # no other learner's GPU work during the capture
                     g = self._capture(name, loader, plan, train, key)
+                    if train and self.use_graphs:
+                        g.alt = [self._capture(name, loader, plan, train, key) for _ in range(EPOCH_GRAPHS - 1)]
                 self._graphs[name] = g
         return g
 
@@ -348,7 +373,7 @@ class FusedCNNLearner(TorchLearner):
         from p2pfl_amd.learning.step_graph import GATE
 
         plan, _ = self._graph_key(name, loader, train)
-        g = self._ensure_graph(name, loader, train)
+        g = self._ensure_graph(name, loader, train).next()
         with GATE.shared():
             if perm is not None:
                 g.perm.copy_(perm, non_blocking=True)
@@ -447,14 +472,15 @@ class FusedCNNLearner(TorchLearner):
                 done.record(cur)
                 base = self._step
                 self._step += steps
-                self._completions.submit(done, lambda h=host, b=base, a=t0, z=t1: self._log_epoch(h, b, steps, bs, n, a, z))
+                prev, self._last_epoch_end = self._last_epoch_end, t1
+                self._completions.submit(done, lambda h=host, b=base, a=t0, z=t1, p=prev: self._log_epoch(h, b, steps, bs, n, a, z, p))
                 if not (self.defer_final_validation and epoch == self.epochs - 1):
                     self._validate_async()
             fit_done = torch.cuda.Event()
             fit_done.record(cur)
             self._fit_hist.append(fit_done)
 
-    def _log_epoch(self, host: torch.Tensor, base: int, steps: int, bs: int, n: int, t0: Any, t1: Any) -> None:
+    def _log_epoch(self, host: torch.Tensor, base: int, steps: int, bs: int, n: int, t0: Any, t1: Any, prev_end: Any = None) -> None:
         loss_sums = [row[0] for row in host.tolist()]
         every = max(1, self.log_every_n_steps)
         for j in range(steps):
@@ -464,6 +490,12 @@ class FusedCNNLearner(TorchLearner):
         # GPU time of the replayed epoch (the host only enqueued it)
         ms = t0.elapsed_time(t1)
         logger.tracer.record(self._addr, "train_epoch_gpu", time.perf_counter() - ms * 1e-3, ms * 1e-3)
+        if prev_end is not None:
+            # device time from the previous epoch's end to this one's start: the
+            # round's other GPU work (evaluation, readbacks, optimizer reset)
+            # plus any idle time the host left between them
+            gap = prev_end.elapsed_time(t0)
+            logger.tracer.record(self._addr, "inter_epoch_gpu", time.perf_counter() - gap * 1e-3, gap * 1e-3)
 
     def _eval_async(self, name: str, loader, on_done) -> None:
         """Enqueue an evaluation pass on the current stream; ``on_done(loss, metric)``
