@@ -246,34 +246,12 @@ class _EvalForward:
         C.head(self.slabs1, e.S1, M, e.params, e.off, labels, idx, B, False, self.H, self.dH, self.dlogits, stats, e.w2bf)
 
 
-# Instantiations of the training-epoch graph replayed in turn.  hipGraphLaunch
-# of an executable graph whose previous launch is still running blocks the host
-# until that launch finishes (rocprofv3 --hip-trace: 6.4 ms per round in
-# hipGraphLaunch, the whole epoch), so with ONE instance the host could never
-# enqueue round r + 1's epoch before round r's ended, and the device idled for
-# the graph's submission at every round boundary (profiles/r5_cnn_gaps.md).
-# Two instances (each with its own permutation / stats buffers) let the next
-# epoch's launch overlap the running one.
-EPOCH_GRAPHS = max(1, int(os.environ.get("P2PFL_EPOCH_GRAPHS", "2")))
-
-
 class _EpochGraph:
-    """One captured HIP graph per (dataset, batch plan); ``alt``: further
-    instances of the same pass, replayed round-robin."""
+    """One captured HIP graph per (dataset, batch plan)."""
 
     def __init__(self, graph: Optional[torch.cuda.CUDAGraph], key: Tuple) -> None:
         self.graph = graph
         self.key = key
-        self.alt: List["_EpochGraph"] = []
-        self.turn = 0
-
-    def next(self) -> "_EpochGraph":
-        """The instance to replay now."""
-        if not self.alt:
-            return self
-        inst = ([self] + self.alt)[self.turn % (1 + len(self.alt))]
-        self.turn += 1
-        return inst
 
 
 class FusedCNNLearner(TorchLearner):
@@ -363,8 +341,6 @@ class FusedCNNLearner(TorchLearner):
                     gc.collect()
                 with GATE.exclusive():  # no other learner's GPU work during the capture
                     g = self._capture(name, loader, plan, train, key)
-                    if train and self.use_graphs:
-                        g.alt = [self._capture(name, loader, plan, train, key) for _ in range(EPOCH_GRAPHS - 1)]
                 self._graphs[name] = g
         return g
 
@@ -373,7 +349,7 @@ class FusedCNNLearner(TorchLearner):
         from p2pfl_amd.learning.step_graph import GATE
 
         plan, _ = self._graph_key(name, loader, train)
-        g = self._ensure_graph(name, loader, train).next()
+        g = self._ensure_graph(name, loader, train)
         with GATE.shared():
             if perm is not None:
                 g.perm.copy_(perm, non_blocking=True)
