@@ -224,6 +224,29 @@ torch::Tensor attn_bwd(torch::Tensor qkv, torch::Tensor o, torch::Tensor dout, t
   return dqkv;
 }
 
+// dsts[i] <- srcs[i] for every pair, one launch (same byte size per pair, any dtype)
+void multi_copy(std::vector<torch::Tensor> dsts, std::vector<torch::Tensor> srcs) {
+  TORCH_CHECK(dsts.size() == srcs.size() && !dsts.empty() && int(dsts.size()) <= p2fused::kMaxCopies,
+              "multi_copy: 1..", p2fused::kMaxCopies, " (dst, src) pairs");
+  const c10::DeviceGuard g(dsts[0].device());
+  p2fused::CopyList cl{};
+  cl.n = int(dsts.size());
+  for (int i = 0; i < cl.n; ++i) {
+    const auto &d = dsts[i], &s = srcs[i];
+    TORCH_CHECK(d.is_cuda() && s.is_cuda() && d.device() == s.device() && d.device() == dsts[0].device(),
+                "multi_copy: tensors must be on one GPU");
+    TORCH_CHECK(d.is_contiguous() && s.is_contiguous(), "multi_copy: tensors must be contiguous");
+    const int64_t nb = d.numel() * d.element_size();
+    TORCH_CHECK(nb == s.numel() * s.element_size() && nb % 4 == 0, "multi_copy: pair ", i, " byte sizes differ or not % 4");
+    TORCH_CHECK(reinterpret_cast<uintptr_t>(d.data_ptr()) % 16 == 0 && reinterpret_cast<uintptr_t>(s.data_ptr()) % 16 == 0,
+                "multi_copy: pair ", i, " not 16-byte aligned");
+    cl.dst[i] = d.data_ptr();
+    cl.src[i] = s.data_ptr();
+    cl.bytes[i] = nb;
+  }
+  p2fused::multi_copy(cl, stream());
+}
+
 }  // namespace
 
 void register_fused(pybind11::module& m) {
@@ -234,6 +257,7 @@ void register_fused(pybind11::module& m) {
         pybind11::arg("rstd"), pybind11::arg("gsum") = pybind11::none());
   f.def("column_sum", &column_sum, "column sums of a [N, H] bf16/fp32 activation (linear bias gradient), fp32 or bf16 out",
         pybind11::arg("x"), pybind11::arg("bf16_out") = false);
+  f.def("multi_copy", &multi_copy, "dsts[i] <- srcs[i] for up to 12 pairs in one launch");
   f.def("split_sum_bf16", &split_sum_bf16, "bf16 sum over dim 0 of [S, ...] bf16 partials, fp32 accumulation");
   f.def("bias_gelu_fwd", &bias_gelu_fwd);
   f.def("bias_gelu_bwd", &bias_gelu_bwd);

@@ -31,6 +31,17 @@ void column_sum(bool bf16, const void* x, float* part, float* out, uint16_t* out
 // out[i] = bf16(sum_s parts[s][i]) over S bf16 partial arrays of n elements (n % 8 == 0)
 void split_sum_bf16(const uint16_t* parts, uint16_t* out, int64_t n, int S, hipStream_t s);
 
+// (dst, src, bytes) regions copied by one launch; pointers 16-byte aligned,
+// byte counts multiples of 4
+constexpr int kMaxCopies = 12;
+struct CopyList {
+  void* dst[kMaxCopies];
+  const void* src[kMaxCopies];
+  int64_t bytes[kMaxCopies];
+  int n;
+};
+void multi_copy(const CopyList& cl, hipStream_t s);
+
 void xent_fwd(bool bf16, const void* z, const int64_t* y, float* loss, float* lse, int N, int K, hipStream_t s);
 void xent_bwd(bool bf16, const void* z, const int64_t* y, const float* lse, const float* gscale, void* dz, int N, int K,
               hipStream_t s);

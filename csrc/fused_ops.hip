@@ -633,6 +633,25 @@ void column_sum(bool bf16, const void* dy, float* part, float* out, uint16_t* ou
 // reduction of split-K weight-gradient partials (one pass; replaces a generic
 // reduce kernel + a float->bf16 cast kernel).  n % 8 == 0, 16-B accesses.
 // ---------------------------------------------------------------------------
+// ---------------------------------------------------------------------------
+// Multi-region device copy: up to kMaxCopies (dst, src, bytes) regions in ONE
+// launch (a weight snapshot of several tensors was one blit kernel per region,
+// ~5 us each on the learner's stream).  Workgroups stride over the regions'
+// 16-byte chunks; a region's dword tail is copied by its first workgroup.
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void multi_copy_kernel(p2fused::CopyList cl) {
+  const int64_t stride = int64_t(gridDim.x) * 256;
+  for (int r = 0; r < cl.n; ++r) {
+    const int64_t n16 = cl.bytes[r] >> 4;
+    const uint4* __restrict__ s16 = reinterpret_cast<const uint4*>(cl.src[r]);
+    uint4* __restrict__ d16 = reinterpret_cast<uint4*>(cl.dst[r]);
+    for (int64_t i = int64_t(blockIdx.x) * 256 + threadIdx.x; i < n16; i += stride) d16[i] = s16[i];
+    const int64_t tail = (cl.bytes[r] & 15) >> 2;
+    if (blockIdx.x == 0 && threadIdx.x < tail)
+      reinterpret_cast<uint32_t*>(cl.dst[r])[n16 * 4 + threadIdx.x] = reinterpret_cast<const uint32_t*>(cl.src[r])[n16 * 4 + threadIdx.x];
+  }
+}
+
 __global__ __launch_bounds__(256) void split_sum_bf16_kernel(const uint16_t* __restrict__ parts,
                                                              uint16_t* __restrict__ out, int64_t n8, int S) {
   const int64_t stride = int64_t(gridDim.x) * blockDim.x;
@@ -659,6 +678,13 @@ __global__ __launch_bounds__(256) void split_sum_bf16_kernel(const uint16_t* __r
 void split_sum_bf16(const uint16_t* parts, uint16_t* out, int64_t n, int S, hipStream_t s) {
   const int64_t n8 = n / 8;
   hipLaunchKernelGGL(split_sum_bf16_kernel, dim3(stream_grid(n8, 256)), dim3(256), 0, s, parts, out, n8, S);
+}
+
+void multi_copy(const CopyList& cl, hipStream_t s) {
+  int64_t chunks = 0;
+  for (int r = 0; r < cl.n; ++r) chunks = std::max<int64_t>(chunks, cl.bytes[r] >> 4);
+  const int grid = int(std::min<int64_t>(std::max<int64_t>((chunks + 255) / 256, 1), 2048));
+  hipLaunchKernelGGL(multi_copy_kernel, dim3(grid), dim3(256), 0, s, cl);
 }
 
 void xent_fwd(bool bf16, const void* z, const int64_t* y, float* loss, float* lse, int N, int K, hipStream_t s) {

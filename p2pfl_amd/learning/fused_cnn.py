@@ -215,15 +215,58 @@ class FusedCNNEngine:
         return self.arena.module(x.float() / 255.0)
 
 
+class _EvalSnapshot:
+    """The weights one kind of evaluation pass reads, copied out of the engine.
+
+    An evaluation pass runs on the learner's evaluation stream NEXT TO the
+    training that follows it (the test pass beside the round's epoch, the
+    validation pass beside the next round's), so it must not read the arena
+    the optimizer is rewriting.  The copy is taken on the learner's stream at
+    the point the pass's semantics fix (after the epoch / the aggregation):
+    the fp32 ranges the forward kernels read (conv1 weight + bias, conv2 bias,
+    l1 bias, l2 weight + bias; a few tens of KB) and the bf16 shadows (conv2,
+    FC1, FC2; 13 MB).  Before, the passes sat between two epochs on the
+    device's critical path: 0.45 ms of a 7.9 ms round (profiles/r5_cnn_gaps.md).
+    """
+
+    READ = ("conv1.weight", "conv1.bias", "conv2.bias", "l1.bias", "l2.weight", "l2.bias")
+
+    def __init__(self, eng: "FusedCNNEngine") -> None:
+        self.params = torch.zeros_like(eng.params)
+        self.w2r = torch.zeros_like(eng.w2r)
+        self.w1bf = torch.zeros_like(eng.w1bf)
+        self.w2bf = None if eng.w2bf is None else torch.zeros_like(eng.w2bf)
+        ends = list(eng.off[1:]) + [eng.params.numel()]
+        spans = sorted((eng.off[_NAMES.index(n)], ends[_NAMES.index(n)]) for n in self.READ)
+        self.ranges: List[Tuple[int, int]] = []
+        for a, b in spans:  # adjacent parameters: one copy
+            if self.ranges and self.ranges[-1][1] == a:
+                self.ranges[-1] = (self.ranges[-1][0], b)
+            else:
+                self.ranges.append((a, b))
+        self.done: Optional[torch.cuda.Event] = None  # end of the last pass that read this copy
+
+    def take(self, eng: "FusedCNNEngine") -> None:
+        """Enqueue the copy on the current stream: ONE launch of the multi-region
+        copy kernel (csrc/fused_ops.hip; one blit kernel per region was ~45 us
+        for a snapshot on the learner's stream, profiles/r5_cnn_gaps.md)."""
+        dst = [self.params[a:b] for a, b in self.ranges] + [self.w2r, self.w1bf]
+        src = [eng.params[a:b] for a, b in self.ranges] + [eng.w2r, eng.w1bf]
+        if self.w2bf is not None:
+            dst.append(self.w2bf)
+            src.append(eng.w2bf)
+        ops.ext().fused.multi_copy(dst, src)
+
+
 class _EvalForward:
     """Forward-only view of a :class:`FusedCNNEngine` at 128 samples per launch.
 
     Evaluation has no optimizer step between batches, so it runs the same
-    forward kernels (reading the engine's fp32 parameters and bf16 shadows)
-    on 128-sample batches: a quarter of the launches per pass, and the FC1
-    GEMM -- bound by streaming its 12.8 MB weight -- costs little more per
-    launch at 128 rows than at 32.  Per-sample losses and predictions do not
-    depend on how the set is batched.
+    forward kernels (reading a :class:`_EvalSnapshot` of the engine's fp32
+    parameters and bf16 shadows) on 128-sample batches: a quarter of the
+    launches per pass, and the FC1 GEMM -- bound by streaming its 12.8 MB
+    weight -- costs little more per launch at 128 rows than at 32.
+    Per-sample losses and predictions do not depend on how the set is batched.
     """
 
     MROWS = 128
@@ -237,13 +280,22 @@ class _EvalForward:
         self.slabs1 = z(eng.S1 * M * HID)
         self.H, self.dH = z(M * HID, dt=bf), z(M * HID, dt=bf)
         self.dlogits = z(M * 10)
+        self.snaps: Dict[str, _EvalSnapshot] = {}
 
-    def forward(self, x: torch.Tensor, labels: torch.Tensor, idx: Optional[torch.Tensor], B: int, stats: torch.Tensor) -> None:
+    def snapshot(self, name: str) -> _EvalSnapshot:
+        """The weight copy the ``name`` pass (its captured graph) reads."""
+        if name not in self.snaps:
+            self.snaps[name] = _EvalSnapshot(self.eng)
+        return self.snaps[name]
+
+    def forward(self, x: torch.Tensor, labels: torch.Tensor, idx: Optional[torch.Tensor], B: int, stats: torch.Tensor,
+                snap: _EvalSnapshot) -> None:
         e, C, M = self.eng, self.eng.C, self.MROWS
-        C.conv1_fwd(x, idx, e.params, e.off, self.p1, self.am1, None, B)
-        C.conv2_fwd(self.p1, e.w2r, e.params, e.off, self.a1, self.am2, B, M)
-        C.gemm_skinny(self.a1, e.w1bf, self.slabs1, M, HID, FEAT, e.S1)
-        C.head(self.slabs1, e.S1, M, e.params, e.off, labels, idx, B, False, self.H, self.dH, self.dlogits, stats, e.w2bf)
+        C.conv1_fwd(x, idx, snap.params, e.off, self.p1, self.am1, None, B)
+        C.conv2_fwd(self.p1, snap.w2r, snap.params, e.off, self.a1, self.am2, B, M)
+        C.gemm_skinny(self.a1, snap.w1bf, self.slabs1, M, HID, FEAT, e.S1)
+        C.head(self.slabs1, e.S1, M, snap.params, e.off, labels, idx, B, False, self.H, self.dH, self.dlogits, stats,
+               snap.w2bf)
 
 
 class _EpochGraph:
@@ -282,11 +334,10 @@ class FusedCNNLearner(TorchLearner):
         self._dirty_shadows = False
         self._eval_fwd = _EvalForward(self.engine)
         # asynchronous passes: metrics are read back by a completion thread;
-        # the validation pass runs on its own stream next to whatever follows
-        # the training epoch (the gossip snapshot + RCCL push of the weights)
+        # the evaluation passes (validation, test) run on their own stream, on
+        # weight snapshots, next to the training that follows them
         self._completions = HostCompletions(self_addr)
-        self._val_stream = private_stream(self.device)
-        self._val_done: Optional[torch.cuda.Event] = None  # last side-stream reader of the arena
+        self._eval_stream = private_stream(self.device)
         # completion events of the last RUN_AHEAD fits: the host may enqueue
         # round r + 1 while round r still trains, so the device never idles
         # while the stage machine moves between rounds (with a one-fit bound the
@@ -296,18 +347,10 @@ class FusedCNNLearner(TorchLearner):
         self._last_epoch_end: Optional[torch.cuda.Event] = None
 
     # -- parameters: keep the bf16 shadows in sync -------------------------
-    def _wait_arena_readers(self) -> None:
-        """Order the caller's stream after the side-stream validation pass (it
-        reads the weights and shares the evaluation buffers)."""
-        ev = self._val_done
-        if ev is not None:
-            torch.cuda.current_stream(self.device).wait_event(ev)
-
     def set_parameters(self, params) -> None:
         if isinstance(params, FlatParams) and params.flat.data_ptr() == self.engine.params.data_ptr():
             self._arena_changed()
             return  # the arena itself: weights and bf16 shadows are already current
-        self._wait_arena_readers()
         super().set_parameters(params)
         with torch.cuda.stream(torch.cuda.current_stream(self.device)):
             self.engine.pack_shadows()
@@ -357,22 +400,25 @@ class FusedCNNLearner(TorchLearner):
             if g.graph is not None:
                 g.graph.replay()
             else:
-                self._enqueue(loader, plan, train, g.perm, g.stats)
+                self._enqueue(name, loader, plan, train, g.perm, g.stats)
         return g.stats
 
-    def _enqueue(self, loader, plan, train, perm, stats) -> None:
+    def _enqueue(self, name, loader, plan, train, perm, stats) -> None:
         x = loader.x.reshape(-1, 784)
         y = loader.y
+        snap = None if train else self._eval_fwd.snapshot(name)
         for j, (s, b) in enumerate(plan):
             idx = perm[s : s + b]
             st = stats[j] if train else stats[0]
             if train:
                 self.engine.train_step_async(x, y, idx, b, st, j + 1)
             else:
-                self._eval_fwd.forward(x, y, idx, b, st)
+                self._eval_fwd.forward(x, y, idx, b, st, snap)
 
     def _capture(self, name, loader, plan, train, key) -> _EpochGraph:
         n = len(loader.dataset)
+        if not train:
+            self._eval_fwd.snapshot(name)  # its buffers exist before (outside) the capture
         eg = _EpochGraph(None, key)
         eg.perm = torch.arange(n, dtype=torch.int64, device=self.device)
         eg.stats = torch.zeros((len(plan) if train else 1, 4), dtype=torch.float32, device=self.device)
@@ -388,7 +434,7 @@ class FusedCNNLearner(TorchLearner):
             torch.cuda.synchronize(self.device)
             graph = torch.cuda.CUDAGraph()
             with no_gc(collect=False), torch.cuda.graph(graph, stream=self._stream, capture_error_mode="relaxed"):
-                self._enqueue(loader, plan, train, eg.perm, eg.stats)
+                self._enqueue(name, loader, plan, train, eg.perm, eg.stats)
             torch.cuda.synchronize(self.device)
         eg.graph = graph
         return eg
@@ -437,7 +483,6 @@ class FusedCNNLearner(TorchLearner):
             for epoch in range(self.epochs):
                 if self._interrupt.is_set():
                     return
-                self._wait_arena_readers()  # the previous epoch's validation read these weights
                 self.engine.adam_t.fill_(epoch * steps)  # Adam step base for this epoch's graph
                 t0, t1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                 t0.record(cur)
@@ -474,14 +519,27 @@ class FusedCNNLearner(TorchLearner):
             logger.tracer.record(self._addr, "inter_epoch_gpu", time.perf_counter() - gap * 1e-3, gap * 1e-3)
 
     def _eval_async(self, name: str, loader, on_done) -> None:
-        """Enqueue an evaluation pass on the current stream; ``on_done(loss, metric)``
-        runs on the completion thread."""
+        """Enqueue an evaluation pass of the weights as the current stream has
+        them now; ``on_done(loss, metric)`` runs on the completion thread.
+
+        The weights are copied on the current stream (the only cost left on its
+        timeline); the pass itself runs on the evaluation stream beside whatever
+        the current stream does next.  The evaluation passes share their
+        activation buffers, so they stay serialised on that one stream."""
         self._ensure_graph(name, loader, False)  # first-use capture outside the lock
+        snap = self._eval_fwd.snapshot(name)
+        cur, es = torch.cuda.current_stream(self.device), self._eval_stream
         with self._lock:
-            stats = self._run(name, loader, False, None)
-        host = self._readback(stats[0, :2])
-        ev = torch.cuda.Event()
-        ev.record(torch.cuda.current_stream(self.device))
+            if snap.done is not None:
+                cur.wait_event(snap.done)  # the previous pass on this copy finished reading it
+            snap.take(self.engine)
+            es.wait_stream(cur)
+            with torch.cuda.stream(es):
+                stats = self._run(name, loader, False, None)
+                host = self._readback(stats[0, :2])
+                ev = torch.cuda.Event()
+                ev.record(es)
+            snap.done = ev
         n = max(1, len(loader.dataset))
 
         def fin() -> None:
@@ -495,13 +553,8 @@ class FusedCNNLearner(TorchLearner):
         loader = self.data.val_dataloader()
         if loader is None or len(loader.dataset) == 0:
             return
-        vs = self._val_stream
-        vs.wait_stream(torch.cuda.current_stream(self.device))  # after the epoch that produced the weights
         step = self._step
-        with torch.cuda.stream(vs):
-            self._val_done = self._eval_async(
-                "val", loader, lambda loss, acc: (self._log("val_loss", loss, step=step), self._log("val_metric", acc, step=step))
-            )
+        self._eval_async("val", loader, lambda loss, acc: (self._log("val_loss", loss, step=step), self._log("val_metric", acc, step=step)))
 
     def _validate(self) -> None:
         self._validate_async()
@@ -522,7 +575,6 @@ class FusedCNNLearner(TorchLearner):
                 on_results(results)
 
         with logger.span(self._addr, "evaluate"), self._on_stream():
-            self._wait_arena_readers()  # shares the evaluation buffers with validation
             self._eval_async("test", self.data.test_dataloader(), done)
         return True
 

@@ -251,3 +251,29 @@ def test_async_fit_orders_validation_before_replaced_weights():
     assert got[0][1] == pytest.approx(got[1][1], rel=1e-5) and got[0][2] == got[1][2]
     # validation of a zeroed CNN would give the uniform loss log(10)
     assert abs(got[0][1] - 2.302585) > 1e-3
+
+
+def test_evaluation_pass_beside_next_fit_reads_its_snapshot():
+    """evaluate_async() copies the weights it evaluates and runs beside the fit()
+    enqueued right after it: the metrics are the PRE-fit weights', equal to an
+    evaluation that finished before the fit started."""
+    from p2pfl_amd.data import MnistFederatedDM
+    from p2pfl_amd.learning.fused_cnn import FusedCNNLearner
+
+    res = []
+    for overlap in (True, False):
+        torch.manual_seed(5)
+        ln = FusedCNNLearner(CNN(seed=5), MnistFederatedDM(sub_id=0, number_sub=40, batch_size=32), "p", 1)
+        ln.fit()
+        ln.drain()
+        box = {}
+        assert ln.evaluate_async(box.update)
+        if not overlap:
+            ln.drain()
+        ln.fit()  # rewrites every weight while (overlap) the test pass may still run
+        ln.drain()
+        torch.cuda.synchronize()
+        res.append(box)
+    # (the loss sum's fp32 accumulation order may differ in the last bit)
+    assert res[0]["test_metric"] == res[1]["test_metric"], res
+    assert abs(res[0]["test_loss"] - res[1]["test_loss"]) <= 1e-6 * abs(res[1]["test_loss"]), res

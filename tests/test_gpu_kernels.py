@@ -277,3 +277,17 @@ def test_weighted_sum_running_fold_is_bitwise_equal_to_one_shot():
     torch.testing.assert_close(one.double(), ref, rtol=1e-5, atol=1e-5)
     # the wrapper FedAvg uses
     torch.testing.assert_close(ops.weighted_average(flats, w), one, rtol=0, atol=0)
+
+
+def test_multi_copy_regions():
+    """fused.multi_copy: every (dst, src) pair copied in one launch, dword tails included, dtypes mixed."""
+    C = ops.ext().fused
+    g = torch.Generator(device="cuda").manual_seed(0)
+    srcs = [torch.randn(n, device="cuda", generator=g) for n in (3, 4, 17, 4096 + 5, 1 << 20)]
+    srcs.append(torch.randn(6002, device="cuda", generator=g).to(torch.bfloat16))
+    dsts = [torch.zeros_like(s) for s in srcs]
+    C.multi_copy(dsts, srcs)
+    for d, s in zip(dsts, srcs):
+        assert torch.equal(d, s)
+    with pytest.raises(RuntimeError):
+        C.multi_copy([torch.zeros(4, device="cuda")], [torch.zeros(5, device="cuda")])

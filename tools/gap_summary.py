@@ -22,6 +22,9 @@ def main() -> None:
     ap.add_argument("--top", type=int, default=15)
     ap.add_argument("--min-gap-us", type=float, default=5.0)
     ap.add_argument("--out", default=None)
+    ap.add_argument("--around", default=None, help="also list the kernels (all queues) around the second-to-last "
+                    "launch whose name contains this string, with start offsets and durations")
+    ap.add_argument("--span", type=int, default=30, help="kernels listed on each side for --around")
     args = ap.parse_args()
     rows = []
     for r in csv.DictReader(open(args.trace)):
@@ -58,6 +61,18 @@ def main() -> None:
              "| gap us | after | before |", "|---:|---|---|"]
     for g, a, b in sorted(big, key=lambda x: -x[0])[: args.top]:
         lines.append(f"| {g:.1f} | `{short(a)}` | `{short(b)}` |")
+    if args.around:
+        hits = [i for i, x in enumerate(rows) if args.around in x[2]]
+        if len(hits) >= 2:
+            c = hits[-2]
+            seg = rows[max(0, c - args.span): c + args.span]
+            t0 = seg[0][0]
+            lines += ["", f"## kernels around the second-to-last `{args.around}`", "",
+                      "| start us | dur us | idle before us | kernel |", "|---:|---:|---:|---|"]
+            prev_end = seg[0][0]
+            for s_, e_, n_ in seg:
+                lines.append(f"| {(s_ - t0) / 1e3:.1f} | {(e_ - s_) / 1e3:.1f} | {max(0, s_ - prev_end) / 1e3:.1f} | `{short(n_)}` |")
+                prev_end = max(prev_end, e_)
     text = "\n".join(lines)
     print(text)
     if args.out:
