@@ -106,8 +106,8 @@ void sgd_step(torch::Tensor p, torch::Tensor g, c10::optional<torch::Tensor> buf
 }
 
 // ---- multi-tensor optimizer steps (mixed-precision learners) ----------------
-// tens: int64 [T, 3] (offset, numel, flags) on the GPU; chunks: int32 [C, 2]
-// (tensor, chunk) on the GPU; grads: one entry per tensor (None = skip).
+// tens: int64 [T, 4] (offset, numel, flags, chunk) on the GPU; chunks: int32 [C, 2]
+// (tensor, first element) on the GPU; grads: one entry per tensor (None = skip).
 torch::Tensor grad_table(const std::vector<c10::optional<torch::Tensor>>& grads, const std::vector<int64_t>& numels,
                          const std::vector<bool>& grad_bf16, const std::vector<bool>& grad_cl, const torch::Device& dev) {
   const size_t T = grads.size();
@@ -133,9 +133,9 @@ torch::Tensor grad_table(const std::vector<c10::optional<torch::Tensor>>& grads,
 }
 
 void check_tables(const torch::Tensor& tens, const torch::Tensor& chunks, const torch::Device& dev) {
-  TORCH_CHECK(tens.device() == dev && tens.scalar_type() == torch::kInt64 && tens.dim() == 2 && tens.size(1) == 3 &&
+  TORCH_CHECK(tens.device() == dev && tens.scalar_type() == torch::kInt64 && tens.dim() == 2 && tens.size(1) == 4 &&
                   tens.is_contiguous(),
-              "tensor table must be int64 [T, 3] on the arena's device");
+              "tensor table must be int64 [T, 4] on the arena's device");
   TORCH_CHECK(chunks.device() == dev && chunks.scalar_type() == torch::kInt32 && chunks.dim() == 2 &&
                   chunks.size(1) == 2 && chunks.is_contiguous(),
               "chunk table must be int32 [C, 2] on the arena's device");

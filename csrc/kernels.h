@@ -36,15 +36,20 @@ struct SgdParams {
 void sgd_step(float* p, const float* g, float* buf, uint16_t* p_bf16, int64_t n, const SgdParams& h, hipStream_t s);
 
 // Multi-tensor optimizer steps (mixed-precision learners, optim.hip).
-constexpr int kMTChunk = 4096;  // elements per block
+constexpr int kMTChunk = 4096;  // elements per block (dense tensors)
+constexpr int kMTMaxCL = 4608;  // elements per block of a channels-last tensor staged through LDS
+                                // (whole output-channel slabs: the largest ResNet slab is 512 x 3 x 3)
 constexpr int kMTGradBf16 = 1;  // gradient tensor is bf16 (else fp32)
 constexpr int kMTShadow = 2;    // also write the bf16 shadow of the weight
 constexpr int kMTPermCL = 4;    // grad + shadow in channels-last (O, kh, kw, I) order; fp32 state OIHW.
                                 // flags bits 8..31 = I, bits 32..55 = kh * kw
+// Tables built by p2pfl_amd/learning/optim.py mt_tables(): chunks are int32
+// (tensor, first element) pairs; a block covers [first, first + min(chunk, n - first)).
 struct MTTensor {
-  int64_t off;  // element offset in the flat arenas
-  int64_t n;    // elements
+  int64_t off;    // element offset in the flat arenas
+  int64_t n;      // elements
   int64_t flags;
+  int64_t chunk;  // elements per block (kMTChunk, or whole (I, kh, kw) slabs for the LDS-staged path)
 };
 void adam_mt_step(float* p, float* m, float* v, uint16_t* p_bf16, const MTTensor* tens, const int2* chunks,
                   int n_chunks, const uint64_t* grad_ptrs, const AdamParams& h, hipStream_t s);

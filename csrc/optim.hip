@@ -145,6 +145,44 @@ P2_DEVICE uint32_t cl_index_fast(uint32_t i, uint32_t C, const FastDivU& per_o, 
 P2_DEVICE uint32_t cl_c(int64_t flags) { return uint32_t((flags >> 8) & 0xFFFFFF); }
 P2_DEVICE uint32_t cl_hw(int64_t flags) { return uint32_t((flags >> 32) & 0xFFFFFF); }
 
+// ---- channels-last chunks staged through LDS ---------------------------------
+// A chunk of whole output-channel slabs covers the SAME element range in the
+// OIHW state and in the (O, kh, kw, I) gradient / shadow, only permuted inside
+// each slab.  So every global access can be contiguous: the gradient is read
+// as 8 / 16-byte vectors into LDS (one pad word after every I-run, so the
+// OIHW-order reads that follow -- I-runs apart -- hit distinct banks), the
+// fp32 state is streamed in OIHW order as 16-byte vectors, and the new bf16
+// weights go back through LDS to 8-byte stores.  The per-element gather /
+// scatter of the fallback path below (2-byte gradient loads and shadow stores
+// at channels-last positions) ran sgd_mt at 50-65 % of HBM roofline on
+// ResNet-18 (profiles/r4_resnet18_steady_state.md).
+constexpr int kMTClPad = kMTMaxCL + kMTMaxCL / 4;  // gradient words incl. pads (I >= 4)
+struct ClStage {
+  float g[kMTClPad];
+  uint16_t sh[kMTMaxCL];
+};
+P2_DEVICE bool cl_staged(uint32_t C, uint32_t HW, int64_t len) { return HW > 1 && C % 4 == 0 && len <= kMTMaxCL; }
+// LDS word of channels-last element j (one pad word per I-run of C elements)
+P2_DEVICE uint32_t cl_pad(uint32_t j, const FastDivU& fc) { return j + fdivu(j, fc); }
+P2_DEVICE void cl_load_grad(ClStage& st, const void* g, bool gbf, int64_t first, int len, const FastDivU& fc) {
+  for (int j = threadIdx.x * 4; j < len; j += 1024) {
+    float v[4];
+    load_grad4(g, gbf, first + j, v);
+    const uint32_t q = cl_pad(uint32_t(j), fc);  // the 4 share one I-run (I % 4 == 0)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) st.g[q + e] = v[e];
+  }
+}
+// channels-last position (within the chunk) of OIHW element i
+P2_DEVICE uint32_t cl_local(uint32_t i, uint32_t C, const FastDivU& per_o, const FastDivU& hw) {
+  const uint32_t o = fdivu(i, per_o), r = i - o * per_o.d, c = fdivu(r, hw), s = r - c * hw.d;
+  return o * per_o.d + s * C + c;
+}
+P2_DEVICE void cl_store_shadow(const ClStage& st, uint16_t* __restrict__ sb, int len) {
+  for (int j = threadIdx.x * 4; j < len; j += 1024)
+    *reinterpret_cast<uint2*>(sb + j) = *reinterpret_cast<const uint2*>(st.sh + j);
+}
+
 P2_DEVICE void adam_elem(float& p, float g, float& m, float& v, const AdamParams& h) {
   if (h.weight_decay != 0.f) {
     if (h.decoupled)
@@ -167,18 +205,50 @@ __global__ __launch_bounds__(256) void adam_mt_kernel(float* __restrict__ p, flo
     h.step_size = h.lr / (1.f - powf(h.beta1, t));
     h.inv_sqrt_bc2 = rsqrtf(1.f - powf(h.beta2, t));
   }
+  __shared__ ClStage st;
   const int2 ch = chunks[blockIdx.x];
   const void* g = reinterpret_cast<const void*>(gptr[ch.x]);
   if (g == nullptr) return;
   const MTTensor T = tens[ch.x];
   const bool gbf = T.flags & kMTGradBf16, shadow = (T.flags & kMTShadow) && pbf;
-  const int64_t start = int64_t(ch.y) * kMTChunk;
-  const int64_t len = T.n - start < kMTChunk ? T.n - start : kMTChunk;
+  const int64_t start = ch.y;
+  const int64_t len = T.n - start < T.chunk ? T.n - start : T.chunk;
   const int64_t len4 = len & ~int64_t(3);
   float* P = p + T.off + start;
   float* M = m + T.off + start;
   float* V = v + T.off + start;
   uint16_t* PB = shadow ? pbf + T.off + start : nullptr;
+  if ((T.flags & kMTPermCL) && cl_staged(cl_c(T.flags), cl_hw(T.flags), len)) {
+    const uint32_t C = cl_c(T.flags), HW = cl_hw(T.flags);
+    const FastDivU fpo = make_fastdiv_u(C * HW), fhw = make_fastdiv_u(HW), fc = make_fastdiv_u(C);
+    cl_load_grad(st, g, gbf, start, int(len), fc);
+    __syncthreads();
+    for (int i = threadIdx.x * 4; i < len; i += 1024) {
+      float4 pp = *reinterpret_cast<float4*>(P + i), mm = *reinterpret_cast<float4*>(M + i),
+             vv = *reinterpret_cast<float4*>(V + i);
+      uint32_t j[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) j[e] = cl_local(uint32_t(i + e), C, fpo, fhw);
+      adam_elem(pp.x, st.g[cl_pad(j[0], fc)], mm.x, vv.x, h);
+      adam_elem(pp.y, st.g[cl_pad(j[1], fc)], mm.y, vv.y, h);
+      adam_elem(pp.z, st.g[cl_pad(j[2], fc)], mm.z, vv.z, h);
+      adam_elem(pp.w, st.g[cl_pad(j[3], fc)], mm.w, vv.w, h);
+      *reinterpret_cast<float4*>(P + i) = pp;
+      *reinterpret_cast<float4*>(M + i) = mm;
+      *reinterpret_cast<float4*>(V + i) = vv;
+      if (PB) {
+        st.sh[j[0]] = f32_to_bf16(pp.x);
+        st.sh[j[1]] = f32_to_bf16(pp.y);
+        st.sh[j[2]] = f32_to_bf16(pp.z);
+        st.sh[j[3]] = f32_to_bf16(pp.w);
+      }
+    }
+    if (PB) {
+      __syncthreads();
+      cl_store_shadow(st, PB, int(len));
+    }
+    return;
+  }
   if (T.flags & kMTPermCL) {
     // fp32 state in logical (coalesced) order; the bf16 gradient and shadow
     // are gathered / scattered at their channels-last positions (the whole
@@ -268,17 +338,48 @@ __global__ __launch_bounds__(256) void sgd_mt_kernel(float* __restrict__ p, floa
                                                      uint16_t* __restrict__ pbf, const MTTensor* __restrict__ tens,
                                                      const int2* __restrict__ chunks, const uint64_t* __restrict__ gptr,
                                                      SgdParams h) {
+  __shared__ ClStage st;
   const int2 ch = chunks[blockIdx.x];
   const void* g = reinterpret_cast<const void*>(gptr[ch.x]);
   if (g == nullptr) return;
   const MTTensor T = tens[ch.x];
   const bool gbf = T.flags & kMTGradBf16, shadow = (T.flags & kMTShadow) && pbf;
-  const int64_t start = int64_t(ch.y) * kMTChunk;
-  const int64_t len = T.n - start < kMTChunk ? T.n - start : kMTChunk;
+  const int64_t start = ch.y;
+  const int64_t len = T.n - start < T.chunk ? T.n - start : T.chunk;
   float* P = p + T.off + start;
   float* B = buf ? buf + T.off + start : nullptr;
   uint16_t* PB = shadow ? pbf + T.off + start : nullptr;
-  if (T.flags & kMTPermCL) {  // see adam_mt_kernel (4 elements per thread in flight)
+  if ((T.flags & kMTPermCL) && cl_staged(cl_c(T.flags), cl_hw(T.flags), len)) {  // see adam_mt_kernel
+    const uint32_t C = cl_c(T.flags), HW = cl_hw(T.flags);
+    const FastDivU fpo = make_fastdiv_u(C * HW), fhw = make_fastdiv_u(HW), fc = make_fastdiv_u(C);
+    cl_load_grad(st, g, gbf, start, int(len), fc);
+    __syncthreads();
+    for (int i = threadIdx.x * 4; i < len; i += 1024) {
+      float4 pp = *reinterpret_cast<float4*>(P + i);
+      float4 bb = B ? *reinterpret_cast<float4*>(B + i) : float4{0.f, 0.f, 0.f, 0.f};
+      uint32_t j[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) j[e] = cl_local(uint32_t(i + e), C, fpo, fhw);
+      sgd_regs(pp.x, st.g[cl_pad(j[0], fc)], bb.x, B != nullptr, h);
+      sgd_regs(pp.y, st.g[cl_pad(j[1], fc)], bb.y, B != nullptr, h);
+      sgd_regs(pp.z, st.g[cl_pad(j[2], fc)], bb.z, B != nullptr, h);
+      sgd_regs(pp.w, st.g[cl_pad(j[3], fc)], bb.w, B != nullptr, h);
+      *reinterpret_cast<float4*>(P + i) = pp;
+      if (B) *reinterpret_cast<float4*>(B + i) = bb;
+      if (PB) {
+        st.sh[j[0]] = f32_to_bf16(pp.x);
+        st.sh[j[1]] = f32_to_bf16(pp.y);
+        st.sh[j[2]] = f32_to_bf16(pp.z);
+        st.sh[j[3]] = f32_to_bf16(pp.w);
+      }
+    }
+    if (PB) {
+      __syncthreads();
+      cl_store_shadow(st, PB, int(len));
+    }
+    return;
+  }
+  if (T.flags & kMTPermCL) {  // gather path (4 elements per thread in flight, see adam_mt_kernel)
     const uint32_t C = cl_c(T.flags), HW = cl_hw(T.flags);
     FastDivU fpo{}, fhw{};
     if (FD) fpo = make_fastdiv_u(C * HW), fhw = make_fastdiv_u(HW);

@@ -14,7 +14,7 @@ left to torch.
 
 from __future__ import annotations
 
-from typing import Optional
+from typing import Optional, Tuple
 
 import torch
 
@@ -149,17 +149,45 @@ def fuse_optimizer(opt: torch.optim.Optimizer, arena: ModuleArena):
 # ----------------------------------------------------------------------------
 # Multi-tensor optimizers for mixed-precision arenas (ModuleArena(compute_dtype=...))
 # ----------------------------------------------------------------------------
+MT_CHUNK = 4096  # csrc/kernels.h kMTChunk
+MT_MAX_CL = 4608  # csrc/kernels.h kMTMaxCL
+
+
+def mt_layout(table, dev) -> Tuple[torch.Tensor, torch.Tensor]:
+    """Device tables of the multi-tensor kernels for ``table`` = [(offset, numel,
+    flags)]: ``tens`` int64 [T, 4] = (offset, numel, flags, elements per
+    block) and ``chunks`` int32 [C, 2] = (tensor, first element), one GPU
+    block per chunk.  A channels-last tensor (flags bit 2) whose output-channel
+    slab (I x kh x kw elements, I % 4 == 0) fits csrc/optim.hip's LDS stage
+    gets chunks of whole slabs, which the kernel reads and writes contiguously;
+    every other tensor 4096-element chunks."""
+    rows, chunks = [], []
+    for t, (off, n, flags) in enumerate(table):
+        chunk = MT_CHUNK
+        if flags & 4:
+            i, hw = (flags >> 8) & 0xFFFFFF, (flags >> 32) & 0xFFFFFF
+            per_o = i * hw
+            if hw > 1 and i % 4 == 0 and per_o <= MT_MAX_CL:
+                chunk = per_o * (MT_MAX_CL // per_o)
+        rows.append((off, n, flags, chunk))
+        chunks.extend((t, c) for c in range(0, n, chunk))
+    if any(c >= 2**31 for _, c in chunks):
+        raise ValueError("multi-tensor chunk offset exceeds int32")
+    tens = torch.tensor(rows, dtype=torch.int64, device=dev).reshape(-1, 4)
+    return tens, torch.tensor(chunks, dtype=torch.int32, device=dev).reshape(-1, 2)
+
+
 class MTTables:
     """Static per-tensor and per-chunk tables for the multi-tensor kernels.
 
-    ``tens`` int64 [T, 3] = (arena offset, numel, flags) with flags bit 0 =
-    bf16 gradient, bit 1 = write the bf16 shadow, bit 2 = gradient and shadow
-    are channels-last (O, kh, kw, I) with I in bits 8..31 and kh*kw in bits
-    32..55 (the fp32 state stays OIHW); ``chunks`` int32 [C, 2] =
-    (tensor, chunk index) -- one GPU block per 4096-element chunk.
+    ``table`` = [(arena offset, numel, flags)] with flags bit 0 = bf16
+    gradient, bit 1 = write the bf16 shadow, bit 2 = gradient and shadow are
+    channels-last (O, kh, kw, I) with I in bits 8..31 and kh*kw in bits
+    32..55 (the fp32 state stays OIHW); ``tens`` / ``chunks``: the device
+    tables of :func:`mt_layout`.
     """
 
-    CHUNK = 4096
+    CHUNK = MT_CHUNK
 
     def __init__(self, arena: ModuleArena) -> None:
         lay = arena.layout
@@ -167,7 +195,6 @@ class MTTables:
         self.params = [p for _, p in arena.module.named_parameters()]
         names = [n for n, _ in arena.module.named_parameters()]
         self.table = []
-        chunks = []
         for t, (name, p) in enumerate(zip(names, self.params)):
             off = lay.offsets[lay.names.index(name)]
             flags = (1 if p.dtype == torch.bfloat16 else 0) | (2 if name in shadow else 0)
@@ -175,13 +202,11 @@ class MTTables:
                 o, i, kh, kw = arena.shadow_cl[name][1]
                 flags |= 4 | (i << 8) | ((kh * kw) << 32)
             self.table.append((off, p.numel(), flags))
-            chunks.extend((t, c) for c in range((p.numel() + self.CHUNK - 1) // self.CHUNK))
         dev = arena.flat.device
         self.numels = [n for _, n, _ in self.table]
         self.grad_bf16 = [bool(f & 1) for _, _, f in self.table]
         self.grad_cl = [bool(f & 4) for _, _, f in self.table]
-        self.tens = torch.tensor(self.table, dtype=torch.int64, device=dev).reshape(-1, 3)
-        self.chunks = torch.tensor(chunks, dtype=torch.int32, device=dev).reshape(-1, 2)
+        self.tens, self.chunks = mt_layout(self.table, dev)
 
     def grads(self):
         return [p.grad for p in self.params]

@@ -6,6 +6,7 @@ import pytest
 import torch
 
 from p2pfl_amd import ops
+from p2pfl_amd.learning.optim import mt_layout
 
 pytestmark = pytest.mark.gpu
 
@@ -101,21 +102,19 @@ class _Tables:
     """Minimal MTTables stand-in: tensors at 64-aligned offsets of one arena."""
 
     def __init__(self, sizes, bf16_flags, dev, cl=None):
-        self.table, chunks, off = [], [], 0
+        self.table, off = [], 0
         cl = cl or [None] * len(sizes)
         for t, (n, bf) in enumerate(zip(sizes, bf16_flags)):
             flags = (1 if bf else 0) | (2 if bf else 0)
             if cl[t] is not None:  # (in_channels, kh*kw): channels-last grad + shadow
                 flags |= 4 | (cl[t][0] << 8) | (cl[t][1] << 32)
             self.table.append((off, n, flags))
-            chunks.extend((t, c) for c in range((n + 4095) // 4096))
             off = (off + n + 63) // 64 * 64
         self.numel = max(off, 64)
         self.numels = list(sizes)
         self.grad_bf16 = list(bf16_flags)
         self.grad_cl = [c is not None for c in cl]
-        self.tens = torch.tensor(self.table, dtype=torch.int64, device=dev).reshape(-1, 3)
-        self.chunks = torch.tensor(chunks, dtype=torch.int32, device=dev).reshape(-1, 2)
+        self.tens, self.chunks = mt_layout(self.table, dev)
 
 
 @pytest.mark.parametrize("decoupled,wd", [(False, 0.01), (True, 0.05)])
@@ -209,7 +208,10 @@ def test_gpu_learner_uses_mixed_precision(model):
 @pytest.mark.parametrize("opt", ["adam", "sgd"])
 def test_multi_tensor_channels_last(opt):
     """Conv weights with channels-last grads/shadows: fp32 state in OIHW order, shadow written at OHWI positions."""
-    shapes = [(64, 32, 3, 3), (10, 7), (128, 64, 5, 5), (16, 3, 7, 7)]
+    # staged through LDS (csrc/optim.hip ClStage): 64x32x3x3 (slab 288: 16 slabs per chunk), 128x64x5x5
+    # (slab 1600: 2 per chunk), 512x512x3x3 (one 4608 slab per chunk), 40x36x3x3 (slab 324: 14 per
+    # chunk); gather path: 16x3x7x7 (I = 3); no permutation: 24x8x1x1
+    shapes = [(64, 32, 3, 3), (10, 7), (128, 64, 5, 5), (16, 3, 7, 7), (512, 512, 3, 3), (40, 36, 3, 3), (24, 8, 1, 1)]
     cl = [(s[1], s[2] * s[3]) if len(s) == 4 else None for s in shapes]
     sizes = [int(torch.Size(s).numel()) for s in shapes]
     mt = _Tables(sizes, [True] * len(shapes), "cuda", cl=cl)
