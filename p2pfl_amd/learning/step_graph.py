@@ -139,13 +139,16 @@ def graphable_loader(loader: Any) -> bool:
 
 
 class TrainStepGraph:
-    def __init__(self, learner: Any, opt: Any, loader: Any) -> None:
+    """HIP graph of one training step of ``batch`` samples (default the loader's
+    batch; the learner captures a second one for an epoch's short last batch)."""
+
+    def __init__(self, learner: Any, opt: Any, loader: Any, batch: Optional[int] = None) -> None:
         self.learner = learner
         self.opt = opt
         self.loader = loader
-        self.B = int(loader.batch_size)
+        self.B = int(batch or loader.batch_size)
         dev = learner.device
-        self.key = self.make_key(learner, opt, loader)
+        self.key = self.make_key(learner, opt, loader, self.B)
         self.idx = torch.zeros(self.B, dtype=torch.int64, device=dev)
         self.gtab = torch.zeros(len(opt.mt.params), dtype=torch.int64, device=dev)
         self.stream = private_stream(dev)
@@ -153,8 +156,8 @@ class TrainStepGraph:
         self.loss: Optional[torch.Tensor] = None
 
     @staticmethod
-    def make_key(learner: Any, opt: Any, loader: Any) -> Tuple:
-        return (id(opt), opt.config(), int(loader.batch_size), loader.x.data_ptr(), loader.y.data_ptr(),
+    def make_key(learner: Any, opt: Any, loader: Any, batch: Optional[int] = None) -> Tuple:
+        return (id(opt), opt.config(), int(batch or loader.batch_size), loader.x.data_ptr(), loader.y.data_ptr(),
                 learner.arena.flat.data_ptr(), id(learner.model))
 
     # -- body ---------------------------------------------------------------
@@ -229,7 +232,7 @@ class TrainStepGraph:
         self.graph = g
 
     def run(self, idx: torch.Tensor) -> torch.Tensor:
-        """One training step on the samples ``idx`` (len == batch size)."""
+        """One training step on the samples ``idx`` (len == this graph's batch)."""
         self.idx.copy_(idx, non_blocking=True)
         assert self.graph is not None
         self.graph.replay()
@@ -245,22 +248,24 @@ class EvalStepGraph:
     the end (one host sync per pass instead of one per logged value).
     """
 
-    def __init__(self, learner: Any, loader: Any, hook: Any) -> None:
+    def __init__(self, learner: Any, loader: Any, hook: Any, batch: Optional[int] = None,
+                 sums_of: Optional["EvalStepGraph"] = None) -> None:
         self.learner = learner
         self.loader = loader
         self.hook = hook
-        self.B = int(loader.batch_size)
+        self.B = int(batch or loader.batch_size)
         dev = learner.device
-        self.key = self.make_key(learner, loader, hook)
+        self.key = self.make_key(learner, loader, hook, self.B)
         self.idx = torch.zeros(self.B, dtype=torch.int64, device=dev)
-        self.keys: list = []
-        self.sums: Optional[torch.Tensor] = None
+        # a pass's remainder graph accumulates into the full-batch graph's sums
+        self.keys: list = list(sums_of.keys) if sums_of is not None else []
+        self.sums: Optional[torch.Tensor] = sums_of.sums if sums_of is not None else None
         self.stream = private_stream(dev)
         self.graph: Optional[torch.cuda.CUDAGraph] = None
 
     @staticmethod
-    def make_key(learner: Any, loader: Any, hook: Any) -> Tuple:
-        return (getattr(hook, "__name__", str(hook)), int(loader.batch_size), loader.x.data_ptr(), loader.y.data_ptr(),
+    def make_key(learner: Any, loader: Any, hook: Any, batch: Optional[int] = None) -> Tuple:
+        return (getattr(hook, "__name__", str(hook)), int(batch or loader.batch_size), loader.x.data_ptr(), loader.y.data_ptr(),
                 learner.arena.flat.data_ptr(), id(learner.model))
 
     def batch(self, idx: torch.Tensor):

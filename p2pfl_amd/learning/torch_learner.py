@@ -102,6 +102,7 @@ class TorchLearner(NodeLearner):
         # aggregation / transport work left on the default stream
         self._compute_stream: Optional[torch.cuda.Stream] = None
         self._step_graph: Any = None
+        self._tail_graphs: Dict[int, Any] = {}  # short last batch of an epoch, by size
         self._eval_graphs: Dict[str, Any] = {}
         self.model: Any = None
         self.arena: Optional[ModuleArena] = None
@@ -433,7 +434,17 @@ class TorchLearner(NodeLearner):
                     sg.capture(idx)  # takes the gate exclusively
                 with self._gate():
                     logged = {"train_loss": sg.run(idx)}
-            else:  # first step when it must seed optimizer state eagerly, and a short last batch
+            elif first_ok and idx.numel() > 1:
+                # the epoch's short last batch: a graph of its own size (captured once; the
+                # same remainder every epoch) instead of ~200 eager launches per round
+                nb = int(idx.numel())
+                tg = self._tail_graphs.get(nb)
+                if tg is None or tg.key != TrainStepGraph.make_key(self, opt, loader, nb):
+                    tg = self._tail_graphs[nb] = TrainStepGraph(self, opt, loader, nb)
+                    tg.capture(idx)
+                with self._gate():
+                    logged = {"train_loss": tg.run(idx)}
+            else:  # first step when it must seed optimizer state eagerly (and a one-sample batch)
                 with self._gate():
                     x = loader.x.index_select(0, idx)
                     if loader.normalize:
@@ -486,24 +497,50 @@ class TorchLearner(NodeLearner):
 
         return graphable_loader(loader) and len(loader.dataset) >= loader.batch_size
 
+    @staticmethod
+    def _eval_batch(loader: Any) -> int:
+        """Samples per captured evaluation step: ``Settings.EVAL_BATCH_FACTOR`` x the
+        loader's batch, halved until it fits the set.  Evaluation has no optimizer
+        step and BatchNorm uses its running statistics, so per-sample losses and
+        predictions -- and the pass's means -- do not depend on the batching; the
+        larger products (ViT-B: M = 4 x 6304 tokens) run at a higher MFMA rate."""
+        from p2pfl_amd.settings import Settings
+
+        bs, n = int(loader.batch_size), len(loader.dataset)
+        k = max(1, int(Settings.EVAL_BATCH_FACTOR))
+        while k > 1 and bs * k > n:
+            k //= 2
+        return bs * k
+
     def _run_eval_graph(self, loader: Any, hook: Any) -> Dict[str, float]:
         """Full batches replay a captured evaluation graph; sums stay on the device."""
         from p2pfl_amd.learning.step_graph import EvalStepGraph
 
-        B, n = int(loader.batch_size), len(loader.dataset)
+        B, n = self._eval_batch(loader), len(loader.dataset)
         name = getattr(hook, "__name__", str(hook))
-        key = EvalStepGraph.make_key(self, loader, hook)
+        key = EvalStepGraph.make_key(self, loader, hook, B)
         eg = self._eval_graphs.get(name)
         perm = loader.permutation()
         if eg is None or eg.key != key:
-            eg = self._eval_graphs[name] = EvalStepGraph(self, loader, hook)
+            eg = self._eval_graphs[name] = EvalStepGraph(self, loader, hook, B)
             eg.capture(perm[:B])  # takes the gate exclusively
+        tail = n % B
+        tg = None
+        if tail > 1:  # the set's remainder: a graph of its own size, accumulating into the same sums
+            tkey = ("tail",) + EvalStepGraph.make_key(self, loader, hook, tail)
+            tg = self._eval_graphs.get(name + "/tail")
+            if tg is None or tg.key != tkey:
+                tg = self._eval_graphs[name + "/tail"] = EvalStepGraph(self, loader, hook, tail, sums_of=eg)
+                tg.key = tkey
+                tg.capture(perm[n - tail:])
         with self._gate():
             eg.sums.zero_()
             for s in range(0, n, B):
                 idx = perm[s : s + B]
                 if idx.numel() == B:
                     eg.run(idx)
+                elif tg is not None:
+                    tg.run(idx)
                 else:
                     eg.step(idx, float(idx.numel()))
             vals = eg.sums.tolist()

@@ -26,6 +26,7 @@ import torch
 _LOCK = threading.Lock()
 _CHOICE: Dict[Hashable, str] = {}
 _TIMES: Dict[Hashable, Dict[str, float]] = {}
+PASSES = max(1, int(os.environ.get("P2PFL_AUTOTUNE_PASSES", "3")))
 
 
 def policy(env: str) -> str:
@@ -76,7 +77,15 @@ def choose(key: Hashable, candidates: Sequence[Tuple[str, Callable[[], object]]]
         got = _CHOICE.get(key)
         if got is not None:
             return got
-        times = {name: _time(fn, iters) for name, fn in candidates}
+        # round-robin passes, best of each candidate: the chip's clock ramps and
+        # settles over milliseconds (DVFS), so one pass in a fixed order times the
+        # first candidates at a different clock than the last ones
+        times: Dict[str, float] = {}
+        for k in range(PASSES):
+            order = list(candidates[k % len(candidates):]) + list(candidates[: k % len(candidates)])
+            for name, fn in order:
+                t = _time(fn, iters)
+                times[name] = min(times.get(name, t), t)
         best = min(times, key=times.get)
         _CHOICE[key] = best
         _TIMES[key] = times

@@ -64,6 +64,9 @@ def test_step_graph_matches_eager(name):
         for (k, x), y in zip(eager.get_parameters().items(), graph.get_parameters().values()):
             torch.testing.assert_close(y, x, atol=1e-2, rtol=1e-2, msg=lambda m, k=k: f"{name} {k}: {m}")
     assert graph._step_graph is not None and graph._step_graph.graph is not None
+    n_train = len(graph.data.train_dataloader().dataset)
+    if n_train % 32 > 1:  # the short last batch replays a graph of its own size
+        assert set(graph._tail_graphs) == {n_train % 32}
     assert graph._step == eager._step
     # evaluation passes replay a captured forward graph: same metrics as the eager loop
     graph.set_parameters(eager.get_parameters())
@@ -136,3 +139,24 @@ def test_resnet_channels_last_weight_shadows():
     torch.cuda.synchronize()
     for n in arena.shadow_names:
         assert torch.equal(named[n].detach(), arena.params[n].to(torch.bfloat16)), n
+
+
+def test_eval_graph_batches_several_loader_batches():
+    """Captured evaluation steps take Settings.EVAL_BATCH_FACTOR loader batches at once
+    (ragged tail eager): same metrics as the eager per-batch loop."""
+    from p2pfl_amd.data import Cifar10FederatedDM
+    from p2pfl_amd.learning.torch_learner import TorchLearner
+    from p2pfl_amd.models.vit import ViT_Tiny
+
+    out = []
+    for graphs in (False, True):
+        torch.manual_seed(0)
+        dm = Cifar10FederatedDM(sub_id=0, number_sub=30, batch_size=32)
+        ln = TorchLearner(ViT_Tiny(seed=0), dm, "p", 1, device=torch.device("cuda", 0), use_step_graphs=graphs)
+        out.append((ln, ln.evaluate()))
+    (eager, ev_e), (graph, ev_g) = out
+    n = len(graph.data.test_dataloader().dataset)
+    assert n % 128 and n > 128, n  # several 128-sample replays plus an eager tail
+    assert {g.B for g in graph._eval_graphs.values()} == {128, n % 128}  # full batches + the remainder's graph
+    for k in ev_e:
+        assert abs(ev_e[k] - ev_g[k]) <= 2e-3 + 2e-3 * abs(ev_e[k]), (k, ev_e, ev_g)
