@@ -29,6 +29,7 @@ from __future__ import annotations
 import os
 import contextlib
 import threading
+import time
 from collections import OrderedDict
 from typing import Any, Dict, Mapping, Optional, Tuple
 
@@ -43,6 +44,11 @@ from p2pfl_amd.management.logger import logger
 from p2pfl_amd.utils.streams import private_stream
 from p2pfl_amd.settings import Settings
 from p2pfl_amd.utils import finite
+
+# A/B switches (read once): graphs for an epoch's short last batch, and
+# evaluation passes whose metrics are read back by a completion thread
+_TAIL_GRAPHS = os.environ.get("P2PFL_TAIL_GRAPHS", "1") != "0"
+_ASYNC_EVAL = os.environ.get("P2PFL_ASYNC_EVAL", "1") != "0"
 
 
 def default_device() -> torch.device:
@@ -104,6 +110,7 @@ class TorchLearner(NodeLearner):
         self._step_graph: Any = None
         self._tail_graphs: Dict[int, Any] = {}  # short last batch of an epoch, by size
         self._eval_graphs: Dict[str, Any] = {}
+        self._completions: Any = None  # metric read-backs of asynchronous evaluation passes
         self.model: Any = None
         self.arena: Optional[ModuleArena] = None
         self.data: Any = None
@@ -367,11 +374,16 @@ class TorchLearner(NodeLearner):
                 model.train()
                 loader = self.data.train_dataloader()
                 if self._graph_ok(opt, loader):
+                    cur = torch.cuda.current_stream(self.device)
+                    t0, t1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                    t0.record(cur)
                     with logger.span(self._addr, "train_epoch"):
                         if not self._fit_epoch_graph(opt, loader):
                             return
+                    t1.record(cur)
                     if not (self.defer_final_validation and _epoch == self.epochs - 1):
                         self._validate()
+                    self._record_epoch_gpu(t0, t1)
                     continue
                 with logger.span(self._addr, "train_epoch"):
                     for i, batch in enumerate(loader):
@@ -395,6 +407,21 @@ class TorchLearner(NodeLearner):
         except Exception as e:
             logger.error(self._addr, f"Fit error: {e}")
             raise
+
+    def _record_epoch_gpu(self, t0: Any, t1: Any) -> None:
+        """Device time of the epoch just enqueued ("train_epoch_gpu") and from the
+        previous epoch's end to its start ("inter_epoch_gpu": evaluation passes,
+        host hand-offs, idle time) -- read without a host sync of its own: the
+        events are resolved when the NEXT epoch records them (bench.py spans)."""
+        prev = getattr(self, "_epoch_events", None)
+        self._epoch_events = (t0, t1)
+        if prev is None or not prev[1].query():
+            return
+        now = time.perf_counter()
+        ms = prev[0].elapsed_time(prev[1])
+        logger.tracer.record(self._addr, "train_epoch_gpu", now - ms * 1e-3, ms * 1e-3)
+        gap = prev[1].elapsed_time(t0)
+        logger.tracer.record(self._addr, "inter_epoch_gpu", now - gap * 1e-3, gap * 1e-3)
 
     def _gate(self):
         """Shared hold of the process's GPU gate around one step / eval pass (see step_graph.DeviceGate)."""
@@ -434,7 +461,7 @@ class TorchLearner(NodeLearner):
                     sg.capture(idx)  # takes the gate exclusively
                 with self._gate():
                     logged = {"train_loss": sg.run(idx)}
-            elif first_ok and idx.numel() > 1:
+            elif first_ok and idx.numel() > 1 and _TAIL_GRAPHS:
                 # the epoch's short last batch: a graph of its own size (captured once; the
                 # same remainder every epoch) instead of ~200 eager launches per round
                 nb = int(idx.numel())
@@ -512,8 +539,11 @@ class TorchLearner(NodeLearner):
             k //= 2
         return bs * k
 
-    def _run_eval_graph(self, loader: Any, hook: Any) -> Dict[str, float]:
-        """Full batches replay a captured evaluation graph; sums stay on the device."""
+    def _run_eval_graph(self, loader: Any, hook: Any, on_done: Any = None) -> Optional[Dict[str, float]]:
+        """Full batches replay a captured evaluation graph; sums stay on the device.
+        With ``on_done`` the pass is only enqueued: the sums are read back into
+        pinned memory behind it and ``on_done(metrics)`` runs on the completion
+        thread when they land (no host sync; returns None)."""
         from p2pfl_amd.learning.step_graph import EvalStepGraph
 
         B, n = self._eval_batch(loader), len(loader.dataset)
@@ -543,19 +573,68 @@ class TorchLearner(NodeLearner):
                     tg.run(idx)
                 else:
                     eg.step(idx, float(idx.numel()))
-            vals = eg.sums.tolist()
+            if on_done is not None:
+                host = torch.empty(eg.sums.shape, dtype=eg.sums.dtype, pin_memory=True)
+                host.copy_(eg.sums, non_blocking=True)
+                ev = torch.cuda.Event()
+                ev.record(torch.cuda.current_stream(self.device))
+            else:
+                vals = eg.sums.tolist()
+        if on_done is not None:
+            keys = list(eg.keys)
+            if self._completions is None:
+                from p2pfl_amd.learning.host_completion import HostCompletions
+
+                self._completions = HostCompletions(self._addr)
+            self._completions.submit(ev, lambda: on_done({k: v / max(1, n) for k, v in zip(keys, host.tolist())}))
+            return None
         return {k: v / max(1, n) for k, v in zip(eg.keys, vals)}
 
     def _validate(self) -> None:
         loader = self.data.val_dataloader()
         if loader is None or len(loader.dataset) == 0:
             return
+        step = self._step
+        if _ASYNC_EVAL and self._eval_graph_ok(loader):  # metrics logged when they land; the next epoch is already queued
+            self.model.eval()
+            self._run_eval_graph(loader, self.model.validation_step,
+                                 lambda res: [self._log(k, v, step=step) for k, v in res.items()])
+            return
         for k, v in self._run_eval(loader, self.model.validation_step).items():
-            self._log(k, v, step=self._step)
+            self._log(k, v, step=step)
+
+    def evaluate_async(self, on_results: Any = None) -> bool:
+        """Graph-replayed test pass enqueued on the node's stream (ahead of the next
+        fit, which the stream orders after it); metrics are logged and handed to
+        ``on_results`` by the completion thread.  False (use :meth:`evaluate`)
+        where the pass would run eagerly."""
+        if self.epochs <= 0 or self.model is None:
+            return False
+        loader = self.data.test_dataloader()
+        if not (_ASYNC_EVAL and self._eval_graph_ok(loader)):
+            return False
+
+        def done(results: Dict[str, float]) -> None:
+            for k, v in results.items():
+                self._log(k, v)
+            if on_results is not None:
+                on_results(results)
+
+        with logger.span(self._addr, "evaluate"), self._on_stream():
+            self.model.eval()
+            self._run_eval_graph(loader, self.model.test_step, done)
+        return True
+
+    def drain(self, timeout: Optional[float] = None) -> bool:
+        return self._completions.drain(timeout) if self._completions is not None else True
 
     def evaluate(self) -> Dict[str, float]:
         if self.epochs <= 0 or self.model is None:
             return {}
+        box: Dict[str, float] = {}
+        if self.evaluate_async(box.update):
+            self.drain()
+            return box
         with logger.span(self._addr, "evaluate"), self._on_stream():
             results = self._run_eval(self.data.test_dataloader(), self.model.test_step)
         for k, v in results.items():

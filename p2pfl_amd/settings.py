@@ -74,7 +74,7 @@ class Settings:
     learner enqueues on the caller's stream).  The hand-off between the
     learner's stream and the default stream is event-ordered (no host sync)."""
 
-    EVAL_BATCH_FACTOR: int = 4
+    EVAL_BATCH_FACTOR: int = 8
     """New: captured evaluation steps (test / validation passes of the graph
     learners) take this many loader batches at once.  Results are the same
     per-sample losses and predictions; the larger launches run at a higher

@@ -155,8 +155,9 @@ def test_eval_graph_batches_several_loader_batches():
         ln = TorchLearner(ViT_Tiny(seed=0), dm, "p", 1, device=torch.device("cuda", 0), use_step_graphs=graphs)
         out.append((ln, ln.evaluate()))
     (eager, ev_e), (graph, ev_g) = out
-    n = len(graph.data.test_dataloader().dataset)
-    assert n % 128 and n > 128, n  # several 128-sample replays plus an eager tail
-    assert {g.B for g in graph._eval_graphs.values()} == {128, n % 128}  # full batches + the remainder's graph
+    ld = graph.data.test_dataloader()
+    n, B = len(ld.dataset), graph._eval_batch(ld)
+    assert B > 32 and n % B and n > B, (n, B)  # several multi-batch replays plus a remainder
+    assert {g.B for g in graph._eval_graphs.values()} == {B, n % B}  # full batches + the remainder's graph
     for k in ev_e:
         assert abs(ev_e[k] - ev_g[k]) <= 2e-3 + 2e-3 * abs(ev_e[k]), (k, ev_e, ev_g)
