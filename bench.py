@@ -339,7 +339,7 @@ def run_gossip(args, env: _Env) -> dict:
         from p2pfl_amd.ops import autotune
 
         if env.rank == 0 and autotune.choices():
-            n_nat = sum(1 for v, _ in autotune.choices().values() if v == "native")
+            n_nat = sum(1 for v, _ in autotune.choices().values() if v.startswith("native"))
             print(f"[bench rank 0] kernel choice per shape (native vs library, ms): {n_nat}/{len(autotune.choices())} native\n"
                   + autotune.summary(), file=sys.stderr, flush=True)
         n_train = len(data.train_dataloader().dataset)
