@@ -47,7 +47,7 @@ constexpr int kOff = -(1 << 28);  // pixel coordinate that fails every bounds ch
 struct ConvFwdA {
   static constexpr bool KMAJ = true;
   const uint16_t* x;
-  FastDiv ohw, ow;
+  FastDiv ohw, ow, cdiv, kwdiv;  // cdiv / kwdiv: the per-K-tile tap decode by multiply-high
   int M, H, W, C, stride, pad, dil, kw;
   struct St {
     int64_t base[4];  // element offset of X[n][ih0][iw0][kk]
@@ -69,8 +69,10 @@ struct ConvFwdA {
     return st;
   }
   P2_DEVICE const void* src(const St& st, int i, int k0, int) const {
-    const int tap = k0 / C, cb = k0 - tap * C;  // wave-uniform
-    const int ky = tap / kw, kx = tap - ky * kw;
+    // wave-uniform tap decode: scalar multiply-high, not two ~40-instruction
+    // scalar divisions per chunk (they were most of the K loop's scalar work)
+    const int tap = fdiv(k0, cdiv), cb = k0 - tap * C;
+    const int ky = fdiv(tap, kwdiv), kx = tap - ky * kw;
     const int ih = st.ih0[i] + ky * dil, iw = st.iw0[i] + kx * dil;
     const bool ok = unsigned(ih) < unsigned(H) && unsigned(iw) < unsigned(W);
     return ok ? static_cast<const void*>(x + st.base[i] + (int64_t(ky * dil) * W + kx * dil) * C + cb)
@@ -82,7 +84,7 @@ struct ConvFwdA {
 struct ConvDgradA {
   static constexpr bool KMAJ = true;
   const uint16_t* dy;
-  FastDiv hw, w;
+  FastDiv hw, w, odiv, kwdiv;
   int M, OH, OW, O, stride, pad, dil, kw;
   struct St {
     int64_t nbase[4];  // element offset of dY[n][0][0][kk]
@@ -104,8 +106,8 @@ struct ConvDgradA {
     return st;
   }
   P2_DEVICE const void* src(const St& st, int i, int k0, int) const {
-    const int tap = k0 / O, ob = k0 - tap * O;  // wave-uniform
-    const int ky = tap / kw, kx = tap - ky * kw;
+    const int tap = fdiv(k0, odiv), ob = k0 - tap * O;  // wave-uniform, multiply-high
+    const int ky = fdiv(tap, kwdiv), kx = tap - ky * kw;
     int oh = st.thp[i] - ky * dil, ow = st.twp[i] - kx * dil;
     bool ok = oh >= 0 && ow >= 0;
     if (stride == 2) {
@@ -123,6 +125,7 @@ struct ConvDgradA {
 struct ConvDgradB {
   static constexpr bool KMAJ = false;
   const uint16_t* w;
+  FastDiv odiv;
   int C, O, T;  // T = kh * kw
   struct St {
     const uint16_t* col;
@@ -133,7 +136,7 @@ struct ConvDgradB {
     return St{c < C ? w + c : nullptr, tid >> 4};
   }
   P2_DEVICE const void* src(const St& st, int i, int k0, int) const {
-    const int tap = k0 / O, ob = k0 - tap * O;  // wave-uniform
+    const int tap = fdiv(k0, odiv), ob = k0 - tap * O;  // wave-uniform
     const int o = ob + 16 * i + st.kr;
     return st.col ? static_cast<const void*>(st.col + (int64_t(o) * T + tap) * C) : zero_chunk();
   }
@@ -165,22 +168,35 @@ struct ConvWgradB {
   }
 };
 
-template <int NBUF, class LA, class LB, int BN>
+// EPI (gemm_core.h epilogue_kind): 0 = plain bf16 / fp32 store -- the common
+// convolution launch, whose compact epilogue avoids fetching the ~60 KB of
+// unrolled split-K / bias / GELU / residual / BatchNorm code every workgroup
+// otherwise pulls cold from L2 once (the GEMM measurement: a launch with no K
+// loop 12.9 -> 8.6 us, profiles/r5_vit_gemm_sweep.md); 1 = every feature.
+template <int NBUF, class LA, class LB, int BN, int EPI>
 __global__ __launch_bounds__(NT, NBUF == 1 ? 3 : (NBUF == 2 ? 2 : 1)) void conv_kernel(GemmParams p, LA la, LB lb, int tiles_m, int tiles_n) {
   __shared__ __attribute__((aligned(16))) char smem[smem_bytes<Tile128, NBUF>()];
-  gemm_body<Tile128, NBUF, LA, LB, BN>(p, la, lb, tiles_m, tiles_n, smem);
+  gemm_body<Tile128, NBUF, LA, LB, BN, EPI>(p, la, lb, tiles_m, tiles_n, smem);
+}
+
+template <class LA, class LB, int BN, int EPI>
+static void launch_e(const GemmParams& p, const LA& la, const LB& lb, int grid, int tm, int tn, hipStream_t s) {
+  if (p.variant & 4096)  // 4-stage ring, one workgroup per CU: short-K / small-grid shapes
+    hipLaunchKernelGGL((conv_kernel<4, LA, LB, BN, EPI>), dim3(grid), dim3(NT), 0, s, p, la, lb, tm, tn);
+  else if (p.variant & 8)
+    hipLaunchKernelGGL((conv_kernel<1, LA, LB, BN, EPI>), dim3(grid), dim3(NT), 0, s, p, la, lb, tm, tn);
+  else
+    hipLaunchKernelGGL((conv_kernel<2, LA, LB, BN, EPI>), dim3(grid), dim3(NT), 0, s, p, la, lb, tm, tn);
 }
 
 template <class LA, class LB, int BN>
 static void launch_t(const GemmParams& p, const LA& la, const LB& lb, hipStream_t s) {
   int tm, tn;
   const int grid = gemm_grid<Tile128>(p, tm, tn);
-  if (p.variant & 4096)  // 4-stage ring, one workgroup per CU: short-K / small-grid shapes
-    hipLaunchKernelGGL((conv_kernel<4, LA, LB, BN>), dim3(grid), dim3(NT), 0, s, p, la, lb, tm, tn);
-  else if (p.variant & 8)
-    hipLaunchKernelGGL((conv_kernel<1, LA, LB, BN>), dim3(grid), dim3(NT), 0, s, p, la, lb, tm, tn);
+  if (BN == 0 && epilogue_kind(p) == 0)
+    launch_e<LA, LB, BN, 0>(p, la, lb, grid, tm, tn, s);
   else
-    hipLaunchKernelGGL((conv_kernel<2, LA, LB, BN>), dim3(grid), dim3(NT), 0, s, p, la, lb, tm, tn);
+    launch_e<LA, LB, BN, 1>(p, la, lb, grid, tm, tn, s);
 }
 
 // the BatchNorm-statistics instantiation only where a launch asks for it; BNK: the
@@ -252,7 +268,8 @@ void conv_fwd(const ConvShape& s, const uint16_t* x, const uint16_t* w, void* y,
   const int M = s.N * s.OH * s.OW, K = s.kh * s.kw * s.C;
   GemmParams p = base_params(M, s.O, K, y, s.O, k.splits <= 1 || k.counters, k, variant);
   if (bn) p.bn = *bn;
-  const ConvFwdA la{x, make_fastdiv(s.OH * s.OW), make_fastdiv(s.OW), M, s.H, s.W, s.C, s.stride, s.pad, s.dil, s.kw};
+  const ConvFwdA la{x,   make_fastdiv(s.OH * s.OW), make_fastdiv(s.OW), make_fastdiv(s.C), make_fastdiv(s.kw), M, s.H, s.W,
+                    s.C, s.stride, s.pad, s.dil, s.kw};
   launch<1>(p, la, PlainK{w, K, s.O, K}, st);
 }
 
@@ -262,8 +279,9 @@ void conv_dgrad(const ConvShape& s, const uint16_t* dy, const uint16_t* w, void*
   const int M = s.N * s.H * s.W, K = s.kh * s.kw * s.O;
   GemmParams p = base_params(M, s.C, K, dx, s.C, k.splits <= 1 || k.counters, k, variant);
   if (bn) p.bn = *bn;
-  const ConvDgradA la{dy, make_fastdiv(s.H * s.W), make_fastdiv(s.W), M, s.OH, s.OW, s.O, s.stride, s.pad, s.dil, s.kw};
-  launch<2>(p, la, ConvDgradB{w, s.C, s.O, s.kh * s.kw}, st);
+  const ConvDgradA la{dy,  make_fastdiv(s.H * s.W), make_fastdiv(s.W), make_fastdiv(s.O), make_fastdiv(s.kw), M, s.OH, s.OW,
+                      s.O, s.stride, s.pad, s.dil, s.kw};
+  launch<2>(p, la, ConvDgradB{w, make_fastdiv(s.O), s.C, s.O, s.kh * s.kw}, st);
 }
 
 void conv_wgrad(const ConvShape& s, const uint16_t* dy, const uint16_t* x, void* out, int out_bf16, const SplitK& k,
