@@ -31,6 +31,15 @@ void conv_fwd(const ConvShape& s, const uint16_t* x, const uint16_t* w, void* y,
               hipStream_t st, const BnEpi* bn = nullptr);
 // bn (optional, backward mode: BnEpi::bx set): BatchNorm backward statistics of the
 // BN whose output this dgrad differentiates, computed in the launch.
+// stride-2 input gradient by output phase (conv.hip ConvDgradS2A): dx_phases is
+// [4 N (H/2) (W/2)][C] phase-major (or its split-K slabs); phase_interleave
+// writes it into dX [N, H, W, C].  conv_dgrad_s2_ok: the shapes it takes.
+bool conv_dgrad_s2_ok(const ConvShape& s);
+// phases conv_dgrad_s2 computes (rows = s2_phases * N (H/2) (W/2)): 4, or 1 for a 1x1 kernel
+int s2_phases(const ConvShape& s);
+void conv_dgrad_s2(const ConvShape& s, const uint16_t* dy, const uint16_t* w, void* dx_phases, const SplitK& k,
+                   int variant, hipStream_t st);
+void phase_interleave(const ConvShape& s, const uint16_t* src, uint16_t* dx, hipStream_t st);
 void conv_dgrad(const ConvShape& s, const uint16_t* dy, const uint16_t* w, void* dx, const SplitK& k, int variant,
                 hipStream_t st, const BnEpi* bn = nullptr);
 // dw[O][kh*kw*C] = sum over output pixels of dy (x) im2col(x)    (O % 8 == 0, C % 8 == 0)

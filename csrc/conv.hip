@@ -142,6 +142,118 @@ struct ConvDgradB {
   }
 };
 
+// ---- dgrad, stride 2: one output phase per tile ------------------------------
+// A stride-2 input gradient receives, at pixel (ih, iw), only the taps with
+// ky = (ih + pad) mod 2 (mod 2) and kx likewise: for a 3x3 kernel 4, 2, 2 or 1
+// of the 9 taps, 2.25 on average.  The plain gather above runs all 9 for every
+// pixel (the holes read the zero page), 4x the MFMA work and K-tiles needed.
+// Here the rows of the product are the dX pixels grouped by phase q = (a, b),
+// a = (ih + pad) & 1, b = (iw + pad) & 1 -- row m of phase q (Mq rows each,
+// a multiple of 128, so a tile never straddles two phases) is pixel
+// (n, 2 ih2 + ((a - pad) & 1), 2 iw2 + ((b - pad) & 1)) -- and k = (tap of the
+// phase, o) runs over ceil(kh/2) x ceil(kw/2) taps (fewer for odd phases: the
+// surplus reads the zero page; the slowest phase sets the launch's time
+// anyway).  The result is phase-major; phase_interleave_kernel puts it into
+// dX.  H and W are even (the host falls back to ConvDgradA otherwise).
+P2_DEVICE void s2_tap(int t, int a, int b, int kh, int kw, int& ky, int& kx, bool& valid) {
+  const int nkx = (kw - b + 1) >> 1, nky = (kh - a + 1) >> 1;  // taps of this phase per axis
+  if (nkx == 0) {  // kw == 1, odd column phase: no taps (never launched, see conv_dgrad_s2)
+    ky = kx = 0;
+    valid = false;
+    return;
+  }
+  const int ty = nkx == 1 ? t : (nkx == 2 ? (t >> 1) : t / nkx);
+  const int tx = t - ty * nkx;
+  ky = a + 2 * ty;
+  kx = b + 2 * tx;
+  valid = ty < nky;
+}
+
+struct ConvDgradS2A {
+  static constexpr bool KMAJ = true;
+  const uint16_t* dy;
+  FastDiv hw2, w2, odiv;
+  int Mq, W2, OH, OW, O, pad, kh, kw;
+  struct St {
+    int64_t nbase[4];    // element offset of dY[n][0][0][kk]
+    int thp[4], twp[4];  // ih + pad, iw + pad
+    int kk, a, b;
+  };
+  P2_DEVICE St prep(int r0, int tid) const {
+    St st;
+    st.kk = kmaj_k(tid);
+    const int q = min(r0 / Mq, 3);  // tile-uniform (Mq % 128 == 0)
+    st.a = q >> 1;
+    st.b = q & 1;
+    const int ihoff = (st.a - pad) & 1, iwoff = (st.b - pad) & 1;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int m = r0 + kmaj_row(i, tid), loc = m - q * Mq;
+      const int n = fdiv(loc, hw2), r = loc - n * int(hw2.d);
+      const int ih2 = fdiv(r, w2), iw2 = r - ih2 * W2;
+      st.thp[i] = m < 4 * Mq ? 2 * ih2 + ihoff + pad : kOff;
+      st.twp[i] = 2 * iw2 + iwoff + pad;
+      st.nbase[i] = int64_t(n) * OH * OW * O + st.kk;
+    }
+    return st;
+  }
+  P2_DEVICE const void* src(const St& st, int i, int k0, int) const {
+    const int t = fdiv(k0, odiv), ob = k0 - t * O;  // wave-uniform
+    int ky, kx;
+    bool ok;
+    s2_tap(t, st.a, st.b, kh, kw, ky, kx, ok);
+    const int dh = st.thp[i] - ky, dw = st.twp[i] - kx;  // even by construction
+    ok = ok && dh >= 0 && dw >= 0 && (dh >> 1) < OH && (dw >> 1) < OW;
+    return ok ? static_cast<const void*>(dy + st.nbase[i] + (int64_t(dh >> 1) * OW + (dw >> 1)) * O + ob)
+              : zero_chunk();
+  }
+};
+
+// B = W[o][ky][kx][c] at the taps of the tile's phase (bound by tile_bound)
+struct ConvDgradS2B {
+  static constexpr bool KMAJ = false;
+  const uint16_t* w;
+  FastDiv odiv;
+  int C, O, Mq, kh, kw, a, b;
+  struct St {
+    const uint16_t* col;
+    int kr;
+  };
+  P2_DEVICE St prep(int r0, int tid) const {
+    const int c = r0 + mnmaj_col(tid);
+    return St{c < C ? w + c : nullptr, tid >> 4};
+  }
+  P2_DEVICE const void* src(const St& st, int i, int k0, int) const {
+    const int t = fdiv(k0, odiv), ob = k0 - t * O;  // wave-uniform
+    int ky, kx;
+    bool ok;
+    s2_tap(t, a, b, kh, kw, ky, kx, ok);
+    const int o = ob + 16 * i + st.kr;
+    return (ok && st.col) ? static_cast<const void*>(st.col + (int64_t(o) * kh * kw + ky * kw + kx) * C) : zero_chunk();
+  }
+};
+P2_DEVICE ConvDgradS2B tile_bound(const ConvDgradS2B& l, int m0) {
+  ConvDgradS2B t = l;
+  const int q = min(m0 / l.Mq, 3);
+  t.a = q >> 1;
+  t.b = q & 1;
+  return t;
+}
+
+// dX[n][ih][iw][:] <- phase-major row of (ih, iw): one thread per 16-byte chunk.
+// Phases q >= nq were not computed (no taps: a 1x1 kernel) and are zero.
+__global__ __launch_bounds__(256) void phase_interleave_kernel(const uint4* __restrict__ src, uint4* __restrict__ dst,
+                                                               int64_t nchunks, int cpr, FastDiv cprd, FastDiv hw2,
+                                                               FastDiv w2, int Mq, int nq, int H, int W, int pad) {
+  const int64_t i = int64_t(blockIdx.x) * 256 + threadIdx.x;
+  if (i >= nchunks) return;
+  const int m = fdiv(int(i), cprd), c = int(i) - m * cpr;  // phase-major row, chunk within the row
+  const int q = m / Mq, loc = m - q * Mq;
+  const int n = fdiv(loc, hw2), r = loc - n * int(hw2.d), ih2 = fdiv(r, w2), iw2 = r - ih2 * int(w2.d);
+  const int ih = 2 * ih2 + (((q >> 1) - pad) & 1), iw = 2 * iw2 + (((q & 1) - pad) & 1);
+  dst[((int64_t(n) * H + ih) * W + iw) * cpr + c] = q < nq ? src[i] : make_uint4(0, 0, 0, 0);
+}
+
 // ---- wgrad: B = im2col(X) read c-contiguous, mn-major, cols = (ky, kx, c), k = pixel
 struct ConvWgradB {
   static constexpr bool KMAJ = false;
@@ -282,6 +394,36 @@ void conv_dgrad(const ConvShape& s, const uint16_t* dy, const uint16_t* w, void*
   const ConvDgradA la{dy,  make_fastdiv(s.H * s.W), make_fastdiv(s.W), make_fastdiv(s.O), make_fastdiv(s.kw), M, s.OH, s.OW,
                       s.O, s.stride, s.pad, s.dil, s.kw};
   launch<2>(p, la, ConvDgradB{w, make_fastdiv(s.O), s.C, s.O, s.kh * s.kw}, st);
+}
+
+// phases with taps: all four, or only (0, 0) for a 1x1 kernel (pad 0; with pad p
+// the tap-less phases are the ones with (ih + p) odd -- still phases 1..3)
+int s2_phases(const ConvShape& s) { return (s.kh == 1 && s.kw == 1) ? 1 : 4; }
+
+bool conv_dgrad_s2_ok(const ConvShape& s) {
+  const int64_t Mq = int64_t(s.N) * (s.H / 2) * (s.W / 2);
+  return s.stride == 2 && s.dil == 1 && s.H % 2 == 0 && s.W % 2 == 0 && Mq % 128 == 0 && 4 * Mq < (int64_t(1) << 31);
+}
+
+void conv_dgrad_s2(const ConvShape& s, const uint16_t* dy, const uint16_t* w, void* dx_phases, const SplitK& k, int variant,
+                   hipStream_t st) {
+  using namespace p2gemm;
+  const int H2 = s.H / 2, W2 = s.W / 2, Mq = s.N * H2 * W2;
+  const int K = ((s.kh + 1) / 2) * ((s.kw + 1) / 2) * s.O;
+  GemmParams p = base_params(s2_phases(s) * Mq, s.C, K, dx_phases, s.C, k.splits <= 1 || k.counters, k, variant);
+  const ConvDgradS2A la{dy, make_fastdiv(H2 * W2), make_fastdiv(W2), make_fastdiv(s.O), Mq, W2, s.OH, s.OW, s.O,
+                        s.pad, s.kh, s.kw};
+  const ConvDgradS2B lb{w, make_fastdiv(s.O), s.C, s.O, Mq, s.kh, s.kw, 0, 0};
+  launch<0>(p, la, lb, st);
+}
+
+void phase_interleave(const ConvShape& s, const uint16_t* src, uint16_t* dx, hipStream_t st) {
+  using namespace p2gemm;
+  const int H2 = s.H / 2, W2 = s.W / 2, Mq = s.N * H2 * W2, cpr = s.C / 8;
+  const int64_t nchunks = int64_t(4) * Mq * cpr;
+  hipLaunchKernelGGL(phase_interleave_kernel, dim3(int((nchunks + 255) / 256)), dim3(256), 0, st,
+                     reinterpret_cast<const uint4*>(src), reinterpret_cast<uint4*>(dx), nchunks, cpr, make_fastdiv(cpr),
+                     make_fastdiv(H2 * W2), make_fastdiv(W2), Mq, s2_phases(s), s.H, s.W, s.pad);
 }
 
 void conv_wgrad(const ConvShape& s, const uint16_t* dy, const uint16_t* x, void* out, int out_bf16, const SplitK& k,

@@ -236,6 +236,51 @@ void conv_dgrad(torch::Tensor dy, torch::Tensor w, int64_t stride, int64_t pad, 
                  dx.data_ptr(), k, int(variant), stream_of(dy));
 }
 
+// stride-2 input gradient by output phase: dy [N, OH, OW, O], w [O, kh, kw, C] -> out:
+// phase-major [4 N (H/2) (W/2), C] bf16 (or split-K slabs / a counter-reduced bf16 out),
+// for phase_interleave to scatter into dX; dx_shape (N, H, W, C) must pass conv_dgrad_s2_ok
+void conv_dgrad_s2(torch::Tensor dy, torch::Tensor w, int64_t pad, torch::Tensor out, std::vector<int64_t> dx_shape,
+                   int64_t splits, int64_t variant, OptT ws, OptT counters) {
+  check_nhwc(dy, "dy");
+  check_nhwc(w, "w");
+  TORCH_CHECK(dx_shape.size() == 4, "conv_dgrad_s2: dx_shape is (N, H, W, C)");
+  const auto s = make_shape(dx_shape[0], dx_shape[1], dx_shape[2], dx_shape[3], w.size(0), w.size(1), w.size(2), 2, pad, 1);
+  TORCH_CHECK(p2::conv_dgrad_s2_ok(s), "conv_dgrad_s2: needs even H, W and N H W / 4 % 128 == 0");
+  TORCH_CHECK(w.size(3) == s.C && s.O % 64 == 0 && s.C % 8 == 0, "conv_dgrad_s2: needs O % 64 == 0 and C % 8 == 0");
+  TORCH_CHECK(dy.size(0) == s.N && dy.size(1) == s.OH && dy.size(2) == s.OW && dy.size(3) == s.O, "conv_dgrad_s2: dy shape");
+  const int64_t rows = int64_t(p2::s2_phases(s)) * s.N * (s.H / 2) * (s.W / 2);  // phases with taps x N (H/2) (W/2)
+  const auto k = make_splitk(splits, ws, counters, rows, s.C, dy, "conv_dgrad_s2");
+  if (k.splits == 1 || k.counters) {
+    TORCH_CHECK(out.is_cuda() && out.scalar_type() == torch::kBFloat16 && out.is_contiguous() && out.numel() == rows * s.C &&
+                    reinterpret_cast<uintptr_t>(out.data_ptr()) % 16 == 0,
+                "conv_dgrad_s2: out must be contiguous bf16 with s2_phases N (H/2) (W/2) C elements");
+  } else {
+    TORCH_CHECK(out.is_cuda() && out.scalar_type() == torch::kFloat32 && out.is_contiguous() &&
+                    out.numel() >= int64_t(k.splits) * slab_elems(rows, s.C) && reinterpret_cast<uintptr_t>(out.data_ptr()) % 16 == 0,
+                "conv_dgrad_s2: split-K out must be contiguous fp32 with splits * slab_elems(rows, C) elements");
+  }
+  TORCH_CHECK(dy.device() == w.device() && out.device() == dy.device(), "conv_dgrad_s2: device mismatch");
+  const c10::DeviceGuard g(dy.device());
+  p2::conv_dgrad_s2(s, reinterpret_cast<const uint16_t*>(dy.data_ptr()), reinterpret_cast<const uint16_t*>(w.data_ptr()),
+                    out.data_ptr(), k, int(variant), stream_of(dy));
+}
+
+// phase-major [s2_phases N (H/2) (W/2), C] bf16 -> dX [N, H, W, C] (conv_dgrad_s2's output
+// order for a kh x kw kernel; the phases without taps are written as zeros)
+void phase_interleave(torch::Tensor src, torch::Tensor dx, int64_t pad, int64_t kh, int64_t kw) {
+  check_nhwc(dx, "dx");
+  TORCH_CHECK(kh >= 1 && kw >= 1 && dx.size(1) + 2 * pad >= kh && dx.size(2) + 2 * pad >= kw, "phase_interleave: kernel size");
+  const auto s = make_shape(dx.size(0), dx.size(1), dx.size(2), dx.size(3), 64, kh, kw, 2, pad, 1);
+  TORCH_CHECK(p2::conv_dgrad_s2_ok(s) && s.C % 8 == 0, "phase_interleave: needs even H, W, N H W / 4 % 128 == 0, C % 8 == 0");
+  const int64_t rows = int64_t(p2::s2_phases(s)) * s.N * (s.H / 2) * (s.W / 2);
+  TORCH_CHECK(src.is_cuda() && src.device() == dx.device() && src.scalar_type() == torch::kBFloat16 && src.is_contiguous() &&
+                  src.numel() == rows * s.C && reinterpret_cast<uintptr_t>(src.data_ptr()) % 16 == 0,
+              "phase_interleave: src must be contiguous bf16 with s2_phases N (H/2) (W/2) C elements");
+  const c10::DeviceGuard g(dx.device());
+  p2::phase_interleave(s, reinterpret_cast<const uint16_t*>(src.data_ptr()), reinterpret_cast<uint16_t*>(dx.data_ptr()),
+                       stream_of(dx));
+}
+
 // dy [N, OH, OW, O], x [N, H, W, C]  ->  out: [O, kh, kw, C] bf16/fp32, or raw fp32 slabs
 // [splits, O*kh*kw*C] for a split-K launch without counters
 void conv_wgrad(torch::Tensor dy, torch::Tensor x, int64_t kh, int64_t kw, int64_t stride, int64_t pad, int64_t dil,
@@ -374,6 +419,11 @@ void register_conv(pybind11::module& m) {
   m.def("conv_dgrad", &conv_dgrad, "implicit-GEMM conv input gradient", arg("dy"), arg("w"), arg("stride"), arg("pad"),
         arg("dil"), arg("dx"), arg("dx_shape"), arg("splits") = 1, arg("variant") = 10, arg("ws") = pybind11::none(),
         arg("counters") = pybind11::none());
+  m.def("conv_dgrad_s2", &conv_dgrad_s2, "stride-2 conv input gradient by output phase (phase-major out)", arg("dy"),
+        arg("w"), arg("pad"), arg("out"), arg("dx_shape"), arg("splits") = 1, arg("variant") = 10,
+        arg("ws") = pybind11::none(), arg("counters") = pybind11::none());
+  m.def("phase_interleave", &phase_interleave, "phase-major stride-2 input gradient -> NHWC dX", arg("src"), arg("dx"),
+        arg("pad"), arg("kh") = 3, arg("kw") = 3);
   m.def("conv_wgrad", &conv_wgrad, "implicit-GEMM conv weight gradient", arg("dy"), arg("x"), arg("kh"), arg("kw"),
         arg("stride"), arg("pad"), arg("dil"), arg("out"), arg("splits") = 1, arg("variant") = 2,
         arg("ws") = pybind11::none(), arg("counters") = pybind11::none());

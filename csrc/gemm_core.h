@@ -411,8 +411,17 @@ P2_DEVICE void bn_epilogue_reduce(const GemmParams& p, Moments mo, int tm, int t
 // EPI (epilogue_kind): 0 compact epilogue for plain stores, 2 bias only (see
 // gemm_pp.hip's note on instruction fetch); 1 every epilogue feature behind
 // runtime flags.
+// A loader sees the output tile it serves through tile_bound (default: itself);
+// a loader whose gather depends on the tile's rows -- the stride-2 input
+// gradient's B operand takes the taps of its tile's output phase (conv.hip) --
+// overloads it to return a copy bound to the tile's first row.
+template <class L>
+P2_DEVICE const L& tile_bound(const L& l, int) {
+  return l;
+}
+
 template <class CFG, int NBUF, class LA, class LB, int BN = 0, int EPI = 1>
-P2_DEVICE void gemm_body(const GemmParams& p, const LA& la, const LB& lb, int tiles_m, int tiles_n, char* smem) {
+P2_DEVICE void gemm_body(const GemmParams& p, const LA& la0, const LB& lb0, int tiles_m, int tiles_n, char* smem) {
   constexpr int FM = CFG::FM, FN = CFG::FN, HA = CFG::HA, HB = CFG::HB, G = CFG::GROUPS;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave / CFG::WAVES_N, wn = wave % CFG::WAVES_N;
@@ -431,6 +440,8 @@ P2_DEVICE void gemm_body(const GemmParams& p, const LA& la, const LB& lb, int ti
   int tm, tn;
   tile_coords(p.variant, t, tiles_m, tiles_n, tm, tn);
   const int m0 = tm * CFG::BM, n0 = tn * CFG::BN;
+  const LA la = tile_bound(la0, m0);
+  const LB lb = tile_bound(lb0, m0);
   int kper = (p.K + p.splits - 1) / p.splits;
   kper = (kper + BK - 1) / BK * BK;
   const int kb = split * kper, ke = min(p.K, kb + kper);

@@ -111,6 +111,138 @@ def _run_split(launch, rows: int, cols: int, s: int, out: torch.Tensor, variant:
     _C().tile_slab_reduce(ws, s, rows, cols, out.view(rows, cols), variant)
 
 
+# Per-shape launch configuration.  One fixed (variant, split-K) per direction left
+# whole stages on the floor: the CIFAR ResNet's 16x16 / 8x8 stages give 128-256
+# output tiles, one workgroup per CU, and the single-LDS-buffer kernel (variant
+# bit 3, chosen for occupancy on big grids) then waits a full load latency per
+# K-tile (l2 3x3 stride-2 input gradient: 21 us for 8 K-tiles, scripts/conv_one.py
+# under rocprofv3).  The first eager call of each (direction, shape) times the
+# single-buffer, double-buffer and 4-stage-ring kernels at the default split-K
+# and 2x / 4x it (and, for a stride-2 input gradient, the by-phase and the
+# all-taps products) and keeps the fastest -- captured step graphs replay it.
+# P2PFL_CONV_TUNE=0: the fixed defaults.
+_TUNE = os.environ.get("P2PFL_CONV_TUNE", "1") != "0"
+_TUNE_VARIANTS = (10, 2, 4096 | 2)
+
+
+def _split_options(base: int, K: int, min_k: int = 128) -> Tuple[int, ...]:
+    """The default split-K and up to two doublings that keep >= min_k of K per slice."""
+    out = [base]
+    while len(out) < 3 and K // (out[-1] * 2) >= min_k and out[-1] < 64:
+        out.append(out[-1] * 2)
+    return tuple(out)
+
+
+def _pick(key, cands, default: str, out: torch.Tensor) -> None:
+    """Run ``cands[name](out)`` for the measured-fastest name of ``key`` (``default``
+    untuned, or unseen inside a capture); candidates are timed into a scratch output."""
+    if not _TUNE or len(cands) == 1:
+        cands[default](out)
+        return
+    scratch = []
+
+    def timed(f):
+        def run():
+            if not scratch:
+                scratch.append(torch.empty_like(out))
+            f(scratch[0])
+        return run
+
+    name = autotune.choose(key, [(n, timed(f)) for n, f in cands.items()], default=default)
+    cands[name](out)
+
+
+# stride-2 input gradients by output phase (env P2PFL_CONV_S2_PHASES=0: the all-taps gather)
+_S2_PHASES = os.environ.get("P2PFL_CONV_S2_PHASES", "1") != "0"
+
+
+def s2_phases_ok(stride: int, dil: int, dx_shape, k: Tuple[int, int] = (3, 3)) -> bool:
+    """Shapes csrc/conv.hip conv_dgrad_s2 takes: stride 2, no dilation, even H and W,
+    and whole 128-row tiles per phase (N H W / 4 % 128 == 0).  Not offered for 1x1
+    kernels: one phase of the output, but the extra interleave launch made it slower
+    than the gather (l3 shortcut 8.6 -> 14.4 us; the models run 1x1 convolutions as
+    GEMMs anyway, conv1x1_gemm)."""
+    N, H, W = dx_shape[0], dx_shape[1], dx_shape[2]
+    return (_S2_PHASES and stride == 2 and dil == 1 and k[0] * k[1] > 1 and H % 2 == 0 and W % 2 == 0
+            and (N * H * W // 4) % 128 == 0)
+
+
+def dgrad_into(dy4: torch.Tensor, w4: torch.Tensor, stride: int, pad: int, dil: int, dx4: torch.Tensor) -> None:
+    """dX [N, H, W, C] bf16 <- conv input gradient of dY [N, OH, OW, O] and W [O, kh, kw, C]
+    (NHWC views).  Stride 2: by output phase (csrc/conv.hip ConvDgradS2A: ~4x fewer
+    K-tiles for 3x3 than gathering all taps) then phase_interleave, or the all-taps
+    gather (ConvDgradA), whichever configuration measured faster (:func:`_pick`)."""
+    C = _C()
+    shape = list(dx4.shape)
+    O, kh, kw = w4.shape[0], w4.shape[1], w4.shape[2]
+    rows = shape[0] * shape[1] * shape[2]
+    K = kh * kw * O
+
+    def gather(v, sp):
+        return lambda dst: _run_split(
+            lambda o, s, ws, cnt: C.conv_dgrad(dy4, w4, stride, pad, dil, o, shape, s, v, ws, cnt),
+            rows, shape[3], sp, dst, v)
+
+    def phases(v, sp):
+        def run(dst):
+            ph = torch.empty((rows, shape[3]), dtype=torch.bfloat16, device=dx4.device)
+            _run_split(lambda o, s, ws, cnt: C.conv_dgrad_s2(dy4, w4, pad, o, shape, s, v, ws, cnt),
+                       rows, shape[3], sp, ph, v)
+            C.phase_interleave(ph, dst, pad, kh, kw)
+        return run
+
+    variants = _TUNE_VARIANTS if _TUNE else (_V_DGRAD,)
+    base = mn_splits(rows, shape[3], K)
+    cands = {f"gather_v{v}_s{sp}": gather(v, sp) for v in variants for sp in _split_options(base, K)}
+    default = f"gather_v{_V_DGRAD}_s{base}"
+    if s2_phases_ok(stride, dil, shape, (kh, kw)):
+        kq = ((kh + 1) // 2) * ((kw + 1) // 2) * O  # K of one phase
+        pbase = mn_splits(rows, shape[3], kq)
+        cands.update({f"phase_v{v}_s{sp}": phases(v, sp) for v in variants for sp in _split_options(pbase, kq)})
+        default = f"phase_v{_V_DGRAD}_s{pbase}"
+        cands.setdefault(default, phases(_V_DGRAD, pbase))
+    cands.setdefault(default, gather(_V_DGRAD, base))
+    _pick(("conv_dgrad", tuple(shape), O, kh, kw, stride, pad, dil), cands, default, dx4)
+
+
+def fwd_into(x4: torch.Tensor, w4: torch.Tensor, stride: int, pad: int, dil: int, y4: torch.Tensor) -> None:
+    """Y [N, OH, OW, O] bf16 <- conv of X [N, H, W, C] and W [O, kh, kw, C] (NHWC views),
+    in the measured-fastest (variant, split-K) of the shape (:func:`_pick`)."""
+    C = _C()
+    N, OH, OW, O = y4.shape
+    kh, kw, Cin = w4.shape[1], w4.shape[2], w4.shape[3]
+    rows, K = N * OH * OW, kh * kw * Cin
+
+    def one(v, sp):
+        return lambda dst: _run_split(lambda o, s, ws, cnt: C.conv_fwd(x4, w4, stride, pad, dil, o, s, v, ws, cnt),
+                                      rows, O, sp, dst, v)
+
+    base = mn_splits(rows, O, K)
+    cands = {f"v{v}_s{sp}": one(v, sp) for v in (_TUNE_VARIANTS if _TUNE else (_V_FWD,)) for sp in _split_options(base, K)}
+    _pick(("conv_fwd", tuple(x4.shape), O, kh, kw, stride, pad, dil), cands, f"v{_V_FWD}_s{base}", y4)
+
+
+def wgrad_into(dy4: torch.Tensor, x4: torch.Tensor, stride: int, pad: int, dil: int, dw4: torch.Tensor) -> None:
+    """dW [O, kh, kw, C] <- conv weight gradient (NHWC views), in the measured-fastest
+    (variant, split-K) of the shape (:func:`_pick`; splits: the default, half and double)."""
+    C = _C()
+    O, kh, kw, Cin = dw4.shape
+    npix = dy4.shape[0] * dy4.shape[1] * dy4.shape[2]
+    ncols = kh * kw * Cin
+
+    def one(v, sp):
+        return lambda dst: _run_split(
+            lambda o, s, ws, cnt: C.conv_wgrad(dy4, x4, kh, kw, stride, pad, dil, o, s, v, ws, cnt), O, ncols, sp, dst, v)
+
+    base = wgrad_splits(O, ncols, npix)
+    splits = sorted({max(1, base // 2), base} | ({base * 2} if npix // (base * 2) >= 256 else set()))
+    cands = {f"v{v}_s{sp}": one(v, sp) for v in (_TUNE_VARIANTS if _TUNE else (_V_WGRAD,)) for sp in splits}
+    default = f"v{_V_WGRAD}_s{base}"
+    if default not in cands:
+        cands[default] = one(_V_WGRAD, base)
+    _pick(("conv_wgrad", tuple(x4.shape), O, kh, kw, stride, pad, dil), cands, default, dw4)
+
+
 def native_ok(x: torch.Tensor, conv: nn.Conv2d) -> bool:
     from p2pfl_amd.ops import _gpu
 
@@ -145,11 +277,7 @@ class _Conv2dNHWC(torch.autograd.Function):
         O, kh, kw = w4.shape[0], w4.shape[1], w4.shape[2]
         OH, OW = out_hw(H, W_, (kh, kw), stride, pad, dil)
         y4 = torch.empty((N, OH, OW, O), dtype=torch.bfloat16, device=x.device)
-        rows = N * OH * OW
-        _run_split(
-            lambda o, s, ws, cnt: _C().conv_fwd(x4, w4, stride, pad, dil, o, s, _V_FWD, ws, cnt),
-            rows, O, mn_splits(rows, O, kh * kw * C), y4, _V_FWD,
-        )
+        fwd_into(x4, w4, stride, pad, dil, y4)
         ctx.save_for_backward(x4, w)
         ctx.cfg = (stride, pad, dil)
         return y4.permute(0, 3, 1, 2)
@@ -164,26 +292,14 @@ class _Conv2dNHWC(torch.autograd.Function):
         if not dy4.is_contiguous() or dy4.data_ptr() % 16:
             dy4 = dy4.contiguous()
         w4 = w.permute(0, 2, 3, 1)
-        C = _C()
         dx = dw = None
         if ctx.needs_input_grad[0]:
             dx4 = torch.empty(x4.shape, dtype=torch.bfloat16, device=x4.device)
-            shape = list(x4.shape)
-            O, kh, kw = w4.shape[0], w4.shape[1], w4.shape[2]
-            rows = shape[0] * shape[1] * shape[2]
-            _run_split(
-                lambda o, s, ws, cnt: C.conv_dgrad(dy4, w4, stride, pad, dil, o, shape, s, _V_DGRAD, ws, cnt),
-                rows, shape[3], mn_splits(rows, shape[3], kh * kw * O), dx4, _V_DGRAD,
-            )
+            dgrad_into(dy4, w4, stride, pad, dil, dx4)
             dx = dx4.permute(0, 3, 1, 2)
         if ctx.needs_input_grad[1]:
-            O, kh, kw, Cin = w4.shape
-            npix = dy4.shape[0] * dy4.shape[1] * dy4.shape[2]
-            dw4 = torch.empty((O, kh, kw, Cin), dtype=w.dtype, device=w.device)
-            _run_split(
-                lambda o, s, ws, cnt: C.conv_wgrad(dy4, x4, kh, kw, stride, pad, dil, o, s, _V_WGRAD, ws, cnt),
-                O, kh * kw * Cin, wgrad_splits(O, kh * kw * Cin, npix), dw4, _V_WGRAD,
-            )
+            dw4 = torch.empty(w4.shape, dtype=w.dtype, device=w.device)
+            wgrad_into(dy4, x4, stride, pad, dil, dw4)
             dw = dw4.permute(0, 3, 1, 2)
         return dx, dw, None, None, None
 
@@ -226,13 +342,8 @@ def _fwd_bn_launch(x4, w, stride, pad, dil, bn_w, bn_b, rm, rv, nbt, eps, moment
 
 
 def _wgrad_launch(dy4, x4, w, stride, pad, dil):
-    O, kh, kw, Cin = w.shape[0], w.shape[2], w.shape[3], w.shape[1]
-    npix = dy4.shape[0] * dy4.shape[1] * dy4.shape[2]
-    dw4 = torch.empty((O, kh, kw, Cin), dtype=w.dtype, device=w.device)
-    _run_split(
-        lambda o, s, ws, cnt: _C().conv_wgrad(dy4, x4, kh, kw, stride, pad, dil, o, s, _V_WGRAD, ws, cnt),
-        O, kh * kw * Cin, wgrad_splits(O, kh * kw * Cin, npix), dw4, _V_WGRAD,
-    )
+    dw4 = torch.empty(w.permute(0, 2, 3, 1).shape, dtype=w.dtype, device=w.device)
+    wgrad_into(dy4, x4, stride, pad, dil, dw4)
     return dw4.permute(0, 3, 1, 2)
 
 

@@ -17,8 +17,9 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import torch  # noqa: E402
 
 from p2pfl_amd import ops  # noqa: E402
-from p2pfl_amd.ops.conv import _run_split, mn_splits, out_hw, wgrad_splits  # noqa: E402
+from p2pfl_amd.ops import autotune  # noqa: E402
 from p2pfl_amd.ops.autotune import _time  # noqa: E402
+from p2pfl_amd.ops.conv import dgrad_into, fwd_into, out_hw, wgrad_into  # noqa: E402
 
 
 def timeit(fn, iters=30):
@@ -32,11 +33,9 @@ def main() -> None:
     ap = argparse.ArgumentParser()
     ap.add_argument("--batch", type=int, default=32)
     ap.add_argument("--out", default=None)
-    ap.add_argument("--variants", default="10,10,2", help="csrc/gemm.h variant bits for fwd,dgrad,wgrad")
     args = ap.parse_args()
-    C_ = ops.ext()
+    ops.ext()
     torch.backends.cudnn.benchmark = True  # MIOpen find mode, as the learner runs it
-    vf, vd, vw = (int(v) for v in args.variants.split(","))
     N = args.batch
     bf = torch.bfloat16
     # (name, C, H, O, k, stride, pad, count in ResNet-18)
@@ -63,11 +62,11 @@ def main() -> None:
         y4 = torch.empty(N, OH, OW, O, device="cuda", dtype=bf)
         dx4 = torch.empty(N, H, H, C, device="cuda", dtype=bf)
         dw4 = torch.empty(O, k, k, C, device="cuda", dtype=bf)
-        sf, sd, sw = mn_splits(N * OH * OW, O, k * k * C), mn_splits(N * H * H, C, k * k * O), wgrad_splits(O, k * k * C, N * OH * OW)
+        # the autograd's own entry points: per-shape measured (variant, split-K, stride-2 by phase)
         mine = [
-            timeit(lambda: _run_split(lambda o, sp, ws, cnt: C_.conv_fwd(x4, w4, s, p, 1, o, sp, vf, ws, cnt), N * OH * OW, O, sf, y4, vf)),
-            timeit(lambda: _run_split(lambda o, sp, ws, cnt: C_.conv_dgrad(dy4, w4, s, p, 1, o, [N, H, H, C], sp, vd, ws, cnt), N * H * H, C, sd, dx4, vd)),
-            timeit(lambda: _run_split(lambda o, sp, ws, cnt: C_.conv_wgrad(dy4, x4, k, k, s, p, 1, o, sp, vw, ws, cnt), O, k * k * C, sw, dw4, vw)),
+            timeit(lambda: fwd_into(x4, w4, s, p, 1, y4)),
+            timeit(lambda: dgrad_into(dy4, w4, s, p, 1, dx4)),
+            timeit(lambda: wgrad_into(dy4, x4, s, p, 1, dw4)),
         ]
         xr = x.clone().requires_grad_()
         wr = w.clone().requires_grad_()
@@ -78,12 +77,16 @@ def main() -> None:
         ]
         del xr, wr
         fl = 2.0 * N * OH * OW * O * C * k * k
+        picked = {key[0]: v for key, (v, _) in autotune.choices().items()
+                  if isinstance(key, tuple) and key[0].startswith("conv_") and key[1][1:] == (H, H, C) and key[2:6] == (O, k, k, s)}
         for kind, t1, t2 in zip(("fwd", "dgrad", "wgrad"), mine, theirs):
-            rows.append((f"{name} {kind}", cnt, t1 * 1e6, fl / t1 / 1e12, t2 * 1e6, fl / t2 / 1e12))
+            rows.append((f"{name} {kind}", cnt, t1 * 1e6, fl / t1 / 1e12, t2 * 1e6, fl / t2 / 1e12,
+                         picked.get("conv_" + kind, "-")))
             tot_n += cnt * t1 * 1e6
             tot_m += cnt * t2 * 1e6
-    head = "| conv | x in R18 | native us | native TF/s | MIOpen us | MIOpen TF/s |\n|---|---:|---:|---:|---:|---:|"
-    lines = [head] + [f"| {r[0]} | {r[1]} | {r[2]:.1f} | {r[3]:.0f} | {r[4]:.1f} | {r[5]:.0f} |" for r in rows]
+    head = ("| conv | x in R18 | native us | native TF/s | MIOpen us | MIOpen TF/s | native config |\n"
+            "|---|---:|---:|---:|---:|---:|---|")
+    lines = [head] + [f"| {r[0]} | {r[1]} | {r[2]:.1f} | {r[3]:.0f} | {r[4]:.1f} | {r[5]:.0f} | {r[6]} |" for r in rows]
     lines.append(f"\nResNet-18 block convolutions per training step (batch {N}): native {tot_n:.0f} us, MIOpen {tot_m:.0f} us")
     text = "\n".join(lines)
     print(text, flush=True)

@@ -1,6 +1,9 @@
 """Run one convolution product repeatedly (for rocprofv3 counter collection).
 
-    python scripts/conv_one.py [fwd|dgrad|wgrad] [N C H O k stride pad]
+    python scripts/conv_one.py [fwd|dgrad|dgrad_auto|wgrad] [N C H O k stride pad]
+
+dgrad_auto runs the autograd's input-gradient path (ops/conv.py dgrad_into: split-K
+choice, stride 2 by phase).
 """
 import os
 import sys
@@ -9,7 +12,7 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import torch  # noqa: E402
 
 from p2pfl_amd import ops  # noqa: E402
-from p2pfl_amd.ops.conv import out_hw  # noqa: E402
+from p2pfl_amd.ops.conv import dgrad_into, out_hw  # noqa: E402
 
 kind = sys.argv[1] if len(sys.argv) > 1 else "fwd"
 N, C, H, O, k, s, p = (int(v) for v in (sys.argv[2:9] if len(sys.argv) > 8 else (32, 64, 32, 64, 3, 1, 1)))
@@ -22,6 +25,8 @@ X = ops.ext()
 for _ in range(20):
     if kind == "fwd":
         X.conv_fwd(x4, w4, s, p, 1, torch.empty(N, OH, OW, O, device="cuda", dtype=bf), 1, 10)
+    elif kind == "dgrad_auto":
+        dgrad_into(dy4, w4, s, p, 1, torch.empty(N, H, H, C, device="cuda", dtype=bf))
     elif kind == "dgrad":
         X.conv_dgrad(dy4, w4, s, p, 1, torch.empty(N, H, H, C, device="cuda", dtype=bf), [N, H, H, C], 1, 10)
     else:

@@ -147,6 +147,106 @@ def test_conv_split_k_in_launch_reduction(splits):
     assert int(cnt.abs().sum()) == 0
 
 
+S2_CASES = [
+    # N, C, H, W, O, k, pad: shapes the by-phase stride-2 input gradient takes (N H W / 4 % 128 == 0)
+    (8, 64, 16, 16, 128, 3, 1),
+    (8, 128, 16, 16, 256, 1, 0),
+    (2, 64, 32, 32, 64, 3, 0),
+    (32, 64, 8, 8, 128, 5, 2),
+]
+
+
+@pytest.mark.parametrize("N,C,H,W,O,k,p", S2_CASES)
+@pytest.mark.parametrize("mode", ["plain", "slabs", "in_launch"])
+def test_conv_dgrad_stride2_by_phase_exact(N, C, H, W, O, k, p, mode):
+    """conv_dgrad_s2 + phase_interleave equals the fp32 input gradient exactly on integer
+    operands: each phase's taps addressed right, tap-less phases (1x1) zero."""
+    from p2pfl_amd.ops.splitk import slab_elems, tiles_of
+
+    x, w = _operands(N, C, H, W, O, k, seed=N + H + k, integer=True)
+    OH, OW = conv_ops.out_hw(H, W, (k, k), 2, p, 1)
+    dy = torch.randint(-2, 3, (N, O, OH, OW), device="cuda").to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    C_ = ops.ext()
+    dy4, w4 = dy.permute(0, 2, 3, 1), w.permute(0, 2, 3, 1)
+    rows = N * H * W // (4 if k == 1 else 1)
+    ph = torch.empty(rows, C, device="cuda", dtype=torch.bfloat16)
+    if mode == "plain":
+        C_.conv_dgrad_s2(dy4, w4, p, ph, [N, H, W, C])
+    elif mode == "slabs":
+        slabs = torch.empty(4 * slab_elems(rows, C), device="cuda")
+        C_.conv_dgrad_s2(dy4, w4, p, slabs, [N, H, W, C], 4, 10)
+        acc = torch.empty(rows, C, device="cuda")
+        C_.tile_slab_reduce(slabs, 4, rows, C, acc, 10)
+        ph.copy_(acc)
+    else:
+        ws = torch.empty(8 * slab_elems(rows, C), device="cuda")
+        cnt = torch.zeros(tiles_of(rows, C), dtype=torch.int32, device="cuda")
+        C_.conv_dgrad_s2(dy4, w4, p, ph, [N, H, W, C], 8, 10, ws, cnt)
+        assert int(cnt.abs().sum()) == 0
+    dx4 = torch.full((N, H, W, C), float("nan"), device="cuda", dtype=torch.bfloat16)
+    C_.phase_interleave(ph, dx4, p, k, k)
+    xr = x.float().requires_grad_()
+    _ref(xr, w.float(), 2, p, 1).backward(dy.float())
+    torch.testing.assert_close(dx4.permute(0, 3, 1, 2).float(), xr.grad.to(torch.bfloat16).float(), atol=0, rtol=0)
+
+
+def test_stride2_autograd_takes_phase_path(monkeypatch):
+    """The conv autograd's stride-2 input gradient runs by phase (and the all-taps gather
+    when switched off) with the same result."""
+    N, C, H, W, O, k = 8, 64, 16, 16, 128, 3
+    x, w = _operands(N, C, H, W, O, k, seed=11)
+    assert conv_ops.s2_phases_ok(2, 1, [N, H, W, C])
+    assert not conv_ops.s2_phases_ok(2, 1, [N, H, W, C], (1, 1))
+    conv = nn.Conv2d(C, O, k, 2, 1, bias=False).cuda()
+    conv.weight.data = w
+    grads = []
+    for on, tune in ((True, False), (False, False), (True, True)):
+        monkeypatch.setattr(conv_ops, "_S2_PHASES", on)
+        monkeypatch.setattr(conv_ops, "_TUNE", tune)  # untuned: the default path of each setting
+        xg = x.clone().requires_grad_()
+        y = ops.conv2d(xg, conv)
+        torch.manual_seed(0)
+        y.backward(torch.randn(y.shape, device="cuda").to(torch.bfloat16).contiguous(memory_format=torch.channels_last))
+        grads.append(xg.grad.float())
+    torch.testing.assert_close(grads[0], grads[1], atol=2e-2, rtol=1e-2)
+    torch.testing.assert_close(grads[2], grads[1], atol=2e-2, rtol=1e-2)
+    key = ("conv_dgrad", (N, H, W, C), O, k, k, 2, 1, 1)
+    assert key in conv_ops.autotune.choices(), "tuned run did not time the stride-2 input gradient"
+
+
+def test_tuned_configs_all_agree(monkeypatch):
+    """Every (variant, split-K) candidate the per-shape tuning may pick gives the same
+    exact result on integer operands (forward, input and weight gradient)."""
+    N, C, H, W, O, k = 4, 128, 8, 8, 256, 3
+    x, w = _operands(N, C, H, W, O, k, seed=5, integer=True)
+    dy = torch.randint(-2, 3, (N, O, H, W), device="cuda").to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    x4, w4, dy4 = x.permute(0, 2, 3, 1), w.permute(0, 2, 3, 1), dy.permute(0, 2, 3, 1)
+    seen = {}
+
+    def grab(key, cands, default, out):
+        for name, f in cands.items():
+            dst = torch.full_like(out, float("nan"))
+            f(dst)
+            seen.setdefault(key[0], []).append((name, dst))
+        cands[default](out)
+
+    monkeypatch.setattr(conv_ops, "_pick", grab)
+    monkeypatch.setattr(conv_ops, "_TUNE", True)
+    conv_ops.fwd_into(x4, w4, 1, 1, 1, torch.empty(N, H, W, O, device="cuda", dtype=torch.bfloat16))
+    conv_ops.dgrad_into(dy4, w4, 1, 1, 1, torch.empty(N, H, W, C, device="cuda", dtype=torch.bfloat16))
+    conv_ops.wgrad_into(dy4, x4, 1, 1, 1, torch.empty(O, k, k, C, device="cuda", dtype=torch.float32))
+    xr, wr = x.float().requires_grad_(), w.float().requires_grad_()
+    y = _ref(xr, wr, 1, 1, 1)
+    y.backward(dy.float())
+    refs = {"conv_fwd": y.detach().permute(0, 2, 3, 1).to(torch.bfloat16).float(),
+            "conv_dgrad": xr.grad.permute(0, 2, 3, 1).to(torch.bfloat16).float(),
+            "conv_wgrad": wr.grad.permute(0, 2, 3, 1)}
+    for kind, outs in seen.items():
+        assert len(outs) >= 3, kind
+        for name, dst in outs:
+            torch.testing.assert_close(dst.float(), refs[kind], atol=0, rtol=0, msg=f"{kind} {name}")
+
+
 @pytest.mark.parametrize("splits", [1, 2, 8, 64])
 def test_conv_wgrad_split_k(splits):
     N, C, H, W, O, k = 8, 64, 16, 16, 64, 3
