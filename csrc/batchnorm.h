@@ -50,7 +50,7 @@ void bn_fwd_eval(bool bf16, const void* x, const void* res, const float* w, cons
 //   db = sum dz, dw = rstd * sum dz (x - mean)
 //   dx = w rstd (dz - db / M - xhat dw / M);   dres = dz (if dres != null)
 // part: [2, S, C]; coef: [3, C] scratch; ctr as bn_fwd_train.
-void bn_bwd(bool bf16, const void* dy, const void* y, const void* x, const float* w, const float* mean,
+void bn_bwd(bool bf16, const void* dy, const void* dy2, const void* y, const void* x, const float* w, const float* mean,
             const float* rstd, void* dx, void* dres, float* dw, float* db, float* coef, float* part, int* ctr, int M,
             int C, bool relu, hipStream_t s);
 

@@ -135,9 +135,12 @@ __global__ __launch_bounds__(kThreads) void bn_stats_kernel(const T* __restrict_
   phase_reduce_store(s1, s2, active, tg, ph, tpr, rp, part, C);
 }
 
-// backward statistics: sum dz and sum dz * (x - mean) per channel
+// backward statistics: sum dz and sum dz * (x - mean) per channel.  dy2 (or null):
+// a second gradient of the same output, summed on load -- a residual block's
+// input feeds two branches, and the two gradients never need an add pass
 template <typename T, bool RELU>
-__global__ __launch_bounds__(kThreads) void bn_bwd_stats_kernel(const T* __restrict__ dy, const T* __restrict__ y,
+__global__ __launch_bounds__(kThreads) void bn_bwd_stats_kernel(const T* __restrict__ dy, const T* __restrict__ dy2,
+                                                                const T* __restrict__ y,
                                                                 const T* __restrict__ x,
                                                                 const float* __restrict__ mean,
                                                                 float* __restrict__ part, int M, int C, int tpr,
@@ -162,6 +165,16 @@ __global__ __launch_bounds__(kThreads) void bn_bwd_stats_kernel(const T* __restr
         V8<T>::load(dy + e, g[u]);
         V8<T>::load(x + e, xv[u]);
         if (RELU) V8<T>::load(y + e, yv[u]);
+      }
+      if (dy2) {
+#pragma unroll
+        for (int u = 0; u < kInFlight; ++u) {
+          const int ru = r + u * step;
+          float g2[8];
+          V8<T>::load(dy2 + size_t(ru < M ? ru : 0) * C + c, g2);
+#pragma unroll
+          for (int j = 0; j < 8; ++j) g[u][j] += g2[j];
+        }
       }
 #pragma unroll
       for (int u = 0; u < kInFlight; ++u) {
@@ -311,7 +324,8 @@ __global__ __launch_bounds__(kThreads) void bn_apply_fwd_kernel(const T* __restr
 }
 
 template <typename T, bool RELU, bool RES>
-__global__ __launch_bounds__(kThreads) void bn_apply_bwd_kernel(const T* __restrict__ dy, const T* __restrict__ y,
+__global__ __launch_bounds__(kThreads) void bn_apply_bwd_kernel(const T* __restrict__ dy, const T* __restrict__ dy2,
+                                                                const T* __restrict__ y,
                                                                 const T* __restrict__ x,
                                                                 const float* __restrict__ mean,
                                                                 const float* __restrict__ coef, T* __restrict__ dx,
@@ -322,6 +336,12 @@ __global__ __launch_bounds__(kThreads) void bn_apply_bwd_kernel(const T* __restr
     float g[8], xv[8], mu[8], A[8], B[8], D[8];
     V8<T>::load(dy + e, g);
     V8<T>::load(x + e, xv);
+    if (dy2) {
+      float g2[8];
+      V8<T>::load(dy2 + e, g2);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) g[j] += g2[j];
+    }
     if (RELU) {
       float yv[8];
       V8<T>::load(y + e, yv);
@@ -624,18 +644,18 @@ static void apply_fwd(const T* x, const T* r, const float* coef, T* y, int M, in
 }
 
 template <typename T>
-static void apply_bwd(const T* dy, const T* y, const T* x, const float* mean, const float* coef, T* dx, T* dres, int M,
-                      int C, bool relu, hipStream_t s) {
+static void apply_bwd(const T* dy, const T* dy2, const T* y, const T* x, const float* mean, const float* coef, T* dx,
+                      T* dres, int M, int C, bool relu, hipStream_t s) {
   const int64_t n8 = int64_t(M) * C / 8;
   const dim3 grid(stream_grid(n8, kThreads)), blk(kThreads);
   if (relu && dres)
-    hipLaunchKernelGGL((bn_apply_bwd_kernel<T, true, true>), grid, blk, 0, s, dy, y, x, mean, coef, dx, dres, n8, C);
+    hipLaunchKernelGGL((bn_apply_bwd_kernel<T, true, true>), grid, blk, 0, s, dy, dy2, y, x, mean, coef, dx, dres, n8, C);
   else if (relu)
-    hipLaunchKernelGGL((bn_apply_bwd_kernel<T, true, false>), grid, blk, 0, s, dy, y, x, mean, coef, dx, dres, n8, C);
+    hipLaunchKernelGGL((bn_apply_bwd_kernel<T, true, false>), grid, blk, 0, s, dy, dy2, y, x, mean, coef, dx, dres, n8, C);
   else if (dres)
-    hipLaunchKernelGGL((bn_apply_bwd_kernel<T, false, true>), grid, blk, 0, s, dy, y, x, mean, coef, dx, dres, n8, C);
+    hipLaunchKernelGGL((bn_apply_bwd_kernel<T, false, true>), grid, blk, 0, s, dy, dy2, y, x, mean, coef, dx, dres, n8, C);
   else
-    hipLaunchKernelGGL((bn_apply_bwd_kernel<T, false, false>), grid, blk, 0, s, dy, y, x, mean, coef, dx, dres, n8, C);
+    hipLaunchKernelGGL((bn_apply_bwd_kernel<T, false, false>), grid, blk, 0, s, dy, dy2, y, x, mean, coef, dx, dres, n8, C);
 }
 
 template <typename T>
@@ -700,7 +720,7 @@ void bn_apply_train(bool bf16, const void* x, const void* res, const float* coef
 
 void bn_apply_bwd_only(const void* dy, const void* y, const void* x, const float* mean, const float* coef, void* dx,
                        int M, int C, bool relu, hipStream_t s) {
-  apply_bwd<uint16_t>(static_cast<const uint16_t*>(dy), static_cast<const uint16_t*>(y), static_cast<const uint16_t*>(x),
+  apply_bwd<uint16_t>(static_cast<const uint16_t*>(dy), nullptr, static_cast<const uint16_t*>(y), static_cast<const uint16_t*>(x),
                       mean, coef, static_cast<uint16_t*>(dx), nullptr, M, C, relu, s);
 }
 
@@ -713,44 +733,45 @@ void bn_fwd_eval(bool bf16, const void* x, const void* res, const float* w, cons
 }
 
 template <typename T>
-static void bwd_t(const void* dyv, const void* yv, const void* xv, const float* w, const float* mean,
+static void bwd_t(const void* dyv, const void* dy2v, const void* yv, const void* xv, const float* w, const float* mean,
                   const float* rstd, void* dxv, void* dresv, float* dw, float* db, float* coef, float* part, int* ctr,
                   int M, int C, bool relu, hipStream_t s) {
   const T* dy = static_cast<const T*>(dyv);
+  const T* dy2 = static_cast<const T*>(dy2v);
   const T* y = static_cast<const T*>(yv);
   const T* x = static_cast<const T*>(xv);
   T* dx = static_cast<T*>(dxv);
   T* dres = static_cast<T*>(dresv);
   if constexpr (sizeof(T) == 2) {
     const BnPlan f = bn_fused_plan(M, C);
-    if (ctr && f.S > 0) {
+    if (ctr && f.S > 0 && !dy2) {
       if (relu)
         hipLaunchKernelGGL(bn_bwd_stats_fin_kernel<true>, dim3(1, f.S), dim3(kThreads), 0, s, dy, y, x, w, mean, rstd, dw,
                            db, coef, part, ctr, M, C, f.tpr, f.rp);
       else
         hipLaunchKernelGGL(bn_bwd_stats_fin_kernel<false>, dim3(1, f.S), dim3(kThreads), 0, s, dy, y, x, w, mean, rstd, dw,
                            db, coef, part, ctr, M, C, f.tpr, f.rp);
-      apply_bwd(dy, y, x, mean, coef, dx, dres, M, C, relu, s);
+      apply_bwd(dy, dy2, y, x, mean, coef, dx, dres, M, C, relu, s);
       return;
     }
   }
   const BnPlan p = bn_plan(M, C);
   const dim3 sgrid(p.gx, p.S), blk(kThreads);
   if (relu)
-    hipLaunchKernelGGL((bn_bwd_stats_kernel<T, true>), sgrid, blk, 0, s, dy, y, x, mean, part, M, C, p.tpr, p.rp);
+    hipLaunchKernelGGL((bn_bwd_stats_kernel<T, true>), sgrid, blk, 0, s, dy, dy2, y, x, mean, part, M, C, p.tpr, p.rp);
   else
-    hipLaunchKernelGGL((bn_bwd_stats_kernel<T, false>), sgrid, blk, 0, s, dy, y, x, mean, part, M, C, p.tpr, p.rp);
+    hipLaunchKernelGGL((bn_bwd_stats_kernel<T, false>), sgrid, blk, 0, s, dy, dy2, y, x, mean, part, M, C, p.tpr, p.rp);
   hipLaunchKernelGGL(bn_finalize_bwd_kernel, dim3((C + kFinCols - 1) / kFinCols), blk, 0, s, part, p.S, w, rstd, dw, db, coef, M, C);
-  apply_bwd(dy, y, x, mean, coef, dx, dres, M, C, relu, s);
+  apply_bwd(dy, dy2, y, x, mean, coef, dx, dres, M, C, relu, s);
 }
 
-void bn_bwd(bool bf16, const void* dy, const void* y, const void* x, const float* w, const float* mean,
+void bn_bwd(bool bf16, const void* dy, const void* dy2, const void* y, const void* x, const float* w, const float* mean,
             const float* rstd, void* dx, void* dres, float* dw, float* db, float* coef, float* part, int* ctr, int M,
             int C, bool relu, hipStream_t s) {
   if (bf16)
-    bwd_t<uint16_t>(dy, y, x, w, mean, rstd, dx, dres, dw, db, coef, part, ctr, M, C, relu, s);
+    bwd_t<uint16_t>(dy, dy2, y, x, w, mean, rstd, dx, dres, dw, db, coef, part, ctr, M, C, relu, s);
   else
-    bwd_t<float>(dy, y, x, w, mean, rstd, dx, dres, dw, db, coef, part, nullptr, M, C, relu, s);
+    bwd_t<float>(dy, dy2, y, x, w, mean, rstd, dx, dres, dw, db, coef, part, nullptr, M, C, relu, s);
 }
 
 }  // namespace p2bn

@@ -148,15 +148,17 @@ torch::Tensor bn_fwd_eval(torch::Tensor x, torch::Tensor w, torch::Tensor b, c10
   return y;
 }
 
-// returns {dx, dw, db} or {dx, dw, db, dres}
+// returns {dx, dw, db} or {dx, dw, db, dres}; dy2 (optional): a second gradient of the output, summed with dy
 std::vector<torch::Tensor> bn_bwd(torch::Tensor dy, torch::Tensor y, torch::Tensor x, torch::Tensor w,
                                   torch::Tensor mean, torch::Tensor rstd, bool relu, bool need_dres,
-                                  c10::optional<torch::Tensor> counters) {
+                                  c10::optional<torch::Tensor> counters, c10::optional<torch::Tensor> dy2) {
   const c10::DeviceGuard g(x.device());
   check_shape(x);
   const int64_t M = x.size(0), C = x.size(1);
   const bool bf = act(x, x, "x");
   act(dy, x, "dy");
+  const bool two = dy2.has_value() && dy2->defined();
+  if (two) act(*dy2, x, "dy2");
   if (relu) act(y, x, "y");
   auto dx = torch::empty_like(x);
   auto dres = need_dres ? torch::empty_like(x) : torch::Tensor();
@@ -164,7 +166,7 @@ std::vector<torch::Tensor> bn_bwd(torch::Tensor dy, torch::Tensor y, torch::Tens
   auto dw = torch::empty({C}, opt), db = torch::empty({C}, opt), coef = torch::empty({3, C}, opt);
   int* ctr = opt_ctr(counters, x);
   auto part = torch::empty({2, part_rows(M, C, ctr != nullptr), C}, opt);
-  p2bn::bn_bwd(bf, dy.data_ptr(), relu ? y.data_ptr() : nullptr, x.data_ptr(), f32(w, C, x, "weight"),
+  p2bn::bn_bwd(bf, dy.data_ptr(), two ? dy2->data_ptr() : nullptr, relu ? y.data_ptr() : nullptr, x.data_ptr(), f32(w, C, x, "weight"),
                f32(mean, C, x, "mean"), f32(rstd, C, x, "rstd"), dx.data_ptr(), need_dres ? dres.data_ptr() : nullptr,
                dw.data_ptr<float>(), db.data_ptr<float>(), coef.data_ptr<float>(), part.data_ptr<float>(), ctr, int(M),
                int(C), relu, stream());
@@ -186,7 +188,7 @@ void register_bn(pybind11::module& m) {
   f.def("fwd_eval", &bn_fwd_eval, py::arg("x"), py::arg("w"), py::arg("b"), py::arg("residual") = py::none(),
         py::arg("running_mean"), py::arg("running_var"), py::arg("eps") = 1e-5, py::arg("relu") = true);
   f.def("bwd", &bn_bwd, py::arg("dy"), py::arg("y"), py::arg("x"), py::arg("w"), py::arg("mean"), py::arg("rstd"),
-        py::arg("relu"), py::arg("need_dres"), py::arg("counters") = py::none());
+        py::arg("relu"), py::arg("need_dres"), py::arg("counters") = py::none(), py::arg("dy2") = py::none());
   f.def("fused_rows", [](int64_t M, int64_t C) { return p2bn::bn_fused_plan(int(M), int(C)).S; },
         "partial rows of the statistics + finalize kernels for an [M, C] activation (0: not eligible)");
 }

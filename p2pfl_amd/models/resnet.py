@@ -56,6 +56,18 @@ _NATIVE_STEM = os.environ.get("P2PFL_NATIVE_STEM", "1") != "0"
 _NATIVE_HEAD = os.environ.get("P2PFL_NATIVE_HEAD", "1") != "0"
 
 
+# A block's input feeds its first convolution and its shortcut.  The producing BN
+# returns two autograd outputs for them (batch_norm_act(..., fork=True)), so the
+# two gradients are summed inside that BN's backward kernels rather than by an
+# autograd add pass per block (P2PFL_RESNET_FORK=0: one output, autograd adds).
+_FORK = os.environ.get("P2PFL_RESNET_FORK", "1") != "0"
+
+
+def _pair(x):
+    """(input of the first convolution, input of the shortcut) of a block."""
+    return x if isinstance(x, tuple) else (x, x)
+
+
 def _shortcut(sc: nn.Module, x: torch.Tensor) -> torch.Tensor:
     """Identity, or the projection conv + BN (no activation)."""
     if isinstance(sc, nn.Identity):
@@ -76,13 +88,16 @@ class BasicBlock(nn.Module):
         if stride != 1 or cin != cout:
             self.shortcut = nn.Sequential(nn.Conv2d(cin, cout, 1, stride, bias=False), nn.BatchNorm2d(cout))
 
-    def forward(self, x: torch.Tensor) -> torch.Tensor:
+    def forward(self, x):
+        """``x``: a tensor or the (conv input, shortcut input) pair of a forked BN output;
+        returns such a pair (see ``_FORK``)."""
+        x, xs = _pair(x)
         st = conv_bn_stats(x, self.conv1, self.bn1)
         st = bn_act_conv_bn_stats(st, self.bn1, True, self.conv2, self.bn2) if st is not None else None
         if st is not None:  # conv1 -> [bn1 apply, conv2] -> bn2 apply: 3 launches forward
-            return batch_norm_apply(st[0], self.bn2, st[1], st[2], st[3], _shortcut(self.shortcut, x), True)
+            return batch_norm_apply(st[0], self.bn2, st[1], st[2], st[3], _shortcut(self.shortcut, xs), True, _FORK)
         out = conv_bn_act(x, self.conv1, self.bn1)
-        return conv_bn_act(out, self.conv2, self.bn2, residual=_shortcut(self.shortcut, x))
+        return conv_bn_act(out, self.conv2, self.bn2, residual=_shortcut(self.shortcut, xs), fork=_FORK)
 
 
 class Bottleneck(nn.Module):
@@ -101,15 +116,17 @@ class Bottleneck(nn.Module):
         if stride != 1 or cin != cout:
             self.shortcut = nn.Sequential(nn.Conv2d(cin, cout, 1, stride, bias=False), nn.BatchNorm2d(cout))
 
-    def forward(self, x: torch.Tensor) -> torch.Tensor:
+    def forward(self, x):
+        """As :meth:`BasicBlock.forward`: a tensor or a pair in, a pair out."""
+        x, xs = _pair(x)
         st = conv_bn_stats(x, self.conv1, self.bn1)
         st = bn_act_conv_bn_stats(st, self.bn1, True, self.conv2, self.bn2) if st is not None else None
         st = bn_act_conv_bn_stats(st, self.bn2, True, self.conv3, self.bn3) if st is not None else None
         if st is not None:
-            return batch_norm_apply(st[0], self.bn3, st[1], st[2], st[3], _shortcut(self.shortcut, x), True)
+            return batch_norm_apply(st[0], self.bn3, st[1], st[2], st[3], _shortcut(self.shortcut, xs), True, _FORK)
         out = conv_bn_act(x, self.conv1, self.bn1)
         out = conv_bn_act(out, self.conv2, self.bn2)
-        return conv_bn_act(out, self.conv3, self.bn3, residual=_shortcut(self.shortcut, x))
+        return conv_bn_act(out, self.conv3, self.bn3, residual=_shortcut(self.shortcut, xs), fork=_FORK)
 
 
 class ResNet(FLModule):
@@ -171,10 +188,11 @@ class ResNet(FLModule):
             if x.is_cuda and _CHANNELS_LAST:
                 x = x.contiguous(memory_format=torch.channels_last)
             x = conv2d(x, stem)
-        x = batch_norm_act(x, self.stem[1])
         if len(self.stem) > 3:
-            x = self.stem[3](x)
-        return self.layer4(self.layer3(self.layer2(self.layer1(x))))
+            x = self.stem[3](batch_norm_act(x, self.stem[1]))
+        else:
+            x = batch_norm_act(x, self.stem[1], fork=_FORK)
+        return _pair(self.layer4(self.layer3(self.layer2(self.layer1(x)))))[0]
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
         x = torch.flatten(nn.functional.adaptive_avg_pool2d(self.features(x), 1), 1)

@@ -24,7 +24,7 @@ from torch import nn
 
 
 # host-side counters of the extra passes the backward had to insert
-STATS = {"dy_cast": 0, "dy_relayout": 0}
+STATS = {"dy_cast": 0, "dy_relayout": 0, "dy_pairs": 0}
 # statistics + finalize as one launch for eligible bf16 shapes (P2PFL_BN_FUSED_STATS=1).  Off by
 # default: per call it is 8.4 us against 4.9 + 4.9 us for the two launches, but the ResNet-18 /
 # ResNet-50 rounds measured 3.5 % / 2.5 % slower with it (profiles/r3_bn_stats_finalize.md).
@@ -65,9 +65,28 @@ def batch_norm_act_reference(x, weight, bias, running_mean, running_var, trainin
     return torch.relu(y) if relu else y
 
 
+def _outputs(ctx, y2, shape, fork: bool):
+    """The NCHW view of y2, or with ``fork`` that view and an alias of it: two autograd
+    outputs for the two consumers of a residual block's input (its first convolution
+    and its shortcut), whose gradients the backward then sums inside the BN kernels
+    instead of autograd adding them in a separate pass."""
+    y = _from_2d(y2, shape)
+    if not fork:
+        return y
+    ctx.set_materialize_grads(False)  # an unused alias brings None, not a zero-filled gradient
+    return y, y.view_as(y)
+
+
+def _grads(dy, dy2):
+    """(dy, dy2) of a forked output with None for a branch that sent no gradient."""
+    if dy is None:
+        return dy2, None
+    return dy, dy2
+
+
 class _BatchNormAct(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, weight, bias, residual, running_mean, running_var, nbt, momentum, eps, relu):
+    def forward(ctx, x, weight, bias, residual, running_mean, running_var, nbt, momentum, eps, relu, fork=False):
         shape = x.shape
         x2 = _nhwc_2d(x)
         r2 = _nhwc_2d(residual.to(x.dtype)) if residual is not None else None
@@ -76,23 +95,33 @@ class _BatchNormAct(torch.autograd.Function):
         ctx.save_for_backward(x2, y2, weight, mean, rstd)
         ctx.shape, ctx.relu, ctx.has_res = shape, bool(relu), residual is not None
         ctx.res_dtype = residual.dtype if residual is not None else None
-        return _from_2d(y2, shape)
+        return _outputs(ctx, y2, shape, fork)
 
     @staticmethod
-    def backward(ctx, dy):
-        return _bn_backward(ctx, dy) + (None, None, None, None, None, None)
+    def backward(ctx, dy, dy2=None):
+        return _bn_backward(ctx, *_grads(dy, dy2)) + (None,) * 7
 
 
-def _bn_backward(ctx, dy):
-    """(dx, dweight, dbias, dresidual) of act(bn(x) [+ residual]) from the saved x2, y2, weight, mean, rstd."""
+def _bn_backward(ctx, dy, dy2=None):
+    """(dx, dweight, dbias, dresidual) of act(bn(x) [+ residual]) from the saved x2, y2, weight,
+    mean, rstd; ``dy2``: the gradient of the forked alias output, summed with dy in the kernels."""
     x2, y2, weight, mean, rstd = ctx.saved_tensors
-    if dy.dtype != x2.dtype:
-        STATS["dy_cast"] += 1
-        dy = dy.to(x2.dtype)
-    if not dy.is_contiguous(memory_format=torch.channels_last):
-        STATS["dy_relayout"] += 1
-        dy = dy.contiguous(memory_format=torch.channels_last)
-    out = _bx().bwd(_nhwc_2d(dy), y2, x2, weight, mean, rstd, ctx.relu, ctx.has_res and ctx.needs_input_grad[3], _counter(x2))
+    if dy is None:  # neither branch used the output
+        return None, None, None, None
+
+    def prep(g):
+        if g.dtype != x2.dtype:
+            STATS["dy_cast"] += 1
+            g = g.to(x2.dtype)
+        if not g.is_contiguous(memory_format=torch.channels_last):
+            STATS["dy_relayout"] += 1
+            g = g.contiguous(memory_format=torch.channels_last)
+        return _nhwc_2d(g)
+
+    if dy2 is not None:
+        STATS["dy_pairs"] += 1
+    out = _bx().bwd(prep(dy), y2, x2, weight, mean, rstd, ctx.relu, ctx.has_res and ctx.needs_input_grad[3], _counter(x2),
+                    prep(dy2) if dy2 is not None else None)
     dx = _from_2d(out[0], ctx.shape)
     dres = _from_2d(out[3], ctx.shape).to(ctx.res_dtype) if len(out) > 3 else None
     return dx, out[1].to(weight.dtype), out[2].to(weight.dtype), dres
@@ -105,7 +134,7 @@ class _BatchNormApply(torch.autograd.Function):
     Backward is the fused BN backward of :class:`_BatchNormAct`."""
 
     @staticmethod
-    def forward(ctx, x, weight, bias, residual, mean, rstd, coef, relu):
+    def forward(ctx, x, weight, bias, residual, mean, rstd, coef, relu, fork=False):
         shape = x.shape
         x2 = _nhwc_2d(x)
         r2 = _nhwc_2d(residual.to(x.dtype)) if residual is not None else None
@@ -113,17 +142,18 @@ class _BatchNormApply(torch.autograd.Function):
         ctx.save_for_backward(x2, y2, weight, mean, rstd)
         ctx.shape, ctx.relu, ctx.has_res = shape, bool(relu), residual is not None
         ctx.res_dtype = residual.dtype if residual is not None else None
-        return _from_2d(y2, shape)
+        return _outputs(ctx, y2, shape, fork)
 
     @staticmethod
-    def backward(ctx, dy):
-        return _bn_backward(ctx, dy) + (None, None, None, None)
+    def backward(ctx, dy, dy2=None):
+        return _bn_backward(ctx, *_grads(dy, dy2)) + (None,) * 5
 
 
 def batch_norm_apply(x: torch.Tensor, bn: nn.BatchNorm2d, mean: torch.Tensor, rstd: torch.Tensor, coef: torch.Tensor,
-                     residual: Optional[torch.Tensor] = None, relu: bool = True) -> torch.Tensor:
-    """``act(bn(x) [+ residual])`` in training mode with precomputed statistics (see :class:`_BatchNormApply`)."""
-    return _BatchNormApply.apply(x, bn.weight, bn.bias, residual, mean, rstd, coef, relu)
+                     residual: Optional[torch.Tensor] = None, relu: bool = True, fork: bool = False):
+    """``act(bn(x) [+ residual])`` in training mode with precomputed statistics (see :class:`_BatchNormApply`);
+    ``fork``: a pair of outputs (see :func:`batch_norm_act`)."""
+    return _BatchNormApply.apply(x, bn.weight, bn.bias, residual, mean, rstd, coef, relu, bool(fork))
 
 
 def fused_stats_ok(bn: nn.BatchNorm2d) -> bool:
@@ -147,8 +177,24 @@ def _native_ok(x: torch.Tensor, bn: nn.BatchNorm2d, residual: Optional[torch.Ten
     return x.data_ptr() % 16 == 0 and (residual is None or residual.data_ptr() % 16 == 0)
 
 
-def batch_norm_act(x: torch.Tensor, bn: nn.BatchNorm2d, residual: Optional[torch.Tensor] = None, relu: bool = True) -> torch.Tensor:
-    """``act(bn(x) [+ residual])`` for a ``BatchNorm2d`` module, fused on MI355X."""
+def batch_norm_act(x: torch.Tensor, bn: nn.BatchNorm2d, residual: Optional[torch.Tensor] = None, relu: bool = True,
+                   fork: bool = False):
+    """``act(bn(x) [+ residual])`` for a ``BatchNorm2d`` module, fused on MI355X.
+
+    ``fork=True`` returns a pair ``(y, y_alias)`` for an output with two consumers (a
+    residual block's first convolution and its shortcut): on the fused training path
+    the two branches' gradients reach this BN's backward kernels separately and are
+    summed there, so autograd runs no add pass for them.  Elsewhere the pair is
+    ``(y, y)``."""
+    if fork:
+        if _native_ok(x, bn, residual) and (bn.training or not bn.track_running_stats) and bn.momentum is not None:
+            track = bn.training and bn.track_running_stats
+            rm = bn.running_mean if track else None
+            rv = bn.running_var if track else None
+            nbt = bn.num_batches_tracked if track and bn.num_batches_tracked is not None else None
+            return _BatchNormAct.apply(x, bn.weight, bn.bias, residual, rm, rv, nbt, bn.momentum, bn.eps, relu, True)
+        y = batch_norm_act(x, bn, residual, relu)
+        return y, y
     training = bn.training or not bn.track_running_stats
     if not _native_ok(x, bn, residual) or (training and bn.momentum is None):
         y = bn(x)

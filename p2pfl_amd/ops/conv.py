@@ -21,7 +21,7 @@ reference trains its convolutions through torch.nn.Conv2d
 from __future__ import annotations
 
 import os
-from typing import Tuple
+from typing import Optional, Tuple
 
 import torch
 import torch.nn.functional as F
@@ -96,15 +96,17 @@ def mn_splits(M: int, N: int, K: int) -> int:
 _CONV_IN_LAUNCH_MAX_SPLITS = int(os.environ.get("P2PFL_CONV_IN_LAUNCH_SPLITS", "1"))
 
 
-def _run_split(launch, rows: int, cols: int, s: int, out: torch.Tensor, variant: int = 0) -> None:
+def _run_split(launch, rows: int, cols: int, s: int, out: torch.Tensor, variant: int = 0,
+               in_launch: Optional[bool] = None) -> None:
     """``launch(target, splits, ws, counters)`` producing ``out``: directly, split-K reduced
     in the launch, or split-K into fp32 slabs (fragment-native tiles) reduced by one
-    ``tile_slab_reduce`` launch (``variant``: the launch's tile order)."""
+    ``tile_slab_reduce`` launch (``variant``: the launch's tile order; ``in_launch``
+    None: in the launch up to P2PFL_CONV_IN_LAUNCH_SPLITS slices)."""
     if s == 1:
         launch(out, 1, None, None)
         return
     ws = torch.empty(s * slab_elems(rows, cols), dtype=torch.float32, device=out.device)
-    if s <= _CONV_IN_LAUNCH_MAX_SPLITS:
+    if in_launch if in_launch is not None else s <= _CONV_IN_LAUNCH_MAX_SPLITS:
         launch(out, s, ws, counters(tiles_of(rows, cols), out.device))
         return
     launch(ws, s, None, None)
@@ -131,6 +133,23 @@ def _split_options(base: int, K: int, min_k: int = 128) -> Tuple[int, ...]:
     while len(out) < 3 and K // (out[-1] * 2) >= min_k and out[-1] < 64:
         out.append(out[-1] * 2)
     return tuple(out)
+
+
+def _configs(prefix: str, make, default_variant: int, splits) -> dict:
+    """Candidates ``{name: run(dst)}`` of one path: every tuned variant x split-K, and
+    for split-K both reductions -- slabs + tile_slab_reduce (name ``..._s<k>``) and the
+    last-arriving slice in the launch (``..._s<k>_il``).  Untuned: the default variant,
+    the global reduction rule."""
+    pre = f"{prefix}_" if prefix else ""
+    out = {}
+    for v in (_TUNE_VARIANTS if _TUNE else (default_variant,)):
+        for sp in splits:
+            if _TUNE and sp > 1:
+                out[f"{pre}v{v}_s{sp}"] = make(v, sp, False)
+                out[f"{pre}v{v}_s{sp}_il"] = make(v, sp, True)
+            else:
+                out[f"{pre}v{v}_s{sp}"] = make(v, sp)
+    return out
 
 
 def _pick(key, cands, default: str, out: torch.Tensor) -> None:
@@ -178,27 +197,26 @@ def dgrad_into(dy4: torch.Tensor, w4: torch.Tensor, stride: int, pad: int, dil: 
     rows = shape[0] * shape[1] * shape[2]
     K = kh * kw * O
 
-    def gather(v, sp):
+    def gather(v, sp, il=None):
         return lambda dst: _run_split(
             lambda o, s, ws, cnt: C.conv_dgrad(dy4, w4, stride, pad, dil, o, shape, s, v, ws, cnt),
-            rows, shape[3], sp, dst, v)
+            rows, shape[3], sp, dst, v, il)
 
-    def phases(v, sp):
+    def phases(v, sp, il=None):
         def run(dst):
             ph = torch.empty((rows, shape[3]), dtype=torch.bfloat16, device=dx4.device)
             _run_split(lambda o, s, ws, cnt: C.conv_dgrad_s2(dy4, w4, pad, o, shape, s, v, ws, cnt),
-                       rows, shape[3], sp, ph, v)
+                       rows, shape[3], sp, ph, v, il)
             C.phase_interleave(ph, dst, pad, kh, kw)
         return run
 
-    variants = _TUNE_VARIANTS if _TUNE else (_V_DGRAD,)
     base = mn_splits(rows, shape[3], K)
-    cands = {f"gather_v{v}_s{sp}": gather(v, sp) for v in variants for sp in _split_options(base, K)}
+    cands = _configs("gather", gather, _V_DGRAD, _split_options(base, K))
     default = f"gather_v{_V_DGRAD}_s{base}"
     if s2_phases_ok(stride, dil, shape, (kh, kw)):
         kq = ((kh + 1) // 2) * ((kw + 1) // 2) * O  # K of one phase
         pbase = mn_splits(rows, shape[3], kq)
-        cands.update({f"phase_v{v}_s{sp}": phases(v, sp) for v in variants for sp in _split_options(pbase, kq)})
+        cands.update(_configs("phase", phases, _V_DGRAD, _split_options(pbase, kq)))
         default = f"phase_v{_V_DGRAD}_s{pbase}"
         cands.setdefault(default, phases(_V_DGRAD, pbase))
     cands.setdefault(default, gather(_V_DGRAD, base))
@@ -213,12 +231,12 @@ def fwd_into(x4: torch.Tensor, w4: torch.Tensor, stride: int, pad: int, dil: int
     kh, kw, Cin = w4.shape[1], w4.shape[2], w4.shape[3]
     rows, K = N * OH * OW, kh * kw * Cin
 
-    def one(v, sp):
+    def one(v, sp, il=None):
         return lambda dst: _run_split(lambda o, s, ws, cnt: C.conv_fwd(x4, w4, stride, pad, dil, o, s, v, ws, cnt),
-                                      rows, O, sp, dst, v)
+                                      rows, O, sp, dst, v, il)
 
     base = mn_splits(rows, O, K)
-    cands = {f"v{v}_s{sp}": one(v, sp) for v in (_TUNE_VARIANTS if _TUNE else (_V_FWD,)) for sp in _split_options(base, K)}
+    cands = _configs("", one, _V_FWD, _split_options(base, K))
     _pick(("conv_fwd", tuple(x4.shape), O, kh, kw, stride, pad, dil), cands, f"v{_V_FWD}_s{base}", y4)
 
 
@@ -230,13 +248,13 @@ def wgrad_into(dy4: torch.Tensor, x4: torch.Tensor, stride: int, pad: int, dil: 
     npix = dy4.shape[0] * dy4.shape[1] * dy4.shape[2]
     ncols = kh * kw * Cin
 
-    def one(v, sp):
+    def one(v, sp, il=None):
         return lambda dst: _run_split(
-            lambda o, s, ws, cnt: C.conv_wgrad(dy4, x4, kh, kw, stride, pad, dil, o, s, v, ws, cnt), O, ncols, sp, dst, v)
+            lambda o, s, ws, cnt: C.conv_wgrad(dy4, x4, kh, kw, stride, pad, dil, o, s, v, ws, cnt), O, ncols, sp, dst, v, il)
 
     base = wgrad_splits(O, ncols, npix)
     splits = sorted({max(1, base // 2), base} | ({base * 2} if npix // (base * 2) >= 256 else set()))
-    cands = {f"v{v}_s{sp}": one(v, sp) for v in (_TUNE_VARIANTS if _TUNE else (_V_WGRAD,)) for sp in splits}
+    cands = _configs("", one, _V_WGRAD, splits)
     default = f"v{_V_WGRAD}_s{base}"
     if default not in cands:
         cands[default] = one(_V_WGRAD, base)
@@ -466,11 +484,12 @@ def bn_act_conv_bn_stats(st, bn1: nn.BatchNorm2d, relu1: bool, conv: nn.Conv2d, 
                               _sym(conv.padding), _sym(conv.dilation), bn.weight, bn.bias, rm, rv, nbt, bn.eps, bn.momentum)
 
 
-def conv_bn_act(x: torch.Tensor, conv: nn.Conv2d, bn: nn.BatchNorm2d, residual=None, relu: bool = True) -> torch.Tensor:
+def conv_bn_act(x: torch.Tensor, conv: nn.Conv2d, bn: nn.BatchNorm2d, residual=None, relu: bool = True, fork: bool = False):
     """``act(bn(conv(x)) [+ residual])``.  In training, on the native implicit-GEMM
     kernels, the convolution's launch computes the batch statistics (and updates the
     running ones): only the BN apply pass remains a separate launch.  Anything else
-    composes :func:`conv2d` and :func:`~p2pfl_amd.ops.batchnorm.batch_norm_act`."""
+    composes :func:`conv2d` and :func:`~p2pfl_amd.ops.batchnorm.batch_norm_act`.
+    ``fork``: return the pair of :func:`~p2pfl_amd.ops.batchnorm.batch_norm_act`."""
     from p2pfl_amd.ops import batchnorm as bnops
 
     if residual is None or residual.is_contiguous(memory_format=torch.channels_last):
@@ -478,8 +497,8 @@ def conv_bn_act(x: torch.Tensor, conv: nn.Conv2d, bn: nn.BatchNorm2d, residual=N
         if st is not None:
             if residual is not None and residual.shape != st[0].shape:
                 raise ValueError("conv_bn_act: residual shape mismatch")
-            return bnops.batch_norm_apply(st[0], bn, st[1], st[2], st[3], residual, relu)
-    return bnops.batch_norm_act(conv2d(x, conv), bn, residual=residual, relu=relu)
+            return bnops.batch_norm_apply(st[0], bn, st[1], st[2], st[3], residual, relu, fork)
+    return bnops.batch_norm_act(conv2d(x, conv), bn, residual=residual, relu=relu, fork=fork)
 
 
 # 1x1 convolutions (ResNet-50 bottlenecks and downsample shortcuts) run as the

@@ -281,11 +281,14 @@ def test_fused_block_chain_matches_separate_bn_kernels_and_fp32(monkeypatch, blo
     parameter gradient."""
     import copy
 
-    from p2pfl_amd.models.resnet import BasicBlock, Bottleneck
+    from p2pfl_amd.models.resnet import BasicBlock, Bottleneck, _pair
     from p2pfl_amd.ops import conv as conv_ops
 
     ops.ext()
     monkeypatch.setattr(conv_ops, "_POLICY", "native")
+
+    def _blk(m, x):  # blocks return a forked (conv input, shortcut input) pair
+        return _pair(m(x))[0]
     torch.manual_seed(cin + cout + stride)
     blk = (BasicBlock(cin, cout, stride) if block == "basic" else Bottleneck(cin, cout, stride)).cuda().train()
     ref = copy.deepcopy(blk).float()
@@ -297,7 +300,7 @@ def test_fused_block_chain_matches_separate_bn_kernels_and_fp32(monkeypatch, blo
         if isinstance(m, nn.Conv2d):
             m.weight.data = m.weight.data.to(torch.bfloat16).float()
     x0 = _cl(torch.randn(16, cin, hw, hw, device="cuda")).to(torch.bfloat16)
-    dy = _cl(torch.randn(blk(x0.clone()).shape, device="cuda")).to(torch.bfloat16)
+    dy = _cl(torch.randn(_blk(blk, x0.clone()).shape, device="cuda")).to(torch.bfloat16)
     for m in (blk, sep):  # the probe call above advanced blk's running statistics: start both fresh
         for b in m.modules():
             if isinstance(b, nn.BatchNorm2d):
@@ -310,7 +313,7 @@ def test_fused_block_chain_matches_separate_bn_kernels_and_fp32(monkeypatch, blo
         monkeypatch.setattr(conv_ops, "_FUSED_BN", fused)
         x = x0.clone().requires_grad_(True)
         before = conv_ops.STATS["bn_act_conv"]
-        y = model(x)
+        y = _blk(model, x)
         assert (conv_ops.STATS["bn_act_conv"] > before) == fused
         y.backward(dy)
         return x, y
@@ -318,7 +321,7 @@ def test_fused_block_chain_matches_separate_bn_kernels_and_fp32(monkeypatch, blo
     xf, yf = run(blk, True)
     xs, ys = run(sep, False)
     xr = x0.float().requires_grad_(True)
-    yr = ref(xr)
+    yr = _blk(ref, xr)
     yr.backward(dy.float())
 
     def rel(a, e):
@@ -339,3 +342,48 @@ def test_fused_block_chain_matches_separate_bn_kernels_and_fp32(monkeypatch, blo
         # (b) vs fp32: bf16 activations flip a few ReLU masks; a loose sanity bound
         assert rel(a, c) < 0.12, f"{n}: fused vs fp32, relative L2 error {rel(a, c):.3g}"
     torch.testing.assert_close(yf.float(), yr, atol=8e-2, rtol=5e-2)
+
+
+@pytest.mark.parametrize("block", ["basic", "bottleneck"])
+def test_forked_block_inputs_sum_gradients_in_bn_kernels(monkeypatch, block):
+    """Two blocks in a row: the first block's output BN forks (conv input, shortcut input)
+    and the second block's two branch gradients are summed inside that BN's backward
+    kernels (dy2) -- same output and gradients as one output with autograd's add."""
+    import copy
+
+    from p2pfl_amd.models import resnet as rn
+    from p2pfl_amd.ops import batchnorm as bn_ops
+    from p2pfl_amd.ops import conv as conv_ops
+
+    ops.ext()
+    monkeypatch.setattr(conv_ops, "_POLICY", "native")
+    torch.manual_seed(3)
+    mk = (lambda: rn.BasicBlock(64, 64, 1)) if block == "basic" else (lambda: rn.Bottleneck(256, 64, 1))
+    net = nn.Sequential(mk(), mk()).cuda().train()
+    for m in net.modules():
+        if isinstance(m, nn.Conv2d):
+            m.weight.data = m.weight.data.to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    twin = copy.deepcopy(net)
+    cin = 64 if block == "basic" else 256
+    x0 = _cl(torch.randn(8, cin, 16, 16, device="cuda")).to(torch.bfloat16)
+    dy = _cl(torch.randn(8, cin, 16, 16, device="cuda")).to(torch.bfloat16)
+
+    def run(model, fork):
+        monkeypatch.setattr(rn, "_FORK", fork)
+        x = x0.clone().requires_grad_(True)
+        before = bn_ops.STATS["dy_pairs"]
+        y = rn._pair(model(x))[0]
+        y.backward(dy)
+        assert (bn_ops.STATS["dy_pairs"] > before) == fork
+        return x, y
+
+    xf, yf = run(net, True)
+    xu, yu = run(twin, False)
+    torch.testing.assert_close(yf.float(), yu.float(), atol=0, rtol=0)
+
+    def rel(a, e):  # relative norm: the two runs differ only in where the branch sum is rounded to bf16
+        return ((a.float() - e.float()).norm() / (e.float().norm() + 1e-12)).item()
+
+    assert rel(xf.grad, xu.grad) < 1e-2
+    for (n, a), b in zip(net.named_parameters(), twin.parameters()):
+        assert rel(a.grad, b.grad) < 2e-2, (n, rel(a.grad, b.grad))
