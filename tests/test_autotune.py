@@ -48,6 +48,27 @@ def test_conv_split_choices():
     assert wgrad_splits(64, 576, 32768) >= 16
 
 
+def test_conv_tuning_candidates(monkeypatch):
+    """The per-shape conv candidates: every tuned variant x split option, split-K in both
+    reductions; untuned only the default variant with the global reduction rule; the
+    stride-2 by-phase path offered for k > 1 only."""
+    from p2pfl_amd.ops import conv as cv
+
+    seen = []
+    make = lambda v, sp, il=None: seen.append((v, sp, il)) or (v, sp, il)  # noqa: E731
+    monkeypatch.setattr(cv, "_TUNE", True)
+    c = cv._configs("gather", make, 10, (1, 2))
+    assert set(c) == {f"gather_v{v}_s1" for v in cv._TUNE_VARIANTS} | {f"gather_v{v}_s2{il}" for v in cv._TUNE_VARIANTS
+                                                                        for il in ("", "_il")}
+    assert c["gather_v10_s2"] == (10, 2, False) and c["gather_v10_s2_il"] == (10, 2, True) and c["gather_v10_s1"] == (10, 1, None)
+    monkeypatch.setattr(cv, "_TUNE", False)
+    assert cv._configs("", make, 10, (4,)) == {"v10_s4": (10, 4, None)}
+    assert cv._split_options(1, 512) == (1, 2, 4)
+    assert cv._split_options(8, 1152) == (8,)
+    assert cv.s2_phases_ok(2, 1, [32, 32, 32, 64]) and not cv.s2_phases_ok(2, 1, [32, 32, 32, 64], (1, 1))
+    assert not cv.s2_phases_ok(1, 1, [32, 32, 32, 64]) and not cv.s2_phases_ok(2, 1, [2, 9, 9, 64])
+
+
 def test_split_k_counters_of_a_captured_graph_come_from_its_own_ring():
     """Two graphs captured on one pooled stream must never share counter slices
     (concurrent replays would corrupt each other's tile counts); eager launches
