@@ -136,20 +136,12 @@ def _split_options(base: int, K: int, min_k: int = 128) -> Tuple[int, ...]:
 
 
 def _configs(prefix: str, make, default_variant: int, splits) -> dict:
-    """Candidates ``{name: run(dst)}`` of one path: every tuned variant x split-K, and
-    for split-K both reductions -- slabs + tile_slab_reduce (name ``..._s<k>``) and the
-    last-arriving slice in the launch (``..._s<k>_il``).  Untuned: the default variant,
-    the global reduction rule."""
+    """Candidates ``{name: run(dst)}`` of one path: every tuned variant x split-K (untuned:
+    the default variant).  Split-K reduces through slabs + tile_slab_reduce: the in-launch
+    reduction (``_run_split(..., in_launch=True)``) was also offered per shape and never won
+    a ResNet-18 product (``profiles/r5_conv_bench.md``)."""
     pre = f"{prefix}_" if prefix else ""
-    out = {}
-    for v in (_TUNE_VARIANTS if _TUNE else (default_variant,)):
-        for sp in splits:
-            if _TUNE and sp > 1:
-                out[f"{pre}v{v}_s{sp}"] = make(v, sp, False)
-                out[f"{pre}v{v}_s{sp}_il"] = make(v, sp, True)
-            else:
-                out[f"{pre}v{v}_s{sp}"] = make(v, sp)
-    return out
+    return {f"{pre}v{v}_s{sp}": make(v, sp) for v in (_TUNE_VARIANTS if _TUNE else (default_variant,)) for sp in splits}
 
 
 def _pick(key, cands, default: str, out: torch.Tensor) -> None:
@@ -197,16 +189,16 @@ def dgrad_into(dy4: torch.Tensor, w4: torch.Tensor, stride: int, pad: int, dil: 
     rows = shape[0] * shape[1] * shape[2]
     K = kh * kw * O
 
-    def gather(v, sp, il=None):
+    def gather(v, sp):
         return lambda dst: _run_split(
             lambda o, s, ws, cnt: C.conv_dgrad(dy4, w4, stride, pad, dil, o, shape, s, v, ws, cnt),
-            rows, shape[3], sp, dst, v, il)
+            rows, shape[3], sp, dst, v)
 
-    def phases(v, sp, il=None):
+    def phases(v, sp):
         def run(dst):
             ph = torch.empty((rows, shape[3]), dtype=torch.bfloat16, device=dx4.device)
             _run_split(lambda o, s, ws, cnt: C.conv_dgrad_s2(dy4, w4, pad, o, shape, s, v, ws, cnt),
-                       rows, shape[3], sp, ph, v, il)
+                       rows, shape[3], sp, ph, v)
             C.phase_interleave(ph, dst, pad, kh, kw)
         return run
 
@@ -231,9 +223,9 @@ def fwd_into(x4: torch.Tensor, w4: torch.Tensor, stride: int, pad: int, dil: int
     kh, kw, Cin = w4.shape[1], w4.shape[2], w4.shape[3]
     rows, K = N * OH * OW, kh * kw * Cin
 
-    def one(v, sp, il=None):
+    def one(v, sp):
         return lambda dst: _run_split(lambda o, s, ws, cnt: C.conv_fwd(x4, w4, stride, pad, dil, o, s, v, ws, cnt),
-                                      rows, O, sp, dst, v, il)
+                                      rows, O, sp, dst, v)
 
     base = mn_splits(rows, O, K)
     cands = _configs("", one, _V_FWD, _split_options(base, K))
@@ -248,9 +240,9 @@ def wgrad_into(dy4: torch.Tensor, x4: torch.Tensor, stride: int, pad: int, dil: 
     npix = dy4.shape[0] * dy4.shape[1] * dy4.shape[2]
     ncols = kh * kw * Cin
 
-    def one(v, sp, il=None):
+    def one(v, sp):
         return lambda dst: _run_split(
-            lambda o, s, ws, cnt: C.conv_wgrad(dy4, x4, kh, kw, stride, pad, dil, o, s, v, ws, cnt), O, ncols, sp, dst, v, il)
+            lambda o, s, ws, cnt: C.conv_wgrad(dy4, x4, kh, kw, stride, pad, dil, o, s, v, ws, cnt), O, ncols, sp, dst, v)
 
     base = wgrad_splits(O, ncols, npix)
     splits = sorted({max(1, base // 2), base} | ({base * 2} if npix // (base * 2) >= 256 else set()))

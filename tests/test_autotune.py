@@ -49,20 +49,16 @@ def test_conv_split_choices():
 
 
 def test_conv_tuning_candidates(monkeypatch):
-    """The per-shape conv candidates: every tuned variant x split option, split-K in both
-    reductions; untuned only the default variant with the global reduction rule; the
-    stride-2 by-phase path offered for k > 1 only."""
+    """The per-shape conv candidates: every tuned variant x split option; untuned only the
+    default variant; the stride-2 by-phase path offered for k > 1 only."""
     from p2pfl_amd.ops import conv as cv
 
-    seen = []
-    make = lambda v, sp, il=None: seen.append((v, sp, il)) or (v, sp, il)  # noqa: E731
+    make = lambda v, sp: (v, sp)  # noqa: E731
     monkeypatch.setattr(cv, "_TUNE", True)
     c = cv._configs("gather", make, 10, (1, 2))
-    assert set(c) == {f"gather_v{v}_s1" for v in cv._TUNE_VARIANTS} | {f"gather_v{v}_s2{il}" for v in cv._TUNE_VARIANTS
-                                                                        for il in ("", "_il")}
-    assert c["gather_v10_s2"] == (10, 2, False) and c["gather_v10_s2_il"] == (10, 2, True) and c["gather_v10_s1"] == (10, 1, None)
+    assert c == {f"gather_v{v}_s{sp}": (v, sp) for v in cv._TUNE_VARIANTS for sp in (1, 2)}
     monkeypatch.setattr(cv, "_TUNE", False)
-    assert cv._configs("", make, 10, (4,)) == {"v10_s4": (10, 4, None)}
+    assert cv._configs("", make, 10, (4,)) == {"v10_s4": (10, 4)}
     assert cv._split_options(1, 512) == (1, 2, 4)
     assert cv._split_options(8, 1152) == (8,)
     assert cv.s2_phases_ok(2, 1, [32, 32, 32, 64]) and not cv.s2_phases_ok(2, 1, [32, 32, 32, 64], (1, 1))
