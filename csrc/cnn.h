@@ -40,6 +40,10 @@ constexpr int kFeat = 3136;  // 64 * 7 * 7
 constexpr int kHid = 2048;
 constexpr int kCls = 10;
 constexpr int kTaps = 25;
+// FC1 K-splits whose layout the XCDs share (gemm_skinny / route_rm, xcd_align):
+// 49 K-groups of 64 features -> 7 splits of 448 features = 14 routing tiles each
+constexpr int kXcdSplits = 7;
+bool xcd_align();
 
 // Adam hyper-parameters.  The step count t is read from device memory as
 // (*adam_t + t_off): the host sets the base once per epoch and each captured

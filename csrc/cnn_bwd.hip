@@ -257,13 +257,24 @@ __global__ __launch_bounds__(512) void route_rm_kernel(const uint16_t* __restric
                                                        float* __restrict__ m, float* __restrict__ v,
                                                        float* __restrict__ gdump, Offsets off,
                                                        const int* __restrict__ adam_t, int t_off, AdamCfg cfg,
-                                                       float* __restrict__ ws, int* __restrict__ ctr) {
+                                                       float* __restrict__ ws, int* __restrict__ ctr, int xa) {
   constexpr int NB = kRouteBlocks * KS;
-  if (int(blockIdx.x) >= NB) {
-    fc2_role<512>(blockIdx.x - NB, dlogits, H, B, p, m, v, gdump, off, adam_t, t_off, cfg);
+  // xa > 0 (KS = 1): 8 x xa routing blocks, block b on XCD b % 8 takes feature tile
+  // (b % 8) xa + b / 8 -- the tiles of FC1 split b % 8, whose W1 columns the skinny
+  // GEMM's blocks on that XCD just read into its L2 (gemm_skinny_kernel XA)
+  const int nbl = xa ? 8 * xa : NB;
+  if (int(blockIdx.x) >= nbl) {
+    fc2_role<512>(blockIdx.x - nbl, dlogits, H, B, p, m, v, gdump, off, adam_t, t_off, cfg);
     return;
   }
-  const int bid = xcd_local(blockIdx.x, NB);
+  int bid;
+  if (xa) {
+    const int x = blockIdx.x & 7, r = blockIdx.x >> 3;
+    bid = x * xa + r;
+    if (bid >= NB) return;
+  } else {
+    bid = xcd_local(blockIdx.x, NB);
+  }
   const int tile = bid / KS, split = bid % KS;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   static_assert(8 * MT * 1024 * 4 <= kRouteRmLds / KS, "reduction buffer must fit the tile");
@@ -393,11 +404,13 @@ void route_fc2_rm(const uint16_t* dH, const uint16_t* w1, const uint8_t* am2, in
                   float* gdump, Offsets off, const int* adam_t, int t_off, AdamCfg cfg, bool with_fc2,
                   float* ws, int* ctr, hipStream_t s) {
   const int ks = (ws && ctr) ? 2 : 1;
-  const dim3 grid(kRouteBlocks * ks + (with_fc2 ? kFc2Blocks : 0));
+  const int xa = (ks == 1 && xcd_align()) ? kRouteBlocks / kXcdSplits : 0;
+  static_assert(kRouteBlocks % kXcdSplits == 0 && kXcdSplits <= 8, "routing tiles split evenly over the aligned XCDs");
+  const dim3 grid((xa ? 8 * xa : kRouteBlocks * ks) + (with_fc2 ? kFc2Blocks : 0));
   const int lds = kRouteRmLds / ks;
 #define P2_ROUTE(MT, KS)                                                                                            \
   hipLaunchKernelGGL((route_rm_kernel<MT, KS>), grid, dim3(512), lds, s, dH, w1, am2, B, dc2m, gb, dlogits, H, params, \
-                     m, v, gdump, off, adam_t, t_off, cfg, ws, ctr)
+                     m, v, gdump, off, adam_t, t_off, cfg, ws, ctr, xa)
   if (mrows == 32) {
     if (ks == 2) P2_ROUTE(1, 2); else P2_ROUTE(1, 1);
   } else {

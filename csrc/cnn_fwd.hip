@@ -311,13 +311,21 @@ void conv2_fwd(const uint16_t* p1, const uint16_t* w2r, const float* params, Off
 //    operands, so no shuffles are needed.  Waves reduce through LDS; one fp32
 //    slab per split keeps the result deterministic.
 // ---------------------------------------------------------------------------
-template <int MT>
+// XA (XCD-aligned split layout, S <= 8): a 1-D grid of 8 x N/32 blocks; block b
+// runs on XCD b % 8 (round-robin dispatch) and takes K split b % 8, column tile
+// b / 8 (blocks of XCDs >= S exit), so XCD s reads -- through its own L2, plain
+// loads -- exactly the W1 columns of split s: the feature columns the dA1 routing
+// blocks on XCD s read next (route_rm_kernel, same alignment), from that L2
+// instead of from the Infinity Cache.
+template <int MT, bool XA>
 __global__ __launch_bounds__(256) void gemm_skinny_kernel(const uint16_t* __restrict__ A,
                                                           const uint16_t* __restrict__ Bt, float* __restrict__ slabs,
                                                           int N, int K, int S) {
   constexpr int RT = MT < 2 ? MT : 2;  // row tiles reduced per LDS pass (<= 32 KB)
   __shared__ float red[4 * RT * 16 * 64];
-  const int nt = blockIdx.x, sp = blockIdx.y, tid = threadIdx.x;
+  const int nt = XA ? int(blockIdx.x >> 3) : int(blockIdx.x), sp = XA ? int(blockIdx.x & 7) : int(blockIdx.y);
+  if (XA && sp >= S) return;
+  const int tid = threadIdx.x;
   const int wave = tid >> 6, lane = tid & 63, r = lane & 31, h = lane >> 5;
   const int n0 = nt * 32;
   const int ng = K / 64, gps = (ng + S - 1) / S;
@@ -336,7 +344,8 @@ __global__ __launch_bounds__(256) void gemm_skinny_kernel(const uint16_t* __rest
   auto load = [&](int gg, uint4 (&bb)[4], uint4 (&aa)[MT][4]) {
     const int k0 = gg * 64;
 #pragma unroll
-    for (int q = 0; q < 4; ++q) bb[q] = ld_nt16(brow + k0 + q * 8);
+    for (int q = 0; q < 4; ++q)
+      bb[q] = XA ? reinterpret_cast<const uint4*>(brow + k0)[q] : ld_nt16(brow + k0 + q * 8);
 #pragma unroll
     for (int mt = 0; mt < MT; ++mt)
 #pragma unroll
@@ -378,14 +387,30 @@ __global__ __launch_bounds__(256) void gemm_skinny_kernel(const uint16_t* __rest
   }
 }
 
+// P2CNN_XCD_ALIGN=0: the skinny GEMM's (column tile, split) grid and the routing
+// kernel's XCD-local tile runs, without the shared split <-> XCD layout
+bool xcd_align() {
+  static const bool on = [] {
+    const char* e = getenv("P2CNN_XCD_ALIGN");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
+
 void gemm_skinny(const uint16_t* A, const uint16_t* Bt, float* slabs, int mrows, int N, int K, int S, hipStream_t s) {
+#define P2_SKINNY(MT, XA, GRID) hipLaunchKernelGGL((gemm_skinny_kernel<MT, XA>), GRID, dim3(256), 0, s, A, Bt, slabs, N, K, S)
+  if (xcd_align() && S == kXcdSplits && N == kHid && K == kFeat) {
+    const dim3 grid(8 * (N / 32));
+    if (mrows == 32) P2_SKINNY(1, true, grid);
+    else if (mrows == 64) P2_SKINNY(2, true, grid);
+    else P2_SKINNY(4, true, grid);
+    return;
+  }
   const dim3 grid(N / 32, S);
-  if (mrows == 32)
-    hipLaunchKernelGGL(gemm_skinny_kernel<1>, grid, dim3(256), 0, s, A, Bt, slabs, N, K, S);
-  else if (mrows == 64)
-    hipLaunchKernelGGL(gemm_skinny_kernel<2>, grid, dim3(256), 0, s, A, Bt, slabs, N, K, S);
-  else
-    hipLaunchKernelGGL(gemm_skinny_kernel<4>, grid, dim3(256), 0, s, A, Bt, slabs, N, K, S);
+  if (mrows == 32) P2_SKINNY(1, false, grid);
+  else if (mrows == 64) P2_SKINNY(2, false, grid);
+  else P2_SKINNY(4, false, grid);
+#undef P2_SKINNY
 }
 
 // ---------------------------------------------------------------------------
