@@ -63,13 +63,17 @@ class DeviceLoader:
         self.y = self.y.to(device)
         return self
 
-    def permutation(self) -> torch.Tensor:
+    def permutation(self, host: bool = False) -> torch.Tensor:
+        """This epoch's sample order on the data's device, or (``host``) in pinned host
+        memory for the caller to copy straight into its own device buffer."""
         n = len(self.dataset)
         if not self.shuffle:
-            return torch.arange(n, device=self.y.device)
+            return torch.arange(n) if host else torch.arange(n, device=self.y.device)
         g = torch.Generator().manual_seed(self._seed * 100003 + self._epoch)
         self._epoch += 1
         perm = torch.randperm(n, generator=g)
+        if host:
+            return perm.pin_memory() if self.y.device.type == "cuda" else perm
         if self.y.device.type == "cuda":
             # pinned + non-blocking: the host never waits for the GPU's queue
             # to drain just to hand it the next epoch's batch order
