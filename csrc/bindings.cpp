@@ -215,10 +215,15 @@ void sgd_mt_step(torch::Tensor p, c10::optional<torch::Tensor> buf, c10::optiona
 // fixed pool of 32 per device, round robin: two learners (virtual peers) can
 // then share one HIP stream, and an event one records on it while the other
 // captures a graph on it becomes part of that capture (hipErrorCapturedEvent).
-int64_t new_stream(int64_t device) {
+// priority: 0 the default queue priority, > 0 the device's lowest, < 0 its highest
+int64_t new_stream(int64_t device, int64_t priority) {
   const c10::DeviceGuard guard(c10::Device(c10::DeviceType::CUDA, c10::DeviceIndex(device)));
   hipStream_t s = nullptr;
-  const hipError_t e = hipStreamCreateWithFlags(&s, hipStreamNonBlocking);
+  int least = 0, greatest = 0;
+  hipError_t e = hipDeviceGetStreamPriorityRange(&least, &greatest);
+  TORCH_CHECK(e == hipSuccess, "new_stream: ", hipGetErrorString(e));
+  const int prio = priority > 0 ? least : (priority < 0 ? greatest : 0);
+  e = prio == 0 ? hipStreamCreateWithFlags(&s, hipStreamNonBlocking) : hipStreamCreateWithPriority(&s, hipStreamNonBlocking, prio);
   TORCH_CHECK(e == hipSuccess, "new_stream: ", hipGetErrorString(e));
   return reinterpret_cast<int64_t>(s);
 }
@@ -253,7 +258,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         pybind11::arg("grads"), pybind11::arg("numels"), pybind11::arg("grad_bf16"), pybind11::arg("grad_cl"), pybind11::arg("lr"),
         pybind11::arg("momentum"), pybind11::arg("dampening"), pybind11::arg("weight_decay"),
         pybind11::arg("nesterov"), pybind11::arg("first_step"), pybind11::arg("gtab") = pybind11::none());
-  m.def("new_stream", &new_stream, "create a private non-blocking HIP stream on a device (returns its handle)");
+  m.def("new_stream", &new_stream, "create a private non-blocking HIP stream on a device (returns its handle)",
+        pybind11::arg("device"), pybind11::arg("priority") = 0);
   m.def("destroy_stream", &destroy_stream, "destroy a stream made by new_stream");
   register_cnn(m);
   register_fused(m);

@@ -52,6 +52,7 @@ _ROUTE_RM = os.environ.get("P2PFL_CNN_ROUTE_RM", "1") != "0"
 # measured 17.2 us vs 7.5 us unsplit (scripts/kbench.py, MI355X, round 4) -- the
 # cross-CU hand-off costs more than the halved per-workgroup stream saves.
 _ROUTE_SPLIT = os.environ.get("P2PFL_CNN_ROUTE_SPLIT", "0") == "1"
+_EVAL_LOW = os.environ.get("P2PFL_EVAL_STREAM_LOW", "1") != "0"
 _NAMES = ("conv1.weight", "conv1.bias", "conv2.weight", "conv2.bias", "l1.weight", "l1.bias", "l2.weight", "l2.bias")
 FEAT, HID = 3136, 2048
 
@@ -340,7 +341,10 @@ class FusedCNNLearner(TorchLearner):
         # the evaluation passes (validation, test) run on their own stream, on
         # weight snapshots, next to the training that follows them
         self._completions = HostCompletions(self_addr)
-        self._eval_stream = private_stream(self.device)
+        # evaluation passes fill the gaps of the latency-bound training kernels
+        # beside them: lowest queue priority, so the epoch's kernels dispatch first
+        # (P2PFL_EVAL_STREAM_LOW=0: default priority)
+        self._eval_stream = private_stream(self.device, 1 if _EVAL_LOW else 0)
         # completion events of the last RUN_AHEAD fits: the host may enqueue
         # round r + 1 while round r still trains, so the device never idles
         # while the stage machine moves between rounds (with a one-fit bound the

@@ -47,6 +47,9 @@ from p2pfl_amd.utils import finite
 
 # A/B switches (read once): graphs for an epoch's short last batch, and
 # evaluation passes whose metrics are read back by a completion thread
+# queue priority of the learners' compute streams (P2PFL_COMPUTE_STREAM_PRIORITY: -1 highest,
+# 0 default; measurement knob -- the evaluation streams sit at the lowest priority)
+_COMPUTE_PRIORITY = int(os.environ.get("P2PFL_COMPUTE_STREAM_PRIORITY", "0"))
 _TAIL_GRAPHS = os.environ.get("P2PFL_TAIL_GRAPHS", "1") != "0"
 _ASYNC_EVAL = os.environ.get("P2PFL_ASYNC_EVAL", "1") != "0"
 
@@ -172,7 +175,7 @@ class TorchLearner(NodeLearner):
         if not want:
             return None
         if self._compute_stream is None:
-            self._compute_stream = private_stream(self.device)
+            self._compute_stream = private_stream(self.device, _COMPUTE_PRIORITY)
         return self._compute_stream
 
     @contextlib.contextmanager

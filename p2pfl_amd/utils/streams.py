@@ -28,8 +28,11 @@ _STREAMS: list = []
 _LOCK = threading.Lock()
 
 
-def private_stream(device: torch.device) -> torch.cuda.Stream:
-    """A non-blocking HIP stream no other caller is handed (see module doc)."""
+def private_stream(device: torch.device, priority: int = 0) -> torch.cuda.Stream:
+    """A non-blocking HIP stream no other caller is handed (see module doc).
+    ``priority`` > 0: the device's lowest queue priority (work that should fill
+    the gaps of other streams, e.g. evaluation passes beside training), < 0 its
+    highest, 0 the default."""
     from p2pfl_amd.learning.step_graph import GATE
     from p2pfl_amd.ops import ext
 
@@ -37,7 +40,7 @@ def private_stream(device: torch.device) -> torch.cuda.Stream:
     idx = device.index if device.index is not None else torch.cuda.current_device()
     # created under the shared device gate: never while another thread records a graph
     with GATE.shared():
-        handle = int(ext().new_stream(idx))
+        handle = int(ext().new_stream(idx, int(priority)))
     s = torch.cuda.ExternalStream(handle, device=torch.device("cuda", idx))
     with _LOCK:
         _STREAMS.append(s)
