@@ -363,8 +363,13 @@ class FusedCNNLearner(TorchLearner):
             self._arena_changed()
             return  # the arena itself: weights and bf16 shadows are already current
         super().set_parameters(params)
-        with torch.cuda.stream(torch.cuda.current_stream(self.device)):
-            self.engine.pack_shadows()
+
+    def _set_parameters(self, params) -> None:
+        """The copy into the arena and the bf16 shadow refresh, both on the learner's
+        stream inside set_parameters' hand-off (fit() does not wait on the caller's
+        stream, so nothing it reads may be left there)."""
+        super()._set_parameters(params)
+        self.engine.pack_shadows()
 
     # -- plans ----------------------------------------------------------------
     def _plan(self, n: int, B: int) -> List[Tuple[int, int]]:
@@ -463,7 +468,10 @@ class FusedCNNLearner(TorchLearner):
         if self.epochs <= 0 or self.model is None:
             return
         try:
-            with self._on_stream():
+            # the weights a fit reads arrive through set_parameters (its own hand-off):
+            # no wait on the caller's stream, so consecutive epochs do not pay a
+            # cross-queue wake-up round trip between them
+            with self._on_stream(wait_caller=False):
                 self._fit_fused()
         finally:
             self._arena_changed()  # no snapshot taken mid-fit survives it
@@ -588,7 +596,9 @@ class FusedCNNLearner(TorchLearner):
             if on_results is not None:
                 on_results(results)
 
-        with logger.span(self._addr, "evaluate"), self._on_stream():
+        # the weights come from fit() / set_parameters on this learner's stream: no wait
+        # on the caller's stream (a cross-queue wake-up ahead of the next epoch)
+        with logger.span(self._addr, "evaluate"), self._on_stream(wait_caller=False):
             self._eval_async("test", self.data.test_dataloader(), done)
         return True
 
