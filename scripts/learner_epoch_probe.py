@@ -173,15 +173,29 @@ def main() -> None:
             g.graph.replay()
         side.wait_stream(cs)
 
-    from p2pfl_amd.utils.streams import private_stream
-
-    priv = private_stream(dev)
 
     def cs_replay_private_waits():
         with torch.cuda.stream(cs):
             g.graph.replay()
         priv.wait_stream(cs)
 
+    from p2pfl_amd.utils.streams import private_stream
+
+    priv = private_stream(dev)
+    hi = private_stream(dev, -1)
+
+    def hi_replay_legacy_waits():
+        with torch.cuda.stream(hi):
+            g.graph.replay()
+        legacy.wait_stream(hi)
+
+    def hi_replay_private_waits():
+        with torch.cuda.stream(hi):
+            g.graph.replay()
+        priv.wait_stream(hi)
+
+    timed_on(hi, hi_replay_legacy_waits, "HIGH-priority stream: replay + legacy stream waits for it")
+    timed_on(hi, hi_replay_private_waits, "HIGH-priority stream: replay + private stream waits for it")
     timed_on(cs, cs_replay_side_waits, "replay + pooled stream waits for it")
     timed_on(cs, cs_replay_private_waits, "replay + private stream waits for it")
     timed_on(cs, cs_replay, "replay only")
