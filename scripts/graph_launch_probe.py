@@ -99,6 +99,18 @@ def cnn_epoch(steps: int = 94, B: int = 32) -> None:
     print(f"CNN epoch graph ({steps} steps x 7 kernels): hipGraphLaunch host {res['idle']:.0f} us (device idle), "
           f"{res['busy']:.0f} us (device busy), {res['back-to-back']:.0f} us (second of two back-to-back replays); "
           f"device time {a.elapsed_time(b) * 1e3:.0f} us", flush=True)
+    # sustained: 150 replays back to back (about a second of load, as in a benchmark
+    # run), device time per replay over consecutive windows -- clock settling shows here
+    evs = [torch.cuda.Event(enable_timing=True) for _ in range(151)]
+    with torch.cuda.stream(s):
+        evs[0].record(s)
+        for i in range(150):
+            g.replay()
+            evs[i + 1].record(s)
+    torch.cuda.synchronize()
+    per = [evs[i].elapsed_time(evs[i + 1]) * 1e3 for i in range(150)]
+    win = [sum(per[i:i + 30]) / 30 for i in range(0, 150, 30)]
+    print("sustained replays, mean device us per epoch over windows of 30: " + ", ".join(f"{w:.0f}" for w in win), flush=True)
 
 
 if __name__ == "__main__":
