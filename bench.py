@@ -254,6 +254,9 @@ def run_gossip(args, env: _Env) -> dict:
     Settings.GOSSIP_MODELS_PER_ROUND = max(1, N - 1)
     Settings.TTL = 1
     Settings.WIRE_DTYPE = args.wire_dtype
+    if os.environ.get("P2PFL_BENCH_NODE_STREAMS"):  # measurement knob: "0" / "1" / "auto"
+        v = os.environ["P2PFL_BENCH_NODE_STREAMS"]
+        Settings.NODE_STREAMS = v if v == "auto" else v == "1"
     # node addresses are machine-wide bus names: unique per job (self-launched
     # jobs carry P2PFL_JOB_ID, torchrun jobs their rendezvous port)
     job_id = os.environ.get("P2PFL_JOB_ID") or f"tr{os.environ.get('MASTER_PORT', '0')}-{os.getppid()}"

@@ -53,10 +53,13 @@ _ROUTE_RM = os.environ.get("P2PFL_CNN_ROUTE_RM", "1") != "0"
 # cross-CU hand-off costs more than the halved per-workgroup stream saves.
 _ROUTE_SPLIT = os.environ.get("P2PFL_CNN_ROUTE_SPLIT", "0") == "1"
 _EVAL_LOW = os.environ.get("P2PFL_EVAL_STREAM_LOW", "1") != "0"
-# evaluation passes on their own stream beside the next training (1) or in line
-# on the learner's stream (0: measured 7.35-7.43 vs 7.28 ms/round, the epoch
-# 0.2 ms shorter but 0.3 ms of passes between two epochs; bench.py spans)
-_EVAL_SIDE = os.environ.get("P2PFL_EVAL_SIDE_STREAM", "1") != "0"
+# evaluation passes on their own stream beside the next training ("1") or in line
+# on the learner's stream ("0"); "auto" (default): beside it only when the learner
+# trains on a stream of its own (NODE_STREAMS) -- a lone trainer on the caller's
+# stream runs them in line, as the stream hand-offs cost more than the overlap
+# saves (1-peer round: in line 6.65 vs 7.23 ms; with node streams the side stream
+# wins, 7.28 vs 7.35-7.43 ms; profiles/r5_handoff_probe.md)
+_EVAL_SIDE = os.environ.get("P2PFL_EVAL_SIDE_STREAM", "auto")
 _NAMES = ("conv1.weight", "conv1.bias", "conv2.weight", "conv2.bias", "l1.weight", "l1.bias", "l2.weight", "l2.bias")
 FEAT, HID = 3136, 2048
 
@@ -550,7 +553,8 @@ class FusedCNNLearner(TorchLearner):
         self._ensure_graph(name, loader, False)  # first-use capture outside the lock
         snap = self._eval_fwd.snapshot(name)
         cur = torch.cuda.current_stream(self.device)
-        es = self._eval_stream if _EVAL_SIDE else cur
+        side = self._stream_for_block() is not None if _EVAL_SIDE == "auto" else _EVAL_SIDE != "0"
+        es = self._eval_stream if side else cur
         with self._lock:
             if snap.done is not None:
                 cur.wait_event(snap.done)  # the previous pass on this copy finished reading it

@@ -30,6 +30,7 @@ import os
 import contextlib
 import threading
 import time
+import weakref
 from collections import OrderedDict
 from typing import Any, Dict, Mapping, Optional, Tuple
 
@@ -50,6 +51,8 @@ from p2pfl_amd.utils import finite
 # queue priority of the learners' compute streams (P2PFL_COMPUTE_STREAM_PRIORITY: -1 highest,
 # 0 default; measurement knob -- the evaluation streams sit at the lowest priority)
 _COMPUTE_PRIORITY = int(os.environ.get("P2PFL_COMPUTE_STREAM_PRIORITY", "0"))
+# live GPU learners of this process (virtual peers share the device: NODE_STREAMS "auto")
+_GPU_LEARNERS: "weakref.WeakSet" = weakref.WeakSet()
 _TAIL_GRAPHS = os.environ.get("P2PFL_TAIL_GRAPHS", "1") != "0"
 _ASYNC_EVAL = os.environ.get("P2PFL_ASYNC_EVAL", "1") != "0"
 
@@ -110,6 +113,8 @@ class TorchLearner(NodeLearner):
         # one process train concurrently, and their training overlaps the
         # aggregation / transport work left on the default stream
         self._compute_stream: Optional[torch.cuda.Stream] = None
+        if self.device.type == "cuda":
+            _GPU_LEARNERS.add(self)
         self._step_graph: Any = None
         self._tail_graphs: Dict[int, Any] = {}  # short last batch of an epoch, by size
         self._eval_graphs: Dict[str, Any] = {}
@@ -167,11 +172,19 @@ class TorchLearner(NodeLearner):
         return self.arena.params
 
     def _stream_for_block(self) -> Optional[torch.cuda.Stream]:
-        """This learner's compute stream if ``Settings.NODE_STREAMS`` wants one now."""
+        """This learner's compute stream if ``Settings.NODE_STREAMS`` wants one now.
+
+        ``"auto"``: when there is something to overlap -- other trainers in the round
+        (``Settings.TRAIN_SET_SIZE > 1``: arriving models to fold, gossip to push) or
+        other learners in this process (virtual peers).  A lone trainer runs on the
+        caller's stream: every hand-off between two streams on different hardware
+        queues costs the next epoch ~0.55 ms of device time
+        (``profiles/r5_handoff_probe.md``), with nothing to gain (1-peer MNIST round
+        7.23 -> 6.65 ms)."""
         if self.device.type != "cuda":
             return None
         mode = Settings.NODE_STREAMS
-        want = True if mode == "auto" else bool(mode)
+        want = (Settings.TRAIN_SET_SIZE > 1 or len(_GPU_LEARNERS) > 1) if mode == "auto" else bool(mode)
         if not want:
             return None
         if self._compute_stream is None:
