@@ -367,13 +367,6 @@ class FusedCNNLearner(TorchLearner):
             return  # the arena itself: weights and bf16 shadows are already current
         super().set_parameters(params)
 
-    def _auto_stream(self) -> bool:
-        """NODE_STREAMS "auto": a stream of its own unless this is a lone trainer.  Every
-        hand-off between two streams on different hardware queues costs the next epoch
-        ~0.55 ms of device time (``profiles/r5_handoff_probe.md``); alone, there is
-        nothing to overlap (1-peer MNIST round 7.23 -> 6.64-6.67 ms)."""
-        return not self._lone_trainer()
-
     def _set_parameters(self, params) -> None:
         """The copy into the arena and the bf16 shadow refresh, both on the learner's
         stream inside set_parameters' hand-off (fit() does not wait on the caller's

@@ -174,25 +174,22 @@ class TorchLearner(NodeLearner):
     def _stream_for_block(self) -> Optional[torch.cuda.Stream]:
         """This learner's compute stream if ``Settings.NODE_STREAMS`` wants one now.
 
-        ``"auto"``: :meth:`_auto_stream`."""
+        ``"auto"``: when there is something to overlap -- other trainers in the round
+        (``Settings.TRAIN_SET_SIZE > 1``: arriving models to fold, gossip to push) or
+        other learners in this process (virtual peers).  A lone trainer runs on the
+        caller's stream: every hand-off between two streams on different hardware
+        queues costs the next epoch ~0.55 ms of device time
+        (``profiles/r5_handoff_probe.md``), with nothing to gain (1-peer MNIST round
+        7.23 -> 6.65 ms)."""
         if self.device.type != "cuda":
             return None
         mode = Settings.NODE_STREAMS
-        want = self._auto_stream() if mode == "auto" else bool(mode)
+        want = (Settings.TRAIN_SET_SIZE > 1 or len(_GPU_LEARNERS) > 1) if mode == "auto" else bool(mode)
         if not want:
             return None
         if self._compute_stream is None:
             self._compute_stream = private_stream(self.device, _COMPUTE_PRIORITY)
         return self._compute_stream
-
-    def _auto_stream(self) -> bool:
-        """NODE_STREAMS "auto": every GPU learner trains on a stream of its own."""
-        return True
-
-    def _lone_trainer(self) -> bool:
-        """No other trainer in the round (``Settings.TRAIN_SET_SIZE == 1``) and no other
-        learner in this process: nothing a private stream could overlap."""
-        return Settings.TRAIN_SET_SIZE <= 1 and len(_GPU_LEARNERS) <= 1
 
     @contextlib.contextmanager
     def _on_stream(self, hold_gate: bool = False, wait_caller: bool = True):
