@@ -45,7 +45,19 @@ void gemm(torch::Tensor a, torch::Tensor b, bool a_kmajor, bool b_kmajor, torch:
   TORCH_CHECK(a_kmajor || M % 8 == 0, "gemm: an m-major A needs M % 8 == 0");
   TORCH_CHECK(M < (int64_t(1) << 31) && N < (int64_t(1) << 31) && K < (int64_t(1) << 31), "gemm: size overflow");
   TORCH_CHECK(a.device() == b.device() && out.device() == a.device(), "gemm: device mismatch");
-  TORCH_CHECK(splits >= 1 && splits <= 64, "gemm: 1 <= splits <= 64");
+  // stream-K schedule of the ping-pong kernel (variant bits 11 + 17): `splits` is its grid size
+  const bool sk = (variant & 2048) && (variant & (1 << 17));
+  const int64_t sk_iters = ((M + 255) / 256) * ((N + 255) / 256) * ((K + 63) / 64);
+  if (variant & 2048) {
+    TORCH_CHECK(!((variant & (1 << 21)) && (splits > 1 || sk)), "gemm: the 256 x 128 ping-pong tile takes no split-K / stream-K");
+  }
+  if (sk) {
+    TORCH_CHECK(splits >= 1 && splits <= sk_iters && splits <= 4096,
+                "gemm: stream-K grid must be 1..min(4096, tiles x K-tiles = ", sk_iters, ")");
+    TORCH_CHECK(counters.has_value() && counters->defined(), "gemm: stream-K needs counters and a workspace");
+  } else {
+    TORCH_CHECK(splits >= 1 && splits <= 64, "gemm: 1 <= splits <= 64");
+  }
   p2::GemmParams p{};
   p.a = reinterpret_cast<const uint16_t*>(a.data_ptr());
   p.b = reinterpret_cast<const uint16_t*>(b.data_ptr());
@@ -60,19 +72,21 @@ void gemm(torch::Tensor a, torch::Tensor b, bool a_kmajor, bool b_kmajor, torch:
   p.variant = int(variant);
   const bool in_launch = counters.has_value() && counters->defined();
   if (in_launch) {  // split-K reduced inside the launch: slabs in ws, epilogue into out
-    TORCH_CHECK(splits > 1, "gemm: counters only with splits > 1");
+    TORCH_CHECK(splits > 1 || sk, "gemm: counters only with splits > 1 or stream-K");
     const int64_t tiles = ((M + 127) / 128) * ((N + 127) / 128);
     TORCH_CHECK(counters->is_cuda() && counters->scalar_type() == torch::kInt32 && counters->is_contiguous() &&
                     counters->numel() >= tiles && counters->device() == a.device(),
                 "gemm: counters must be a contiguous int32 GPU tensor with one entry per 128x128 tile");
+    // stream-K: two 256 x 256 fp32 slabs per workgroup (its first and last tile)
+    const int64_t ws_need = sk ? 2 * splits * 65536 : splits * slab_elems(M, N, variant);
     TORCH_CHECK(ws.has_value() && ws->defined() && ws->is_cuda() && ws->scalar_type() == torch::kFloat32 &&
-                    ws->is_contiguous() && ws->numel() >= splits * slab_elems(M, N, variant) && ws->device() == a.device() &&
+                    ws->is_contiguous() && ws->numel() >= ws_need && ws->device() == a.device() &&
                     reinterpret_cast<uintptr_t>(ws->data_ptr()) % 16 == 0,
                 "gemm: split-K workspace must be contiguous fp32 with splits * slab_elems(M, N) elements");
     p.ws = ws->data_ptr<float>();
     p.counters = counters->data_ptr<int>();
   }
-  if (splits > 1 && !in_launch) {
+  if (splits > 1 && !in_launch && !sk) {
     TORCH_CHECK(out.scalar_type() == torch::kFloat32 && out.is_contiguous() && out.numel() >= splits * slab_elems(M, N, variant),
                 "gemm: split-K output must be contiguous fp32 with splits * slab_elems(M, N) elements (reduce with tile_slab_reduce)");
     TORCH_CHECK(!bias.has_value() && !gelu && !residual.has_value(), "gemm: no epilogue with split-K");

@@ -161,7 +161,12 @@ struct ClStage {
   float g[kMTClPad];
   uint16_t sh[kMTMaxCL];
 };
-P2_DEVICE bool cl_staged(uint32_t C, uint32_t HW, int64_t len) { return HW > 1 && C % 4 == 0 && len <= kMTMaxCL; }
+// Staged only when the chunk is whole slabs: ops.optim's layout gives whole-slab chunks
+// only to tensors whose slab C x HW fits kMTMaxCL; a larger slab is cut into plain
+// chunks that start mid-slab, which the slab-local permutation cannot map (gather path).
+P2_DEVICE bool cl_staged(uint32_t C, uint32_t HW, int64_t len) {
+  return HW > 1 && C % 4 == 0 && len <= kMTMaxCL && C * HW <= uint32_t(kMTMaxCL);
+}
 // LDS word of channels-last element j (one pad word per I-run of C elements)
 P2_DEVICE uint32_t cl_pad(uint32_t j, const FastDivU& fc) { return j + fdivu(j, fc); }
 P2_DEVICE void cl_load_grad(ClStage& st, const void* g, bool gbf, int64_t first, int len, const FastDivU& fc) {

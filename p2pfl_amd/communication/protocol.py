@@ -149,6 +149,10 @@ class BaseCommunicationProtocol(CommunicationProtocol):
     def get_neighbors(self, only_direct: bool = False) -> Dict[str, Any]:
         return self._neighbors.get_all(only_direct)
 
+    def experiment_boundary(self) -> None:
+        """Hook called when an experiment starts or ends on this node (transports
+        that keep per-experiment state reset it here)."""
+
     def add_neighbor_listener(self, fn: Callable[[], None]) -> None:
         self._neighbors.add_listener(fn)
 

@@ -297,8 +297,11 @@ class XgmiCommunicationProtocol(BaseCommunicationProtocol):
         self._departed: set = set()
         self._inbound: set = set()
         # keys of models already received (an identical proposal arriving
-        # between the transfer and the handler's bookkeeping is declined)
+        # between the transfer and the handler's bookkeeping is declined).  Keys
+        # carry the experiment generation: a second experiment on the same node
+        # restarts at round 0 with the same (round, command, contributors).
         self._received: set = set()
+        self._exp_gen = 0
 
     def _resolve_address(self, addr: str) -> str:
         if addr in (None, "", "127.0.0.1"):
@@ -330,6 +333,14 @@ class XgmiCommunicationProtocol(BaseCommunicationProtocol):
     @property
     def supports_device_payloads(self) -> bool:
         return True
+
+    def experiment_boundary(self) -> None:
+        """An experiment starts or ends on this node: forget the dedupe keys of the
+        previous one (transfers still in flight finish under their old generation)."""
+        with self._req_lock:
+            self._exp_gen += 1
+            self._received = set()
+            self._inbound = set()
 
     # -- request / reply (handshake) ---------------------------------------
     def request(self, dst: str, kind: str, args: List[Any], timeout: float) -> Optional[str]:
@@ -442,8 +453,9 @@ class XgmiCommunicationProtocol(BaseCommunicationProtocol):
         # another peer (an init model or a full aggregate offered by several
         # neighbours at once; equal contributors = the same average): one
         # transfer is enough
-        key = (rnd, cmd_name, tuple(sorted(contributors)))
         with self._req_lock:
+            gen = self._exp_gen
+            key = (gen, rnd, cmd_name, tuple(sorted(contributors)))
             if key in self._inbound:
                 return nack("already in flight", False)
             if key in self._received:
@@ -460,8 +472,8 @@ class XgmiCommunicationProtocol(BaseCommunicationProtocol):
             with self._req_lock:
                 self._inbound.discard(key)
                 if buf is not None:
-                    if len(self._received) > 4096:  # keep the recent rounds only
-                        self._received = {k for k in self._received if k[0] >= rnd - 2}
+                    if len(self._received) > 4096:  # keep this experiment's recent rounds only
+                        self._received = {k for k in self._received if k[0] == self._exp_gen and k[1] >= rnd - 2}
                     self._received.add(key)
             if buf is None:
                 return

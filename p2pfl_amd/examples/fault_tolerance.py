@@ -107,6 +107,7 @@ def main(argv=None) -> None:
         try:
             check_equal_models(survivors)
         except AssertionError as e:
+            torch.cuda.synchronize()  # every learner's stream (diagnostics only)
             ref = survivors[0].state.learner.get_parameters().flat
             for s_ in survivors:
                 d = float((s_.state.learner.get_parameters().flat - ref).abs().max())

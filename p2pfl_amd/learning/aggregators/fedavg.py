@@ -10,6 +10,7 @@ grid sized for HBM3E bandwidth.  On CPU tensors the same math runs in torch.
 
 from __future__ import annotations
 
+import contextlib
 from dataclasses import dataclass, field
 from typing import Any, Dict, List, Optional, Tuple
 
@@ -17,7 +18,7 @@ import torch
 
 from p2pfl_amd import ops
 from p2pfl_amd.learning.aggregators.aggregator import Aggregator, NoModelsToAggregateError
-from p2pfl_amd.learning.arena import FlatParams, flatten
+from p2pfl_amd.learning.arena import FlatParams, flatten, reading
 from p2pfl_amd.management.logger import logger
 from p2pfl_amd.utils import finite
 
@@ -32,6 +33,14 @@ class _RunningSum:
     keys: List[str] = field(default_factory=list)
     entries: List[Any] = field(default_factory=list)  # the (model, weight) tuples folded, by identity
     weights: List[float] = field(default_factory=list)
+
+
+def _reading_all(flats: List[FlatParams]) -> contextlib.ExitStack:
+    """``arena.reading`` of every input (the WeightGuard hand-off of live learner weights)."""
+    st = contextlib.ExitStack()
+    for f in flats:
+        st.enter_context(reading(f))
+    return st
 
 
 def _used_here(t: torch.Tensor) -> None:
@@ -107,7 +116,7 @@ class FedAvg(Aggregator):
             return
         w = [float(x) for _, x in entries]
         acc = torch.empty(flats[0].flat.numel(), dtype=torch.float32, device=device)
-        with logger.span(self.node_name, "fold_models", k=len(fold)):
+        with logger.span(self.node_name, "fold_models", k=len(fold)), _reading_all(flats):
             if base is not None:
                 _used_here(base.acc)
             ops.weighted_sum_into(acc, [f.flat for f in flats], w, acc_in=base.acc if base is not None else None)
@@ -149,7 +158,8 @@ class FedAvg(Aggregator):
             if not f.layout.compatible(layout):
                 raise ValueError("Cannot average models with different layouts")
         out = torch.empty(flats[0].flat.numel() if flats else acc.numel(), dtype=torch.float32, device=device)
-        ops.weighted_sum_into(out, [f.flat for f in flats], w[start:], acc_in=acc, scale=scale)
+        with _reading_all(flats):  # a learner's live weights: after its last write, before its next
+            ops.weighted_sum_into(out, [f.flat for f in flats], w[start:], acc_in=acc, scale=scale)
         if finite.ENABLED:
             for k, f in zip(keys[start:], flats):
                 finite.check(self.node_name, "FedAvg input", f, key=k)

@@ -21,7 +21,7 @@ from __future__ import annotations
 
 from collections import OrderedDict
 from dataclasses import dataclass
-from typing import Dict, Iterable, Mapping, Optional, Tuple
+from typing import Any, Dict, Iterable, Mapping, Optional, Tuple
 
 import torch
 
@@ -110,12 +110,126 @@ class FlatParams(OrderedDict):
         return self.flat.device
 
     def clone(self) -> "FlatParams":  # type: ignore[override]
-        return FlatParams.from_flat(self.flat.clone(), self.layout)
+        with reading(self):  # a learner's live weights: after its last write (WeightGuard)
+            return FlatParams.from_flat(self.flat.clone(), self.layout)
 
     def to(self, device: torch.device, non_blocking: bool = False) -> "FlatParams":
         if self.flat.device == torch.device(device):
             return self
-        return FlatParams.from_flat(self.flat.to(device, non_blocking=non_blocking), self.layout)
+        with reading(self):
+            return FlatParams.from_flat(self.flat.to(device, non_blocking=non_blocking), self.layout)
+
+
+class WeightGuard:
+    """Lazy stream ordering of one learner's live weights (the arena) across HIP streams.
+
+    The learner writes its weights on its own compute stream (``fit``,
+    ``set_parameters``); other threads read them on theirs (the FedAvg fold, the
+    gossip snapshot, wire encoding, checkpoints).  Instead of handing the whole
+    compute stream back to the caller's stream after every block -- a cross-queue
+    wait that cost the next epoch ~0.55 ms of device time per round
+    (``profiles/r5_handoff_probe.md``) -- each write block records a ready event,
+    and each reader waits on it only where it launches a read (RAW); readers record
+    an event after their reads, which the next write block waits on (WAR).  A
+    block whose predecessor ran on the same stream waits on nothing: a lone
+    trainer pays no hand-off at all.  Replaces the reference's synchronous
+    ``learner.get_parameters()`` after ``fit`` (``train_stage.py:70-74``,
+    ``lightning_learner.py:180-198``), where Lightning finished the epoch on the host.
+    """
+
+    def __init__(self) -> None:
+        import threading
+
+        self._lock = threading.Lock()
+        self._ready: Optional[Tuple[Any, Any]] = None  # (event, stream) after the last write block
+        self._reads: Dict[Any, Any] = {}  # stream -> event after the latest reads on it since then
+        self._handed: Dict[Any, None] = {}  # streams the weights were handed to with no read event
+
+    @staticmethod
+    def _gated():
+        from p2pfl_amd.learning.step_graph import GATE
+
+        return GATE.shared()  # event record / wait on the default stream: never beside a capture
+
+    def acquire(self, stream: Any) -> None:
+        """Order work about to be launched on ``stream`` after the last write of the weights."""
+        if stream is None:
+            return
+        with self._lock:
+            r = self._ready
+        if r is not None and r[1] != stream:
+            with self._gated():
+                stream.wait_event(r[0])
+
+    def release(self, stream: Any) -> None:
+        """Reads of the weights were launched on ``stream``: the next write waits for them."""
+        if stream is None:
+            return
+        with self._gated():
+            ev = torch.cuda.Event()
+            ev.record(stream)
+        with self._lock:
+            self._reads[stream] = ev
+
+    def hand_out(self, stream: Any) -> None:
+        """The weights were given to code that may read them on ``stream`` without
+        recording when it is done (a public ``get_parameters()``): the stream waits
+        for the last write now, and the next write waits for everything queued on
+        it until then."""
+        if stream is None:
+            return
+        self.acquire(stream)
+        with self._lock:
+            self._handed[stream] = None
+
+    def begin_write(self, stream: Any) -> None:
+        """A write block starts on ``stream``: after every read and the previous write
+        launched on other streams."""
+        if stream is None:
+            return
+        with self._lock:
+            waits = [ev for s, ev in self._reads.items() if s != stream]
+            handed = [s for s in self._handed if s != stream]
+            self._reads = {}
+            self._handed = {}
+            r = self._ready
+        if r is not None and r[1] != stream:
+            waits.append(r[0])
+        if waits or handed:
+            with self._gated():
+                for ev in waits:
+                    stream.wait_event(ev)
+                for s in handed:
+                    stream.wait_stream(s)
+
+    def end_write(self, stream: Any) -> None:
+        if stream is None:
+            return
+        with self._gated():
+            ev = torch.cuda.Event()
+            ev.record(stream)
+        with self._lock:
+            self._ready = (ev, stream)
+
+
+class reading:
+    """``with reading(params): <launch reads of params.flat on the current stream>`` --
+    the :class:`WeightGuard` hand-off for a learner's live weights (a no-op for any
+    other FlatParams and on the CPU)."""
+
+    def __init__(self, params: Any) -> None:
+        self.guard = getattr(params, "guard", None)
+        flat = getattr(params, "flat", None)
+        self.stream = torch.cuda.current_stream(flat.device) if (self.guard is not None and flat is not None and flat.is_cuda) else None
+
+    def __enter__(self) -> "reading":
+        if self.stream is not None:
+            self.guard.acquire(self.stream)
+        return self
+
+    def __exit__(self, *exc) -> None:
+        if self.stream is not None:
+            self.guard.release(self.stream)
 
 
 def flatten(params: Mapping[str, torch.Tensor], device: Optional[torch.device] = None) -> FlatParams:
@@ -164,6 +278,7 @@ class ModuleArena:
         self.layout = ParamLayout.from_tensors((k, v) for k, v in sd.items())
         flat = torch.zeros(self.layout.numel, dtype=torch.float32, device=device)
         self.params = FlatParams.from_flat(flat, self.layout)
+        self.params.guard = WeightGuard()  # stream ordering of the live weights (learner hand-offs)
         self._int_buffers: Dict[str, torch.Tensor] = {}
         for name, t in sd.items():
             view = self.params[name]

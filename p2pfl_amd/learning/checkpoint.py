@@ -43,7 +43,10 @@ def save_checkpoint(
 ) -> str:
     """Write ``params`` (a :class:`FlatParams` or any name->tensor mapping) to ``path``."""
     fp = params if isinstance(params, FlatParams) else flatten(params)
-    tensors = {"arena": fp.flat.detach().to("cpu", torch.float32).contiguous()}
+    from p2pfl_amd.learning.arena import reading
+
+    with reading(fp):  # a learner's live weights: after its last write (WeightGuard)
+        tensors = {"arena": fp.flat.detach().to("cpu", torch.float32).contiguous()}
     for k, v in (extra or {}).items():
         if k == "arena":
             raise ValueError("'arena' is reserved")

@@ -54,12 +54,10 @@ _ROUTE_RM = os.environ.get("P2PFL_CNN_ROUTE_RM", "1") != "0"
 _ROUTE_SPLIT = os.environ.get("P2PFL_CNN_ROUTE_SPLIT", "0") == "1"
 _EVAL_LOW = os.environ.get("P2PFL_EVAL_STREAM_LOW", "1") != "0"
 # evaluation passes on their own stream beside the next training ("1") or in line
-# on the learner's stream ("0"); "auto" (default): beside it only when the learner
-# trains on a stream of its own (NODE_STREAMS) -- a lone trainer on the caller's
-# stream runs them in line, as the stream hand-offs cost more than the overlap
-# saves (1-peer round: in line 6.65 vs 7.23 ms; with node streams the side stream
-# wins, 7.28 vs 7.35-7.43 ms; profiles/r5_handoff_probe.md)
-_EVAL_SIDE = os.environ.get("P2PFL_EVAL_SIDE_STREAM", "auto")
+# on the learner's stream ("0", default; "auto": beside it when the learner has a
+# stream of its own).  In line: no stream hand-offs between the epoch and its
+# validation pass (1-peer round: in line 6.65 vs 7.23 ms, profiles/r5_handoff_probe.md).
+_EVAL_SIDE = os.environ.get("P2PFL_EVAL_SIDE_STREAM", "0")
 _NAMES = ("conv1.weight", "conv1.bias", "conv2.weight", "conv2.bias", "l1.weight", "l1.bias", "l2.weight", "l2.bias")
 FEAT, HID = 3136, 2048
 
@@ -386,8 +384,9 @@ class FusedCNNLearner(TorchLearner):
     def _ensure_graph(self, name: str, loader, train: bool) -> "_EpochGraph":
         """The captured pass for ``loader`` (capturing it on first use).  Called
         WITHOUT ``self._lock``: waiting for the exclusive device gate can take as
-        long as another peer's warm-up, and the capture saves / restores the state
-        it touches inside the exclusive section, so no other enqueue can see it."""
+        long as another peer's warm-up.  Recording a capture executes nothing, so
+        the state the graph mutates (weights, Adam moments, step counter) is left
+        untouched -- nothing to save or restore (see ``_capture``)."""
         from p2pfl_amd.learning.step_graph import GATE
 
         plan, key = self._graph_key(name, loader, train)
@@ -471,10 +470,10 @@ class FusedCNNLearner(TorchLearner):
         if self.epochs <= 0 or self.model is None:
             return
         try:
-            # the weights a fit reads arrive through set_parameters (its own hand-off):
-            # no wait on the caller's stream, so consecutive epochs do not pay a
-            # cross-queue wake-up round trip between them
-            with self._on_stream(wait_caller=False):
+            # the weights a fit reads arrive through set_parameters (its own hand-off);
+            # the fit waits only for reads of the weights launched on other streams
+            # since then (WeightGuard), so consecutive epochs pay no cross-queue wake-up
+            with self._on_stream():
                 self._fit_fused()
         finally:
             self._arena_changed()  # no snapshot taken mid-fit survives it
@@ -602,7 +601,7 @@ class FusedCNNLearner(TorchLearner):
 
         # the weights come from fit() / set_parameters on this learner's stream: no wait
         # on the caller's stream (a cross-queue wake-up ahead of the next epoch)
-        with logger.span(self._addr, "evaluate"), self._on_stream(wait_caller=False):
+        with logger.span(self._addr, "evaluate"), self._on_stream(writes=False):
             self._eval_async("test", self.data.test_dataloader(), done)
         return True
 

@@ -30,7 +30,6 @@ import os
 import contextlib
 import threading
 import time
-import weakref
 from collections import OrderedDict
 from typing import Any, Dict, Mapping, Optional, Tuple
 
@@ -46,13 +45,11 @@ from p2pfl_amd.utils.streams import private_stream
 from p2pfl_amd.settings import Settings
 from p2pfl_amd.utils import finite
 
-# A/B switches (read once): graphs for an epoch's short last batch, and
-# evaluation passes whose metrics are read back by a completion thread
 # queue priority of the learners' compute streams (P2PFL_COMPUTE_STREAM_PRIORITY: -1 highest,
 # 0 default; measurement knob -- the evaluation streams sit at the lowest priority)
 _COMPUTE_PRIORITY = int(os.environ.get("P2PFL_COMPUTE_STREAM_PRIORITY", "0"))
-# live GPU learners of this process (virtual peers share the device: NODE_STREAMS "auto")
-_GPU_LEARNERS: "weakref.WeakSet" = weakref.WeakSet()
+# A/B switches (read once): graphs for an epoch's short last batch, and
+# evaluation passes whose metrics are read back by a completion thread
 _TAIL_GRAPHS = os.environ.get("P2PFL_TAIL_GRAPHS", "1") != "0"
 _ASYNC_EVAL = os.environ.get("P2PFL_ASYNC_EVAL", "1") != "0"
 
@@ -113,8 +110,6 @@ class TorchLearner(NodeLearner):
         # one process train concurrently, and their training overlaps the
         # aggregation / transport work left on the default stream
         self._compute_stream: Optional[torch.cuda.Stream] = None
-        if self.device.type == "cuda":
-            _GPU_LEARNERS.add(self)
         self._step_graph: Any = None
         self._tail_graphs: Dict[int, Any] = {}  # short last batch of an epoch, by size
         self._eval_graphs: Dict[str, Any] = {}
@@ -165,77 +160,98 @@ class TorchLearner(NodeLearner):
     # parameters
     # ------------------------------------------------------------------
     def get_parameters(self) -> FlatParams:
+        """The live weights (no copy), safe to read on the caller's current stream:
+        it waits for the learner's last write, and the learner's next write waits
+        for what the caller queued on it meanwhile (WeightGuard ``hand_out``)."""
+        params = self.live_parameters()
+        guard = self._guard()
+        if guard is not None and self.device.type == "cuda":
+            guard.hand_out(torch.cuda.current_stream(self.device))
+        return params
+
+    def live_parameters(self) -> FlatParams:
+        """The live weights with no stream ordering: the framework's own consumers
+        (FedAvg, gossip snapshots, encoding) launch their reads under
+        ``arena.reading(params)``, which orders exactly those reads (the
+        :class:`~p2pfl_amd.learning.arena.WeightGuard` the arena carries) -- a
+        lone trainer's round then pays no cross-queue wait."""
         assert self.arena is not None
         if self.arena._int_buffers:
-            with self._gate():  # integer-buffer mirror copies (BatchNorm counters)
+            # integer-buffer mirror copies (BatchNorm counters): a write of the
+            # arena on the caller's stream, after the learner's last block
+            guard = self._guard()
+            cur = torch.cuda.current_stream(self.device) if self.device.type == "cuda" else None
+            with self._gate():
+                if guard is not None:
+                    guard.begin_write(cur)
                 self.arena.sync_in()
+                if guard is not None:
+                    guard.end_write(cur)
         return self.arena.params
 
-    def _stream_for_block(self) -> Optional[torch.cuda.Stream]:
-        """This learner's compute stream if ``Settings.NODE_STREAMS`` wants one now.
+    def _guard(self):
+        return getattr(self.arena.params, "guard", None) if self.arena is not None else None
 
-        ``"auto"``: when there is something to overlap -- other trainers in the round
-        (``Settings.TRAIN_SET_SIZE > 1``: arriving models to fold, gossip to push) or
-        other learners in this process (virtual peers).  A lone trainer runs on the
-        caller's stream: every hand-off between two streams on different hardware
-        queues costs the next epoch ~0.55 ms of device time
-        (``profiles/r5_handoff_probe.md``), with nothing to gain (1-peer MNIST round
-        7.23 -> 6.65 ms)."""
-        if self.device.type != "cuda":
-            return None
-        mode = Settings.NODE_STREAMS
-        want = (Settings.TRAIN_SET_SIZE > 1 or len(_GPU_LEARNERS) > 1) if mode == "auto" else bool(mode)
-        if not want:
+    def _stream_for_block(self) -> Optional[torch.cuda.Stream]:
+        """This learner's compute stream (``Settings.NODE_STREAMS``; ``"auto"``: every
+        GPU learner), or None to enqueue on the caller's stream.  The hand-offs to
+        the threads that read the weights on other streams are lazy (the arena's
+        WeightGuard): a block waits only for reads / writes launched elsewhere
+        since the last one, so a lone trainer pays no cross-queue wait at all."""
+        if self.device.type != "cuda" or not Settings.NODE_STREAMS:
             return None
         if self._compute_stream is None:
             self._compute_stream = private_stream(self.device, _COMPUTE_PRIORITY)
         return self._compute_stream
 
     @contextlib.contextmanager
-    def _on_stream(self, hold_gate: bool = False, wait_caller: bool = True):
+    def _on_stream(self, hold_gate: bool = False, wait_caller: bool = False, writes: bool = True):
         """Run a block on this learner's compute stream.
 
-        Event-ordered hand-off, no host synchronisation: the compute stream
-        first waits for what the caller's stream already holds (e.g. the
-        aggregate a ``set_parameters`` copies), and the caller's stream -- the
-        default stream every other thread of the node enqueues on (gossip
-        snapshots, FedAvg, transport producer events) -- waits for the block's
-        kernels afterwards.  With ``NODE_STREAMS=False`` everything simply runs
-        on the caller's stream.
+        Ordering, without host synchronisation and without handing the stream back
+        to the caller's (``profiles/r5_handoff_probe.md``: every such hand-back cost
+        the next epoch ~0.55 ms of device time):
 
-        ``wait_caller=False`` skips the first half: for a block that reads nothing the
-        caller's stream produces (a fit whose weights arrived through
-        :meth:`set_parameters`, itself a hand-off).  Each cross-queue wait costs the
-        waiting queue's wake-up when it has gone idle -- two of them between
-        consecutive fits added ~0.58 ms of device time per epoch graph
-        (scripts/learner_epoch_probe.py: 6.89 vs 6.29 ms).
+        * ``writes`` (fit, set_parameters): the block starts after every read of the
+          weights launched on other streams since the last write (FedAvg folds,
+          gossip snapshots -- WAR), and records the weights' ready event at its end,
+          which readers on other streams wait on where they launch (RAW);
+        * otherwise (evaluation) the block only waits for the last write if that ran
+          on another stream;
+        * ``wait_caller``: the block also consumes something the caller's stream
+          produced (``set_parameters`` copying an aggregate the FedAvg kernel wrote
+          there): the compute stream first waits for the caller's stream.
+
+        ``hold_gate``: the whole block is short GPU work issued from a non-learning
+        thread (set_parameters from a command handler): it runs under the shared
+        device gate, never beside another peer's capture (a copy launched from a
+        handler thread during a capture crashed the HIP runtime once under rocprofv3
+        in the 8-peer scenario).
         """
         cs = self._stream_for_block()
-        cur = torch.cuda.current_stream(self.device) if cs is not None else None
+        cur = torch.cuda.current_stream(self.device) if self.device.type == "cuda" else None
+        run = cs if cs is not None else cur
+        guard = self._guard()
         gate = self._gate() if hold_gate else contextlib.nullcontext()
-        if cs is None or cur == cs:
-            with gate:
-                yield
-            return
         from p2pfl_amd.learning.step_graph import GATE
 
-        # the hand-off events are recorded on the caller's stream -- usually the
-        # legacy default stream, which ROCm treats as part of a graph capture in
-        # progress on another peer's thread (hipErrorCapturedEvent): never while
-        # another thread records.  hold_gate: the whole block is short GPU work
-        # issued from a non-learning thread (set_parameters from a command
-        # handler): it runs under the shared gate too, never beside another
-        # peer's capture (a copy launched from a handler thread during a capture
-        # crashed the HIP runtime once under rocprofv3 in the 8-peer scenario)
-        if wait_caller:
+        if wait_caller and cs is not None and cur != cs:
+            # recorded on the caller's stream -- usually the legacy default stream,
+            # which ROCm treats as part of a capture in progress on another peer's
+            # thread (hipErrorCapturedEvent): never while another thread captures
             with GATE.shared():
                 cs.wait_stream(cur)
+        if guard is not None:
+            if writes:
+                guard.begin_write(run)
+            else:
+                guard.acquire(run)
         try:
-            with gate, torch.cuda.stream(cs):
+            with gate, (torch.cuda.stream(cs) if (cs is not None and cur != cs) else contextlib.nullcontext()):
                 yield
         finally:
-            with GATE.shared():
-                cur.wait_stream(cs)
+            if writes and guard is not None:
+                guard.end_write(run)
 
     def set_parameters(self, params: Mapping[str, torch.Tensor]) -> None:
         finite.check(self._addr, "set_parameters input", params if isinstance(params, FlatParams) else None)
@@ -243,8 +259,17 @@ class TorchLearner(NodeLearner):
                 and params.flat.data_ptr() == self.arena.params.flat.data_ptr()):
             self._arena_changed()
             return  # the arena itself (a one-member aggregate): no copy, so no stream hand-off either
-        with self._on_stream(hold_gate=True):
+        with self._on_stream(hold_gate=True, wait_caller=True):
             self._set_parameters(params)
+            cs = self._stream_for_block()
+            if cs is not None:
+                # the source (an aggregate or a received model, allocated on another
+                # stream) is read by this stream's copy: no hand-back orders its
+                # release after the copy, so tell the caching allocator
+                srcs = [params.flat] if isinstance(params, FlatParams) else list(params.values())
+                for t in srcs:
+                    if isinstance(t, torch.Tensor) and t.is_cuda:
+                        t.record_stream(cs)
         if finite.ENABLED and self.arena is not None:
             finite.check(self._addr, "parameters after set_parameters", self.arena.flat)
 
@@ -273,8 +298,11 @@ class TorchLearner(NodeLearner):
 
     def encode_parameters(self, params: Optional[Mapping[str, torch.Tensor]] = None) -> bytes:
         if params is None:
-            params = self.get_parameters()
-        return encode_params(params)
+            params = self.live_parameters()
+        from p2pfl_amd.learning.arena import reading
+
+        with reading(params):
+            return encode_params(params)
 
     def snapshot_parameters(self, params: Optional[Mapping[str, torch.Tensor]] = None) -> FlatParams:
         """Immutable device payload for gossip.
@@ -285,13 +313,17 @@ class TorchLearner(NodeLearner):
         received models are fresh buffers nobody mutates: they go out as is.
         """
         if params is None:
-            params = self.get_parameters()
+            params = self.live_parameters()
         if isinstance(params, FlatParams):
             if self.arena is None or params.flat.data_ptr() != self.arena.flat.data_ptr():
                 return params
             snap = self._snapshot
             if snap is None or snap[0] != self._arena_version:
-                with self._gate():  # a copy launched from a gossip thread: never beside a capture
+                from p2pfl_amd.learning.arena import reading
+
+                # a copy launched from a gossip thread: never beside a capture; after
+                # the last write of the weights, before the next (WeightGuard)
+                with self._gate(), reading(params):
                     snap = self._snapshot = (self._arena_version, params.clone())
             return snap[1]
         from p2pfl_amd.learning.arena import flatten
@@ -542,7 +574,7 @@ class TorchLearner(NodeLearner):
 
     def validate(self) -> None:
         """The per-epoch validation pass (metrics to the local store)."""
-        with self._on_stream():
+        with self._on_stream(writes=False):
             self._validate()
 
     def _eval_graph_ok(self, loader: Any) -> bool:
@@ -648,7 +680,7 @@ class TorchLearner(NodeLearner):
             if on_results is not None:
                 on_results(results)
 
-        with logger.span(self._addr, "evaluate"), self._on_stream():
+        with logger.span(self._addr, "evaluate"), self._on_stream(writes=False):
             self.model.eval()
             self._run_eval_graph(loader, self.model.test_step, done)
         return True
@@ -663,7 +695,7 @@ class TorchLearner(NodeLearner):
         if self.evaluate_async(box.update):
             self.drain()
             return box
-        with logger.span(self._addr, "evaluate"), self._on_stream():
+        with logger.span(self._addr, "evaluate"), self._on_stream(writes=False):
             results = self._run_eval(self.data.test_dataloader(), self.model.test_step)
         for k, v in results.items():
             self._log(k, v)

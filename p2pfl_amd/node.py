@@ -239,6 +239,7 @@ class Node:
             self.state.learner.interrupt_fit()
         self.aggregator.clear()
         self.state.clear()
+        getattr(self._communication_protocol, "experiment_boundary", lambda: None)()
         logger.experiment_finished(self.addr)
 
     # ------------------------------------------------------------------

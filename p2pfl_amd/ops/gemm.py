@@ -91,6 +91,14 @@ _VARIANT_ENV = os.environ.get("P2PFL_GEMM_VARIANT")
 
 PP = 2048  # variant bit 11: the ping-pong 256 x 256 pipeline (csrc/gemm_pp.hip)
 PP_M16 = 1 << 16  # with PP: the same pipeline on v_mfma_f32_16x16x32_bf16
+PP_SK = 1 << 17  # with PP: stream-K schedule, ``splits`` = grid size (csrc/gemm_pp.hip)
+PP_N128 = 1 << 21  # with PP: the 256 x 128 output tile (150 whole tiles for the N = 768 products)
+SK_SLAB = 256 * 256  # fp32 elements of one stream-K partial tile (two per workgroup)
+
+
+def sk_iters(M: int, N: int, K: int) -> int:
+    """K-tile iterations a stream-K launch divides among its workgroups."""
+    return -(-M // 256) * -(-N // 256) * -(-K // 64)
 
 
 def pp_eligible(M: int, N: int, K: int, a_kmajor: bool, b_kmajor: bool) -> bool:
@@ -142,6 +150,13 @@ def gemm(
     N = b.shape[0] if b_kmajor else b.shape[1]
     K = a.shape[1] if a_kmajor else a.shape[0]
     dev = a.device
+    if variant is not None and variant & PP_SK:  # stream-K: `splits` workgroups share the K-tile iterations
+        if out is None:
+            out = torch.empty((M, N), dtype=out_dtype, device=dev)
+        z = torch.empty((M, N), dtype=torch.bfloat16, device=dev) if (gelu and want_z) else None
+        ws = torch.empty(2 * splits * SK_SLAB, dtype=torch.float32, device=dev)
+        _C().gemm(a, b, a_kmajor, b_kmajor, out, bias, gelu, z, residual, splits, variant, ws, counters(tiles_of(M, N), dev))
+        return out, z
     if splits > 1:
         if out is None:
             out = torch.empty((M, N), dtype=out_dtype, device=dev)

@@ -70,9 +70,11 @@ class Settings:
     aggregation and transport work left on the default stream (FedAvg folds of
     arriving models, payload snapshots, the RCCL comm stream's hand-offs) and
     other virtual peers' training overlap a running ``fit()``.  ``"auto"``
-    (default): every GPU learner; ``True`` / ``False`` force it (``False``: the
-    learner enqueues on the caller's stream).  The hand-off between the
-    learner's stream and the default stream is event-ordered (no host sync)."""
+    (default) and ``True``: every GPU learner; ``False``: the learner enqueues on
+    the caller's stream.  The hand-offs are lazy and event-ordered (the arena's
+    ``WeightGuard``): readers of the weights on other streams wait for the last
+    write only where they launch, the next write waits for those reads, and a
+    lone trainer pays no cross-queue wait at all."""
 
     EVAL_BATCH_FACTOR: int = 8
     """New: captured evaluation steps (test / validation passes of the graph

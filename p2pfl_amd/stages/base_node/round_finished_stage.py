@@ -56,6 +56,7 @@ class RoundFinishedStage(Stage):
         state.train_set = []
         state.model_initialized.clear()
         state.clear()
+        getattr(communication_protocol, "experiment_boundary", lambda: None)()
         logger.info(state.addr, "Training finished!!.")
         return None
 

@@ -43,6 +43,7 @@ class StartLearningStage(Stage):
             if state.round is not None:
                 return None
             state.set_experiment("experiment", rounds)
+            getattr(communication_protocol, "experiment_boundary", lambda: None)()
             logger.experiment_started(state.addr)
             state.learner = learner_class(model, data, state.addr, epochs, **(learner_kwargs or {}))
         begin = time.time()

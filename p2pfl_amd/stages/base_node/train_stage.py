@@ -56,7 +56,10 @@ class TrainStage(Stage):
                 state.learner.fit()
         if not early_stopping_fn():
             learner = state.learner
-            models_added = aggregator.add_model(learner.get_parameters(), [state.addr], learner.get_num_samples()[0])
+            # the live weights, unordered: the aggregator's kernels read them under the
+            # arena's WeightGuard (arena.reading), a one-model round reads nothing
+            own = getattr(learner, "live_parameters", learner.get_parameters)()
+            models_added = aggregator.add_model(own, [state.addr], learner.get_num_samples()[0])
             state.changed.bump()
             communication_protocol.broadcast(
                 communication_protocol.build_msg(ModelsAggregatedCommand.get_name(), models_added, round=state.round)

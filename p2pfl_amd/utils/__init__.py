@@ -64,11 +64,15 @@ def check_equal_models(nodes: List[Any], atol: float = 1e-1) -> None:
         if node.state.learner is None:
             raise AssertionError("learner not set")
         params = node.state.learner.get_parameters()
+        from p2pfl_amd.learning.arena import reading
+
+        with reading(params):  # after the learner's last write on its own stream
+            host = {k: v.detach().float().cpu().numpy().copy() for k, v in params.items()}
         if first is None:
-            first = {k: v.detach().float().cpu().numpy().copy() for k, v in params.items()}
+            first = host
             continue
         for layer, ref in first.items():
-            cur = params[layer].detach().float().cpu().numpy()
+            cur = host[layer]
             if not np.allclose(ref, cur, atol=atol):
                 diff = float(np.abs(ref - cur).max())
                 raise AssertionError(f"{layer}: {nodes[0].addr} vs {node.addr} differ (max |diff| {diff:.3g})")

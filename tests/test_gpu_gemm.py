@@ -273,3 +273,141 @@ def test_in_launch_splitk_reused_workspace(splits, kernel):
     C.gemm(A.t().contiguous(), B.t().contiguous(), False, False, ws2, None, False, None, None, splits, 0, None, None)
     C.tile_slab_reduce(ws2, splits, M, N, out2, 0)
     assert torch.equal(out2, refs[-1])
+
+
+# ---- stream-K schedule of the ping-pong kernel (variant bits 11 + 17) ---------------------
+@pytest.mark.parametrize("m16", [False, True], ids=["mfma32", "mfma16"])
+@pytest.mark.parametrize("a_kmajor,b_kmajor", [(True, True), (True, False), (False, True), (False, False)])
+@pytest.mark.parametrize("M,N,K,grid", [(1000, 776, 448, 37), (512, 512, 1024, 24), (600, 264, 3072, 256),
+                                        (264, 520, 200, 5), (6304 // 4, 768, 3072, 256), (256, 256, 64, 1)])
+def test_stream_k_layouts_vs_fp32(a_kmajor, b_kmajor, M, N, K, grid, m16):
+    """Stream-K: workgroups whose K-tile ranges cut tiles anywhere (grids that do and do
+    not divide the iteration count, one workgroup spanning several tiles, several
+    workgroups per tile), every operand layout, M / N tails, a K tail (m/n-major)."""
+    from p2pfl_amd.ops.gemm import PP, PP_M16, PP_SK, sk_iters
+
+    if (a_kmajor or b_kmajor) and K % 64:
+        pytest.skip("k-major operands need K % 64 == 0 on this kernel")
+    if not a_kmajor and M % 8:
+        pytest.skip("m-major A needs M % 8 == 0")
+    assert grid <= sk_iters(M, N, K)
+    a, b = _operands(M, N, K, a_kmajor, b_kmajor, seed=M + 5 * N + K)
+    out, _ = ops.gemm(a, b, a_kmajor, b_kmajor, out_dtype=torch.float32, splits=grid,
+                      variant=PP | PP_SK | (PP_M16 if m16 else 0))
+    ref, _ = ops.gemm_reference(a, b, a_kmajor, b_kmajor)
+    torch.testing.assert_close(out, ref, atol=5e-3, rtol=1e-4)
+
+
+@pytest.mark.parametrize("m16", [False, True], ids=["mfma32", "mfma16"])
+def test_stream_k_epilogues(m16):
+    """Bias + GELU (+ pre-activation) and bias + residual epilogues applied by the
+    workgroup that completes each cut tile, bf16 out (the ViT fc1 / proj shapes)."""
+    from p2pfl_amd.ops.gemm import PP, PP_M16, PP_SK
+
+    v = PP | PP_SK | (PP_M16 if m16 else 0)
+    M, N, K = 6304, 3072, 768
+    a, b = _operands(M, N, K, True, True, seed=21)
+    bias = torch.randn(N, device="cuda")
+    out, z = ops.gemm(a, b, bias=bias, gelu=True, want_z=True, splits=256, variant=v)
+    ref, zr = ops.gemm_reference(a, b, True, True, bias, True)
+    torch.testing.assert_close(z.float(), zr, atol=0.25, rtol=1e-2)
+    torch.testing.assert_close(out.float(), ref, atol=0.25, rtol=1e-2)
+    res = torch.randn(M, 768, device="cuda").to(torch.bfloat16)
+    a2, b2 = _operands(M, 768, 3072, True, True, seed=22)
+    out2, _ = ops.gemm(a2, b2, bias=bias[:768].to(torch.bfloat16), residual=res, splits=200, variant=v)
+    ref2, _ = ops.gemm_reference(a2, b2, True, True, bias[:768].to(torch.bfloat16), False, res)
+    torch.testing.assert_close(out2.float(), ref2, atol=0.5, rtol=1e-2)
+
+
+@pytest.mark.parametrize("local", [False, True], ids=["sc1", "xcd_local"])
+@pytest.mark.parametrize("grid", [96, 256])
+def test_stream_k_reused_workspace_bitwise(grid, local):
+    """Back-to-back stream-K launches over one reused counter array: every launch sees
+    only its own partials (the sc1 hand-off), and the fix-up sums the partials in a
+    fixed order whichever workgroup completes a tile, so repeated launches on the same
+    operands are bitwise identical (random operands: summation order matters)."""
+    from p2pfl_amd.ops.gemm import PP, PP_SK, SK_SLAB
+    from p2pfl_amd.ops.splitk import counters, tiles_of
+
+    C = ops.ext()
+    V = PP | PP_SK | ((1 << 20) if local else 0)  # bit 20: XCD-local partials published with plain stores
+    M, N, K = 6304, 768, 3072  # the fc2 forward: 75 tiles of 48 K-tiles
+    cnt = counters(tiles_of(M, N), torch.device("cuda"))
+    ws = torch.empty(2 * grid * SK_SLAB, device="cuda")
+    a, b = _operands(M, N, K, True, True, seed=31)
+    outs = []
+    for it in range(12):
+        out = torch.empty(M, N, device="cuda", dtype=torch.float32)
+        C.gemm(a, b, True, True, out, None, False, None, None, grid, V, ws, cnt)
+        outs.append(out)
+    torch.cuda.synchronize()
+    assert int(cnt.abs().sum()) == 0, "tile counters must be left zero"
+    ref, _ = ops.gemm_reference(a, b)
+    torch.testing.assert_close(outs[0], ref, atol=5e-3, rtol=1e-4)
+    for it, o in enumerate(outs[1:], 1):
+        assert torch.equal(o, outs[0]), f"launch {it} differs: max {(o - outs[0]).abs().max().item()}"
+    # integer operands: exact whatever the order, across a fresh operand every launch
+    for it in range(8):
+        g = torch.Generator(device="cuda").manual_seed(200 + it)
+        A = torch.randint(-2, 3, (M, K), device="cuda", generator=g).to(torch.bfloat16)
+        B = torch.randint(-2, 3, (N, K), device="cuda", generator=g).to(torch.bfloat16)
+        out = torch.empty(M, N, device="cuda", dtype=torch.float32)
+        C.gemm(A, B, True, True, out, None, False, None, None, grid, V, ws, cnt)
+        assert torch.equal(out, A.float() @ B.float().t()), it
+
+
+def test_stream_k_refuses_bad_grid():
+    from p2pfl_amd.ops.gemm import PP, PP_SK, sk_iters
+
+    a, b = _operands(256, 256, 128, True, True)
+    with pytest.raises(RuntimeError):
+        ops.gemm(a, b, splits=sk_iters(256, 256, 128) + 1, variant=PP | PP_SK)
+
+
+# ---- 256 x 128 ping-pong tile (variant bits 11 + 21) --------------------------------------
+@pytest.mark.parametrize("a_kmajor,b_kmajor", [(True, True), (True, False), (False, True), (False, False)])
+@pytest.mark.parametrize("M,N,K", [(512, 256, 256), (296, 200, 128), (1000, 776, 448), (264, 520, 200), (6304, 768, 3072),
+                                   (72, 136, 64)])
+def test_pingpong128_layouts_vs_fp32(a_kmajor, b_kmajor, M, N, K):
+    """The 256 x 128 tile: every layout, M / N tails (clamped rows, masked stores), odd and
+    even K-tile counts (the two-K-tile phase schedule's tail), a K tail (m/n-major only)."""
+    from p2pfl_amd.ops.gemm import PP, PP_N128
+
+    if (a_kmajor or b_kmajor) and K % 64:
+        pytest.skip("k-major operands need K % 64 == 0 on this kernel")
+    if not a_kmajor and M % 8:
+        pytest.skip("m-major A needs M % 8 == 0")
+    a, b = _operands(M, N, K, a_kmajor, b_kmajor, seed=M + 7 * N + K)
+    out, _ = ops.gemm(a, b, a_kmajor, b_kmajor, out_dtype=torch.float32, variant=PP | PP_N128)
+    ref, _ = ops.gemm_reference(a, b, a_kmajor, b_kmajor)
+    torch.testing.assert_close(out, ref, atol=5e-3, rtol=1e-4)
+    outb, _ = ops.gemm(a, b, a_kmajor, b_kmajor, out_dtype=torch.bfloat16, variant=PP | PP_N128)
+    torch.testing.assert_close(outb.float(), ref, atol=0.25, rtol=1e-2)
+
+
+def test_pingpong128_exact_integers_and_epilogues():
+    from p2pfl_amd.ops.gemm import PP, PP_N128
+
+    v = PP | PP_N128
+    M, N, K = 520, 392, 256
+    A = torch.randint(-3, 4, (M, K), device="cuda").to(torch.bfloat16)
+    B = (torch.arange(N * K, device="cuda").view(N, K) % 7 - 3).to(torch.bfloat16)
+    for ak, bk in [(True, True), (True, False), (False, True), (False, False)]:
+        a = A if ak else A.t().contiguous()
+        b = B if bk else B.t().contiguous()
+        out, _ = ops.gemm(a, b, ak, bk, out_dtype=torch.float32, variant=v)
+        assert torch.equal(out, A.float() @ B.float().t()), (ak, bk)
+    # bias + GELU (+ pre-activation), bias + residual (the ViT fc2 / proj forward)
+    M, N, K = 6304, 768, 3072
+    a, b = _operands(M, N, K, True, True, seed=41)
+    bias = torch.randn(N, device="cuda")
+    out, z = ops.gemm(a, b, bias=bias, gelu=True, want_z=True, variant=v)
+    ref, zr = ops.gemm_reference(a, b, True, True, bias, True)
+    torch.testing.assert_close(z.float(), zr, atol=0.5, rtol=1e-2)
+    torch.testing.assert_close(out.float(), ref, atol=0.5, rtol=1e-2)
+    res = torch.randn(M, N, device="cuda").to(torch.bfloat16)
+    out2, _ = ops.gemm(a, b, bias=bias.to(torch.bfloat16), residual=res, variant=v)
+    ref2, _ = ops.gemm_reference(a, b, True, True, bias.to(torch.bfloat16), False, res)
+    torch.testing.assert_close(out2.float(), ref2, atol=0.5, rtol=1e-2)
+    with pytest.raises(RuntimeError):
+        ops.gemm(a, b, splits=2, variant=v)

@@ -210,8 +210,10 @@ def test_multi_tensor_channels_last(opt):
     """Conv weights with channels-last grads/shadows: fp32 state in OIHW order, shadow written at OHWI positions."""
     # staged through LDS (csrc/optim.hip ClStage): 64x32x3x3 (slab 288: 16 slabs per chunk), 128x64x5x5
     # (slab 1600: 2 per chunk), 512x512x3x3 (one 4608 slab per chunk), 40x36x3x3 (slab 324: 14 per
-    # chunk); gather path: 16x3x7x7 (I = 3); no permutation: 24x8x1x1
-    shapes = [(64, 32, 3, 3), (10, 7), (128, 64, 5, 5), (16, 3, 7, 7), (512, 512, 3, 3), (40, 36, 3, 3), (24, 8, 1, 1)]
+    # chunk); gather path: 16x3x7x7 (I = 3), 8x1024x3x3 and 8x192x5x5 (slabs 9216 / 4800 > 4608:
+    # plain chunks that start mid-slab); no permutation: 24x8x1x1
+    shapes = [(64, 32, 3, 3), (10, 7), (128, 64, 5, 5), (16, 3, 7, 7), (512, 512, 3, 3), (40, 36, 3, 3), (24, 8, 1, 1),
+              (8, 1024, 3, 3), (8, 192, 5, 5)]
     cl = [(s[1], s[2] * s[3]) if len(s) == 4 else None for s in shapes]
     sizes = [int(torch.Size(s).numel()) for s in shapes]
     mt = _Tables(sizes, [True] * len(shapes), "cuda", cl=cl)

@@ -249,6 +249,35 @@ def test_rank_killed_mid_transfer_survivors_finish():
     assert abs(rec["sums"][0] - rec["sums"][1]) < 1e-3 * max(1.0, abs(rec["sums"][0]))
 
 
+@pytest.mark.timeout(600)
+def test_two_consecutive_experiments_on_the_same_nodes():
+    """A second experiment restarts at round 0 with the same (round, command,
+    contributors) as the first: the transport's dedupe of received models is per
+    experiment, so nothing is declined and no node waits for a timeout."""
+    port = _free_port()
+    out = os.path.join("/tmp", f"xgmi_twice_{port}.json")
+    env = _env()
+    procs = []
+    for r in range(3):
+        e = dict(env, RANK=str(r), WORLD_SIZE="3", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.join(ROOT, "tests", "xgmi_worker.py"), out, "twice"],
+                                      cwd=ROOT, env=e, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True))
+    outs = []
+    for p in procs:
+        try:
+            o, _ = p.communicate(timeout=400)
+        except subprocess.TimeoutExpired:
+            p.kill()
+            o, _ = p.communicate()
+        outs.append(o)
+    for r, p in enumerate(procs):
+        assert p.returncode == 0, outs[r][-4000:]
+    with open(out) as f:
+        rec = json.load(f)
+    os.unlink(out)
+    assert rec["digests"][0] == rec["digests"][1]
+
+
 def test_primary_backend_failure_on_one_rank_switches_every_rank_to_fallback():
     import torch.distributed as dist
 

@@ -8,6 +8,9 @@ launched a receive that can never complete, so the survivors must abort the
 communicator and rebuild it over ranks {0, 1}.  Ranks 0 and 1 must still
 finish every round with the same model; rank 0 writes the outcome to OUT_JSON.
 
+``twice``: two consecutive experiments on the same nodes; the second must
+finish promptly with equal models (no model declined as "already received").
+
 ``P2PFL_WORKER_DEVICE=cuda``: the same scenario on the GPU with the RCCL data
 plane (no fallback): every rank is its own RCCL "host" (``NCCL_HOSTID`` set by
 the test), so three processes on one MI355X form a real 3-rank communicator;
@@ -90,6 +93,21 @@ def main(out: str, mode: str) -> None:
         time.sleep(0.01)
     rounds_done = {"n": 0}
     assert node.wait_learning(timeout=240), "learning did not finish"
+    if mode == "twice":
+        # a second experiment on the same nodes: it restarts at round 0, so the
+        # transport's dedupe keys of the first one must not decline its models
+        store.set(f"first/{rank}", "1")
+        store.wait([f"first/{r}" for r in range(world)])
+        node._learning_thread = None
+        if rank == 0:
+            node.set_start_learning(rounds=rounds, epochs=1)
+        t0 = time.time()
+        while node._learning_thread is None:
+            assert time.time() - t0 < 60, "second experiment did not start"
+            time.sleep(0.01)
+        t0 = time.time()
+        assert node.wait_learning(timeout=240), "second experiment did not finish"
+        assert time.time() - t0 < 60, "second experiment stalled (waited for a timeout)"
     flat = node.state.learner.get_parameters().flat if node.state.learner is not None else None
     s = float(flat.double().sum()) if flat is not None else float("nan")
     digest = ""
