@@ -5,7 +5,7 @@ FedAvg at 1/2/4/8 peers.  ``value`` is the whole-job aggregate training
 throughput (train samples/s summed over peers); ``ms_per_step`` is the
 wall-clock of one federated round.
 
-What runs (default ``--aggregation gossip``): every rank is a full p2pfl
+What runs: every rank is a full p2pfl
 :class:`~p2pfl_amd.node.Node` driven through the reference's stage machine
 (``Node.set_start_learning`` -> StartLearning -> VoteTrainSet -> Train ->
 GossipModel -> RoundFinished, reference ``node.py:297-364``) on the xGMI
@@ -29,10 +29,10 @@ Per-peer round work matches the reference example shard
 test MNIST-shaped samples, batch 32, the reference CNN (6.5 M params), Adam
 1e-3 re-created per round, 1 local epoch.
 
-Other modes: ``--aggregation allreduce`` (round-1 data-path runner: one
-weighted RCCL all-reduce instead of the protocol), ``--impl reference``
-(reference-equivalent fp32 eager path, used for the measured baseline),
-``--model resnet18|resnet50|vit_b16`` (BASELINE configs 3-5).
+Other modes: ``--impl torch`` (the generic TorchLearner instead of the fused
+CNN engine), ``--model resnet18|resnet50|vit_b16`` (BASELINE configs 3-5).  The
+reference-equivalent baseline (fp32 eager, pickle, per-layer FedAvg) is measured
+by ``scripts/reference_baseline.py``.
 
 Launch: ``python bench.py --gpus N`` starts N worker processes itself (the
 launcher never touches the GPU); under ``torchrun`` each process is one rank.
@@ -43,7 +43,6 @@ from __future__ import annotations
 import argparse
 import json
 import os
-import pickle
 import signal
 import socket
 import subprocess
@@ -59,8 +58,8 @@ from p2pfl_amd.data import MnistFederatedDM  # noqa: E402
 from p2pfl_amd.models import CNN  # noqa: E402
 
 # Reference-equivalent baseline, measured (not published -- the reference
-# publishes no timing): `python bench.py --impl reference --aggregation
-# allreduce` on one MI355X, 99.6 ms per round = 27,120.7 train samples/s per
+# publishes no timing): `python scripts/reference_baseline.py` (round 1:
+# `bench.py --impl reference`) on one MI355X, 99.6 ms per round = 27,120.7 train samples/s per
 # peer.  vs_baseline compares per-peer throughput with it; it is
 # context, not a published comparison (the reference's own control plane
 # sleeps >= 2 s per round on top of that work).
@@ -390,125 +389,12 @@ def _print_round_breakdown(rank, addr, tracer, round_ends, W, K) -> None:
               + ", ".join(f"->{p} {v / 1e6:.1f} MB" for p, v in sorted(links.items())), file=sys.stderr, flush=True)
 
 
-def run_allreduce(args, env: _Env) -> dict:
-    """Round-1 data-path runner: weighted RCCL all-reduce of the arenas (no protocol)."""
-    from p2pfl_amd.parallel import CollectiveFedAvg, DistEnv
-    from p2pfl_amd.parallel.rounds import FederatedRoundRunner
-
-    if env.world > 1 and env.device.type == "cuda":
-        import torch.distributed as dist
-
-        dist.destroy_process_group()
-        dist.init_process_group("nccl", rank=env.rank, world_size=env.world, device_id=env.device)
-    denv = DistEnv(env.rank, env.world, env.local, env.device)
-    torch.manual_seed(1234)
-    model, data, desc, data_desc = build_config(args, env.rank)
-    fed = CollectiveFedAvg(denv)
-    if args.impl == "reference":
-        learner = ReferenceEquivalentLearner(model, data, env.device)
-        weight = float(learner.get_num_samples()[0])
-        run = lambda: reference_round(learner, denv, weight)  # noqa: E731
-    else:
-        learner = learner_class(args)(model, data, f"peer{env.rank}", args.epochs, device=env.device)
-        runner = FederatedRoundRunner(learner, fed, name=f"peer{env.rank}")
-        run = lambda: runner.run_round().seconds  # noqa: E731
-    for i in range(args.warmup):
-        t = run()
-        print(f"[bench rank {env.rank}] warmup round {i}: {t * 1e3:.2f} ms", file=sys.stderr, flush=True)
-    fed.barrier()
-    _sync(env.device)
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        run()
-    _sync(env.device)
-    fed.barrier()
-    elapsed = fed.max_over_ranks(time.perf_counter() - t0)
-    n_train = len(data.train_dataloader().dataset)
-    per_peer = n_train * args.epochs * args.steps / elapsed
-    return {
-        "elapsed": elapsed, "desc": desc, "data_desc": data_desc, "n_train": n_train,
-        "n_val": len(data.val_dataloader().dataset), "n_test": len(data.test_dataloader().dataset),
-        "total": per_peer * env.world, "parallelism": f"fedavg-allreduce-dp{env.world}", "transport": "rccl-allreduce",
-    }
-
-
-class ReferenceEquivalentLearner:
-    """What p2pfl's LightningLearner does per round, minus Lightning itself."""
-
-    def __init__(self, model, data, device):
-        self.model = model.to(device)
-        self.data = data.to(device)
-        self.device = device
-
-    def get_num_samples(self):
-        return len(self.data.train_dataloader().dataset), len(self.data.test_dataloader().dataset)
-
-    def _eval(self, loader):
-        self.model.eval()
-        tot, n = 0.0, 0
-        with torch.no_grad():
-            for x, y in loader:
-                logits = self.model(x)
-                loss = torch.nn.functional.cross_entropy(self.model(x), y)  # double forward (reference cnn.py:103-104)
-                acc = (logits.argmax(1) == y).float().mean()
-                tot += float(loss) * len(y) + 0 * float(acc)
-                n += len(y)
-        return tot / max(n, 1)
-
-    def fit(self):
-        self.model.train()
-        opt = torch.optim.Adam(self.model.parameters(), lr=1e-3)
-        for x, y in self.data.train_dataloader():
-            opt.zero_grad()
-            loss = torch.nn.functional.cross_entropy(self.model(x), y)
-            loss.backward()
-            opt.step()
-        self._eval(self.data.val_dataloader())
-
-    def get_parameters(self):
-        # reference encode: .cpu().numpy() + pickle; decode: pickle.loads + torch.tensor (own data, trusted)
-        blob = pickle.dumps([v.cpu().numpy() for v in self.model.state_dict().values()])
-        arrays = pickle.loads(blob)
-        self._keys = list(self.model.state_dict().keys())
-        return [torch.tensor(a, device=self.device) for a in arrays]
-
-    def set_parameters(self, params):
-        self.model.load_state_dict(dict(zip(self._keys, params)))
-
-
-def reference_round(learner, env, weight):
-    import torch.distributed as dist
-
-    t0 = time.perf_counter()
-    learner._eval(learner.data.test_dataloader())
-    learner.fit()
-    params = learner.get_parameters()
-    gathered = [params]
-    if env.world_size > 1:
-        gathered = [[None] * len(params) for _ in range(env.world_size)]
-        for i, p in enumerate(params):
-            outs = [torch.empty_like(p) for _ in range(env.world_size)]
-            dist.all_gather(outs, p)
-            for r in range(env.world_size):
-                gathered[r][i] = outs[r]
-    accum = [torch.zeros_like(p) for p in params]
-    for model in gathered:  # per-layer FedAvg loop (reference fedavg.py:49-58)
-        for i, layer in enumerate(model):
-            accum[i] = accum[i] + layer * weight
-    accum = [a / (weight * len(gathered)) for a in accum]
-    learner.set_parameters(accum)
-    _sync(env.device)
-    return time.perf_counter() - t0
-
-
 def main() -> None:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=3, help="timed federated rounds")
     ap.add_argument("--warmup", type=int, default=1, help="untimed federated rounds")
-    ap.add_argument("--aggregation", choices=["gossip", "allreduce"], default="gossip",
-                    help="gossip: the product (Node + stages + xGMI gossip); allreduce: LEGACY round-1 comparison runner")
-    ap.add_argument("--impl", choices=["fused", "torch", "reference"], default="fused")
+    ap.add_argument("--impl", choices=["fused", "torch"], default="fused")
     ap.add_argument("--model", choices=["cnn", "resnet18", "resnet50", "vit_b16"], default="cnn")
     ap.add_argument("--epochs", type=int, default=1)
     ap.add_argument("--number-sub", type=int, default=None, help="shards of the dataset (default per model)")
@@ -522,8 +408,6 @@ def main() -> None:
                          "'transport' then says xgmi/gloo)")
     argv = sys.argv[1:]
     args = ap.parse_args(argv)
-    if args.impl == "reference":
-        args.aggregation = "allreduce"
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
         sys.exit(launch(args, argv))
 
@@ -533,7 +417,7 @@ def main() -> None:
     env = _Env()
     if env.world != args.gpus:
         raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={env.world}")
-    res = run_gossip(args, env) if args.aggregation == "gossip" else run_allreduce(args, env)
+    res = run_gossip(args, env)
     ms_per_round = res["elapsed"] / args.steps * 1e3
     total = res["total"]
     per_peer = total / env.world
@@ -552,7 +436,7 @@ def main() -> None:
                     "higher_is_better": True,
                     "scaling": "weak",
                     "vs_baseline": (round(per_peer / BASELINE_SAMPLES_PER_SEC_PER_PEER, 3) if args.model == "cnn" else None),
-                    "dtype": "bf16" if (args.impl != "reference" and env.device.type == "cuda") else "fp32",
+                    "dtype": "bf16" if env.device.type == "cuda" else "fp32",
                     "data": res["data_desc"],
                     "impl": args.impl if (args.model == "cnn" or args.impl != "fused") else "torch",
                     "transport": res["transport"],

@@ -518,8 +518,7 @@ class FusedCNNLearner(TorchLearner):
                 self._step += steps
                 prev, self._last_epoch_end = self._last_epoch_end, t1
                 self._completions.submit(done, lambda h=host, b=base, a=t0, z=t1, p=prev: self._log_epoch(h, b, steps, bs, n, a, z, p))
-                if not (self.defer_final_validation and epoch == self.epochs - 1):
-                    self._validate_async()
+                self._validate_async()
             fit_done = torch.cuda.Event()
             fit_done.record(cur)
             self._fit_hist.append(fit_done)

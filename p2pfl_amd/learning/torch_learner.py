@@ -97,10 +97,6 @@ class TorchLearner(NodeLearner):
 
         # per-step metric sink (reference: the Lightning logger plugged into the Trainer)
         self.metrics_logger = FederatedLogger(self_addr)
-        # True: fit() skips the LAST epoch's validation pass and the caller runs
-        # validate() itself -- the round runner overlaps it with the FedAvg
-        # collective of the freshly trained weights (parallel/rounds.py)
-        self.defer_final_validation = False
         # HIP-graph replay of the training step (mixed precision, device-resident data)
         self.use_step_graphs = use_step_graphs and os.environ.get("P2PFL_STEP_GRAPHS", "1") != "0"
         self._mt_opt: Any = None
@@ -441,8 +437,7 @@ class TorchLearner(NodeLearner):
                         if not self._fit_epoch_graph(opt, loader):
                             return
                     t1.record(cur)
-                    if not (self.defer_final_validation and _epoch == self.epochs - 1):
-                        self._validate()
+                    self._validate()
                     self._record_epoch_gpu(t0, t1)
                     continue
                 with logger.span(self._addr, "train_epoch"):
@@ -462,8 +457,7 @@ class TorchLearner(NodeLearner):
                                 self._log(k, float(v), step=self._step)
                 if self.arena is not None and not self.arena.grads_bound():
                     self.arena.rebind_grads()
-                if not (self.defer_final_validation and _epoch == self.epochs - 1):
-                    self._validate()
+                self._validate()
         except Exception as e:
             logger.error(self._addr, f"Fit error: {e}")
             raise

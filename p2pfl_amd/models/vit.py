@@ -9,10 +9,13 @@ MLP 3072, 86.6 M parameters.
 
 On an AMD GPU with the native extension loaded, the fused ops come from
 :mod:`p2pfl_amd.ops` (hand-written HIP kernels): LayerNorm forward/backward,
-bias+GELU forward/backward and the softmax cross-entropy loss; the plain
-GEMMs are hipBLASLt (``torch.matmul``) and multi-head attention is the
-hand-written MFMA kernel of ``csrc/attention.hip`` (forward + two-pass
-backward, straight on the QKV projection layout).  Optimiser: AdamW (fused over the arena by the learner).
+bias+GELU forward/backward and the softmax cross-entropy loss; every Linear
+product (patch embedding, QKV, projection, MLP, head -- forward, input and
+weight gradient) is the hand-written MFMA GEMM of ``csrc/gemm_pp.hip`` /
+``csrc/gemm.hip`` (``ops.linear``: per-shape kernel configuration, bias / GELU /
+pre-activation in the epilogue) and multi-head attention is the hand-written
+MFMA kernel of ``csrc/attention.hip`` (forward + two-pass backward, straight on
+the QKV projection layout).  Optimiser: AdamW (fused over the arena by the learner).
 """
 
 from __future__ import annotations

@@ -551,6 +551,12 @@ def conv2d(x: torch.Tensor, conv: nn.Conv2d) -> torch.Tensor:
         STATS["native_fwd"] += 1
         return _Conv2dNHWC.apply(x, conv.weight, _sym(conv.stride), _sym(conv.padding), _sym(conv.dilation))
     STATS["torch_fwd"] += 1
+    if x.is_cuda:
+        import importlib
+
+        if importlib.import_module("p2pfl_amd.ops.gemm").STRICT:
+            raise RuntimeError(f"native convolution refused {tuple(x.shape)} x {tuple(conv.weight.shape)} "
+                               f"stride {conv.stride} pad {conv.padding} (P2PFL_STRICT_NATIVE=1)")
     return conv(x)
 
 

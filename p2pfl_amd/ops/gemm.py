@@ -70,13 +70,29 @@ def supported(M: int, N: int, K: int, a_kmajor: bool, b_kmajor: bool) -> bool:
     return a_kmajor or M % 8 == 0
 
 
+# Products the MFMA kernels refuse (N % 8, K % 8 on a k-major operand, ...) fall back
+# to torch; every fallback is counted here, and P2PFL_STRICT_NATIVE=1 turns it into an
+# error (tests/test_gpu_native_coverage.py runs whole ResNet / ViT fits that way).
+STATS = {"native": 0, "torch": 0}
+STRICT = os.environ.get("P2PFL_STRICT_NATIVE", "0") == "1"
+
+
+def torch_fallback(what: str) -> None:
+    """Record (or, strict, refuse) a GPU product that leaves the hand-written kernels."""
+    STATS["torch"] += 1
+    if STRICT:
+        raise RuntimeError(f"native GEMM path refused {what} (P2PFL_STRICT_NATIVE=1)")
+
+
 def _product(a, b, a_kmajor, b_kmajor, dtype, splits=1):
     """One Linear product on the MFMA kernel, or torch for shapes it does not take."""
     M = a.shape[0] if a_kmajor else a.shape[1]
     N = b.shape[0] if b_kmajor else b.shape[1]
     K = a.shape[1] if a_kmajor else a.shape[0]
     if supported(M, N, K, a_kmajor, b_kmajor):
+        STATS["native"] += 1
         return gemm(a, b, a_kmajor, b_kmajor, out_dtype=dtype, splits=splits)[0]
+    torch_fallback(f"M={M} N={N} K={K} a_kmajor={a_kmajor} b_kmajor={b_kmajor}")
     A = a if a_kmajor else a.t()
     B = b if b_kmajor else b.t()
     return (A @ B.t()).to(dtype)
@@ -207,15 +223,27 @@ def _rows(x: torch.Tensor) -> torch.Tensor:
 
 _NAT, _LIB = "native", "library"
 
-# Native configurations tried per product at first use: (variant, split-K).
-# From scripts/vit_gemm_sweep.py on the ViT-B/16 products (profiles/r5_vit_gemm_sweep.md):
-# the forward products by the ping-pong kernel (its 16x16x32 form on qkv / proj /
-# patch) or the 128 x 128 single-buffer tile (fc1), the input gradients by the
-# ping-pong kernel (2 in-launch slices when N = 768) or the 128 x 128 double
-# buffer, the weight gradients (K = 6304 tokens, few output tiles) by the
-# ping-pong kernel or the 4-stage ring at 6-8 slices.
-_FWD_CFGS = ((PP | PP_M16, 1), (PP, 1), (PP, 2), (2, 1), (10, 1))
-_DGRAD_CFGS = ((PP, 1), (PP, 2), (2, 1), (10, 1), (2, 3), (10, 2))
+# Native configurations tried per product at first use: (variant, split-K or, with
+# PP_SK, stream-K grid).  From scripts/sk_sweep.py on the ViT-B/16 products
+# (profiles/r6_vit_gemm_sweep.md): the N = 768 forward products and input gradients
+# on the 256 x 128 ping-pong tile (150 whole tiles, no partial sums), the wider ones
+# on the 256 x 256 ping-pong kernel (its 16x16x32 MFMA form where it wins) or the
+# 128 x 128 single-buffer tile, the weight gradients (K = 6304 tokens, few output
+# tiles) on the ping-pong kernel or the 4-stage ring at 6-8 K-slices.
+def _fwd_cfgs(M: int, N: int, K: int):
+    return ((PP | PP_N128, 1), (PP | PP_M16, 1), (PP, 1), (PP, 2), (10, 1), (2, 1),
+            (PP | PP_SK | PP_M16, _sk_grid(M, N, K)))
+
+
+def _dgrad_cfgs(M: int, N: int, K: int):
+    return ((PP | PP_N128, 1), (PP, 1), (PP, 2), (2, 1), (10, 1), (2, 3), (PP | PP_SK, _sk_grid(M, N, K)))
+
+
+def _sk_grid(M: int, N: int, K: int) -> int:
+    """Stream-K grid: one workgroup per CU, never more than the K-tile iterations."""
+    return max(1, min(240, sk_iters(M, N, K)))
+
+
 _WGRAD_CFGS = ((PP, 6), (PP, 8), (10, 6), (4096 | 2, 6), (2, 3))
 
 
@@ -231,8 +259,14 @@ def _cfg(choice: str) -> Tuple[int, int]:
 
 def _cfg_ok(v: int, sp: int, M: int, N: int, K: int, a_kmajor: bool, b_kmajor: bool, epilogue: bool) -> bool:
     """Configurations the kernels take for this product (no launch may fail)."""
-    if not supported(M, N, K, a_kmajor, b_kmajor) or (sp > 1 and K // sp < 256):
+    if not supported(M, N, K, a_kmajor, b_kmajor):
         return False
+    if v & PP and v & PP_SK:  # stream-K: any grid up to the iteration count, every epilogue
+        return pp_eligible_any(M, N, K, a_kmajor, b_kmajor) and 1 <= sp <= sk_iters(M, N, K)
+    if sp > 1 and K // sp < 256:
+        return False
+    if v & PP and v & PP_N128:  # the 256 x 128 tile: no split-K
+        return sp == 1 and pp_eligible_any(M, N, K, a_kmajor, b_kmajor)
     if v & PP:
         return pp_eligible_any(M, N, K, a_kmajor, b_kmajor) and not (epilogue and sp > IN_LAUNCH_MAX_SPLITS)
     return not (epilogue and sp > IN_LAUNCH_MAX_SPLITS)
@@ -240,34 +274,26 @@ def _cfg_ok(v: int, sp: int, M: int, N: int, K: int, a_kmajor: bool, b_kmajor: b
 
 class _LinearP(torch.autograd.Function):
     """``y = x W^T + b`` (or ``gelu(x W^T + b)``) whose three products -- forward,
-    input gradient, weight gradient -- each run on the path measured fastest for
-    its own shape (``plan``): the MFMA kernel of ``csrc/gemm*.hip`` or hipBLASLt.
-    The forward's bias / GELU ride in the native epilogue (which also keeps the
-    pre-activation for the backward), or in the fused bias+GELU kernel after a
-    bias-free hipBLASLt GEMM; the bias gradient is the column-sum kernel, or comes
-    out of the fused GELU backward."""
+    input gradient, weight gradient -- each run on the MFMA kernel configuration
+    (``csrc/gemm*.hip``: tile, pipeline, split-K / stream-K) measured fastest for its
+    own shape (``_plan``).  The forward's bias / GELU ride in the kernel's epilogue
+    (which also keeps the pre-activation for the backward); the bias gradient is the
+    column-sum kernel, or comes out of the fused GELU backward."""
 
     @staticmethod
     @torch.amp.custom_fwd(device_type="cuda")  # operands cast here, the bias keeps its dtype (no cast kernels)
     def forward(ctx, x, w, b, gelu, plan):
-        from p2pfl_amd.ops.fused import _fx
-
         fwd = plan[0]
         x2 = _rows(x.to(torch.bfloat16))
         wc = w.to(torch.bfloat16).contiguous()
+        v, sp = _cfg(fwd)
         pre = gb = None
-        nat = fwd.startswith(_NAT)
-        v, sp = _cfg(fwd) if ":" in fwd else (None, 1)
         if not gelu:
-            # the native epilogue reads an fp32 or a bf16 bias; hipBLASLt needs x's dtype
-            y = gemm(x2, wc, bias=b, variant=v, splits=sp)[0] if nat else F.linear(x2, wc, b.to(torch.bfloat16) if b is not None else None)
-        elif nat:
+            y = gemm(x2, wc, bias=b, variant=v, splits=sp)[0]  # the epilogue reads an fp32 or a bf16 bias
+        else:
             y, pre = gemm(x2, wc, bias=b, gelu=True, want_z=True, variant=v, splits=sp)  # pre-activation includes the bias
             gb = torch.zeros(w.shape[0], dtype=torch.float32, device=x.device)
-        else:
-            pre = torch.mm(x2, wc.t())  # bias-free; the GELU kernel adds it (fp32: fc1.bias is an fp32 parameter)
-            gb = b if (b.dtype == torch.float32 and b.is_contiguous()) else b.float().contiguous()
-            y = _fx().bias_gelu_fwd(pre, gb)
+        STATS["native"] += 1
         ctx.save_for_backward(x2, wc, pre, gb)
         ctx.gelu, ctx.plan = gelu, plan
         ctx.w_dtype = w.dtype
@@ -278,7 +304,7 @@ class _LinearP(torch.autograd.Function):
     @staticmethod
     @torch.amp.custom_bwd(device_type="cuda")
     def backward(ctx, dy):
-        from p2pfl_amd.ops.fused import _fx, _wgrad as wgrad_blas
+        from p2pfl_amd.ops.fused import _fx
 
         x2, w, pre, gb = ctx.saved_tensors
         _, dg, wg = ctx.plan
@@ -290,89 +316,85 @@ class _LinearP(torch.autograd.Function):
             db = _bias_grad(dz, ctx.b_dtype)
         dx = dw = None
         if ctx.needs_input_grad[0]:
-            if dg.startswith(_NAT):
-                v, sp = _cfg(dg) if ":" in dg else (None, 1)
-                dx = gemm(dz, w, True, False, splits=sp, variant=v)[0] if v is not None else _product(dz, w, True, False, torch.bfloat16)
-            else:
-                dx = torch.mm(dz, w)
-            dx = dx.view(ctx.xshape)
+            v, sp = _cfg(dg)
+            dx = gemm(dz, w, True, False, splits=sp, variant=v)[0].view(ctx.xshape)
         if ctx.needs_input_grad[1]:
-            if wg.startswith(_NAT):
-                dw = _wgrad(dz, x2, ctx.w_dtype, _cfg(wg) if ":" in wg else None)
-            else:
-                dw = wgrad_blas(dz, x2).to(ctx.w_dtype)
+            dw = _wgrad(dz, x2, ctx.w_dtype, _cfg(wg))
         if db is not None and ctx.b_dtype is not None:
             db = db.to(ctx.b_dtype)
         return dx, dw, db if (ctx.b_dtype is not None and ctx.needs_input_grad[2]) else None, None, None
 
 
-# "native" | "library" | "auto" (measured per product and shape, ops/autotune.py); env P2PFL_NATIVE_GEMM.
-# The library side is hipBLASLt (torch.mm / F.linear) plus the fused bias+GELU kernel.
+# P2PFL_NATIVE_GEMM: "native" / "auto" (default): every bf16 Linear product on the
+# hand-written kernels; "library": hipBLASLt (torch.mm / F.linear) -- an A/B
+# measurement knob only, never chosen at run time.
 _POLICY = autotune.policy("P2PFL_NATIVE_GEMM")
+_FALLBACK_CFG = _cfg_name(0, 1)  # the 128 x 128 double-buffer tile: takes every supported shape
 
 
 def _plan(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor], gelu: bool) -> Tuple[str, str, str]:
-    """(forward, input gradient, weight gradient): each product timed once per
-    shape on both paths (HIP events, ops/autotune.py) and the winner remembered.
-    Deciding per product, not per layer, keeps e.g. a native weight gradient that
-    beats hipBLASLt even where the library forward is faster
-    (profiles/r4_gemm_w4.md: native wins all four ViT weight gradients)."""
-    if _POLICY == _NAT:
-        return _NAT, _NAT, _NAT
+    """(forward, input gradient, weight gradient) kernel configurations: each product
+    timed once per shape over the native configurations it admits (HIP events,
+    ops/autotune.py) and the fastest remembered -- tile shape (256 x 256 / 256 x 128
+    ping-pong, 128 x 128), MFMA form, split-K or stream-K
+    (profiles/r6_vit_gemm_sweep.md).  Inside a capture nothing can be timed: an
+    unseen product takes a configuration every shape admits."""
     grad = torch.is_grad_enabled() and (x.requires_grad or w.requires_grad)
     M = x.numel() // x.shape[-1]
     N, K = w.shape
     keys = (("linear_fwd", M, N, K, bool(gelu), bias is not None), ("linear_dgrad", M, N, K), ("linear_wgrad", M, N, K))
     got = [autotune._CHOICE.get(k) for k in keys]
     if got[0] is not None and (not grad or (got[1] is not None and got[2] is not None)):
-        return (got[0], got[1], got[2]) if grad else (got[0], _LIB, _LIB)  # steady state: no allocation
-    if torch.cuda.is_current_stream_capturing():  # nothing can be timed inside a capture
-        return tuple(g or _NAT for g in got)  # type: ignore[return-value]
-    from p2pfl_amd.ops.fused import _fx, _wgrad as wgrad_blas
-
+        return (got[0], got[1] or _FALLBACK_CFG, got[2] or _FALLBACK_CFG)  # steady state: no allocation
+    if torch.cuda.is_current_stream_capturing():
+        return tuple(g or _FALLBACK_CFG for g in got)  # type: ignore[return-value]
     x2 = x.detach().reshape(M, K).to(torch.bfloat16)
     wd = w.detach().to(torch.bfloat16).contiguous()
     bd = bias.detach() if bias is not None else None
-    bd16 = bd.to(torch.bfloat16) if bd is not None else None
-    g32 = bd.float().contiguous() if bd is not None else None
-
-    def fwd_library():
-        if gelu:
-            _fx().bias_gelu_fwd(torch.mm(x2, wd.t()), g32)
-        else:
-            F.linear(x2, wd, bd16)
-
     epi = gelu or bias is not None
     fwd_c = [(_cfg_name(v, sp), (lambda v=v, sp=sp: gemm(x2, wd, bias=bd, gelu=gelu, want_z=gelu and grad, variant=v, splits=sp)))
-             for v, sp in _FWD_CFGS if _cfg_ok(v, sp, M, N, K, True, True, epi)]
-    fwd = autotune.choose(keys[0], fwd_c + [(_LIB, fwd_library)])
+             for v, sp in _fwd_cfgs(M, N, K) if _cfg_ok(v, sp, M, N, K, True, True, epi)]
+    fwd = autotune.choose(keys[0], fwd_c or [(_FALLBACK_CFG, lambda: None)])
     if not grad:
-        return fwd, _LIB, _LIB
+        return fwd, _FALLBACK_CFG, _FALLBACK_CFG
     dy = torch.randn(M, N, device=x.device).to(torch.bfloat16)
     dg_c = [(_cfg_name(v, sp), (lambda v=v, sp=sp: gemm(dy, wd, True, False, splits=sp, variant=v)))
-            for v, sp in _DGRAD_CFGS if _cfg_ok(v, sp, M, K, N, True, False, False)]
-    dg = autotune.choose(keys[1], dg_c + [(_LIB, lambda: torch.mm(dy, wd))])
+            for v, sp in _dgrad_cfgs(M, K, N) if _cfg_ok(v, sp, M, K, N, True, False, False)]
+    dg = autotune.choose(keys[1], dg_c or [(_FALLBACK_CFG, lambda: None)])
     wg_c = [(_cfg_name(v, sp), (lambda v=v, sp=sp: _wgrad(dy, x2, torch.bfloat16, (v, sp))))
             for v, sp in _WGRAD_CFGS if _cfg_ok(v, sp, N, K, M, False, False, False)]
-    wg = autotune.choose(keys[2], wg_c + [(_LIB, lambda: wgrad_blas(dy, x2))])
+    wg = autotune.choose(keys[2], wg_c or [(_FALLBACK_CFG, lambda: None)])
     return fwd, dg, wg
 
 
+def _bf16_call(x: torch.Tensor) -> bool:
+    """A bf16 product: a bf16 input, or an fp32 one under bf16 autocast (an fp32
+    product outside autocast keeps fp32 math)."""
+    return x.dtype == torch.bfloat16 or (
+        x.dtype == torch.float32 and torch.is_autocast_enabled("cuda") and torch.get_autocast_dtype("cuda") == torch.bfloat16)
+
+
 def _ok(x: torch.Tensor, w: torch.Tensor) -> bool:
-    """bf16 products on the GPU: a bf16 input, or an fp32 one under bf16 autocast
-    (an fp32 product outside autocast keeps fp32 math on hipBLASLt)."""
+    """bf16 products on the GPU whose shapes the kernels take."""
     from p2pfl_amd.ops import _gpu
 
-    bf16 = x.dtype == torch.bfloat16 or (
-        x.dtype == torch.float32 and torch.is_autocast_enabled("cuda") and torch.get_autocast_dtype("cuda") == torch.bfloat16)
-    return _gpu(x) and bf16 and w.shape[0] % 8 == 0 and w.shape[1] % 8 == 0 and x.shape[-1] == w.shape[1]
+    return _gpu(x) and _bf16_call(x) and w.shape[0] % 8 == 0 and w.shape[1] % 8 == 0 and x.shape[-1] == w.shape[1]
+
+
+def _library(x: torch.Tensor) -> bool:
+    """hipBLASLt for this call: the A/B knob, or a bf16 product the kernels refuse
+    (counted, and refused under P2PFL_STRICT_NATIVE)."""
+    if _POLICY == _LIB:
+        return True
+    torch_fallback(f"Linear {tuple(x.shape)}")
+    return True
 
 
 def linear(x: torch.Tensor, weight: torch.Tensor, bias: Optional[torch.Tensor] = None) -> torch.Tensor:
-    """``F.linear`` with each of its three products on the MFMA GEMM or hipBLASLt, per measured shape."""
+    """``F.linear`` with its three products on the MFMA GEMM (per-shape kernel configuration)."""
     if _POLICY != _LIB and _ok(x, weight):
         return _LinearP.apply(x, weight, bias, False, _plan(x, weight, bias, False))
-    if x.is_cuda:
+    if x.is_cuda and (_POLICY == _LIB or _bf16_call(x)) and _library(x):
         from p2pfl_amd.ops.fused import linear as linear_blas
 
         return linear_blas(x, weight, bias)
@@ -383,7 +405,7 @@ def linear_gelu(x: torch.Tensor, weight: torch.Tensor, bias: torch.Tensor) -> to
     """``gelu(F.linear(x, weight, bias))`` (exact erf GELU), fused epilogue."""
     if _POLICY != _LIB and _ok(x, weight):
         return _LinearP.apply(x, weight, bias, True, _plan(x, weight, bias, True))
-    if x.is_cuda:
+    if x.is_cuda and (_POLICY == _LIB or _bf16_call(x)) and _library(x):
         from p2pfl_amd.ops.fused import bias_gelu, linear as linear_blas
 
         return bias_gelu(linear_blas(x, weight, None), bias)

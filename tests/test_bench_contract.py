@@ -55,10 +55,10 @@ def test_bench_json_line(world, launcher):
 
 
 @pytest.mark.timeout(600)
-def test_bench_allreduce_mode_still_available():
-    cmd = [sys.executable, "bench.py", "--gpus", "1", "--steps", "1", "--warmup", "1", "--impl", "torch",
-           "--number-sub", "200", "--aggregation", "allreduce"]
+def test_reference_baseline_script_runs():
+    """The reference-equivalent baseline (scripts/reference_baseline.py) still runs."""
+    cmd = [sys.executable, "scripts/reference_baseline.py", "--steps", "1", "--warmup", "0", "--number-sub", "200"]
     r = subprocess.run(cmd, cwd=ROOT, env=_env(), capture_output=True, text=True, timeout=560)
     assert r.returncode == 0, r.stderr[-3000:]
     rec = _json_lines(r.stdout)[0]
-    assert rec["config"]["parallelism"] == "fedavg-allreduce-dp1"
+    assert rec["ms_per_round"] > 0 and rec["dtype"] == "fp32"

@@ -130,21 +130,21 @@ def test_graph_replay_matches_eager():
     assert abs(outs[0][1]["test_loss"] - outs[1][1]["test_loss"]) < 1e-4
 
 
-def test_fused_learner_accuracy_and_round_runner():
+def test_fused_learner_accuracy_over_rounds():
+    """evaluate -> fit -> set_parameters(own model) rounds, as the stages drive a lone
+    peer: the test accuracy rises and the loss falls."""
     from p2pfl_amd.data import MnistFederatedDM
     from p2pfl_amd.learning.fused_cnn import FusedCNNLearner
-    from p2pfl_amd.parallel import CollectiveFedAvg, init_distributed
-    from p2pfl_amd.parallel.rounds import FederatedRoundRunner
 
-    env = init_distributed()
-    ln = FusedCNNLearner(CNN(seed=11), MnistFederatedDM(sub_id=0, number_sub=20), "peer", 1, device=env.device)
-    runner = FederatedRoundRunner(ln, CollectiveFedAvg(env))
-    r0 = runner.run_round()
-    r1 = runner.run_round()
-    r2 = runner.run_round()
-    r3 = runner.run_round()
-    accs = [r.metrics["test_metric"] for r in (r1, r2, r3)]
-    assert max(accs) > 0.8 and r3.metrics["test_loss"] < r0.metrics["test_loss"], (r0.metrics, accs)
+    ln = FusedCNNLearner(CNN(seed=11), MnistFederatedDM(sub_id=0, number_sub=20), "peer", 1, device=torch.device("cuda"))
+    res = []
+    for _ in range(4):
+        res.append(ln.evaluate())
+        ln.fit()
+        ln.set_parameters(ln.get_parameters().clone())
+    res.append(ln.evaluate())
+    accs = [r["test_metric"] for r in res[2:]]
+    assert max(accs) > 0.8 and res[-1]["test_loss"] < res[0]["test_loss"], (res, accs)
 
 
 def test_fused_and_torch_peers_federate():
@@ -277,3 +277,40 @@ def test_evaluation_pass_beside_next_fit_reads_its_snapshot():
     # (the loss sum's fp32 accumulation order may differ in the last bit)
     assert res[0]["test_metric"] == res[1]["test_metric"], res
     assert abs(res[0]["test_loss"] - res[1]["test_loss"]) <= 1e-6 * abs(res[1]["test_loss"]), res
+
+
+@pytest.mark.parametrize("kind", ["fused", "torch"])
+def test_weight_guard_orders_snapshots_around_fit(kind):
+    """Lazy stream hand-off (learning/arena.py WeightGuard): the learner trains on its
+    own stream and never hands it back to the caller's.  A gossip snapshot queued on
+    the default stream behind a long kernel must still read the PRE-fit weights when
+    fit() is enqueued right after it (WAR: the fit waits for the snapshot's read), and
+    a snapshot taken right after fit() with no host sync must read the trained ones
+    (RAW: the snapshot waits for the fit's ready event)."""
+    from p2pfl_amd.data import MnistFederatedDM
+    from p2pfl_amd.learning.fused_cnn import FusedCNNLearner
+    from p2pfl_amd.learning.torch_learner import TorchLearner
+    from p2pfl_amd.models import MLP
+
+    ops.ext()
+    dev = torch.device("cuda")
+    if kind == "fused":
+        ln = FusedCNNLearner(CNN(seed=9), MnistFederatedDM(sub_id=0, number_sub=40), "war", 1, device=dev)
+    else:
+        ln = TorchLearner(MLP(seed=9), MnistFederatedDM(sub_id=0, number_sub=40), "war-t", 1, device=dev)
+    assert ln._stream_for_block() is not None  # a private compute stream (NODE_STREAMS auto)
+    ln.fit()
+    ln.drain()
+    torch.cuda.synchronize()
+    before = ln.live_parameters().flat.clone()
+    torch.cuda._sleep(int(3e8))  # ~0.1 s on the default stream
+    snap = ln.snapshot_parameters()  # its clone waits behind the sleep
+    ln.fit()  # enqueued at once on the learner's stream
+    torch.cuda.synchronize()
+    assert torch.equal(snap.flat, before), "the fit overwrote the weights before the snapshot read them"
+    assert not torch.equal(ln.live_parameters().flat, before)  # the fit did train
+    ln.fit()
+    snap2 = ln.snapshot_parameters()  # no host sync in between
+    torch.cuda.synchronize()
+    assert torch.equal(snap2.flat, ln.live_parameters().flat), "the snapshot read the weights before the fit ended"
+    ln.drain()

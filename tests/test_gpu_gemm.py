@@ -86,13 +86,20 @@ def test_gemm_epilogue_bias_gelu_residual(bias_dtype):
     torch.testing.assert_close(z.float(), zref, atol=3e-2, rtol=8e-3)  # z is stored in bf16
 
 
-_PLANS = [None] + [(f, d, w) for f in ("native", "library") for d in ("native", "library") for w in ("native", "library")]
+# None = the measured plan; then explicit kernel configurations per product ("native:variant:splits"):
+# 128 x 128 tile, 256 x 256 ping-pong (32x32x16 / 16x16x32 MFMA), 256 x 128 ping-pong, split-K, stream-K
+_PLANS = [None,
+          ("native:0:1", "native:0:1", "native:2:3"),
+          ("native:2048:1", "native:2048:2", "native:2048:6"),
+          ("native:67584:1", "native:2099200:1", "native:4098:6"),
+          ("native:2099200:1", "native:133120:24", "native:10:6"),
+          ("native:198656:17", "native:2048:1", "native:2048:8")]
 
 
 @pytest.mark.parametrize("plan", _PLANS)
 @pytest.mark.parametrize("gelu", [False, True])
 def test_linear_autograd_vs_fp32(gelu, plan):
-    """Every mix of paths for the three products (forward / input gradient / weight
+    """Kernel configurations for the three products (forward / input gradient / weight
     gradient, chosen per product by ops.gemm._plan) against fp32; None = the measured plan."""
     import importlib
 
