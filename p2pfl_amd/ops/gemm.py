@@ -202,7 +202,7 @@ def _wgrad(dy2: torch.Tensor, x2: torch.Tensor, dtype: torch.dtype, cfg: Optiona
     """dW[n, k] = sum_m dy[m, n] x[m, k]: both operands m-major, split over m."""
     M, N = dy2.shape
     K = x2.shape[1]
-    if cfg is None:
+    if cfg is None or not supported(N, K, M, False, False):  # e.g. a last batch of < 8 tokens
         return _product(dy2, x2, False, False, dtype, splits_for(N, K, M))
     v, sp = cfg
     return gemm(dy2, x2, False, False, out_dtype=dtype, splits=sp, variant=v)[0]
@@ -230,18 +230,15 @@ _NAT, _LIB = "native", "library"
 # on the 256 x 256 ping-pong kernel (its 16x16x32 MFMA form where it wins) or the
 # 128 x 128 single-buffer tile, the weight gradients (K = 6304 tokens, few output
 # tiles) on the ping-pong kernel or the 4-stage ring at 6-8 K-slices.
+# The stream-K schedule (PP_SK) is not offered: on every ViT product its partial-tile
+# fix-up (256 KB fp32 per workgroup, ~15-18 us of chip-wide traffic) lost to the
+# 256 x 128 tile's whole tiles (profiles/r6_vit_gemm_sweep.md, scripts/sk_anatomy.py).
 def _fwd_cfgs(M: int, N: int, K: int):
-    return ((PP | PP_N128, 1), (PP | PP_M16, 1), (PP, 1), (PP, 2), (10, 1), (2, 1),
-            (PP | PP_SK | PP_M16, _sk_grid(M, N, K)))
+    return ((PP | PP_N128, 1), (PP | PP_M16, 1), (PP, 1), (PP, 2), (10, 1), (2, 1))
 
 
 def _dgrad_cfgs(M: int, N: int, K: int):
-    return ((PP | PP_N128, 1), (PP, 1), (PP, 2), (2, 1), (10, 1), (2, 3), (PP | PP_SK, _sk_grid(M, N, K)))
-
-
-def _sk_grid(M: int, N: int, K: int) -> int:
-    """Stream-K grid: one workgroup per CU, never more than the K-tile iterations."""
-    return max(1, min(240, sk_iters(M, N, K)))
+    return ((PP | PP_N128, 1), (PP, 1), (PP, 2), (2, 1), (10, 1), (2, 3))
 
 
 _WGRAD_CFGS = ((PP, 6), (PP, 8), (10, 6), (4096 | 2, 6), (2, 3))
@@ -317,7 +314,10 @@ class _LinearP(torch.autograd.Function):
         dx = dw = None
         if ctx.needs_input_grad[0]:
             v, sp = _cfg(dg)
-            dx = gemm(dz, w, True, False, splits=sp, variant=v)[0].view(ctx.xshape)
+            if supported(dz.shape[0], w.shape[1], w.shape[0], True, False):
+                dx = gemm(dz, w, True, False, splits=sp, variant=v)[0].view(ctx.xshape)
+            else:
+                dx = _product(dz, w, True, False, torch.bfloat16).view(ctx.xshape)
         if ctx.needs_input_grad[1]:
             dw = _wgrad(dz, x2, ctx.w_dtype, _cfg(wg))
         if db is not None and ctx.b_dtype is not None:

@@ -16,6 +16,8 @@
 #                                           (PROF_GAPS=1: also the GPU idle-gap table, tools/gap_summary.py)
 #   scripts/gpu.sh overlap [on|off] [rounds] 8 virtual ResNet-50 peers (fault-tolerance scenario) under a
 #                                           kernel trace + cross-stream overlap summary of training / FedAvg
+#   scripts/gpu.sh rccl_overlap [N]         N split-host ranks (default 2) under a kernel trace: RCCL transfers /
+#                                           FedAvg fold beside training, per rank (tools/overlap_summary.py)
 #   scripts/gpu.sh pmc <tag> <cmd...>       rocprofv3 --kernel-trace --pmc passes of <cmd> (one counter group
 #                                           per pass, each under its own kill timer; groups from $PMC_PASSES,
 #                                           ";"-separated) + scripts/pmc_summary.py table -> gpurun_out/pmc_<tag>.md
@@ -88,6 +90,24 @@ run_mode() {
       step 120 "overlap_${mode}_fedavg" python tools/overlap_summary.py "$csv" --a 'wsum|weighted' \
         --b 'conv_kernel|p2bn|sgd_mt|p2head' --out "$d/overlap_fedavg.md"
       rm -f "$csv" ;;
+    rccl_overlap)
+      # 2 split-host ranks (a real 2-rank RCCL communicator over RCCL's socket transport,
+      # time-sharing the one GPU -- not xGMI) under a kernel trace, one trace per rank:
+      # how much of the RCCL transfer kernels and of the FedAvg fold ran beside training
+      local n=${1:-2} d=gpurun_out/prof_rccl
+      rm -rf "$d"
+      step 600 rccl_overlap env P2PFL_RCCL_SPLIT_HOSTS=1 P2PFL_BENCH_SPANS=1 rocprofv3 --kernel-trace --output-format csv \
+        -d "$d" -o %pid%_run -- python -u bench.py --gpus "$n" --steps 6 --warmup 2 --watchdog 240
+      local csv k=0
+      for csv in $(ls "$d"/*kernel_trace.csv "$d"/*/*kernel_trace.csv 2>/dev/null); do
+        k=$((k + 1))
+        step 120 "rccl_overlap_r${k}_nccl" python tools/overlap_summary.py "$csv" --a 'nccl|rccl' \
+          --b 'p2cnn::' --out "$d/overlap_nccl_$k.md"
+        step 120 "rccl_overlap_r${k}_wsum" python tools/overlap_summary.py "$csv" --a 'wsum' \
+          --b 'p2cnn::' --out "$d/overlap_wsum_$k.md"
+        step 120 "rccl_overlap_r${k}_timeline" python tools/rccl_timeline.py "$csv" --out "$d/timeline_$k.md"
+        rm -f "$csv"
+      done ;;
     pmc)
       # per-pass limits of the hardware (MI355X_MICROARCH.md): <= 8 SQ, 4 TCC (FETCH_SIZE 3, WRITE_SIZE 2), 2 GRBM
       local tag=$1; shift
