@@ -76,6 +76,10 @@ run_mode() {
       if [ -n "${PROF_GAPS:-}" ]; then  # idle-gap table of the trace, then drop it (too big to copy back)
         step 120 "prof_${tag}_gaps" python tools/gap_summary.py "gpurun_out/prof_$tag/run_kernel_trace.csv" \
           --window-ms "${PROF_WINDOW_MS:-150}" --out "gpurun_out/prof_${tag}_gaps.md"
+        if [ -n "${PROF_OVERLAP:-}" ]; then  # "A_REGEX;B_REGEX": cross-stream overlap of two kernel classes
+          step 120 "prof_${tag}_overlap" python tools/overlap_summary.py "gpurun_out/prof_$tag/run_kernel_trace.csv" \
+            --a "${PROF_OVERLAP%%;*}" --b "${PROF_OVERLAP#*;}" --out "gpurun_out/prof_${tag}_overlap.md"
+        fi
         rm -f "gpurun_out/prof_$tag/run_kernel_trace.csv"
       fi ;;
     overlap)
