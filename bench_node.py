@@ -39,6 +39,7 @@ def main() -> None:
     ap.add_argument("--number-sub", type=int, default=20)
     ap.add_argument("--learner", choices=["fused", "torch"], default="fused")
     ap.add_argument("--watchdog", type=float, default=600)
+    ap.add_argument("--log-level", default="WARNING", help="node log level (INFO shows every stage / gossip step)")
     args = ap.parse_args()
     import faulthandler
 
@@ -52,7 +53,7 @@ def main() -> None:
     from p2pfl_amd.settings import Settings
     from p2pfl_amd.utils import wait_4_results, wait_convergence
 
-    Settings.LOG_LEVEL = "WARNING"
+    Settings.LOG_LEVEL = args.log_level
     Settings.TRAIN_SET_SIZE = max(Settings.TRAIN_SET_SIZE, args.peers)
     if args.learner == "fused":
         from p2pfl_amd.learning.fused_cnn import FusedCNNLearner as L
@@ -76,6 +77,7 @@ def main() -> None:
         ends = sorted(s.start + s.duration for s in logger.tracer.spans(nodes[0].addr, "stage:RoundFinishedStage"))
         per_round = [b - a for a, b in zip(ends, ends[1:])]
         steady = sum(per_round) / len(per_round) if per_round else total / args.rounds
+        median = sorted(per_round)[len(per_round) // 2] if per_round else steady
         first = (ends[0] - t0) if ends else total
         n_train = len(nodes[0].data.train_dataloader().dataset)
         acc = nodes[0].state.learner.evaluate()["test_metric"] if nodes[0].state.learner else None
@@ -91,6 +93,8 @@ def main() -> None:
                 "higher_is_better": False,
                 "peers": args.peers,
                 "rounds": args.rounds,
+                "median_round_ms": round(median * 1e3, 2),
+                "rounds_ms": [round(x * 1e3, 2) for x in per_round],
                 "first_round_ms": round(first * 1e3, 2),
                 "total_s": round(total, 3),
                 "samples_per_sec_per_peer": round(n_train * args.epochs / steady, 1),

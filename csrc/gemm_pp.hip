@@ -721,7 +721,7 @@ __global__ __launch_bounds__(512) void gemm_pp_kernel(GemmParams p, int tiles_m,
 //   ph1 Ahi(j+1)->b1   ph2 Alo,B(j+2)->b0   ph3 Ahi(j+2)->b0   ph4 Alo,B(j+3)->b1
 // (a piece is restaged one phase after its last read), so every phase retires
 // exactly the piece(s) the next phase reads with one s_waitcnt vmcnt(6).
-template <class SA, class SB, bool KA, bool KB, int EPI>
+template <class SA, class SB, bool KA, bool KB, int EPI, bool M16>
 __global__ __launch_bounds__(512) void gemm_pp128_kernel(GemmParams p, int tiles_m, int tiles_n) {
   constexpr int LROW = 128 * 2 + 16;  // bf16 staging image [256][128] + 16 B row pad
   constexpr int SMEM = 6 * TILE > 256 * LROW ? 6 * TILE : 256 * LROW;
@@ -747,12 +747,20 @@ __global__ __launch_bounds__(512) void gemm_pp128_kernel(GemmParams p, int tiles
   sa.init(p.a, p.lda, p.M, p.K, m0, grp, gt);
   sb.init(p.b, p.ldb, p.N, p.K, n0, grp, gt);
 
-  constexpr int NI = 4, NA = 2, NKS = 4;
-  f32x16 acc[NI];
+  // 32x32x16 form: 4 row blocks of 32 x 1 column block of 32 (f32x16 each), per phase
+  // 2 A blocks x 4 k-substeps of 16; M16 (16x16x32, variant bit 16; the chip holds a
+  // higher clock under it): 8 row blocks of 16 x 2 column blocks of 16 (f32x4 each),
+  // per phase 4 A blocks x 2 B blocks x 2 k-substeps of 32 -- same registers
+  constexpr int NI = M16 ? 8 : 4, NJ = M16 ? 2 : 1, NA = M16 ? 4 : 2, NB = M16 ? 2 : 1, NKS = M16 ? 2 : 4;
+  constexpr int RBLK = M16 ? 16 : 32, TR_KS = M16 ? 8192 : 4096;
+  using AccT = std::conditional_t<M16, f32x4, f32x16>;
+  AccT acc[NI][NJ];
 #pragma unroll
   for (int i = 0; i < NI; ++i)
 #pragma unroll
-    for (int e = 0; e < 16; ++e) acc[i][e] = 0.f;
+    for (int j = 0; j < NJ; ++j)
+#pragma unroll
+      for (int e = 0; e < (M16 ? 4 : 16); ++e) acc[i][j][e] = 0.f;
 
   // LDS piece q (0 Alo, 1 Ahi, 2 B) of buffer b at (2 q + b) x 16 KB
   auto stage = [&](int q, int tile, int buf) __attribute__((always_inline)) {
@@ -768,34 +776,34 @@ __global__ __launch_bounds__(512) void gemm_pp128_kernel(GemmParams p, int tiles
         sb.dma(d, 0, c, l);
     }
   };
-  const int lr = lane % 32, lc = lane / 32;
+  const int lr = lane % RBLK, lc = lane / RBLK;
   auto kbase = [&](int row0, int ks) __attribute__((always_inline)) {
-    const int c = (2 * ks) | lc;
+    const int c = M16 ? (4 * ks) | lc : (2 * ks) | lc;
     return uint32_t((row0 + lr) * 128 + ((c ^ ((lr >> 1) & 7)) << 4));
   };
-  constexpr int NVA = KA ? NKS : 2 * NA, NVB = KB ? NKS : 2;
+  constexpr int NVA = KA ? NKS : 2 * NA, NVB = KB ? NKS : 2 * NB;
   uint32_t va[NVA], vb[NVB];
   if constexpr (KA) {
 #pragma unroll
     for (int ks = 0; ks < NKS; ++ks) va[ks] = kbase(64 * wr, ks);
   } else {
 #pragma unroll
-    for (int u = 0; u < 2 * NA; ++u) va[u] = mn_base<false>(64 * wr + 32 * (u >> 1), u & 1, lane);
+    for (int u = 0; u < 2 * NA; ++u) va[u] = mn_base<M16>(64 * wr + RBLK * (u >> 1), u & 1, lane);
   }
   if constexpr (KB) {
 #pragma unroll
     for (int ks = 0; ks < NKS; ++ks) vb[ks] = 4 * TILE + kbase(32 * wc, ks);
   } else {
 #pragma unroll
-    for (int u = 0; u < 2; ++u) vb[u] = 4 * TILE + mn_base<false>(32 * wc, u & 1, lane);
+    for (int u = 0; u < 2 * NB; ++u) vb[u] = 4 * TILE + mn_base<M16>(32 * wc + RBLK * (u >> 1), u & 1, lane);
   }
   auto frag_pp = [&](const uint32_t* v, bool kmaj, int cst, int i, int ks) __attribute__((always_inline)) {
-    if (kmaj) return *reinterpret_cast<const uint4*>(smem + v[ks] + cst + i * 32 * 128);
+    if (kmaj) return *reinterpret_cast<const uint4*>(smem + v[ks] + cst + i * RBLK * 128);
     uint4 out;
     const s16x4 x0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-        (__attribute__((address_space(3))) s16x4*)(smem + v[2 * i] + cst + ks * 4096));
+        (__attribute__((address_space(3))) s16x4*)(smem + v[2 * i] + cst + ks * TR_KS));
     const s16x4 x1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-        (__attribute__((address_space(3))) s16x4*)(smem + v[2 * i + 1] + cst + ks * 4096));
+        (__attribute__((address_space(3))) s16x4*)(smem + v[2 * i + 1] + cst + ks * TR_KS));
     const uint2 u0 = __builtin_bit_cast(uint2, x0), u1 = __builtin_bit_cast(uint2, x1);
     out.x = u0.x;
     out.y = u0.y;
@@ -803,7 +811,7 @@ __global__ __launch_bounds__(512) void gemm_pp128_kernel(GemmParams p, int tiles
     out.w = u1.y;
     return out;
   };
-  uint4 fa[NA][NKS], fb[NKS];
+  uint4 fa[NA][NKS], fb[NB][NKS];
   auto read_a = [&](int buf, int h) __attribute__((always_inline)) {
 #pragma unroll
     for (int ks = 0; ks < NKS; ++ks)
@@ -812,14 +820,23 @@ __global__ __launch_bounds__(512) void gemm_pp128_kernel(GemmParams p, int tiles
   };
   auto read_b = [&](int buf) __attribute__((always_inline)) {
 #pragma unroll
-    for (int ks = 0; ks < NKS; ++ks) fb[ks] = frag_pp(vb, KB, buf * TILE, 0, ks);
+    for (int ks = 0; ks < NKS; ++ks)
+#pragma unroll
+      for (int j = 0; j < NB; ++j) fb[j][ks] = frag_pp(vb, KB, buf * TILE, j, ks);
   };
   auto mma = [&](int h) __attribute__((always_inline)) {
     __builtin_amdgcn_s_setprio(1);
 #pragma unroll
     for (int ks = 0; ks < NKS; ++ks)
 #pragma unroll
-      for (int i = 0; i < NA; ++i) acc[NA * h + i] = mfma(fb[ks], fa[i][ks], acc[NA * h + i]);
+      for (int i = 0; i < NA; ++i)
+#pragma unroll
+        for (int j = 0; j < NB; ++j) {
+          if constexpr (M16)
+            acc[NA * h + i][j] = mfma16(fb[j][ks], fa[i][ks], acc[NA * h + i][j]);
+          else
+            acc[NA * h + i][0] = mfma(fb[0][ks], fa[i][ks], acc[NA * h + i][0]);
+        }
     __builtin_amdgcn_s_setprio(0);
   };
   auto bar = []() __attribute__((always_inline)) {
@@ -899,13 +916,24 @@ __global__ __launch_bounds__(512) void gemm_pp128_kernel(GemmParams p, int tiles
     }
     if (wr == 0) bar();  // balance the stagger
   }
-  // ---- epilogue: block i -> tile rows 128 (i >> 1) + 64 wr + 32 (i & 1) + (lane & 31),
-  // cols 32 wc + 8 g + 4 (lane >> 5) + e in acc[i][4 g + e]
+  // ---- epilogue.  32x32x16: block i -> tile rows 128 (i >> 1) + 64 wr + 32 (i & 1) +
+  // (lane & 31), cols 32 wc + 8 g + 4 (lane >> 5) + e in acc[i][0][4 g + e].  16x16x32:
+  // block (i, j) -> rows 128 (i >> 2) + 64 wr + 16 (i & 3) + (lane & 15), cols 32 wc +
+  // 16 j + 4 (lane >> 4) + e in acc[i][j][e]
   int ln;
   asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(ln));
   const int tid2 = wave * 64 + ln, hh = ln >> 5;
-  auto row_of = [&](int i) __attribute__((always_inline)) { return m0 + 128 * (i >> 1) + 64 * wr + 32 * (i & 1) + (ln & 31); };
-  auto col_of = [&](int g) __attribute__((always_inline)) { return n0 + 32 * wc + 8 * g + 4 * hh; };
+  auto row_of = [&](int i) __attribute__((always_inline)) {
+    return M16 ? m0 + 128 * (i >> 2) + 64 * wr + 16 * (i & 3) + (ln & 15) : m0 + 128 * (i >> 1) + 64 * wr + 32 * (i & 1) + (ln & 31);
+  };
+  // column group q: (32x32x16) g = q of the lane's 4 groups, (16x16x32) j = q of its 2 blocks
+  constexpr int NQ = M16 ? 2 : 4;
+  auto col_of = [&](int q) __attribute__((always_inline)) {
+    return M16 ? n0 + 32 * wc + 16 * q + 4 * (ln >> 4) : n0 + 32 * wc + 8 * q + 4 * hh;
+  };
+  auto accv = [&](int i, int q, int e) __attribute__((always_inline)) {
+    return M16 ? acc[i][q][e] : acc[i][0][4 * q + e];
+  };
   __syncthreads();  // LDS free for the bf16 staging image
   auto bias4 = [&](int n) __attribute__((always_inline)) {
     if (!p.bias) return f32x4{0.f, 0.f, 0.f, 0.f};
@@ -916,18 +944,18 @@ __global__ __launch_bounds__(512) void gemm_pp128_kernel(GemmParams p, int tiles
     }
     return *reinterpret_cast<const f32x4*>(reinterpret_cast<const float*>(p.bias) + n);
   };
-  f32x4 bv[4];
+  f32x4 bv[NQ];
   if constexpr (EPI != 0) {
 #pragma unroll
-    for (int g = 0; g < 4; ++g) bv[g] = bias4(min(col_of(g), p.N - 4));
+    for (int g = 0; g < NQ; ++g) bv[g] = bias4(min(col_of(g), p.N - 4));
   }
 #pragma unroll
   for (int i = 0; i < NI; ++i)
 #pragma unroll
-    for (int g = 0; g < 4; ++g) {
+    for (int g = 0; g < NQ; ++g) {
       const int m = row_of(i), n = col_of(g);
       if (m >= p.M || n >= p.N) continue;
-      float v[4] = {acc[i][4 * g], acc[i][4 * g + 1], acc[i][4 * g + 2], acc[i][4 * g + 3]};
+      float v[4] = {accv(i, g, 0), accv(i, g, 1), accv(i, g, 2), accv(i, g, 3)};
       const int64_t off = int64_t(m) * p.ldc + n;
       if constexpr (EPI != 0) {
 #pragma unroll
@@ -964,19 +992,27 @@ __global__ __launch_bounds__(512) void gemm_pp128_kernel(GemmParams p, int tiles
   }
 }
 
-template <bool KA, bool KB>
-static void launch_pp128(const GemmParams& p, hipStream_t s) {
+template <bool KA, bool KB, bool M16>
+static void launch_pp128_m(const GemmParams& p, hipStream_t s) {
   const int tm = (p.M + 255) / 256, tn = (p.N + 127) / 128;
   switch (epilogue_kind(p)) {
     case 0:
-      hipLaunchKernelGGL((gemm_pp128_kernel<PPSrc<KA>, PPSrc<KB>, KA, KB, 0>), dim3(tm * tn), dim3(512), 0, s, p, tm, tn);
+      hipLaunchKernelGGL((gemm_pp128_kernel<PPSrc<KA>, PPSrc<KB>, KA, KB, 0, M16>), dim3(tm * tn), dim3(512), 0, s, p, tm, tn);
       break;
     case 2:
-      hipLaunchKernelGGL((gemm_pp128_kernel<PPSrc<KA>, PPSrc<KB>, KA, KB, 2>), dim3(tm * tn), dim3(512), 0, s, p, tm, tn);
+      hipLaunchKernelGGL((gemm_pp128_kernel<PPSrc<KA>, PPSrc<KB>, KA, KB, 2, M16>), dim3(tm * tn), dim3(512), 0, s, p, tm, tn);
       break;
     default:
-      hipLaunchKernelGGL((gemm_pp128_kernel<PPSrc<KA>, PPSrc<KB>, KA, KB, 1>), dim3(tm * tn), dim3(512), 0, s, p, tm, tn);
+      hipLaunchKernelGGL((gemm_pp128_kernel<PPSrc<KA>, PPSrc<KB>, KA, KB, 1, M16>), dim3(tm * tn), dim3(512), 0, s, p, tm, tn);
   }
+}
+
+template <bool KA, bool KB>
+static void launch_pp128(const GemmParams& p, hipStream_t s) {
+  if (p.variant & PP_M16)
+    launch_pp128_m<KA, KB, true>(p, s);
+  else
+    launch_pp128_m<KA, KB, false>(p, s);
 }
 
 template <bool KA, bool KB, bool M16, bool SK>

@@ -105,10 +105,14 @@ class AddModelCommand(Command):
                 models_added = self.aggregator.add_model(params, list(contributors), weight)
             if models_added:
                 self.state.changed.bump()
+                # the report carries the round of the models it lists: the add that
+                # completes the aggregation can let the learning thread move on at once,
+                # and a report stamped with the NEW round is ignored by every peer still
+                # in this one -- they kept offering this node models until their gossip
+                # loop's equal-rounds exit (~GOSSIP_EXIT_ON_X_EQUAL_ROUNDS periods, 9 s
+                # stalls of the 8-peer bench_node rounds)
                 self.communication_protocol.broadcast(
-                    self.communication_protocol.build_msg(
-                        ModelsAggregatedCommand.get_name(), models_added, round=self.state.round
-                    )
+                    self.communication_protocol.build_msg(ModelsAggregatedCommand.get_name(), models_added, round=round)
                 )
         except DecodingParamsError:
             logger.error(self.state.addr, "Error decoding parameters.")

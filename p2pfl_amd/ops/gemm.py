@@ -234,11 +234,11 @@ _NAT, _LIB = "native", "library"
 # fix-up (256 KB fp32 per workgroup, ~15-18 us of chip-wide traffic) lost to the
 # 256 x 128 tile's whole tiles (profiles/r6_vit_gemm_sweep.md, scripts/sk_anatomy.py).
 def _fwd_cfgs(M: int, N: int, K: int):
-    return ((PP | PP_N128, 1), (PP | PP_M16, 1), (PP, 1), (PP, 2), (10, 1), (2, 1))
+    return ((PP | PP_N128, 1), (PP | PP_N128 | PP_M16, 1), (PP | PP_M16, 1), (PP, 1), (PP, 2), (10, 1), (2, 1))
 
 
 def _dgrad_cfgs(M: int, N: int, K: int):
-    return ((PP | PP_N128, 1), (PP, 1), (PP, 2), (2, 1), (10, 1), (2, 3))
+    return ((PP | PP_N128, 1), (PP | PP_N128 | PP_M16, 1), (PP, 1), (PP, 2), (2, 1), (10, 1), (2, 3))
 
 
 _WGRAD_CFGS = ((PP, 6), (PP, 8), (10, 6), (4096 | 2, 6), (2, 3))

@@ -372,30 +372,33 @@ def test_stream_k_refuses_bad_grid():
 
 
 # ---- 256 x 128 ping-pong tile (variant bits 11 + 21) --------------------------------------
+@pytest.mark.parametrize("m16", [False, True], ids=["mfma32", "mfma16"])
 @pytest.mark.parametrize("a_kmajor,b_kmajor", [(True, True), (True, False), (False, True), (False, False)])
 @pytest.mark.parametrize("M,N,K", [(512, 256, 256), (296, 200, 128), (1000, 776, 448), (264, 520, 200), (6304, 768, 3072),
                                    (72, 136, 64)])
-def test_pingpong128_layouts_vs_fp32(a_kmajor, b_kmajor, M, N, K):
+def test_pingpong128_layouts_vs_fp32(a_kmajor, b_kmajor, M, N, K, m16):
     """The 256 x 128 tile: every layout, M / N tails (clamped rows, masked stores), odd and
     even K-tile counts (the two-K-tile phase schedule's tail), a K tail (m/n-major only)."""
-    from p2pfl_amd.ops.gemm import PP, PP_N128
+    from p2pfl_amd.ops.gemm import PP, PP_M16, PP_N128
 
     if (a_kmajor or b_kmajor) and K % 64:
         pytest.skip("k-major operands need K % 64 == 0 on this kernel")
     if not a_kmajor and M % 8:
         pytest.skip("m-major A needs M % 8 == 0")
+    v = PP | PP_N128 | (PP_M16 if m16 else 0)
     a, b = _operands(M, N, K, a_kmajor, b_kmajor, seed=M + 7 * N + K)
-    out, _ = ops.gemm(a, b, a_kmajor, b_kmajor, out_dtype=torch.float32, variant=PP | PP_N128)
+    out, _ = ops.gemm(a, b, a_kmajor, b_kmajor, out_dtype=torch.float32, variant=v)
     ref, _ = ops.gemm_reference(a, b, a_kmajor, b_kmajor)
     torch.testing.assert_close(out, ref, atol=5e-3, rtol=1e-4)
-    outb, _ = ops.gemm(a, b, a_kmajor, b_kmajor, out_dtype=torch.bfloat16, variant=PP | PP_N128)
+    outb, _ = ops.gemm(a, b, a_kmajor, b_kmajor, out_dtype=torch.bfloat16, variant=v)
     torch.testing.assert_close(outb.float(), ref, atol=0.25, rtol=1e-2)
 
 
-def test_pingpong128_exact_integers_and_epilogues():
-    from p2pfl_amd.ops.gemm import PP, PP_N128
+@pytest.mark.parametrize("m16", [False, True], ids=["mfma32", "mfma16"])
+def test_pingpong128_exact_integers_and_epilogues(m16):
+    from p2pfl_amd.ops.gemm import PP, PP_M16, PP_N128
 
-    v = PP | PP_N128
+    v = PP | PP_N128 | (PP_M16 if m16 else 0)
     M, N, K = 520, 392, 256
     A = torch.randint(-3, 4, (M, K), device="cuda").to(torch.bfloat16)
     B = (torch.arange(N * K, device="cuda").view(N, K) % 7 - 3).to(torch.bfloat16)
