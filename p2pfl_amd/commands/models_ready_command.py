@@ -37,6 +37,11 @@ class ModelsReadyCommand(Command):
             self.state.nei_status[source] = max(self.state.nei_status.get(source, -1), round)
             self.state.changed.bump()
         elif round > r:
+            # a neighbour already past this node's round: it needs none of this
+            # round's models (the partial-aggregate gossip stops offering them) and
+            # none of this round's diffusion
             logger.debug(self.state.addr, f"Models ready from {source} for round {round} ahead of ours ({r}).")
+            self.state.nei_status[source] = max(self.state.nei_status.get(source, -1), round)
+            self.state.changed.bump()
         else:
             logger.error(self.state.addr, f"Models ready from {source} in a late round. Ignored. {round} != {r} / {r - 1}")

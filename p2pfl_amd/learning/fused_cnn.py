@@ -461,9 +461,14 @@ class FusedCNNLearner(TorchLearner):
     # -- NodeLearner ------------------------------------------------------
     @staticmethod
     def _readback(stats: torch.Tensor) -> torch.Tensor:
-        """Pinned host copy of a device stats tensor, enqueued behind the pass."""
-        host = torch.empty(stats.shape, dtype=stats.dtype, pin_memory=True)
-        host.copy_(stats, non_blocking=True)
+        """Pinned host copy of a device stats tensor, enqueued behind the pass (under the
+        shared device gate: the host allocator queries events, which must never happen
+        beside another peer's capture -- hipErrorCapturedEvent)."""
+        from p2pfl_amd.learning.step_graph import GATE
+
+        with GATE.shared():
+            host = torch.empty(stats.shape, dtype=stats.dtype, pin_memory=True)
+            host.copy_(stats, non_blocking=True)
         return host
 
     def fit(self) -> None:
@@ -488,6 +493,8 @@ class FusedCNNLearner(TorchLearner):
         epoch by the stream.  The host runs at most ``RUN_AHEAD`` fits ahead of
         the GPU.
         """
+        from p2pfl_amd.learning.step_graph import GATE
+
         self._interrupt.clear()
         self._arena_changed()
         if len(self._fit_hist) == RUN_AHEAD:
@@ -509,7 +516,9 @@ class FusedCNNLearner(TorchLearner):
                     self.engine.adam_t.fill_(epoch * steps)
                 t0, t1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                 t0.record(cur)
-                stats = self._run("train", loader, True, loader.permutation(host=True))  # one H2D copy into the graph's buffer
+                with GATE.shared():  # pinned host buffer: never beside another peer's capture
+                    perm = loader.permutation(host=True)
+                stats = self._run("train", loader, True, perm)  # one H2D copy into the graph's buffer
                 t1.record(cur)
                 host = self._readback(stats)
                 done = torch.cuda.Event()

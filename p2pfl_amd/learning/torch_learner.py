@@ -498,7 +498,12 @@ class TorchLearner(NodeLearner):
 
         model = self.model
         B, n = int(loader.batch_size), len(loader.dataset)
-        perm = loader.permutation()  # the same batch order as iterating the loader
+        # the same batch order as iterating the loader.  A pinned host buffer and an H2D
+        # copy: under the shared gate, never beside another peer's capture (the host
+        # allocator queries events that may have been recorded in a capturing stream:
+        # hipErrorCapturedEvent, scripts/repro_virtual_peers.py)
+        with self._gate():
+            perm = loader.permutation()
         key = TrainStepGraph.make_key(self, opt, loader)
         for i, s in enumerate(range(0, n, B)):
             if self._interrupt.is_set():
@@ -604,7 +609,8 @@ class TorchLearner(NodeLearner):
         name = getattr(hook, "__name__", str(hook))
         key = EvalStepGraph.make_key(self, loader, hook, B)
         eg = self._eval_graphs.get(name)
-        perm = loader.permutation()
+        with self._gate():  # pinned host buffer + H2D copy: never beside another peer's capture
+            perm = loader.permutation()
         if eg is None or eg.key != key:
             eg = self._eval_graphs[name] = EvalStepGraph(self, loader, hook, B)
             eg.capture(perm[:B])  # takes the gate exclusively

@@ -99,10 +99,16 @@ class TrainStage(Stage):
             # (its own comment flags the hazard): on a partial topology that
             # leaves peers waiting for AGGREGATION_TIMEOUT.
             have = set(aggregator.get_aggregated_models())
+            rnd = state.round if state.round is not None else -1
             return [
                 n
                 for n in protocol.get_neighbors(only_direct=False)
                 if n in state.train_set and n != state.addr and (have - set(peer_has(n)))
+                # a peer that announced models_ready for this round (or a later one) has
+                # its aggregate: its last report of this round may never have reached this
+                # node (sent while this node was still in the previous round), and pushes
+                # to it would be declined until the loop's equal-rounds exit
+                and state.nei_status.get(n, -1) < rnd
             ]
 
         def status() -> Any:

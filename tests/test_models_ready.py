@@ -35,9 +35,9 @@ def test_previous_round_ready_is_recorded_as_reported(state, monkeypatch, async_
 def test_rounds_outside_the_window(state, monkeypatch):
     monkeypatch.setattr(Settings, "ASYNC_DIFFUSION", False)
     cmd = ModelsReadyCommand(state)
-    cmd.execute("mem://b", 4)  # ahead of us: ignored
+    cmd.execute("mem://b", 4)  # ahead of us: recorded (it needs nothing of round 3 any more)
     cmd.execute("mem://c", 0)  # two or more rounds late: ignored (reference window r-1, r)
-    assert "mem://b" not in state.nei_status and "mem://c" not in state.nei_status
+    assert state.nei_status["mem://b"] == 4 and "mem://c" not in state.nei_status
     monkeypatch.setattr(Settings, "ASYNC_DIFFUSION", True)
     cmd.execute("mem://c", 0)  # background diffusion keeps any older round
     assert state.nei_status["mem://c"] == 0
@@ -110,3 +110,35 @@ def test_sync_diffusion_ends_by_stall_exit_when_a_neighbour_stays_behind(monkeyp
     assert st.nei_status["mem://lag"] == 2
     assert 1 <= len(sent) <= 5 and all(n == "mem://lag" for n, _ in sent), sent
     assert took < 2.0, took  # 3 equal snapshots one period apart, then out
+
+
+def test_partial_gossip_skips_a_peer_already_past_the_round():
+    """TrainStage's partial-aggregate gossip: a peer whose models_ready says it has this
+    round's aggregate is no candidate even if its last models_aggregated report of the
+    round never arrived (it was sent while this node was still in the previous round).
+    Before, the loop kept offering it models it declined until the equal-rounds exit
+    (~9 s stalls with 8 virtual peers, bench_node.py)."""
+    from p2pfl_amd.stages.base_node.train_stage import TrainStage
+
+    st = NodeState("mem://me")
+    st.round = 5
+    st.train_set = ["mem://me", "mem://a", "mem://b"]
+    st.models_aggregated = {"mem://a": ["mem://a"], "mem://b": ["mem://b"]}  # stale reports
+    seen = {}
+
+    class Agg:
+        def get_aggregated_models(self):
+            return ["mem://me", "mem://a", "mem://b"]
+
+    class Proto:
+        def get_neighbors(self, only_direct=False):
+            return {"mem://a": None, "mem://b": None}
+
+        def gossip_weights(self, stop, candidates, status, model_fn, **kw):
+            seen["before"] = sorted(candidates())
+            ModelsReadyCommand(st).execute("mem://a", 5)  # a finished round 5
+            ModelsReadyCommand(st).execute("mem://b", 6)  # b is already past it
+            seen["after"] = sorted(candidates())
+
+    TrainStage._gossip_model_aggregation(st, Proto(), Agg())
+    assert seen == {"before": ["mem://a", "mem://b"], "after": []}
