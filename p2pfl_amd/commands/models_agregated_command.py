@@ -18,7 +18,13 @@ class ModelsAggregatedCommand(Command):
 
     def execute(self, source: str, round: int, *args, **kwargs) -> None:
         if round == self.state.round:
-            self.state.models_aggregated[source] = list(args)
+            # a node's set of aggregated models only grows within a round, but its
+            # reports travel on concurrent sender threads (two models added at once
+            # broadcast 7/8 and 8/8 side by side): a stale report overwriting a newer
+            # one made peers push models the node already held until their
+            # equal-rounds exit (the reference assigns: models_agregated_command.py:49)
+            prev = self.state.models_aggregated.get(source, [])
+            self.state.models_aggregated[source] = prev + [c for c in args if c not in prev]
             self.state.changed.bump()
         else:
             logger.debug(

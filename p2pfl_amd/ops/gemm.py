@@ -109,6 +109,7 @@ PP = 2048  # variant bit 11: the ping-pong 256 x 256 pipeline (csrc/gemm_pp.hip)
 PP_M16 = 1 << 16  # with PP: the same pipeline on v_mfma_f32_16x16x32_bf16
 PP_SK = 1 << 17  # with PP: stream-K schedule, ``splits`` = grid size (csrc/gemm_pp.hip)
 PP_N128 = 1 << 21  # with PP: the 256 x 128 output tile (150 whole tiles for the N = 768 products)
+PP_ROWSPLIT = 1 << 22  # with PP: rows split into one full wave of 256 x 256 tiles + a 256 x 128 tail launch
 SK_SLAB = 256 * 256  # fp32 elements of one stream-K partial tile (two per workgroup)
 
 
@@ -166,6 +167,8 @@ def gemm(
     N = b.shape[0] if b_kmajor else b.shape[1]
     K = a.shape[1] if a_kmajor else a.shape[0]
     dev = a.device
+    if variant is not None and variant & PP_ROWSPLIT:
+        return _gemm_rowsplit(a, b, a_kmajor, b_kmajor, out_dtype, bias, gelu, want_z, residual, out, variant & ~PP_ROWSPLIT)
     if variant is not None and variant & PP_SK:  # stream-K: `splits` workgroups share the K-tile iterations
         if out is None:
             out = torch.empty((M, N), dtype=out_dtype, device=dev)
@@ -195,6 +198,35 @@ def gemm(
     z = torch.empty((M, N), dtype=torch.bfloat16, device=dev) if (gelu and want_z) else None
     v = _variant(a_kmajor, 1, M, N, K, b_kmajor) if variant is None else variant
     _C().gemm(a, b, a_kmajor, b_kmajor, out, bias, gelu, z, residual, 1, v)
+    return out, z
+
+
+def rowsplit_rows(M: int, N: int) -> int:
+    """Rows of the 256 x 256 launch of a row-split product: whole tile rows filling at
+    most one wave of the 256 CUs (0 when the product has no second wave to trim)."""
+    tiles_n = -(-N // 256)
+    m1 = (256 // tiles_n) * 256 if tiles_n <= 256 else 0
+    return m1 if 0 < m1 < M else 0
+
+
+def _gemm_rowsplit(a, b, a_kmajor, b_kmajor, out_dtype, bias, gelu, want_z, residual, out, v):
+    """A product whose 256 x 256 tiles spill a little past one wave (ViT fc2 input
+    gradient / fc1 forward: 300 tiles on 256 CUs, 1.17 waves) as two launches over
+    row ranges: the first ``rowsplit_rows`` rows on the 256 x 256 ping-pong kernel (one
+    full wave), the rest on the 256 x 128 tile (its tail wave at half the work per
+    workgroup).  Row slices of a k-major A / m-major A and of C, z, residual are views."""
+    M = a.shape[0] if a_kmajor else a.shape[1]
+    N = b.shape[0] if b_kmajor else b.shape[1]
+    m1 = rowsplit_rows(M, N)
+    if m1 == 0:
+        return gemm(a, b, a_kmajor, b_kmajor, out_dtype, bias, gelu, want_z, residual, 1, out, v)
+    if out is None:
+        out = torch.empty((M, N), dtype=out_dtype, device=a.device)
+    z = torch.empty((M, N), dtype=torch.bfloat16, device=a.device) if (gelu and want_z) else None
+    for r0, r1, vv in ((0, m1, v), (m1, M, v | PP_N128)):
+        aa = a[r0:r1] if a_kmajor else a[:, r0:r1]
+        res = residual[r0:r1] if residual is not None else None
+        _C().gemm(aa, b, a_kmajor, b_kmajor, out[r0:r1], bias, gelu, z[r0:r1] if z is not None else None, res, 1, vv)
     return out, z
 
 
@@ -234,14 +266,18 @@ _NAT, _LIB = "native", "library"
 # fix-up (256 KB fp32 per workgroup, ~15-18 us of chip-wide traffic) lost to the
 # 256 x 128 tile's whole tiles (profiles/r6_vit_gemm_sweep.md, scripts/sk_anatomy.py).
 def _fwd_cfgs(M: int, N: int, K: int):
-    return ((PP | PP_N128, 1), (PP | PP_N128 | PP_M16, 1), (PP | PP_M16, 1), (PP, 1), (PP, 2), (10, 1), (2, 1))
+    split = ((PP | PP_ROWSPLIT | PP_M16, 1), (PP | PP_ROWSPLIT, 1)) if rowsplit_rows(M, N) else ()
+    return ((PP | PP_N128, 1), (PP | PP_N128 | PP_M16, 1), (PP | PP_M16, 1), (PP, 1), (PP, 2), (10, 1), (2, 1)) + split
 
 
 def _dgrad_cfgs(M: int, N: int, K: int):
-    return ((PP | PP_N128, 1), (PP | PP_N128 | PP_M16, 1), (PP, 1), (PP, 2), (2, 1), (10, 1), (2, 3))
+    split = ((PP | PP_ROWSPLIT | PP_M16, 1), (PP | PP_ROWSPLIT, 1)) if rowsplit_rows(M, N) else ()
+    return ((PP | PP_N128, 1), (PP | PP_N128 | PP_M16, 1), (PP, 1), (PP, 2), (2, 1), (10, 1), (2, 3)) + split
 
 
-_WGRAD_CFGS = ((PP, 6), (PP, 8), (10, 6), (4096 | 2, 6), (2, 3))
+# ping-pong at 3-4 slices reduces inside the launch (no slab-sum launch); at 6-8 slices
+# through a separate slab_sum pass
+_WGRAD_CFGS = ((PP, 6), (PP, 8), (PP, 4), (PP, 3), (PP | PP_M16, 6), (10, 6), (4096 | 2, 6), (2, 3))
 
 
 def _cfg_name(v: int, sp: int) -> str:
@@ -262,8 +298,9 @@ def _cfg_ok(v: int, sp: int, M: int, N: int, K: int, a_kmajor: bool, b_kmajor: b
         return pp_eligible_any(M, N, K, a_kmajor, b_kmajor) and 1 <= sp <= sk_iters(M, N, K)
     if sp > 1 and K // sp < 256:
         return False
-    if v & PP and v & PP_N128:  # the 256 x 128 tile: no split-K
-        return sp == 1 and pp_eligible_any(M, N, K, a_kmajor, b_kmajor)
+    if v & PP and v & (PP_N128 | PP_ROWSPLIT):  # the 256 x 128 tile (alone or as the row-split tail): no split-K
+        return sp == 1 and pp_eligible_any(M, N, K, a_kmajor, b_kmajor) and (a_kmajor or not v & PP_ROWSPLIT
+                                                                             or rowsplit_rows(M, N) % 8 == 0)
     if v & PP:
         return pp_eligible_any(M, N, K, a_kmajor, b_kmajor) and not (epilogue and sp > IN_LAUNCH_MAX_SPLITS)
     return not (epilogue and sp > IN_LAUNCH_MAX_SPLITS)

@@ -21,9 +21,9 @@ import torch  # noqa: E402
 
 from p2pfl_amd.ops import autotune  # noqa: E402
 from p2pfl_amd.ops.fused import _fx  # noqa: E402
-from p2pfl_amd.ops.gemm import PP, PP_M16, PP_N128, PP_SK, gemm, gemm_reference, sk_iters  # noqa: E402
+from p2pfl_amd.ops.gemm import PP, PP_M16, PP_N128, PP_ROWSPLIT, PP_SK, gemm, gemm_reference, sk_iters  # noqa: E402
 
-DP = [(PP | PP_N128, 1), (PP | PP_N128 | PP_M16, 1), (PP | PP_M16, 1), (PP, 1), (PP, 2), (PP, 3), (2, 1), (10, 1), (PP, 6), (PP, 8), (10, 6), (4096 | 2, 6)]
+DP = [(PP | PP_ROWSPLIT | PP_M16, 1), (PP | PP_ROWSPLIT, 1), (PP | PP_N128, 1), (PP | PP_N128 | PP_M16, 1), (PP | PP_M16, 1), (PP, 1), (PP, 2), (PP, 3), (2, 1), (10, 1), (PP, 6), (PP, 8), (PP, 4), (PP, 3), (PP | PP_M16, 6), (10, 6), (4096 | 2, 6)]
 GRIDS = (240, 160) if os.environ.get('SK_FULL') is None else (256, 240, 224, 192, 160, 128)
 
 

@@ -48,3 +48,17 @@ def test_report_keeps_the_round_of_the_added_models():
     cmd = AddModelCommand(state, stop=lambda: None, aggregator=Agg(), comm_proto=Proto())
     cmd.execute("b", 8, weights={"w": 1}, contributors=["b"], weight=1)
     assert sent == [(ModelsAggregatedCommand.get_name(), ["a", "b"], 8)]
+
+
+def test_stale_report_does_not_shrink_a_newer_one():
+    """Reports of one round arrive out of order (two adds broadcast from concurrent
+    handler threads): the 7-model report landing after the 8-model one must not make
+    this node believe the peer lacks a model (it pushed until its equal-rounds exit)."""
+    state = SimpleNamespace(round=1, models_aggregated={}, changed=_Changed(), addr="x")
+    cmd = ModelsAggregatedCommand(state)
+    full = [f"n{i}" for i in range(8)]
+    cmd.execute("n0", 1, *full)
+    cmd.execute("n0", 1, *full[:7])
+    assert sorted(state.models_aggregated["n0"]) == sorted(full)
+    cmd.execute("n0", 0, "late")  # another round's report is still ignored
+    assert "late" not in state.models_aggregated["n0"]

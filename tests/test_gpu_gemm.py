@@ -421,3 +421,32 @@ def test_pingpong128_exact_integers_and_epilogues(m16):
     torch.testing.assert_close(out2.float(), ref2, atol=0.5, rtol=1e-2)
     with pytest.raises(RuntimeError):
         ops.gemm(a, b, splits=2, variant=v)
+
+
+@pytest.mark.parametrize("m16", [False, True], ids=["mfma32", "mfma16"])
+@pytest.mark.parametrize("kind", ["fwd_gelu", "dgrad", "wgrad_layout"])
+def test_rowsplit_vs_fp32(kind, m16):
+    """Row-split schedule (variant bit 22): one full wave of 256 x 256 tiles over the first
+    rows, the 256 x 128 tile over the rest, as two launches on row views of A / C / z."""
+    from p2pfl_amd.ops.gemm import PP, PP_M16, PP_ROWSPLIT, rowsplit_rows
+
+    v = PP | PP_ROWSPLIT | (PP_M16 if m16 else 0)
+    M, N, K = 6304, 3072, 768
+    assert rowsplit_rows(M, N) == 5376
+    if kind == "fwd_gelu":
+        a, b = _operands(M, N, K, True, True, seed=51)
+        bias = torch.randn(N, device="cuda")
+        out, z = ops.gemm(a, b, bias=bias, gelu=True, want_z=True, variant=v)
+        ref, zr = ops.gemm_reference(a, b, True, True, bias, True)
+        torch.testing.assert_close(z.float(), zr, atol=0.25, rtol=1e-2)
+        torch.testing.assert_close(out.float(), ref, atol=0.25, rtol=1e-2)
+    elif kind == "dgrad":
+        a, b = _operands(M, N, K, True, False, seed=52)
+        out, _ = ops.gemm(a, b, True, False, out_dtype=torch.float32, variant=v)
+        ref, _ = ops.gemm_reference(a, b, True, False)
+        torch.testing.assert_close(out, ref, atol=5e-3, rtol=1e-4)
+    else:  # m-major A: the row split is a column view of the stored operand
+        a, b = _operands(M, N, K, False, True, seed=53)
+        out, _ = ops.gemm(a, b, False, True, out_dtype=torch.float32, variant=v)
+        ref, _ = ops.gemm_reference(a, b, False, True)
+        torch.testing.assert_close(out, ref, atol=5e-3, rtol=1e-4)
