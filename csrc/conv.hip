@@ -291,6 +291,27 @@ __global__ __launch_bounds__(NT, NBUF == 1 ? 3 : (NBUF == 2 ? 2 : 1)) void conv_
   gemm_body<Tile128, NBUF, LA, LB, BN, EPI>(p, la, lb, tiles_m, tiles_n, smem);
 }
 
+// 64 x 64 output tiles (variant bit 14, kConvT64): four 32 x 32 waves; a k-major
+// operand stages only its 64 rows (8 KB per half), so the forward's 4-stage ring is
+// 64 KB -- two workgroups per CU -- and a 16x16 / 8x8 / 4x4 stage fills the chip
+// with tiles instead of split-K slices (no slab reduce launch).  No BatchNorm
+// statistics epilogue (BN = 0 only).
+template <int NBUF, class LA, class LB, int EPI>
+__global__ __launch_bounds__(NT, NBUF >= 3 ? 2 : 4) void conv64_kernel(GemmParams p, LA la, LB lb, int tiles_m, int tiles_n) {
+  __shared__ __attribute__((aligned(16))) char smem[smem_bytes_l<Tile64, NBUF, LA, LB>()];
+  gemm_body<Tile64, NBUF, LA, LB, 0, EPI>(p, la, lb, tiles_m, tiles_n, smem);
+}
+
+template <class LA, class LB, int EPI>
+static void launch_e64(const GemmParams& p, const LA& la, const LB& lb, int grid, int tm, int tn, hipStream_t s) {
+  if (p.variant & 4096)
+    hipLaunchKernelGGL((conv64_kernel<4, LA, LB, EPI>), dim3(grid), dim3(NT), 0, s, p, la, lb, tm, tn);
+  else if (p.variant & 8)
+    hipLaunchKernelGGL((conv64_kernel<1, LA, LB, EPI>), dim3(grid), dim3(NT), 0, s, p, la, lb, tm, tn);
+  else
+    hipLaunchKernelGGL((conv64_kernel<2, LA, LB, EPI>), dim3(grid), dim3(NT), 0, s, p, la, lb, tm, tn);
+}
+
 template <class LA, class LB, int BN, int EPI>
 static void launch_e(const GemmParams& p, const LA& la, const LB& lb, int grid, int tm, int tn, hipStream_t s) {
   if (p.variant & 4096)  // 4-stage ring, one workgroup per CU: short-K / small-grid shapes
@@ -304,6 +325,16 @@ static void launch_e(const GemmParams& p, const LA& la, const LB& lb, int grid, 
 template <class LA, class LB, int BN>
 static void launch_t(const GemmParams& p, const LA& la, const LB& lb, hipStream_t s) {
   int tm, tn;
+  if constexpr (BN == 0) {
+    if (p.variant & kConvT64) {
+      const int grid = gemm_grid<Tile64>(p, tm, tn);
+      if (epilogue_kind(p) == 0)
+        launch_e64<LA, LB, 0>(p, la, lb, grid, tm, tn, s);
+      else
+        launch_e64<LA, LB, 1>(p, la, lb, grid, tm, tn, s);
+      return;
+    }
+  }
   const int grid = gemm_grid<Tile128>(p, tm, tn);
   if (BN == 0 && epilogue_kind(p) == 0)
     launch_e<LA, LB, BN, 0>(p, la, lb, grid, tm, tn, s);

@@ -48,8 +48,12 @@ int64_t slab_elems(int64_t rows, int64_t cols) { return ((rows + 127) / 128) * (
 // output tile, all zero) the slabs go to `ws` (fp32, splits * slab_elems) and the launch
 // reduces them itself.
 p2::SplitK make_splitk(int64_t splits, const c10::optional<torch::Tensor>& ws, const c10::optional<torch::Tensor>& counters,
-                       int64_t rows, int64_t cols, const torch::Tensor& like, const char* who) {
+                       int64_t rows, int64_t cols, const torch::Tensor& like, const char* who, int64_t variant) {
   TORCH_CHECK(splits >= 1 && splits <= 128, who, ": 1 <= splits <= 128");
+  // 64 x 64 tiles (conv.hip kConvT64) reduce split-K through slabs + tile_slab_reduce only:
+  // the in-launch counters (one per 128 x 128 tile) do not cover their tiles
+  TORCH_CHECK(!(variant & p2::kConvT64) || !(counters.has_value() && counters->defined()), who,
+              ": 64x64-tile launches take no split-K counters");
   p2::SplitK k;
   k.splits = int(splits);
   const bool have_cnt = counters.has_value() && counters->defined();
@@ -94,7 +98,7 @@ void conv_fwd(torch::Tensor x, torch::Tensor w, int64_t stride, int64_t pad, int
   TORCH_CHECK(w.size(3) == x.size(3), "conv_fwd: channel mismatch");
   const auto s = make_shape(x.size(0), x.size(1), x.size(2), x.size(3), w.size(0), w.size(1), w.size(2), stride, pad, dil);
   TORCH_CHECK(s.C % 64 == 0 && s.O % 8 == 0, "conv_fwd: needs C % 64 == 0 and O % 8 == 0 (C=", s.C, " O=", s.O, ")");
-  const auto k = make_splitk(splits, ws, counters, int64_t(s.N) * s.OH * s.OW, s.O, x, "conv_fwd");
+  const auto k = make_splitk(splits, ws, counters, int64_t(s.N) * s.OH * s.OW, s.O, x, "conv_fwd", variant);
   check_out(y, k, s.N, s.OH, s.OW, s.O, "conv_fwd");
   TORCH_CHECK(x.device() == w.device() && y.device() == x.device(), "conv_fwd: device mismatch");
   const c10::DeviceGuard g(x.device());
@@ -117,7 +121,8 @@ void conv_fwd_bn(torch::Tensor x, torch::Tensor w, int64_t stride, int64_t pad, 
   const auto s = make_shape(x.size(0), x.size(1), x.size(2), x.size(3), w.size(0), w.size(1), w.size(2), stride, pad, dil);
   TORCH_CHECK(s.C % 64 == 0 && s.O % 8 == 0, "conv_fwd_bn: needs C % 64 == 0 and O % 8 == 0");
   const int64_t M = int64_t(s.N) * s.OH * s.OW;
-  const auto k = make_splitk(splits, ws, counters, M, s.O, x, "conv_fwd_bn");
+  const auto k = make_splitk(splits, ws, counters, M, s.O, x, "conv_fwd_bn", variant);
+  TORCH_CHECK(!(variant & p2::kConvT64), "conv_fwd_bn: the BatchNorm-statistics epilogue runs on 128x128 tiles only");
   TORCH_CHECK(k.splits == 1 || k.counters, "conv_fwd_bn: split-K needs the in-launch reduction (counters)");
   check_out(y, k, s.N, s.OH, s.OW, s.O, "conv_fwd_bn");
   const int64_t tiles_m = (M + 127) / 128, tiles_n = (s.O + 127) / 128, groups = bn_groups(tiles_m);
@@ -178,7 +183,8 @@ void conv_dgrad_bn(torch::Tensor dy, torch::Tensor w, int64_t stride, int64_t pa
   TORCH_CHECK(s.O % 64 == 0 && s.C % 8 == 0, "conv_dgrad_bn: needs O % 64 == 0 and C % 8 == 0");
   TORCH_CHECK(dy.size(0) == s.N && dy.size(1) == s.OH && dy.size(2) == s.OW && dy.size(3) == s.O, "conv_dgrad_bn: dy shape");
   const int64_t M = int64_t(s.N) * s.H * s.W;
-  const auto k = make_splitk(splits, ws, counters, M, s.C, dy, "conv_dgrad_bn");
+  const auto k = make_splitk(splits, ws, counters, M, s.C, dy, "conv_dgrad_bn", variant);
+  TORCH_CHECK(!(variant & p2::kConvT64), "conv_dgrad_bn: the BatchNorm-statistics epilogue runs on 128x128 tiles only");
   TORCH_CHECK(k.splits == 1 || k.counters, "conv_dgrad_bn: split-K needs the in-launch reduction (counters)");
   check_out(dx, k, s.N, s.H, s.W, s.C, "conv_dgrad_bn");
   const int64_t tiles_m = (M + 127) / 128, tiles_n = (s.C + 127) / 128, groups = bn_groups(tiles_m);
@@ -228,7 +234,7 @@ void conv_dgrad(torch::Tensor dy, torch::Tensor w, int64_t stride, int64_t pad, 
   TORCH_CHECK(w.size(3) == s.C, "conv_dgrad: channel mismatch");
   TORCH_CHECK(s.O % 64 == 0 && s.C % 8 == 0, "conv_dgrad: needs O % 64 == 0 and C % 8 == 0 (C=", s.C, " O=", s.O, ")");
   TORCH_CHECK(dy.size(0) == s.N && dy.size(1) == s.OH && dy.size(2) == s.OW && dy.size(3) == s.O, "conv_dgrad: dy shape");
-  const auto k = make_splitk(splits, ws, counters, int64_t(s.N) * s.H * s.W, s.C, dy, "conv_dgrad");
+  const auto k = make_splitk(splits, ws, counters, int64_t(s.N) * s.H * s.W, s.C, dy, "conv_dgrad", variant);
   check_out(dx, k, s.N, s.H, s.W, s.C, "conv_dgrad");
   TORCH_CHECK(dy.device() == w.device() && dx.device() == dy.device(), "conv_dgrad: device mismatch");
   const c10::DeviceGuard g(dy.device());
@@ -249,7 +255,7 @@ void conv_dgrad_s2(torch::Tensor dy, torch::Tensor w, int64_t pad, torch::Tensor
   TORCH_CHECK(w.size(3) == s.C && s.O % 64 == 0 && s.C % 8 == 0, "conv_dgrad_s2: needs O % 64 == 0 and C % 8 == 0");
   TORCH_CHECK(dy.size(0) == s.N && dy.size(1) == s.OH && dy.size(2) == s.OW && dy.size(3) == s.O, "conv_dgrad_s2: dy shape");
   const int64_t rows = int64_t(p2::s2_phases(s)) * s.N * (s.H / 2) * (s.W / 2);  // phases with taps x N (H/2) (W/2)
-  const auto k = make_splitk(splits, ws, counters, rows, s.C, dy, "conv_dgrad_s2");
+  const auto k = make_splitk(splits, ws, counters, rows, s.C, dy, "conv_dgrad_s2", variant);
   if (k.splits == 1 || k.counters) {
     TORCH_CHECK(out.is_cuda() && out.scalar_type() == torch::kBFloat16 && out.is_contiguous() && out.numel() == rows * s.C &&
                     reinterpret_cast<uintptr_t>(out.data_ptr()) % 16 == 0,
@@ -293,7 +299,7 @@ void conv_wgrad(torch::Tensor dy, torch::Tensor x, int64_t kh, int64_t kw, int64
   TORCH_CHECK(out.is_cuda() && out.is_contiguous() && reinterpret_cast<uintptr_t>(out.data_ptr()) % 16 == 0,
               "conv_wgrad: out must be contiguous and 16-byte aligned");
   const int64_t n = int64_t(s.O) * kh * kw * s.C;
-  const auto k = make_splitk(splits, ws, counters, s.O, kh * kw * s.C, x, "conv_wgrad");
+  const auto k = make_splitk(splits, ws, counters, s.O, kh * kw * s.C, x, "conv_wgrad", variant);
   int out_bf16 = 0;
   if (k.splits > 1 && !k.counters) {
     TORCH_CHECK(out.scalar_type() == torch::kFloat32 && out.is_contiguous() && out.numel() >= splits * slab_elems(s.O, kh * kw * s.C),

@@ -76,6 +76,11 @@ struct GemmParams {
   int variant;  // tuning experiments: bit0 setprio around MFMAs, bit1 A-panel tile order, bit2 no XCD remap, bit3 single LDS buffer (4 workgroups / CU), bit4/bit5 timing probes (no stores / no K loop), bit6 256 x 256 tile (8 waves), bit7 no DMA after the prologue (probe), bit8 legacy panel tile order instead of grouped (bit1 then picks A- vs B-panel order), bits 9-10 where the double-buffer prefetch is issued (0 before the K-tile's fragment reads, 1 after the first ones, 2 one chunk per k-substep), bit11 the ping-pong 256 x 256 pipeline of gemm_pp.hip (continuous per-phase DMA, staggered wave halves); with bit 11, bits 12-15 are the ping-pong kernel's timing probes (gemm_pp.hip).  Bit 12 is also the conv kernels' 4-stage ring (conv.hip), whose split-K slabs are 128 x 128 tiles
 };
 
+// conv.hip variant bit 14: 64 x 64 output tiles (gemm_core.h Tile64; split-K slabs of that
+// geometry, reduced by tile_slab_reduce with the same bit).  The convolutions only -- with
+// bit 11 (the ping-pong GEMM) bit 14 is one of its timing probes.
+constexpr int kConvT64 = 1 << 14;
+
 void gemm_bf16(const GemmParams& p, hipStream_t s);
 // out[M][ldc] = sum of the `splits` fragment-native split-K slabs (gemm_core.h SlabGeom)
 // that a launch without counters wrote to `ws`; `variant` = that launch's (tile shape, order)

@@ -110,6 +110,11 @@ void tile_slab_reduce(const float* ws, int splits, int M, int N, int64_t ldc, vo
     const int64_t groups = int64_t(tm) * tn * (256 * 256 / 4);
     hipLaunchKernelGGL(tile_slab_reduce_kernel<Tile256>, dim3(int((groups + 255) / 256)), dim3(256), 0, s, ws, splits, M,
                        N, ldc, out, out_bf16, variant, tm, tn);
+  } else if ((variant & kConvT64) && !(variant & 2048)) {  // the convolutions' 64 x 64 tiles (conv.hip)
+    const int tm = (M + 63) / 64, tn = (N + 63) / 64;
+    const int64_t groups = int64_t(tm) * tn * (64 * 64 / 4);
+    hipLaunchKernelGGL(tile_slab_reduce_kernel<Tile64>, dim3(int((groups + 255) / 256)), dim3(256), 0, s, ws, splits, M,
+                       N, ldc, out, out_bf16, variant, tm, tn);
   } else {
     const int tm = (M + 127) / 128, tn = (N + 127) / 128;
     const int64_t groups = int64_t(tm) * tn * (128 * 128 / 4);

@@ -44,13 +44,18 @@ struct TileCfg {
   static constexpr int BM = BM_, BN = BN_, WAVES_M = WAVES_M_, WAVES_N = WAVES_N_;
   static constexpr int NT = 64 * WAVES_M * WAVES_N;
   static constexpr int GROUPS = NT / 256;
-  static constexpr int HA = BM / 128, HB = BN / 128;  // operand halves
+  static constexpr int HA = (BM + 127) / 128, HB = (BN + 127) / 128;  // operand halves (Tile64: one partial half)
   static constexpr int FM = BM / WAVES_M / 32, FN = BN / WAVES_N / 32;
   static constexpr int STAGE = (HA + HB) * TILE;  // bytes per pipeline stage
   static_assert(NT % 256 == 0 && HA % GROUPS == 0 && HB % GROUPS == 0, "staging groups must split the halves");
 };
 using Tile128 = TileCfg<128, 128, 2, 2>;
 using Tile256 = TileCfg<256, 256, 2, 4>;
+//   Tile64:  64 x 64, 4 waves (2 x 2), one 32 x 32 MFMA tile per wave -- for
+//            the CIFAR ResNet's 16x16 / 8x8 / 4x4 stages and 64-channel
+//            products, where 128 x 128 tiles leave most CUs idle (or half of
+//            every MFMA on zero columns) and needed split-K slabs + a reduce.
+using Tile64 = TileCfg<64, 64, 2, 2>;
 
 // Zero page for out-of-operand chunks (one copy per translation unit).  It is
 // 64 KB, not 16 B: a tile whose rows or taps fall outside the operand sends
@@ -155,11 +160,28 @@ P2_DEVICE void dma16(const void* gsrc, char* lds_dst) {
       : "memory");
 }
 
-template <class L>
+// NCH chunks per thread (4: a full 128-row half; a k-major operand of a 64-row
+// tile stages chunks 0-1 = its rows 0-63 only, into the first 8 KB)
+template <int NCH, class L>
 P2_DEVICE void stage(const L& ld, const typename L::St& st, int k0, char* lds, int tid) {
   const int wave = tid >> 6;
 #pragma unroll
-  for (int i = 0; i < 4; ++i) dma16(ld.src(st, i, k0, tid), lds + (i * NT + wave * 64) * 16);  // lane L writes dst + 16 L
+  for (int i = 0; i < NCH; ++i) dma16(ld.src(st, i, k0, tid), lds + (i * NT + wave * 64) * 16);  // lane L writes dst + 16 L
+}
+
+// Chunks per thread of one staged half of an operand with `rows` tile rows: a
+// k-major image is row-linear (128 B per row), so a narrow tile stages (and
+// keeps) only its rows; an mn-major image is k-linear over 128 columns (its
+// fragment reads address columns inside that 256-B row) and stays whole.
+template <int ROWS, bool KMAJ>
+constexpr int half_chunks() {
+  return (KMAJ && ROWS < 128) ? ROWS / 32 : 4;
+}
+// LDS bytes of one pipeline stage (A halves, then B halves) for these loaders
+template <class CFG, class LA, class LB>
+constexpr int stage_bytes() {
+  return CFG::HA * half_chunks<(CFG::BM < 128 ? CFG::BM : 128), LA::KMAJ>() * NT * 16 +
+         CFG::HB * half_chunks<(CFG::BN < 128 ? CFG::BN : 128), LB::KMAJ>() * NT * 16;
 }
 
 // Fragment of a 32-row block (rows rb..rb+31 of the tile) for k-substep ks:
@@ -206,6 +228,13 @@ P2_DEVICE int xcd_remap(int orig, int nwg) {
 template <class CFG, int NBUF>
 constexpr int smem_bytes() {  // NBUF: LDS stages of the K loop (1, 2, or a 3-5 stage ring)
   constexpr int pipe = NBUF * CFG::STAGE, epi = CFG::BM * (CFG::BN * 2 + 16);
+  return (CFG::NT >= 512 && epi > pipe) ? epi : pipe;
+}
+// the same for a kernel that knows its loaders (narrow k-major halves staged compactly);
+// equal to smem_bytes for the 128- and 256-row tiles
+template <class CFG, int NBUF, class LA, class LB>
+constexpr int smem_bytes_l() {
+  constexpr int pipe = NBUF * stage_bytes<CFG, LA, LB>(), epi = CFG::BM * (CFG::BN * 2 + 16);
   return (CFG::NT >= 512 && epi > pipe) ? epi : pipe;
 }
 
@@ -423,6 +452,11 @@ P2_DEVICE const L& tile_bound(const L& l, int) {
 template <class CFG, int NBUF, class LA, class LB, int BN = 0, int EPI = 1>
 P2_DEVICE void gemm_body(const GemmParams& p, const LA& la0, const LB& lb0, int tiles_m, int tiles_n, char* smem) {
   constexpr int FM = CFG::FM, FN = CFG::FN, HA = CFG::HA, HB = CFG::HB, G = CFG::GROUPS;
+  // chunks per thread and bytes of one staged half of A / B, bytes of a pipeline stage
+  constexpr int CHA = half_chunks<(CFG::BM < 128 ? CFG::BM : 128), LA::KMAJ>();
+  constexpr int CHB = half_chunks<(CFG::BN < 128 ? CFG::BN : 128), LB::KMAJ>();
+  constexpr int HALF_A = CHA * NT * 16, HALF_B = CHB * NT * 16, STG = HA * HALF_A + HB * HALF_B;
+  constexpr int SMEM = smem_bytes_l<CFG, NBUF, LA, LB>();
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave / CFG::WAVES_N, wn = wave % CFG::WAVES_N;
   const int grp = tid >> 8, gt = tid & 255;  // staging group, thread within it
@@ -464,17 +498,19 @@ P2_DEVICE void gemm_body(const GemmParams& p, const LA& la0, const LB& lb0, int 
   for (int q = 0; q < HB / G; ++q) stb[q] = lb.prep(n0 + 128 * (grp + G * q), gt);
   auto stage_all = [&](int k0, char* dst) {
 #pragma unroll
-    for (int q = 0; q < HA / G; ++q) stage(la, sta[q], k0, dst + (grp + G * q) * TILE, gt);
+    for (int q = 0; q < HA / G; ++q) stage<CHA>(la, sta[q], k0, dst + (grp + G * q) * HALF_A, gt);
 #pragma unroll
-    for (int q = 0; q < HB / G; ++q) stage(lb, stb[q], k0, dst + (HA + grp + G * q) * TILE, gt);
+    for (int q = 0; q < HB / G; ++q) stage<CHB>(lb, stb[q], k0, dst + HA * HALF_A + (grp + G * q) * HALF_B, gt);
   };
   // chunk c (0..3) of every half this group stages: stage_all split in four
   auto stage_chunk = [&](int c, int k0, char* dst) {
     const int wo = (c * NT + (gt >> 6) * 64) * 16;
+    if (c < CHA)
 #pragma unroll
-    for (int q = 0; q < HA / G; ++q) dma16(la.src(sta[q], c, k0, gt), dst + (grp + G * q) * TILE + wo);
+      for (int q = 0; q < HA / G; ++q) dma16(la.src(sta[q], c, k0, gt), dst + (grp + G * q) * HALF_A + wo);
+    if (c < CHB)
 #pragma unroll
-    for (int q = 0; q < HB / G; ++q) dma16(lb.src(stb[q], c, k0, gt), dst + (HA + grp + G * q) * TILE + wo);
+      for (int q = 0; q < HB / G; ++q) dma16(lb.src(stb[q], c, k0, gt), dst + HA * HALF_A + (grp + G * q) * HALF_B + wo);
   };
   // where the next K-tile's DMA is issued (variant bits 9-10): 0 before this
   // K-tile's first fragment reads, 1 right after them, 2 spread over the four
@@ -483,11 +519,11 @@ P2_DEVICE void gemm_body(const GemmParams& p, const LA& la0, const LB& lb0, int 
   // fragment rows: wave (wm, wn) owns A rows wm * 32 FM + 32 i, B rows wn * 32 FN + 32 j
   auto frag_a = [&](const char* s, int i, int ks) {
     const int r = wm * 32 * FM + 32 * i;
-    return frag<LA::KMAJ>(s + (r >> 7) * TILE, r & 127, ks, lane);
+    return frag<LA::KMAJ>(s + (r >> 7) * HALF_A, r & 127, ks, lane);
   };
   auto frag_b = [&](const char* s, int j, int ks) {
     const int r = wn * 32 * FN + 32 * j;
-    return frag<LB::KMAJ>(s + (HA + (r >> 7)) * TILE, r & 127, ks, lane);
+    return frag<LB::KMAJ>(s + HA * HALF_A + (r >> 7) * HALF_B, r & 127, ks, lane);
   };
   if constexpr (NBUF == 2) {
     if (nt > 0) {
@@ -534,8 +570,8 @@ P2_DEVICE void gemm_body(const GemmParams& p, const LA& la0, const LB& lb0, int 
     // the counted vmcnt retires exactly the tile read next (never vmcnt(0)
     // until the tail); the buffer restaged at iteration it is the one read at
     // it - 1, which every wave finished before passing this barrier.
-    constexpr int LPT = (HA / G + HB / G) * 4;  // DMAs per thread per K-tile
-    auto buf = [&](int t) { return smem + (t % NBUF) * CFG::STAGE; };
+    constexpr int LPT = (HA / G) * CHA + (HB / G) * CHB;  // DMAs per thread per K-tile
+    auto buf = [&](int t) { return smem + (t % NBUF) * STG; };
     for (int j = 0; j < NBUF - 1 && j < nt; ++j) stage_all(kb + j * BK, buf(j));
     for (int it = 0; it < nt; ++it) {
       const int ahead = min(nt - it - 1, NBUF - 2);  // K-tiles allowed to stay in flight
@@ -554,11 +590,11 @@ P2_DEVICE void gemm_body(const GemmParams& p, const LA& la0, const LB& lb0, int 
     // did, which serialised load and compute.
     const bool dma = !(p.variant & 128);  // bit 7: no DMA after the prologue (timing probe: compute only)
     for (int it = 0; it < nt; it += 2) {
-      compute(smem, (dma && it + 1 < nt) ? kb + (it + 1) * BK : -1, smem + CFG::STAGE);
+      compute(smem, (dma && it + 1 < nt) ? kb + (it + 1) * BK : -1, smem + STG);
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __syncthreads();
       if (it + 1 < nt) {
-        compute(smem + CFG::STAGE, (dma && it + 2 < nt) ? kb + (it + 2) * BK : -1, smem);
+        compute(smem + STG, (dma && it + 2 < nt) ? kb + (it + 2) * BK : -1, smem);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
       }
@@ -693,8 +729,8 @@ P2_DEVICE void gemm_body(const GemmParams& p, const LA& la0, const LB& lb0, int 
     float* s1p = reinterpret_cast<float*>(smem);          // [WAVES_M][16][CW]
     float* s2p = s1p + CFG::WAVES_M * 16 * CW;            // [WAVES_M][16][CW]
     float* shp = s2p + CFG::WAVES_M * 16 * CW;            // [WAVES_M][CW]
-    static_assert((2 * 16 + 1) * CFG::WAVES_M * CW * 4 <= smem_bytes<CFG, NBUF>(), "BN pass buffers fit the LDS");
-    static_assert(CFG::WAVES_M * CFG::BN * 3 * 4 <= smem_bytes<CFG, NBUF>(), "BN merge buffer fits the LDS");
+    static_assert(!BN || (2 * 16 + 1) * CFG::WAVES_M * CW * 4 <= SMEM, "BN pass buffers fit the LDS");
+    static_assert(!BN || CFG::WAVES_M * CFG::BN * 3 * 4 <= SMEM, "BN merge buffer fits the LDS");
     float keep[FN][3];
 #pragma unroll
     for (int j = 0; j < FN; ++j) {
@@ -877,9 +913,9 @@ P2_DEVICE void gemm_body(const GemmParams& p, const LA& la0, const LB& lb0, int 
   constexpr int LROW = CFG::BN * 2 + 16, CPR = CFG::BN / 8;
   // one pass over the whole tile when the kernel's LDS holds its image
   // (smem_bytes), else one pass per wave row
-  constexpr bool ONE = CFG::BM * LROW <= smem_bytes<CFG, NBUF>();
+  constexpr bool ONE = CFG::BM * LROW <= SMEM;
   constexpr int PASSES = ONE ? 1 : CFG::WAVES_M, ROWS = CFG::BM / PASSES;
-  static_assert(ROWS * LROW <= smem_bytes<CFG, NBUF>(), "epilogue image must fit the kernel's LDS");
+  static_assert(ROWS * LROW <= SMEM, "epilogue image must fit the kernel's LDS");
   static_assert((ROWS * CPR) % CFG::NT == 0, "whole chunks per thread");
 #pragma unroll
   for (int pass = 0; pass < PASSES; ++pass) {

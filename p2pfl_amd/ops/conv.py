@@ -78,10 +78,10 @@ def wgrad_splits(O: int, ncols: int, npix: int) -> int:
     return s
 
 
-def mn_splits(M: int, N: int, K: int) -> int:
-    """Split-K for a forward / input-gradient product whose output has few 128x128 tiles
-    (the 8x8 and 4x4 stages of a CIFAR ResNet): aim at one workgroup per CU, >= 256 deep."""
-    tiles = -(-M // 128) * -(-N // 128)
+def mn_splits(M: int, N: int, K: int, tile: int = 128) -> int:
+    """Split-K for a forward / input-gradient product whose output has few tile x tile
+    tiles (the 8x8 and 4x4 stages of a CIFAR ResNet): aim at one workgroup per CU, >= 256 deep."""
+    tiles = -(-M // tile) * -(-N // tile)
     s = 1
     while tiles * s < 256 and K // (s * 2) >= 256 and s < 16:
         s *= 2
@@ -106,6 +106,8 @@ def _run_split(launch, rows: int, cols: int, s: int, out: torch.Tensor, variant:
         launch(out, 1, None, None)
         return
     ws = torch.empty(s * slab_elems(rows, cols), dtype=torch.float32, device=out.device)
+    if variant & T64:  # 64 x 64 tiles: slabs + tile_slab_reduce only (no per-tile counters for them)
+        in_launch = False
     if in_launch if in_launch is not None else s <= _CONV_IN_LAUNCH_MAX_SPLITS:
         launch(out, s, ws, counters(tiles_of(rows, cols), out.device))
         return
@@ -125,6 +127,14 @@ def _run_split(launch, rows: int, cols: int, s: int, out: torch.Tensor, variant:
 # P2PFL_CONV_TUNE=0: the fixed defaults.
 _TUNE = os.environ.get("P2PFL_CONV_TUNE", "1") != "0"
 _TUNE_VARIANTS = (10, 2, 4096 | 2)
+# csrc/gemm.h kConvT64: 64 x 64 output tiles (gemm_core.h Tile64).  The 16x16 / 8x8 / 4x4
+# stages get 4x the tiles of a 128 x 128 grid -- the chip fills without split-K slabs and
+# their reduce launch -- and 64-channel products stop running half of every MFMA on
+# zero columns.  Offered beside the 128 x 128 kernels (single / double buffer, 4-stage
+# ring) with its own split-K options; P2PFL_CONV_T64=0 withdraws it.
+T64 = 1 << 14
+_T64 = os.environ.get("P2PFL_CONV_T64", "1") != "0"
+_TUNE_VARIANTS_T64 = (T64 | 10, T64 | 2, T64 | 4096 | 2)
 
 
 def _split_options(base: int, K: int, min_k: int = 128) -> Tuple[int, ...]:
@@ -142,6 +152,14 @@ def _configs(prefix: str, make, default_variant: int, splits) -> dict:
     a ResNet-18 product (``profiles/r5_conv_bench.md``)."""
     pre = f"{prefix}_" if prefix else ""
     return {f"{pre}v{v}_s{sp}": make(v, sp) for v in (_TUNE_VARIANTS if _TUNE else (default_variant,)) for sp in splits}
+
+
+def _configs_t64(prefix: str, make, splits) -> dict:
+    """The 64 x 64-tile candidates of one path (tuned runs only; P2PFL_CONV_T64=0: none)."""
+    if not (_TUNE and _T64):
+        return {}
+    pre = f"{prefix}_" if prefix else ""
+    return {f"{pre}v{v}_s{sp}": make(v, sp) for v in _TUNE_VARIANTS_T64 for sp in splits}
 
 
 def _pick(key, cands, default: str, out: torch.Tensor) -> None:
@@ -204,11 +222,13 @@ def dgrad_into(dy4: torch.Tensor, w4: torch.Tensor, stride: int, pad: int, dil: 
 
     base = mn_splits(rows, shape[3], K)
     cands = _configs("gather", gather, _V_DGRAD, _split_options(base, K))
+    cands.update(_configs_t64("gather", gather, _split_options(mn_splits(rows, shape[3], K, 64), K)))
     default = f"gather_v{_V_DGRAD}_s{base}"
     if s2_phases_ok(stride, dil, shape, (kh, kw)):
         kq = ((kh + 1) // 2) * ((kw + 1) // 2) * O  # K of one phase
         pbase = mn_splits(rows, shape[3], kq)
         cands.update(_configs("phase", phases, _V_DGRAD, _split_options(pbase, kq)))
+        cands.update(_configs_t64("phase", phases, _split_options(mn_splits(rows, shape[3], kq, 64), kq)))
         default = f"phase_v{_V_DGRAD}_s{pbase}"
         cands.setdefault(default, phases(_V_DGRAD, pbase))
     cands.setdefault(default, gather(_V_DGRAD, base))
@@ -229,6 +249,7 @@ def fwd_into(x4: torch.Tensor, w4: torch.Tensor, stride: int, pad: int, dil: int
 
     base = mn_splits(rows, O, K)
     cands = _configs("", one, _V_FWD, _split_options(base, K))
+    cands.update(_configs_t64("", one, _split_options(mn_splits(rows, O, K, 64), K)))
     _pick(("conv_fwd", tuple(x4.shape), O, kh, kw, stride, pad, dil), cands, f"v{_V_FWD}_s{base}", y4)
 
 
@@ -247,6 +268,7 @@ def wgrad_into(dy4: torch.Tensor, x4: torch.Tensor, stride: int, pad: int, dil: 
     base = wgrad_splits(O, ncols, npix)
     splits = sorted({max(1, base // 2), base} | ({base * 2} if npix // (base * 2) >= 256 else set()))
     cands = _configs("", one, _V_WGRAD, splits)
+    cands.update(_configs_t64("", one, splits))
     default = f"v{_V_WGRAD}_s{base}"
     if default not in cands:
         cands[default] = one(_V_WGRAD, base)

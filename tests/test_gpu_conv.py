@@ -147,6 +147,63 @@ def test_conv_split_k_in_launch_reduction(splits):
     assert int(cnt.abs().sum()) == 0
 
 
+@pytest.mark.parametrize("N,C,H,W,O,k,s,p,d", CASES)
+@pytest.mark.parametrize("variant", [conv_ops.T64 | 10, conv_ops.T64 | 2, conv_ops.T64 | 4096 | 2])
+@pytest.mark.parametrize("splits", [1, 3])
+def test_conv_t64_tiles_exact(N, C, H, W, O, k, s, p, d, variant, splits):
+    """64 x 64 output tiles (csrc/conv.hip conv64_kernel, variant bit 14) in all three
+    pipelines: forward, input and weight gradient equal the fp32 products exactly on
+    integer operands -- plain stores, and split-K slabs of the 64 x 64 geometry summed by
+    tile_slab_reduce with the same variant (ragged M / N tails included)."""
+    from p2pfl_amd.ops.splitk import slab_elems
+
+    x, w = _operands(N, C, H, W, O, k, seed=N + C + H + O + variant % 7, integer=True)
+    C_ = ops.ext()
+    x4, w4 = x.permute(0, 2, 3, 1), w.permute(0, 2, 3, 1)
+    OH, OW = conv_ops.out_hw(H, W, (k, k), s, p, d)
+    dy = torch.randint(-2, 3, (N, O, OH, OW), device="cuda").to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    dy4 = dy.permute(0, 2, 3, 1)
+    xr, wr = x.float().requires_grad_(), w.float().requires_grad_()
+    yr = _ref(xr, wr, s, p, d)
+    yr.backward(dy.float())
+
+    def run(launch, rows, cols, out_bf16):
+        if splits == 1:
+            out = torch.empty(rows, cols, device="cuda", dtype=torch.bfloat16 if out_bf16 else torch.float32)
+            launch(out, 1)
+            return out.float()
+        slabs = torch.empty(splits * slab_elems(rows, cols), device="cuda")
+        launch(slabs, splits)
+        out = torch.empty(rows, cols, device="cuda")
+        C_.tile_slab_reduce(slabs, splits, rows, cols, out, variant)
+        return out
+
+    y = run(lambda o, sp: C_.conv_fwd(x4, w4, s, p, d, o.view(N, OH, OW, O) if sp == 1 else o, sp, variant),
+            N * OH * OW, O, True)
+    ref_y = yr.detach().permute(0, 2, 3, 1).reshape(-1, O)
+    torch.testing.assert_close(y, ref_y.to(torch.bfloat16).float() if splits == 1 else ref_y, atol=0, rtol=0)
+    dx = run(lambda o, sp: C_.conv_dgrad(dy4, w4, s, p, d, o.view(N, H, W, C) if sp == 1 else o, [N, H, W, C], sp, variant),
+             N * H * W, C, True)
+    ref_dx = xr.grad.permute(0, 2, 3, 1).reshape(-1, C)
+    torch.testing.assert_close(dx, ref_dx.to(torch.bfloat16).float() if splits == 1 else ref_dx, atol=0, rtol=0)
+    dw = run(lambda o, sp: C_.conv_wgrad(dy4, x4, k, k, s, p, d, o.view(O, k, k, C) if sp == 1 else o, sp, variant),
+             O, k * k * C, False)
+    torch.testing.assert_close(dw, wr.grad.permute(0, 2, 3, 1).reshape(O, -1), atol=0, rtol=0)
+
+
+def test_conv_t64_refuses_counters_and_bn():
+    """The 64 x 64 tiles take split-K only through slabs: the in-launch reduction's
+    per-tile counters (sized for 128 x 128 tiles) are refused rather than overrun."""
+    from p2pfl_amd.ops.splitk import slab_elems, tiles_of
+
+    x, w = _operands(2, 64, 8, 8, 64, 3, seed=1, integer=True)
+    y4 = torch.empty(2, 8, 8, 64, device="cuda", dtype=torch.bfloat16)
+    ws = torch.empty(2 * slab_elems(128, 64), device="cuda")
+    cnt = torch.zeros(tiles_of(128, 64), dtype=torch.int32, device="cuda")
+    with pytest.raises(RuntimeError, match="64x64"):
+        ops.ext().conv_fwd(x.permute(0, 2, 3, 1), w.permute(0, 2, 3, 1), 1, 1, 1, y4, 2, conv_ops.T64 | 10, ws, cnt)
+
+
 S2_CASES = [
     # N, C, H, W, O, k, pad: shapes the by-phase stride-2 input gradient takes (N H W / 4 % 128 == 0)
     (8, 64, 16, 16, 128, 3, 1),
