@@ -65,6 +65,11 @@ void conv1_fwd(const uint8_t* x, const int64_t* idx, const float* params, Offset
 void conv2_fwd(const uint16_t* p1, const uint16_t* w2r, const float* params, Offsets off, uint16_t* a1, uint8_t* am2,
                int B, hipStream_t s);
 
+// conv1_fwd + conv2_fwd in one launch (P1 window in LDS per pooled row): writes AM1,
+// P1s (may be null = inference), A1, AM2 -- and P1 only when p1 is non-null
+void conv12_fwd(const uint8_t* x, const int64_t* idx, const float* params, Offsets off, const uint16_t* w2r,
+                uint16_t* p1, uint8_t* am1, uint16_t* p1s, uint16_t* a1, uint8_t* am2, int B, hipStream_t s);
+
 void gemm_skinny(const uint16_t* A, const uint16_t* Bt, float* slabs, int mrows, int N, int K, int S, hipStream_t s);
 
 // w2bf non-null: the FC2 weight is read from its bf16 copy [10][2048] (half the

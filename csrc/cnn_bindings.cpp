@@ -82,6 +82,25 @@ void k_conv2_fwd(torch::Tensor p1, torch::Tensor w2r, torch::Tensor params, std:
                    ptr<uint8_t>(am2, torch::kUInt8, B * 3136, "am2"), int(B), stream());
 }
 
+void k_conv12_fwd(torch::Tensor x, c10::optional<torch::Tensor> idx, torch::Tensor params, std::vector<int64_t> off,
+                  torch::Tensor w2r, c10::optional<torch::Tensor> p1, torch::Tensor am1, c10::optional<torch::Tensor> p1s,
+                  torch::Tensor a1, torch::Tensor am2, int64_t B, int64_t mrows) {
+  const c10::DeviceGuard g(params.device());
+  check_batch(int(B), int(mrows));
+  TORCH_CHECK(!(p1s.has_value() && p1s->defined()) || B <= 64, "conv12_fwd: training launches hold <= 64 images");
+  Offsets o = offsets(off);
+  TORCH_CHECK(x.numel() % 784 == 0, "x must be [N,1,28,28] uint8");
+  if (!idx.has_value()) TORCH_CHECK(x.numel() / 784 >= B, "x has fewer than B rows");
+  p2cnn::conv12_fwd(ptr<uint8_t>(x, torch::kUInt8, 784, "x", 1), idx_ptr(idx, int(B)),
+                    ptr<float>(params, torch::kFloat32, params_end(o), "params"), o,
+                    reinterpret_cast<uint16_t*>(ptr<at::BFloat16>(w2r, torch::kBFloat16, 51200, "w2r")),
+                    reinterpret_cast<uint16_t*>(optr<at::BFloat16>(p1, torch::kBFloat16, B * 196 * 32, "p1")),
+                    ptr<uint8_t>(am1, torch::kUInt8, B * 196 * 32, "am1"),
+                    reinterpret_cast<uint16_t*>(optr<at::BFloat16>(p1s, torch::kBFloat16, B * p2cnn::kP1s, "p1s")),
+                    reinterpret_cast<uint16_t*>(ptr<at::BFloat16>(a1, torch::kBFloat16, mrows * 3136, "a1")),
+                    ptr<uint8_t>(am2, torch::kUInt8, B * 3136, "am2"), int(B), stream());
+}
+
 void k_gemm_skinny(torch::Tensor A, torch::Tensor Bt, torch::Tensor slabs, int64_t mrows, int64_t N, int64_t K,
                    int64_t S) {
   const c10::DeviceGuard g(A.device());
@@ -258,6 +277,7 @@ void register_cnn(pybind11::module& m) {
   c.def("init", &p2cnn::init_attributes, "set kernel attributes (call before HIP graph capture)");
   c.def("conv1_fwd", &k_conv1_fwd);
   c.def("conv2_fwd", &k_conv2_fwd);
+  c.def("conv12_fwd", &k_conv12_fwd);
   c.def("gemm_skinny", &k_gemm_skinny);
   c.def("head", &k_head, pybind11::arg("slabs"), pybind11::arg("S"), pybind11::arg("mrows"), pybind11::arg("params"),
         pybind11::arg("off"), pybind11::arg("labels"), pybind11::arg("idx"), pybind11::arg("B"), pybind11::arg("train"),

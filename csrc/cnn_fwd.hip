@@ -284,6 +284,193 @@ __global__ __launch_bounds__(448) void conv2_fwd_lds_kernel(const uint16_t* __re
   }
 }
 
+// ---------------------------------------------------------------------------
+// 2+3. conv1 + conv2 in one launch.  Grid (7, B), 256 threads.  Block q of image
+//    b computes the pooled conv1 rows that conv2's pooled row q reads -- P1 rows
+//    2q-2 .. 2q+3, clipped to the image -- into an LDS window (HWC), with
+//    conv1_fwd_kernel's fp32 arithmetic in the same order (bitwise-equal values).
+//    Waves 0 and 1 then run conv2_fwd_kernel's MFMA sequence for (row q, oc half =
+//    wave), A fragments from the window instead of from global P1 (bitwise-equal
+//    A1), while waves 2 and 3 write AM1 / P1s (and P1 if asked) of the block's own
+//    rows 2q, 2q+1 -- what conv1_fwd_kernel block q writes.  The rows 2q +- 2 are
+//    also computed by the neighbouring blocks (3x conv1's VALU work); in exchange
+//    there is no P1 round trip through L2 and no second launch.  Measured arm,
+//    opt-in (learning/fused_cnn.py P2PFL_CNN_CONV12=1): 16.3 us against conv1 4.6 +
+//    conv2 6.0 us as two kernels (scripts/kbench.py, round 6) -- the recomputed
+//    rows put ~10 us of serial VALU work in front of every block's conv2.
+// ---------------------------------------------------------------------------
+constexpr int kWinRows = 6;  // P1 rows 2q-2 .. 2q+3
+
+__global__ __launch_bounds__(256) void conv12_fwd_kernel(const uint8_t* __restrict__ x,
+                                                         const int64_t* __restrict__ idx, const float* __restrict__ w1,
+                                                         const float* __restrict__ b1, const uint16_t* __restrict__ w2r,
+                                                         const float* __restrict__ b2, uint16_t* __restrict__ p1,
+                                                         uint8_t* __restrict__ am1, uint16_t* __restrict__ p1s,
+                                                         uint16_t* __restrict__ a1, uint8_t* __restrict__ am2) {
+  __shared__ float img[16][33];                                        // input rows 4q-6 .. 4q+9, padded
+  __shared__ __attribute__((aligned(16))) uint16_t win[kWinRows * 14 * kC1];  // P1 window, [row][px][ic]
+  __shared__ uint16_t sv[kC1][2][16];                                  // own rows, [oc][row][px], cols 14/15 zero
+  __shared__ __attribute__((aligned(16))) uint8_t sa[28][kC1];         // own rows' argmax codes [pos][oc]
+  __shared__ float sout[2][32][33];                                    // conv2 pool exchange, per wave
+  const int b = blockIdx.y, q = blockIdx.x, tid = threadIdx.x;
+  const int64_t row = idx ? idx[b] : b;
+  const uint8_t* src = x + row * (kImg * kImg);
+  for (int i = tid; i < 16 * 32; i += 256) {
+    const int yy = i >> 5, xx = i & 31, sy = 4 * q - 6 + yy, sx = xx - 2;
+    float v = 0.f;
+    if (sy >= 0 && sy < kImg && sx >= 0 && sx < kImg) v = float(src[sy * kImg + sx]) * (1.f / 255.f);
+    img[yy][xx] = v;
+  }
+  const int oc = tid & 31;
+  float w[kTaps];
+#pragma unroll
+  for (int t = 0; t < kTaps; ++t) w[t] = w1[oc * kTaps + t];
+  const float bias = b1[oc];
+  if (tid < kC1 * 2 * 2) sv[tid >> 2][(tid >> 1) & 1][14 + (tid & 1)] = 0;
+  __syncthreads();
+  // conv1: 6 window rows x 14 pooled columns per oc; rows outside the image stay zero
+  for (int k = tid >> 5; k < kWinRows * 14; k += 8) {
+    const int wr = k / 14, px = k % 14, prow = 2 * q - 2 + wr;
+    uint16_t out = 0;
+    if (prow >= 0 && prow < 14) {
+      float wv[6][6];
+#pragma unroll
+      for (int i = 0; i < 6; ++i)
+#pragma unroll
+        for (int j = 0; j < 6; ++j) wv[i][j] = img[2 * wr + i][2 * px + j];
+      float best = -3.4e38f;
+      int arg = 0;
+#pragma unroll
+      for (int d = 0; d < 4; ++d) {
+        const int dy = d >> 1, dx = d & 1;
+        float sacc = bias;
+#pragma unroll
+        for (int ky = 0; ky < 5; ++ky)
+#pragma unroll
+          for (int kx = 0; kx < 5; ++kx) sacc = fmaf(w[ky * 5 + kx], wv[dy + ky][dx + kx], sacc);
+        if (sacc > best) {
+          best = sacc;
+          arg = d;
+        }
+      }
+      out = f32_to_bf16(fmaxf(best, 0.f));
+      if (wr == 2 || wr == 3) {  // this block's own rows: AM1 / P1 / P1s come from here
+        sv[oc][wr - 2][px] = out;
+        sa[(wr - 2) * 14 + px][oc] = best > 0.f ? uint8_t(arg) : uint8_t(4);
+      }
+    }
+    win[k * kC1 + oc] = out;
+  }
+  __syncthreads();
+  const int wave = tid >> 6, lane = tid & 63;
+  if (wave < 2) {
+    // conv2 for pooled row q, oc half `wave`: conv2_fwd_kernel's loads and MFMA order
+    const int nh = wave, r = lane & 31, h = lane >> 5;
+    const int rr = r < 28 ? r : 27;
+    const int y = 2 * q + (rr >= 14 ? 1 : 0), xq = rr >= 14 ? rr - 14 : rr;
+    const uint16_t* wl = win + 8 * h;
+    const uint16_t* wrow = w2r + size_t(nh * 32 + r) * kTaps * kC1 + 8 * h;
+    const uint4 z4 = make_uint4(0, 0, 0, 0);
+    auto load = [&](int c, uint4 (&A)[10], uint4 (&Bv)[10]) {
+#pragma unroll
+      for (int j = 0; j < 10; ++j) {
+        const int st = c * 10 + j, t = st >> 1, ky = t / 5, kx = t % 5, ic = (st & 1) * 16;
+        const int iy = y + ky - 2, ix = xq + kx - 2;
+        const bool ok = iy >= 0 && iy < 14 && ix >= 0 && ix < 14;
+        const int pix = ok ? (iy - 2 * q + 2) * 14 + ix : 0;
+        const uint4 v = *reinterpret_cast<const uint4*>(wl + pix * kC1 + ic);
+        A[j] = ok ? v : z4;
+        Bv[j] = *reinterpret_cast<const uint4*>(wrow + t * kC1 + ic);
+      }
+    };
+    uint4 A0[10], B0[10], A1[10], B1[10];
+    f32x16 acc = {};
+    load(0, A0, B0);
+#pragma unroll
+    for (int c = 0; c < 5; c += 2) {
+      if (c + 1 < 5) load(c + 1, A1, B1);
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int j = 0; j < 10; ++j) acc = mfma32(A0[j], B0[j], acc);
+      __builtin_amdgcn_sched_barrier(0);
+      if (c + 1 < 5) {
+        if (c + 2 < 5) load(c + 2, A0, B0);
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int j = 0; j < 10; ++j) acc = mfma32(A1[j], B1[j], acc);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      const int rw = acc_row(i, h);
+      if (rw < 28) sout[nh][rw][r] = acc[i];
+    }
+  } else {
+    // conv1_fwd_kernel's stores of rows 2q, 2q+1 (threads 0..127 of waves 2-3)
+    const int t2 = tid - 128;
+    const size_t pix0 = size_t(b) * 196 + q * 28;
+    if (p1 && t2 < 28 * 4) {
+      const int k = t2 >> 2, c0 = (t2 & 3) * 8;
+      uint16_t u[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) u[j] = sv[c0 + j][k / 14][k % 14];
+      uint4 o;
+      o.x = uint32_t(u[0]) | (uint32_t(u[1]) << 16);
+      o.y = uint32_t(u[2]) | (uint32_t(u[3]) << 16);
+      o.z = uint32_t(u[4]) | (uint32_t(u[5]) << 16);
+      o.w = uint32_t(u[6]) | (uint32_t(u[7]) << 16);
+      reinterpret_cast<uint4*>(p1 + (pix0 + k) * kC1)[t2 & 3] = o;
+    }
+    if (t2 < 28 * 2) {
+      const int k = t2 >> 1, c0 = (t2 & 1) * 16;
+      reinterpret_cast<uint4*>(am1 + (pix0 + k) * kC1)[t2 & 1] = *reinterpret_cast<const uint4*>(&sa[k][c0]);
+    }
+    if (p1s) {
+      for (int i = t2; i < 5 * kC1 * 2 * 2; i += 128) {
+        const int half = i & 1, rr2 = (i >> 1) & 1, o = (i >> 2) % kC1, kx = i / (4 * kC1);
+        uint16_t u[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const int xs = half * 8 + j + kx - 2;
+          u[j] = (xs >= 0 && xs < 14) ? sv[o][rr2][xs] : uint16_t(0);
+        }
+        uint4 v;
+        v.x = uint32_t(u[0]) | (uint32_t(u[1]) << 16);
+        v.y = uint32_t(u[2]) | (uint32_t(u[3]) << 16);
+        v.z = uint32_t(u[4]) | (uint32_t(u[5]) << 16);
+        v.w = uint32_t(u[6]) | (uint32_t(u[7]) << 16);
+        *reinterpret_cast<uint4*>(p1s + ((size_t(b) * 5 + kx) * kC1 + o) * kP1sPlane + (2 * q + rr2 + 2) * 16 + half * 8) = v;
+      }
+    }
+  }
+  __syncthreads();
+  // conv2's bias + ReLU + 2x2 pool of both oc halves (conv2_fwd_kernel's epilogue)
+  for (int e = tid; e < 2 * 7 * 32; e += 256) {
+    const int nh = e / 224, ocx = (e % 224) / 7, px = e % 7;
+    const float v[4] = {sout[nh][2 * px][ocx], sout[nh][2 * px + 1][ocx], sout[nh][14 + 2 * px][ocx],
+                        sout[nh][15 + 2 * px][ocx]};
+    float best = v[0];
+    int arg = 0;
+#pragma unroll
+    for (int d = 1; d < 4; ++d)
+      if (v[d] > best) {
+        best = v[d];
+        arg = d;
+      }
+    best += b2[nh * 32 + ocx];
+    const size_t o = size_t(b) * kFeat + (nh * 32 + ocx) * 49 + q * 7 + px;
+    a1[o] = f32_to_bf16(fmaxf(best, 0.f));
+    am2[o] = best > 0.f ? uint8_t(arg) : uint8_t(4);
+  }
+}
+
+void conv12_fwd(const uint8_t* x, const int64_t* idx, const float* params, Offsets off, const uint16_t* w2r,
+                uint16_t* p1, uint8_t* am1, uint16_t* p1s, uint16_t* a1, uint8_t* am2, int B, hipStream_t s) {
+  hipLaunchKernelGGL(conv12_fwd_kernel, dim3(7, B), dim3(256), 0, s, x, idx, params + off.c1w, params + off.c1b, w2r,
+                     params + off.c2b, p1, am1, p1s, a1, am2);
+}
+
 void init_fwd_attributes() {}
 
 void conv2_fwd(const uint16_t* p1, const uint16_t* w2r, const float* params, Offsets off, uint16_t* a1,

@@ -58,6 +58,12 @@ _EVAL_LOW = os.environ.get("P2PFL_EVAL_STREAM_LOW", "1") != "0"
 # stream of its own).  In line: no stream hand-offs between the epoch and its
 # validation pass (1-peer round: in line 6.65 vs 7.23 ms, profiles/r5_handoff_probe.md).
 _EVAL_SIDE = os.environ.get("P2PFL_EVAL_SIDE_STREAM", "0")
+# conv1 + conv2 in one launch (csrc/cnn_fwd.hip conv12_fwd_kernel: each pooled-row block
+# recomputes the P1 rows its conv2 reads in LDS; no P1 round trip, one launch less).
+# Opt-in (P2PFL_CNN_CONV12=1): measured slower, 16.3 us vs 4.6 + 6.0 us for the two
+# kernels and 7.27 vs 6.66 ms per headline round (scripts/kbench.py, MI355X, round 6) --
+# the 3x conv1 VALU work of the recomputed halo rows sits in front of conv2 in every block.
+_CONV12 = os.environ.get("P2PFL_CNN_CONV12", "0") == "1"
 _NAMES = ("conv1.weight", "conv1.bias", "conv2.weight", "conv2.bias", "l1.weight", "l1.bias", "l2.weight", "l2.bias")
 FEAT, HID = 3136, 2048
 
@@ -159,8 +165,12 @@ class FusedCNNEngine:
 
     def forward(self, x: torch.Tensor, labels: torch.Tensor, idx: Optional[torch.Tensor], B: int, stats: torch.Tensor, train: bool) -> None:
         C, M = self.C, self.mrows
-        C.conv1_fwd(x, idx, self.params, self.off, self.p1, self.am1, self.p1s if train else None, B)
-        C.conv2_fwd(self.p1, self.w2r, self.params, self.off, self.a1, self.am2, B, M)
+        if _CONV12:
+            C.conv12_fwd(x, idx, self.params, self.off, self.w2r, None, self.am1, self.p1s if train else None, self.a1,
+                         self.am2, B, M)
+        else:
+            C.conv1_fwd(x, idx, self.params, self.off, self.p1, self.am1, self.p1s if train else None, B)
+            C.conv2_fwd(self.p1, self.w2r, self.params, self.off, self.a1, self.am2, B, M)
         C.gemm_skinny(self.a1, self.w1bf, self.slabs1, M, HID, FEAT, self.S1)
         C.head(self.slabs1, self.S1, M, self.params, self.off, labels, idx, B, train, self.H, self.dH, self.dlogits, stats,
                self.w2bf)
@@ -300,8 +310,11 @@ class _EvalForward:
     def forward(self, x: torch.Tensor, labels: torch.Tensor, idx: Optional[torch.Tensor], B: int, stats: torch.Tensor,
                 snap: _EvalSnapshot) -> None:
         e, C, M = self.eng, self.eng.C, self.MROWS
-        C.conv1_fwd(x, idx, snap.params, e.off, self.p1, self.am1, None, B)
-        C.conv2_fwd(self.p1, snap.w2r, snap.params, e.off, self.a1, self.am2, B, M)
+        if _CONV12:
+            C.conv12_fwd(x, idx, snap.params, e.off, snap.w2r, None, self.am1, None, self.a1, self.am2, B, M)
+        else:
+            C.conv1_fwd(x, idx, snap.params, e.off, self.p1, self.am1, None, B)
+            C.conv2_fwd(self.p1, snap.w2r, snap.params, e.off, self.a1, self.am2, B, M)
         C.gemm_skinny(self.a1, snap.w1bf, self.slabs1, M, HID, FEAT, e.S1)
         C.head(self.slabs1, e.S1, M, snap.params, e.off, labels, idx, B, False, self.H, self.dH, self.dlogits, stats,
                snap.w2bf)

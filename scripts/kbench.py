@@ -52,6 +52,7 @@ def main() -> None:
     ks = {
         "conv1_fwd": lambda: C.conv1_fwd(x, None, eng.params, eng.off, eng.p1, eng.am1, eng.p1s, B),
         "conv2_fwd": lambda: C.conv2_fwd(eng.p1, eng.w2r, eng.params, eng.off, eng.a1, eng.am2, B, M),
+        "conv12_fwd": lambda: C.conv12_fwd(x, None, eng.params, eng.off, eng.w2r, None, eng.am1, eng.p1s, eng.a1, eng.am2, B, M),
         "gemm_fc1": lambda: C.gemm_skinny(eng.a1, eng.w1bf, eng.slabs1, M, 2048, 3136, eng.S1),
         "head": lambda: C.head(eng.slabs1, eng.S1, M, eng.params, eng.off, y, None, B, True, eng.H, eng.dH, eng.dlogits, stats, eng.w2bf),
         "head_w2fp32": lambda: C.head(eng.slabs1, eng.S1, M, eng.params, eng.off, y, None, B, True, eng.H, eng.dH, eng.dlogits, stats),

@@ -44,10 +44,17 @@ def _close(got, want, rtol=1e-2, atol=1e-3):
     return frac
 
 
-def _forward(eng, x, train=False):
+def _forward(eng, x, train=False, nb=B):
+    from p2pfl_amd.learning import fused_cnn
+
     stats = torch.zeros(4, device="cuda")
-    y = torch.zeros(B, dtype=torch.int64, device="cuda")
-    eng.forward(x.reshape(-1, 784), y, None, B, stats, train)
+    y = torch.zeros(nb, dtype=torch.int64, device="cuda")
+    old = fused_cnn._CONV12
+    fused_cnn._CONV12 = False  # the per-kernel tests read P1, which only the two-kernel path writes
+    try:
+        eng.forward(x.reshape(-1, 784), y, None, nb, stats, train)
+    finally:
+        fused_cnn._CONV12 = old
     torch.cuda.synchronize()
 
 
@@ -109,6 +116,34 @@ def test_conv2_fwd(eng):
     ref = F.max_pool2d(F.relu(F.conv2d(p1, w, b, padding=2)), 2).reshape(B, -1)  # [B,3136]
     got = eng.a1.view(-1, 3136)[:B].float()
     assert _close(got, _bf(ref), rtol=1e-2, atol=1e-4) < 1e-3
+
+
+@pytest.mark.parametrize("train", [True, False])
+@pytest.mark.parametrize("nb", [B, 5])
+def test_conv12_fwd_bitwise_equals_two_kernels(eng, train, nb):
+    """conv1 + conv2 in one launch (P1 window recomputed per pooled-row block in LDS)
+    writes exactly what conv1_fwd + conv2_fwd write: P1, AM1, P1s, A1 and AM2 bitwise
+    (same fp32 conv1 arithmetic, same MFMA sequence for conv2), full and ragged batches."""
+    x = _x(11 + nb).reshape(-1, 784)
+    idx = torch.randperm(B, device="cuda")[:nb].contiguous()
+    C, M = eng.C, eng.mrows
+    bufs = {}
+    for fused in (False, True):
+        p1 = torch.full((M * 196 * 32,), 7, dtype=torch.bfloat16, device="cuda")
+        am1 = torch.full((M * 196 * 32,), 9, dtype=torch.uint8, device="cuda")
+        p1s = torch.full((M * 5 * 32 * 18 * 16,), 3, dtype=torch.bfloat16, device="cuda") if train else None
+        a1 = torch.zeros(M * 3136, dtype=torch.bfloat16, device="cuda")
+        am2 = torch.full((M * 3136,), 9, dtype=torch.uint8, device="cuda")
+        if fused:
+            C.conv12_fwd(x, idx, eng.params, eng.off, eng.w2r, p1, am1, p1s, a1, am2, nb, M)
+        else:
+            C.conv1_fwd(x, idx, eng.params, eng.off, p1, am1, p1s, nb)
+            C.conv2_fwd(p1, eng.w2r, eng.params, eng.off, a1, am2, nb, M)
+        torch.cuda.synchronize()
+        bufs[fused] = (p1, am1, p1s, a1, am2)
+    for name, u, v in zip(("p1", "am1", "p1s", "a1", "am2"), bufs[False], bufs[True]):
+        if u is not None:
+            assert torch.equal(u, v), name
 
 
 @pytest.mark.parametrize("N,K,S", [(2048, 3136, 7), (3136, 2048, 4), (64, 128, 3)])
@@ -283,9 +318,7 @@ def test_conv2_bwd(eng):
 def test_conv2_bwd_partial_batch(eng, Bp):
     """Odd / tiny batches: the last wgrad image pair holds one image."""
     x = _x(9)
-    stats = torch.zeros(4, device="cuda")
-    y = torch.zeros(Bp, dtype=torch.int64, device="cuda")
-    eng.forward(x.reshape(-1, 784), y, None, Bp, stats, True)
+    _forward(eng, x, True, Bp)  # two-kernel forward: the reference below reads its P1
     g = torch.Generator(device="cuda").manual_seed(5)
     dh = (torch.randn(32, 2048, device="cuda", generator=g) * 1e-2).to(torch.bfloat16)
     dh[Bp:] = 0
