@@ -10,10 +10,10 @@ uint8 on the device); normalisation to [0, 1] happens in ``forward``.
 Activations run channels-last on the GPU.  What runs per convolution
 (:func:`~p2pfl_amd.ops.conv.conv2d`):
 
-* 1x1 convolutions (bottlenecks, downsample shortcuts) are GEMMs over the
-  channels-last pixels (:func:`~p2pfl_amd.ops.conv.conv1x1_gemm` ->
-  :func:`~p2pfl_amd.ops.gemm.linear`: the hand-written MFMA GEMM or hipBLASLt,
-  whichever measured faster for the shape);
+* 1x1 convolutions (bottlenecks, downsample shortcuts) run on the same
+  implicit-GEMM conv kernels as the 3x3 ones, tuned per shape by the eager step
+  (``P2PFL_CONV1X1_MODE=gemm``: as native GEMMs over the channels-last pixels,
+  :func:`~p2pfl_amd.ops.conv.conv1x1_gemm` -> :func:`~p2pfl_amd.ops.gemm.linear`);
 * every other convolution but the 3-channel stem, inside the captured HIP step
   graphs (all full-batch training and evaluation steps), runs on the
   hand-written implicit-GEMM MFMA kernels (``csrc/conv.hip``: forward, input and

@@ -523,6 +523,16 @@ def conv_bn_act(x: torch.Tensor, conv: nn.Conv2d, bn: nn.BatchNorm2d, residual=N
 # weight gradients whenever PyTorch's allocator had to map new segments
 # (profiles/r3_nan_root_cause.md).  P2PFL_CONV1X1_GEMM=0 restores conv2d.
 _ONE_BY_ONE_GEMM = os.environ.get("P2PFL_CONV1X1_GEMM", "1") != "0"
+# Where a 1x1 convolution runs, eager and captured alike (P2PFL_CONV1X1_MODE):
+#   "conv"   (default) the implicit-GEMM conv kernels in both, tuned per shape by the eager
+#            step (64 x 64 tiles included), so the captured step replays measured choices;
+#   "gemm"   ops.gemm.linear in both (the GEMM is native-only, so graph-safe; under
+#            P2PFL_NATIVE_GEMM=library a capture takes the conv kernels);
+#   "legacy" round 5: GEMM eagerly, conv kernels inside a capture -- where no eager call
+#            had timed them, so every captured 1x1 ran the untuned default configuration.
+# Measured (MI355X, bench.py --steps 8, scripts/ab_conv1x1.sh): ResNet-50 conv 103.6 /
+# gemm 121.5 / legacy 108.8 ms per round; ResNet-18 conv 38.9 / gemm 40.7 ms.
+_1X1_MODE = os.environ.get("P2PFL_CONV1X1_MODE", "conv")
 
 
 def _is_1x1(x: torch.Tensor, conv: nn.Conv2d) -> bool:
@@ -562,10 +572,15 @@ def conv2d(x: torch.Tensor, conv: nn.Conv2d) -> torch.Tensor:
     # autotune against it).  This holds under every policy, "library" included,
     # and for 1x1 convolutions too (no hipBLASLt GEMM inside a graph).
     capturing = x.is_cuda and torch.cuda.is_current_stream_capturing()
+    if _1X1_MODE == "gemm" and _is_1x1(x, conv):
+        import importlib
+
+        if not capturing or importlib.import_module("p2pfl_amd.ops.gemm")._POLICY != "library":
+            return conv1x1_gemm(x, conv)
     if capturing and native_ok(x, conv):
         STATS["native_fwd"] += 1
         return _Conv2dNHWC.apply(x, conv.weight, _sym(conv.stride), _sym(conv.padding), _sym(conv.dilation))
-    if _is_1x1(x, conv):
+    if _1X1_MODE == "legacy" and _is_1x1(x, conv):
         return conv1x1_gemm(x, conv)
     if x.shape[1] < 8 and stem_ok(x, conv) and _POLICY != "library":
         return stem_conv2d(x, conv)

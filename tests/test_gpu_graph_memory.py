@@ -3,8 +3,9 @@
 The round-2 NaN of the 8-peer ResNet-50 scenario under rocprofv3 came from
 MIOpen's 1x1-convolution path replayed inside a captured step graph: once the
 allocator had to map new segments (a profiler allocates), the first replay of
-the next fit wrote non-finite weights.  1x1 convolutions now run as GEMMs over
-channels-last pixels (:func:`p2pfl_amd.ops.conv.conv1x1_gemm`).
+the next fit wrote non-finite weights.  1x1 convolutions now run on the hand-written
+implicit-GEMM conv kernels (default) or as native GEMMs over channels-last pixels
+(:func:`p2pfl_amd.ops.conv.conv1x1_gemm`, ``P2PFL_CONV1X1_MODE=gemm``).
 """
 
 from __future__ import annotations
@@ -31,8 +32,9 @@ def test_conv1x1_gemm_matches_fp32_conv(stride):
     m = m.to(torch.bfloat16).to(memory_format=torch.channels_last)
     x = torch.randn(4, 256, 14, 14, device="cuda", generator=g).to(torch.bfloat16)
     x = x.contiguous(memory_format=torch.channels_last).requires_grad_()
-    y = conv_ops.conv2d(x, m)
-    assert conv_ops.STATS["gemm_1x1_fwd"] > 0
+    before = conv_ops.STATS["gemm_1x1_fwd"]
+    y = conv_ops.conv1x1_gemm(x, m)
+    assert conv_ops.STATS["gemm_1x1_fwd"] == before + 1
     assert y.is_contiguous(memory_format=torch.channels_last)
     dy = torch.randn(y.shape, device="cuda", generator=g).to(torch.bfloat16)
     y.backward(dy)
