@@ -125,6 +125,31 @@ P2_DEVICE void stage_transposed(uint16_t* img, const uint16_t* src, int64_t rs, 
   }
 }
 
+// Row-major LDS image img[t][0..63] = src[min(t, T - 1)][0..63] for t < Tp, rows
+// kRS elements apart (144 B: the 16-B fragment reads of 16 lanes at rows t0..t0+15
+// land on distinct bank quads).  The main loops read their row-operand fragments
+// (K in the forward, Q / dO in dK/dV, K / V in dQ) from here instead of from
+// global memory -- they used to prefetch one 32-token tile ahead from L2, so every
+// tile waited out most of a load round trip (~10 tiles of ~0.4 us of compute each).
+// Clamped rows reproduce the loops' clampT addressing, so results are bitwise equal.
+constexpr int kRS = 72;
+template <int kThreads>
+P2_DEVICE void stage_rows(uint16_t* img, const uint16_t* src, int64_t rs, int T, int Tp) {
+  constexpr int kItems = (kMaxT * 8 + kThreads - 1) / kThreads;
+  uint4 v[kItems];
+#pragma unroll
+  for (int u = 0; u < kItems; ++u) {
+    const int i = threadIdx.x + u * kThreads, t = i >> 3, c = (i & 7) * 8;
+    v[u] = ld16_if(t < Tp, src + clampT(t, T) * rs + c);
+  }
+#pragma unroll
+  for (int u = 0; u < kItems; ++u) {
+    const int i = threadIdx.x + u * kThreads, t = i >> 3, c = (i & 7) * 8;
+    if (t < Tp) *reinterpret_cast<uint4*>(img + t * kRS + c) = v[u];
+  }
+}
+P2_DEVICE uint4 row_frag(const uint16_t* img, int t, int c) { return *reinterpret_cast<const uint4*>(img + t * kRS + c); }
+
 // rowsum(dO * O) over the 64 head dims of token t
 P2_DEVICE float dot64(const uint16_t* a, const uint16_t* b) {
   float s = 0.f;
@@ -144,10 +169,11 @@ P2_DEVICE float dot64(const uint16_t* a, const uint16_t* b) {
 // ---------------------------------------------------------------------------
 // forward.  Grid (T / 128, H, B), 4 waves: wave w owns queries [32 (4 x + w), +32).  lse2 = log2-domain log-sum-exp of the scaled scores.
 // ---------------------------------------------------------------------------
-template <int kWaves>
+template <int kWaves, bool kRows>
 __global__ __launch_bounds__(64 * kWaves) void attn_fwd_kernel(const uint16_t* __restrict__ qkv, uint16_t* __restrict__ o,
                                                        float* __restrict__ lse2, AttnShape sh) {
   __shared__ __attribute__((aligned(16))) uint16_t vt[kD * kSP];
+  __shared__ __attribute__((aligned(16))) uint16_t kr[kRows ? kMaxT * kRS : 8];  // K rows (kRows)
   const int b = blockIdx.z, hd = blockIdx.y, T = sh.T;
   const int64_t rs = sh.qkv_row;
   const uint16_t* Q = qkv + b * sh.qkv_batch + hd * kD;
@@ -155,6 +181,7 @@ __global__ __launch_bounds__(64 * kWaves) void attn_fwd_kernel(const uint16_t* _
   const uint16_t* V = Q + 2 * sh.C;
   const int nkt = (T + 31) >> 5;
   stage_transposed<64 * kWaves>(vt, V, rs, T, nkt * 32);
+  if constexpr (kRows) stage_rows<64 * kWaves>(kr, K, rs, T, nkt * 32);
   __syncthreads();
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, r = lane & 31, h = lane >> 5;
   const int q0 = (blockIdx.x * kWaves + wave) * 32;
@@ -167,15 +194,22 @@ __global__ __launch_bounds__(64 * kWaves) void attn_fwd_kernel(const uint16_t* _
   float m = -INFINITY, l = 0.f;
   const float sl2 = sh.scale * kLog2e;
   uint4 kn[4];
+  if constexpr (!kRows) {
 #pragma unroll
-  for (int s = 0; s < 4; ++s) kn[s] = ld16(K + clampT(r, T) * rs + 16 * s + 8 * h);
+    for (int s = 0; s < 4; ++s) kn[s] = ld16(K + clampT(r, T) * rs + 16 * s + 8 * h);
+  }
   for (int kt = 0; kt < nkt; ++kt) {
     uint4 kf[4];
+    if constexpr (kRows) {
 #pragma unroll
-    for (int s = 0; s < 4; ++s) kf[s] = kn[s];
-    const int nkey = (kt + 1) * 32 + r;  // prefetch the next key tile
+      for (int s = 0; s < 4; ++s) kf[s] = row_frag(kr, kt * 32 + r, 16 * s + 8 * h);
+    } else {
 #pragma unroll
-    for (int s = 0; s < 4; ++s) kn[s] = ld16(K + clampT(nkey, T) * rs + 16 * s + 8 * h);
+      for (int s = 0; s < 4; ++s) kf[s] = kn[s];
+      const int nkey = (kt + 1) * 32 + r;  // prefetch the next key tile
+#pragma unroll
+      for (int s = 0; s < 4; ++s) kn[s] = ld16(K + clampT(nkey, T) * rs + 16 * s + 8 * h);
+    }
     f32x16 st = zero16();
 #pragma unroll
     for (int s = 0; s < 4; ++s) st = mfma(kf[s], qf[s], st);
@@ -235,7 +269,7 @@ __global__ __launch_bounds__(64 * kWaves) void attn_fwd_kernel(const uint16_t* _
 // backward pass 1: dK, dV.  Grid (T / 128, H, B), wave w owns keys [32 (4 x + w), +32)
 // and loops over all query tiles (next tile's Q / dO rows prefetched).
 // ---------------------------------------------------------------------------
-template <int kWaves>
+template <int kWaves, bool kRows>
 __global__ __launch_bounds__(64 * kWaves) void attn_bwd_dkdv_kernel(const uint16_t* __restrict__ qkv,
                                                             const uint16_t* __restrict__ o,
                                                             const uint16_t* __restrict__ dout,
@@ -244,6 +278,8 @@ __global__ __launch_bounds__(64 * kWaves) void attn_bwd_dkdv_kernel(const uint16
   __shared__ __attribute__((aligned(16))) uint16_t qtl[kD * kSP];   // Q^T
   __shared__ __attribute__((aligned(16))) uint16_t dotl[kD * kSP];  // dO^T
   __shared__ float s_lse[kMaxT], s_dvec[kMaxT];
+  __shared__ __attribute__((aligned(16))) uint16_t qr[kRows ? kMaxT * kRS : 8];   // Q rows (kRows)
+  __shared__ __attribute__((aligned(16))) uint16_t dr[kRows ? kMaxT * kRS : 8];   // dO rows (kRows)
   const int b = blockIdx.z, hd = blockIdx.y, T = sh.T;
   const int64_t rs = sh.qkv_row;
   const uint16_t* Q = qkv + b * sh.qkv_batch + hd * kD;
@@ -255,6 +291,10 @@ __global__ __launch_bounds__(64 * kWaves) void attn_bwd_dkdv_kernel(const uint16
   const int nqt = (T + 31) >> 5, Tp = nqt * 32;
   stage_transposed<64 * kWaves>(qtl, Q, rs, T, Tp);
   stage_transposed<64 * kWaves>(dotl, DO, sh.o_row, T, Tp);
+  if constexpr (kRows) {
+    stage_rows<64 * kWaves>(qr, Q, rs, T, Tp);
+    stage_rows<64 * kWaves>(dr, DO, sh.o_row, T, Tp);
+  }
   for (int t = threadIdx.x; t < Tp; t += blockDim.x) {
     const bool ok = t < T;
     s_lse[t] = ok ? L[t] : INFINITY;  // padded queries: P = exp2(-inf) = 0
@@ -274,23 +314,33 @@ __global__ __launch_bounds__(64 * kWaves) void attn_bwd_dkdv_kernel(const uint16
   f32x16 dv0 = zero16(), dv1 = zero16(), dk0 = zero16(), dk1 = zero16();
   const float sl2 = sh.scale * kLog2e;
   uint4 qn[4], dn[4];
+  if constexpr (!kRows) {
 #pragma unroll
-  for (int s = 0; s < 4; ++s) {
-    qn[s] = ld16(Q + clampT(r, T) * rs + 16 * s + 8 * h);
-    dn[s] = ld16(DO + clampT(r, T) * sh.o_row + 16 * s + 8 * h);
+    for (int s = 0; s < 4; ++s) {
+      qn[s] = ld16(Q + clampT(r, T) * rs + 16 * s + 8 * h);
+      dn[s] = ld16(DO + clampT(r, T) * sh.o_row + 16 * s + 8 * h);
+    }
   }
   for (int qt = 0; qt < nqt; ++qt) {
     uint4 qa[4], da[4];
+    if constexpr (kRows) {
 #pragma unroll
-    for (int s = 0; s < 4; ++s) {
-      qa[s] = qn[s];
-      da[s] = dn[s];
-    }
-    const int nq = (qt + 1) * 32 + r;  // prefetch the next query tile
+      for (int s = 0; s < 4; ++s) {
+        qa[s] = row_frag(qr, qt * 32 + r, 16 * s + 8 * h);
+        da[s] = row_frag(dr, qt * 32 + r, 16 * s + 8 * h);
+      }
+    } else {
 #pragma unroll
-    for (int s = 0; s < 4; ++s) {
-      qn[s] = ld16(Q + clampT(nq, T) * rs + 16 * s + 8 * h);
-      dn[s] = ld16(DO + clampT(nq, T) * sh.o_row + 16 * s + 8 * h);
+      for (int s = 0; s < 4; ++s) {
+        qa[s] = qn[s];
+        da[s] = dn[s];
+      }
+      const int nq = (qt + 1) * 32 + r;  // prefetch the next query tile
+#pragma unroll
+      for (int s = 0; s < 4; ++s) {
+        qn[s] = ld16(Q + clampT(nq, T) * rs + 16 * s + 8 * h);
+        dn[s] = ld16(DO + clampT(nq, T) * sh.o_row + 16 * s + 8 * h);
+      }
     }
     f32x16 sacc = zero16(), dp = zero16();
 #pragma unroll
@@ -335,13 +385,15 @@ __global__ __launch_bounds__(64 * kWaves) void attn_bwd_dkdv_kernel(const uint16
 // backward pass 2: dQ.  Grid (T / 128, H, B), wave w owns queries [32 (4 x + w), +32)
 // and loops over all key tiles (next tile's K / V rows prefetched).
 // ---------------------------------------------------------------------------
-template <int kWaves>
+template <int kWaves, bool kRows>
 __global__ __launch_bounds__(64 * kWaves) void attn_bwd_dq_kernel(const uint16_t* __restrict__ qkv,
                                                           const uint16_t* __restrict__ o,
                                                           const uint16_t* __restrict__ dout,
                                                           const float* __restrict__ lse2, uint16_t* __restrict__ dqkv,
                                                           AttnShape sh) {
   __shared__ __attribute__((aligned(16))) uint16_t ktl[kD * kSP];  // K^T
+  __shared__ __attribute__((aligned(16))) uint16_t kr[kRows ? kMaxT * kRS : 8];  // K rows (kRows)
+  __shared__ __attribute__((aligned(16))) uint16_t vr[kRows ? kMaxT * kRS : 8];  // V rows (kRows)
   const int b = blockIdx.z, hd = blockIdx.y, T = sh.T;
   const int64_t rs = sh.qkv_row;
   const uint16_t* Q = qkv + b * sh.qkv_batch + hd * kD;
@@ -351,6 +403,10 @@ __global__ __launch_bounds__(64 * kWaves) void attn_bwd_dq_kernel(const uint16_t
   const uint16_t* DO = dout + b * sh.o_batch + hd * kD;
   const int nkt = (T + 31) >> 5;
   stage_transposed<64 * kWaves>(ktl, K, rs, T, nkt * 32);
+  if constexpr (kRows) {
+    stage_rows<64 * kWaves>(kr, K, rs, T, nkt * 32);
+    stage_rows<64 * kWaves>(vr, V, rs, T, nkt * 32);
+  }
   __syncthreads();
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, r = lane & 31, h = lane >> 5;
   const int q0 = (blockIdx.x * kWaves + wave) * 32;
@@ -383,23 +439,33 @@ __global__ __launch_bounds__(64 * kWaves) void attn_bwd_dq_kernel(const uint16_t
   f32x16 dq0 = zero16(), dq1 = zero16();
   const float sl2 = sh.scale * kLog2e;
   uint4 kn[4], vn[4];
+  if constexpr (!kRows) {
 #pragma unroll
-  for (int s = 0; s < 4; ++s) {
-    kn[s] = ld16(K + clampT(r, T) * rs + 16 * s + 8 * h);
-    vn[s] = ld16(V + clampT(r, T) * rs + 16 * s + 8 * h);
+    for (int s = 0; s < 4; ++s) {
+      kn[s] = ld16(K + clampT(r, T) * rs + 16 * s + 8 * h);
+      vn[s] = ld16(V + clampT(r, T) * rs + 16 * s + 8 * h);
+    }
   }
   for (int kt = 0; kt < nkt; ++kt) {
     uint4 ka[4], va[4];
+    if constexpr (kRows) {
 #pragma unroll
-    for (int s = 0; s < 4; ++s) {
-      ka[s] = kn[s];
-      va[s] = vn[s];
-    }
-    const int nk = (kt + 1) * 32 + r;  // prefetch the next key tile
+      for (int s = 0; s < 4; ++s) {
+        ka[s] = row_frag(kr, kt * 32 + r, 16 * s + 8 * h);
+        va[s] = row_frag(vr, kt * 32 + r, 16 * s + 8 * h);
+      }
+    } else {
 #pragma unroll
-    for (int s = 0; s < 4; ++s) {
-      kn[s] = ld16(K + clampT(nk, T) * rs + 16 * s + 8 * h);
-      vn[s] = ld16(V + clampT(nk, T) * rs + 16 * s + 8 * h);
+      for (int s = 0; s < 4; ++s) {
+        ka[s] = kn[s];
+        va[s] = vn[s];
+      }
+      const int nk = (kt + 1) * 32 + r;  // prefetch the next key tile
+#pragma unroll
+      for (int s = 0; s < 4; ++s) {
+        kn[s] = ld16(K + clampT(nk, T) * rs + 16 * s + 8 * h);
+        vn[s] = ld16(V + clampT(nk, T) * rs + 16 * s + 8 * h);
+      }
     }
     f32x16 st = zero16(), dpt = zero16();
 #pragma unroll
@@ -450,23 +516,42 @@ static int attention_waves() {
   }();
   return w;
 }
+// row operands staged in LDS (default) or streamed from L2 one tile ahead
+// (P2PFL_ATTN_LDS_ROWS=0, the round-5 kernels)
+static bool attention_rows() {
+  static const bool on = [] {
+    const char* e = getenv("P2PFL_ATTN_LDS_ROWS");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
+
+template <int W, bool R>
+static void fwd_w(const uint16_t* qkv, uint16_t* o, float* lse2, const AttnShape& sh, hipStream_t s) {
+  hipLaunchKernelGGL((attn_fwd_kernel<W, R>), grid_of<W>(sh), dim3(64 * W), 0, s, qkv, o, lse2, sh);
+}
+template <int W, bool R>
+static void bwd_w(const uint16_t* qkv, const uint16_t* o, const uint16_t* dout, const float* lse2, uint16_t* dqkv,
+                  const AttnShape& sh, hipStream_t s) {
+  hipLaunchKernelGGL((attn_bwd_dkdv_kernel<W, R>), grid_of<W>(sh), dim3(64 * W), 0, s, qkv, o, dout, lse2, dqkv, sh);
+  hipLaunchKernelGGL((attn_bwd_dq_kernel<W, R>), grid_of<W>(sh), dim3(64 * W), 0, s, qkv, o, dout, lse2, dqkv, sh);
+}
 
 void attention_fwd(const uint16_t* qkv, uint16_t* o, float* lse2, const AttnShape& sh, hipStream_t s) {
+  const bool r = attention_rows();
   if (attention_waves() == 8)
-    hipLaunchKernelGGL(attn_fwd_kernel<8>, grid_of<8>(sh), dim3(512), 0, s, qkv, o, lse2, sh);
+    r ? fwd_w<8, true>(qkv, o, lse2, sh, s) : fwd_w<8, false>(qkv, o, lse2, sh, s);
   else
-    hipLaunchKernelGGL(attn_fwd_kernel<4>, grid_of<4>(sh), dim3(256), 0, s, qkv, o, lse2, sh);
+    r ? fwd_w<4, true>(qkv, o, lse2, sh, s) : fwd_w<4, false>(qkv, o, lse2, sh, s);
 }
 
 void attention_bwd(const uint16_t* qkv, const uint16_t* o, const uint16_t* dout, const float* lse2, uint16_t* dqkv,
                    const AttnShape& sh, hipStream_t s) {
-  if (attention_waves() == 8) {
-    hipLaunchKernelGGL(attn_bwd_dkdv_kernel<8>, grid_of<8>(sh), dim3(512), 0, s, qkv, o, dout, lse2, dqkv, sh);
-    hipLaunchKernelGGL(attn_bwd_dq_kernel<8>, grid_of<8>(sh), dim3(512), 0, s, qkv, o, dout, lse2, dqkv, sh);
-  } else {
-    hipLaunchKernelGGL(attn_bwd_dkdv_kernel<4>, grid_of<4>(sh), dim3(256), 0, s, qkv, o, dout, lse2, dqkv, sh);
-    hipLaunchKernelGGL(attn_bwd_dq_kernel<4>, grid_of<4>(sh), dim3(256), 0, s, qkv, o, dout, lse2, dqkv, sh);
-  }
+  const bool r = attention_rows();
+  if (attention_waves() == 8)
+    r ? bwd_w<8, true>(qkv, o, dout, lse2, dqkv, sh, s) : bwd_w<8, false>(qkv, o, dout, lse2, dqkv, sh, s);
+  else
+    r ? bwd_w<4, true>(qkv, o, dout, lse2, dqkv, sh, s) : bwd_w<4, false>(qkv, o, dout, lse2, dqkv, sh, s);
 }
 
 }  // namespace p2attn

@@ -306,6 +306,22 @@ def _cfg_ok(v: int, sp: int, M: int, N: int, K: int, a_kmajor: bool, b_kmajor: b
     return not (epilogue and sp > IN_LAUNCH_MAX_SPLITS)
 
 
+_ZERO_BIAS: dict = {}
+
+
+def _zero_bias(n: int, device: torch.device) -> torch.Tensor:
+    """A read-only fp32 zero vector of ``n`` (the bias operand of the fused GELU backward,
+    whose pre-activation already includes the bias): allocated once per (n, device) outside
+    a capture, so replayed steps carry no fill kernel (12 per ViT-B step before)."""
+    key = (n, device)
+    z = _ZERO_BIAS.get(key)
+    if z is None:
+        z = torch.zeros(n, dtype=torch.float32, device=device)
+        if not (device.type == "cuda" and torch.cuda.is_current_stream_capturing()):
+            _ZERO_BIAS[key] = z
+    return z
+
+
 class _LinearP(torch.autograd.Function):
     """``y = x W^T + b`` (or ``gelu(x W^T + b)``) whose three products -- forward,
     input gradient, weight gradient -- each run on the MFMA kernel configuration
@@ -326,7 +342,7 @@ class _LinearP(torch.autograd.Function):
             y = gemm(x2, wc, bias=b, variant=v, splits=sp)[0]  # the epilogue reads an fp32 or a bf16 bias
         else:
             y, pre = gemm(x2, wc, bias=b, gelu=True, want_z=True, variant=v, splits=sp)  # pre-activation includes the bias
-            gb = torch.zeros(w.shape[0], dtype=torch.float32, device=x.device)
+            gb = _zero_bias(w.shape[0], x.device)
         STATS["native"] += 1
         ctx.save_for_backward(x2, wc, pre, gb)
         ctx.gelu, ctx.plan = gelu, plan
