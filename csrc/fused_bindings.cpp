@@ -24,6 +24,60 @@ void check_f32(const torch::Tensor& t, int64_t n, const char* name) {
   TORCH_CHECK(t.numel() >= n, name, " too small");
 }
 
+// uint8 [B, C, H, W] -> bf16 [B, (H/P)(W/P), C P P] / 255
+torch::Tensor patchify_u8(torch::Tensor x, int64_t P) {
+  const c10::DeviceGuard g(x.device());
+  TORCH_CHECK(x.is_cuda() && x.is_contiguous() && x.scalar_type() == torch::kUInt8 && x.dim() == 4,
+              "patchify_u8: x must be a contiguous uint8 [B, C, H, W] GPU tensor");
+  const int64_t B = x.size(0), C = x.size(1), H = x.size(2), W = x.size(3);
+  TORCH_CHECK(P > 0 && P % 8 == 0 && H % P == 0 && W % P == 0, "patchify_u8: P % 8 == 0 and P | H, W");
+  auto out = torch::empty({B, (H / P) * (W / P), C * P * P}, x.options().dtype(torch::kBFloat16));
+  if (out.numel() > 0)
+    p2fused::patchify_u8(x.data_ptr<uint8_t>(), reinterpret_cast<uint16_t*>(out.data_ptr()), int(B), int(C), int(H),
+                         int(W), int(P), stream());
+  return out;
+}
+
+void check_bf16(const torch::Tensor& t, const char* name) {
+  TORCH_CHECK(t.is_cuda() && t.is_contiguous() && t.scalar_type() == torch::kBFloat16 &&
+                  reinterpret_cast<uintptr_t>(t.data_ptr()) % 16 == 0,
+              name, " must be a contiguous 16-byte aligned bf16 GPU tensor");
+}
+
+// y [B, N, D], cls [D], pos [N + 1, D] (bf16) -> h [B, N + 1, D]
+torch::Tensor embed_tokens_fwd(torch::Tensor y, torch::Tensor cls, torch::Tensor pos) {
+  const c10::DeviceGuard g(y.device());
+  check_bf16(y, "y");
+  check_bf16(cls, "cls");
+  check_bf16(pos, "pos");
+  TORCH_CHECK(y.dim() == 3, "embed_tokens: y must be [B, N, D]");
+  const int64_t B = y.size(0), N = y.size(1), D = y.size(2);
+  TORCH_CHECK(D % 8 == 0 && cls.numel() == D && pos.numel() == (N + 1) * D, "embed_tokens: shapes");
+  TORCH_CHECK(cls.device() == y.device() && pos.device() == y.device(), "embed_tokens: devices");
+  auto h = torch::empty({B, N + 1, D}, y.options());
+  if (h.numel() > 0)
+    p2fused::embed_tokens_fwd(reinterpret_cast<const uint16_t*>(y.data_ptr()), reinterpret_cast<const uint16_t*>(cls.data_ptr()),
+                              reinterpret_cast<const uint16_t*>(pos.data_ptr()), reinterpret_cast<uint16_t*>(h.data_ptr()),
+                              int(B), int(N), int(D), stream());
+  return h;
+}
+
+// dh [B, N + 1, D] -> (dy [B, N, D], dpos [N + 1, D], dcls [D])
+std::vector<torch::Tensor> embed_tokens_bwd(torch::Tensor dh) {
+  const c10::DeviceGuard g(dh.device());
+  check_bf16(dh, "dh");
+  TORCH_CHECK(dh.dim() == 3 && dh.size(1) >= 1 && dh.size(2) % 8 == 0, "embed_tokens_bwd: dh must be [B, N + 1, D]");
+  const int64_t B = dh.size(0), N = dh.size(1) - 1, D = dh.size(2);
+  auto dy = torch::empty({B, N, D}, dh.options());
+  auto dpos = torch::empty({N + 1, D}, dh.options());
+  auto dcls = torch::empty({D}, dh.options());
+  if (dpos.numel() > 0)
+    p2fused::embed_tokens_bwd(reinterpret_cast<const uint16_t*>(dh.data_ptr()), reinterpret_cast<uint16_t*>(dy.data_ptr()),
+                              reinterpret_cast<uint16_t*>(dpos.data_ptr()), reinterpret_cast<uint16_t*>(dcls.data_ptr()),
+                              int(B), int(N), int(D), stream());
+  return {dy, dpos, dcls};
+}
+
 std::vector<torch::Tensor> ln_fwd(torch::Tensor x, torch::Tensor w, torch::Tensor b, double eps,
                                   c10::optional<torch::Tensor> residual) {
   const c10::DeviceGuard g(x.device());
@@ -251,6 +305,9 @@ void multi_copy(std::vector<torch::Tensor> dsts, std::vector<torch::Tensor> srcs
 
 void register_fused(pybind11::module& m) {
   auto f = m.def_submodule("fused", "fused LayerNorm / bias+GELU / softmax cross-entropy kernels");
+  f.def("patchify_u8", &patchify_u8, "uint8 images -> bf16 ViT patch rows / 255", pybind11::arg("x"), pybind11::arg("P"));
+  f.def("embed_tokens_fwd", &embed_tokens_fwd, "cat(cls, y) + pos in one pass (bf16)");
+  f.def("embed_tokens_bwd", &embed_tokens_bwd, "dy = dh[:, 1:], dpos = sum_b dh, dcls = dpos[0]");
   f.def("ln_fwd", &ln_fwd, pybind11::arg("x"), pybind11::arg("w"), pybind11::arg("b"), pybind11::arg("eps"),
         pybind11::arg("residual") = pybind11::none());
   f.def("ln_bwd", &ln_bwd, pybind11::arg("dy"), pybind11::arg("x"), pybind11::arg("w"), pybind11::arg("mean"),

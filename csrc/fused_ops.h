@@ -42,6 +42,16 @@ struct CopyList {
 };
 void multi_copy(const CopyList& cl, hipStream_t s);
 
+// ViT patch embedding input: uint8 images [B][C][H][W] -> bf16 patch rows [B * (H/P) * (W/P)][C * P * P]
+// in Conv2d(C, D, P, stride P) weight order, values / 255 (P % 8 == 0)
+void patchify_u8(const uint8_t* x, uint16_t* out, int B, int C, int H, int W, int P, hipStream_t s);
+// h[b][0] = cls + pos[0], h[b][1 + i] = y[b][i] + pos[1 + i]  (bf16, D % 8 == 0): the token concat + position
+// embedding of a ViT in one pass; backward: dy = dh[:, 1:] (contiguous), dpos = sum_b dh[b], dcls = dpos[0]
+void embed_tokens_fwd(const uint16_t* y, const uint16_t* cls, const uint16_t* pos, uint16_t* h, int B, int N, int D,
+                      hipStream_t s);
+void embed_tokens_bwd(const uint16_t* dh, uint16_t* dy, uint16_t* dpos, uint16_t* dcls, int B, int N, int D,
+                      hipStream_t s);
+
 void xent_fwd(bool bf16, const void* z, const int64_t* y, float* loss, float* lse, int N, int K, hipStream_t s);
 void xent_bwd(bool bf16, const void* z, const int64_t* y, const float* lse, const float* gscale, void* dz, int N, int K,
               hipStream_t s);

@@ -499,6 +499,101 @@ static int rows_grid(int N) {
   return g > 4096 ? 4096 : (g < 1 ? 1 : g);
 }
 
+// ---------------------------------------------------------------------------
+// ViT embedding: patchify of the uint8 batch, token concat + position embedding
+// ---------------------------------------------------------------------------
+// One thread per 8 consecutive patch-row elements (same channel and patch row,
+// 8 adjacent pixels): one 8-byte load, one 16-byte store.  Replaces the float
+// cast, the /255 multiply, the patch permute copy and the bf16 cast of the
+// model's eager prologue (4 launches over the fp32 image).
+__global__ __launch_bounds__(256) void patchify_u8_kernel(const uint8_t* __restrict__ x, uint16_t* __restrict__ out,
+                                                          int B, int C, int H, int W, int P) {
+  const int gw = W / P, np = (H / P) * gw, cols = C * P * P, c8 = cols / 8;
+  const int64_t i = int64_t(blockIdx.x) * 256 + threadIdx.x;
+  if (i >= int64_t(B) * np * c8) return;
+  const int64_t prow = i / c8;
+  const int k = int(i - prow * c8) * 8;  // column within the patch row
+  const int b = int(prow / np), pi = int(prow - int64_t(b) * np), py = pi / gw, px = pi - py * gw;
+  const int c = k / (P * P), rem = k - c * P * P, iy = rem / P, ix = rem - iy * P;
+  const uint2 u = *reinterpret_cast<const uint2*>(x + ((int64_t(b) * C + c) * H + py * P + iy) * W + px * P + ix);
+  const uint32_t w[2] = {u.x, u.y};
+  float v[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) v[j] = float((w[j >> 2] >> (8 * (j & 3))) & 0xffu) * (1.f / 255.f);
+  Vec8<uint16_t>::store(out + prow * cols + k, v);
+}
+
+void patchify_u8(const uint8_t* x, uint16_t* out, int B, int C, int H, int W, int P, hipStream_t s) {
+  const int64_t n = int64_t(B) * (H / P) * (W / P) * (C * P * P / 8);
+  hipLaunchKernelGGL(patchify_u8_kernel, dim3(int((n + 255) / 256)), dim3(256), 0, s, x, out, B, C, H, W, P);
+}
+
+// h = cat(cls, y) + pos, rounded once to bf16 (what the bf16 cat + add stored)
+__global__ __launch_bounds__(256) void embed_tokens_fwd_kernel(const uint16_t* __restrict__ y,
+                                                               const uint16_t* __restrict__ cls,
+                                                               const uint16_t* __restrict__ pos, uint16_t* __restrict__ h,
+                                                               int B, int N, int D) {
+  const int d8 = D / 8;
+  const int64_t i = int64_t(blockIdx.x) * 256 + threadIdx.x;
+  if (i >= int64_t(B) * (N + 1) * d8) return;
+  const int64_t row = i / d8;
+  const int k = int(i - row * d8) * 8;
+  const int b = int(row / (N + 1)), t = int(row - int64_t(b) * (N + 1));
+  float a[8], p[8];
+  Vec8<uint16_t>::load(t == 0 ? cls + k : y + (int64_t(b) * N + t - 1) * D + k, a);
+  Vec8<uint16_t>::load(pos + int64_t(t) * D + k, p);
+#pragma unroll
+  for (int j = 0; j < 8; ++j) a[j] += p[j];
+  Vec8<uint16_t>::store(h + row * D + k, a);
+}
+
+// One thread per (token, 8 channels): the batch sum of dh in fixed order (fp32,
+// rounded to the bf16 parameter gradient), and the patch tokens' rows copied out
+// contiguously for the patch-embedding GEMM's backward -- all B loads in flight.
+__global__ __launch_bounds__(256) void embed_tokens_bwd_kernel(const uint16_t* __restrict__ dh,
+                                                               uint16_t* __restrict__ dy,
+                                                               uint16_t* __restrict__ dpos,
+                                                               uint16_t* __restrict__ dcls, int B, int N, int D) {
+  const int d8 = D / 8;
+  const int64_t i = int64_t(blockIdx.x) * 256 + threadIdx.x;
+  if (i >= int64_t(N + 1) * d8) return;
+  const int t = int(i / d8), k = int(i - int64_t(t) * d8) * 8;
+  float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  constexpr int kU = 8;
+  for (int b0 = 0; b0 < B; b0 += kU) {
+    uint4 u[kU];
+#pragma unroll
+    for (int q = 0; q < kU; ++q)
+      u[q] = b0 + q < B ? *reinterpret_cast<const uint4*>(dh + ((int64_t(b0 + q) * (N + 1)) + t) * D + k)
+                        : make_uint4(0, 0, 0, 0);
+#pragma unroll
+    for (int q = 0; q < kU; ++q) {
+      if (b0 + q >= B) break;
+      if (t > 0) *reinterpret_cast<uint4*>(dy + (int64_t(b0 + q) * N + t - 1) * D + k) = u[q];
+      const uint32_t w[4] = {u[q].x, u[q].y, u[q].z, u[q].w};
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        acc[2 * j] += __uint_as_float(w[j] << 16);
+        acc[2 * j + 1] += __uint_as_float(w[j] & 0xffff0000u);
+      }
+    }
+  }
+  Vec8<uint16_t>::store(dpos + int64_t(t) * D + k, acc);
+  if (t == 0) Vec8<uint16_t>::store(dcls + k, acc);
+}
+
+void embed_tokens_fwd(const uint16_t* y, const uint16_t* cls, const uint16_t* pos, uint16_t* h, int B, int N, int D,
+                      hipStream_t s) {
+  const int64_t n = int64_t(B) * (N + 1) * (D / 8);
+  hipLaunchKernelGGL(embed_tokens_fwd_kernel, dim3(int((n + 255) / 256)), dim3(256), 0, s, y, cls, pos, h, B, N, D);
+}
+
+void embed_tokens_bwd(const uint16_t* dh, uint16_t* dy, uint16_t* dpos, uint16_t* dcls, int B, int N, int D,
+                      hipStream_t s) {
+  const int64_t n = int64_t(N + 1) * (D / 8);
+  hipLaunchKernelGGL(embed_tokens_bwd_kernel, dim3(int((n + 255) / 256)), dim3(256), 0, s, dh, dy, dpos, dcls, B, N, D);
+}
+
 template <typename T>
 static void ln_fwd_t(const void* x, const void* r, const float* w, const float* b, void* y, void* sum, float* mean,
                      float* rstd, int N, int C, float eps, hipStream_t s) {

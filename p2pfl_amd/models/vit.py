@@ -123,10 +123,19 @@ class ViT(FLModule):
         nn.init.uniform_(w, -1 / math.sqrt(w[0].numel()), 1 / math.sqrt(w[0].numel()))
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
-        if x.dtype == torch.uint8:
-            x = x.float().mul_(1.0 / 255.0)
-        x = self._patchify_embed(x)
-        x = torch.cat([self.cls_token.expand(x.shape[0], -1, -1).to(x.dtype), x], dim=1) + self.pos_embed.to(x.dtype)
+        P = self.patch_embed.weight.shape[-1]
+        if x.dtype == torch.uint8 and _fused(x) and P % 8 == 0 and x.shape[2] % P == 0 and x.shape[3] % P == 0:
+            # one kernel: uint8 -> bf16 patch rows / 255 (the same values the float cast, the
+            # scale and the GEMM's bf16 cast produced), then the patch-embedding GEMM
+            w = self.patch_embed.weight
+            x = ops.linear(ops.patchify_u8(x, P), w.view(w.shape[0], -1), self.patch_embed.bias)
+        else:
+            if x.dtype == torch.uint8:
+                x = x.float().mul_(1.0 / 255.0)
+            x = self._patchify_embed(x)
+        # class token + position embedding (one kernel each way on the GPU, bf16)
+        x = ops.embed_tokens(x, self.cls_token, self.pos_embed) if _fused(x) else (
+            torch.cat([self.cls_token.expand(x.shape[0], -1, -1).to(x.dtype), x], dim=1) + self.pos_embed.to(x.dtype))
         if _fused(x):
             return ops.linear(self._encoder_fused(x)[:, 0], self.head.weight, self.head.bias)
         x = self.norm(self.blocks(x))

@@ -253,8 +253,10 @@ from p2pfl_amd.ops.fused import (  # noqa: E402
     attention_qkv_reference,
     bias_gelu,
     bias_gelu_reference,
+    embed_tokens,
     layer_norm,
     layer_norm_reference,
+    patchify_u8,
     softmax_xent,
     softmax_xent_reference,
 )

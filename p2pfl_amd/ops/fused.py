@@ -230,6 +230,35 @@ def softmax_xent(logits: torch.Tensor, labels: torch.Tensor) -> torch.Tensor:
 
 
 # -- multi-head self-attention --------------------------------------------------------
+class _EmbedTokens(torch.autograd.Function):
+    """``cat([cls, y], 1) + pos`` of a ViT in one kernel each way (``csrc/fused_ops.hip``
+    embed_tokens_*): the backward writes the patch tokens' gradient contiguously for the
+    patch-embedding GEMM and the batch sums of the position / class-token gradients."""
+
+    @staticmethod
+    def forward(ctx, y, cls, pos):
+        ctx.shapes = (cls.shape, pos.shape)
+        return _fx().embed_tokens_fwd(y.contiguous(), cls.contiguous().view(-1), pos.contiguous().view(-1, y.shape[-1]))
+
+    @staticmethod
+    def backward(ctx, dh):
+        dy, dpos, dcls = _fx().embed_tokens_bwd(dh.to(torch.bfloat16).contiguous())
+        cs, ps = ctx.shapes
+        return dy, dcls.view(cs), dpos.view(ps)
+
+
+def embed_tokens(y: torch.Tensor, cls: torch.Tensor, pos: torch.Tensor) -> torch.Tensor:
+    """``torch.cat([cls.expand(B, -1, -1), y], 1) + pos`` for bf16 ViT tokens on the GPU."""
+    if _native(y) and y.dtype == cls.dtype == pos.dtype == torch.bfloat16 and y.shape[-1] % 8 == 0:
+        return _EmbedTokens.apply(y, cls, pos)
+    return torch.cat([cls.expand(y.shape[0], -1, -1).to(y.dtype), y], dim=1) + pos.to(y.dtype)
+
+
+def patchify_u8(x: torch.Tensor, patch: int) -> torch.Tensor:
+    """uint8 images [B, C, H, W] -> bf16 patch rows [B, (H/P)(W/P), C P P] scaled by 1/255 (one kernel)."""
+    return _fx().patchify_u8(x.contiguous(), int(patch))
+
+
 class _AttentionQKV(torch.autograd.Function):
     @staticmethod
     def forward(ctx, qkv, heads):

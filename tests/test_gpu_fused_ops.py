@@ -212,3 +212,43 @@ def test_split_sum_and_bf16_column_sum():
     b16 = ops.ext().fused.column_sum(g, True)
     assert b16.dtype == torch.bfloat16 and torch.equal(b16, f32.to(torch.bfloat16))
     torch.testing.assert_close(f32, g.float().sum(0), atol=1e-2, rtol=1e-4)
+
+
+def test_patchify_u8_matches_the_eager_prologue():
+    """One kernel: the same bf16 patch rows as float cast, /255, patch permute and the
+    GEMM's bf16 cast (bitwise)."""
+    from p2pfl_amd import ops as O
+
+    O.ext()
+    g = torch.Generator(device="cuda").manual_seed(3)
+    x = torch.randint(0, 256, (3, 3, 32, 48), dtype=torch.uint8, device="cuda", generator=g)
+    P = 16
+    xf = x.float().mul_(1.0 / 255.0)
+    B, C, H, W = x.shape
+    want = xf.view(B, C, H // P, P, W // P, P).permute(0, 2, 4, 1, 3, 5).reshape(B, (H // P) * (W // P), C * P * P)
+    got = O.patchify_u8(x, P)
+    assert got.dtype == torch.bfloat16 and got.shape == want.shape
+    assert torch.equal(got, want.to(torch.bfloat16))
+
+
+@pytest.mark.parametrize("B,N,D", [(4, 196, 768), (3, 5, 64)])
+def test_embed_tokens_fwd_bwd(B, N, D):
+    """cat(cls, y) + pos and its backward (patch-token gradient, batch sums for pos / cls)
+    against the torch composition on the same bf16 operands."""
+    from p2pfl_amd import ops as O
+
+    O.ext()
+    g = torch.Generator(device="cuda").manual_seed(B + N)
+    y = torch.randn(B, N, D, device="cuda", generator=g).to(torch.bfloat16).requires_grad_()
+    cls = (torch.randn(1, 1, D, device="cuda", generator=g) * 0.02).to(torch.bfloat16).requires_grad_()
+    pos = (torch.randn(1, N + 1, D, device="cuda", generator=g) * 0.02).to(torch.bfloat16).requires_grad_()
+    h = O.embed_tokens(y, cls, pos)
+    ref = torch.cat([cls.expand(B, -1, -1), y], dim=1) + pos
+    assert torch.equal(h, ref)
+    dh = torch.randn(B, N + 1, D, device="cuda", generator=g).to(torch.bfloat16)
+    gy, gc, gp = torch.autograd.grad(h, (y, cls, pos), dh)
+    ry, rc, rp = torch.autograd.grad(ref, (y, cls, pos), dh)
+    assert torch.equal(gy, ry)
+    assert gc.shape == rc.shape and gp.shape == rp.shape
+    torch.testing.assert_close(gp.float(), dh.float().sum(0, keepdim=True), atol=2e-2, rtol=1e-2)
+    torch.testing.assert_close(gc.float(), dh[:, :1].float().sum(0, keepdim=True), atol=2e-2, rtol=1e-2)
