@@ -112,6 +112,28 @@ void conv_adam(const float* wslab1, const float* wslab2, const float* gb, int B,
 // reduction + Adam blocks hide behind the HBM-bound FC1 Adam stream.  With
 // dlogits / H non-null the FC2 gradient + Adam blocks join the launch too
 // (then route_fc2 runs with with_fc2 = false).
+// The next step's forward inputs / outputs for fc1_conv_adam_fwd: the uint8 dataset,
+// its row indices, P1 / AM1 / P1s / A1 / AM2 buffers (A1: the other of two
+// step-parity buffers -- this launch's FC1 wgrad still reads the current one), the
+// next batch size, and 4 zero int32 (3 tickets, reset by the launch itself, and a
+// timeout flag).
+struct FwdNext {
+  const uint8_t* x;
+  const int64_t* idx;
+  uint16_t* p1;
+  uint8_t* am1;
+  uint16_t* p1s;
+  uint16_t* a1;
+  uint8_t* am2;
+  int B;
+  int* sync;
+};
+void fc1_conv_adam_fwd(const uint16_t* dH, const uint16_t* a1, int mrows, const float* wslab1, const float* wslab2,
+                       const float* gb, int B, float* params, float* m, float* v, float* gdump, uint16_t* w1bf,
+                       uint16_t* w1tbf, uint16_t* w2r, uint16_t* w2q, Offsets off, const int* adam_t, int t_off,
+                       AdamCfg cfg, const float* dlogits, const uint16_t* H, uint16_t* w2bf, const FwdNext& f,
+                       hipStream_t s);
+
 void fc1_conv_adam(const uint16_t* dH, const uint16_t* a1, int mrows, const float* wslab1, const float* wslab2,
                    const float* gb, int B, float* params, float* m, float* v, float* gdump, uint16_t* w1bf,
                    uint16_t* w1tbf, uint16_t* w2r, uint16_t* w2q, Offsets off, const int* adam_t, int t_off,

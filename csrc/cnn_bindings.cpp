@@ -253,6 +253,56 @@ void k_fc1_conv_adam(torch::Tensor dH, torch::Tensor a1, int64_t mrows, torch::T
       reinterpret_cast<uint16_t*>(optr<at::BFloat16>(w2bf, torch::kBFloat16, 10 * 2048, "w2bf")), stream());
 }
 
+// fc1_conv_adam + the next step's conv1 / conv2 (p2cnn::fc1_conv_adam_fwd): the same
+// arguments, then the next step's x / idx / P1 / AM1 / P1s / A1 (the other parity
+// buffer) / AM2, its batch size and 4 zero int32 (tickets + timeout flag)
+void k_fc1_conv_adam_fwd(torch::Tensor dH, torch::Tensor a1, int64_t mrows, torch::Tensor wslab1, torch::Tensor wslab2,
+                         torch::Tensor gb, int64_t B, torch::Tensor params, torch::Tensor m, torch::Tensor v,
+                         c10::optional<torch::Tensor> gdump, torch::Tensor w1bf, c10::optional<torch::Tensor> w1tbf,
+                         torch::Tensor w2r, torch::Tensor w2q, std::vector<int64_t> off, torch::Tensor adam_t,
+                         int64_t t_off, double lr, double b1, double b2, double eps, double wd,
+                         c10::optional<torch::Tensor> dlogits, c10::optional<torch::Tensor> H,
+                         c10::optional<torch::Tensor> w2bf, torch::Tensor x, c10::optional<torch::Tensor> idx,
+                         torch::Tensor p1, torch::Tensor am1, torch::Tensor p1s, torch::Tensor a1n, torch::Tensor am2,
+                         int64_t Bn, torch::Tensor sync) {
+  const c10::DeviceGuard g(params.device());
+  check_batch(int(B), int(mrows));
+  check_batch(int(Bn), int(mrows));
+  TORCH_CHECK(mrows <= 64, "fc1_conv_adam_fwd: mrows must be 32 or 64");
+  TORCH_CHECK(dlogits.has_value() == H.has_value(), "fc1_conv_adam_fwd: pass both dlogits and H or neither");
+  TORCH_CHECK(x.numel() % 784 == 0, "x must be [N,1,28,28] uint8");
+  if (!idx.has_value()) TORCH_CHECK(x.numel() / 784 >= Bn, "x has fewer than Bn rows");
+  TORCH_CHECK(a1n.data_ptr() != a1.data_ptr(), "fc1_conv_adam_fwd: the next step's A1 must be the other buffer");
+  Offsets o = offsets(off);
+  const int64_t n = params_end(o);
+  p2cnn::FwdNext f{};
+  f.x = ptr<uint8_t>(x, torch::kUInt8, 784, "x", 1);
+  f.idx = idx_ptr(idx, int(Bn));
+  f.p1 = reinterpret_cast<uint16_t*>(ptr<at::BFloat16>(p1, torch::kBFloat16, Bn * 196 * 32, "p1"));
+  f.am1 = ptr<uint8_t>(am1, torch::kUInt8, Bn * 196 * 32, "am1");
+  f.p1s = reinterpret_cast<uint16_t*>(ptr<at::BFloat16>(p1s, torch::kBFloat16, Bn * p2cnn::kP1s, "p1s"));
+  f.a1 = reinterpret_cast<uint16_t*>(ptr<at::BFloat16>(a1n, torch::kBFloat16, mrows * 3136, "a1n"));
+  f.am2 = ptr<uint8_t>(am2, torch::kUInt8, Bn * 3136, "am2");
+  f.B = int(Bn);
+  f.sync = ptr<int>(sync, torch::kInt32, 4, "sync", 4);
+  p2cnn::fc1_conv_adam_fwd(
+      reinterpret_cast<uint16_t*>(ptr<at::BFloat16>(dH, torch::kBFloat16, mrows * 2048, "dH")),
+      reinterpret_cast<uint16_t*>(ptr<at::BFloat16>(a1, torch::kBFloat16, mrows * 3136, "a1")), int(mrows),
+      ptr<float>(wslab1, torch::kFloat32, B * p2cnn::kDgTiles * p2cnn::kSlab1, "wslab1"),
+      ptr<float>(wslab2, torch::kFloat32, p2cnn::wgrad_groups(int(B)) * int64_t(p2cnn::kSlab2), "wslab2"),
+      ptr<float>(gb, torch::kFloat32, B * 3136, "gb"), int(B), ptr<float>(params, torch::kFloat32, n, "params"),
+      ptr<float>(m, torch::kFloat32, n, "m"), ptr<float>(v, torch::kFloat32, n, "v"),
+      optr<float>(gdump, torch::kFloat32, n, "gdump"),
+      reinterpret_cast<uint16_t*>(ptr<at::BFloat16>(w1bf, torch::kBFloat16, 2048 * 3136, "w1bf")),
+      reinterpret_cast<uint16_t*>(optr<at::BFloat16>(w1tbf, torch::kBFloat16, 2048 * 3136, "w1tbf")),
+      reinterpret_cast<uint16_t*>(ptr<at::BFloat16>(w2r, torch::kBFloat16, 51200, "w2r")),
+      reinterpret_cast<uint16_t*>(ptr<at::BFloat16>(w2q, torch::kBFloat16, 51200, "w2q")), o,
+      ptr<int>(adam_t, torch::kInt32, 1, "adam_t", 4), int(t_off), cfg(lr, b1, b2, eps, wd),
+      optr<float>(dlogits, torch::kFloat32, B * 10, "dlogits"),
+      reinterpret_cast<const uint16_t*>(optr<at::BFloat16>(H, torch::kBFloat16, B * 2048, "H")),
+      reinterpret_cast<uint16_t*>(optr<at::BFloat16>(w2bf, torch::kBFloat16, 10 * 2048, "w2bf")), f, stream());
+}
+
 void k_pack_shadows(torch::Tensor params, std::vector<int64_t> off, torch::Tensor w2r, torch::Tensor w2q,
                     torch::Tensor w1bf, c10::optional<torch::Tensor> w1tbf, c10::optional<torch::Tensor> w2bf) {
   const c10::DeviceGuard g(params.device());
@@ -297,6 +347,7 @@ void register_cnn(pybind11::module& m) {
         pybind11::arg("t_off"), pybind11::arg("lr"), pybind11::arg("b1"), pybind11::arg("b2"), pybind11::arg("eps"), pybind11::arg("wd"),
         pybind11::arg("dlogits") = pybind11::none(), pybind11::arg("H") = pybind11::none(),
         pybind11::arg("w2bf") = pybind11::none());
+  c.def("fc1_conv_adam_fwd", &k_fc1_conv_adam_fwd);
   c.def("pack_shadows", &k_pack_shadows, pybind11::arg("params"), pybind11::arg("off"), pybind11::arg("w2r"),
         pybind11::arg("w2q"), pybind11::arg("w1bf"), pybind11::arg("w1tbf"), pybind11::arg("w2bf") = pybind11::none());
   c.def("wgrad_groups", [](int64_t B) { return int64_t(p2cnn::wgrad_groups(int(B))); },

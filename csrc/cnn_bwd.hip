@@ -13,6 +13,7 @@
 #include <cstdlib>
 
 #include "cnn.h"
+#include "cnn_fwd_dev.h"
 #include "common.h"
 
 namespace p2cnn {
@@ -997,6 +998,25 @@ constexpr int kC1Blocks = kSlab1 / 16;  // 52
 
 constexpr int kConvAdamLds = (kTaps * (kC1 + 1) + 256) * 4;
 
+// Stores of the values the next step's forward reads inside the same launch
+// (fc1_conv_adam_fwd_kernel: conv weights / biases and the W2r shadow) go
+// write-through with WT (device-coherent sc1 stores, as cnn_fwd_dev.h reads them).
+template <bool WT>
+P2_DEVICE void st_p(float* p, float v) {
+  if constexpr (WT)
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  else
+    *p = v;
+}
+template <bool WT>
+P2_DEVICE void st_h(uint16_t* p, uint16_t v) {
+  if constexpr (WT)
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  else
+    *p = v;
+}
+
+template <bool WT = false>
 P2_DEVICE void conv_adam_body(int blk, const float* __restrict__ ws1, const float* __restrict__ ws2,
                               const float* __restrict__ gb, int B, float* __restrict__ p, float* __restrict__ m,
                               float* __restrict__ v, float* __restrict__ gdump, uint16_t* __restrict__ w2r,
@@ -1071,17 +1091,17 @@ P2_DEVICE void conv_adam_body(int blk, const float* __restrict__ ws1, const floa
       const int64_t e = off.c2w + int64_t(oc) * kC1 * kTaps + j;
       if (gdump) gdump[e] = g;
       adam_regs(pr[u], mr[u], vr[u], g, cfg, sc);
-      p[e] = pr[u];
+      st_p<WT>(p + e, pr[u]);
       m[e] = mr[u];
       v[e] = vr[u];
       const uint16_t hb = f32_to_bf16(pr[u]);
-      w2r[(oc * kTaps + t) * kC1 + ic] = hb;
+      st_h<WT>(w2r + (oc * kTaps + t) * kC1 + ic, hb);
       w2q[(ic * kTaps + t) * kC2 + oc] = hb;
     }
     if (tid == 0) {
       if (gdump) gdump[off.c2b + oc] = red[0];
       adam_regs(pb, mb, vb, red[0], cfg, sc);
-      p[off.c2b + oc] = pb;
+      st_p<WT>(p + off.c2b + oc, pb);
       m[off.c2b + oc] = mb;
       v[off.c2b + oc] = vb;
     }
@@ -1114,7 +1134,7 @@ P2_DEVICE void conv_adam_body(int blk, const float* __restrict__ ws1, const floa
       for (int k = 0; k < 16; ++k) g += red[k * 16 + tid];
       if (gdump) gdump[e] = g;
       adam_regs(pe, me, ve, g, cfg, sc);
-      p[e] = pe;
+      st_p<WT>(p + e, pe);
       m[e] = me;
       v[e] = ve;
     }
@@ -1180,6 +1200,116 @@ void fc1_conv_adam(const uint16_t* dH, const uint16_t* a1, int mrows, const floa
   else
     hipLaunchKernelGGL(fc1_conv_adam_kernel<64>, grid, dim3(256), 0, s, dH, a1, wslab1, wslab2, gb, B, params, m, v,
                        gdump, w1bf, w1tbf, w2r, w2q, off, adam_t, t_off, cfg, dlogits, H, nf2, w2bf);
+}
+
+// ---------------------------------------------------------------------------
+// fc1_conv_adam + the NEXT step's conv1 and conv2 in one launch.  The FC1 Adam
+// stream is HBM-bound (~28 us); conv1 + conv2 of the next step are latency-bound
+// (~4.6 + 6.0 us as their own launches) and only need the conv parameters this
+// launch's conv-Adam workgroups produce -- so they run beside the stream instead
+// of after it.  Workgroup roles in id order: FC2 Adam, conv-parameter Adam (WT
+// stores, then a ticket on sync[0]), the FC1 wgrad + Adam stream, conv1 of (row
+// pair, image) (waits for every conv-Adam ticket; WT P1 stores, ticket on
+// sync[1]), conv2 (4 (row, oc half, image) items per workgroup; waits for every
+// conv1 ticket; the last one to finish resets sync[0..2]).  The convolution
+// workgroups come last so they take CU slots as the stream's first workgroups
+// retire: placed ahead of the stream, their waits held the slots it needed
+// (72 us for the launch vs 28.8 + 4.6 + 6.0 us for the three kernels).  A waiting role
+// only waits for roles with lower workgroup ids, which the dispatcher starts
+// first and which wait for nothing later, so the launch always drains; the wait
+// is bounded anyway (sync[3] records a timeout).  Same arithmetic as the
+// separate launches: the parameters and activations are bitwise equal.
+// ---------------------------------------------------------------------------
+P2_DEVICE void wait_tickets(int* ctr, int target, int* stall) {
+  if (threadIdx.x == 0) {
+    int it = 0;
+    while (__hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
+      if (++it > (1 << 22)) {
+        __hip_atomic_store(stall, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        break;
+      }
+      __builtin_amdgcn_s_sleep(2);
+    }
+  }
+  __syncthreads();
+}
+// after this workgroup's write-through stores: drain them, then one ticket
+P2_DEVICE void put_ticket(int* ctr) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) __hip_atomic_fetch_add(ctr, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+template <int MR>
+__global__ __launch_bounds__(256) void fc1_conv_adam_fwd_kernel(
+    const uint16_t* __restrict__ dH, const uint16_t* __restrict__ a1, const float* __restrict__ ws1,
+    const float* __restrict__ ws2, const float* __restrict__ gb, int B, float* __restrict__ p, float* __restrict__ m,
+    float* __restrict__ v, float* __restrict__ gdump, uint16_t* __restrict__ w1bf, uint16_t* __restrict__ w1tbf,
+    uint16_t* __restrict__ w2r, uint16_t* __restrict__ w2q, Offsets off, const int* __restrict__ adam_t, int t_off,
+    AdamCfg cfg, const float* __restrict__ dlogits, const uint16_t* __restrict__ H, int nf2,
+    uint16_t* __restrict__ w2bf, FwdNext f) {
+  constexpr int kA = Fc1Lds<MR>::kBytes > kConvAdamLds ? Fc1Lds<MR>::kBytes : kConvAdamLds;
+  constexpr int kB = int(sizeof(Conv1Smem)) > 4 * 32 * 33 * 4 ? int(sizeof(Conv1Smem)) : 4 * 32 * 33 * 4;
+  __shared__ __attribute__((aligned(16))) char smem[kA > kB ? kA : kB];
+  constexpr int kCA = kC2 + kC1Blocks, kBx = (kFeat + 127) / 128;
+  const int n1 = 7 * f.B, n2 = (14 * f.B + 3) / 4;
+  int j = blockIdx.x;
+  if (j < nf2) {
+    fc2_role<256>(j, dlogits, H, B, p, m, v, gdump, off, adam_t, t_off, cfg, w2bf);
+    return;
+  }
+  j -= nf2;
+  if (j < kCA) {
+    conv_adam_body<true>(j, ws1, ws2, gb, B, p, m, v, gdump, w2r, w2q, off, adam_t, t_off, cfg, smem);
+    put_ticket(f.sync);
+    return;
+  }
+  j -= kCA;
+  constexpr int nfc1 = kBx * (kHid / 32);
+  if (j < nfc1) {
+    fc1_wgrad_adam_body<MR>(j % kBx, j / kBx, dH, a1, p, m, v, gdump, w1bf, w1tbf, off, adam_t, t_off, cfg, smem);
+    return;
+  }
+  j -= nfc1;
+  if (j < n1) {
+    wait_tickets(f.sync, kCA, f.sync + 3);
+    conv1_body<true>(j % 7, j / 7, f.x, f.idx, p + off.c1w, p + off.c1b, f.p1, f.am1, f.p1s,
+                     *reinterpret_cast<Conv1Smem*>(smem));
+    put_ticket(f.sync + 1);
+    return;
+  }
+  j -= n1;
+  if (j < n2) {
+    wait_tickets(f.sync + 1, n1, f.sync + 3);
+    const int wave = threadIdx.x >> 6, item = j * 4 + wave;  // item = (image, oc half, pooled row)
+    float(*sout)[33] = reinterpret_cast<float(*)[33]>(smem + wave * (32 * 33 * 4));
+    conv2_body<true>(item < 14 * f.B, item % 7, (item / 7) & 1, item / 14, threadIdx.x & 63, f.p1, w2r, p + off.c2b,
+                     f.a1, f.am2, sout);
+    __syncthreads();
+    if (threadIdx.x == 0 &&
+        __hip_atomic_fetch_add(f.sync + 2, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == n2 - 1) {
+      // every conv1 / conv2 workgroup is past its wait: the counters are free for the next launch
+      __hip_atomic_store(f.sync, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(f.sync + 1, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(f.sync + 2, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+}
+
+void fc1_conv_adam_fwd(const uint16_t* dH, const uint16_t* a1, int mrows, const float* wslab1, const float* wslab2,
+                       const float* gb, int B, float* params, float* m, float* v, float* gdump, uint16_t* w1bf,
+                       uint16_t* w1tbf, uint16_t* w2r, uint16_t* w2q, Offsets off, const int* adam_t, int t_off,
+                       AdamCfg cfg, const float* dlogits, const uint16_t* H, uint16_t* w2bf, const FwdNext& f,
+                       hipStream_t s) {
+  const int nf2 = dlogits ? kFc2Blocks256 : 0;
+  const int n1 = 7 * f.B, n2 = (14 * f.B + 3) / 4;
+  const dim3 grid(nf2 + kC2 + kC1Blocks + n1 + n2 + ((kFeat + 127) / 128) * (kHid / 32));
+  if (mrows == 32)
+    hipLaunchKernelGGL(fc1_conv_adam_fwd_kernel<32>, grid, dim3(256), 0, s, dH, a1, wslab1, wslab2, gb, B, params, m,
+                       v, gdump, w1bf, w1tbf, w2r, w2q, off, adam_t, t_off, cfg, dlogits, H, nf2, w2bf, f);
+  else
+    hipLaunchKernelGGL(fc1_conv_adam_fwd_kernel<64>, grid, dim3(256), 0, s, dH, a1, wslab1, wslab2, gb, B, params, m,
+                       v, gdump, w1bf, w1tbf, w2r, w2q, off, adam_t, t_off, cfg, dlogits, H, nf2, w2bf, f);
 }
 
 void conv_adam(const float* wslab1, const float* wslab2, const float* gb, int B, float* params, float* m, float* v,

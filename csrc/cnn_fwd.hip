@@ -18,6 +18,7 @@
 #include <cstdlib>
 
 #include "cnn.h"
+#include "cnn_fwd_dev.h"
 #include "common.h"
 
 namespace p2cnn {
@@ -45,86 +46,8 @@ __global__ __launch_bounds__(256) void conv1_fwd_kernel(const uint8_t* __restric
                                                         const float* __restrict__ w1, const float* __restrict__ b1,
                                                         uint16_t* __restrict__ p1, uint8_t* __restrict__ am1,
                                                         uint16_t* __restrict__ p1s) {
-  __shared__ float img[8][33];  // padded input rows 4q .. 4q+7 (all this block's windows read)
-  __shared__ uint16_t sv[kC1][2][16];  // pooled values [oc][row][px], cols 14/15 zero
-  __shared__ __attribute__((aligned(16))) uint8_t sa[28][kC1];  // argmax codes [pos][oc]
-  const int b = blockIdx.y, q = blockIdx.x, tid = threadIdx.x;
-  const int64_t row = idx ? idx[b] : b;
-  const uint8_t* src = x + row * (kImg * kImg);
-  {
-    const int i = tid, yy = i >> 5, xx = i & 31, sy = 4 * q + yy - 2, sx = xx - 2;
-    float v = 0.f;
-    if (sy >= 0 && sy < kImg && sx >= 0 && sx < kImg) v = float(src[sy * kImg + sx]) * (1.f / 255.f);
-    img[yy][xx] = v;
-  }
-  const int oc = tid & 31;
-  float w[kTaps];
-#pragma unroll
-  for (int t = 0; t < kTaps; ++t) w[t] = w1[oc * kTaps + t];
-  const float bias = b1[oc];
-  if (tid < kC1 * 2 * 2) sv[tid >> 2][(tid >> 1) & 1][14 + (tid & 1)] = 0;
-  __syncthreads();
-  for (int k = tid >> 5; k < 28; k += 8) {
-    const int rr = k / 14, px = k % 14;
-    float win[6][6];
-#pragma unroll
-    for (int i = 0; i < 6; ++i)
-#pragma unroll
-      for (int j = 0; j < 6; ++j) win[i][j] = img[2 * rr + i][2 * px + j];
-    float best = -3.4e38f;
-    int arg = 0;
-#pragma unroll
-    for (int d = 0; d < 4; ++d) {
-      const int dy = d >> 1, dx = d & 1;
-      float s = bias;
-#pragma unroll
-      for (int ky = 0; ky < 5; ++ky)
-#pragma unroll
-        for (int kx = 0; kx < 5; ++kx) s = fmaf(w[ky * 5 + kx], win[dy + ky][dx + kx], s);
-      if (s > best) {
-        best = s;
-        arg = d;
-      }
-    }
-    sv[oc][rr][px] = f32_to_bf16(fmaxf(best, 0.f));
-    sa[k][oc] = best > 0.f ? uint8_t(arg) : uint8_t(4);
-  }
-  __syncthreads();
-  const size_t pix0 = size_t(b) * 196 + q * 28;
-  // P1 (HWC): 28 pixels x 4 chunks of 8 channels;  AM1: 28 pixels x 2 chunks of 16
-  if (tid < 28 * 4) {
-    const int k = tid >> 2, c0 = (tid & 3) * 8;
-    uint16_t u[8];
-#pragma unroll
-    for (int j = 0; j < 8; ++j) u[j] = sv[c0 + j][k / 14][k % 14];
-    uint4 o;
-    o.x = uint32_t(u[0]) | (uint32_t(u[1]) << 16);
-    o.y = uint32_t(u[2]) | (uint32_t(u[3]) << 16);
-    o.z = uint32_t(u[4]) | (uint32_t(u[5]) << 16);
-    o.w = uint32_t(u[6]) | (uint32_t(u[7]) << 16);
-    reinterpret_cast<uint4*>(p1 + (pix0 + k) * kC1)[tid & 3] = o;
-  } else if (tid < 28 * 4 + 28 * 2) {
-    const int i = tid - 28 * 4, k = i >> 1, c0 = (i & 1) * 16;
-    reinterpret_cast<uint4*>(am1 + (pix0 + k) * kC1)[i & 1] = *reinterpret_cast<const uint4*>(&sa[k][c0]);
-  }
-  if (p1s) {
-    // P1s[b][kx][oc][2q + rr + 2][c] = P1[oc][2q + rr][c + kx - 2]  (0 outside)
-    for (int i = tid; i < 5 * kC1 * 2 * 2; i += 256) {
-      const int half = i & 1, rr = (i >> 1) & 1, o = (i >> 2) % kC1, kx = i / (4 * kC1);
-      uint16_t u[8];
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const int xs = half * 8 + j + kx - 2;
-        u[j] = (xs >= 0 && xs < 14) ? sv[o][rr][xs] : uint16_t(0);
-      }
-      uint4 v;
-      v.x = uint32_t(u[0]) | (uint32_t(u[1]) << 16);
-      v.y = uint32_t(u[2]) | (uint32_t(u[3]) << 16);
-      v.z = uint32_t(u[4]) | (uint32_t(u[5]) << 16);
-      v.w = uint32_t(u[6]) | (uint32_t(u[7]) << 16);
-      *reinterpret_cast<uint4*>(p1s + ((size_t(b) * 5 + kx) * kC1 + o) * kP1sPlane + (2 * q + rr + 2) * 16 + half * 8) = v;
-    }
-  }
+  __shared__ Conv1Smem sm;
+  conv1_body<false>(blockIdx.x, blockIdx.y, x, idx, w1, b1, p1, am1, p1s, sm);
 }
 
 void conv1_fwd(const uint8_t* x, const int64_t* idx, const float* params, Offsets off, uint16_t* p1, uint8_t* am1,
@@ -150,65 +73,7 @@ __global__ __launch_bounds__(64) void conv2_fwd_kernel(const uint16_t* __restric
                                                        const float* __restrict__ b2, uint16_t* __restrict__ a1,
                                                        uint8_t* __restrict__ am2) {
   __shared__ float sout[32][33];
-  const int py = blockIdx.x, nh = blockIdx.y, b = blockIdx.z;
-  const int lane = threadIdx.x, r = lane & 31, h = lane >> 5;
-  const int rr = r < 28 ? r : 27;
-  const int y = 2 * py + (rr >= 14 ? 1 : 0), x = rr >= 14 ? rr - 14 : rr;
-  const uint16_t* img = p1 + size_t(b) * 196 * kC1 + 8 * h;
-  const uint16_t* wrow = w2r + size_t(nh * 32 + r) * kTaps * kC1 + 8 * h;
-  const uint4 z4 = make_uint4(0, 0, 0, 0);
-  auto load = [&](int c, uint4 (&A)[10], uint4 (&Bv)[10]) {
-#pragma unroll
-    for (int j = 0; j < 10; ++j) {
-      const int s = c * 10 + j, t = s >> 1, ky = t / 5, kx = t % 5, ic = (s & 1) * 16;
-      const int iy = y + ky - 2, ix = x + kx - 2;
-      const bool ok = iy >= 0 && iy < 14 && ix >= 0 && ix < 14;
-      const int pix = ok ? iy * 14 + ix : 0;
-      const uint4 v = *reinterpret_cast<const uint4*>(img + pix * kC1 + ic);
-      A[j] = ok ? v : z4;
-      Bv[j] = *reinterpret_cast<const uint4*>(wrow + t * kC1 + ic);
-    }
-  };
-  uint4 A0[10], B0[10], A1[10], B1[10];
-  f32x16 acc = {};
-  load(0, A0, B0);
-#pragma unroll
-  for (int c = 0; c < 5; c += 2) {
-    if (c + 1 < 5) load(c + 1, A1, B1);
-    __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-    for (int j = 0; j < 10; ++j) acc = mfma32(A0[j], B0[j], acc);
-    __builtin_amdgcn_sched_barrier(0);
-    if (c + 1 < 5) {
-      if (c + 2 < 5) load(c + 2, A0, B0);
-      __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-      for (int j = 0; j < 10; ++j) acc = mfma32(A1[j], B1[j], acc);
-      __builtin_amdgcn_sched_barrier(0);
-    }
-  }
-#pragma unroll
-  for (int i = 0; i < 16; ++i) {
-    const int row = acc_row(i, h);
-    if (row < 28) sout[row][r] = acc[i];
-  }
-  __syncthreads();
-  for (int e = lane; e < 7 * 32; e += 64) {
-    const int oc = e / 7, px = e % 7;
-    const float v[4] = {sout[2 * px][oc], sout[2 * px + 1][oc], sout[14 + 2 * px][oc], sout[15 + 2 * px][oc]};
-    float best = v[0];
-    int arg = 0;
-#pragma unroll
-    for (int d = 1; d < 4; ++d)
-      if (v[d] > best) {
-        best = v[d];
-        arg = d;
-      }
-    best += b2[nh * 32 + oc];
-    const size_t o = size_t(b) * kFeat + (nh * 32 + oc) * 49 + py * 7 + px;
-    a1[o] = f32_to_bf16(fmaxf(best, 0.f));
-    am2[o] = best > 0.f ? uint8_t(arg) : uint8_t(4);
-  }
+  conv2_body<false>(true, blockIdx.x, blockIdx.y, blockIdx.z, threadIdx.x, p1, w2r, b2, a1, am2, sout);
 }
 
 // Same conv2, LDS-staged: one 7-wave block per (oc half, image).  The kernel

@@ -64,6 +64,15 @@ _EVAL_SIDE = os.environ.get("P2PFL_EVAL_SIDE_STREAM", "0")
 # kernels and 7.27 vs 6.66 ms per headline round (scripts/kbench.py, MI355X, round 6) --
 # the 3x conv1 VALU work of the recomputed halo rows sits in front of conv2 in every block.
 _CONV12 = os.environ.get("P2PFL_CNN_CONV12", "0") == "1"
+# The next step's conv1 + conv2 inside this step's last launch, beside the FC1 Adam
+# stream (csrc/cnn_bwd.hip fc1_conv_adam_fwd_kernel; A1 double-buffered by step
+# parity).  Opt-in (P2PFL_CNN_FWD_IN_ADAM=1), measured slower on MI355X (round 6,
+# rocprofv3 of bench.py): the launch takes 66-72 us against 28.8 + 4.6 + 6.0 us for
+# the three kernels, 8.6-9.4 vs 6.66 ms per headline round -- the convolutions'
+# device-coherent (sc1) reads of the freshly updated weights and of P1 miss every
+# cache, and their waits hold CU slots; bitwise-equal results
+# (tests/test_gpu_fused_cnn.py::test_next_forward_inside_the_adam_launch_is_bitwise_equal).
+_FWD_IN_ADAM = os.environ.get("P2PFL_CNN_FWD_IN_ADAM", "0") == "1"
 _NAMES = ("conv1.weight", "conv1.bias", "conv2.weight", "conv2.bias", "l1.weight", "l1.bias", "l2.weight", "l2.bias")
 FEAT, HID = 3136, 2048
 
@@ -127,7 +136,12 @@ class FusedCNNEngine:
         self.p1, self.am1 = z(M * 196 * 32, dt=bf), z(M * 196 * 32, dt=torch.uint8)
         # kx-shifted planar P1 copies for conv2_wgrad; padding cells stay zero
         self.p1s = z(M * 5 * 32 * 18 * 16, dt=bf)
-        self.a1, self.am2 = z(M * FEAT, dt=bf), z(M * FEAT, dt=torch.uint8)
+        # A1 by step parity: a launch that runs the next step's conv2 (fc1_conv_adam_fwd)
+        # writes the other buffer while its FC1 weight gradient reads the current one
+        self._a1s = (z(M * FEAT, dt=bf), z(M * FEAT, dt=bf))
+        self._par = 0
+        self.am2 = z(M * FEAT, dt=torch.uint8)
+        self._fwd_sync = z(4, dt=torch.int32)  # fc1_conv_adam_fwd tickets (self-resetting) + timeout flag
         self.slabs1 = z(self.S1 * M * HID)
         self.H, self.dH = z(M * HID, dt=bf), z(M * HID, dt=bf)
         self.dlogits = z(M * 10)
@@ -143,6 +157,11 @@ class FusedCNNEngine:
         self.pack_shadows()
 
     # -- parameters -------------------------------------------------------
+    @property
+    def a1(self) -> torch.Tensor:
+        """The pooled conv2 output of the current step (parity buffer)."""
+        return self._a1s[self._par]
+
     @property
     def params(self) -> torch.Tensor:
         return self.arena.flat
@@ -163,9 +182,14 @@ class FusedCNNEngine:
     def _adam(self):
         return (self.lr, self.betas[0], self.betas[1], self.eps, self.wd)
 
-    def forward(self, x: torch.Tensor, labels: torch.Tensor, idx: Optional[torch.Tensor], B: int, stats: torch.Tensor, train: bool) -> None:
+    def forward(self, x: torch.Tensor, labels: torch.Tensor, idx: Optional[torch.Tensor], B: int, stats: torch.Tensor, train: bool,
+                convs: bool = True) -> None:
+        """The forward pass (``convs`` False: conv1 / conv2 already ran -- inside the
+        previous step's last launch -- only the FC1 GEMM and the head remain)."""
         C, M = self.C, self.mrows
-        if _CONV12:
+        if not convs:
+            pass
+        elif _CONV12:
             C.conv12_fwd(x, idx, self.params, self.off, self.w2r, None, self.am1, self.p1s if train else None, self.a1,
                          self.am2, B, M)
         else:
@@ -176,7 +200,8 @@ class FusedCNNEngine:
                self.w2bf)
 
     def train_step_async(
-        self, x: torch.Tensor, labels: torch.Tensor, idx: Optional[torch.Tensor], B: int, stats: torch.Tensor, t_off: int
+        self, x: torch.Tensor, labels: torch.Tensor, idx: Optional[torch.Tensor], B: int, stats: torch.Tensor, t_off: int,
+        nxt: Optional[Tuple[Optional[torch.Tensor], int]] = None, fwd_done: bool = False,
     ) -> None:
         """Enqueue one training step (no host sync; graph-capturable).
 
@@ -201,7 +226,7 @@ class FusedCNNEngine:
         if B > self.mrows:
             raise ValueError(f"batch {B} > engine capacity {self.mrows}")
         C, M, a = self.C, self.mrows, self._adam()
-        self.forward(x, labels, idx, B, stats, True)
+        self.forward(x, labels, idx, B, stats, True, convs=not fwd_done)
         if _MERGED_ADAM:
             # dA1 routing alone, the conv backward, then ONE launch for the
             # FC2 and conv-parameter Adam (latency-bound) and the FC1 wgrad +
@@ -210,6 +235,16 @@ class FusedCNNEngine:
                         self.params, self.m, self.v, self.gdump, self.off, self.adam_t, t_off, *a, False, self.route_rm,
                         self.route_ws, self.route_ctr)
             C.conv2_bwd(self.dc2m, self.p1s, self.am1, self.w2q, x, idx, self.wslab1, self.wslab2, B)
+            if nxt is not None and M <= 64:
+                # ... with the next step's conv1 + conv2 (nxt = its row indices and batch) in the
+                # same launch; the next step then passes fwd_done
+                idx_n, Bn = nxt
+                C.fc1_conv_adam_fwd(self.dH, self.a1, M, self.wslab1, self.wslab2, self.gb, B, self.params, self.m,
+                                    self.v, self.gdump, self.w1bf, self.w1tbf, self.w2r, self.w2q, self.off, self.adam_t,
+                                    t_off, *a, self.dlogits, self.H, self.w2bf, x, idx_n, self.p1, self.am1, self.p1s,
+                                    self._a1s[1 - self._par], self.am2, Bn, self._fwd_sync)
+                self._par ^= 1
+                return
             C.fc1_conv_adam(self.dH, self.a1, M, self.wslab1, self.wslab2, self.gb, B, self.params, self.m, self.v,
                             self.gdump, self.w1bf, self.w1tbf, self.w2r, self.w2q, self.off, self.adam_t, t_off, *a,
                             self.dlogits, self.H, self.w2bf)
@@ -438,11 +473,18 @@ class FusedCNNLearner(TorchLearner):
         x = loader.x.reshape(-1, 784)
         y = loader.y
         snap = None if train else self._eval_fwd.snapshot(name)
+        chain = train and _FWD_IN_ADAM and _MERGED_ADAM and self.engine.mrows <= 64
+        if train:
+            self.engine._par = 0  # the captured sequence of A1 parities starts here on every replay
         for j, (s, b) in enumerate(plan):
             idx = perm[s : s + b]
             st = stats[j] if train else stats[0]
             if train:
-                self.engine.train_step_async(x, y, idx, b, st, j + 1)
+                nxt = None
+                if chain and j + 1 < len(plan):
+                    s2, b2 = plan[j + 1]
+                    nxt = (perm[s2 : s2 + b2], b2)
+                self.engine.train_step_async(x, y, idx, b, st, j + 1, nxt=nxt, fwd_done=chain and j > 0)
             else:
                 self._eval_fwd.forward(x, y, idx, b, st, snap)
 

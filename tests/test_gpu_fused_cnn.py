@@ -314,3 +314,32 @@ def test_weight_guard_orders_snapshots_around_fit(kind):
     torch.cuda.synchronize()
     assert torch.equal(snap2.flat, ln.live_parameters().flat), "the snapshot read the weights before the fit ended"
     ln.drain()
+
+
+@pytest.mark.parametrize("plan", [[(0, 32), (32, 32), (64, 32), (96, 4)], [(0, 7), (7, 32)]])
+def test_next_forward_inside_the_adam_launch_is_bitwise_equal(plan):
+    """The next step's conv1 + conv2 running inside this step's FC1 / conv Adam launch
+    (fc1_conv_adam_fwd: write-through hand-off of the freshly updated conv weights and
+    of P1 between workgroups) give exactly the parameters, moments and shadows of the
+    separate launches, ragged batches included; the in-launch tickets are back at zero
+    and no wait timed out."""
+    n = plan[-1][0] + plan[-1][1]
+    x, y = _batch(n, seed=21)
+    x = x.reshape(-1, 784)
+    perm = torch.randperm(n, device="cuda")
+    out = []
+    for chain in (False, True):
+        eng, _ = _engine(seed=5)
+        eng._par = 0
+        stats = torch.zeros((len(plan), 4), device="cuda")
+        for j, (s, b) in enumerate(plan):
+            nxt = (perm[plan[j + 1][0] : plan[j + 1][0] + plan[j + 1][1]], plan[j + 1][1]) if chain and j + 1 < len(plan) else None
+            eng.train_step_async(x, y, perm[s : s + b], b, stats[j], j + 1, nxt=nxt, fwd_done=chain and j > 0)
+        torch.cuda.synchronize()
+        out.append((eng.params.clone(), eng.m.clone(), eng.v.clone(), eng.w1bf.clone(), eng.w2r.clone(), eng.w2q.clone(),
+                    stats.clone(), eng._fwd_sync.clone()))
+    for name, a, b in zip(("params", "m", "v", "w1bf", "w2r", "w2q"), out[0], out[1]):
+        assert torch.equal(a, b), name
+    # the loss / accuracy sums are float atomics of the head (order-dependent last bits)
+    torch.testing.assert_close(out[0][6], out[1][6], rtol=1e-5, atol=1e-5)
+    assert int(out[1][-1].abs().sum()) == 0, out[1][-1]
