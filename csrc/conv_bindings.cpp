@@ -44,22 +44,21 @@ hipStream_t stream_of(const torch::Tensor& t) { return c10::hip::getCurrentHIPSt
 int64_t slab_elems(int64_t rows, int64_t cols) { return ((rows + 127) / 128) * ((cols + 127) / 128) * 128 * 128; }
 
 // Split-K configuration: without `counters`, splits > 1 writes fp32 slabs to the output
-// tensor itself (reduce with tile_slab_reduce); with `counters` (int32, one per 128 x 128
-// output tile, all zero) the slabs go to `ws` (fp32, splits * slab_elems) and the launch
-// reduces them itself.
+// tensor itself (reduce with tile_slab_reduce); with `counters` (int32, one per output
+// tile of the launch's tile shape, all zero) the slabs go to `ws` (fp32, splits *
+// slab_elems) and the launch reduces them itself.
 p2::SplitK make_splitk(int64_t splits, const c10::optional<torch::Tensor>& ws, const c10::optional<torch::Tensor>& counters,
                        int64_t rows, int64_t cols, const torch::Tensor& like, const char* who, int64_t variant) {
   TORCH_CHECK(splits >= 1 && splits <= 128, who, ": 1 <= splits <= 128");
-  // 64 x 64 tiles (conv.hip kConvT64) reduce split-K through slabs + tile_slab_reduce only:
-  // the in-launch counters (one per 128 x 128 tile) do not cover their tiles
-  TORCH_CHECK(!(variant & p2::kConvT64) || !(counters.has_value() && counters->defined()), who,
-              ": 64x64-tile launches take no split-K counters");
+  // in-launch counters: one per output tile of the launch's tile shape (64 x 64 with
+  // conv.hip kConvT64, else 128 x 128)
+  const int64_t ts = (variant & p2::kConvT64) ? 64 : 128;
   p2::SplitK k;
   k.splits = int(splits);
   const bool have_cnt = counters.has_value() && counters->defined();
   if (have_cnt) {
     TORCH_CHECK(splits > 1, who, ": counters only with splits > 1");
-    const int64_t tiles = ((rows + 127) / 128) * ((cols + 127) / 128);
+    const int64_t tiles = ((rows + ts - 1) / ts) * ((cols + ts - 1) / ts);
     TORCH_CHECK(counters->is_cuda() && counters->scalar_type() == torch::kInt32 && counters->is_contiguous() &&
                     counters->numel() >= tiles && counters->device() == like.device(),
                 who, ": counters must be a contiguous int32 GPU tensor with >= ", tiles, " entries");

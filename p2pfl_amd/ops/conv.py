@@ -106,10 +106,8 @@ def _run_split(launch, rows: int, cols: int, s: int, out: torch.Tensor, variant:
         launch(out, 1, None, None)
         return
     ws = torch.empty(s * slab_elems(rows, cols), dtype=torch.float32, device=out.device)
-    if variant & T64:  # 64 x 64 tiles: slabs + tile_slab_reduce only (no per-tile counters for them)
-        in_launch = False
     if in_launch if in_launch is not None else s <= _CONV_IN_LAUNCH_MAX_SPLITS:
-        launch(out, s, ws, counters(tiles_of(rows, cols), out.device))
+        launch(out, s, ws, counters(tiles_of(rows, cols, 64 if variant & T64 else 128), out.device))
         return
     launch(ws, s, None, None)
     _C().tile_slab_reduce(ws, s, rows, cols, out.view(rows, cols), variant)
@@ -135,6 +133,8 @@ _TUNE_VARIANTS = (10, 2, 4096 | 2)
 T64 = 1 << 14
 _T64 = os.environ.get("P2PFL_CONV_T64", "1") != "0"
 _TUNE_VARIANTS_T64 = (T64 | 10, T64 | 2, T64 | 4096 | 2)
+# the 64 x 64 tiles' split-K also reduced in the launch (P2PFL_CONV_T64_IL=0: slabs + reduce only)
+_T64_IL = os.environ.get("P2PFL_CONV_T64_IL", "1") != "0"
 
 
 def _split_options(base: int, K: int, min_k: int = 128) -> Tuple[int, ...]:
@@ -155,11 +155,16 @@ def _configs(prefix: str, make, default_variant: int, splits) -> dict:
 
 
 def _configs_t64(prefix: str, make, splits) -> dict:
-    """The 64 x 64-tile candidates of one path (tuned runs only; P2PFL_CONV_T64=0: none)."""
+    """The 64 x 64-tile candidates of one path (tuned runs only; P2PFL_CONV_T64=0: none):
+    each variant x split-K through slabs + tile_slab_reduce, and (suffix ``_il``) the
+    split-K reduced in the launch by the last-arriving slice (no reduce launch)."""
     if not (_TUNE and _T64):
         return {}
     pre = f"{prefix}_" if prefix else ""
-    return {f"{pre}v{v}_s{sp}": make(v, sp) for v in _TUNE_VARIANTS_T64 for sp in splits}
+    out = {f"{pre}v{v}_s{sp}": make(v, sp) for v in _TUNE_VARIANTS_T64 for sp in splits}
+    if _T64_IL:
+        out.update({f"{pre}v{v}_s{sp}_il": make(v, sp, True) for v in _TUNE_VARIANTS_T64 for sp in splits if sp > 1})
+    return out
 
 
 def _pick(key, cands, default: str, out: torch.Tensor) -> None:
@@ -207,16 +212,16 @@ def dgrad_into(dy4: torch.Tensor, w4: torch.Tensor, stride: int, pad: int, dil: 
     rows = shape[0] * shape[1] * shape[2]
     K = kh * kw * O
 
-    def gather(v, sp):
+    def gather(v, sp, il=None):
         return lambda dst: _run_split(
             lambda o, s, ws, cnt: C.conv_dgrad(dy4, w4, stride, pad, dil, o, shape, s, v, ws, cnt),
-            rows, shape[3], sp, dst, v)
+            rows, shape[3], sp, dst, v, il)
 
-    def phases(v, sp):
+    def phases(v, sp, il=None):
         def run(dst):
             ph = torch.empty((rows, shape[3]), dtype=torch.bfloat16, device=dx4.device)
             _run_split(lambda o, s, ws, cnt: C.conv_dgrad_s2(dy4, w4, pad, o, shape, s, v, ws, cnt),
-                       rows, shape[3], sp, ph, v)
+                       rows, shape[3], sp, ph, v, il)
             C.phase_interleave(ph, dst, pad, kh, kw)
         return run
 
@@ -243,9 +248,9 @@ def fwd_into(x4: torch.Tensor, w4: torch.Tensor, stride: int, pad: int, dil: int
     kh, kw, Cin = w4.shape[1], w4.shape[2], w4.shape[3]
     rows, K = N * OH * OW, kh * kw * Cin
 
-    def one(v, sp):
+    def one(v, sp, il=None):
         return lambda dst: _run_split(lambda o, s, ws, cnt: C.conv_fwd(x4, w4, stride, pad, dil, o, s, v, ws, cnt),
-                                      rows, O, sp, dst, v)
+                                      rows, O, sp, dst, v, il)
 
     base = mn_splits(rows, O, K)
     cands = _configs("", one, _V_FWD, _split_options(base, K))
@@ -261,9 +266,10 @@ def wgrad_into(dy4: torch.Tensor, x4: torch.Tensor, stride: int, pad: int, dil: 
     npix = dy4.shape[0] * dy4.shape[1] * dy4.shape[2]
     ncols = kh * kw * Cin
 
-    def one(v, sp):
+    def one(v, sp, il=None):
         return lambda dst: _run_split(
-            lambda o, s, ws, cnt: C.conv_wgrad(dy4, x4, kh, kw, stride, pad, dil, o, s, v, ws, cnt), O, ncols, sp, dst, v)
+            lambda o, s, ws, cnt: C.conv_wgrad(dy4, x4, kh, kw, stride, pad, dil, o, s, v, ws, cnt), O, ncols, sp, dst, v,
+            il)
 
     base = wgrad_splits(O, ncols, npix)
     splits = sorted({max(1, base // 2), base} | ({base * 2} if npix // (base * 2) >= 256 else set()))

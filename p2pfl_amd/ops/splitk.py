@@ -90,8 +90,8 @@ def counters(tiles: int, device: torch.device) -> torch.Tensor:
         return ring[0][off : off + tiles]
 
 
-def tiles_of(rows: int, cols: int) -> int:
-    return -(-rows // 128) * -(-cols // 128)
+def tiles_of(rows: int, cols: int, tile: int = 128) -> int:
+    return -(-rows // tile) * -(-cols // tile)
 
 
 def slab_elems(rows: int, cols: int, variant: int = 0) -> int:

@@ -191,17 +191,40 @@ def test_conv_t64_tiles_exact(N, C, H, W, O, k, s, p, d, variant, splits):
     torch.testing.assert_close(dw, wr.grad.permute(0, 2, 3, 1).reshape(O, -1), atol=0, rtol=0)
 
 
-def test_conv_t64_refuses_counters_and_bn():
-    """The 64 x 64 tiles take split-K only through slabs: the in-launch reduction's
-    per-tile counters (sized for 128 x 128 tiles) are refused rather than overrun."""
+@pytest.mark.parametrize("splits", [2, 5])
+def test_conv_t64_in_launch_split_k_exact(splits):
+    """64 x 64 tiles with the split-K reduced in the launch (last-arriving slice, one
+    counter per 64 x 64 tile): exact on integer operands for all three products, and
+    the counters are back at zero afterwards."""
     from p2pfl_amd.ops.splitk import slab_elems, tiles_of
 
-    x, w = _operands(2, 64, 8, 8, 64, 3, seed=1, integer=True)
-    y4 = torch.empty(2, 8, 8, 64, device="cuda", dtype=torch.bfloat16)
-    ws = torch.empty(2 * slab_elems(128, 64), device="cuda")
-    cnt = torch.zeros(tiles_of(128, 64), dtype=torch.int32, device="cuda")
-    with pytest.raises(RuntimeError, match="64x64"):
-        ops.ext().conv_fwd(x.permute(0, 2, 3, 1), w.permute(0, 2, 3, 1), 1, 1, 1, y4, 2, conv_ops.T64 | 10, ws, cnt)
+    N, C, H, W, O, k = 4, 128, 8, 8, 256, 3
+    x, w = _operands(N, C, H, W, O, k, seed=9 * splits, integer=True)
+    x4, w4 = x.permute(0, 2, 3, 1), w.permute(0, 2, 3, 1)
+    rows, v = N * H * W, conv_ops.T64 | 2
+    C_ = ops.ext()
+    dy = torch.randint(-2, 3, (N, O, H, W), device="cuda").to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    xr, wr = x.float().requires_grad_(), w.float().requires_grad_()
+    yr = _ref(xr, wr, 1, 1, 1)
+    yr.backward(dy.float())
+    for _ in range(2):  # counters reusable launch after launch
+        cnt = torch.zeros(tiles_of(rows, O, 64), dtype=torch.int32, device="cuda")
+        ws = torch.empty(splits * slab_elems(rows, max(O, C)), device="cuda")
+        y4 = torch.empty(N, H, W, O, device="cuda", dtype=torch.bfloat16)
+        C_.conv_fwd(x4, w4, 1, 1, 1, y4, splits, v, ws, cnt)
+        torch.testing.assert_close(y4.permute(0, 3, 1, 2).float(), yr.detach().to(torch.bfloat16).float(), atol=0, rtol=0)
+        assert int(cnt.abs().sum()) == 0
+        cnt = torch.zeros(tiles_of(rows, C, 64), dtype=torch.int32, device="cuda")
+        dx4 = torch.empty(N, H, W, C, device="cuda", dtype=torch.bfloat16)
+        C_.conv_dgrad(dy.permute(0, 2, 3, 1), w4, 1, 1, 1, dx4, [N, H, W, C], splits, v, ws, cnt)
+        torch.testing.assert_close(dx4.permute(0, 3, 1, 2).float(), xr.grad.to(torch.bfloat16).float(), atol=0, rtol=0)
+        assert int(cnt.abs().sum()) == 0
+        cnt = torch.zeros(tiles_of(O, k * k * C, 64), dtype=torch.int32, device="cuda")
+        wsw = torch.empty(splits * slab_elems(O, k * k * C), device="cuda")
+        dw4 = torch.empty(O, k, k, C, device="cuda", dtype=torch.float32)
+        C_.conv_wgrad(dy.permute(0, 2, 3, 1), x4, k, k, 1, 1, 1, dw4, splits, v, wsw, cnt)
+        torch.testing.assert_close(dw4, wr.grad.permute(0, 2, 3, 1), atol=0, rtol=0)
+        assert int(cnt.abs().sum()) == 0
 
 
 S2_CASES = [
