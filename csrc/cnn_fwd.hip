@@ -347,7 +347,9 @@ void conv2_fwd(const uint16_t* p1, const uint16_t* w2r, const float* params, Off
     const char* e = getenv("P2CNN_CONV2_FWD_LDS");
     return e && atoi(e) != 0;
   }();
-  if (lds)
+  // ... but at the evaluation passes' 128-image launches the staged copy is reused by
+  // 7 waves x 2 blocks per image and wins: 9.2 vs 14.1 us (scripts/eval_fwd_probe.py)
+  if (lds || B > 64)
     hipLaunchKernelGGL(conv2_fwd_lds_kernel, dim3(2, B), dim3(448), 0, s, p1, w2r, params + off.c2b, a1, am2);
   else
     hipLaunchKernelGGL(conv2_fwd_kernel, dim3(7, 2, B), dim3(64), 0, s, p1, w2r, params + off.c2b, a1, am2);
