@@ -405,3 +405,22 @@ def test_w2_bf16_copy_tracks_the_fp32_weight():
     torch.cuda.synchronize()
     w2 = e.params[o : o + 20480]
     assert torch.equal(e.w2bf, w2.to(torch.bfloat16))
+
+
+def test_conv2_fwd_eval_sized_launch(eng):
+    """The evaluation passes' 128-image launches take the LDS-staged conv2 (B > 64): same
+    reference check as test_conv2_fwd, on 100 images."""
+    nb, M = 100, 128
+    g = torch.Generator(device="cuda").manual_seed(17)
+    x = torch.randint(0, 256, (nb, 784), dtype=torch.uint8, device="cuda", generator=g)
+    p1 = torch.zeros(M * 196 * 32, dtype=torch.bfloat16, device="cuda")
+    am1 = torch.zeros(M * 196 * 32, dtype=torch.uint8, device="cuda")
+    a1 = torch.zeros(M * 3136, dtype=torch.bfloat16, device="cuda")
+    am2 = torch.zeros(M * 3136, dtype=torch.uint8, device="cuda")
+    eng.C.conv1_fwd(x, None, eng.params, eng.off, p1, am1, None, nb)
+    eng.C.conv2_fwd(p1, eng.w2r, eng.params, eng.off, a1, am2, nb, M)
+    torch.cuda.synchronize()
+    p1f = p1.view(M, 14, 14, 32)[:nb].permute(0, 3, 1, 2).float()
+    w, b = _bf(_p(eng, "conv2.weight")), _p(eng, "conv2.bias")
+    ref = F.max_pool2d(F.relu(F.conv2d(p1f, w, b, padding=2)), 2).reshape(nb, -1)
+    assert _close(a1.view(-1, 3136)[:nb].float(), _bf(ref), rtol=1e-2, atol=1e-4) < 1e-3
