@@ -110,6 +110,9 @@ PP_M16 = 1 << 16  # with PP: the same pipeline on v_mfma_f32_16x16x32_bf16
 PP_SK = 1 << 17  # with PP: stream-K schedule, ``splits`` = grid size (csrc/gemm_pp.hip)
 PP_N128 = 1 << 21  # with PP: the 256 x 128 output tile (150 whole tiles for the N = 768 products)
 PP_ROWSPLIT = 1 << 22  # with PP: rows split into one full wave of 256 x 256 tiles + a 256 x 128 tail launch
+# split-K reduced in the launch (last-arriving slice per tile) at any slice count, not only up to
+# IN_LAUNCH_MAX_SPLITS: a configuration bit of this module, never passed to the kernels
+GEMM_IL = 1 << 23
 SK_SLAB = 256 * 256  # fp32 elements of one stream-K partial tile (two per workgroup)
 
 
@@ -169,6 +172,9 @@ def gemm(
     dev = a.device
     if variant is not None and variant & PP_ROWSPLIT:
         return _gemm_rowsplit(a, b, a_kmajor, b_kmajor, out_dtype, bias, gelu, want_z, residual, out, variant & ~PP_ROWSPLIT)
+    force_il = variant is not None and bool(variant & GEMM_IL)
+    if force_il:
+        variant &= ~GEMM_IL
     if variant is not None and variant & PP_SK:  # stream-K: `splits` workgroups share the K-tile iterations
         if out is None:
             out = torch.empty((M, N), dtype=out_dtype, device=dev)
@@ -182,7 +188,7 @@ def gemm(
         z = torch.empty((M, N), dtype=torch.bfloat16, device=dev) if (gelu and want_z) else None
         v = _variant(a_kmajor, splits) if variant is None else variant
         ws = torch.empty(splits * slab_elems(M, N, v), dtype=torch.float32, device=dev)
-        if splits <= IN_LAUNCH_MAX_SPLITS:  # the last slice of each tile reduces it in the launch
+        if splits <= IN_LAUNCH_MAX_SPLITS or force_il:  # the last slice of each tile reduces it in the launch
             _C().gemm(a, b, a_kmajor, b_kmajor, out, bias, gelu, z, residual, splits, v, ws, counters(tiles_of(M, N), dev))
             return out, z
         if bias is not None or gelu or residual is not None:
@@ -277,7 +283,8 @@ def _dgrad_cfgs(M: int, N: int, K: int):
 
 # ping-pong at 3-4 slices reduces inside the launch (no slab-sum launch); at 6-8 slices
 # through a separate slab_sum pass
-_WGRAD_CFGS = ((PP, 6), (PP, 8), (PP, 4), (PP, 3), (PP | PP_M16, 6), (10, 6), (4096 | 2, 6), (2, 3))
+_WGRAD_CFGS = ((PP, 6), (PP, 8), (PP, 4), (PP, 3), (PP | PP_M16, 6), (10, 6), (4096 | 2, 6), (2, 3),
+                (PP | GEMM_IL, 6), (PP | GEMM_IL, 8), (4096 | 2 | GEMM_IL, 6))
 
 
 def _cfg_name(v: int, sp: int) -> str:
@@ -294,6 +301,12 @@ def _cfg_ok(v: int, sp: int, M: int, N: int, K: int, a_kmajor: bool, b_kmajor: b
     """Configurations the kernels take for this product (no launch may fail)."""
     if not supported(M, N, K, a_kmajor, b_kmajor):
         return False
+    il = bool(v & GEMM_IL)  # forced in-launch reduction: split-K only, takes every epilogue
+    if il:
+        if sp <= 1 or v & (PP_SK | PP_N128 | PP_ROWSPLIT):
+            return False
+        v &= ~GEMM_IL
+        epilogue = False
     if v & PP and v & PP_SK:  # stream-K: any grid up to the iteration count, every epilogue
         return pp_eligible_any(M, N, K, a_kmajor, b_kmajor) and 1 <= sp <= sk_iters(M, N, K)
     if sp > 1 and K // sp < 256:

@@ -450,3 +450,23 @@ def test_rowsplit_vs_fp32(kind, m16):
         out, _ = ops.gemm(a, b, False, True, out_dtype=torch.float32, variant=v)
         ref, _ = ops.gemm_reference(a, b, False, True)
         torch.testing.assert_close(out, ref, atol=5e-3, rtol=1e-4)
+
+
+@pytest.mark.parametrize("v_name", ["pingpong", "ring"])
+@pytest.mark.parametrize("splits", [6, 8])
+def test_forced_in_launch_split_k_beyond_four_slices(v_name, splits):
+    """GEMM_IL: the weight-gradient configurations that reduce 6-8 K-slices in the launch
+    (instead of slabs + a separate reduce) equal the fp32 product exactly on integer
+    operands (m-major operands, the wgrad layout)."""
+    import importlib
+
+    g_mod = importlib.import_module("p2pfl_amd.ops.gemm")
+    v = {"pingpong": g_mod.PP, "ring": 4096 | 2}[v_name] | g_mod.GEMM_IL
+    M, N, K = 768, 3072, 6304  # dW = dY^T X of the ViT-B fc products, K = tokens
+    g = torch.Generator(device="cuda").manual_seed(splits)
+    dy = torch.randint(-2, 3, (K, M), device="cuda", generator=g).to(torch.bfloat16)
+    x = torch.randint(-2, 3, (K, N), device="cuda", generator=g).to(torch.bfloat16)
+    assert g_mod._cfg_ok(v, splits, M, N, K, False, False, False)
+    for _ in range(3):
+        out, _ = g_mod.gemm(dy, x, False, False, out_dtype=torch.float32, splits=splits, variant=v)
+        torch.testing.assert_close(out, dy.float().t() @ x.float(), atol=0, rtol=0)
