@@ -21,6 +21,7 @@ the QKV projection layout).  Optimiser: AdamW (fused over the arena by the learn
 from __future__ import annotations
 
 import math
+import os
 from typing import Optional
 
 import torch
@@ -32,6 +33,15 @@ from p2pfl_amd.models.base import FLModule, seed_everything
 
 def _fused(x: torch.Tensor) -> bool:
     return x.is_cuda and ops.available()
+
+
+# The classifier reads only the class token of the last block's output, and every op
+# after that block's attention (projection, residual adds, LayerNorms, MLP) is per
+# token: the fused encoder runs them on the B class-token rows alone.  The output and
+# every gradient are the same function of the inputs (the other rows' outputs of those
+# ops are never read, and their gradients are exactly zero); the attention itself still
+# runs over all tokens.  P2PFL_VIT_CLS_ONLY=0 computes the dead rows too.
+_CLS_ONLY = os.environ.get("P2PFL_VIT_CLS_ONLY", "1") != "0"
 
 
 class LayerNorm(nn.LayerNorm):
@@ -72,6 +82,14 @@ class Attention(nn.Module):
         qkv = self.qkv(x).view(B, T, 3, self.heads, C // self.heads).permute(2, 0, 3, 1, 4)
         y = nn.functional.scaled_dot_product_attention(qkv[0], qkv[1], qkv[2])
         return self.proj(y.transpose(1, 2).reshape(B, T, C))
+
+    def forward_cls(self, x: torch.Tensor) -> torch.Tensor:
+        """``forward(x)[:, 0]`` ([B, C]): attention over every token, the projection of
+        the class-token rows only (a strided row view, read in place by the GEMM)."""
+        if _fused(x):
+            qkv = ops.linear(x, self.qkv.weight, self.qkv.bias)
+            return ops.linear(ops.attention_qkv(qkv, self.heads)[:, 0], self.proj.weight, self.proj.bias)
+        return self.forward(x)[:, 0]
 
 
 class Block(nn.Module):
@@ -137,7 +155,8 @@ class ViT(FLModule):
         x = ops.embed_tokens(x, self.cls_token, self.pos_embed) if _fused(x) else (
             torch.cat([self.cls_token.expand(x.shape[0], -1, -1).to(x.dtype), x], dim=1) + self.pos_embed.to(x.dtype))
         if _fused(x):
-            return ops.linear(self._encoder_fused(x)[:, 0], self.head.weight, self.head.bias)
+            y = self._encoder_fused(x)
+            return ops.linear(y if y.dim() == 2 else y[:, 0], self.head.weight, self.head.bias)
         x = self.norm(self.blocks(x))
         return self.head(x[:, 0])
 
@@ -147,10 +166,16 @@ class ViT(FLModule):
         ``h`` is the residual stream; ``add_layer_norm`` returns the new stream
         and its normalisation (norm2 of the same block, or norm1 of the next /
         the final norm), so no separate add kernel runs forward or backward.
+        With ``_CLS_ONLY`` the last block continues from its attention on the
+        class-token rows only and the result is [B, C] (else [B, T, C]).
         """
         blocks = list(self.blocks)
         y = blocks[0].norm1(h)
         for i, blk in enumerate(blocks):
+            if _CLS_ONLY and i + 1 == len(blocks):
+                h0, y0 = ops.add_layer_norm(h[:, 0], blk.attn.forward_cls(y), blk.norm2.weight, blk.norm2.bias,
+                                            blk.norm2.eps)
+                return ops.add_layer_norm(h0, blk.mlp(y0), self.norm.weight, self.norm.bias, self.norm.eps)[1]
             h, y = ops.add_layer_norm(h, blk.attn(y), blk.norm2.weight, blk.norm2.bias, blk.norm2.eps)
             nxt = blocks[i + 1].norm1 if i + 1 < len(blocks) else self.norm
             h, y = ops.add_layer_norm(h, blk.mlp(y), nxt.weight, nxt.bias, nxt.eps)

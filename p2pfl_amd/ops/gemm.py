@@ -282,9 +282,10 @@ def _dgrad_cfgs(M: int, N: int, K: int):
 
 
 # ping-pong at 3-4 slices reduces inside the launch (no slab-sum launch); at 6-8 slices
-# through a separate slab_sum pass
+# through a separate slab_sum pass; unsplit tiles for short reductions (the ViT's
+# class-token-only last block: K = batch rows)
 _WGRAD_CFGS = ((PP, 6), (PP, 8), (PP, 4), (PP, 3), (PP | PP_M16, 6), (10, 6), (4096 | 2, 6), (2, 3),
-                (PP | GEMM_IL, 6), (PP | GEMM_IL, 8), (4096 | 2 | GEMM_IL, 6))
+                (PP | GEMM_IL, 6), (PP | GEMM_IL, 8), (4096 | 2 | GEMM_IL, 6), (2, 1), (PP, 1))
 
 
 def _cfg_name(v: int, sp: int) -> str:
@@ -345,7 +346,7 @@ class _LinearP(torch.autograd.Function):
 
     @staticmethod
     @torch.amp.custom_fwd(device_type="cuda")  # operands cast here, the bias keeps its dtype (no cast kernels)
-    def forward(ctx, x, w, b, gelu, plan):
+    def forward(ctx, x, w, b, gelu, plan, keep_z=True):
         fwd = plan[0]
         x2 = _rows(x.to(torch.bfloat16))
         wc = w.to(torch.bfloat16).contiguous()
@@ -354,8 +355,10 @@ class _LinearP(torch.autograd.Function):
         if not gelu:
             y = gemm(x2, wc, bias=b, variant=v, splits=sp)[0]  # the epilogue reads an fp32 or a bf16 bias
         else:
-            y, pre = gemm(x2, wc, bias=b, gelu=True, want_z=True, variant=v, splits=sp)  # pre-activation includes the bias
-            gb = _zero_bias(w.shape[0], x.device)
+            # the pre-activation (bias included) is kept only for a backward: an evaluation
+            # forward skips its store (M x N bf16, as many bytes as the output itself)
+            y, pre = gemm(x2, wc, bias=b, gelu=True, want_z=keep_z, variant=v, splits=sp)
+            gb = _zero_bias(w.shape[0], x.device) if keep_z else None
         STATS["native"] += 1
         ctx.save_for_backward(x2, wc, pre, gb)
         ctx.gelu, ctx.plan = gelu, plan
@@ -388,7 +391,7 @@ class _LinearP(torch.autograd.Function):
             dw = _wgrad(dz, x2, ctx.w_dtype, _cfg(wg))
         if db is not None and ctx.b_dtype is not None:
             db = db.to(ctx.b_dtype)
-        return dx, dw, db if (ctx.b_dtype is not None and ctx.needs_input_grad[2]) else None, None, None
+        return dx, dw, db if (ctx.b_dtype is not None and ctx.needs_input_grad[2]) else None, None, None, None
 
 
 # P2PFL_NATIVE_GEMM: "native" / "auto" (default): every bf16 Linear product on the
@@ -470,7 +473,8 @@ def linear(x: torch.Tensor, weight: torch.Tensor, bias: Optional[torch.Tensor] =
 def linear_gelu(x: torch.Tensor, weight: torch.Tensor, bias: torch.Tensor) -> torch.Tensor:
     """``gelu(F.linear(x, weight, bias))`` (exact erf GELU), fused epilogue."""
     if _POLICY != _LIB and _ok(x, weight):
-        return _LinearP.apply(x, weight, bias, True, _plan(x, weight, bias, True))
+        grad = torch.is_grad_enabled() and (x.requires_grad or weight.requires_grad or bias.requires_grad)
+        return _LinearP.apply(x, weight, bias, True, _plan(x, weight, bias, True), grad)
     if x.is_cuda and (_POLICY == _LIB or _bf16_call(x)) and _library(x):
         from p2pfl_amd.ops.fused import bias_gelu, linear as linear_blas
 

@@ -105,6 +105,45 @@ def test_vit_uses_fused_kernels_and_trains():
     torch.testing.assert_close(a, b, atol=1e-3, rtol=1e-3)
 
 
+def test_vit_class_token_only_last_block_matches_full(monkeypatch):
+    """The fused encoder's last block after its attention on the class-token rows only:
+    the same logits and parameter gradients as running it over every token."""
+    from p2pfl_amd.models import vit
+
+    x = torch.randint(0, 255, (8, 3, 32, 32), dtype=torch.uint8, device="cuda")
+    y = torch.randint(0, 10, (8,), device="cuda")
+    outs = []
+    for cls_only in (False, True):
+        monkeypatch.setattr(vit, "_CLS_ONLY", cls_only)
+        m = vit.ViT_Tiny(seed=0).cuda()
+        with torch.autocast("cuda", dtype=torch.bfloat16):
+            z = m(x)
+            loss = m.loss_fn(z, y)
+        loss.backward()
+        outs.append((z.float(), {n: p.grad.float() for n, p in m.named_parameters()}))
+    (za, ga), (zb, gb) = outs
+    torch.testing.assert_close(zb, za, atol=2e-2, rtol=2e-2)
+    for n in ga:
+        torch.testing.assert_close(gb[n], ga[n], atol=2e-3, rtol=5e-2, msg=lambda m: f"{n}: {m}")
+
+
+def test_linear_gelu_eval_forward_without_pre_activation():
+    """Under no_grad the GELU epilogue skips the pre-activation store; the output is the
+    training forward's, bit for bit (same tuned kernel configuration)."""
+    torch.manual_seed(3)
+    x = torch.randn(512, 256, device="cuda").to(torch.bfloat16)
+    w = (torch.randn(1024, 256, device="cuda") * 0.05).requires_grad_(True)
+    b = torch.randn(1024, device="cuda").requires_grad_(True)
+    with torch.autocast("cuda", dtype=torch.bfloat16):
+        yt = ops.linear_gelu(x, w, b)
+        with torch.no_grad():
+            ye = ops.linear_gelu(x, w, b)
+    assert yt.requires_grad and not ye.requires_grad
+    assert torch.equal(yt.detach(), ye)
+    ref = torch.nn.functional.gelu(x.float() @ w.detach().to(torch.bfloat16).float().t() + b.detach())
+    torch.testing.assert_close(ye.float(), ref, atol=3e-2, rtol=2e-2)
+
+
 @pytest.mark.parametrize("B,T,H", [(2, 197, 12), (3, 65, 3), (1, 1, 2), (2, 32, 1), (1, 256, 2), (2, 100, 4)])
 def test_attention_fwd_bwd(B, T, H):
     """Fused MHSA kernel vs fp32 SDPA on the same bf16 inputs (forward, dq/dk/dv)."""
