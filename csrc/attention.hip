@@ -226,22 +226,30 @@ __global__ __launch_bounds__(64 * kWaves) void attn_fwd_kernel(const uint16_t* _
       }
     }
     tmax = fmaxf(tmax, __shfl_xor(tmax, 32, 64));
-    const float mn = fmaxf(m, tmax * sl2);  // finite: key tile 0 always holds key 0
-    const float alpha = ex2(m - mn);
+    // Lazy rescale: the running max m only moves (and O, l are rescaled) when some
+    // query's tile max exceeds it by more than 2^8 in the exponent -- in practice on
+    // the first tile only.  Otherwise P = 2^(s - m) <= 256 against a stale m, which
+    // leaves O / l and lse2 = m + log2 l exact (both are invariant to the reference
+    // m) and saves the 32 rescale multiplies + one exp2 per lane and tile.
+    if (__any(tmax * sl2 > m + 8.f)) {  // wave-uniform; always true on tile 0 (m = -inf)
+      const float mn = fmaxf(m, tmax * sl2);  // finite: key tile 0 always holds key 0
+      const float alpha = ex2(m - mn);
+      l *= alpha;
+      m = mn;
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        o0[i] *= alpha;
+        o1[i] *= alpha;
+      }
+    }
     float ps = 0.f;
 #pragma unroll
     for (int i = 0; i < 16; ++i) {
-      const float p = ex2(fmaf(st[i], sl2, -mn));
+      const float p = ex2(fmaf(st[i], sl2, -m));
       st[i] = p;
       ps += p;
     }
-    l = fmaf(l, alpha, ps);
-    m = mn;
-#pragma unroll
-    for (int i = 0; i < 16; ++i) {
-      o0[i] *= alpha;
-      o1[i] *= alpha;
-    }
+    l += ps;
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
       const uint4 pb = pack_frag(st, s);

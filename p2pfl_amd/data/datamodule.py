@@ -92,6 +92,12 @@ class DeviceLoader:
             yield xb, self.y.index_select(0, idx)
 
 
+def wants_float(loader, model) -> bool:
+    """Whether a batch of ``loader`` is normalised to [0, 1] float before ``model``:
+    not for models that read the uint8 batch themselves (``takes_uint8``)."""
+    return bool(loader.normalize) and not getattr(model, "takes_uint8", False)
+
+
 class FederatedDataModule:
     def __init__(
         self,

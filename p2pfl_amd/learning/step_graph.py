@@ -26,6 +26,8 @@ from typing import Any, Optional, Tuple
 
 import torch
 
+from p2pfl_amd.data.datamodule import wants_float
+
 from p2pfl_amd.ops import splitk
 from p2pfl_amd.utils.lockcheck import make_lock
 from p2pfl_amd.utils.streams import private_stream
@@ -164,7 +166,7 @@ class TrainStepGraph:
     def _body(self, graph: bool) -> torch.Tensor:
         ld, model, opt = self.loader, self.learner.model, self.opt
         x = ld.x.index_select(0, self.idx)
-        if ld.normalize:
+        if wants_float(ld, model):
             x = x.float().div_(255.0)
         y = ld.y.index_select(0, self.idx)
         for p in opt.mt.params:
@@ -271,7 +273,7 @@ class EvalStepGraph:
     def batch(self, idx: torch.Tensor):
         ld = self.loader
         x = ld.x.index_select(0, idx)
-        if ld.normalize:
+        if wants_float(ld, self.learner.model):
             x = x.float().div_(255.0)
         return x, ld.y.index_select(0, idx)
 

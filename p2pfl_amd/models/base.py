@@ -39,6 +39,10 @@ class FLModule(nn.Module):
     def configure_optimizers(self) -> torch.optim.Optimizer:
         return torch.optim.Adam(self.parameters(), lr=self.lr_rate)
 
+    # True: forward() takes the raw uint8 batch and folds the /255 into its first
+    # kernel (the learners then skip the float normalisation pass of the loader)
+    takes_uint8 = False
+
     def training_step(self, batch: Tuple[torch.Tensor, torch.Tensor], batch_idx: int) -> torch.Tensor:
         x, y = batch
         loss = self.loss_fn(self(x), y)

@@ -130,6 +130,8 @@ class Bottleneck(nn.Module):
 
 
 class ResNet(FLModule):
+    takes_uint8 = True  # forward folds the /255 of a uint8 batch into its first kernel
+
     def __init__(
         self,
         block: Type[Union[BasicBlock, Bottleneck]],

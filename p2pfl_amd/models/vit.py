@@ -106,6 +106,8 @@ class Block(nn.Module):
 
 
 class ViT(FLModule):
+    takes_uint8 = True  # forward folds the /255 of a uint8 batch into its first kernel
+
     def __init__(
         self,
         img_size: int = 224,
