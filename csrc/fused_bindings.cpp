@@ -136,6 +136,85 @@ std::vector<torch::Tensor> ln_bwd(torch::Tensor dy, torch::Tensor x, torch::Tens
   return {dx, dw, db};
 }
 
+// The backward passes above without their column reduction: the partials are returned
+// and reduced later, many at a time, by col_reduce_multi (a training step's deferred
+// parameter-gradient reductions, ops/fused.py deferred_param_grads).
+std::vector<torch::Tensor> ln_bwd_parts(torch::Tensor dy, torch::Tensor x, torch::Tensor w, torch::Tensor mean,
+                                        torch::Tensor rstd, c10::optional<torch::Tensor> gsum) {
+  const c10::DeviceGuard g(x.device());
+  const int64_t N = x.size(0), C = x.size(1);
+  TORCH_CHECK(N > 0, "ln_bwd_parts: empty input");
+  TORCH_CHECK(dy.sizes() == x.sizes() && dy.scalar_type() == x.scalar_type(), "dy must match x");
+  const bool bf = act_dtype(x, "x");
+  act_dtype(dy, "dy");
+  check_f32(w, C, "weight");
+  check_f32(mean, N, "mean");
+  check_f32(rstd, N, "rstd");
+  const bool has_gs = gsum.has_value() && gsum->defined();
+  if (has_gs)
+    TORCH_CHECK(gsum->sizes() == x.sizes() && gsum->scalar_type() == x.scalar_type(), "gsum must match x");
+  auto dx = torch::empty_like(x);
+  auto opt = x.options().dtype(torch::kFloat32);
+  const int G = p2fused::layer_norm_bwd_blocks(int(N));
+  auto pdw = torch::empty({G, C}, opt), pdb = torch::empty({G, C}, opt);
+  p2fused::layer_norm_bwd(bf, dy.data_ptr(), x.data_ptr(), w.data_ptr<float>(), mean.data_ptr<float>(),
+                          rstd.data_ptr<float>(), has_gs ? gsum->data_ptr() : nullptr, dx.data_ptr(),
+                          pdw.data_ptr<float>(), pdb.data_ptr<float>(), nullptr, nullptr, int(N), int(C), stream());
+  return {dx, pdw, pdb};
+}
+
+std::vector<torch::Tensor> bias_gelu_bwd_parts(torch::Tensor dy, torch::Tensor x, torch::Tensor b) {
+  const c10::DeviceGuard g(x.device());
+  const int64_t H = x.size(-1), N = x.numel() / H;
+  TORCH_CHECK(N > 0, "bias_gelu_bwd_parts: empty input");
+  TORCH_CHECK(dy.sizes() == x.sizes() && dy.scalar_type() == x.scalar_type(), "dy must match x");
+  const bool bf = act_dtype(x, "x");
+  act_dtype(dy, "dy");
+  check_f32(b, H, "bias");
+  auto dx = torch::empty_like(x);
+  auto pdb = torch::empty({p2fused::bias_gelu_bwd_splits(int(N)), H}, x.options().dtype(torch::kFloat32));
+  p2fused::bias_gelu_bwd(bf, dy.data_ptr(), x.data_ptr(), b.data_ptr<float>(), dx.data_ptr(), pdb.data_ptr<float>(),
+                         nullptr, int(N), int(H), stream());
+  return {dx, pdb};
+}
+
+torch::Tensor column_sum_parts(torch::Tensor x) {
+  const c10::DeviceGuard g(x.device());
+  TORCH_CHECK(x.dim() == 2 && x.size(0) > 0, "x must be a non-empty [N, H]");
+  const int64_t N = x.size(0), H = x.size(1);
+  TORCH_CHECK(H % 8 == 0, "H must be a multiple of 8");
+  const bool bf = act_dtype(x, "x");
+  auto part = torch::empty({p2fused::bias_gelu_bwd_splits(int(N)), H}, x.options().dtype(torch::kFloat32));
+  p2fused::column_sum(bf, x.data_ptr(), part.data_ptr<float>(), nullptr, nullptr, int(N), int(H), stream());
+  return part;
+}
+
+// outs[i] (fp32 or bf16 [C]) = column sums of parts[i] (fp32 [R, C]), up to kCrMaxJobs per launch
+void col_reduce_multi(std::vector<torch::Tensor> parts, std::vector<torch::Tensor> outs) {
+  TORCH_CHECK(parts.size() == outs.size(), "col_reduce_multi: parts / outs length mismatch");
+  if (parts.empty()) return;
+  const c10::DeviceGuard g(parts[0].device());
+  p2fused::CrJobs jobs{};
+  for (size_t i = 0; i < parts.size(); ++i) {
+    const auto& a = parts[i];
+    const auto& o = outs[i];
+    TORCH_CHECK(a.is_cuda() && a.scalar_type() == torch::kFloat32 && a.dim() == 2 && a.is_contiguous() && a.size(0) > 0,
+                "col_reduce_multi: parts must be non-empty contiguous fp32 [R, C] GPU tensors");
+    TORCH_CHECK(a.device() == parts[0].device() && o.device() == a.device(), "col_reduce_multi: one device");
+    TORCH_CHECK(o.is_contiguous() && o.numel() == a.size(1) &&
+                    (o.scalar_type() == torch::kFloat32 || o.scalar_type() == torch::kBFloat16),
+                "col_reduce_multi: outs must be contiguous fp32 / bf16 [C] matching their partials");
+    const bool bf = o.scalar_type() == torch::kBFloat16;
+    jobs.j[jobs.n++] = p2fused::CrJob{a.data_ptr<float>(), bf ? nullptr : o.data_ptr<float>(), nullptr, nullptr,
+                                      bf ? reinterpret_cast<uint16_t*>(o.data_ptr<at::BFloat16>()) : nullptr,
+                                      int(a.size(0)), int(a.size(1)), 0, 0};
+    if (jobs.n == p2fused::kCrMaxJobs || i + 1 == parts.size()) {
+      p2fused::col_reduce_multi(jobs, stream());
+      jobs.n = 0;
+    }
+  }
+}
+
 torch::Tensor split_sum_bf16(torch::Tensor parts) {
   const c10::DeviceGuard g(parts.device());
   TORCH_CHECK(parts.is_cuda() && parts.scalar_type() == torch::kBFloat16 && parts.is_contiguous() && parts.dim() >= 2,
@@ -314,6 +393,10 @@ void register_fused(pybind11::module& m) {
         pybind11::arg("rstd"), pybind11::arg("gsum") = pybind11::none());
   f.def("column_sum", &column_sum, "column sums of a [N, H] bf16/fp32 activation (linear bias gradient), fp32 or bf16 out",
         pybind11::arg("x"), pybind11::arg("bf16_out") = false);
+  f.def("ln_bwd_parts", &ln_bwd_parts, "LayerNorm backward: dx and the [G, C] dgamma / dbeta partials");
+  f.def("bias_gelu_bwd_parts", &bias_gelu_bwd_parts, "bias+GELU backward: dx and the [S, H] dbias partials");
+  f.def("column_sum_parts", &column_sum_parts, "[S, H] partial column sums of a [N, H] activation");
+  f.def("col_reduce_multi", &col_reduce_multi, "outs[i] = column sums of parts[i], many per launch");
   f.def("multi_copy", &multi_copy, "dsts[i] <- srcs[i] for up to 12 pairs in one launch");
   f.def("split_sum_bf16", &split_sum_bf16, "bf16 sum over dim 0 of [S, ...] bf16 partials, fp32 accumulation");
   f.def("bias_gelu_fwd", &bias_gelu_fwd);

@@ -28,6 +28,27 @@ void bias_gelu_bwd(bool bf16, const void* dy, const void* x, const float* b, voi
 // (out_bf != nullptr: the result is written as bf16 to out_bf instead of out)
 void column_sum(bool bf16, const void* x, float* part, float* out, uint16_t* out_bf, int N, int H, hipStream_t s);
 
+// dw / db (layer_norm_bwd), db (bias_gelu_bwd), out and out_bf (column_sum) all nullptr: only
+// the partials are written; their column reduction is left to col_reduce_multi.
+
+// Column reductions out[c] = sum_r part[r][c] (fixed order, as the single launches) of many
+// [R, C] fp32 partial arrays in one launch; a job reduces a (and b if set); oa_bf set: a's
+// result as bf16 into oa_bf instead of oa.  blk0 is filled by col_reduce_multi.
+struct CrJob {
+  const float* a;
+  float* oa;
+  const float* b;
+  float* ob;
+  uint16_t* oa_bf;
+  int R, C, blk0, pad;
+};
+constexpr int kCrMaxJobs = 40;  // 2.2 KB of kernel arguments
+struct CrJobs {
+  CrJob j[kCrMaxJobs];
+  int n;
+};
+void col_reduce_multi(CrJobs& jobs, hipStream_t s);
+
 // out[i] = bf16(sum_s parts[s][i]) over S bf16 partial arrays of n elements (n % 8 == 0)
 void split_sum_bf16(const uint16_t* parts, uint16_t* out, int64_t n, int S, hipStream_t s);
 

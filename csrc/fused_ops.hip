@@ -269,12 +269,11 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const T* __restrict__ dy, c
 // latency (the previous 64 x 4 split needed up to 13: 6.7 us per call at
 // the ViT sizes); the 16 phase partials are combined in LDS in fixed order.
 constexpr int kCrCols = 16, kCrPh = 256 / kCrCols;
-__global__ __launch_bounds__(256) void col_reduce_kernel(const float* __restrict__ a, float* __restrict__ oa,
-                                                         const float* __restrict__ b, float* __restrict__ ob, int R,
-                                                         int C, uint16_t* __restrict__ oa_bf = nullptr) {
+P2_DEVICE void col_reduce_body(const float* __restrict__ a, float* __restrict__ oa, const float* __restrict__ b,
+                               float* __restrict__ ob, int R, int C, uint16_t* __restrict__ oa_bf, int cblock) {
   __shared__ float red[2][kCrPh][kCrCols];
   const int cl = threadIdx.x % kCrCols, q = threadIdx.x / kCrCols;
-  const int c = blockIdx.x * kCrCols + cl;
+  const int c = cblock * kCrCols + cl;
   float sa = 0.f, sb = 0.f;
   if (c < C) {
     for (int r0 = q; r0 < R; r0 += kCrPh * 8) {
@@ -308,6 +307,33 @@ __global__ __launch_bounds__(256) void col_reduce_kernel(const float* __restrict
       oa[c] = xa;
     if (b) ob[c] = xb;
   }
+}
+
+__global__ __launch_bounds__(256) void col_reduce_kernel(const float* __restrict__ a, float* __restrict__ oa,
+                                                         const float* __restrict__ b, float* __restrict__ ob, int R,
+                                                         int C, uint16_t* __restrict__ oa_bf = nullptr) {
+  col_reduce_body(a, oa, b, ob, R, C, oa_bf, blockIdx.x);
+}
+
+// Many column reductions in one launch (the parameter gradients whose reduction a
+// training step defers to the end of its backward: LayerNorm dgamma / dbeta, bias
+// gradients): the job table rides in the kernel arguments, a block takes the job
+// whose block range holds blockIdx.x and runs exactly the col_reduce_kernel body,
+// so every result is bitwise the separate launch's.
+__global__ __launch_bounds__(256) void col_reduce_multi_kernel(CrJobs jobs) {
+  int j = 0;
+  while (j + 1 < jobs.n && int(blockIdx.x) >= jobs.j[j + 1].blk0) ++j;  // block-uniform
+  const CrJob& t = jobs.j[j];
+  col_reduce_body(t.a, t.oa, t.b, t.ob, t.R, t.C, t.oa_bf, int(blockIdx.x) - t.blk0);
+}
+
+void col_reduce_multi(CrJobs& jobs, hipStream_t s) {
+  int blocks = 0;
+  for (int i = 0; i < jobs.n; ++i) {
+    jobs.j[i].blk0 = blocks;
+    blocks += (jobs.j[i].C + kCrCols - 1) / kCrCols;
+  }
+  if (blocks > 0) hipLaunchKernelGGL(col_reduce_multi_kernel, dim3(blocks), dim3(256), 0, s, jobs);
 }
 
 // ---------------------------------------------------------------------------
@@ -671,7 +697,7 @@ static void ln_bwd_t(const void* dy, const void* x, const float* w, const float*
   else
     P2_LN_BWD(4);
 #undef P2_LN_BWD
-  hipLaunchKernelGGL(col_reduce_kernel, dim3((C + kCrCols - 1) / kCrCols), blk, 0, s, pdw, dw, pdb, db, G, C);
+  if (dw) hipLaunchKernelGGL(col_reduce_kernel, dim3((C + kCrCols - 1) / kCrCols), blk, 0, s, pdw, dw, pdb, db, G, C);
 }
 
 void layer_norm_bwd(bool bf16, const void* dy, const void* x, const float* w, const float* mean, const float* rstd,
@@ -709,7 +735,8 @@ void bias_gelu_bwd(bool bf16, const void* dy, const void* x, const float* b, voi
   else
     hipLaunchKernelGGL(bias_gelu_bwd_kernel<float>, grid, blk, 0, s, static_cast<const float*>(dy),
                        static_cast<const float*>(x), b, static_cast<float*>(dx), pdb, N, H);
-  hipLaunchKernelGGL(col_reduce_kernel, dim3((H + kCrCols - 1) / kCrCols), blk, 0, s, pdb, db, nullptr, nullptr, S, H);
+  if (db)
+    hipLaunchKernelGGL(col_reduce_kernel, dim3((H + kCrCols - 1) / kCrCols), blk, 0, s, pdb, db, nullptr, nullptr, S, H);
 }
 
 void column_sum(bool bf16, const void* dy, float* part, float* out, uint16_t* out_bf, int N, int H, hipStream_t s) {
@@ -719,8 +746,9 @@ void column_sum(bool bf16, const void* dy, float* part, float* out, uint16_t* ou
     hipLaunchKernelGGL(colsum_kernel<uint16_t>, grid, blk, 0, s, static_cast<const uint16_t*>(dy), part, N, H);
   else
     hipLaunchKernelGGL(colsum_kernel<float>, grid, blk, 0, s, static_cast<const float*>(dy), part, N, H);
-  hipLaunchKernelGGL(col_reduce_kernel, dim3((H + kCrCols - 1) / kCrCols), blk, 0, s, part, out, nullptr, nullptr, S, H,
-                     out_bf);
+  if (out || out_bf)
+    hipLaunchKernelGGL(col_reduce_kernel, dim3((H + kCrCols - 1) / kCrCols), blk, 0, s, part, out, nullptr, nullptr, S,
+                       H, out_bf);
 }
 
 // ---------------------------------------------------------------------------

@@ -27,6 +27,7 @@ from typing import Any, Optional, Tuple
 import torch
 
 from p2pfl_amd.data.datamodule import wants_float
+from p2pfl_amd.ops.fused import deferred_param_grads
 
 from p2pfl_amd.ops import splitk
 from p2pfl_amd.utils.lockcheck import make_lock
@@ -171,9 +172,10 @@ class TrainStepGraph:
         y = ld.y.index_select(0, self.idx)
         for p in opt.mt.params:
             p.grad = None
-        with torch.autocast(device_type="cuda", dtype=torch.bfloat16, cache_enabled=False):
-            loss = model.training_step((x, y), 0)
-        loss.backward()
+        with deferred_param_grads():  # column-sum parameter gradients reduced in one launch at the end
+            with torch.autocast(device_type="cuda", dtype=torch.bfloat16, cache_enabled=False):
+                loss = model.training_step((x, y), 0)
+            loss.backward()
         if graph:
             opt.step_graph(self.gtab)
         else:

@@ -8,6 +8,10 @@ definitions the numerics tests compare against.
 
 from __future__ import annotations
 
+import os
+import threading
+from contextlib import contextmanager
+
 import torch
 import torch.nn.functional as F
 
@@ -46,7 +50,83 @@ def attention_qkv_reference(qkv, heads):
     return y.transpose(1, 2).reshape(B, T, C)
 
 
+# -- deferred parameter-gradient reductions ------------------------------------------
+# A parameter gradient that is a column sum over the batch rows (LayerNorm dgamma /
+# dbeta, a linear bias gradient, the bias gradient of the fused GELU backward) is a
+# [S, C] partial-sum pass followed by a small fixed-order reduction launch (~5 us,
+# latency-bound): 73 of them per ViT-B/16 step.  Inside ``deferred_param_grads()``
+# (the training step graphs' backward) the backward passes return their partials
+# instead; on exit ONE ``col_reduce_multi`` launch reduces them all -- bitwise the
+# same sums -- and assigns the parameters' ``.grad`` (the autograd output for those
+# parameters is None).  The context must enclose the FORWARD too: a Function records
+# the open collection in its ctx when it runs forward (on the caller's thread), since
+# autograd runs CUDA backward nodes on its own device thread -- so another peer's
+# concurrent backward can never land in this step's collection.
+# P2PFL_DEFER_GRAD_REDUCE=0 keeps the per-pass reductions.
+_DEFER_ON = os.environ.get("P2PFL_DEFER_GRAD_REDUCE", "1") != "0"
+_TLS = threading.local()
+
+
+class _Deferred:
+    def __init__(self) -> None:
+        self.open = True
+        self.params: list = []
+        self.parts: list = []
+
+
+def defer_scope():
+    """The collection a Function's forward should record in its ctx (None outside one)."""
+    return getattr(_TLS, "d", None)
+
+
+def defer_grad(d, param, part: torch.Tensor) -> bool:
+    """Register ``param``'s gradient as the column sums of ``part`` ([S, C] fp32) in the
+    collection ``d`` recorded at forward time; False (reduce now) if there is none."""
+    if d is None or not d.open or not isinstance(param, torch.nn.Parameter):
+        return False
+    d.params.append(param)
+    d.parts.append(part)
+    return True
+
+
+@contextmanager
+def deferred_param_grads(enabled: bool = True):
+    """Wrap the forward AND backward of a training step: the deferrable parameter-gradient
+    reductions of its backward run as one launch on exit, which also sets ``.grad``."""
+    if not (enabled and _DEFER_ON) or getattr(_TLS, "d", None) is not None:
+        yield
+        return
+    d = _TLS.d = _Deferred()
+    try:
+        yield
+    finally:
+        _TLS.d = None
+        d.open = False
+    if not d.parts:
+        return
+    outs = [torch.empty(p.shape, dtype=p.dtype, device=part.device) for p, part in zip(d.params, d.parts)]
+    _fx().col_reduce_multi(d.parts, [o.view(-1) for o in outs])
+    for p, g in zip(d.params, outs):
+        if p.grad is None:
+            p.grad = g
+        else:
+            p.grad.add_(g)
+
+
 # -- LayerNorm ----------------------------------------------------------------
+def _ln_bwd(ctx, dy2, x2, w, mean, rstd, gs2=None):
+    """dx, dgamma, dbeta -- the parameter gradients deferred where possible (None)."""
+    wp, bp = ctx.params
+    d = ctx.defer
+    if d is not None and d.open and (ctx.needs_input_grad[ctx.wi] or ctx.needs_input_grad[ctx.wi + 1]):
+        dx, pdw, pdb = _fx().ln_bwd_parts(dy2, x2, w.contiguous(), mean, rstd, gs2)
+        dw = None if ctx.needs_input_grad[ctx.wi] and defer_grad(d, wp, pdw) else pdw.sum(0).to(w.dtype)
+        db = None if ctx.needs_input_grad[ctx.wi + 1] and defer_grad(d, bp, pdb) else pdb.sum(0).to(w.dtype)
+        return dx, dw, db
+    dx, dw, db = _fx().ln_bwd(dy2, x2, w.contiguous(), mean, rstd, gs2)
+    return dx, dw.to(w.dtype), db.to(w.dtype)
+
+
 class _LayerNorm(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, w, b, eps):
@@ -55,14 +135,15 @@ class _LayerNorm(torch.autograd.Function):
         y, mean, rstd = _fx().ln_fwd(x2, w.contiguous(), b.contiguous(), float(eps))
         ctx.save_for_backward(x2, w, mean, rstd)
         ctx.shape = shape
+        ctx.params, ctx.wi, ctx.defer = (w, b), 1, defer_scope()
         return y.view(shape)
 
     @staticmethod
     def backward(ctx, dy):
         x2, w, mean, rstd = ctx.saved_tensors
         dy2 = dy.reshape(x2.shape).to(x2.dtype).contiguous()
-        dx, dw, db = _fx().ln_bwd(dy2, x2, w.contiguous(), mean, rstd)
-        return dx.view(ctx.shape), dw.to(w.dtype), db.to(w.dtype), None
+        dx, dw, db = _ln_bwd(ctx, dy2, x2, w, mean, rstd)
+        return dx.view(ctx.shape), dw, db, None
 
 
 def layer_norm(x: torch.Tensor, weight: torch.Tensor, bias: torch.Tensor, eps: float = 1e-5) -> torch.Tensor:
@@ -90,6 +171,7 @@ class _AddLayerNorm(torch.autograd.Function):
         y, mean, rstd, s = _fx().ln_fwd(x2, w.contiguous(), b.contiguous(), float(eps), r2)
         ctx.save_for_backward(s, w, mean, rstd)
         ctx.shape = shape
+        ctx.params, ctx.wi, ctx.defer = (w, b), 2, defer_scope()
         return s.view(shape), y.view(shape)
 
     @staticmethod
@@ -99,9 +181,9 @@ class _AddLayerNorm(torch.autograd.Function):
             dy = torch.zeros_like(s)
         dy2 = dy.reshape(s.shape).to(s.dtype).contiguous()
         gs2 = gs.reshape(s.shape).to(s.dtype).contiguous() if gs is not None else None
-        dx, dw, db = _fx().ln_bwd(dy2, s, w.contiguous(), mean, rstd, gs2)
+        dx, dw, db = _ln_bwd(ctx, dy2, s, w, mean, rstd, gs2)
         dx = dx.view(ctx.shape)
-        return dx, dx, dw.to(w.dtype), db.to(w.dtype), None
+        return dx, dx, dw, db, None
 
 
 def add_layer_norm_reference(x, r, w, b, eps):

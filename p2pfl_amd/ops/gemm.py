@@ -364,6 +364,10 @@ class _LinearP(torch.autograd.Function):
         ctx.gelu, ctx.plan = gelu, plan
         ctx.w_dtype = w.dtype
         ctx.b_dtype = b.dtype if b is not None else None
+        ctx.bias = b
+        from p2pfl_amd.ops.fused import defer_scope
+
+        ctx.defer = defer_scope()  # recorded on the caller's thread (see ops.fused.deferred_param_grads)
         ctx.xshape = x.shape
         return y.view(*x.shape[:-1], w.shape[0])
 
@@ -374,11 +378,23 @@ class _LinearP(torch.autograd.Function):
 
         x2, w, pre, gb = ctx.saved_tensors
         _, dg, wg = ctx.plan
+        from p2pfl_amd.ops.fused import defer_grad
+
         dz = _rows(dy.to(torch.bfloat16))
         db = None
-        if ctx.gelu:
+        want_db = ctx.b_dtype is not None and ctx.needs_input_grad[2]
+        d = ctx.defer if ctx.defer is not None and ctx.defer.open else None
+        if ctx.gelu and want_db and d is not None:  # the column reduction runs at the end of the backward
+            dz, pdb = _fx().bias_gelu_bwd_parts(dz, pre, gb)
+            if not defer_grad(d, ctx.bias, pdb):
+                db = pdb.sum(0)
+        elif ctx.gelu:
             dz, db = _fx().bias_gelu_bwd(dz, pre, gb)  # dz = dy * gelu'(pre), db = column sums of dz
-        elif ctx.b_dtype is not None and ctx.needs_input_grad[2]:
+        elif want_db and d is not None and dz.shape[0] > 0:
+            part = _fx().column_sum_parts(dz)
+            if not defer_grad(d, ctx.bias, part):
+                db = part.sum(0)
+        elif want_db:
             db = _bias_grad(dz, ctx.b_dtype)
         dx = dw = None
         if ctx.needs_input_grad[0]:
