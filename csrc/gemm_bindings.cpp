@@ -120,6 +120,11 @@ void gemm(torch::Tensor a, torch::Tensor b, bool a_kmajor, bool b_kmajor, torch:
                 "gemm: residual must be bf16 [M, N] with out's row stride");
     p.residual = reinterpret_cast<const uint16_t*>(residual->data_ptr());
   }
+  // the ping-pong kernel does not range-check a k-major K tail: a plain ping-pong request
+  // for such a shape runs on the 128 x 128 core kernel (gemm_bf16), but the stream-K
+  // schedule has no such fallback (its workspace is sized per workgroup), so refuse it
+  TORCH_CHECK(!sk || p2::gemm_pp_supported(p),
+              "gemm: the stream-K schedule needs K % 64 == 0 with a k-major operand (M=", M, " N=", N, " K=", K, ")");
   const c10::DeviceGuard guard(a.device());
   p2::gemm_bf16(p, c10::hip::getCurrentHIPStream().stream());
 }

@@ -34,8 +34,15 @@ def _operands(M, N, K, a_kmajor, b_kmajor, seed=0):
 @pytest.mark.parametrize("M,N,K", [(128, 128, 64), (256, 384, 192), (200, 136, 200), (6304 // 8, 768, 768), (72, 1000, 96)])
 def test_gemm_layouts_vs_fp32(a_kmajor, b_kmajor, M, N, K):
     """Every operand layout; ragged M (row clamping), N (masked stores) and K (zeroed tail)."""
-    if not a_kmajor and M % 8:
-        pytest.skip("m-major A needs M % 8 == 0")
+    if not a_kmajor and M % 8:  # refused loudly, by the planner and by the binding
+        from p2pfl_amd.ops.gemm import supported
+
+        assert not supported(M, N, K, a_kmajor, b_kmajor)
+        a, b = _operands(M + 8 - M % 8, N, K, a_kmajor, b_kmajor, seed=1)
+        a = a[:, :M]  # an m-major [K, M] view with M % 8 != 0
+        with pytest.raises(RuntimeError):
+            ops.ext().gemm(a, b, a_kmajor, b_kmajor, torch.empty(M, N, device="cuda"), None, False, None, None, 1, 10)
+        return
     a, b = _operands(M, N, K, a_kmajor, b_kmajor, seed=M + N + K)
     out, _ = ops.gemm(a, b, a_kmajor, b_kmajor, out_dtype=torch.float32)
     ref, _ = ops.gemm_reference(a, b, a_kmajor, b_kmajor)
@@ -197,12 +204,11 @@ def test_pingpong_gemm_layouts_vs_fp32(a_kmajor, b_kmajor, M, N, K, m16):
     """The ping-pong 256 x 256 kernel (variant bit 11) in both MFMA forms (32x32x16, and
     16x16x32 with bit 16): every layout, M / N tails (clamped rows), odd K-tile counts,
     and (m/n-major only) a K tail through the buffer range check."""
-    from p2pfl_amd.ops.gemm import PP, PP_M16
+    from p2pfl_amd.ops.gemm import PP, PP_M16, pp_eligible_any
 
-    if (a_kmajor or b_kmajor) and K % 64:
-        pytest.skip("k-major operands need K % 64 == 0 on this kernel")
-    if not a_kmajor and M % 8:
-        pytest.skip("m-major A needs M % 8 == 0")
+    # a k-major K tail is not range-checked by this kernel: the planner never offers it
+    # there, and a direct request runs on the 128 x 128 core kernel (checked below too)
+    assert pp_eligible_any(M, N, K, a_kmajor, b_kmajor) == (not ((a_kmajor or b_kmajor) and K % 64))
     a, b = _operands(M, N, K, a_kmajor, b_kmajor, seed=M + 3 * N + K)
     out = torch.empty(M, N, device="cuda", dtype=torch.float32)
     ops.ext().gemm(a, b, a_kmajor, b_kmajor, out, None, False, None, None, 1, PP | (PP_M16 if m16 else 0))
@@ -293,11 +299,15 @@ def test_stream_k_layouts_vs_fp32(a_kmajor, b_kmajor, M, N, K, grid, m16):
     workgroups per tile), every operand layout, M / N tails, a K tail (m/n-major)."""
     from p2pfl_amd.ops.gemm import PP, PP_M16, PP_SK, sk_iters
 
-    if (a_kmajor or b_kmajor) and K % 64:
-        pytest.skip("k-major operands need K % 64 == 0 on this kernel")
-    if not a_kmajor and M % 8:
-        pytest.skip("m-major A needs M % 8 == 0")
     assert grid <= sk_iters(M, N, K)
+    if (a_kmajor or b_kmajor) and K % 64:  # no fallback for the stream-K schedule: refused loudly
+        a, b = _operands(M, N, K, a_kmajor, b_kmajor, seed=2)
+        ws = torch.empty(2 * grid * 65536, device="cuda")
+        cnt = torch.zeros(-(-M // 128) * -(-N // 128), dtype=torch.int32, device="cuda")
+        with pytest.raises(RuntimeError, match="stream-K"):
+            ops.ext().gemm(a, b, a_kmajor, b_kmajor, torch.empty(M, N, device="cuda"), None, False, None, None, grid,
+                           PP | PP_SK, ws, cnt)
+        return
     a, b = _operands(M, N, K, a_kmajor, b_kmajor, seed=M + 5 * N + K)
     out, _ = ops.gemm(a, b, a_kmajor, b_kmajor, out_dtype=torch.float32, splits=grid,
                       variant=PP | PP_SK | (PP_M16 if m16 else 0))
@@ -379,12 +389,10 @@ def test_stream_k_refuses_bad_grid():
 def test_pingpong128_layouts_vs_fp32(a_kmajor, b_kmajor, M, N, K, m16):
     """The 256 x 128 tile: every layout, M / N tails (clamped rows, masked stores), odd and
     even K-tile counts (the two-K-tile phase schedule's tail), a K tail (m/n-major only)."""
-    from p2pfl_amd.ops.gemm import PP, PP_M16, PP_N128
+    from p2pfl_amd.ops.gemm import PP, PP_M16, PP_N128, pp_eligible_any
 
-    if (a_kmajor or b_kmajor) and K % 64:
-        pytest.skip("k-major operands need K % 64 == 0 on this kernel")
-    if not a_kmajor and M % 8:
-        pytest.skip("m-major A needs M % 8 == 0")
+    # k-major K tail: never planned on this kernel; a direct request runs on the core kernel
+    assert pp_eligible_any(M, N, K, a_kmajor, b_kmajor) == (not ((a_kmajor or b_kmajor) and K % 64))
     v = PP | PP_N128 | (PP_M16 if m16 else 0)
     a, b = _operands(M, N, K, a_kmajor, b_kmajor, seed=M + 7 * N + K)
     out, _ = ops.gemm(a, b, a_kmajor, b_kmajor, out_dtype=torch.float32, variant=v)
