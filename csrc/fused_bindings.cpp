@@ -189,6 +189,34 @@ torch::Tensor column_sum_parts(torch::Tensor x) {
   return part;
 }
 
+// parts[i] = the [S, H] column partials of xs[i] (bf16 [N, H], N > 0), many per launch
+void column_sum_parts_multi(std::vector<torch::Tensor> xs, std::vector<torch::Tensor> parts) {
+  TORCH_CHECK(xs.size() == parts.size(), "column_sum_parts_multi: xs / parts length mismatch");
+  if (xs.empty()) return;
+  const c10::DeviceGuard g(xs[0].device());
+  p2fused::CsJobs jobs{};
+  for (size_t i = 0; i < xs.size(); ++i) {
+    const auto& x = xs[i];
+    const auto& pt = parts[i];
+    TORCH_CHECK(x.is_cuda() && x.scalar_type() == torch::kBFloat16 && x.dim() == 2 && x.stride(1) == 1 &&
+                    x.stride(0) == x.size(1) && x.size(0) > 0 && x.size(1) % 8 == 0 &&
+                    reinterpret_cast<uintptr_t>(x.data_ptr()) % 16 == 0,
+                "column_sum_parts_multi: xs must be contiguous, 16-byte aligned bf16 [N, H] (H % 8 == 0)");
+    const int N = int(x.size(0)), H = int(x.size(1)), S = p2fused::bias_gelu_bwd_splits(N);
+    TORCH_CHECK(pt.is_cuda() && pt.scalar_type() == torch::kFloat32 && pt.is_contiguous() && pt.dim() == 2 &&
+                    pt.size(0) == S && pt.size(1) == H && pt.device() == x.device() && x.device() == xs[0].device(),
+                "column_sum_parts_multi: parts[i] must be contiguous fp32 [bias_gelu_bwd_splits(N), H] on xs' device");
+    jobs.j[jobs.n++] = p2fused::CsJob{reinterpret_cast<const uint16_t*>(x.data_ptr<at::BFloat16>()),
+                                      pt.data_ptr<float>(), N, H, S, 0};
+    if (jobs.n == p2fused::kCsMaxJobs || i + 1 == xs.size()) {
+      p2fused::colsum_multi(jobs, stream());
+      jobs.n = 0;
+    }
+  }
+}
+
+int64_t colsum_splits(int64_t N) { return p2fused::bias_gelu_bwd_splits(int(N)); }
+
 // outs[i] (fp32 or bf16 [C]) = column sums of parts[i] (fp32 [R, C]), up to kCrMaxJobs per launch
 void col_reduce_multi(std::vector<torch::Tensor> parts, std::vector<torch::Tensor> outs) {
   TORCH_CHECK(parts.size() == outs.size(), "col_reduce_multi: parts / outs length mismatch");
@@ -397,6 +425,8 @@ void register_fused(pybind11::module& m) {
   f.def("bias_gelu_bwd_parts", &bias_gelu_bwd_parts, "bias+GELU backward: dx and the [S, H] dbias partials");
   f.def("column_sum_parts", &column_sum_parts, "[S, H] partial column sums of a [N, H] activation");
   f.def("col_reduce_multi", &col_reduce_multi, "outs[i] = column sums of parts[i], many per launch");
+  f.def("column_sum_parts_multi", &column_sum_parts_multi, "parts[i] = column_sum partials of xs[i], many per launch");
+  f.def("colsum_splits", &colsum_splits, "row splits S of column_sum's [S, H] partials for N rows");
   f.def("multi_copy", &multi_copy, "dsts[i] <- srcs[i] for up to 12 pairs in one launch");
   f.def("split_sum_bf16", &split_sum_bf16, "bf16 sum over dim 0 of [S, ...] bf16 partials, fp32 accumulation");
   f.def("bias_gelu_fwd", &bias_gelu_fwd);

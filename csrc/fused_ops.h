@@ -49,6 +49,20 @@ struct CrJobs {
 };
 void col_reduce_multi(CrJobs& jobs, hipStream_t s);
 
+// column_sum's [S = bias_gelu_bwd_splits(N), H] partials of many bf16 [N, H] activations
+// in one launch (blk0 filled by colsum_multi); reduce them with col_reduce_multi
+struct CsJob {
+  const uint16_t* x;
+  float* part;
+  int N, H, S, blk0;
+};
+constexpr int kCsMaxJobs = 64;  // 1.5 KB of kernel arguments
+struct CsJobs {
+  CsJob j[kCsMaxJobs];
+  int n;
+};
+void colsum_multi(CsJobs& jobs, hipStream_t s);
+
 // out[i] = bf16(sum_s parts[s][i]) over S bf16 partial arrays of n elements (n % 8 == 0)
 void split_sum_bf16(const uint16_t* parts, uint16_t* out, int64_t n, int S, hipStream_t s);
 

@@ -434,14 +434,13 @@ __global__ __launch_bounds__(256) void bias_gelu_bwd_kernel(const T* __restrict_
 // db[c] = sum_r dy[r][c] (bias gradient of a linear layer): same grid and
 // fixed-order partials as bias_gelu_bwd, without the GELU and the dx write.
 template <typename T>
-__global__ __launch_bounds__(256) void colsum_kernel(const T* __restrict__ dy, float* __restrict__ part, int N, int H) {
+P2_DEVICE void colsum_body(const T* __restrict__ dy, float* __restrict__ part, int N, int H, int bx, int by, int S) {
   __shared__ float red[4][512];
   const int lane = threadIdx.x & 63, ph = threadIdx.x >> 6;
-  const int c = (blockIdx.x * 64 + lane) * 8;
-  const int S = gridDim.y;
+  const int c = (bx * 64 + lane) * 8;
   float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
   if (c < H) {
-    for (int r = blockIdx.y * 4 + ph; r < N; r += 4 * S) {
+    for (int r = by * 4 + ph; r < N; r += 4 * S) {
       float dv[8];
       Vec8<T>::load(dy + size_t(r) * H + c, dv);
 #pragma unroll
@@ -452,9 +451,34 @@ __global__ __launch_bounds__(256) void colsum_kernel(const T* __restrict__ dy, f
   for (int j = 0; j < 8; ++j) red[ph][lane * 8 + j] = acc[j];
   __syncthreads();
   for (int i = threadIdx.x; i < 512; i += 256) {
-    const int cc = blockIdx.x * 512 + i;
-    if (cc < H) part[size_t(blockIdx.y) * H + cc] = (red[0][i] + red[1][i]) + (red[2][i] + red[3][i]);
+    const int cc = bx * 512 + i;
+    if (cc < H) part[size_t(by) * H + cc] = (red[0][i] + red[1][i]) + (red[2][i] + red[3][i]);
   }
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void colsum_kernel(const T* __restrict__ dy, float* __restrict__ part, int N, int H) {
+  colsum_body<T>(dy, part, N, H, blockIdx.x, blockIdx.y, gridDim.y);
+}
+
+// The [S, H] column partials of many bf16 activations in one launch (the deferred bias
+// gradients of a training step): block -> (job, column block, row split) through the job
+// table in the kernel arguments; each block runs exactly colsum_kernel's body.
+__global__ __launch_bounds__(256) void colsum_multi_kernel(CsJobs jobs) {
+  int j = 0;
+  while (j + 1 < jobs.n && int(blockIdx.x) >= jobs.j[j + 1].blk0) ++j;  // block-uniform
+  const CsJob& t = jobs.j[j];
+  const int nbx = (t.H + 511) / 512, lid = int(blockIdx.x) - t.blk0;
+  colsum_body<uint16_t>(t.x, t.part, t.N, t.H, lid % nbx, lid / nbx, t.S);
+}
+
+void colsum_multi(CsJobs& jobs, hipStream_t s) {
+  int blocks = 0;
+  for (int i = 0; i < jobs.n; ++i) {
+    jobs.j[i].blk0 = blocks;
+    blocks += (jobs.j[i].H + 511) / 512 * jobs.j[i].S;
+  }
+  if (blocks > 0) hipLaunchKernelGGL(colsum_multi_kernel, dim3(blocks), dim3(256), 0, s, jobs);
 }
 
 // ---------------------------------------------------------------------------

@@ -64,6 +64,9 @@ def attention_qkv_reference(qkv, heads):
 # concurrent backward can never land in this step's collection.
 # P2PFL_DEFER_GRAD_REDUCE=0 keeps the per-pass reductions.
 _DEFER_ON = os.environ.get("P2PFL_DEFER_GRAD_REDUCE", "1") != "0"
+# the bias column sums themselves too (their partial pass batched as well); P2PFL_DEFER_COLSUM=0:
+# partials per backward pass, only the reductions batched
+_DEFER_COLSUM = os.environ.get("P2PFL_DEFER_COLSUM", "1") != "0"
 _TLS = threading.local()
 
 
@@ -72,6 +75,8 @@ class _Deferred:
         self.open = True
         self.params: list = []
         self.parts: list = []
+        self.cs_params: list = []  # bias gradients = column sums of activations, partials deferred too
+        self.cs_x: list = []
 
 
 def defer_scope():
@@ -89,6 +94,18 @@ def defer_grad(d, param, part: torch.Tensor) -> bool:
     return True
 
 
+def defer_colsum(d, param, x: torch.Tensor) -> bool:
+    """Register ``param``'s gradient as the column sums of the bf16 activation ``x``
+    ([N, H], kept alive until the exit): both the partial pass and the reduction run
+    batched at the exit.  False (reduce now) without an open collection."""
+    if (not _DEFER_COLSUM or d is None or not d.open or not isinstance(param, torch.nn.Parameter) or x.dtype != torch.bfloat16
+            or x.dim() != 2 or not x.is_contiguous() or x.shape[0] == 0 or x.shape[1] % 8 or x.data_ptr() % 16):
+        return False
+    d.cs_params.append(param)
+    d.cs_x.append(x)
+    return True
+
+
 @contextmanager
 def deferred_param_grads(enabled: bool = True):
     """Wrap the forward AND backward of a training step: the deferrable parameter-gradient
@@ -102,6 +119,14 @@ def deferred_param_grads(enabled: bool = True):
     finally:
         _TLS.d = None
         d.open = False
+    if d.cs_x:  # the bias partials of every deferred column sum: one launch
+        fx = _fx()
+        parts = [torch.empty(fx.colsum_splits(x.shape[0]), x.shape[1], dtype=torch.float32, device=x.device)
+                 for x in d.cs_x]
+        fx.column_sum_parts_multi(d.cs_x, parts)
+        d.params += d.cs_params
+        d.parts += parts
+        d.cs_x.clear()
     if not d.parts:
         return
     outs = [torch.empty(p.shape, dtype=p.dtype, device=part.device) for p, part in zip(d.params, d.parts)]

@@ -378,7 +378,7 @@ class _LinearP(torch.autograd.Function):
 
         x2, w, pre, gb = ctx.saved_tensors
         _, dg, wg = ctx.plan
-        from p2pfl_amd.ops.fused import defer_grad
+        from p2pfl_amd.ops.fused import defer_colsum, defer_grad
 
         dz = _rows(dy.to(torch.bfloat16))
         db = None
@@ -390,6 +390,8 @@ class _LinearP(torch.autograd.Function):
                 db = pdb.sum(0)
         elif ctx.gelu:
             dz, db = _fx().bias_gelu_bwd(dz, pre, gb)  # dz = dy * gelu'(pre), db = column sums of dz
+        elif want_db and d is not None and defer_colsum(d, ctx.bias, dz):
+            pass  # partials and reduction both run batched after the backward
         elif want_db and d is not None and dz.shape[0] > 0:
             part = _fx().column_sum_parts(dz)
             if not defer_grad(d, ctx.bias, part):

@@ -19,6 +19,16 @@ class _FakeFx:
         for p, o in zip(parts, outs):
             o.copy_(p.sum(0).to(o.dtype))
 
+    @staticmethod
+    def colsum_splits(n):
+        return 2
+
+    def column_sum_parts_multi(self, xs, parts):
+        self.calls += 1
+        for x, p in zip(xs, parts):
+            p.zero_()
+            p[0].copy_(x.float().sum(0))
+
 
 def _patch(monkeypatch) -> _FakeFx:
     fx = _FakeFx()
@@ -69,3 +79,15 @@ def test_scopes_are_per_thread_and_disabled_by_the_switch(monkeypatch):
         assert fused.defer_scope() is None
     with fused.deferred_param_grads(enabled=False):
         assert fused.defer_scope() is None
+
+
+def test_deferred_column_sums_of_activations(monkeypatch):
+    fx = _patch(monkeypatch)
+    b = torch.nn.Parameter(torch.zeros(8, dtype=torch.bfloat16))
+    x = torch.randn(5, 8).to(torch.bfloat16)
+    with fused.deferred_param_grads():
+        d = fused.defer_scope()
+        assert fused.defer_colsum(d, b, x)
+        assert not fused.defer_colsum(d, b, x.t())  # not a contiguous [N, H] activation
+    assert fx.calls == 2  # one partial pass + one reduction for all deferred sums
+    torch.testing.assert_close(b.grad.float(), x.float().sum(0), atol=0.05, rtol=0.01)

@@ -329,3 +329,18 @@ def test_col_reduce_multi_vs_torch():
     for o, r in zip(outs, refs):
         tol = dict(atol=2e-2, rtol=1e-2) if o.dtype == torch.bfloat16 else dict(atol=1e-4, rtol=1e-5)
         torch.testing.assert_close(o.double(), r, **tol)
+
+
+def test_column_sum_parts_multi_bitwise_equals_column_sum():
+    """More activations than one launch's table (64): the batched partials + batched
+    reduction give exactly column_sum's fp32 / bf16 results."""
+    fx = ops.ext().fused
+    torch.manual_seed(6)
+    xs = [torch.randn(1 + (i * 97) % 700, 8 * (1 + (i * 29) % 130), device="cuda").to(torch.bfloat16) for i in range(70)]
+    parts = [torch.empty(fx.colsum_splits(x.shape[0]), x.shape[1], device="cuda") for x in xs]
+    fx.column_sum_parts_multi(xs, parts)
+    outs = [torch.empty(x.shape[1], device="cuda", dtype=torch.bfloat16 if i % 2 else torch.float32)
+            for i, x in enumerate(xs)]
+    fx.col_reduce_multi(parts, outs)
+    for i, (x, o) in enumerate(zip(xs, outs)):
+        assert torch.equal(o, fx.column_sum(x, bool(i % 2))), i
