@@ -18,6 +18,7 @@
 // The reference's heads: nn.Linear + CrossEntropyLoss in
 // /root/reference/p2pfl/learning/pytorch/mnist_examples/models/cnn.py:71-98.
 #include "common.h"
+#include <cstdlib>
 
 namespace p2head {
 using namespace p2;
@@ -31,6 +32,34 @@ template <>
 P2_DEVICE float ldw<float>(const float* w, int64_t i) { return w[i]; }
 template <>
 P2_DEVICE float ldw<uint16_t>(const uint16_t* w, int64_t i) { return bf16_to_f32(w[i]); }
+
+// 8 consecutive weights as fp32 (16-B aligned: C % 8 == 0)
+template <typename TW>
+P2_DEVICE void ldw8(const TW* w, int64_t i, float (&o)[8]);
+template <>
+P2_DEVICE void ldw8<float>(const float* w, int64_t i, float (&o)[8]) {
+  const float4 a = *reinterpret_cast<const float4*>(w + i), b = *reinterpret_cast<const float4*>(w + i + 4);
+  o[0] = a.x; o[1] = a.y; o[2] = a.z; o[3] = a.w;
+  o[4] = b.x; o[5] = b.y; o[6] = b.z; o[7] = b.w;
+}
+template <>
+P2_DEVICE void ldw8<uint16_t>(const uint16_t* w, int64_t i, float (&o)[8]) {
+  const uint4 u = *reinterpret_cast<const uint4*>(w + i);
+  const uint32_t x[4] = {u.x, u.y, u.z, u.w};
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    o[2 * j] = __uint_as_float(x[j] << 16);
+    o[2 * j + 1] = __uint_as_float(x[j] & 0xffff0000u);
+  }
+}
+P2_DEVICE void add8(float (&q)[8], uint4 u) {
+  const uint32_t x[4] = {u.x, u.y, u.z, u.w};
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    q[2 * j] += __uint_as_float(x[j] << 16);
+    q[2 * j + 1] += __uint_as_float(x[j] & 0xffff0000u);
+  }
+}
 
 P2_DEVICE void st_sc1f(float* p, float v) {
   const auto rs = __builtin_amdgcn_make_buffer_rsrc(p, 0, 4, 0x00020000);
@@ -47,7 +76,7 @@ __global__ __launch_bounds__(kT) void head_fwd_kernel(const uint16_t* __restrict
                                                       const float* __restrict__ bias, const int64_t* __restrict__ y,
                                                       float* __restrict__ pooled, float* __restrict__ logits,
                                                       float* __restrict__ loss_rows, float* __restrict__ loss_out, float* __restrict__ acc_out,
-                                                      int* __restrict__ ctr, int B, int HW, int C, int N) {
+                                                      int* __restrict__ ctr, int B, int HW, int C, int N, int vec) {
   __shared__ float red[kMaxN][kT / 64];
   __shared__ float lg[kMaxN];
   __shared__ int last;
@@ -57,6 +86,36 @@ __global__ __launch_bounds__(kT) void head_fwd_kernel(const uint16_t* __restrict
 #pragma unroll
   for (int n = 0; n < kMaxN; ++n) part[n] = 0.f;
   const uint16_t* fb = f + int64_t(b) * HW * C;
+  if (vec) {
+    // 8 consecutive channels per thread, 16-B loads: a pixel's 8 channels in one load and
+    // 8 pixels' loads in flight together (one channel per thread per iteration took a
+    // dependent round trip per channel group: 53 us at ResNet-50's C = 2048)
+    for (int c8 = tid * 8; c8 < C; c8 += kT * 8) {
+      float q[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+      int p = 0;
+      for (; p + 8 <= HW; p += 8) {
+        uint4 u[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) u[k] = *reinterpret_cast<const uint4*>(fb + int64_t(p + k) * C + c8);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) add8(q, u[k]);
+      }
+      for (; p < HW; ++p) add8(q, *reinterpret_cast<const uint4*>(fb + int64_t(p) * C + c8));
+#pragma unroll
+      for (int j = 0; j < 8; ++j) q[j] *= inv;
+      float4* pd = reinterpret_cast<float4*>(pooled + int64_t(b) * C + c8);
+      pd[0] = make_float4(q[0], q[1], q[2], q[3]);
+      pd[1] = make_float4(q[4], q[5], q[6], q[7]);
+#pragma unroll
+      for (int n = 0; n < kMaxN; ++n)
+        if (n < N) {
+          float wv[8];
+          ldw8<TW>(w, int64_t(n) * C + c8, wv);
+#pragma unroll
+          for (int j = 0; j < 8; ++j) part[n] = fmaf(q[j], wv[j], part[n]);
+        }
+    }
+  } else
   for (int c = tid; c < C; c += kT) {
     // 8 independent partial sums: the pixel loads of one channel are all in flight
     // at once instead of one dependent L2 round trip per pixel (HW = 16..49)
@@ -149,7 +208,7 @@ __global__ __launch_bounds__(kT) void head_bwd_kernel(const float* __restrict__ 
                                                       const int64_t* __restrict__ y, const float* __restrict__ pooled,
                                                       const TW* __restrict__ w, uint16_t* __restrict__ df,
                                                       TW* __restrict__ dw, float* __restrict__ db, int B, int HW,
-                                                      int C, int N) {
+                                                      int C, int N, int vec) {
   __shared__ float dl[kMaxN];
   const int b = blockIdx.x, tid = threadIdx.x;
   const float gscale = gloss[0] / float(B);
@@ -158,6 +217,23 @@ __global__ __launch_bounds__(kT) void head_bwd_kernel(const float* __restrict__ 
     __syncthreads();
     const float inv = 1.f / float(HW);
     uint16_t* out = df + int64_t(b) * HW * C;
+    if (vec) {  // 8 channels per thread: 16-B weight loads and 16-B pixel stores
+      for (int c8 = tid * 8; c8 < C; c8 += kT * 8) {
+        float sv[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int n = 0; n < kMaxN; ++n)
+          if (n < N) {
+            float wv[8];
+            ldw8<TW>(w, int64_t(n) * C + c8, wv);
+#pragma unroll
+            for (int j = 0; j < 8; ++j) sv[j] = fmaf(dl[n], wv[j], sv[j]);
+          }
+        const uint4 v = make_uint4(pack_bf16x2(sv[0] * inv, sv[1] * inv), pack_bf16x2(sv[2] * inv, sv[3] * inv),
+                                   pack_bf16x2(sv[4] * inv, sv[5] * inv), pack_bf16x2(sv[6] * inv, sv[7] * inv));
+        for (int p = 0; p < HW; ++p) *reinterpret_cast<uint4*>(out + int64_t(p) * C + c8) = v;
+      }
+      return;
+    }
     for (int c = tid; c < C; c += kT) {
       float s = 0.f;
 #pragma unroll
@@ -209,27 +285,42 @@ __global__ __launch_bounds__(kT) void head_bwd_kernel(const float* __restrict__ 
 
 namespace p2 {
 
+// P2PFL_HEAD_VEC=0: the scalar one-channel-per-thread loops everywhere (A/B knob)
+static bool head_vec_enabled() {
+  static const bool on = [] {
+    const char* e = getenv("P2PFL_HEAD_VEC");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
+
 void head_fwd(const uint16_t* f, const void* w, int w_bf16, const float* bias, const int64_t* y, float* pooled,
               float* logits, float* loss_rows, float* loss, float* acc, int* ctr, int B, int HW, int C, int N,
               hipStream_t s) {
   using namespace p2head;
+  // 16-B vector path: whole 8-channel groups and 16-B aligned features / weights (a weight
+  // inside a shadow arena need not be), for wide features only -- at C = 512 (ResNet-18) it
+  // leaves 3 of 4 waves idle and measured no faster (scripts/ab_head_vec.sh)
+  const int vec = head_vec_enabled() && C % 8 == 0 && C >= 1024 && reinterpret_cast<uintptr_t>(f) % 16 == 0 && reinterpret_cast<uintptr_t>(w) % 16 == 0 &&
+                  reinterpret_cast<uintptr_t>(pooled) % 16 == 0;
   if (w_bf16)
     hipLaunchKernelGGL(head_fwd_kernel<uint16_t>, dim3(B), dim3(kT), 0, s, f, static_cast<const uint16_t*>(w), bias, y,
-                       pooled, logits, loss_rows, loss, acc, ctr, B, HW, C, N);
+                       pooled, logits, loss_rows, loss, acc, ctr, B, HW, C, N, vec);
   else
     hipLaunchKernelGGL(head_fwd_kernel<float>, dim3(B), dim3(kT), 0, s, f, static_cast<const float*>(w), bias, y,
-                       pooled, logits, loss_rows, loss, acc, ctr, B, HW, C, N);
+                       pooled, logits, loss_rows, loss, acc, ctr, B, HW, C, N, vec);
 }
 
 void head_bwd(const float* gloss, const float* logits, const int64_t* y, const float* pooled, const void* w, int w_bf16,
               uint16_t* df, void* dw, float* db, int B, int HW, int C, int N, hipStream_t s) {
   using namespace p2head;
+  const int vec = head_vec_enabled() && C % 8 == 0 && C >= 1024 && reinterpret_cast<uintptr_t>(df) % 16 == 0 && reinterpret_cast<uintptr_t>(w) % 16 == 0;
   if (w_bf16)
     hipLaunchKernelGGL(head_bwd_kernel<uint16_t>, dim3(B + (N * C + kT - 1) / kT), dim3(kT), 0, s, gloss, logits, y, pooled,
-                       static_cast<const uint16_t*>(w), df, static_cast<uint16_t*>(dw), db, B, HW, C, N);
+                       static_cast<const uint16_t*>(w), df, static_cast<uint16_t*>(dw), db, B, HW, C, N, vec);
   else
     hipLaunchKernelGGL(head_bwd_kernel<float>, dim3(B + (N * C + kT - 1) / kT), dim3(kT), 0, s, gloss, logits, y, pooled,
-                       static_cast<const float*>(w), df, static_cast<float*>(dw), db, B, HW, C, N);
+                       static_cast<const float*>(w), df, static_cast<float*>(dw), db, B, HW, C, N, vec);
 }
 
 }  // namespace p2

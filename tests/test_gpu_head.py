@@ -12,7 +12,8 @@ from p2pfl_amd.ops.head import head_ok, head_reference, head_xent
 pytestmark = pytest.mark.gpu
 
 
-@pytest.mark.parametrize("B,C,H,W,N", [(32, 512, 4, 4, 10), (7, 2048, 4, 4, 10), (3, 64, 1, 1, 64), (70, 256, 2, 3, 5)])
+@pytest.mark.parametrize("B,C,H,W,N", [(32, 512, 4, 4, 10), (7, 2048, 4, 4, 10), (3, 64, 1, 1, 64), (70, 256, 2, 3, 5),
+                                       (5, 20, 3, 3, 7), (4, 2048, 7, 7, 10)])
 @pytest.mark.parametrize("wdtype", [torch.float32, torch.bfloat16])
 def test_head_xent_vs_fp32(B, C, H, W, N, wdtype):
     ops.ext()
@@ -96,3 +97,27 @@ def test_resnet_with_custom_loss_fn_skips_the_native_head(monkeypatch):
     with torch.autocast("cuda", dtype=torch.bfloat16):
         loss = m.training_step((x, y), 0)
     assert not calls and torch.isfinite(loss)
+
+
+def test_head_weight_not_16_byte_aligned_takes_the_scalar_path():
+    """A weight inside a shadow arena need not be 16-byte aligned: the launcher keeps the
+    16-B vector path off there and the result still matches fp32."""
+    ops.ext()
+    B, C, H, W, N = 6, 1024, 4, 4, 10
+    g = torch.Generator(device="cuda").manual_seed(11)
+    f = torch.randn(B, C, H, W, device="cuda", generator=g).to(torch.bfloat16)
+    f = f.contiguous(memory_format=torch.channels_last).requires_grad_(True)
+    fc = nn.Linear(C, N).cuda()
+    buf = torch.empty(N * C + 1, device="cuda", dtype=torch.bfloat16)
+    buf[1:].copy_(fc.weight.detach().reshape(-1).to(torch.bfloat16))
+    fc.weight.data = buf[1:].view(N, C)
+    assert fc.weight.data_ptr() % 16 != 0
+    y = torch.randint(0, N, (B,), device="cuda", generator=g)
+    assert head_ok(f, fc, y)
+    loss, logits, _ = head_xent(f, fc, y)
+    fr = f.detach().float().requires_grad_(True)
+    lr, logr = head_reference(fr, fc.weight.detach().float(), fc.bias.detach().float(), y)
+    torch.testing.assert_close(logits, logr, atol=1e-3, rtol=1e-3)
+    loss.backward()
+    lr.backward()
+    torch.testing.assert_close(f.grad.float(), fr.grad, atol=1e-4, rtol=2e-2)
