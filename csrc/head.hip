@@ -86,7 +86,37 @@ __global__ __launch_bounds__(kT) void head_fwd_kernel(const uint16_t* __restrict
 #pragma unroll
   for (int n = 0; n < kMaxN; ++n) part[n] = 0.f;
   const uint16_t* fb = f + int64_t(b) * HW * C;
-  if (vec) {
+  if (vec == 2) {
+    // narrow features (C / 8 divides the 256 threads): G channel groups x P pixel phases, so
+    // every wave loads -- phase ph sums pixels ph, ph + P, ... of 8 channels (16-B loads, all in
+    // flight), the P phase sums are combined in LDS in fixed order by the phase-0 threads
+    __shared__ float psum[kT * 8];
+    const int G = C / 8, P = kT / G, g = tid % G, ph = tid / G;
+    float q[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    for (int p = ph; p < HW; p += P) add8(q, *reinterpret_cast<const uint4*>(fb + int64_t(p) * C + g * 8));
+#pragma unroll
+    for (int j = 0; j < 8; ++j) psum[(ph * G + g) * 8 + j] = q[j];
+    __syncthreads();
+    if (ph == 0) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        float t = 0.f;
+        for (int k = 0; k < P; ++k) t += psum[(k * G + g) * 8 + j];
+        q[j] = t * inv;
+      }
+      float4* pd = reinterpret_cast<float4*>(pooled + int64_t(b) * C + g * 8);
+      pd[0] = make_float4(q[0], q[1], q[2], q[3]);
+      pd[1] = make_float4(q[4], q[5], q[6], q[7]);
+#pragma unroll
+      for (int n = 0; n < kMaxN; ++n)
+        if (n < N) {
+          float wv[8];
+          ldw8<TW>(w, int64_t(n) * C + g * 8, wv);
+#pragma unroll
+          for (int j = 0; j < 8; ++j) part[n] = fmaf(q[j], wv[j], part[n]);
+        }
+    }
+  } else if (vec) {
     // 8 consecutive channels per thread, 16-B loads: a pixel's 8 channels in one load and
     // 8 pixels' loads in flight together (one channel per thread per iteration took a
     // dependent round trip per channel group: 53 us at ResNet-50's C = 2048)
@@ -218,7 +248,11 @@ __global__ __launch_bounds__(kT) void head_bwd_kernel(const float* __restrict__ 
     const float inv = 1.f / float(HW);
     uint16_t* out = df + int64_t(b) * HW * C;
     if (vec) {  // 8 channels per thread: 16-B weight loads and 16-B pixel stores
-      for (int c8 = tid * 8; c8 < C; c8 += kT * 8) {
+      // (vec == 2, narrow features: G channel groups x P pixel phases, each phase storing
+      // every P-th pixel of its group)
+      const int G = vec == 2 ? C / 8 : kT, P = vec == 2 ? kT / G : 1;
+      const int g = tid % G, ph = tid / G;
+      for (int c8 = g * 8; c8 < C; c8 += G * 8) {
         float sv[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
 #pragma unroll
         for (int n = 0; n < kMaxN; ++n)
@@ -230,7 +264,7 @@ __global__ __launch_bounds__(kT) void head_bwd_kernel(const float* __restrict__ 
           }
         const uint4 v = make_uint4(pack_bf16x2(sv[0] * inv, sv[1] * inv), pack_bf16x2(sv[2] * inv, sv[3] * inv),
                                    pack_bf16x2(sv[4] * inv, sv[5] * inv), pack_bf16x2(sv[6] * inv, sv[7] * inv));
-        for (int p = 0; p < HW; ++p) *reinterpret_cast<uint4*>(out + int64_t(p) * C + c8) = v;
+        for (int p = ph; p < HW; p += P) *reinterpret_cast<uint4*>(out + int64_t(p) * C + c8) = v;
       }
       return;
     }
@@ -298,11 +332,14 @@ void head_fwd(const uint16_t* f, const void* w, int w_bf16, const float* bias, c
               float* logits, float* loss_rows, float* loss, float* acc, int* ctr, int B, int HW, int C, int N,
               hipStream_t s) {
   using namespace p2head;
-  // 16-B vector path: whole 8-channel groups and 16-B aligned features / weights (a weight
-  // inside a shadow arena need not be), for wide features only -- at C = 512 (ResNet-18) it
-  // leaves 3 of 4 waves idle and measured no faster (scripts/ab_head_vec.sh)
-  const int vec = head_vec_enabled() && C % 8 == 0 && C >= 1024 && reinterpret_cast<uintptr_t>(f) % 16 == 0 && reinterpret_cast<uintptr_t>(w) % 16 == 0 &&
-                  reinterpret_cast<uintptr_t>(pooled) % 16 == 0;
+  // 16-B vector paths: whole 8-channel groups and 16-B aligned features / weights (a weight
+  // inside a shadow arena need not be).  vec 1 (C >= 1024): 8 channels per thread; vec 2
+  // (C / 8 divides the block): channel groups x pixel phases, so all four waves load -- with
+  // 8 channels per thread alone, C = 512 (ResNet-18) left 3 of 4 waves idle and measured no
+  // faster (scripts/ab_head_vec.sh)
+  const bool al = head_vec_enabled() && C % 8 == 0 && reinterpret_cast<uintptr_t>(f) % 16 == 0 &&
+                  reinterpret_cast<uintptr_t>(w) % 16 == 0 && reinterpret_cast<uintptr_t>(pooled) % 16 == 0;
+  const int vec = !al ? 0 : (C >= 1024 ? 1 : (C >= 64 && kT % (C / 8) == 0 ? 2 : 0));
   if (w_bf16)
     hipLaunchKernelGGL(head_fwd_kernel<uint16_t>, dim3(B), dim3(kT), 0, s, f, static_cast<const uint16_t*>(w), bias, y,
                        pooled, logits, loss_rows, loss, acc, ctr, B, HW, C, N, vec);
@@ -314,7 +351,9 @@ void head_fwd(const uint16_t* f, const void* w, int w_bf16, const float* bias, c
 void head_bwd(const float* gloss, const float* logits, const int64_t* y, const float* pooled, const void* w, int w_bf16,
               uint16_t* df, void* dw, float* db, int B, int HW, int C, int N, hipStream_t s) {
   using namespace p2head;
-  const int vec = head_vec_enabled() && C % 8 == 0 && C >= 1024 && reinterpret_cast<uintptr_t>(df) % 16 == 0 && reinterpret_cast<uintptr_t>(w) % 16 == 0;
+  const bool al = head_vec_enabled() && C % 8 == 0 && reinterpret_cast<uintptr_t>(df) % 16 == 0 &&
+                  reinterpret_cast<uintptr_t>(w) % 16 == 0;
+  const int vec = !al ? 0 : (C >= 1024 ? 1 : (C >= 64 && kT % (C / 8) == 0 ? 2 : 0));
   if (w_bf16)
     hipLaunchKernelGGL(head_bwd_kernel<uint16_t>, dim3(B + (N * C + kT - 1) / kT), dim3(kT), 0, s, gloss, logits, y, pooled,
                        static_cast<const uint16_t*>(w), df, static_cast<uint16_t*>(dw), db, B, HW, C, N, vec);

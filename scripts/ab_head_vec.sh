@@ -4,7 +4,7 @@ set -u
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
-for m in resnet50 resnet18; do
+for m in ${AB_MODELS:-resnet50 resnet18}; do
   for i in 1 2; do
     for v in 1 0; do
       timeout -k 10 300 env P2PFL_HEAD_VEC=$v python -u bench.py --model $m --steps 8 --warmup 1 \
